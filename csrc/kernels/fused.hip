@@ -1,0 +1,292 @@
+// Fused elementwise kernels of the transformer block:
+//   * SwiGLU over the packed [gate | up] output of ONE fused gate+up GEMM
+//   * RoPE + QKV split: the fused QKV GEMM output [T, (H+2KV)*D] is rotated and
+//     split into q [T,H*D], k [T,KV*D], v [T,KV*D] in one pass (the [B,S,H,D]
+//     memory layout that flash attention consumes without a copy); the
+//     backward applies the inverse rotation and re-packs d(qkv).
+//   * Softmax cross-entropy fwd+bwd in one kernel over the [T, V] logits:
+//     loss per row, and the logits buffer is overwritten IN PLACE with
+//     softmax - onehot (vocab 128256 bf16 logits are 2 GB at 8k tokens; no
+//     second buffer is allocated).
+// All kernels move 16 B per lane (8 bf16) per access.
+//
+// Capability source: Llama-3 workloads of BASELINE.json configs 3 and 5
+// (SURVEY.md §2.9); the reference ships no kernels.
+#include "common.h"
+
+using namespace edl;
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// SwiGLU
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void swiglu_fwd_kernel(const bf16_t* __restrict__ gu, bf16_t* __restrict__ out,
+                                                         int64_t rows, int F) {
+  const int fc = F >> 3;
+  const int64_t total = rows * fc;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += stride) {
+    const int64_t r = e / fc;
+    const int c = (int)(e - r * fc);
+    const u32x4* row = reinterpret_cast<const u32x4*>(gu + r * 2 * F);
+    float g[8], u[8], o[8];
+    unpack8(row[c], g);
+    unpack8(row[fc + c], u);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o[k] = g[k] * sigmoidf_(g[k]) * u[k];
+    reinterpret_cast<u32x4*>(out + r * F)[c] = pack8(o);
+  }
+}
+
+__global__ __launch_bounds__(256) void swiglu_bwd_kernel(const bf16_t* __restrict__ dout,
+                                                         const bf16_t* __restrict__ gu, bf16_t* __restrict__ dgu,
+                                                         int64_t rows, int F) {
+  const int fc = F >> 3;
+  const int64_t total = rows * fc;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += stride) {
+    const int64_t r = e / fc;
+    const int c = (int)(e - r * fc);
+    const u32x4* row = reinterpret_cast<const u32x4*>(gu + r * 2 * F);
+    float g[8], u[8], d[8], dg[8], du[8];
+    unpack8(row[c], g);
+    unpack8(row[fc + c], u);
+    unpack8(reinterpret_cast<const u32x4*>(dout + r * F)[c], d);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float s = sigmoidf_(g[k]);
+      const float silu = g[k] * s;
+      du[k] = d[k] * silu;
+      dg[k] = d[k] * u[k] * s * (1.f + g[k] * (1.f - s));
+    }
+    u32x4* orow = reinterpret_cast<u32x4*>(dgu + r * 2 * F);
+    orow[c] = pack8(dg);
+    orow[fc + c] = pack8(du);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// RoPE (rotate-half convention) fused with the QKV split.
+// One work item = (token t, head h in [0, H+KV), chunk j in [0, D/16)):
+// rotates elements [8j, 8j+8) with their partners [D/2+8j, D/2+8j+8).
+// V heads are copied by work items (t, h in [H+KV, H+2KV), chunk j in [0, D/8)).
+// ---------------------------------------------------------------------------
+template <bool BWD>
+__global__ __launch_bounds__(256) void rope_qkv_kernel(const bf16_t* __restrict__ src_qkv,  // fwd: [T,(H+2KV)D]
+                                                       bf16_t* __restrict__ q, bf16_t* __restrict__ k,
+                                                       bf16_t* __restrict__ v, bf16_t* __restrict__ dst_qkv,
+                                                       const float* __restrict__ cos_t,
+                                                       const float* __restrict__ sin_t,  // [S, D/2]
+                                                       int64_t T, int S, int H, int KV, int D) {
+  const int half = D >> 1;
+  const int jr = half >> 3;  // rotate chunks per head
+  const int jv = D >> 3;     // copy chunks per v head
+  const int per_tok = (H + KV) * jr + KV * jv;
+  const int64_t total = T * per_tok;
+  const int W = (H + 2 * KV) * D;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += stride) {
+    const int64_t t = e / per_tok;
+    int r = (int)(e - t * per_tok);
+    const int s = (int)(t % S);
+    if (r < (H + KV) * jr) {
+      const int h = r / jr, j = r - h * jr;
+      bf16_t* dst;
+      int64_t dst_off;
+      if (h < H) { dst = q; dst_off = t * (int64_t)H * D + (int64_t)h * D; }
+      else { dst = k; dst_off = t * (int64_t)KV * D + (int64_t)(h - H) * D; }
+      const int64_t qkv_off = t * W + (int64_t)h * D;
+      const f32x4* cp = reinterpret_cast<const f32x4*>(cos_t + (int64_t)s * half + j * 8);
+      const f32x4* sp = reinterpret_cast<const f32x4*>(sin_t + (int64_t)s * half + j * 8);
+      const f32x4 c0 = cp[0], c1 = cp[1], s0 = sp[0], s1 = sp[1];
+      const float cs[8] = {c0[0], c0[1], c0[2], c0[3], c1[0], c1[1], c1[2], c1[3]};
+      const float sn[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
+      float a[8], b[8], oa[8], ob[8];
+      if (!BWD) {
+        unpack8(*reinterpret_cast<const u32x4*>(src_qkv + qkv_off + j * 8), a);
+        unpack8(*reinterpret_cast<const u32x4*>(src_qkv + qkv_off + half + j * 8), b);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          oa[i] = a[i] * cs[i] - b[i] * sn[i];
+          ob[i] = b[i] * cs[i] + a[i] * sn[i];
+        }
+        *reinterpret_cast<u32x4*>(dst + dst_off + j * 8) = pack8(oa);
+        *reinterpret_cast<u32x4*>(dst + dst_off + half + j * 8) = pack8(ob);
+      } else {
+        unpack8(*reinterpret_cast<const u32x4*>(dst + dst_off + j * 8), a);
+        unpack8(*reinterpret_cast<const u32x4*>(dst + dst_off + half + j * 8), b);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          oa[i] = a[i] * cs[i] + b[i] * sn[i];
+          ob[i] = b[i] * cs[i] - a[i] * sn[i];
+        }
+        *reinterpret_cast<u32x4*>(dst_qkv + qkv_off + j * 8) = pack8(oa);
+        *reinterpret_cast<u32x4*>(dst_qkv + qkv_off + half + j * 8) = pack8(ob);
+      }
+    } else {
+      r -= (H + KV) * jr;
+      const int h = r / jv, j = r - h * jv;
+      const int64_t qkv_off = t * W + (int64_t)(H + KV + h) * D + j * 8;
+      const int64_t v_off = t * (int64_t)KV * D + (int64_t)h * D + j * 8;
+      if (!BWD)
+        *reinterpret_cast<u32x4*>(v + v_off) = *reinterpret_cast<const u32x4*>(src_qkv + qkv_off);
+      else
+        *reinterpret_cast<u32x4*>(dst_qkv + qkv_off) = *reinterpret_cast<const u32x4*>(v + v_off);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Cross-entropy: one 256-lane workgroup per row. Pass 1: online (max, sum-exp)
+// over the row with 16-B loads + target logit. Pass 2 (re-read hits the
+// Infinity Cache): grad = softmax - onehot written in place (unscaled; the
+// autograd wrapper applies dloss / n_valid).  ignore_index rows get loss 0 and
+// zero gradient.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void xent_fwd_bwd_kernel(bf16_t* __restrict__ logits, const int64_t* __restrict__ labels,
+                                                           float* __restrict__ loss, int V, int64_t ignore_index,
+                                                           int write_grad) {
+  __shared__ float sm[4], ss[4];
+  __shared__ float s_tgt;
+  const int64_t row = blockIdx.x;
+  bf16_t* lr = logits + row * (int64_t)V;
+  const int64_t lab = labels[row];
+  const bool ignored = (lab == ignore_index) || lab < 0 || lab >= V;
+  const int nchunk = V >> 3;
+  float m = -INFINITY, s = 0.f;
+  const u32x4* lv = reinterpret_cast<const u32x4*>(lr);
+  for (int c = threadIdx.x; c < nchunk; c += blockDim.x) {
+    float f[8];
+    unpack8(lv[c], f);
+    float cm = f[0];
+#pragma unroll
+    for (int i = 1; i < 8; ++i) cm = fmaxf(cm, f[i]);
+    const float nm = fmaxf(m, cm);
+    float acc = s * __expf(m - nm);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc += __expf(f[i] - nm);
+    m = nm;
+    s = acc;
+  }
+  for (int c = (nchunk << 3) + threadIdx.x; c < V; c += blockDim.x) {  // tail (V % 8)
+    const float f = bf2f(lr[c]);
+    const float nm = fmaxf(m, f);
+    s = s * __expf(m - nm) + __expf(f - nm);
+    m = nm;
+  }
+  // combine (m, s) across the wave, then across waves
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const float om = __shfl_xor(m, off, 64), os = __shfl_xor(s, off, 64);
+    const float nm = fmaxf(m, om);
+    s = (m == -INFINITY ? 0.f : s * __expf(m - nm)) + (om == -INFINITY ? 0.f : os * __expf(om - nm));
+    m = nm;
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  if (lane == 0) { sm[wid] = m; ss[wid] = s; }
+  if (threadIdx.x == 0) s_tgt = ignored ? 0.f : bf2f(lr[lab]);
+  __syncthreads();
+  float M = sm[0];
+  for (int i = 1; i < nw; ++i) M = fmaxf(M, sm[i]);
+  float Ssum = 0.f;
+  for (int i = 0; i < nw; ++i) Ssum += ss[i] * __expf(sm[i] - M);
+  const float lse = M + __logf(Ssum);
+  if (threadIdx.x == 0) loss[row] = ignored ? 0.f : (lse - s_tgt);
+  if (!write_grad) return;
+  const float inv = 1.f / Ssum;
+  u32x4* lw = reinterpret_cast<u32x4*>(lr);
+  for (int c = threadIdx.x; c < nchunk; c += blockDim.x) {
+    float f[8];
+    unpack8(lw[c], f);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float p = ignored ? 0.f : __expf(f[i] - M) * inv;
+      if (!ignored && (int64_t)(c * 8 + i) == lab) p -= 1.f;
+      f[i] = p;
+    }
+    lw[c] = pack8(f);
+  }
+  for (int c = (nchunk << 3) + threadIdx.x; c < V; c += blockDim.x) {
+    float p = ignored ? 0.f : __expf(bf2f(lr[c]) - M) * inv;
+    if (!ignored && (int64_t)c == lab) p -= 1.f;
+    lr[c] = f2bf(p);
+  }
+}
+
+// y = x * s[0] in place over bf16 (s is a device scalar: no host sync).
+__global__ __launch_bounds__(256) void scale_bf16_kernel(bf16_t* __restrict__ x, int64_t n8,
+                                                         const float* __restrict__ s, float hs) {
+  const float sc = (s ? s[0] : 1.f) * hs;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += stride) {
+    float f[8];
+    u32x4* p = reinterpret_cast<u32x4*>(x);
+    unpack8(p[i], f);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) f[k] *= sc;
+    p[i] = pack8(f);
+  }
+}
+
+inline int grid_for(int64_t items, int cap = 4096) {
+  int64_t b = (items + 255) / 256;
+  if (b < 1) b = 1;
+  return (int)(b < cap ? b : cap);
+}
+
+}  // namespace
+
+extern "C" {
+
+int edl_swiglu_fwd(const void* gu, void* out, int64_t rows, int F, hipStream_t s) {
+  if (F % 8) return (int)hipErrorInvalidValue;
+  swiglu_fwd_kernel<<<grid_for(rows * (F / 8)), 256, 0, s>>>((const bf16_t*)gu, (bf16_t*)out, rows, F);
+  EDL_LAUNCH_CHECK();
+  return 0;
+}
+
+int edl_swiglu_bwd(const void* dout, const void* gu, void* dgu, int64_t rows, int F, hipStream_t s) {
+  if (F % 8) return (int)hipErrorInvalidValue;
+  swiglu_bwd_kernel<<<grid_for(rows * (F / 8)), 256, 0, s>>>((const bf16_t*)dout, (const bf16_t*)gu,
+                                                             (bf16_t*)dgu, rows, F);
+  EDL_LAUNCH_CHECK();
+  return 0;
+}
+
+int edl_rope_qkv_fwd(const void* qkv, void* q, void* k, void* v, const float* cos_t, const float* sin_t, int64_t T,
+                     int S, int H, int KV, int D, hipStream_t s) {
+  if (D % 16) return (int)hipErrorInvalidValue;
+  const int64_t items = T * ((H + KV) * (D / 16) + KV * (D / 8));
+  rope_qkv_kernel<false><<<grid_for(items), 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)q, (bf16_t*)k, (bf16_t*)v,
+                                                         nullptr, cos_t, sin_t, T, S, H, KV, D);
+  EDL_LAUNCH_CHECK();
+  return 0;
+}
+
+int edl_rope_qkv_bwd(const void* dq, const void* dk, const void* dv, void* dqkv, const float* cos_t,
+                     const float* sin_t, int64_t T, int S, int H, int KV, int D, hipStream_t s) {
+  if (D % 16) return (int)hipErrorInvalidValue;
+  const int64_t items = T * ((H + KV) * (D / 16) + KV * (D / 8));
+  rope_qkv_kernel<true><<<grid_for(items), 256, 0, s>>>(nullptr, (bf16_t*)dq, (bf16_t*)dk, (bf16_t*)dv,
+                                                        (bf16_t*)dqkv, cos_t, sin_t, T, S, H, KV, D);
+  EDL_LAUNCH_CHECK();
+  return 0;
+}
+
+int edl_xent_fwd_bwd(void* logits, const int64_t* labels, float* loss, int64_t rows, int V, int64_t ignore_index,
+                     int write_grad, hipStream_t s) {
+  if (rows <= 0) return 0;
+  xent_fwd_bwd_kernel<<<(unsigned)rows, 256, 0, s>>>((bf16_t*)logits, labels, loss, V, ignore_index, write_grad);
+  EDL_LAUNCH_CHECK();
+  return 0;
+}
+
+int edl_scale_bf16(void* x, int64_t n, const float* dscale, float hscale, hipStream_t s) {
+  if (n % 8) return (int)hipErrorInvalidValue;
+  scale_bf16_kernel<<<grid_for(n / 8), 256, 0, s>>>((bf16_t*)x, n / 8, dscale, hscale);
+  EDL_LAUNCH_CHECK();
+  return 0;
+}
+
+}  // extern "C"

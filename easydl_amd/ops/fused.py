@@ -1,0 +1,251 @@
+"""Fused transformer ops: SwiGLU, RoPE+QKV split, softmax cross-entropy,
+direct-gradient Linear and Embedding.
+
+HIP kernels live in ``csrc/kernels/fused.hip``; GEMMs go to hipBLASLt through
+``torch.mm`` (plain library GEMMs) with the weight gradient written straight
+into the flat gradient buffer (see :mod:`easydl_amd.ops.gradsink`).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+
+from easydl_amd import _native
+from easydl_amd.ops import gradsink
+
+
+# ----------------------------------------------------------------------------
+# SwiGLU over the packed [gate | up] projection
+# ----------------------------------------------------------------------------
+def swiglu_ref(gu: torch.Tensor) -> torch.Tensor:
+    g, u = gu.float().chunk(2, dim=-1)
+    return (F.silu(g) * u).to(gu.dtype)
+
+
+class _SwiGLUFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, gu):
+        k = _native.kernels()
+        gu = gu.contiguous()
+        F2 = gu.shape[-1]
+        rows = gu.numel() // F2
+        out = torch.empty(*gu.shape[:-1], F2 // 2, dtype=gu.dtype, device=gu.device)
+        k.check("edl_swiglu_fwd", gu.data_ptr(), out.data_ptr(), rows, F2 // 2, _native.stream_of(gu))
+        ctx.save_for_backward(gu)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        k = _native.kernels()
+        (gu,) = ctx.saved_tensors
+        dout = dout.contiguous()
+        F2 = gu.shape[-1]
+        rows = gu.numel() // F2
+        dgu = torch.empty_like(gu)
+        k.check("edl_swiglu_bwd", dout.data_ptr(), gu.data_ptr(), dgu.data_ptr(), rows, F2 // 2,
+                _native.stream_of(gu))
+        return dgu
+
+
+def swiglu(gu: torch.Tensor) -> torch.Tensor:
+    if _native.use_hip(gu):
+        if gu.dtype != torch.bfloat16:
+            raise TypeError("swiglu kernel expects bf16")
+        return _SwiGLUFn.apply(gu)
+    return swiglu_ref(gu)
+
+
+# ----------------------------------------------------------------------------
+# Rotary embedding fused with the QKV split
+# ----------------------------------------------------------------------------
+def rope_tables(seq_len: int, head_dim: int, theta: float = 500000.0, device=None,
+                scaling: dict | None = None):
+    """cos/sin tables [S, D/2] fp32 (rotate-half convention, Llama-3 frequencies).
+
+    ``scaling`` implements Llama-3.1 style frequency scaling when given
+    (``factor``, ``low_freq_factor``, ``high_freq_factor``, ``original_max_position_embeddings``).
+    """
+    inv = 1.0 / (theta ** (torch.arange(0, head_dim, 2, dtype=torch.float64) / head_dim))
+    if scaling:
+        factor = scaling.get("factor", 8.0)
+        lo = scaling.get("low_freq_factor", 1.0)
+        hi = scaling.get("high_freq_factor", 4.0)
+        old = scaling.get("original_max_position_embeddings", 8192)
+        wavelen = 2 * math.pi / inv
+        lo_wl, hi_wl = old / lo, old / hi
+        smooth = (old / wavelen - lo) / (hi - lo)
+        scaled = torch.where(wavelen > lo_wl, inv / factor, inv)
+        mid = (wavelen <= lo_wl) & (wavelen >= hi_wl)
+        inv = torch.where(mid, (1 - smooth) * inv / factor + smooth * inv, scaled)
+    t = torch.arange(seq_len, dtype=torch.float64)
+    fr = torch.outer(t, inv)
+    return fr.cos().float().to(device), fr.sin().float().to(device)
+
+
+def rope_qkv_ref(qkv, cos, sin, B, S, H, KV, D):
+    """qkv [B*S, (H+2KV)*D] -> q [B,H,S,D], k [B,KV,S,D], v [B,KV,S,D] (fp32 math)."""
+    x = qkv.float().view(B, S, H + 2 * KV, D)
+    q, k, v = x[:, :, :H], x[:, :, H:H + KV], x[:, :, H + KV:]
+    c = cos[:S].view(1, S, 1, D // 2)
+    s = sin[:S].view(1, S, 1, D // 2)
+
+    def rot(t):
+        a, b = t[..., : D // 2], t[..., D // 2:]
+        return torch.cat([a * c - b * s, b * c + a * s], dim=-1)
+
+    dt = qkv.dtype
+    return (rot(q).to(dt).transpose(1, 2), rot(k).to(dt).transpose(1, 2), v.to(dt).transpose(1, 2))
+
+
+class _RopeQKVFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, cos, sin, B, S, H, KV, D):
+        k_ = _native.kernels()
+        qkv = qkv.contiguous()
+        T = B * S
+        q = torch.empty(B, S, H, D, dtype=qkv.dtype, device=qkv.device)
+        k = torch.empty(B, S, KV, D, dtype=qkv.dtype, device=qkv.device)
+        v = torch.empty(B, S, KV, D, dtype=qkv.dtype, device=qkv.device)
+        k_.check("edl_rope_qkv_fwd", qkv.data_ptr(), q.data_ptr(), k.data_ptr(), v.data_ptr(), cos.data_ptr(),
+                 sin.data_ptr(), T, S, H, KV, D, _native.stream_of(qkv))
+        ctx.save_for_backward(cos, sin)
+        ctx.dims = (B, S, H, KV, D)
+        # [B,H,S,D] views of [B,S,H,D] memory: what flash attention consumes copy-free
+        return q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2)
+
+    @staticmethod
+    def backward(ctx, dq, dk, dv):
+        k_ = _native.kernels()
+        cos, sin = ctx.saved_tensors
+        B, S, H, KV, D = ctx.dims
+        dev = cos.device
+        dt = (dq if dq is not None else dk if dk is not None else dv).dtype
+
+        def bshd(t, heads):
+            if t is None:
+                return torch.zeros(B, S, heads, D, dtype=dt, device=dev)
+            return t.transpose(1, 2).contiguous()
+
+        dq_, dk_, dv_ = bshd(dq, H), bshd(dk, KV), bshd(dv, KV)
+        dqkv = torch.empty(B * S, (H + 2 * KV) * D, dtype=dt, device=dev)
+        k_.check("edl_rope_qkv_bwd", dq_.data_ptr(), dk_.data_ptr(), dv_.data_ptr(), dqkv.data_ptr(), cos.data_ptr(),
+                 sin.data_ptr(), B * S, S, H, KV, D, _native.stream_of(dqkv))
+        return dqkv, None, None, None, None, None, None, None
+
+
+def rope_qkv(qkv, cos, sin, B, S, H, KV, D):
+    if _native.use_hip(qkv):
+        return _RopeQKVFn.apply(qkv, cos, sin, B, S, H, KV, D)
+    return rope_qkv_ref(qkv, cos, sin, B, S, H, KV, D)
+
+
+# ----------------------------------------------------------------------------
+# Softmax cross-entropy (forward computes the gradient in place)
+# ----------------------------------------------------------------------------
+def cross_entropy_ref(logits, labels, ignore_index=-100):
+    return F.cross_entropy(logits.float(), labels, ignore_index=ignore_index)
+
+
+class _XentFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, labels, ignore_index):
+        k = _native.kernels()
+        if not logits.is_contiguous():
+            logits = logits.contiguous()
+        rows, V = logits.shape
+        loss = torch.empty(rows, dtype=torch.float32, device=logits.device)
+        labels = labels.contiguous().to(torch.int64)
+        want_grad = ctx.needs_input_grad[0]
+        # NOTE: overwrites `logits` with softmax - onehot when a gradient is wanted.
+        k.check("edl_xent_fwd_bwd", logits.data_ptr(), labels.data_ptr(), loss.data_ptr(), rows, V, ignore_index,
+                1 if want_grad else 0, _native.stream_of(logits))
+        nvalid = (labels != ignore_index).sum().clamp_min(1).float()
+        out = loss.sum() / nvalid
+        if want_grad:
+            ctx.save_for_backward(logits, nvalid)
+        return out
+
+    @staticmethod
+    def backward(ctx, dloss):
+        k = _native.kernels()
+        grad, nvalid = ctx.saved_tensors
+        scale = (dloss.float() / nvalid).reshape(1).contiguous()
+        k.check("edl_scale_bf16", grad.data_ptr(), grad.numel(), scale.data_ptr(), 1.0, _native.stream_of(grad))
+        return grad, None, None
+
+
+def cross_entropy(logits, labels, ignore_index: int = -100):
+    """Mean token cross-entropy. On GPU the bf16 logits buffer is consumed (overwritten by its gradient)."""
+    if _native.use_hip(logits) and logits.dtype == torch.bfloat16 and logits.shape[-1] % 8 == 0:
+        return _XentFn.apply(logits.view(-1, logits.shape[-1]), labels.reshape(-1), ignore_index)
+    return cross_entropy_ref(logits.view(-1, logits.shape[-1]), labels.reshape(-1), ignore_index)
+
+
+# ----------------------------------------------------------------------------
+# Linear / Embedding with direct weight-gradient delivery
+# ----------------------------------------------------------------------------
+class _LinearFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b):
+        x2 = x.reshape(-1, x.shape[-1])
+        y = F.linear(x2, w, b)
+        ctx.save_for_backward(x2, w)
+        ctx.has_b = b is not None
+        ctx.b = b
+        return y.view(*x.shape[:-1], w.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w = ctx.saved_tensors
+        dy2 = dy.reshape(-1, dy.shape[-1])
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.mm(dy2, w).view(*dy.shape[:-1], w.shape[1])
+        dw = db = None
+        if ctx.needs_input_grad[1]:
+            if gradsink.is_flat(w):
+                gradsink.write_mm(w, dy2.t(), x2)
+            else:
+                dw = torch.mm(dy2.t(), x2)
+        if ctx.has_b and ctx.needs_input_grad[2]:
+            b = ctx.b
+            g = dy2.sum(0)
+            if gradsink.is_flat(b):
+                gradsink.write(b, g)
+            else:
+                db = g.to(b.dtype)
+        return dx, dw, db
+
+
+def linear(x, w, b=None):
+    if _native.use_hip(x) or gradsink.is_flat(w):
+        return _LinearFn.apply(x, w, b)
+    return F.linear(x, w, b)
+
+
+class _EmbeddingFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, ids, w):
+        ctx.save_for_backward(ids)
+        ctx.wshape = w.shape
+        ctx.w = w
+        return F.embedding(ids, w)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (ids,) = ctx.saved_tensors
+        w = ctx.w
+        V, d = ctx.wshape
+        g = torch.ops.aten.embedding_dense_backward(dy.reshape(-1, d), ids.reshape(-1), V, -1, False)
+        if gradsink.is_flat(w):
+            gradsink.write(w, g)
+            return None, None
+        return None, g
+
+
+def embedding(ids, w):
+    if gradsink.is_flat(w):
+        return _EmbeddingFn.apply(ids, w)
+    return F.embedding(ids, w)

@@ -1,0 +1,107 @@
+"""Flat-buffer optimizer math: fused AdamW / SGD and the global grad-norm clip.
+
+GPU tensors run the kernels of ``csrc/kernels/optim.hip`` (one launch per flat
+group); CPU tensors run the identical math in PyTorch.  The combined gradient
+scale ``pre_scale x clip_coef`` stays on the device (``dscale`` = [coef, norm,
+nonfinite]) so clipping never synchronises the host.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from easydl_amd import _native
+
+
+def _gdtype(g: torch.Tensor) -> int:
+    if g.dtype == torch.bfloat16:
+        return 0
+    if g.dtype == torch.float32:
+        return 1
+    raise TypeError(f"unsupported gradient dtype {g.dtype}")
+
+
+def grad_clip_scale(grads: list[torch.Tensor], max_norm: float, pre_scale: float = 1.0) -> torch.Tensor:
+    """Return a device tensor [coef, norm, nonfinite] for flat gradient buffers.
+
+    ``norm`` is the L2 norm of ``pre_scale * concat(grads)``; ``coef`` =
+    ``pre_scale * min(1, max_norm / norm)`` (``max_norm <= 0`` disables clipping).
+    """
+    dev = grads[0].device
+    if _native.use_hip(grads[0]):
+        k = _native.kernels()
+        nparts = [k("edl_sumsq_nparts", g.numel()) for g in grads]
+        partial = torch.empty(sum(nparts), dtype=torch.float32, device=dev)
+        out = torch.empty(3, dtype=torch.float32, device=dev)
+        st = _native.stream_of(grads[0])
+        off = 0
+        for g, n in zip(grads, nparts):
+            k.check("edl_sumsq_partial", g.data_ptr(), _gdtype(g), g.numel(), partial[off:].data_ptr(), st)
+            off += n
+        k.check("edl_clip_finalize", partial.data_ptr(), off, float(pre_scale), float(max_norm), out.data_ptr(), st)
+        return out
+    sq = torch.zeros((), dtype=torch.float64, device=dev)
+    for g in grads:
+        sq += g.double().pow(2).sum()
+    norm = (sq.sqrt() * pre_scale).float()
+    bad = (~torch.isfinite(norm)).float()
+    coef = torch.tensor(pre_scale, dtype=torch.float32, device=dev)
+    if max_norm > 0:
+        coef = torch.where(norm > max_norm, pre_scale * (max_norm / (norm + 1e-6)), coef)
+    return torch.stack([coef, norm, bad])
+
+
+def adamw_flat_(param16, master, m, v, grad, *, lr, beta1, beta2, eps, weight_decay, step, scale=1.0,
+                dscale=None):
+    """In-place AdamW over flat buffers.
+
+    ``param16``: bf16 model weights (or None when ``master`` is the parameter),
+    ``master``/``m``/``v``: fp32, ``grad``: bf16 or fp32, all the same numel.
+    """
+    n = master.numel()
+    if _native.use_hip(master):
+        k = _native.kernels()
+        for t in (param16, master, m, v, grad):
+            if t is not None and (t.data_ptr() % 16 or not t.is_contiguous()):
+                raise ValueError("flat optimizer buffers must be contiguous and 16-byte aligned")
+        k.check("edl_adamw_flat", _native.ptr(param16), master.data_ptr(), m.data_ptr(), v.data_ptr(),
+                grad.data_ptr(), _gdtype(grad), n, lr, beta1, beta2, eps, weight_decay, int(step), float(scale),
+                _native.ptr(dscale), _native.stream_of(master))
+        return
+    # reference (same operation order as the kernel / torch.optim.AdamW)
+    g = grad.float() * scale
+    if dscale is not None:
+        if float(dscale[2]) != 0.0:
+            return
+        g = g * dscale[0]
+    bc1 = 1.0 - beta1 ** step
+    bc2 = 1.0 - beta2 ** step
+    m.mul_(beta1).add_(g, alpha=1 - beta1)
+    v.mul_(beta2).addcmul_(g, g, value=1 - beta2)
+    denom = v.sqrt() / math.sqrt(bc2) + eps
+    master.mul_(1 - lr * weight_decay).addcdiv_(m, denom, value=-lr / bc1)
+    if param16 is not None:
+        param16.copy_(master)
+
+
+def sgd_flat_(param16, master, mom, grad, *, lr, momentum=0.0, weight_decay=0.0, scale=1.0, dscale=None):
+    n = master.numel()
+    if _native.use_hip(master):
+        k = _native.kernels()
+        k.check("edl_sgd_flat", _native.ptr(param16), master.data_ptr(), _native.ptr(mom), grad.data_ptr(),
+                _gdtype(grad), n, lr, momentum, weight_decay, float(scale), _native.ptr(dscale),
+                _native.stream_of(master))
+        return
+    g = grad.float() * scale
+    if dscale is not None:
+        if float(dscale[2]) != 0.0:
+            return
+        g = g * dscale[0]
+    d = g + weight_decay * master
+    if mom is not None:
+        mom.mul_(momentum).add_(d)
+        d = mom
+    master.add_(d, alpha=-lr)
+    if param16 is not None:
+        param16.copy_(master)

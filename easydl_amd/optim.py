@@ -1,0 +1,136 @@
+"""Optimizers over :class:`~easydl_amd.parallel.flat.FlatParams`.
+
+``FlatAdamW`` keeps fp32 master weights and fp32 moments as flat buffers next
+to the bf16 model weights (16 B/param of state: Llama-3-8B = 128 GB, which
+fits a single 288 GB MI355X with room for activations — SURVEY.md §2.9), and
+performs the whole update with one fused kernel launch per group after one
+grad-norm/clip reduction whose result never leaves the device.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from easydl_amd.ops.optim import adamw_flat_, grad_clip_scale, sgd_flat_
+from easydl_amd.parallel.flat import FlatParams
+
+
+class LRSchedule:
+    """Linear warmup then cosine decay to ``min_ratio * lr``."""
+
+    def __init__(self, lr: float, warmup: int = 0, total: int = 0, min_ratio: float = 0.1):
+        self.lr, self.warmup, self.total, self.min_ratio = lr, warmup, total, min_ratio
+
+    def __call__(self, step: int) -> float:
+        if self.warmup and step <= self.warmup:
+            return self.lr * step / self.warmup
+        if not self.total or step >= self.total:
+            return self.lr if not self.total else self.lr * self.min_ratio
+        p = (step - self.warmup) / max(1, self.total - self.warmup)
+        return self.lr * (self.min_ratio + (1 - self.min_ratio) * 0.5 * (1 + math.cos(math.pi * p)))
+
+    def state_dict(self):
+        return dict(lr=self.lr, warmup=self.warmup, total=self.total, min_ratio=self.min_ratio)
+
+
+class FlatAdamW:
+    def __init__(self, flat: FlatParams, lr: float = 3e-4, betas=(0.9, 0.95), eps: float = 1e-8,
+                 weight_decay: float | None = None, max_grad_norm: float = 1.0, schedule: LRSchedule | None = None):
+        self.flat = flat
+        self.lr = lr
+        self.beta1, self.beta2 = betas
+        self.eps = eps
+        self.max_grad_norm = max_grad_norm
+        self.schedule = schedule
+        self.step_count = 0
+        self.last_stats = None  # device tensor [coef, norm, nonfinite]
+        self.state = []
+        for g in flat.groups:
+            if weight_decay is not None and g.name == "decay":
+                g.weight_decay = weight_decay
+            has16 = g.data.dtype != torch.float32
+            master = g.data.float() if has16 else g.data
+            self.state.append({
+                "master": master,
+                "m": torch.zeros(g.numel, dtype=torch.float32, device=g.data.device),
+                "v": torch.zeros(g.numel, dtype=torch.float32, device=g.data.device),
+            })
+
+    def current_lr(self) -> float:
+        return self.schedule(self.step_count + 1) if self.schedule else self.lr
+
+    @torch.no_grad()
+    def step(self, pre_scale: float = 1.0) -> torch.Tensor:
+        """Apply one update; ``pre_scale`` multiplies the (summed) gradients, e.g. 1/world."""
+        grads = [g.grad for g in self.flat.groups]
+        stats = grad_clip_scale(grads, self.max_grad_norm, pre_scale)
+        self.step_count += 1
+        lr = self.schedule(self.step_count) if self.schedule else self.lr
+        for g, st in zip(self.flat.groups, self.state):
+            p16 = g.data if g.data.dtype != torch.float32 else None
+            adamw_flat_(p16, st["master"], st["m"], st["v"], g.grad, lr=lr, beta1=self.beta1, beta2=self.beta2,
+                        eps=self.eps, weight_decay=g.weight_decay, step=self.step_count, dscale=stats)
+        self.last_stats = stats
+        return stats
+
+    # -- checkpoint ------------------------------------------------------------
+    def state_tensors(self) -> dict[str, torch.Tensor]:
+        """Flat tensors that fully describe optimizer state (model data excluded)."""
+        out = {}
+        for g, st in zip(self.flat.groups, self.state):
+            if st["master"].data_ptr() != g.data.data_ptr():
+                out[f"opt.{g.name}.master"] = st["master"]
+            out[f"opt.{g.name}.m"] = st["m"]
+            out[f"opt.{g.name}.v"] = st["v"]
+        return out
+
+    def scalars(self) -> dict:
+        return {"step_count": self.step_count, "lr": self.lr}
+
+    def load_scalars(self, d: dict) -> None:
+        self.step_count = int(d["step_count"])
+
+
+class FlatSGD:
+    def __init__(self, flat: FlatParams, lr: float = 0.1, momentum: float = 0.9, weight_decay: float = 0.0,
+                 max_grad_norm: float = 0.0, schedule: LRSchedule | None = None):
+        self.flat = flat
+        self.lr, self.momentum, self.max_grad_norm, self.schedule = lr, momentum, max_grad_norm, schedule
+        self.step_count = 0
+        self.state = []
+        for g in flat.groups:
+            if g.name == "decay":
+                g.weight_decay = weight_decay
+            has16 = g.data.dtype != torch.float32
+            self.state.append({
+                "master": g.data.float() if has16 else g.data,
+                "mom": torch.zeros(g.numel, dtype=torch.float32, device=g.data.device) if momentum else None,
+            })
+
+    @torch.no_grad()
+    def step(self, pre_scale: float = 1.0):
+        grads = [g.grad for g in self.flat.groups]
+        stats = grad_clip_scale(grads, self.max_grad_norm, pre_scale)
+        self.step_count += 1
+        lr = self.schedule(self.step_count) if self.schedule else self.lr
+        for g, st in zip(self.flat.groups, self.state):
+            p16 = g.data if g.data.dtype != torch.float32 else None
+            sgd_flat_(p16, st["master"], st["mom"], g.grad, lr=lr, momentum=self.momentum,
+                      weight_decay=g.weight_decay, dscale=stats)
+        return stats
+
+    def state_tensors(self):
+        out = {}
+        for g, st in zip(self.flat.groups, self.state):
+            if st["master"].data_ptr() != g.data.data_ptr():
+                out[f"opt.{g.name}.master"] = st["master"]
+            if st["mom"] is not None:
+                out[f"opt.{g.name}.mom"] = st["mom"]
+        return out
+
+    def scalars(self):
+        return {"step_count": self.step_count, "lr": self.lr}
+
+    def load_scalars(self, d):
+        self.step_count = int(d["step_count"])

@@ -1,0 +1,168 @@
+"""Flat parameter / gradient storage.
+
+Every trainable parameter of a model is re-homed as a view into ONE contiguous
+buffer per group (weight-decay / no-decay), and its ``.grad`` is preset to a
+view of a matching flat gradient buffer.  Consequences that the rest of the
+framework is built on:
+
+* the optimizer is one kernel launch per group over billions of elements
+  (``csrc/kernels/optim.hip``);
+* DDP buckets are plain contiguous slices of the gradient buffer, so an
+  all-reduce needs no pack/unpack copy (SURVEY.md §2.7 K5 becomes a no-op);
+* an in-memory checkpoint of the whole model+optimizer state is a handful of
+  large contiguous D2H copies (``easydl_amd/ckpt``);
+* state transfer to a joining rank is a few large broadcasts.
+
+Parameters are laid out in *reverse registration order* so gradients, which
+backward produces roughly last-layer-first, fill buckets front to back.  Each
+parameter starts on a 64-element boundary (128 B for bf16) so every view is
+16-byte aligned for the vectorised kernels.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import torch
+
+ALIGN = 64
+
+
+def _roundup(n: int, a: int = ALIGN) -> int:
+    return (n + a - 1) // a * a
+
+
+@dataclass
+class ParamSlot:
+    name: str
+    param: torch.nn.Parameter
+    offset: int
+    numel: int
+    shape: tuple
+
+
+@dataclass
+class FlatGroup:
+    name: str
+    weight_decay: float
+    data: torch.Tensor  # model dtype (bf16 or fp32)
+    grad: torch.Tensor  # grad dtype
+    slots: list[ParamSlot] = field(default_factory=list)
+
+    @property
+    def numel(self) -> int:
+        return self.data.numel()
+
+
+class FlatParams:
+    """Re-home a module's parameters into flat buffers.
+
+    Args:
+        module: the model (already on its target device and dtype).
+        grad_dtype: dtype of the gradient buffers (default: parameter dtype).
+        no_decay: predicate ``(name, param) -> bool`` selecting the no-decay group
+            (default: 1-D parameters, i.e. norms and biases).
+    """
+
+    def __init__(self, module: torch.nn.Module, weight_decay: float = 0.0, grad_dtype: torch.dtype | None = None,
+                 no_decay=None):
+        if no_decay is None:
+            no_decay = lambda n, p: p.ndim < 2  # noqa: E731
+        named = [(n, p) for n, p in module.named_parameters() if p.requires_grad]
+        if not named:
+            raise ValueError("module has no trainable parameters")
+        named.reverse()
+        dtypes = {p.dtype for _, p in named}
+        devices = {p.device for _, p in named}
+        if len(dtypes) != 1 or len(devices) != 1:
+            raise ValueError(f"FlatParams needs one dtype/device, got {dtypes} {devices}")
+        self.dtype = dtypes.pop()
+        self.device = devices.pop()
+        self.grad_dtype = grad_dtype or self.dtype
+        buckets = {"decay": [], "no_decay": []}
+        for n, p in named:
+            buckets["no_decay" if no_decay(n, p) else "decay"].append((n, p))
+        self.groups: list[FlatGroup] = []
+        for gname, plist in buckets.items():
+            if not plist:
+                continue
+            total = sum(_roundup(p.numel()) for _, p in plist)
+            data = torch.zeros(total, dtype=self.dtype, device=self.device)
+            grad = torch.zeros(total, dtype=self.grad_dtype, device=self.device)
+            grp = FlatGroup(gname, weight_decay if gname == "decay" else 0.0, data, grad)
+            off = 0
+            for n, p in plist:
+                k = p.numel()
+                view = data[off:off + k].view(p.shape)
+                with torch.no_grad():
+                    view.copy_(p.data)
+                p.data = view
+                p.grad = grad[off:off + k].view(p.shape)
+                p._edl_flat = True
+                p._edl_fresh = True
+                p._edl_name = n
+                grp.slots.append(ParamSlot(n, p, off, k, tuple(p.shape)))
+                off += _roundup(k)
+            self.groups.append(grp)
+        self.saw_autograd = False
+        # autograd-path parameters (ops that return the gradient) accumulate in place
+        for g in self.groups:
+            for s in g.slots:
+                s.param.register_post_accumulate_grad_hook(self._post_accumulate)
+        self._ready_cb = None
+
+    # -- gradient protocol -------------------------------------------------
+    def _post_accumulate(self, p):
+        self.saw_autograd = True
+        p._edl_fresh = False
+        if self._ready_cb is not None:
+            self._ready_cb(p)
+
+    def set_ready_callback(self, cb) -> None:
+        """``cb(param)`` fires when a parameter's gradient is complete for this backward."""
+        self._ready_cb = cb
+        for g in self.groups:
+            for s in g.slots:
+                s.param._edl_ready_cb = cb
+
+    def zero_grad(self) -> None:
+        """Start a new accumulation window.
+
+        Direct-writing ops overwrite on their first write, so no memset is
+        needed unless an autograd-path parameter accumulated last time.
+        """
+        if self.saw_autograd:
+            for g in self.groups:
+                g.grad.zero_()
+            self.saw_autograd = False
+        for g in self.groups:
+            for s in g.slots:
+                s.param._edl_fresh = True
+                # autograd may have replaced .grad (e.g. set_to_none elsewhere): re-bind
+                if s.param.grad is None or s.param.grad.data_ptr() != g.grad[s.offset:].data_ptr():
+                    s.param.grad = g.grad[s.offset:s.offset + s.numel].view(s.shape)
+
+    def finalize_untouched(self) -> None:
+        """Zero gradients of parameters that received none this window (unused params)."""
+        for g in self.groups:
+            for s in g.slots:
+                if s.param._edl_fresh:
+                    s.param.grad.zero_()
+                    s.param._edl_fresh = False
+
+    # -- views ---------------------------------------------------------------
+    def params(self):
+        for g in self.groups:
+            for s in g.slots:
+                yield s.param
+
+    def named_slots(self):
+        for g in self.groups:
+            for s in g.slots:
+                yield g, s
+
+    @property
+    def numel(self) -> int:
+        return sum(g.numel for g in self.groups)
+
+    def num_params(self) -> int:
+        return sum(s.numel for _, s in self.named_slots())

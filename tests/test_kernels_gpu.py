@@ -1,0 +1,169 @@
+"""HIP kernel numerics vs plain PyTorch fp32 references (run on the GPU box)."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from easydl_amd.ops import fused, norms
+from easydl_amd.ops.optim import adamw_flat_, grad_clip_scale
+
+pytestmark = pytest.mark.gpu
+
+
+def _close(a, b, tol):
+    err = (a.float() - b.float()).abs().max().item()
+    scale = b.float().abs().max().item() + 1e-6
+    assert err <= tol * max(1.0, scale), f"max err {err} (scale {scale})"
+
+
+@pytest.mark.parametrize("rows,cols", [(1, 64), (37, 1024), (256, 4096), (64, 8192), (5, 2056)])
+@pytest.mark.parametrize("fused_res", [False, True])
+def test_rmsnorm_fwd_bwd(cuda, rows, cols, fused_res):
+    torch.manual_seed(0)
+    x = torch.randn(rows, cols, device=cuda, dtype=torch.bfloat16, requires_grad=True)
+    r = torch.randn(rows, cols, device=cuda, dtype=torch.bfloat16, requires_grad=True) if fused_res else None
+    w = (1 + 0.1 * torch.randn(cols, device=cuda)).to(torch.bfloat16).requires_grad_()
+    dy = torch.randn(rows, cols, device=cuda, dtype=torch.bfloat16)
+    ds = torch.randn(rows, cols, device=cuda, dtype=torch.bfloat16) if fused_res else None
+    if fused_res:
+        y, s = norms.add_rmsnorm(x, r, w)
+        (y.float() * dy.float()).sum().add_((s.float() * ds.float()).sum()).backward()
+    else:
+        y = norms.rmsnorm(x, w)
+        (y.float() * dy.float()).sum().backward()
+    gx, gw = x.grad.clone(), w.grad.clone()
+    gr = r.grad.clone() if fused_res else None
+    # fp32 reference
+    xf = x.detach().float().requires_grad_()
+    rf = r.detach().float().requires_grad_() if fused_res else None
+    wf = w.detach().float().requires_grad_()
+    sf = (xf + rf) if fused_res else xf
+    sf_b = sf.to(torch.bfloat16).float() if fused_res else sf
+    yr = sf_b * torch.rsqrt(sf_b.pow(2).mean(-1, keepdim=True) + 1e-5) * wf
+    loss = (yr * dy.float()).sum()
+    if fused_res:
+        loss = loss + (sf * ds.float()).sum()
+    loss.backward()
+    _close(y, yr, 2e-2)
+    _close(gx, xf.grad, 3e-2)
+    _close(gw, wf.grad, 3e-2)
+    if fused_res:
+        _close(gr, rf.grad, 3e-2)
+        _close(s, sf, 1e-2)
+
+
+@pytest.mark.parametrize("rows,cols", [(33, 1024), (128, 768)])
+def test_layernorm_fwd_bwd(cuda, rows, cols):
+    torch.manual_seed(1)
+    x = torch.randn(rows, cols, device=cuda, dtype=torch.bfloat16, requires_grad=True)
+    w = (1 + 0.1 * torch.randn(cols, device=cuda)).to(torch.bfloat16).requires_grad_()
+    b = (0.1 * torch.randn(cols, device=cuda)).to(torch.bfloat16).requires_grad_()
+    dy = torch.randn(rows, cols, device=cuda, dtype=torch.bfloat16)
+    y = norms.layernorm(x, w, b)
+    (y.float() * dy.float()).sum().backward()
+    xf, wf, bf = (t.detach().float().requires_grad_() for t in (x, w, b))
+    yr = F.layer_norm(xf, (cols,), wf, bf, 1e-5)
+    (yr * dy.float()).sum().backward()
+    _close(y, yr, 2e-2)
+    _close(x.grad, xf.grad, 3e-2)
+    _close(w.grad, wf.grad, 3e-2)
+    _close(b.grad, bf.grad, 3e-2)
+
+
+@pytest.mark.parametrize("rows,F_", [(7, 64), (1024, 14336 // 4)])
+def test_swiglu(cuda, rows, F_):
+    torch.manual_seed(2)
+    gu = torch.randn(rows, 2 * F_, device=cuda, dtype=torch.bfloat16, requires_grad=True)
+    d = torch.randn(rows, F_, device=cuda, dtype=torch.bfloat16)
+    o = fused.swiglu(gu)
+    (o.float() * d.float()).sum().backward()
+    g = gu.detach().float().requires_grad_()
+    a, b_ = g.chunk(2, -1)
+    orf = F.silu(a) * b_
+    (orf * d.float()).sum().backward()
+    _close(o, orf, 2e-2)
+    _close(gu.grad, g.grad, 3e-2)
+
+
+@pytest.mark.parametrize("B,S,H,KV,D", [(2, 16, 4, 2, 64), (1, 256, 32, 8, 128)])
+def test_rope_qkv(cuda, B, S, H, KV, D):
+    torch.manual_seed(3)
+    cos, sin = fused.rope_tables(S, D, 500000.0, cuda)
+    qkv = torch.randn(B * S, (H + 2 * KV) * D, device=cuda, dtype=torch.bfloat16, requires_grad=True)
+    q, k, v = fused.rope_qkv(qkv, cos, sin, B, S, H, KV, D)
+    assert q.shape == (B, H, S, D) and k.shape == (B, KV, S, D)
+    dq, dk, dv = torch.randn_like(q), torch.randn_like(k), torch.randn_like(v)
+    ((q.float() * dq.float()).sum() + (k.float() * dk.float()).sum() + (v.float() * dv.float()).sum()).backward()
+    qf = qkv.detach().float().requires_grad_()
+    qr, kr, vr = fused.rope_qkv_ref(qf, cos, sin, B, S, H, KV, D)
+    ((qr * dq.float()).sum() + (kr * dk.float()).sum() + (vr * dv.float()).sum()).backward()
+    _close(q, qr, 2e-2)
+    _close(k, kr, 2e-2)
+    _close(v, vr, 1e-6)
+    _close(qkv.grad, qf.grad, 3e-2)
+
+
+@pytest.mark.parametrize("T,V", [(4, 512), (64, 128256), (3, 1000)])
+def test_cross_entropy(cuda, T, V):
+    torch.manual_seed(4)
+    logits = (3 * torch.randn(T, V, device=cuda)).to(torch.bfloat16)
+    labels = torch.randint(0, V, (T,), device=cuda)
+    labels[0] = -100
+    ref_in = logits.detach().float().requires_grad_()
+    lr = F.cross_entropy(ref_in, labels, ignore_index=-100)
+    lr.backward()
+    x = logits.clone().requires_grad_()
+    loss = fused.cross_entropy(x * 1, labels)  # x*1: kernel consumes a non-leaf buffer
+    loss.backward()
+    assert abs(loss.item() - lr.item()) < 2e-3 * max(1, abs(lr.item()))
+    _close(x.grad, ref_in.grad, 2e-2)
+
+
+@pytest.mark.parametrize("gdt", [torch.bfloat16, torch.float32])
+def test_adamw_flat_matches_torch(cuda, gdt):
+    torch.manual_seed(5)
+    n = 4096 * 33
+    w0 = torch.randn(n, device=cuda)
+    master = w0.clone()
+    p16 = w0.to(torch.bfloat16)
+    m = torch.zeros(n, device=cuda)
+    v = torch.zeros(n, device=cuda)
+    ref = torch.nn.Parameter(w0.clone())
+    opt = torch.optim.AdamW([ref], lr=1e-2, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1)
+    for step in range(1, 4):
+        g = torch.randn(n, device=cuda).to(gdt)
+        adamw_flat_(p16, master, m, v, g, lr=1e-2, beta1=0.9, beta2=0.95, eps=1e-8, weight_decay=0.1, step=step,
+                    scale=0.5)
+        ref.grad = g.float() * 0.5
+        opt.step()
+    _close(master, ref.detach(), 1e-5)
+    _close(p16, ref.detach(), 1e-2)
+
+
+def test_grad_clip(cuda):
+    torch.manual_seed(6)
+    gs = [torch.randn(4096 * 7, device=cuda).to(torch.bfloat16), torch.randn(1024, device=cuda)]
+    out = grad_clip_scale(gs, max_norm=1.0, pre_scale=0.5)
+    norm = math.sqrt(sum(float(g.double().pow(2).sum()) for g in gs)) * 0.5
+    assert abs(out[1].item() - norm) < 1e-3 * norm
+    assert abs(out[0].item() - 0.5 * 1.0 / (norm + 1e-6)) < 1e-4
+    assert out[2].item() == 0
+    gs[1][3] = float("nan")
+    out = grad_clip_scale(gs, max_norm=1.0, pre_scale=0.5)
+    assert out[2].item() == 1
+
+
+def test_linear_direct_grad_into_flat(cuda):
+    from easydl_amd.parallel.flat import FlatParams
+    torch.manual_seed(7)
+    lin = torch.nn.Linear(256, 128, bias=False).to(cuda, torch.bfloat16)
+    ref_w = lin.weight.detach().float().clone().requires_grad_()
+    flat = FlatParams(lin)
+    x = torch.randn(64, 256, device=cuda, dtype=torch.bfloat16)
+    for mb in range(2):  # two micro-batches accumulate
+        y = fused.linear(x, lin.weight)
+        y.float().sum().backward()
+        (x.float() @ ref_w.t()).sum().backward()
+    _close(lin.weight.grad, ref_w.grad, 2e-2)
+    assert lin.weight.grad.data_ptr() == flat.groups[0].grad.data_ptr() + 0
