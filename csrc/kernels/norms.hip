@@ -184,20 +184,28 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(const bf16_t* __restrict_
 }
 
 // out[c] (+)= sum_g partial[g][c]; out dtype bf16 (odt=0) or fp32 (odt=1).
+// Workgroup = 16 column groups (4 columns each, f32x4 loads) x 16 row slices;
+// slices are combined through LDS.  cols % 4 == 0.
 __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ partial, int G, int cols,
                                                      void* __restrict__ out, int odt, int accumulate) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= cols) return;
-  float s = 0.f;
-  for (int g = 0; g < G; ++g) s += partial[(int64_t)g * cols + c];
+  __shared__ f32x4 red[16][16];
+  const int cg = threadIdx.x & 15, sl = threadIdx.x >> 4;
+  const int c = (blockIdx.x * 16 + cg) * 4;
+  f32x4 s = {0.f, 0.f, 0.f, 0.f};
+  if (c < cols)
+    for (int g = sl; g < G; g += 16) s += *reinterpret_cast<const f32x4*>(partial + (int64_t)g * cols + c);
+  red[sl][cg] = s;
+  __syncthreads();
+  if (sl != 0 || c >= cols) return;
+  for (int i = 1; i < 16; ++i) s += red[i][cg];
   if (odt == 0) {
-    bf16_t* o = reinterpret_cast<bf16_t*>(out);
-    if (accumulate) s += bf2f(o[c]);
-    o[c] = f2bf(s);
+    bf16_t* o = reinterpret_cast<bf16_t*>(out) + c;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) o[k] = f2bf(accumulate ? s[k] + bf2f(o[k]) : s[k]);
   } else {
-    float* o = reinterpret_cast<float*>(out);
-    if (accumulate) s += o[c];
-    o[c] = s;
+    float* o = reinterpret_cast<float*>(out) + c;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) o[k] = accumulate ? s[k] + o[k] : s[k];
   }
 }
 
@@ -279,7 +287,8 @@ int edl_layernorm_bwd(const void* dy, const void* x, const void* w, const float*
 }
 
 int edl_colsum(const float* partial, int G, int cols, void* out, int odt, int accumulate, hipStream_t s) {
-  colsum_kernel<<<(cols + 255) / 256, 256, 0, s>>>(partial, G, cols, out, odt, accumulate);
+  if (cols % 4) return (int)hipErrorInvalidValue;
+  colsum_kernel<<<(cols + 63) / 64, 256, 0, s>>>(partial, G, cols, out, odt, accumulate);
   EDL_LAUNCH_CHECK();
   return 0;
 }

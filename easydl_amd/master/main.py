@@ -1,0 +1,109 @@
+"""Job master process (the "master face" of EasyDL's ElasticTrainer:
+reference docs/design/elastic-training-operator.md:105-112).
+
+Hosts the job's TCPStore server and runs:
+* the dynamic-membership :class:`RendezvousManager` (epochs, abort flags);
+* the failure detector inputs: exit events written by the operator's
+  supervisor under ``ev/exit/<node>`` and heartbeats (``hb/<node>``);
+* the plan loop: job features -> Brain startup plan -> JobResource, then
+  periodic re-plans from collected metrics — see
+  :mod:`easydl_amd.master.planner`.
+
+Run: ``python -m easydl_amd.master.main --job NAME --port P [--min 1 --max 8]``.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import logging
+import os
+import signal
+import threading
+import time
+
+from easydl_amd.master.rendezvous import RendezvousConfig, RendezvousManager
+from easydl_amd.master.store import KV, make_tcp_store
+from easydl_amd.utils.events import EventLog
+
+log = logging.getLogger("edl.master")
+
+
+class JobMaster:
+    def __init__(self, job: str, port: int, host: str = "127.0.0.1", rdzv: RendezvousConfig | None = None,
+                 run_dir: str | None = None, planner=None):
+        self.job = job
+        self.host = host
+        self.store = make_tcp_store(host, port, True)
+        self.port = self.store.port
+        self.kv = KV(self.store, f"edl/{job}")
+        self.run_dir = run_dir or os.path.join("runs", job)
+        self.events = EventLog(os.path.join(self.run_dir, "events-master.jsonl"), proc="master")
+        self.rdzv = RendezvousManager(self.kv, rdzv or RendezvousConfig(), events=self.events)
+        self.planner = planner
+        self._stop = threading.Event()
+        self._threads: list[threading.Thread] = []
+
+    # exit events from the operator's supervisor -> immediate death marks
+    def _scan_exit_events(self):
+        for n in self.rdzv.joined():
+            if self.kv.exists(f"ev/exit/{n}") and not self.kv.exists(f"ev/dead/{n}"):
+                info = self.kv.get(f"ev/exit/{n}")
+                self.rdzv.mark_dead(n, f"process exit {info}")
+
+    def _loop(self, period):
+        while not self._stop.is_set():
+            try:
+                self._scan_exit_events()
+                self.rdzv.tick()
+                if self.planner is not None:
+                    self.planner.maybe_replan(self)
+            except Exception as e:
+                log.warning("master tick failed: %s", e)
+            self._stop.wait(period)
+
+    def start(self, period: float = 0.01) -> "JobMaster":
+        t = threading.Thread(target=self._loop, args=(period,), name="edl-master", daemon=True)
+        t.start()
+        self._threads.append(t)
+        self.kv.set("master/info", json.dumps({"host": self.host, "port": self.port, "pid": os.getpid(),
+                                               "ts": time.time()}))
+        self.events.emit("master_started", port=self.port)
+        return self
+
+    def stop(self):
+        self._stop.set()
+        for t in self._threads:
+            t.join(timeout=2)
+
+    def serve_forever(self):
+        try:
+            while not self._stop.wait(0.5):
+                if self.kv.exists("master/shutdown"):
+                    break
+        finally:
+            self.stop()
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--job", default=os.environ.get("EDL_JOB", "job"))
+    ap.add_argument("--host", default="127.0.0.1")
+    ap.add_argument("--port", type=int, default=int(os.environ.get("EDL_MASTER_PORT", 29400)))
+    ap.add_argument("--min", type=int, default=1)
+    ap.add_argument("--max", type=int, default=8)
+    ap.add_argument("--join-window", type=float, default=0.5)
+    ap.add_argument("--hb-timeout", type=float, default=15.0)
+    ap.add_argument("--policy", default="shrink")
+    ap.add_argument("--run-dir", default=os.environ.get("EDL_RUN_DIR"))
+    a = ap.parse_args(argv)
+    logging.basicConfig(level=logging.INFO, format="%(asctime)s [master] %(message)s")
+    cfg = RendezvousConfig(min_nodes=a.min, max_nodes=a.max, join_window_s=a.join_window,
+                           heartbeat_timeout_s=a.hb_timeout, policy=a.policy)
+    m = JobMaster(a.job, a.port, a.host, cfg, a.run_dir).start()
+    signal.signal(signal.SIGTERM, lambda *_: m._stop.set())
+    print(json.dumps({"master_port": m.port}), flush=True)
+    m.serve_forever()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,82 @@
+"""Structured event timeline (JSONL) used for time-to-recover accounting.
+
+Every process appends ``{"ts": wall, "mono": monotonic, "kind": ..., ...}``
+records to ``<run_dir>/events-<proc>.jsonl``; wall-clock stamps from processes
+on the same host are directly comparable, which is what the TTR breakdown
+(fault -> detect -> abort -> rendezvous -> comm init -> state sync -> first
+step) uses.
+"""
+from __future__ import annotations
+
+import json
+import os
+import threading
+import time
+
+
+class EventLog:
+    def __init__(self, path: str | None = None, proc: str = "", echo: bool = False):
+        self.path = path
+        self.proc = proc
+        self.echo = echo
+        self._lock = threading.Lock()
+        self.records: list[dict] = []
+        if path:
+            os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+
+    def emit(self, kind: str, **kw) -> dict:
+        rec = {"ts": time.time(), "mono": time.monotonic(), "proc": self.proc, "kind": kind}
+        rec.update(kw)
+        with self._lock:
+            self.records.append(rec)
+            if self.path:
+                with open(self.path, "a") as f:
+                    f.write(json.dumps(rec, default=str) + "\n")
+        if self.echo:
+            print(f"[event] {json.dumps(rec, default=str)}", flush=True)
+        return rec
+
+    def last(self, kind: str) -> dict | None:
+        for r in reversed(self.records):
+            if r["kind"] == kind:
+                return r
+        return None
+
+
+def read_events(run_dir: str) -> list[dict]:
+    out = []
+    if not os.path.isdir(run_dir):
+        return out
+    for fn in sorted(os.listdir(run_dir)):
+        if fn.startswith("events") and fn.endswith(".jsonl"):
+            with open(os.path.join(run_dir, fn)) as f:
+                for line in f:
+                    line = line.strip()
+                    if line:
+                        out.append(json.loads(line))
+    out.sort(key=lambda r: r["ts"])
+    return out
+
+
+def ttr_breakdown(events: list[dict]) -> dict | None:
+    """Time-to-recover phases relative to the first injected fault."""
+    fault = next((e for e in events if e["kind"] == "fault_injected"), None)
+    if fault is None:
+        return None
+    t0 = fault["ts"]
+    after = [e for e in events if e["ts"] >= t0]
+
+    def first(kind, pred=lambda e: True):
+        r = next((e for e in after if e["kind"] == kind and pred(e)), None)
+        return None if r is None else round(r["ts"] - t0, 4)
+
+    out = {
+        "detect_s": first("node_dead"),
+        "abort_s": first("epoch_abort"),
+        "epoch_formed_s": first("epoch_formed"),
+        "comm_ready_s": first("comm_ready"),
+        "state_synced_s": first("state_synced"),
+        "first_step_s": first("step_done"),
+    }
+    out["ttr_s"] = out["first_step_s"]
+    return out

@@ -1,0 +1,36 @@
+"""Worker script for multi-process elastic tests (CPU/gloo).
+
+Env: EDL_* contract (or torchrun-style RANK/WORLD_SIZE/MASTER_*), plus
+TEST_STEPS, TEST_GB (global batch), TEST_OUT (result json path).
+"""
+import hashlib
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+
+from easydl_amd.models.llama import Llama, get_config  # noqa: E402
+from easydl_amd.trainer.data import SyntheticTokens  # noqa: E402
+from easydl_amd.trainer.elastic import ElasticTrainer  # noqa: E402
+
+torch.set_num_threads(1)
+cfg = get_config("llama-tiny", n_layers=1, dim=64, n_heads=4, n_kv_heads=2, ffn_dim=128, vocab_size=128)
+steps = int(os.environ.get("TEST_STEPS", 8))
+gb = int(os.environ.get("TEST_GB", 6))
+tr = ElasticTrainer(lambda dev: Llama(cfg, device=dev, dtype=torch.float32), global_batch=gb, micro_batch=2,
+                    lr=1e-3, device="cpu")
+tr.fit(lambda m, b: m(*b), SyntheticTokens(cfg.vocab_size, 16, num_samples=4096), num_steps=steps,
+       on_step=lambda t, l: time.sleep(float(os.environ.get("TEST_STEP_SLEEP", 0))))
+h = hashlib.sha256()
+for g in tr.flat.groups:
+    h.update(g.data.numpy().tobytes())
+res = {"index": tr.ctx.index, "step": tr.step, "hash": h.hexdigest(),
+       "worlds": [r["world"] for r in tr.history], "epochs": [r["epoch"] for r in tr.history],
+       "loss": float(tr.last_loss) if tr.last_loss is not None else None}
+with open(os.environ["TEST_OUT"], "w") as f:
+    json.dump(res, f)
+tr.close()

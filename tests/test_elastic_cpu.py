@@ -1,0 +1,129 @@
+"""Multi-process elastic training on CPU/gloo: static world, kill-a-worker shrink,
+scale-up join.  Processes are real (subprocess), the store is a real TCPStore."""
+import json
+import os
+import socket
+import subprocess
+import sys
+import time
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+WORKER = os.path.join(ROOT, "tests", "helpers", "elastic_worker.py")
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _env(tmp, idx, extra):
+    e = dict(os.environ)
+    e.update({"EDL_JOB": "t", "EDL_ROLE": "worker", "EDL_INDEX": str(idx), "EDL_RUN_DIR": str(tmp),
+              "TEST_OUT": str(tmp / f"res{idx}.json"), "OMP_NUM_THREADS": "1", "PYTHONPATH": ROOT})
+    e.pop("WORLD_SIZE", None)
+    e.update(extra)
+    return e
+
+
+def _start_master(tmp, port, mn, mx, window=0.3):
+    return subprocess.Popen([sys.executable, "-m", "easydl_amd.master.main", "--job", "t", "--port", str(port),
+                             "--min", str(mn), "--max", str(mx), "--join-window", str(window),
+                             "--run-dir", str(tmp)], cwd=ROOT, env=dict(os.environ, PYTHONPATH=ROOT),
+                            stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+
+
+def _results(tmp, idxs):
+    return {i: json.load(open(tmp / f"res{i}.json")) for i in idxs}
+
+
+def _wait(procs, timeout=240):
+    t_end = time.time() + timeout
+    codes = {}
+    for i, p in procs.items():
+        try:
+            codes[i] = p.wait(timeout=max(1, t_end - time.time()))
+        except subprocess.TimeoutExpired:
+            p.kill()
+            codes[i] = "timeout"
+    return codes
+
+
+@pytest.mark.slow
+def test_torchrun_style_static_world(tmp_path):
+    port = free_port()
+    procs = {}
+    for i in range(2):
+        env = _env(tmp_path, i, {"RANK": str(i), "WORLD_SIZE": "2", "MASTER_ADDR": "127.0.0.1",
+                                 "MASTER_PORT": str(port), "TEST_STEPS": "5", "TEST_GB": "4"})
+        env.pop("EDL_INDEX")
+        procs[i] = subprocess.Popen([sys.executable, WORKER], env=env, cwd=ROOT)
+    codes = _wait(procs)
+    assert codes == {0: 0, 1: 0}, codes
+    r = _results(tmp_path, [0, 1])
+    assert r[0]["hash"] == r[1]["hash"]
+    assert r[0]["step"] == 5 and r[0]["worlds"] == [2] * 5
+
+
+@pytest.mark.slow
+def test_kill_worker_shrinks_and_continues(tmp_path):
+    port = free_port()
+    m = _start_master(tmp_path, port, 1, 3)
+    try:
+        procs = {}
+        for i in range(3):
+            env = _env(tmp_path, i, {"EDL_MASTER_ADDR": "127.0.0.1", "EDL_MASTER_PORT": str(port),
+                                     "TEST_STEPS": "8", "TEST_GB": "6",
+                                     "EDL_FAULT": "kill@step=3,index=2"})
+            procs[i] = subprocess.Popen([sys.executable, WORKER], env=env, cwd=ROOT)
+        # emulate the operator's supervisor: report the exit event
+        t_end = time.time() + 240
+        reported = False
+        while time.time() < t_end and not reported:
+            rc = procs[2].poll()
+            if rc is not None:
+                from easydl_amd.master.store import KV, make_tcp_store
+                kv = KV(make_tcp_store("127.0.0.1", port, False), "edl/t")
+                node = [n for n in (kv.get_str("rdzv/joined") or "").split(",") if n.startswith("t-worker-2:")][0]
+                kv.set(f"ev/exit/{node}", json.dumps({"code": rc}))
+                reported = True
+            time.sleep(0.05)
+        codes = _wait({0: procs[0], 1: procs[1]})
+        assert codes == {0: 0, 1: 0}, codes
+        r = _results(tmp_path, [0, 1])
+        assert r[0]["hash"] == r[1]["hash"], "survivors diverged"
+        assert r[0]["step"] == 8
+        assert r[0]["worlds"][0] == 3 and r[0]["worlds"][-1] == 2
+        from easydl_amd.utils.events import read_events, ttr_breakdown
+        ttr = ttr_breakdown(read_events(str(tmp_path)))
+        assert ttr is not None and ttr["ttr_s"] is not None and ttr["ttr_s"] < 60, ttr
+    finally:
+        m.terminate()
+
+
+@pytest.mark.slow
+def test_scale_up_joiner_receives_state(tmp_path):
+    port = free_port()
+    m = _start_master(tmp_path, port, 1, 3, window=0.2)
+    try:
+        procs = {}
+        for i in range(2):
+            env = _env(tmp_path, i, {"EDL_MASTER_ADDR": "127.0.0.1", "EDL_MASTER_PORT": str(port),
+                                     "TEST_STEPS": "30", "TEST_GB": "6", "TEST_STEP_SLEEP": "0.25"})
+            procs[i] = subprocess.Popen([sys.executable, WORKER], env=env, cwd=ROOT)
+        time.sleep(4.0)
+        env = _env(tmp_path, 2, {"EDL_MASTER_ADDR": "127.0.0.1", "EDL_MASTER_PORT": str(port),
+                                 "TEST_STEPS": "30", "TEST_GB": "6", "TEST_STEP_SLEEP": "0.25"})
+        procs[2] = subprocess.Popen([sys.executable, WORKER], env=env, cwd=ROOT)
+        codes = _wait(procs)
+        assert codes == {0: 0, 1: 0, 2: 0}, codes
+        r = _results(tmp_path, [0, 1, 2])
+        assert r[0]["hash"] == r[1]["hash"] == r[2]["hash"]
+        assert 3 in r[0]["worlds"], r[0]["worlds"]
+        assert r[2]["step"] == 30
+    finally:
+        m.terminate()
