@@ -6,15 +6,18 @@ DDP 1->8 GPUs``).  One process per GPU; for N>1 the driver launches this file
 with ``torch.distributed.run`` and every rank reads RANK / LOCAL_RANK /
 WORLD_SIZE / MASTER_ADDR / MASTER_PORT from the environment.
 
-Each timed step is a COMPLETE training step of the full 32-layer Llama-3-8B
-architecture (random init, synthetic tokens): forward, backward with the
-bucketed RCCL all-reduce overlapped, global grad-norm clip and the fused
-AdamW update of all 8.03e9 parameters (fp32 master + moments).  W untimed
-warmup steps, then exactly K steps bracketed by barrier + synchronize; the
-elapsed time is the MAX over ranks; rank 0 prints one JSON line.
+The timed loop IS the framework's elastic training loop
+(:class:`easydl_amd.trainer.elastic.ElasticTrainer`): rank 0 embeds the
+rendezvous master on torchrun's store, every step runs forward, backward
+with the bucketed RCCL all-reduce overlapped, the store-coordinated step
+commit, the global grad-norm clip and the fused AdamW update of all 8.03e9
+parameters (fp32 master + moments) of the full 32-layer Llama-3-8B (random
+init, synthetic tokens).  W untimed warmup steps, then exactly K steps
+bracketed by barrier + synchronize; the elapsed time is the MAX over ranks;
+rank 0 prints one JSON line.
 
-``--fault-inject`` additionally measures time-to-recover (see
-``easydl_amd/trainer/fault_bench.py``) — not part of the default run.
+``--fault-inject`` (not part of the default run) measures time-to-recover with
+the local operator: see ``easydl_amd/trainer/fault_bench.py``.
 """
 from __future__ import annotations
 
@@ -35,16 +38,19 @@ def parse():
     ap.add_argument("--model", default="llama3-8b")
     ap.add_argument("--seq", type=int, default=8192)
     ap.add_argument("--mbs", type=int, default=1, help="sequences per micro-batch per GPU")
-    ap.add_argument("--accum", type=int, default=1, help="micro-batches per step")
+    ap.add_argument("--accum", type=int, default=1, help="micro-batches per step per GPU")
     ap.add_argument("--bucket-mb", type=float, default=None)
     ap.add_argument("--layers", type=int, default=None, help="override layer count (debug only; invalid for the metric)")
-    ap.add_argument("--profile-steps", type=int, default=0)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--fault-inject", action="store_true", help="measure time-to-recover instead (local operator)")
     return ap.parse_args()
 
 
 def main():
     args = parse()
+    if args.fault_inject:
+        from easydl_amd.trainer import fault_bench
+        return fault_bench.main(args)
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
@@ -52,97 +58,56 @@ def main():
         print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
     use_cuda = torch.cuda.is_available()
     dev = torch.device("cuda", local) if use_cuda else torch.device("cpu")
-    if use_cuda:
-        torch.cuda.set_device(dev)
+    os.environ.setdefault("EDL_JOB", "bench")
+    os.environ.setdefault("EDL_RUN_DIR", os.path.join("gpurun_out", "bench_run") if use_cuda else "/tmp/edl_bench")
 
     from easydl_amd.models.llama import Llama, get_config
-    from easydl_amd.optim import FlatAdamW
-    from easydl_amd.parallel.comm import Communicator, LocalCommunicator
-    from easydl_amd.parallel.ddp import ElasticDDP
-    from easydl_amd.parallel.flat import FlatParams
+    from easydl_amd.trainer.data import SyntheticTokens
+    from easydl_amd.trainer.elastic import ElasticTrainer
 
-    comm = LocalCommunicator(dev)
-    if world > 1:
-        import torch.distributed as dist
-        import datetime
-        addr = os.environ.get("MASTER_ADDR", "127.0.0.1")
-        port = int(os.environ.get("MASTER_PORT", 29500))
-        agent_store = os.environ.get("TORCHELASTIC_USE_AGENT_STORE", "") in ("True", "true", "1")
-        store = dist.TCPStore(addr, port, world, is_master=(rank == 0 and not agent_store),
-                              timeout=datetime.timedelta(seconds=300))
-        comm = Communicator(store, rank, world, epoch=0, device=dev, job="bench")
-        comm.warmup()
-
-    overrides = {}
-    if args.layers:
-        overrides["n_layers"] = args.layers
+    overrides = {"n_layers": args.layers} if args.layers else {}
     cfg = get_config(args.model, **overrides)
-    torch.manual_seed(1234)  # identical init on every rank (also re-broadcast below)
-    model = Llama(cfg, device=dev, dtype=torch.bfloat16 if use_cuda else torch.float32)
-    flat = FlatParams(model, weight_decay=0.1)
-    ddp = ElasticDDP(flat, comm, bucket_mb=args.bucket_mb)
-    ddp.broadcast_params(0)
-    opt = FlatAdamW(flat, lr=3e-4, betas=(0.9, 0.95), weight_decay=0.1, max_grad_norm=1.0)
-
+    dtype = torch.bfloat16 if use_cuda else torch.float32
     S, B = args.seq, args.mbs
-    g = torch.Generator(device=dev)
-    g.manual_seed(42 + rank)
-    batches = [(torch.randint(0, cfg.vocab_size, (B, S), device=dev, generator=g),
-                torch.randint(0, cfg.vocab_size, (B, S), device=dev, generator=g)) for _ in range(2)]
+    gb = world * B * args.accum
+    tr = ElasticTrainer(lambda d: Llama(cfg, device=d, dtype=dtype), lr=3e-4, betas=(0.9, 0.95), weight_decay=0.1,
+                        max_grad_norm=1.0, global_batch=gb, micro_batch=B, device=dev, bucket_mb=args.bucket_mb)
+    marks = {}
 
-    def train_step(i):
-        flat.zero_grad()
-        for a in range(args.accum):
-            ids, labels = batches[(i + a) % 2]
-            if a < args.accum - 1:
-                with ddp.no_sync():
-                    loss = model(ids, labels)
-                    loss.backward()
-            else:
-                loss = model(ids, labels)
-                loss.backward()
-        ddp.finish()
-        opt.step(pre_scale=1.0 / (comm.world_size * args.accum))
-        return loss
-
-    def sync():
+    def sync_barrier(t):
         if use_cuda:
             torch.cuda.synchronize(dev)
-        comm.barrier()
+        t.comm.barrier()
 
-    t_w = time.perf_counter()
-    for i in range(args.warmup):
-        loss = train_step(i)
-    sync()
-    warm_s = time.perf_counter() - t_w
-    if args.profile_steps:
-        for i in range(args.profile_steps):
-            train_step(i)
-        sync()
+    def on_step(t, loss):
+        if t.step == args.warmup:
+            sync_barrier(t)
+            marks["t0"] = time.perf_counter()
+            marks["warm_end"] = time.perf_counter()
+        if t.step == args.warmup + args.steps:
+            sync_barrier(t)
+            marks["t1"] = time.perf_counter()
 
-    sync()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        loss = train_step(i)
-    sync()
-    el = time.perf_counter() - t0
-    el_max = float(comm.ctrl_all_reduce([el], op=__import__("torch.distributed", fromlist=["ReduceOp"]).ReduceOp.MAX)[0]) \
-        if world > 1 else el
-    loss_v = float(loss)
+    t_start = time.perf_counter()
+    tr.fit(lambda m, b: m(*b), SyntheticTokens(cfg.vocab_size, S), num_steps=args.warmup + args.steps,
+           on_step=on_step)
+    comm = tr.comm
+    el = marks["t1"] - marks["t0"]
+    if comm.world_size > 1:
+        import torch.distributed as dist
+        el = float(comm.ctrl_all_reduce([el], op=dist.ReduceOp.MAX)[0])
     tokens = comm.world_size * B * S * args.accum * args.steps
-    tps = tokens / el_max
-    ms = el_max / args.steps * 1e3
+    tps = tokens / el
     fpt = cfg.flops_per_token(S)
     tflops_gpu = tps / comm.world_size * fpt / 1e12
-    mem_gb = torch.cuda.max_memory_allocated(dev) / 2**30 if use_cuda else 0.0
     res = {
-        "metric": "tokens/sec, Llama-3-8B elastic DDP (full train step: fwd+bwd+allreduce+AdamW)",
+        "metric": "tokens/sec, Llama-3-8B elastic DDP (full train step: fwd+bwd+allreduce+commit+AdamW)",
         "value": round(tps, 2),
         "unit": "tokens/s",
         "n_gpus": comm.world_size,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(ms, 3),
+        "ms_per_step": round(el / args.steps * 1e3, 3),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -150,28 +115,28 @@ def main():
         "data": "synthetic (random token ids), random-init weights",
         "config": {
             "model": args.model if not args.layers else f"{args.model}-L{args.layers}",
-            "global_batch": comm.world_size * B * args.accum,
+            "global_batch": gb,
             "seq_len": S,
             "parallelism": f"dp{comm.world_size}",
             "micro_batch": B,
             "grad_accum": args.accum,
             "optimizer": "AdamW fp32 master/moments, clip 1.0",
-            "bucket_mb": ddp.bucket_mb,
+            "bucket_mb": tr.ddp.bucket_mb,
         },
         "tflops_per_gpu": round(tflops_gpu, 1),
         "mfu_vs_2.5PF": round(tflops_gpu / 2500.0, 4),
-        "loss": round(loss_v, 4),
-        "peak_mem_gb": round(mem_gb, 1),
-        "warmup_s": round(warm_s, 2),
+        "loss": round(float(tr.last_loss), 4) if tr.last_loss is not None else None,
+        "peak_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 2**30, 1) if use_cuda else 0.0,
+        "setup_and_warmup_s": round(marks["t0"] - t_start, 2),
         "time_to_recover_s": None,
     }
-    if rank == 0:
+    if comm.rank == 0:
         line = json.dumps(res)
         print(line, flush=True)
         if args.out:
             with open(args.out, "w") as f:
                 f.write(line + "\n")
-    comm.shutdown()
+    tr.close()
 
 
 if __name__ == "__main__":

@@ -1,0 +1,421 @@
+// Shared-memory checkpoint store + asynchronous D2H snapshot engine
+// (SURVEY.md §2.4 N10, §3 CS7, §5.4).
+//
+// Segment  /dev/shm/<name>  (owned by the operator, so it survives worker death):
+//   [SegHdr 4 KiB][SlotHdr x nslots, 4 KiB each][slot 0 data][slot 1 data]...
+// Slots are A/B double-buffered: a snapshot always writes the slot that is NOT
+// current, then publishes {step, epoch, nbytes, checksum, meta} in the slot
+// header, sets state=COMMITTED and finally flips `current` — a writer that
+// dies mid-copy leaves the previous committed slot untouched (torn-write
+// safe).  Slot data is page-locked with hipHostRegister so the copies run as
+// SDMA transfers at PCIe rate.
+//
+// Snapshot engine: a low-priority HIP stream per device.  A snapshot records
+// an event on the caller's compute stream, makes the side stream wait on it,
+// enqueues chunked hipMemcpyAsync D2H copies into the free slot and records a
+// completion event; a committer thread waits for that event and publishes the
+// slot.  The caller makes its NEXT optimizer step wait on the completion
+// event (edl_ckpt_fence), so the copy overlaps forward/backward and never
+// reads a half-updated parameter.
+#include <errno.h>
+#include <fcntl.h>
+#include <hip/hip_runtime_api.h>
+#include <stdint.h>
+#include <string.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <time.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <condition_variable>
+#include <deque>
+#include <map>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+namespace {
+
+constexpr uint64_t kHdr = 4096;
+constexpr uint32_t kEmpty = 0, kWriting = 1, kCommitted = 2;
+
+struct SegHdr {
+  char magic[8];
+  uint64_t version;
+  uint64_t slot_bytes;
+  uint32_t nslots;
+  int32_t current;  // committed slot or -1
+  uint64_t gen;     // incremented on every commit
+};
+
+struct SlotHdr {
+  uint64_t seq;
+  int64_t step;
+  int64_t epoch;
+  uint64_t nbytes;
+  uint64_t checksum;
+  int64_t ts_ns;
+  uint32_t state;
+  uint32_t pad;
+  char meta[4096 - 56];
+};
+static_assert(sizeof(SlotHdr) == 4096, "slot header must be 4 KiB");
+
+struct Seg {
+  std::string name;
+  int fd = -1;
+  uint8_t* base = nullptr;
+  uint64_t total = 0;
+  bool pinned = false;
+  SegHdr* hdr() { return reinterpret_cast<SegHdr*>(base); }
+  SlotHdr* slot(int i) { return reinterpret_cast<SlotHdr*>(base + kHdr * (1 + i)); }
+  uint8_t* data(int i) {
+    return base + kHdr * (1 + hdr()->nslots) + (uint64_t)i * hdr()->slot_bytes;
+  }
+};
+
+int64_t now_ns() {
+  timespec ts;
+  clock_gettime(CLOCK_REALTIME, &ts);
+  return (int64_t)ts.tv_sec * 1000000000LL + ts.tv_nsec;
+}
+
+uint64_t round_up(uint64_t v, uint64_t a) { return (v + a - 1) / a * a; }
+
+}  // namespace
+
+extern "C" {
+
+// create=1: create (or resize) the segment; create=0: open an existing one.
+void* edl_shm_open(const char* name, uint64_t slot_bytes, int nslots, int create) {
+  if (!name) return nullptr;
+  auto* s = new Seg();
+  s->name = name;
+  int flags = O_RDWR | (create ? O_CREAT : 0);
+  s->fd = shm_open(name, flags, 0600);
+  if (s->fd < 0) {
+    delete s;
+    return nullptr;
+  }
+  if (create) {
+    if (nslots <= 0) nslots = 2;
+    slot_bytes = round_up(slot_bytes ? slot_bytes : 4096, 2 << 20);
+    s->total = kHdr * (1 + nslots) + slot_bytes * nslots;
+    struct stat st;
+    fstat(s->fd, &st);
+    bool fresh = (uint64_t)st.st_size != s->total;
+    if (fresh && ftruncate(s->fd, (off_t)s->total) != 0) {
+      close(s->fd);
+      delete s;
+      return nullptr;
+    }
+    s->base = (uint8_t*)mmap(nullptr, s->total, PROT_READ | PROT_WRITE, MAP_SHARED, s->fd, 0);
+    if (s->base == MAP_FAILED) {
+      close(s->fd);
+      delete s;
+      return nullptr;
+    }
+    SegHdr* h = s->hdr();
+    if (fresh || memcmp(h->magic, "EDLSHM01", 8) != 0 || h->slot_bytes != slot_bytes) {
+      memset(s->base, 0, kHdr * (1 + nslots));
+      memcpy(h->magic, "EDLSHM01", 8);
+      h->version = 1;
+      h->slot_bytes = slot_bytes;
+      h->nslots = (uint32_t)nslots;
+      h->current = -1;
+      h->gen = 0;
+    }
+  } else {
+    struct stat st;
+    if (fstat(s->fd, &st) != 0 || (uint64_t)st.st_size < kHdr) {
+      close(s->fd);
+      delete s;
+      return nullptr;
+    }
+    s->total = (uint64_t)st.st_size;
+    s->base = (uint8_t*)mmap(nullptr, s->total, PROT_READ | PROT_WRITE, MAP_SHARED, s->fd, 0);
+    if (s->base == MAP_FAILED || memcmp(s->hdr()->magic, "EDLSHM01", 8) != 0) {
+      close(s->fd);
+      delete s;
+      return nullptr;
+    }
+  }
+  return s;
+}
+
+// Page-lock every slot for DMA (idempotent).  Returns a hipError_t.
+int edl_shm_pin(void* h) {
+  auto* s = static_cast<Seg*>(h);
+  if (s->pinned) return 0;
+  uint8_t* d0 = s->data(0);
+  uint64_t bytes = s->hdr()->slot_bytes * s->hdr()->nslots;
+  hipError_t e = hipHostRegister(d0, bytes, hipHostRegisterPortable);
+  if (e == hipSuccess) s->pinned = true;
+  return (int)e;
+}
+
+void* edl_shm_data(void* h, int slot) { return static_cast<Seg*>(h)->data(slot); }
+uint64_t edl_shm_slot_bytes(void* h) { return static_cast<Seg*>(h)->hdr()->slot_bytes; }
+int edl_shm_nslots(void* h) { return (int)static_cast<Seg*>(h)->hdr()->nslots; }
+int edl_shm_current(void* h) { return __atomic_load_n(&static_cast<Seg*>(h)->hdr()->current, __ATOMIC_ACQUIRE); }
+
+// Claim the slot to write next (never the current one) and mark it WRITING.
+int edl_shm_begin(void* h) {
+  auto* s = static_cast<Seg*>(h);
+  int cur = edl_shm_current(h);
+  int n = (int)s->hdr()->nslots;
+  int slot = (cur + 1) % n;
+  if (slot < 0) slot = 0;
+  __atomic_store_n(&s->slot(slot)->state, kWriting, __ATOMIC_RELEASE);
+  return slot;
+}
+
+int edl_shm_commit(void* h, int slot, int64_t step, int64_t epoch, uint64_t nbytes, uint64_t checksum,
+                   const char* meta) {
+  auto* s = static_cast<Seg*>(h);
+  if (slot < 0 || slot >= (int)s->hdr()->nslots) return -EINVAL;
+  if (nbytes > s->hdr()->slot_bytes) return -E2BIG;
+  SlotHdr* sh = s->slot(slot);
+  sh->step = step;
+  sh->epoch = epoch;
+  sh->nbytes = nbytes;
+  sh->checksum = checksum;
+  sh->ts_ns = now_ns();
+  memset(sh->meta, 0, sizeof(sh->meta));
+  if (meta) strncpy(sh->meta, meta, sizeof(sh->meta) - 1);
+  sh->seq = s->hdr()->gen + 1;
+  __atomic_store_n(&sh->state, kCommitted, __ATOMIC_RELEASE);
+  __atomic_store_n(&s->hdr()->current, slot, __ATOMIC_RELEASE);
+  __atomic_add_fetch(&s->hdr()->gen, 1, __ATOMIC_ACQ_REL);
+  msync(s->base, kHdr * (1 + s->hdr()->nslots), MS_ASYNC);
+  return 0;
+}
+
+// Latest committed slot (or -1) and its header fields.
+int edl_shm_latest(void* h, int64_t* step, int64_t* epoch, uint64_t* nbytes, uint64_t* checksum, char* meta,
+                   int metalen) {
+  auto* s = static_cast<Seg*>(h);
+  int cur = edl_shm_current(h);
+  if (cur < 0) return -1;
+  SlotHdr* sh = s->slot(cur);
+  if (__atomic_load_n(&sh->state, __ATOMIC_ACQUIRE) != kCommitted) return -1;
+  if (step) *step = sh->step;
+  if (epoch) *epoch = sh->epoch;
+  if (nbytes) *nbytes = sh->nbytes;
+  if (checksum) *checksum = sh->checksum;
+  if (meta && metalen > 0) {
+    strncpy(meta, sh->meta, (size_t)metalen - 1);
+    meta[metalen - 1] = 0;
+  }
+  return cur;
+}
+
+int edl_shm_close(void* h, int unlink_seg) {
+  auto* s = static_cast<Seg*>(h);
+  if (!s) return 0;
+  if (s->pinned) hipHostUnregister(s->data(0));
+  munmap(s->base, s->total);
+  close(s->fd);
+  if (unlink_seg) shm_unlink(s->name.c_str());
+  delete s;
+  return 0;
+}
+
+int edl_shm_unlink(const char* name) { return shm_unlink(name) == 0 ? 0 : -errno; }
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// asynchronous snapshot engine
+// ---------------------------------------------------------------------------
+namespace {
+
+struct Job {
+  int64_t ticket;
+  Seg* seg;
+  int slot;
+  int64_t step, epoch;
+  uint64_t nbytes;
+  int64_t checksum_off;
+  std::string meta;
+  hipEvent_t done;
+};
+
+struct Engine {
+  int device = 0;
+  hipStream_t side = nullptr;
+  std::thread committer;
+  std::mutex mu;
+  std::condition_variable cv;
+  std::deque<Job> queue;
+  std::map<int64_t, int> status;         // 0 pending, 1 committed, <0 error
+  std::map<int64_t, hipEvent_t> events;  // completion events (for fences)
+  int64_t next = 1;
+  bool stop = false;
+  uint64_t chunk = 256ull << 20;
+};
+
+void commit_loop(Engine* e) {
+  hipSetDevice(e->device);
+  for (;;) {
+    Job j;
+    {
+      std::unique_lock<std::mutex> g(e->mu);
+      e->cv.wait(g, [&] { return e->stop || !e->queue.empty(); });
+      if (e->queue.empty()) return;
+      j = e->queue.front();
+      e->queue.pop_front();
+    }
+    hipError_t err = hipEventSynchronize(j.done);
+    int st = 1;
+    if (err != hipSuccess) {
+      st = -(int)err;
+    } else {
+      uint64_t cs = 0;
+      if (j.checksum_off >= 0) memcpy(&cs, j.seg->data(j.slot) + j.checksum_off, sizeof(cs));
+      if (edl_shm_commit(j.seg, j.slot, j.step, j.epoch, j.nbytes, cs, j.meta.c_str()) != 0) st = -1;
+    }
+    std::lock_guard<std::mutex> g(e->mu);
+    e->status[j.ticket] = st;
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+void* edl_ckpt_engine_create(int device, uint64_t chunk_bytes) {
+  auto* e = new Engine();
+  e->device = device;
+  if (chunk_bytes) e->chunk = chunk_bytes;
+  if (hipSetDevice(device) != hipSuccess) {
+    delete e;
+    return nullptr;
+  }
+  int lo = 0, hi = 0;
+  hipDeviceGetStreamPriorityRange(&lo, &hi);  // lo = least priority
+  if (hipStreamCreateWithPriority(&e->side, hipStreamNonBlocking, lo) != hipSuccess) {
+    delete e;
+    return nullptr;
+  }
+  e->committer = std::thread(commit_loop, e);
+  return e;
+}
+
+// Enqueue a snapshot of nbuf device buffers into the free slot of `seg`.
+// dev_ptrs/sizes/offsets: per buffer source pointer, byte size, byte offset in
+// the slot.  after_stream: the compute stream whose current position marks the
+// consistent state.  checksum_off: slot offset of an 8-byte checksum that is
+// part of the copied buffers (published in the header), or -1.
+// Returns a ticket (>0) or a negative hipError_t.
+int64_t edl_ckpt_snapshot(void* eng, void* seg, int nbuf, const uint64_t* dev_ptrs, const uint64_t* sizes,
+                          const uint64_t* offsets, hipStream_t after_stream, int64_t step, int64_t epoch,
+                          int64_t checksum_off, const char* meta) {
+  auto* e = static_cast<Engine*>(eng);
+  auto* s = static_cast<Seg*>(seg);
+  hipSetDevice(e->device);
+  uint64_t total = 0;
+  for (int i = 0; i < nbuf; ++i) {
+    if (offsets[i] + sizes[i] > s->hdr()->slot_bytes) return -(int64_t)hipErrorInvalidValue;
+    if (offsets[i] + sizes[i] > total) total = offsets[i] + sizes[i];
+  }
+  int slot = edl_shm_begin(s);
+  hipEvent_t ready, done;
+  hipEventCreateWithFlags(&ready, hipEventDisableTiming);
+  hipEventCreateWithFlags(&done, hipEventDisableTiming);
+  hipError_t err = hipEventRecord(ready, after_stream);
+  if (err == hipSuccess) err = hipStreamWaitEvent(e->side, ready, 0);
+  uint8_t* dst = s->data(slot);
+  for (int i = 0; i < nbuf && err == hipSuccess; ++i) {
+    for (uint64_t off = 0; off < sizes[i] && err == hipSuccess; off += e->chunk) {
+      uint64_t n = sizes[i] - off < e->chunk ? sizes[i] - off : e->chunk;
+      err = hipMemcpyAsync(dst + offsets[i] + off, (const uint8_t*)dev_ptrs[i] + off, n, hipMemcpyDeviceToHost,
+                           e->side);
+    }
+  }
+  if (err == hipSuccess) err = hipEventRecord(done, e->side);
+  hipEventDestroy(ready);
+  if (err != hipSuccess) {
+    hipEventDestroy(done);
+    return -(int64_t)err;
+  }
+  std::lock_guard<std::mutex> g(e->mu);
+  int64_t t = e->next++;
+  e->status[t] = 0;
+  e->events[t] = done;
+  e->queue.push_back(Job{t, s, slot, step, epoch, total, checksum_off, meta ? meta : "", done});
+  e->cv.notify_one();
+  return t;
+}
+
+// Make `stream` wait until snapshot `ticket` has finished reading device memory.
+int edl_ckpt_fence(void* eng, int64_t ticket, hipStream_t stream) {
+  auto* e = static_cast<Engine*>(eng);
+  hipEvent_t ev = nullptr;
+  {
+    std::lock_guard<std::mutex> g(e->mu);
+    auto it = e->events.find(ticket);
+    if (it == e->events.end()) return 0;
+    ev = it->second;
+  }
+  return (int)hipStreamWaitEvent(stream, ev, 0);
+}
+
+// 0 pending, 1 committed, negative = error.  Committed tickets release their event.
+int edl_ckpt_status(void* eng, int64_t ticket) {
+  auto* e = static_cast<Engine*>(eng);
+  std::lock_guard<std::mutex> g(e->mu);
+  auto it = e->status.find(ticket);
+  if (it == e->status.end()) return 1;
+  int st = it->second;
+  if (st != 0) {
+    auto ev = e->events.find(ticket);
+    if (ev != e->events.end()) {
+      hipEventDestroy(ev->second);
+      e->events.erase(ev);
+    }
+    e->status.erase(it);
+  }
+  return st;
+}
+
+int edl_ckpt_wait(void* eng, int64_t ticket, int timeout_ms) {
+  for (int waited = 0;; waited += 1) {
+    int st = edl_ckpt_status(eng, ticket);
+    if (st != 0) return st;
+    if (timeout_ms >= 0 && waited >= timeout_ms) return 0;
+    usleep(1000);
+  }
+}
+
+// Host slot -> device buffers (H2D on `stream`).
+int edl_ckpt_restore(void* seg, int slot, int nbuf, const uint64_t* dev_ptrs, const uint64_t* sizes,
+                     const uint64_t* offsets, hipStream_t stream) {
+  auto* s = static_cast<Seg*>(seg);
+  if (slot < 0) slot = edl_shm_current(s);
+  if (slot < 0) return -1;
+  const uint8_t* src = s->data(slot);
+  for (int i = 0; i < nbuf; ++i) {
+    hipError_t err = hipMemcpyAsync((void*)dev_ptrs[i], src + offsets[i], sizes[i], hipMemcpyHostToDevice, stream);
+    if (err != hipSuccess) return (int)err;
+  }
+  return 0;
+}
+
+void edl_ckpt_engine_destroy(void* eng) {
+  auto* e = static_cast<Engine*>(eng);
+  if (!e) return;
+  {
+    std::lock_guard<std::mutex> g(e->mu);
+    e->stop = true;
+  }
+  e->cv.notify_all();
+  if (e->committer.joinable()) e->committer.join();
+  for (auto& kv : e->events) hipEventDestroy(kv.second);
+  if (e->side) hipStreamDestroy(e->side);
+  delete e;
+}
+
+}  // extern "C"

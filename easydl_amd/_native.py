@@ -65,11 +65,16 @@ class NativeError(RuntimeError):
 class _Lib:
     def __init__(self, path: str, sigs: dict):
         self.path = path
+        # torch is imported first (module top): its bundled libamdhip64.so.7 is then the
+        # one HIP runtime of the process and our code objects register into it.
         self._h = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
-        for name, argtypes in sigs.items():
+        for name, sig in sigs.items():
             fn = getattr(self._h, name)
-            fn.argtypes = argtypes
-            fn.restype = c_int
+            if isinstance(sig, tuple):
+                fn.restype, fn.argtypes = sig
+            else:
+                fn.argtypes = sig
+                fn.restype = c_int
         self.sigs = sigs
 
     def raw(self, name):

@@ -1,0 +1,45 @@
+"""ctypes signatures of libedl_runtime.so (csrc/runtime)."""
+import ctypes
+
+vp = ctypes.c_void_p
+i32 = ctypes.c_int
+i64 = ctypes.c_int64
+u64 = ctypes.c_uint64
+cp = ctypes.c_char_p
+u64p = ctypes.POINTER(ctypes.c_uint64)
+i64p = ctypes.POINTER(ctypes.c_int64)
+
+
+class ExitEvent(ctypes.Structure):
+    _fields_ = [("pid", ctypes.c_int32), ("exit_code", ctypes.c_int32), ("signal", ctypes.c_int32),
+                ("core", ctypes.c_int32), ("ts_ns", ctypes.c_int64)]
+
+
+# name -> (restype, argtypes)
+SIGS = {
+    "edl_sup_create": (vp, []),
+    "edl_sup_spawn": (i32, [vp, cp, ctypes.POINTER(cp), ctypes.POINTER(cp), cp, cp, ctypes.POINTER(i32), i32, i32,
+                            ctypes.POINTER(i32)]),
+    "edl_sup_wait": (i32, [vp, i32, ctypes.POINTER(ExitEvent), i32]),
+    "edl_sup_kill": (i32, [vp, i32, i32, i32]),
+    "edl_sup_num_children": (i32, [vp]),
+    "edl_sup_destroy": (None, [vp]),
+    "edl_shm_open": (vp, [cp, u64, i32, i32]),
+    "edl_shm_pin": (i32, [vp]),
+    "edl_shm_data": (vp, [vp, i32]),
+    "edl_shm_slot_bytes": (u64, [vp]),
+    "edl_shm_nslots": (i32, [vp]),
+    "edl_shm_current": (i32, [vp]),
+    "edl_shm_begin": (i32, [vp]),
+    "edl_shm_commit": (i32, [vp, i32, i64, i64, u64, u64, cp]),
+    "edl_shm_latest": (i32, [vp, i64p, i64p, u64p, u64p, cp, i32]),
+    "edl_shm_close": (i32, [vp, i32]),
+    "edl_shm_unlink": (i32, [cp]),
+    "edl_ckpt_engine_create": (vp, [i32, u64]),
+    "edl_ckpt_snapshot": (i64, [vp, vp, i32, u64p, u64p, u64p, vp, i64, i64, i64, cp]),
+    "edl_ckpt_fence": (i32, [vp, i64, vp]),
+    "edl_ckpt_status": (i32, [vp, i64]),
+    "edl_ckpt_wait": (i32, [vp, i64, i32]),
+    "edl_ckpt_restore": (i32, [vp, i32, i32, u64p, u64p, u64p, vp]),
+    "edl_ckpt_engine_destroy": (None, [vp]),
+}

@@ -1,0 +1,182 @@
+"""Brain planners: startup resources and periodic re-plans
+(reference README.md:13,19-23 "generate resources plans ... monitor the
+performance of a training job and dynamically adjust the resources";
+docs/design/elastic-training-operator.md:106-112).
+
+The reference publishes no algorithm; this is
+easydl_amd's, specialised for one 8x MI355X node:
+
+Startup plan (from job features + node inventory)
+* all-reduce jobs: one worker per free GPU (bounded by min/max workers);
+  memory check — 16 B/param of training state + activations must fit the
+  288 GB HBM of each rank, otherwise the plan refuses with a reason;
+* PS jobs: PS count from the fp32 parameter+optimizer bytes (one PS per
+  ``ps_shard_gb``) and the rest of the GPUs as workers; PS ranks get a CU
+  share (their update kernel is HBM-bound and needs few CUs) — realised by the
+  operator as CU-masked streams (``EDL_CU_MASK``) and an HBM cap;
+* gradient bucket size for xGMI: large enough that each of the 7 links moves
+  >= ~8 MiB per collective step, capped so ~4+ buckets overlap backward;
+* in-memory checkpoint interval so snapshot D2H cost stays < 5 % of step time.
+
+Periodic plan (from per-rank step metrics)
+* straggler eviction: a rank slower than ``straggler_ratio`` x median for a
+  full window is replaced (resource_updation re-creates it);
+* bucket-size autotune: try neighbouring sizes window by window, keep the
+  fastest measured step time;
+* scale up to free GPUs when the job asked for more workers than it got.
+"""
+from __future__ import annotations
+
+import math
+import statistics
+from dataclasses import dataclass, field
+
+from easydl_amd.api.spec import Resource, ResourcePlan, RoleResource
+from easydl_amd.brain.collectors import NodeInventory
+
+HBM_GB = 288.0
+XGMI_LINKS = 7
+
+
+@dataclass
+class JobFeatures:
+    """What the trainer master extracts from the job (reference :106 "extracts features")."""
+    mode: str = "allreduce"
+    params: float = 0.0              # parameter count
+    bytes_per_param_state: float = 16.0
+    tokens_per_step_per_rank: float = 8192.0
+    activation_gb_per_rank: float = 40.0
+    step_time_s: float | None = None
+    min_workers: int = 1
+    max_workers: int = 8
+    host_mem_gb: float | None = None
+
+    @classmethod
+    def from_dict(cls, d: dict) -> "JobFeatures":
+        f = cls()
+        for k, v in (d or {}).items():
+            if hasattr(f, k):
+                setattr(f, k, type(getattr(f, k))(v) if getattr(f, k) is not None and v is not None else v)
+        return f
+
+
+@dataclass
+class BrainConfig:
+    ps_shard_gb: float = 8.0
+    ps_cu: int = 64
+    straggler_ratio: float = 1.3
+    window: int = 20
+    bucket_choices: tuple = (32.0, 64.0, 128.0, 256.0, 512.0)
+    ckpt_overhead: float = 0.05
+    pcie_gbps: float = 50.0
+
+
+def grad_bucket_mb(params: float, world: int, grad_bytes: int = 2) -> float:
+    """Bucket size for an xGMI mesh: >= 8 MiB per link-step, >= 4 buckets per backward."""
+    if world <= 1:
+        return 128.0
+    total_mb = params * grad_bytes / 2**20
+    link_floor = 8.0 * XGMI_LINKS * world / max(1, world - 1)   # MiB so each ring step moves >= 8 MiB
+    cap = max(link_floor, total_mb / 4)
+    choice = 2 ** math.ceil(math.log2(max(link_floor, min(cap, 256.0))))
+    return float(min(512.0, choice))
+
+
+def ckpt_interval(params: float, world: int, step_time_s: float | None, cfg: BrainConfig) -> int:
+    """Steps between in-memory snapshots so the sharded D2H stays under cfg.ckpt_overhead."""
+    state_gb = params * 14 / 2**30            # bf16 params + fp32 master/m/v (grads excluded)
+    per_rank_gb = state_gb / max(1, world)
+    copy_s = per_rank_gb / cfg.pcie_gbps
+    st = step_time_s or 1.0
+    return max(1, int(math.ceil(copy_s / (cfg.ckpt_overhead * st))))
+
+
+class Planner:
+    def __init__(self, cfg: BrainConfig | None = None):
+        self.cfg = cfg or BrainConfig()
+        self._tune: dict = {}
+
+    # ------------------------------------------------------------------ startup
+    def startup_plan(self, feat: JobFeatures, inv: NodeInventory) -> ResourcePlan:
+        ngpu = len(inv.gpus)
+        plan = ResourcePlan(reason="startup")
+        if feat.mode == "ps":
+            state_gb = feat.params * 12 / 2**30  # fp32 param + m + v on the PS
+            n_ps = max(1, math.ceil(state_gb / self.cfg.ps_shard_gb)) if feat.params else 1
+            if ngpu:
+                n_ps = min(n_ps, max(1, ngpu // 4))
+                n_workers = max(feat.min_workers, min(feat.max_workers, ngpu - n_ps))
+                ps_res = Resource(cpu=4, memory=max(4096, state_gb / n_ps * 1024 * 2), gpu=1, cu=self.cfg.ps_cu,
+                                  hbm_gb=min(HBM_GB, state_gb / n_ps * 2 + 8))
+                w_res = Resource(cpu=max(1, inv.cpus // max(1, ngpu)), gpu=1)
+            else:
+                n_workers = max(feat.min_workers, min(feat.max_workers, max(1, (inv.cpus - n_ps) // 2)))
+                ps_res = Resource(cpu=1, memory=1024, gpu=0)
+                w_res = Resource(cpu=1, memory=1024, gpu=0)
+            plan.roles["parameter_server"] = RoleResource(n_ps, ps_res)
+            plan.roles["worker"] = RoleResource(n_workers, w_res)
+            plan.roles["evaluator"] = RoleResource(0, Resource(cpu=1, gpu=0))
+            plan.reason = f"ps: {n_ps} PS for {state_gb:.1f} GB of state, {n_workers} workers"
+        else:
+            need = feat.params * feat.bytes_per_param_state / 2**30 + feat.activation_gb_per_rank
+            if ngpu and need > HBM_GB:
+                plan.reason = f"refused: {need:.0f} GB per rank exceeds {HBM_GB:.0f} GB HBM (use TP)"
+                plan.roles["worker"] = RoleResource(0, Resource(gpu=1))
+                return plan
+            n = min(feat.max_workers, ngpu) if ngpu else feat.min_workers
+            n = max(feat.min_workers, n)
+            cpus = max(1, inv.cpus // max(1, n))
+            plan.roles["worker"] = RoleResource(n, Resource(cpu=cpus, gpu=1 if ngpu else 0))
+            plan.reason = f"allreduce: {n} workers x 1 GPU, {need:.0f} GB/rank"
+        world = plan.roles["worker"].replicas
+        plan.bucket_mb = grad_bucket_mb(feat.params, world)
+        plan.ckpt_interval = ckpt_interval(feat.params, world, feat.step_time_s, self.cfg)
+        return plan
+
+    # ------------------------------------------------------------------ periodic
+    def next_plan(self, feat: JobFeatures, inv: NodeInventory, current: ResourcePlan,
+                  metrics: dict[str, dict]) -> ResourcePlan | None:
+        """Return a changed plan, or None to keep the current one."""
+        import copy
+        plan = copy.deepcopy(current)
+        changed = []
+        times = {n: m.get("step_time") for n, m in metrics.items() if m.get("step_time")}
+        if len(times) >= 2:
+            med = statistics.median(times.values())
+            for n, t in times.items():
+                m = metrics[n]
+                if t > self.cfg.straggler_ratio * med and m.get("window", 0) >= self.cfg.window:
+                    plan.per_rank.setdefault(n, {})["evict"] = True
+                    changed.append(f"straggler {n} ({t:.3f}s vs median {med:.3f}s)")
+        # bucket autotune over windows of identical membership
+        if times:
+            st = statistics.median(times.values())
+            t = self._tune
+            cur = plan.bucket_mb or 128.0
+            t.setdefault("results", {})
+            t["results"][cur] = min(st, t["results"].get(cur, float("inf")))
+            choices = list(self.cfg.bucket_choices)
+            if cur in choices:
+                i = choices.index(cur)
+                untried = [c for c in (choices[i - 1] if i > 0 else None, choices[i + 1] if i + 1 < len(choices)
+                                       else None) if c is not None and c not in t["results"]]
+                if untried:
+                    plan.bucket_mb = untried[0]
+                    changed.append(f"bucket autotune: try {untried[0]} MB")
+                else:
+                    best = min(t["results"], key=t["results"].get)
+                    if best != cur:
+                        plan.bucket_mb = best
+                        changed.append(f"bucket autotune: best {best} MB")
+        # grow into free GPUs
+        wr = plan.roles.get("worker")
+        if wr is not None and feat.mode != "ps":
+            busy = sum(1 for g in inv.gpus if (g.busy_pct or 0) > 50)
+            free = len(inv.gpus) - max(busy, wr.replicas)
+            if free > 0 and wr.replicas < feat.max_workers:
+                wr.replicas = min(feat.max_workers, wr.replicas + free)
+                changed.append(f"scale up to {wr.replicas} workers")
+        if not changed:
+            return None
+        plan.reason = "; ".join(changed)
+        return plan

@@ -95,11 +95,22 @@ def main(argv=None):
     ap.add_argument("--hb-timeout", type=float, default=15.0)
     ap.add_argument("--policy", default="shrink")
     ap.add_argument("--run-dir", default=os.environ.get("EDL_RUN_DIR"))
+    ap.add_argument("--job-spec", default=None, help="ElasticJob JSON/YAML: enables the Brain plan loop")
+    ap.add_argument("--brain-url", default=os.environ.get("EDL_BRAIN_URL"))
+    ap.add_argument("--plan-period", type=float, default=30.0)
     a = ap.parse_args(argv)
     logging.basicConfig(level=logging.INFO, format="%(asctime)s [master] %(message)s")
     cfg = RendezvousConfig(min_nodes=a.min, max_nodes=a.max, join_window_s=a.join_window,
                            heartbeat_timeout_s=a.hb_timeout, policy=a.policy)
-    m = JobMaster(a.job, a.port, a.host, cfg, a.run_dir).start()
+    planner = None
+    if a.job_spec:
+        from easydl_amd.api.spec import ElasticJob, load_yaml_docs
+        from easydl_amd.brain.service import BrainClient
+        from easydl_amd.master.planner import PlanLoop
+        txt = open(a.job_spec).read()
+        doc = json.loads(txt) if txt.lstrip().startswith("{") else load_yaml_docs(txt)[0]
+        planner = PlanLoop(ElasticJob.from_dict(doc), BrainClient(a.brain_url), period_s=a.plan_period)
+    m = JobMaster(a.job, a.port, a.host, cfg, a.run_dir, planner=planner).start()
     signal.signal(signal.SIGTERM, lambda *_: m._stop.set())
     print(json.dumps({"master_port": m.port}), flush=True)
     m.serve_forever()

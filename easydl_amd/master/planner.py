@@ -1,0 +1,99 @@
+"""The trainer master's plan loop (reference docs/design/elastic-training-operator.md:105-112):
+
+1. extract job features, query the Brain for *startup resources*, generate and
+   apply a JobResource (written to the store key ``jobresource``, which the
+   local ElasticOperator watches) — unless the user supplied one;
+2. periodically collect per-rank metrics (``metrics/<node>``), ask the Brain
+   for a new plan and update the JobResource (scale, replace stragglers via
+   ``resource_updation``) and the runtime knobs (``plan/bucket_mb``) that the
+   trainers pick up at step boundaries.
+"""
+from __future__ import annotations
+
+import json
+import logging
+import time
+
+from easydl_amd.api.spec import ElasticJob, JobResource, ResourcePlan, ResourceUpdation, Resource
+from easydl_amd.brain.service import BrainClient
+
+log = logging.getLogger("edl.master.plan")
+
+
+class PlanLoop:
+    def __init__(self, job: ElasticJob, brain: BrainClient | None = None, period_s: float = 30.0,
+                 user_wait_s: float = 0.5):
+        self.job = job
+        self.brain = brain or BrainClient()
+        self.period_s = period_s
+        self.user_wait_s = user_wait_s
+        self.plan: ResourcePlan | None = None
+        self.version = 0
+        self._t_start = time.time()
+        self._last = 0.0
+        self.started = False
+
+    def features(self) -> dict:
+        f = dict(self.job.features)
+        f.setdefault("mode", self.job.mode)
+        f.setdefault("min_workers", self.job.min_workers)
+        f.setdefault("max_workers", self.job.max_workers)
+        return f
+
+    def _apply(self, master, jr: JobResource):
+        self.version += 1
+        jr.version = self.version
+        master.kv.set("jobresource", json.dumps(jr.to_dict()))
+        if jr.bucket_mb:
+            master.kv.set("plan/bucket_mb", str(jr.bucket_mb))
+        if jr.ckpt_interval:
+            master.kv.set("plan/ckpt_interval", str(jr.ckpt_interval))
+        master.kv.add("plan/version", 1)
+        wr = jr.roles.get("worker")
+        if wr is not None and self.job.mode == "allreduce":
+            master.rdzv.target_nodes = wr.replicas
+        master.events.emit("plan_applied", version=self.version, replicas={r: v.replicas for r, v in
+                                                                             jr.roles.items()})
+
+    def maybe_replan(self, master) -> None:
+        now = time.time()
+        if not self.started:
+            if master.kv.exists("jobresource"):
+                raw = master.kv.get("jobresource")
+                jr = JobResource.from_dict(raw if isinstance(raw, dict) else json.loads(raw))
+                self.version = jr.version
+                self.started = True
+                self.plan = ResourcePlan(roles=jr.roles, bucket_mb=jr.bucket_mb, ckpt_interval=jr.ckpt_interval,
+                                         reason="user JobResource")
+                wr = jr.roles.get("worker")
+                if wr is not None and self.job.mode == "allreduce":
+                    master.rdzv.target_nodes = wr.replicas
+                return
+            if now - self._t_start < self.user_wait_s:
+                return
+            self.plan = self.brain.startup_plan(self.features())
+            master.events.emit("startup_plan", plan=self.plan.to_dict())
+            self._apply(master, self.plan.to_job_resource(self.job.name))
+            self.started = True
+            self._last = now
+            return
+        if self.period_s <= 0 or now - self._last < self.period_s:
+            return
+        self._last = now
+        members = master.rdzv.members()
+        metrics = {n: m for n in members if (m := master.kv.get(f"metrics/{n}"))}
+        if not metrics:
+            return
+        newp = self.brain.next_plan(self.features(), self.plan, metrics)
+        if newp is None:
+            return
+        master.events.emit("replan", reason=newp.reason)
+        jr = newp.to_job_resource(self.job.name)
+        for node, d in newp.per_rank.items():
+            if d.get("evict"):
+                name = node.split(":")[0]
+                jr.resource_updation.append(ResourceUpdation(name=name, resource=Resource()))
+        for d in newp.per_rank.values():
+            d.pop("evict", None)
+        self.plan = newp
+        self._apply(master, jr)

@@ -1,0 +1,372 @@
+"""ElasticOperator re-cast as a local process manager for the GPUs of one node
+(BASELINE.json north star; reference README.md:12 and
+docs/design/elastic-training-operator.md:3-4,47-55,97-114).
+
+Reference semantics kept:
+* on ElasticJob submission ONLY the trainer (job master) is created (:47,105);
+* the trainer queries the Brain, generates and applies a JobResource (:106-108);
+* on JobResource create/update the operator creates / removes role processes
+  to match ``replicas`` (:52-55,108-114) — horizontal scaling;
+* ``resource_updation: [{name, resource}]`` launches a new process with the new
+  resource that replaces the named one (:99-101) — vertical scaling;
+* processes are named ``<job>-<role>-<index>`` (:87,91).
+
+Local re-cast: "pods" are processes spawned by the native supervisor
+(csrc/runtime/supervisor.cpp) with one GPU each (``EDL_GPU``), CPU affinity
+and the plan's CU/HBM limits in the environment.  Exit events are forwarded to
+the job master's store (``ev/exit/<node>``) the moment they happen, which is
+what makes worker-death detection sub-millisecond.  Failed workers are
+replaced (same name, new incarnation); clean exits mark completion.
+"""
+from __future__ import annotations
+
+import json
+import logging
+import os
+import shlex
+import signal
+import socket
+import sys
+import time
+from dataclasses import dataclass, field
+
+from easydl_amd.api.spec import ROLE_SHORT, ElasticJob, JobResource, Resource
+from easydl_amd.utils.events import EventLog
+
+log = logging.getLogger("edl.operator")
+
+REPO_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+@dataclass
+class Proc:
+    name: str
+    role: str           # long role name (worker / parameter_server / evaluator / trainer)
+    index: int
+    pid: int
+    gpu: int | None
+    resource: Resource
+    started: float
+    state: str = "running"   # running | leaving | exited | completed | replaced
+    exit_code: int | None = None
+    generation: int = 0
+
+    @property
+    def node_id(self) -> str:
+        return f"{self.name}:{self.pid}"
+
+
+@dataclass
+class OperatorConfig:
+    gpus: list[int] = field(default_factory=list)       # GPU ordinals this operator may hand out
+    cpus: list[int] = field(default_factory=list)       # host CPUs to partition (affinity)
+    max_restarts: int = 100
+    leave_grace_s: float = 30.0
+    master_port: int | None = None
+    python: str = sys.executable
+    replace_failed: bool = True
+
+
+def free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def cu_mask_hex(n_cu: int, total: int = 256, start: int = 0) -> str:
+    """Mask string for ``n_cu`` CUs; spread evenly over the 8 XCDs when possible."""
+    n_cu = max(1, min(total, int(n_cu)))
+    bits = 0
+    per_xcd = total // 8
+    take = [n_cu // 8 + (1 if x < n_cu % 8 else 0) for x in range(8)]
+    for x in range(8):
+        for c in range(take[x]):
+            # hardware CU numbering interleaves XCDs: cu id = c * 8 + xcd
+            bits |= 1 << ((start + c) % per_xcd * 8 + x)
+    return hex(bits)
+
+
+class ElasticOperator:
+    def __init__(self, job: ElasticJob, run_dir: str, launcher=None, cfg: OperatorConfig | None = None,
+                 job_resource: JobResource | None = None, master_argv: list[str] | None = None, kv=None):
+        self.job = job
+        self.run_dir = os.path.abspath(run_dir)
+        os.makedirs(self.run_dir, exist_ok=True)
+        self.cfg = cfg or OperatorConfig()
+        if launcher is None:
+            from easydl_amd.operator.supervisor import Supervisor
+            launcher = Supervisor()
+        self.launcher = launcher
+        self.events = EventLog(os.path.join(self.run_dir, "events-operator.jsonl"), proc="operator")
+        self.procs: dict[str, Proc] = {}          # name -> current incarnation
+        self.history: list[Proc] = []
+        self.restarts = 0
+        self.desired: JobResource | None = job_resource
+        self.applied_version = -1
+        self.applied_updations: set[tuple[int, str]] = set()
+        self.master_port = self.cfg.master_port or free_port()
+        self.master_argv = master_argv
+        self.kv = kv
+        self.overrides: dict[str, Resource] = {}
+        self.done = False
+        self.failed = False
+        self._free_gpus = list(self.cfg.gpus)
+
+    # ------------------------------------------------------------- master
+    def start(self) -> None:
+        """Create ONLY the trainer (job master) process first (reference :47,105-106)."""
+        with open(os.path.join(self.run_dir, "job.json"), "w") as f:
+            json.dump(self.job.to_dict(), f)
+        argv = self.master_argv or [self.cfg.python, "-m", "easydl_amd.master.main", "--job", self.job.name,
+                                    "--port", str(self.master_port), "--run-dir", self.run_dir,
+                                    "--min", str(self.job.min_workers), "--max", str(self.job.max_workers),
+                                    "--job-spec", os.path.join(self.run_dir, "job.json")]
+        name = f"{self.job.name}-trainer-0"
+        pid = self.launcher.spawn(name, argv, env=self._base_env(), cwd=REPO_ROOT,
+                                  log_path=os.path.join(self.run_dir, "logs", f"{name}.log"))
+        self.procs[name] = Proc(name, "trainer", 0, pid, None, Resource(), time.time())
+        self.events.emit("spawn", name=name, pid=pid, role="trainer")
+        if self.kv is None:
+            self.kv = self._connect_master()
+        if self.desired is not None:
+            # a user-supplied JobResource is applied as-is (Brain not consulted)
+            self.kv.set("jobresource", json.dumps(self.desired.to_dict()))
+
+    def _connect_master(self, timeout_s: float = 120.0):
+        from easydl_amd.master.store import KV, make_tcp_store
+        t_end = time.time() + timeout_s
+        last = None
+        while time.time() < t_end:
+            try:
+                st = make_tcp_store("127.0.0.1", self.master_port, False, timeout_s=10)
+                return KV(st, f"edl/{self.job.name}")
+            except Exception as e:  # master not listening yet
+                last = e
+                time.sleep(0.2)
+        raise RuntimeError(f"job master did not come up on port {self.master_port}: {last}")
+
+    def _base_env(self) -> dict:
+        env = dict(os.environ)
+        env.update(self.job.env)
+        env["PYTHONPATH"] = REPO_ROOT + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
+        env.update({"EDL_JOB": self.job.name, "EDL_MASTER_ADDR": "127.0.0.1",
+                    "EDL_MASTER_PORT": str(self.master_port), "EDL_RUN_DIR": self.run_dir})
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_USE_AGENT_STORE"):
+            env.pop(k, None)
+        return env
+
+    # ------------------------------------------------------------- reconcile
+    def _role_procs(self, role: str) -> list[Proc]:
+        return [p for p in self.procs.values() if p.role == role and p.state in ("running", "leaving")]
+
+    def _completed(self, role: str) -> int:
+        return sum(1 for p in self.procs.values() if p.role == role and p.state == "completed")
+
+    def _spawn_role(self, role: str, index: int, res: Resource, generation: int = 0) -> Proc:
+        short = ROLE_SHORT[role]
+        name = f"{self.job.name}-{short}-{index}"
+        env = self._base_env()
+        gpu = None
+        if self._needs_gpu(role, res):
+            if self._free_gpus:
+                gpu = self._free_gpus.pop(0)
+                env["EDL_GPU"] = str(gpu)
+        env.update({"EDL_ROLE": short, "EDL_INDEX": str(index)})
+        if res.cu:
+            env["EDL_CU_MASK"] = cu_mask_hex(res.cu)
+        if res.hbm_gb:
+            env["EDL_HBM_GB"] = str(res.hbm_gb)
+        cpus = []
+        if res.cpu and self.cfg.cpus:
+            n = max(1, int(res.cpu))
+            used = set()
+            for p in self.procs.values():
+                used |= set(getattr(p, "cpus", []))
+            cpus = [c for c in self.cfg.cpus if c not in used][:n]
+            env["OMP_NUM_THREADS"] = str(n)
+        cmd = self.job.command_for(role)
+        if not cmd:
+            raise ValueError(f"no command for role {role}")
+        argv = shlex.split(cmd)
+        if argv[0] in ("python", "python3"):
+            argv[0] = self.cfg.python
+        pid = self.launcher.spawn(name, argv, env=env, cwd=REPO_ROOT,
+                                  log_path=os.path.join(self.run_dir, "logs", f"{name}.log"), cpus=cpus)
+        p = Proc(name, role, index, pid, gpu, res, time.time(), generation=generation)
+        p.cpus = cpus
+        self.procs[name] = p
+        self.events.emit("spawn", name=name, pid=pid, role=role, gpu=gpu, gen=generation, resource=res.to_dict())
+        return p
+
+    def _needs_gpu(self, role: str, res: Resource) -> bool:
+        if res.gpu is not None:
+            return res.gpu > 0
+        return role == "worker" and bool(self.cfg.gpus)
+
+    def reconcile(self) -> None:
+        jr = self.desired
+        if jr is None:
+            return
+        # vertical scaling by replacement (reference :99-101): the old incarnation
+        # leaves at its next step boundary; the new one starts with the merged
+        # resource as soon as its GPU is free.
+        for u in jr.resource_updation:
+            key = (jr.version, u.name)
+            if key in self.applied_updations:
+                continue
+            old = self.procs.get(u.name)
+            if old is None or old.state != "running":
+                continue
+            self.applied_updations.add(key)
+            self.overrides[u.name] = old.resource.merged(u.resource)
+            self._begin_leave(old, replaced=True)
+            del self.procs[old.name]
+            self.history.append(old)
+            self.events.emit("replace", name=u.name, resource=self.overrides[u.name].to_dict())
+        for role, rr in jr.roles.items():
+            running = [p for p in self._role_procs(role) if p.state == "running"]
+            want = max(0, rr.replicas - self._completed(role))
+            if len(running) < want:
+                used = {p.index for p in self.procs.values() if p.role == role}
+                idx = 0
+                for _ in range(want - len(running)):
+                    while idx in used:
+                        idx += 1
+                    name = f"{self.job.name}-{ROLE_SHORT[role]}-{idx}"
+                    res = self.overrides.get(name, rr.resource)
+                    if self._needs_gpu(role, res) and not self._free_gpus:
+                        break  # wait for a GPU to be released
+                    prev = [h for h in self.history if h.name == name]
+                    gen = (max(h.generation for h in prev) + 1) if prev else 0
+                    self._spawn_role(role, idx, res, gen)
+                    used.add(idx)
+            elif len(running) > want:
+                for p in sorted(running, key=lambda p: -p.index)[:len(running) - want]:
+                    self._begin_leave(p)
+
+    def _begin_leave(self, p: Proc, replaced: bool = False) -> None:
+        if p.state != "running":
+            return
+        p.state = "replaced" if replaced else "leaving"
+        p.leave_ts = time.time()
+        if self.kv is not None and p.role != "trainer":
+            self.kv.set(f"rdzv/leave/{p.node_id}", "1")
+        self.events.emit("leave", name=p.name, replaced=replaced)
+
+    def _release_gpu(self, p: Proc) -> None:
+        if p.gpu is not None and p.gpu not in self._free_gpus:
+            self._free_gpus.append(p.gpu)
+            self._free_gpus.sort()
+            p.gpu = None
+
+    def _enforce_grace(self):
+        now = time.time()
+        for p in list(self.procs.values()) + self.history:
+            if p.state in ("leaving", "replaced") and now - getattr(p, "leave_ts", now) > self.cfg.leave_grace_s:
+                try:
+                    self.launcher.kill(p.pid, signal.SIGKILL)
+                except OSError:
+                    pass
+
+    # ------------------------------------------------------------- events
+    def handle_exit(self, ex) -> None:
+        p = next((q for q in list(self.procs.values()) + self.history if q.pid == ex.pid), None)
+        if p is None:
+            return
+        p.exit_code = ex.exit_code if not ex.signal else -ex.signal
+        self.events.emit("exit", name=p.name, pid=p.pid, code=ex.exit_code, signal=ex.signal, role=p.role)
+        if p.role == "trainer":
+            p.state = "exited"
+            if not self.done:
+                self.failed = ex.exit_code != 0 or ex.signal != 0
+            return
+        if self.kv is not None:
+            try:
+                self.kv.set(f"ev/exit/{p.node_id}", json.dumps({"code": ex.exit_code, "signal": ex.signal,
+                                                                 "ts": ex.ts}))
+            except Exception:
+                pass
+        self._release_gpu(p)
+        if p.state in ("leaving", "replaced"):
+            p.state = "exited"
+            if self.procs.get(p.name) is p:
+                del self.procs[p.name]
+                self.history.append(p)
+            return
+        if ex.exit_code == 0 and not ex.signal:
+            p.state = "completed"
+            return
+        p.state = "exited"
+        self.restarts += 1
+        if self.procs.get(p.name) is p:
+            del self.procs[p.name]
+            self.history.append(p)
+        if not self.cfg.replace_failed or self.restarts > self.cfg.max_restarts:
+            log.error("not replacing %s (restarts %d)", p.name, self.restarts)
+
+    def _poll_jobresource(self) -> None:
+        if self.kv is None:
+            return
+        try:
+            raw = self.kv.get("jobresource")
+        except Exception:
+            return
+        if raw is None:
+            return
+        jr = JobResource.from_dict(raw if isinstance(raw, dict) else json.loads(raw))
+        if jr.selector != self.job.name:
+            log.error("JobResource selector %s does not match job %s: ignored", jr.selector, self.job.name)
+            return
+        if self.desired is None or jr.version != self.applied_version or jr.to_dict() != self.desired.to_dict():
+            self.desired = jr
+            self.applied_version = jr.version
+            self.events.emit("jobresource_applied", version=jr.version,
+                             replicas={r: v.replicas for r, v in jr.roles.items()})
+
+    def job_complete(self) -> bool:
+        jr = self.desired
+        if jr is None:
+            return False
+        workers = [p for p in self.procs.values() if p.role == "worker"]
+        return jr.replicas("worker") > 0 and bool(workers) and all(p.state == "completed" for p in workers)
+
+    def tick(self, timeout_s: float = 0.05) -> None:
+        for ex in self.launcher.poll(timeout_s):
+            self.handle_exit(ex)
+        self._poll_jobresource()
+        self.reconcile()
+        self._enforce_grace()
+        if self.job_complete() and not self.done:
+            self.done = True
+            self.events.emit("job_complete")
+
+    def run(self, timeout_s: float | None = None) -> int:
+        self.start()
+        t_end = None if timeout_s is None else time.time() + timeout_s
+        try:
+            while not self.done and not self.failed:
+                self.tick()
+                if t_end is not None and time.time() > t_end:
+                    log.error("operator timeout")
+                    return 2
+        finally:
+            self.shutdown()
+        return 0 if self.done else 1
+
+    def shutdown(self) -> None:
+        if self.kv is not None:
+            try:
+                self.kv.set("master/shutdown", "1")
+            except Exception:
+                pass
+        for p in list(self.procs.values()):
+            if p.state in ("running", "leaving", "replaced"):
+                try:
+                    self.launcher.terminate(p.pid, grace_s=5.0)
+                except Exception:
+                    pass
+        if hasattr(self.launcher, "close"):
+            self.launcher.close()

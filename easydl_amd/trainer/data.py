@@ -29,22 +29,41 @@ class ElasticBatchPlan:
     def steps_per_epoch(self) -> int:
         return max(1, self.n // self.global_batch)
 
-    def _perm_for(self, epoch: int) -> torch.Tensor:
+    _MATERIALIZE_MAX = 1 << 24
+
+    def _perm_for(self, epoch: int):
         if self._perm_epoch != epoch:
-            if self.shuffle:
+            if not self.shuffle:
+                self._perm = None
+            elif self.n <= self._MATERIALIZE_MAX:
                 g = torch.Generator().manual_seed(self.seed * 1000003 + epoch)
                 self._perm = torch.randperm(self.n, generator=g)
             else:
-                self._perm = torch.arange(self.n)
+                # huge index spaces: seeded affine bijection i -> (a*i + b) mod n, no memory
+                import random
+                r = random.Random(self.seed * 1000003 + epoch)
+                while True:
+                    a = r.randrange(1, self.n)
+                    if math.gcd(a, self.n) == 1:
+                        break
+                self._perm = (a, r.randrange(0, self.n))
             self._perm_epoch = epoch
         return self._perm
+
+    def _take(self, perm, lo: int, hi: int) -> torch.Tensor:
+        if perm is None:
+            return torch.arange(lo, hi)
+        if isinstance(perm, tuple):
+            a, b = perm
+            return torch.tensor([(a * i + b) % self.n for i in range(lo, hi)], dtype=torch.long)
+        return perm[lo:hi]
 
     def indices(self, step: int, rank: int, world: int) -> list[list[int]]:
         """Micro-batches (lists of sample indices) of ``rank`` at global ``step``."""
         spe = self.steps_per_epoch()
         epoch, k = divmod(step, spe)
         perm = self._perm_for(epoch)
-        window = perm[k * self.global_batch:(k + 1) * self.global_batch]
+        window = self._take(perm, k * self.global_batch, (k + 1) * self.global_batch)
         mine = window[rank::world].tolist()
         return [mine[i:i + self.micro_batch] for i in range(0, len(mine), self.micro_batch)]
 

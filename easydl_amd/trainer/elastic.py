@@ -224,7 +224,7 @@ class ElasticTrainer:
         # finish() zero-fills untouched gradients before flushing the buckets.
         self.ddp.finish()
         self.fault.maybe_inject("after_backward", self.step, trainer=self)
-        return loss_acc
+        return None if loss_acc is None else loss_acc / total
 
     def _sync_point(self) -> bool:
         """Host-side completion of every gradient all-reduce; False if the epoch broke."""
