@@ -98,6 +98,7 @@ def main(argv=None):
     ap.add_argument("--job-spec", default=None, help="ElasticJob JSON/YAML: enables the Brain plan loop")
     ap.add_argument("--brain-url", default=os.environ.get("EDL_BRAIN_URL"))
     ap.add_argument("--plan-period", type=float, default=30.0)
+    ap.add_argument("--job-resource", default=None, help="user JobResource JSON/YAML (Brain not consulted)")
     a = ap.parse_args(argv)
     logging.basicConfig(level=logging.INFO, format="%(asctime)s [master] %(message)s")
     cfg = RendezvousConfig(min_nodes=a.min, max_nodes=a.max, join_window_s=a.join_window,
@@ -110,7 +111,13 @@ def main(argv=None):
         txt = open(a.job_spec).read()
         doc = json.loads(txt) if txt.lstrip().startswith("{") else load_yaml_docs(txt)[0]
         planner = PlanLoop(ElasticJob.from_dict(doc), BrainClient(a.brain_url), period_s=a.plan_period)
-    m = JobMaster(a.job, a.port, a.host, cfg, a.run_dir, planner=planner).start()
+    m = JobMaster(a.job, a.port, a.host, cfg, a.run_dir, planner=planner)
+    if a.job_resource:
+        from easydl_amd.api.spec import JobResource, load_yaml_docs
+        txt = open(a.job_resource).read()
+        doc = json.loads(txt) if txt.lstrip().startswith("{") else load_yaml_docs(txt)[0]
+        m.kv.set("jobresource", json.dumps(JobResource.from_dict(doc).to_dict()))
+    m.start()
     signal.signal(signal.SIGTERM, lambda *_: m._stop.set())
     print(json.dumps({"master_port": m.port}), flush=True)
     m.serve_forever()

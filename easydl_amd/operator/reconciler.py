@@ -123,6 +123,13 @@ class ElasticOperator:
                                     "--port", str(self.master_port), "--run-dir", self.run_dir,
                                     "--min", str(self.job.min_workers), "--max", str(self.job.max_workers),
                                     "--job-spec", os.path.join(self.run_dir, "job.json")]
+        if self.desired is not None and self.master_argv is None:
+            # a user-supplied JobResource is handed to the master, which applies it
+            # instead of consulting the Brain
+            jr_path = os.path.join(self.run_dir, "jobresource.json")
+            with open(jr_path, "w") as f:
+                json.dump(self.desired.to_dict(), f)
+            argv += ["--job-resource", jr_path]
         name = f"{self.job.name}-trainer-0"
         pid = self.launcher.spawn(name, argv, env=self._base_env(), cwd=REPO_ROOT,
                                   log_path=os.path.join(self.run_dir, "logs", f"{name}.log"))
@@ -130,8 +137,7 @@ class ElasticOperator:
         self.events.emit("spawn", name=name, pid=pid, role="trainer")
         if self.kv is None:
             self.kv = self._connect_master()
-        if self.desired is not None:
-            # a user-supplied JobResource is applied as-is (Brain not consulted)
+        if self.desired is not None and self.master_argv is not None:
             self.kv.set("jobresource", json.dumps(self.desired.to_dict()))
 
     def _connect_master(self, timeout_s: float = 120.0):
@@ -174,7 +180,7 @@ class ElasticOperator:
             if self._free_gpus:
                 gpu = self._free_gpus.pop(0)
                 env["EDL_GPU"] = str(gpu)
-        env.update({"EDL_ROLE": short, "EDL_INDEX": str(index)})
+        env.update({"EDL_ROLE": short, "EDL_INDEX": str(index), "EDL_GENERATION": str(generation)})
         if res.cu:
             env["EDL_CU_MASK"] = cu_mask_hex(res.cu)
         if res.hbm_gb:

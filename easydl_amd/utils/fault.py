@@ -27,6 +27,7 @@ class FaultSpec:
         self.role = args.get("role")
         self.ms = float(args.get("ms", 0))
         self.point = args.get("point", "after_backward" if kind == "nan" else "step_start")
+        self.generation = int(args.get("gen", 0))   # only this incarnation fires (replacements do not)
         self.fired = False
 
     @classmethod
@@ -43,7 +44,9 @@ class FaultSpec:
 
 
 class FaultInjector:
-    def __init__(self, specs: list[FaultSpec], index: int = 0, role: str = "worker", events=None):
+    def __init__(self, specs: list[FaultSpec], index: int = 0, role: str = "worker", events=None,
+                 generation: int = 0):
+        self.generation = generation
         self.specs = specs
         self.index = index
         self.role = role
@@ -51,7 +54,8 @@ class FaultInjector:
 
     @classmethod
     def from_env(cls, ctx, events=None) -> "FaultInjector":
-        return cls(FaultSpec.parse(os.environ.get("EDL_FAULT", "")), ctx.index, ctx.role, events)
+        return cls(FaultSpec.parse(os.environ.get("EDL_FAULT", "")), ctx.index, ctx.role, events,
+                   int(os.environ.get("EDL_GENERATION", 0)))
 
     def maybe_inject(self, point: str, step: int, trainer=None) -> None:
         for s in self.specs:
@@ -60,6 +64,8 @@ class FaultInjector:
             if s.index is not None and s.index != self.index:
                 continue
             if s.role is not None and s.role != self.role:
+                continue
+            if s.generation != self.generation:
                 continue
             s.fired = True
             if self.events is not None:

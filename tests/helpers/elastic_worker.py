@@ -31,6 +31,7 @@ for g in tr.flat.groups:
 res = {"index": tr.ctx.index, "step": tr.step, "hash": h.hexdigest(),
        "worlds": [r["world"] for r in tr.history], "epochs": [r["epoch"] for r in tr.history],
        "loss": float(tr.last_loss) if tr.last_loss is not None else None}
-with open(os.environ["TEST_OUT"], "w") as f:
+out = os.environ.get("TEST_OUT") or os.path.join(os.environ["EDL_RUN_DIR"], f"res{tr.ctx.index}-{os.getpid()}.json")
+with open(out, "w") as f:
     json.dump(res, f)
 tr.close()

@@ -1,0 +1,51 @@
+"""End to end on CPU: `edl submit` -> operator spawns the master first, applies the
+JobResource, spawns workers; a worker is killed mid-run, the survivors shrink
+and continue, the operator replaces the dead worker, the replacement joins
+(scale-up with state broadcast) and the job completes."""
+import glob
+import json
+import os
+import subprocess
+import sys
+import textwrap
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.slow
+def test_submit_kill_replace_complete(tmp_path):
+    spec = tmp_path / "job.yaml"
+    spec.write_text(textwrap.dedent(f"""
+        apiVersion: edl.mi355x/v1
+        kind: ElasticJob
+        metadata: {{name: e2e}}
+        spec:
+          command: "python {ROOT}/tests/helpers/elastic_worker.py"
+          min_workers: 1
+          max_workers: 3
+          env: {{TEST_STEPS: "40", TEST_GB: "6", TEST_STEP_SLEEP: "0.1", EDL_FAULT: "kill@step=6,index=1"}}
+        ---
+        apiVersion: edl.mi355x/v1
+        kind: JobResource
+        metadata: {{name: e2e-resource}}
+        spec:
+          selector: {{name: e2e}}
+          worker: {{replicas: 3, resource: {{cpu: 1, gpu: 0}}}}
+        """))
+    r = subprocess.run([sys.executable, "-m", "easydl_amd.cli", "submit", str(spec), "--gpus", "",
+                        "--run-dir", str(tmp_path / "run"), "--timeout", "240"], cwd=ROOT,
+                       capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1"))
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    res = [json.load(open(f)) for f in glob.glob(str(tmp_path / "run" / "res*.json"))]
+    assert len(res) == 3, res  # workers 0, 2 and the replacement of 1
+    assert len({x["hash"] for x in res}) == 1, "replicas diverged"
+    assert all(x["step"] == 40 for x in res)
+    worlds = max(res, key=lambda x: len(x["worlds"]))["worlds"]
+    assert 2 in worlds and worlds[-1] == 3, worlds
+    ev = [json.loads(l) for f in glob.glob(str(tmp_path / "run" / "events-operator.jsonl")) for l in open(f)]
+    spawns = [e for e in ev if e["kind"] == "spawn"]
+    assert spawns[0]["name"] == "e2e-trainer-0"
+    assert sum(1 for e in spawns if e["name"] == "e2e-worker-1") == 2
