@@ -212,6 +212,24 @@ int edl_shm_latest(void* h, int64_t* step, int64_t* epoch, uint64_t* nbytes, uin
   return cur;
 }
 
+// Header of a specific slot: returns its state (0 empty, 1 writing, 2 committed).
+int edl_shm_slot_info(void* h, int slot, int64_t* step, int64_t* epoch, uint64_t* nbytes, uint64_t* checksum,
+                      char* meta, int metalen) {
+  auto* s = static_cast<Seg*>(h);
+  if (slot < 0 || slot >= (int)s->hdr()->nslots) return -EINVAL;
+  SlotHdr* sh = s->slot(slot);
+  int st = (int)__atomic_load_n(&sh->state, __ATOMIC_ACQUIRE);
+  if (step) *step = sh->step;
+  if (epoch) *epoch = sh->epoch;
+  if (nbytes) *nbytes = sh->nbytes;
+  if (checksum) *checksum = sh->checksum;
+  if (meta && metalen > 0) {
+    strncpy(meta, sh->meta, (size_t)metalen - 1);
+    meta[metalen - 1] = 0;
+  }
+  return st;
+}
+
 int edl_shm_close(void* h, int unlink_seg) {
   auto* s = static_cast<Seg*>(h);
   if (!s) return 0;

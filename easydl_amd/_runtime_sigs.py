@@ -33,6 +33,7 @@ SIGS = {
     "edl_shm_begin": (i32, [vp]),
     "edl_shm_commit": (i32, [vp, i32, i64, i64, u64, u64, cp]),
     "edl_shm_latest": (i32, [vp, i64p, i64p, u64p, u64p, cp, i32]),
+    "edl_shm_slot_info": (i32, [vp, i32, i64p, i64p, u64p, u64p, cp, i32]),
     "edl_shm_close": (i32, [vp, i32]),
     "edl_shm_unlink": (i32, [cp]),
     "edl_ckpt_engine_create": (vp, [i32, u64]),

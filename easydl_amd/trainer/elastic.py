@@ -267,6 +267,8 @@ class ElasticTrainer:
                 else:
                     apply, latest = ok, 0
                 if apply:
+                    if self.checkpoint is not None:
+                        self.checkpoint.fence()  # never update params under an in-flight snapshot
                     self.opt.step(pre_scale=1.0)
                     self.step += 1
                     self.last_loss = loss

@@ -1,0 +1,91 @@
+"""Checkpoint format v1 + shm A/B store + restore (CPU tier; GPU variant in test_ckpt_gpu)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from easydl_amd.ckpt.manager import CheckpointManager, ShmSegment, checksum_np, load_dir, shard_layout, \
+    unlink_job_segments
+from easydl_amd.models.llama import Llama, get_config
+from easydl_amd.trainer.context import TrainerContext
+from easydl_amd.trainer.data import SyntheticTokens
+from easydl_amd.trainer.elastic import ElasticTrainer
+
+CFG = get_config("llama-tiny", n_layers=1, dim=64, n_heads=4, n_kv_heads=2, ffn_dim=128, vocab_size=128)
+
+
+def _trainer(tmp, ckpt, seed=1234):
+    ctx = TrainerContext(job="ck", run_dir=str(tmp))
+    return ElasticTrainer(lambda d: Llama(CFG, device=d, dtype=torch.float32), global_batch=4, micro_batch=2,
+                          lr=1e-3, device="cpu", ctx=ctx, checkpoint=ckpt, seed=seed)
+
+
+def _flat(tr):
+    return torch.cat([g.data.clone() for g in tr.flat.groups] + [t.clone() for t in tr.opt.state_tensors().values()])
+
+
+def test_checksum_reference_properties():
+    a = np.arange(1000, dtype=np.uint32).view(np.uint8)
+    full = checksum_np(a)
+    # piecewise with base index == whole
+    assert (checksum_np(a[:400], 0) + checksum_np(a[400:], 100)) % (1 << 64) == full
+    b = a.copy()
+    b[4], b[8] = a[8], a[4]
+    assert checksum_np(b) != full
+
+
+def test_shard_layout_covers_everything():
+    ts = [("a", torch.zeros(1001)), ("b", torch.zeros(7, dtype=torch.bfloat16))]
+    seen = {"a": 0, "b": 0}
+    for r in range(3):
+        lay, end = shard_layout(ts, r, 3)
+        for d in lay:
+            seen[d["name"]] += d["hi"] - d["lo"]
+            assert d["offset"] % 4096 == 0
+    assert seen == {"a": 1001, "b": 7}
+
+
+def test_shm_ab_slots_survive_torn_write():
+    name = "/edl-test-ab-w1-s0"
+    seg = ShmSegment(name, 1 << 20, create=True)
+    try:
+        s0 = seg.begin()
+        seg.view(s0, 0, 4)[:] = [1, 2, 3, 4]
+        seg.commit(s0, 10, 1, 4, 123, {"x": 1})
+        s1 = seg.begin()
+        assert s1 != s0
+        seg.view(s1, 0, 4)[:] = [9, 9, 9, 9]  # torn: never committed
+        again = ShmSegment(name, create=False)
+        info = again.committed()
+        assert [i["step"] for i in info] == [10] and info[0]["checksum"] == 123
+        assert list(again.view(info[0]["slot"], 0, 4)) == [1, 2, 3, 4]
+        again.close()
+    finally:
+        seg.close(unlink=True)
+
+
+def test_snapshot_restore_resumes_bit_identically(tmp_path):
+    unlink_job_segments("ck")
+    data = SyntheticTokens(CFG.vocab_size, 16, num_samples=1024)
+    ref = _trainer(tmp_path, None)
+    ref.fit(lambda m, b: m(*b), data, num_steps=10)
+    ckpt = CheckpointManager("ck", interval=3, persist_dir=str(tmp_path / "disk"), persist_every=1)
+    try:
+        a = _trainer(tmp_path, ckpt)
+        a.fit(lambda m, b: m(*b), data, num_steps=7)
+        ckpt.wait()
+        assert ckpt.last_snapshot_step == 6
+        # a brand-new process (different init) restores step 6 from /dev/shm and continues
+        ckpt2 = CheckpointManager("ck", interval=100)
+        b = _trainer(tmp_path, ckpt2, seed=999)
+        b.fit(lambda m, b_: m(*b_), data, num_steps=10)
+        assert b.history[0]["step"] == 7  # resumed after step 6
+        assert torch.equal(_flat(b), _flat(ref))
+        # cold resume from disk (format v1)
+        ckpt._persist_thread.join()
+        c = _trainer(tmp_path, None, seed=5)
+        load_dir(str(tmp_path / "disk" / "step-6"), c)
+        assert c.step == 6
+    finally:
+        unlink_job_segments("ck")

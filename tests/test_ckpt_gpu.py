@@ -1,0 +1,50 @@
+"""In-memory snapshot through the native async D2H engine on the GPU + restore."""
+import pytest
+import torch
+
+from easydl_amd.ckpt.manager import CheckpointManager, checksum_np, checksum_tensor, unlink_job_segments
+from easydl_amd.models.llama import Llama, get_config
+from easydl_amd.trainer.context import TrainerContext
+from easydl_amd.trainer.data import SyntheticTokens
+from easydl_amd.trainer.elastic import ElasticTrainer
+
+pytestmark = pytest.mark.gpu
+CFG = get_config("llama-tiny")
+
+
+def _trainer(tmp, ckpt, seed, dev):
+    ctx = TrainerContext(job="ckg", run_dir=str(tmp))
+    return ElasticTrainer(lambda d: Llama(CFG, device=d), global_batch=2, micro_batch=2, lr=1e-3, device=dev,
+                          ctx=ctx, checkpoint=ckpt, seed=seed)
+
+
+def _flat(tr):
+    return torch.cat([g.data.float() for g in tr.flat.groups] + [t.float() for t in tr.opt.state_tensors().values()])
+
+
+def test_gpu_checksum_matches_reference(cuda):
+    x = torch.randint(-2**31, 2**31 - 1, (1 << 20,), dtype=torch.int32, device=cuda)
+    for n in (4, 1000, 4096, (1 << 20)):
+        got = int(checksum_tensor(x[:n], base_index=7).item()) & ((1 << 64) - 1)
+        assert got == checksum_np(x[:n].cpu().numpy().view("uint8"), 7)
+
+
+def test_async_snapshot_and_restore(cuda, tmp_path):
+    unlink_job_segments("ckg")
+    data = SyntheticTokens(CFG.vocab_size, 64, num_samples=4096)
+    ckpt = CheckpointManager("ckg", interval=2)
+    try:
+        a = _trainer(tmp_path, ckpt, 1, cuda)
+        a.fit(lambda m, b: m(*b), data, num_steps=5)
+        ckpt.wait()
+        assert ckpt.last_snapshot_step == 4 and ckpt.stats["snapshots"] == 2
+        a.fit  # keep alive
+        b = _trainer(tmp_path, CheckpointManager("ckg", interval=1000), 2, cuda)
+        b.fit(lambda m, b_: m(*b_), data, num_steps=4)   # restores step 4: nothing left to do
+        assert b.step == 4
+        ref = _trainer(tmp_path, None, 1, cuda)
+        ref.fit(lambda m, b_: m(*b_), data, num_steps=4)
+        assert torch.equal(_flat(b), _flat(ref))
+    finally:
+        ckpt.close()
+        unlink_job_segments("ckg")
