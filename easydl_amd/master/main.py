@@ -91,6 +91,7 @@ def main(argv=None):
     ap.add_argument("--port", type=int, default=int(os.environ.get("EDL_MASTER_PORT", 29400)))
     ap.add_argument("--min", type=int, default=1)
     ap.add_argument("--max", type=int, default=8)
+    ap.add_argument("--initial", type=int, default=0, help="first epoch waits for this many workers")
     ap.add_argument("--join-window", type=float, default=0.5)
     ap.add_argument("--hb-timeout", type=float, default=15.0)
     ap.add_argument("--policy", default="shrink")
@@ -101,7 +102,7 @@ def main(argv=None):
     ap.add_argument("--job-resource", default=None, help="user JobResource JSON/YAML (Brain not consulted)")
     a = ap.parse_args(argv)
     logging.basicConfig(level=logging.INFO, format="%(asctime)s [master] %(message)s")
-    cfg = RendezvousConfig(min_nodes=a.min, max_nodes=a.max, join_window_s=a.join_window,
+    cfg = RendezvousConfig(min_nodes=a.min, max_nodes=a.max, initial_nodes=a.initial, join_window_s=a.join_window,
                            heartbeat_timeout_s=a.hb_timeout, policy=a.policy)
     planner = None
     if a.job_spec:

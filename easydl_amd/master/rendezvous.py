@@ -47,6 +47,8 @@ log = logging.getLogger(__name__)
 class RendezvousConfig:
     min_nodes: int = 1
     max_nodes: int = 8
+    initial_nodes: int = 0          # first epoch waits for this many (0: min_nodes) ...
+    initial_timeout_s: float = 300.0  # ... but not longer than this
     join_window_s: float = 0.5      # wait for stragglers before forming / growing an epoch
     heartbeat_timeout_s: float = 15.0
     policy: str = "shrink"          # on failure: "shrink" (continue with survivors) or "replace" (wait)
@@ -120,19 +122,30 @@ class RendezvousManager:
         members = self.members()
         alive = [n for n in joined if n not in dead and n not in leaving]
         broken = [m for m in members if m in dead]
-        if broken and not self.kv.exists(f"rdzv/abort/{cur}"):
-            self.kv.set(f"rdzv/abort/{cur}", json.dumps({"dead": broken, "ts": now}))
-            self._event("epoch_abort", epoch=cur, dead=broken)
-            self._broken_ts = now
+        # abort every recent epoch that contains a dead node: ranks may still be
+        # running an older epoch (membership changes apply at step boundaries)
+        for e in range(max(1, cur - 4), cur + 1):
+            a = self.assignment(e)
+            if not a or self.kv.exists(f"rdzv/abort/{e}"):
+                continue
+            bad = [m for m in a["members"] if m in dead]
+            if bad:
+                self.kv.set(f"rdzv/abort/{e}", json.dumps({"dead": bad, "ts": now}))
+                self._event("epoch_abort", epoch=e, dead=bad)
+                if e == cur:
+                    self._broken_ts = now
         max_n = self.cfg.max_nodes if self.target_nodes is None else min(self.cfg.max_nodes, self.target_nodes)
         waiting = [n for n in alive if n not in members]
         survivors = [m for m in members if m in alive]
         reason = None
         if cur == 0:
+            want = max(self.cfg.min_nodes, min(self.cfg.initial_nodes, max_n))
             if len(alive) >= self.cfg.min_nodes:
                 if self._first_wait_ts is None:
                     self._first_wait_ts = now
-                if len(alive) >= max_n or now - self._first_wait_ts >= self.cfg.join_window_s:
+                waited = now - self._first_wait_ts
+                if len(alive) >= max_n or (waited >= self.cfg.join_window_s and
+                                           (len(alive) >= want or waited >= self.cfg.initial_timeout_s)):
                     reason = "initial"
         elif broken:
             replace_ok = (self.cfg.policy == "shrink" or len(survivors) + len(waiting) >= len(members)
@@ -240,7 +253,7 @@ class RendezvousClient:
         t_end = time.monotonic() + timeout_s
         while time.monotonic() < t_end:
             e = self.latest_epoch()
-            if e > after_epoch:
+            if e > after_epoch and not self.aborted(e):
                 a = self.kv.get(f"rdzv/assign/{e}")
                 if a and self.node_id in a["members"]:
                     self.epoch = e

@@ -122,6 +122,7 @@ class ElasticOperator:
         argv = self.master_argv or [self.cfg.python, "-m", "easydl_amd.master.main", "--job", self.job.name,
                                     "--port", str(self.master_port), "--run-dir", self.run_dir,
                                     "--min", str(self.job.min_workers), "--max", str(self.job.max_workers),
+                                    "--initial", str(self.desired.replicas("worker") if self.desired else 0),
                                     "--job-spec", os.path.join(self.run_dir, "job.json")]
         if self.desired is not None and self.master_argv is None:
             # a user-supplied JobResource is handed to the master, which applies it

@@ -37,7 +37,7 @@ def _td(s: float) -> datetime.timedelta:
 
 class Communicator:
     def __init__(self, store: dist.Store, rank: int, world_size: int, epoch: int, *, device: torch.device,
-                 job: str = "job", timeout_s: float = 120.0, control_timeout_s: float = 60.0,
+                 job: str = "job", timeout_s: float = 120.0, control_timeout_s: float = 30.0,
                  high_priority: bool = True):
         self.rank = rank
         self.world_size = world_size
@@ -76,10 +76,13 @@ class Communicator:
             if self._aborted:
                 return
             self._aborted = True
-        for pg in (self.data, self.ctrl):
+        # RCCL: ncclCommAbort makes kernels blocked on a dead peer exit.  Gloo
+        # collectives already fail as soon as a peer's sockets close, and
+        # ProcessGroupGloo.abort() leaves worker threads that std::terminate the
+        # process at teardown, so gloo groups are only marked, never aborted.
+        if self.backend == "rccl":
             try:
-                if hasattr(pg, "abort"):
-                    pg.abort()
+                self.data.abort()
             except Exception as e:  # pragma: no cover - best effort
                 log.debug("abort failed: %s", e)
 

@@ -134,25 +134,77 @@ class ElasticTrainer:
         self._watchdog.start()
 
     def _enter_epoch(self):
-        t0 = time.time()
-        if self.rdzv is None:
-            self.comm = LocalCommunicator(self.device)
-            self.assignment = None
-        else:
-            a = self.rdzv.wait_assignment(after_epoch=self.assignment.epoch if self.assignment else 0)
-            self.assignment = a
-            self.events.emit("epoch_joined", epoch=a.epoch, rank=a.rank, world=a.world, reason=a.reason)
-            if a.world == 1:
-                self.comm = LocalCommunicator(self.device, epoch=a.epoch)
+        """Join the next live epoch; retries when the epoch breaks while it is being built."""
+        while True:
+            t0 = time.time()
+            if self.rdzv is None:
+                self.comm = LocalCommunicator(self.device)
+                self.assignment = None
             else:
-                self.comm = Communicator(self._store, a.rank, a.world, a.epoch, device=self.device,
-                                         job=self.ctx.job)
-                self.comm.warmup()
-        self.events.emit("comm_ready", epoch=self.comm.epoch, world=self.comm.world_size,
-                         rank=self.comm.rank, init_s=round(time.time() - t0, 4))
-        self._sync_state()
-        self.ddp.set_comm(self.comm)
-        self.events.emit("state_synced", epoch=self.comm.epoch, step=self.step)
+                a = self.rdzv.wait_assignment(after_epoch=self.assignment.epoch if self.assignment else 0)
+                self.assignment = a
+                self.events.emit("epoch_joined", epoch=a.epoch, rank=a.rank, world=a.world, reason=a.reason)
+                if a.world == 1:
+                    self.comm = LocalCommunicator(self.device, epoch=a.epoch)
+                else:
+                    comm = self._build_comm(a)
+                    if comm is None:
+                        self.events.emit("epoch_skipped", epoch=a.epoch)
+                        continue
+                    self.comm = comm
+            self.events.emit("comm_ready", epoch=self.comm.epoch, world=self.comm.world_size,
+                             rank=self.comm.rank, init_s=round(time.time() - t0, 4))
+            try:
+                self._sync_state()
+            except (CommAborted, RuntimeError) as e:
+                if self.rdzv is None or not (self.comm.aborted or self.rdzv.aborted(self.comm.epoch)
+                                             or _is_comm_error(e)):
+                    raise
+                self.events.emit("epoch_skipped", epoch=self.comm.epoch, during="state_sync")
+                self.comm.abort()
+                continue
+            self.ddp.set_comm(self.comm)
+            self.events.emit("state_synced", epoch=self.comm.epoch, step=self.step)
+            return
+
+    def _build_comm(self, a):
+        """Arrival barrier, then construct + warm up the epoch's communicator.
+
+        Process-group construction blocks inside C++ while holding the GIL, so
+        we first wait — with non-blocking store polls that notice an abort —
+        until every member has arrived; the construction itself then completes
+        promptly.  It still runs in a helper thread as a second line of defence.
+        """
+        self.rdzv.kv.add(f"rdzv/arrive/{a.epoch}", 1)
+        while self.rdzv.kv.counter(f"rdzv/arrive/{a.epoch}") < a.world:
+            if self.rdzv.aborted(a.epoch):
+                return None
+            time.sleep(0.002)
+        box = {}
+
+        def build():
+            try:
+                c = Communicator(self._store, a.rank, a.world, a.epoch, device=self.device, job=self.ctx.job)
+                c.warmup()
+                box["comm"] = c
+            except Exception as e:  # noqa: BLE001 - reported through box
+                box["err"] = e
+
+        th = threading.Thread(target=build, name=f"edl-comm-e{a.epoch}", daemon=True)
+        th.start()
+        while th.is_alive():
+            th.join(0.02)
+            if th.is_alive() and self.rdzv.aborted(a.epoch):
+                return None  # abandon: the thread times out on its own
+        if "err" in box:
+            if self.rdzv.aborted(a.epoch) or _is_comm_error(box["err"]):
+                return None
+            raise box["err"]
+        c = box["comm"]
+        if self.rdzv.aborted(a.epoch):
+            c.abort()
+            return None
+        return c
 
     def _state_tensors(self) -> list[torch.Tensor]:
         ts = [g.data for g in self.flat.groups]
@@ -306,7 +358,15 @@ class ElasticTrainer:
     def close(self):
         self._stop.set()
         if self.rdzv is not None:
+            try:
+                self.rdzv.leave()  # finished: not a failure
+            except Exception:
+                pass
             self.rdzv.stop_heartbeat()
+            if self.rdzv._hb is not None:
+                self.rdzv._hb.join(timeout=5)
+        if self._watchdog is not None:
+            self._watchdog.join(timeout=5)
         if self._manager is not None:
             self._manager.stop()
         if self.comm is not None and not self.comm.aborted:

@@ -30,9 +30,10 @@ def _env(tmp, idx, extra):
     return e
 
 
-def _start_master(tmp, port, mn, mx, window=0.3):
+def _start_master(tmp, port, mn, mx, window=0.3, initial=0):
     return subprocess.Popen([sys.executable, "-m", "easydl_amd.master.main", "--job", "t", "--port", str(port),
                              "--min", str(mn), "--max", str(mx), "--join-window", str(window),
+                             "--initial", str(initial),
                              "--run-dir", str(tmp)], cwd=ROOT, env=dict(os.environ, PYTHONPATH=ROOT),
                             stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
 
@@ -72,7 +73,7 @@ def test_torchrun_style_static_world(tmp_path):
 @pytest.mark.slow
 def test_kill_worker_shrinks_and_continues(tmp_path):
     port = free_port()
-    m = _start_master(tmp_path, port, 1, 3)
+    m = _start_master(tmp_path, port, 1, 3, initial=3)
     try:
         procs = {}
         for i in range(3):
