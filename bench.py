@@ -42,6 +42,8 @@ def parse():
     ap.add_argument("--bucket-mb", type=float, default=None)
     ap.add_argument("--layers", type=int, default=None, help="override layer count (debug only; invalid for the metric)")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--ckpt-interval", type=int, default=0,
+                    help="in-memory sharded snapshot every K steps (async D2H, overlapped)")
     ap.add_argument("--fault-inject", action="store_true", help="measure time-to-recover instead (local operator)")
     return ap.parse_args()
 
@@ -70,8 +72,14 @@ def main():
     dtype = torch.bfloat16 if use_cuda else torch.float32
     S, B = args.seq, args.mbs
     gb = world * B * args.accum
+    ckpt = None
+    if args.ckpt_interval > 0:
+        from easydl_amd.ckpt.manager import CheckpointManager, unlink_job_segments
+        unlink_job_segments("bench")
+        ckpt = CheckpointManager("bench", interval=args.ckpt_interval)
     tr = ElasticTrainer(lambda d: Llama(cfg, device=d, dtype=dtype), lr=3e-4, betas=(0.9, 0.95), weight_decay=0.1,
-                        max_grad_norm=1.0, global_batch=gb, micro_batch=B, device=dev, bucket_mb=args.bucket_mb)
+                        max_grad_norm=1.0, global_batch=gb, micro_batch=B, device=dev, bucket_mb=args.bucket_mb,
+                        checkpoint=ckpt)
     marks = {}
 
     def sync_barrier(t):
@@ -129,6 +137,8 @@ def main():
         "peak_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 2**30, 1) if use_cuda else 0.0,
         "setup_and_warmup_s": round(marks["t0"] - t_start, 2),
         "time_to_recover_s": None,
+        "ckpt": None if ckpt is None else {"interval": args.ckpt_interval, "snapshots": ckpt.stats["snapshots"],
+                                           "bytes_per_snapshot": ckpt.stats["d2h_bytes"] // max(1, ckpt.stats["snapshots"])},
     }
     if comm.rank == 0:
         line = json.dumps(res)
@@ -137,6 +147,10 @@ def main():
             with open(args.out, "w") as f:
                 f.write(line + "\n")
     tr.close()
+    if ckpt is not None:
+        ckpt.close()
+        from easydl_amd.ckpt.manager import unlink_job_segments
+        unlink_job_segments("bench")
 
 
 if __name__ == "__main__":

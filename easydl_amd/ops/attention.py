@@ -1,0 +1,76 @@
+"""Flash attention (csrc/kernels/attention.hip): causal GQA, head_dim 128, bf16.
+
+Inputs are the ``[B, H, S, D]``-shaped views of token-major ``[B, S, H, D]``
+memory that the fused RoPE+QKV kernel produces; the output is returned the
+same way, so ``o.transpose(1, 2).reshape(B*S, H*D)`` feeding the output
+projection is free.  The forward saves only O and the log-sum-exp (fp32
+[B,H,S]); the backward recomputes P tile by tile (dK/dV kernel + dQ kernel,
+no float atomics).  ``EDL_ATTN=sdpa`` falls back to PyTorch SDPA (used for
+A/B comparisons); other head dims also use SDPA.
+"""
+from __future__ import annotations
+
+import math
+import os
+
+import torch
+import torch.nn.functional as F
+
+from easydl_amd import _native
+
+
+def _bshd(t: torch.Tensor) -> torch.Tensor:
+    """[B,H,S,D]-shaped tensor -> contiguous [B,S,H,D] memory (no copy if already laid out so)."""
+    return t.transpose(1, 2).contiguous()
+
+
+class _FlashAttnFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, k, v, causal, scale):
+        kn = _native.kernels()
+        B, H, S, D = q.shape
+        KV = k.shape[1]
+        qm, km, vm = _bshd(q), _bshd(k), _bshd(v)
+        o = torch.empty_like(qm)
+        lse = torch.empty(B, H, S, dtype=torch.float32, device=q.device)
+        kn.check("edl_attn_fwd", qm.data_ptr(), km.data_ptr(), vm.data_ptr(), o.data_ptr(), lse.data_ptr(), B, S, H,
+                 KV, D, 1 if causal else 0, scale, _native.stream_of(q))
+        ctx.save_for_backward(qm, km, vm, o, lse)
+        ctx.causal, ctx.scale = causal, scale
+        return o.transpose(1, 2)
+
+    @staticmethod
+    def backward(ctx, do):
+        kn = _native.kernels()
+        qm, km, vm, o, lse = ctx.saved_tensors
+        B, S, H, D = qm.shape
+        KV = km.shape[2]
+        dom = _bshd(do)
+        dq, dk, dv = torch.empty_like(qm), torch.empty_like(km), torch.empty_like(vm)
+        delta = torch.empty(B, H, S, dtype=torch.float32, device=qm.device)
+        kn.check("edl_attn_bwd", qm.data_ptr(), km.data_ptr(), vm.data_ptr(), o.data_ptr(), dom.data_ptr(),
+                 lse.data_ptr(), delta.data_ptr(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), B, S, H, KV, D,
+                 1 if ctx.causal else 0, ctx.scale, _native.stream_of(qm))
+        return dq.transpose(1, 2), dk.transpose(1, 2), dv.transpose(1, 2), None, None
+
+
+def attention_ref(q, k, v, causal=True, scale=None):
+    """fp32 reference (GQA by head repetition)."""
+    H, KV = q.shape[1], k.shape[1]
+    if H != KV:
+        k = k.repeat_interleave(H // KV, dim=1)
+        v = v.repeat_interleave(H // KV, dim=1)
+    return F.scaled_dot_product_attention(q.float(), k.float(), v.float(), is_causal=causal,
+                                          scale=scale).to(q.dtype)
+
+
+def flash_attention(q, k, v, causal: bool = True, scale: float | None = None):
+    """q [B,H,S,D], k/v [B,KV,S,D] -> [B,H,S,D]."""
+    D = q.shape[-1]
+    scale = 1.0 / math.sqrt(D) if scale is None else scale
+    if q.is_cuda:
+        if D == 128 and q.dtype == torch.bfloat16 and os.environ.get("EDL_ATTN", "hip") == "hip":
+            return _FlashAttnFn.apply(q, k, v, causal, scale)
+        return F.scaled_dot_product_attention(q, k, v, is_causal=causal, scale=scale,
+                                              enable_gqa=q.shape[1] != k.shape[1])
+    return attention_ref(q, k, v, causal, scale)

@@ -1,0 +1,66 @@
+"""Hand-written flash attention vs an fp32 reference (GPU)."""
+import math
+
+import pytest
+import torch
+
+from easydl_amd.ops.attention import attention_ref, flash_attention
+
+pytestmark = pytest.mark.gpu
+
+
+def _mk(B, S, H, KV, dev, seed):
+    g = torch.Generator(device=dev).manual_seed(seed)
+    q = torch.randn(B, S, H, 128, device=dev, generator=g).to(torch.bfloat16).transpose(1, 2)
+    k = torch.randn(B, S, KV, 128, device=dev, generator=g).to(torch.bfloat16).transpose(1, 2)
+    v = torch.randn(B, S, KV, 128, device=dev, generator=g).to(torch.bfloat16).transpose(1, 2)
+    return q, k, v
+
+
+def _err(a, b):
+    return ((a.float() - b.float()).abs().max() / (b.float().abs().max() + 1e-6)).item()
+
+
+@pytest.mark.parametrize("B,S,H,KV,causal", [(1, 128, 4, 4, True), (2, 256, 8, 2, True), (1, 200, 4, 1, True),
+                                             (1, 384, 8, 8, False), (1, 1024, 32, 8, True)])
+def test_flash_attention_fwd_bwd(cuda, B, S, H, KV, causal):
+    q, k, v = _mk(B, S, H, KV, cuda, S + H)
+    q1, k1, v1 = (t.detach().clone().requires_grad_() for t in (q, k, v))
+    o = flash_attention(q1, k1, v1, causal=causal)
+    do = torch.randn_like(o)
+    o.backward(do)
+    q2, k2, v2 = (t.detach().float().requires_grad_() for t in (q, k, v))
+    o2 = attention_ref(q2, k2, v2, causal=causal)
+    o2.backward(do.float())
+    assert _err(o, o2) < 2e-2, "forward"
+    assert _err(q1.grad, q2.grad) < 3e-2, "dq"
+    assert _err(k1.grad, k2.grad) < 3e-2, "dk"
+    assert _err(v1.grad, v2.grad) < 3e-2, "dv"
+
+
+def test_flash_attention_speed_report(cuda):
+    """Not an assertion on speed: prints TFLOP/s of fwd and fwd+bwd at the Llama-3-8B shape."""
+    B, S, H, KV = 1, 8192, 32, 8
+    q, k, v = _mk(B, S, H, KV, cuda, 0)
+    q.requires_grad_()
+    k.requires_grad_()
+    v.requires_grad_()
+    flops = 4 * B * H * S * S * 128 / 2
+    o = flash_attention(q, k, v)
+    do = torch.randn_like(o)
+    for _ in range(2):
+        flash_attention(q, k, v).backward(do)
+    torch.cuda.synchronize()
+    e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+    e0.record()
+    for _ in range(5):
+        flash_attention(q, k, v)
+    e1.record()
+    for _ in range(5):
+        flash_attention(q, k, v).backward(do)
+    e2.record()
+    torch.cuda.synchronize()
+    f = e0.elapsed_time(e1) / 5
+    fb = e1.elapsed_time(e2) / 5
+    print(f"\n[attn] fwd {f:.3f} ms = {flops / f / 1e9:.0f} TF/s ; fwd+bwd {fb:.3f} ms = "
+          f"{3.5 * flops / fb / 1e9:.0f} TF/s")
