@@ -69,7 +69,7 @@ def flash_attention(q, k, v, causal: bool = True, scale: float | None = None):
     D = q.shape[-1]
     scale = 1.0 / math.sqrt(D) if scale is None else scale
     if q.is_cuda:
-        if D == 128 and q.dtype == torch.bfloat16 and os.environ.get("EDL_ATTN", "hip") == "hip":
+        if D == 128 and q.dtype == torch.bfloat16 and os.environ.get("EDL_ATTN", "hip") != "sdpa":
             return _FlashAttnFn.apply(q, k, v, causal, scale)
         return F.scaled_dot_product_attention(q, k, v, is_causal=causal, scale=scale,
                                               enable_gqa=q.shape[1] != k.shape[1])
