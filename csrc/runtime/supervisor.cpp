@@ -242,11 +242,13 @@ void edl_sup_destroy(void* h) {
     if (edl_sup_num_children(s) == 0) break;
     edl_sup_wait(s, 20, ev, 16);
   }
-  std::lock_guard<std::mutex> g(s->mu);
-  for (auto& kv : s->children)
-    if (kv.second.pidfd >= 0) close(kv.second.pidfd);
-  close(s->epfd);
-  s->children.clear();
+  {
+    std::lock_guard<std::mutex> g(s->mu);
+    for (auto& kv : s->children)
+      if (kv.second.pidfd >= 0) close(kv.second.pidfd);
+    close(s->epfd);
+    s->children.clear();
+  }  // the lock must be released before the supervisor (and its mutex) is freed
   delete s;
 }
 

@@ -40,8 +40,19 @@ class JobMaster:
         self.events = EventLog(os.path.join(self.run_dir, "events-master.jsonl"), proc="master")
         self.rdzv = RendezvousManager(self.kv, rdzv or RendezvousConfig(), events=self.events)
         self.planner = planner
+        self.rdzv.on_dead.append(self._requeue_data)
         self._stop = threading.Event()
         self._threads: list[threading.Thread] = []
+
+    def _requeue_data(self, node: str) -> None:
+        cfg = self.kv.get("data/config")
+        if not cfg:
+            return
+        from easydl_amd.master.dispatcher import ShardDispatcher
+        d = ShardDispatcher(self.kv, int(cfg["n"]), int(cfg["shard_size"]), int(cfg.get("epochs", 1)))
+        shards = d.requeue_dead({node})
+        if shards:
+            self.events.emit("data_requeued", node=node, shards=shards)
 
     # exit events from the operator's supervisor -> immediate death marks
     def _scan_exit_events(self):

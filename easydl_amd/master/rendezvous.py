@@ -69,6 +69,7 @@ class RendezvousManager:
         self._thread = None
         self.dead: dict[str, str] = {}
         self.target_nodes: int | None = None  # plan-driven target (Brain / JobResource)
+        self.on_dead = []  # callbacks(node) run once per death (data requeue, metrics)
 
     # -- store views ---------------------------------------------------------
     def joined(self) -> list[str]:
@@ -94,6 +95,11 @@ class RendezvousManager:
         if not self.kv.exists(f"ev/dead/{node}"):
             self.kv.set(f"ev/dead/{node}", reason)
             self._event("node_dead", node=node, reason=reason)
+            for cb in self.on_dead:
+                try:
+                    cb(node)
+                except Exception as e:  # keep the master alive
+                    log.warning("on_dead callback failed: %s", e)
 
     def _event(self, kind, **kw):
         if self.events is not None:

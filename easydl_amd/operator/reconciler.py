@@ -366,6 +366,13 @@ class ElasticOperator:
     def shutdown(self) -> None:
         if self.kv is not None:
             try:
+                self.kv.set("job/done", "1")      # PS / evaluator roles exit on their own
+                t_end = time.time() + 5
+                while time.time() < t_end and any(p.state == "running" and p.role in ("parameter_server",
+                                                                                        "evaluator")
+                                                  for p in self.procs.values()):
+                    for ex in self.launcher.poll(0.1):
+                        self.handle_exit(ex)
                 self.kv.set("master/shutdown", "1")
             except Exception:
                 pass

@@ -1,0 +1,130 @@
+"""Worker-side PS client + parameter partitioner.
+
+Partitioning balances parameter bytes over the PS shards (largest tensors
+first onto the least-loaded shard); it is a pure function of the model's
+parameter names and sizes, so every role computes the same assignment without
+coordination.  PS addresses are discovered through the job master's store
+(``ps/addr/<i>``), and a client transparently reconnects when a PS is replaced
+(new incarnation, new port).
+"""
+from __future__ import annotations
+
+import json
+import socket
+import threading
+import time
+from concurrent.futures import ThreadPoolExecutor
+
+import torch
+
+from easydl_amd.ps.wire import connect, recv_msg, send_msg
+
+
+def partition(named_sizes: list[tuple[str, int]], num_ps: int) -> dict[str, int]:
+    load = [0] * num_ps
+    out = {}
+    for name, n in sorted(named_sizes, key=lambda x: (-x[1], x[0])):
+        i = min(range(num_ps), key=lambda j: (load[j], j))
+        out[name] = i
+        load[i] += n
+    return out
+
+
+def shard_of(model: torch.nn.Module, num_ps: int, index: int) -> dict[str, torch.Tensor]:
+    assign = partition([(n, p.numel()) for n, p in model.named_parameters()], num_ps)
+    return {n: p.detach() for n, p in model.named_parameters() if assign[n] == index}
+
+
+class PSClient:
+    def __init__(self, num_ps: int, resolve, worker_id: str, retry_s: float = 120.0):
+        """``resolve(i) -> (host, port)`` returns the current address of PS i."""
+        self.num_ps = num_ps
+        self.resolve = resolve
+        self.worker_id = worker_id
+        self.retry_s = retry_s
+        self._socks: dict[int, socket.socket] = {}
+        self._locks = [threading.Lock() for _ in range(num_ps)]
+        self._pool = ThreadPoolExecutor(max_workers=max(1, num_ps))
+        self.versions = [0] * num_ps
+        self.assign: dict[str, int] = {}
+
+    def bind(self, model: torch.nn.Module) -> None:
+        self.assign = partition([(n, p.numel()) for n, p in model.named_parameters()], self.num_ps)
+
+    def _call(self, i: int, header: dict, tensors=None):
+        t_end = time.monotonic() + self.retry_s
+        while True:
+            with self._locks[i]:
+                try:
+                    if i not in self._socks:
+                        self._socks[i] = connect(*self.resolve(i))
+                    send_msg(self._socks[i], header, tensors)
+                    return recv_msg(self._socks[i])
+                except (ConnectionError, OSError, TimeoutError):
+                    s = self._socks.pop(i, None)
+                    if s is not None:
+                        try:
+                            s.close()
+                        except OSError:
+                            pass
+                    if time.monotonic() > t_end:
+                        raise
+            time.sleep(0.2)  # PS being replaced: re-resolve and retry
+
+    def pull(self, model: torch.nn.Module, min_versions=None) -> list[int]:
+        params = dict(model.named_parameters())
+
+        def one(i):
+            names = [n for n, j in self.assign.items() if j == i]
+            hdr = {"op": "pull", "names": names}
+            if min_versions is not None:
+                hdr["min_version"] = min_versions[i]
+            h, ts = self._call(i, hdr)
+            with torch.no_grad():
+                for n, t in ts.items():
+                    params[n].copy_(t.to(params[n].device, params[n].dtype), non_blocking=True)
+            return h["version"]
+
+        self.versions = list(self._pool.map(one, range(self.num_ps)))
+        return self.versions
+
+    def push(self, model: torch.nn.Module, step: int = 0) -> list[int]:
+        params = dict(model.named_parameters())
+
+        def one(i):
+            grads = {}
+            for n, j in self.assign.items():
+                if j == i:
+                    g = params[n].grad
+                    grads[n] = (g if g is not None else torch.zeros_like(params[n])).detach().float()
+            h, _ = self._call(i, {"op": "push", "worker": self.worker_id, "step": step}, grads)
+            return h["version"]
+
+        self.versions = list(self._pool.map(one, range(self.num_ps)))
+        return self.versions
+
+    def stats(self) -> list[dict]:
+        return [self._call(i, {"op": "stats"})[0] for i in range(self.num_ps)]
+
+    def close(self):
+        for s in self._socks.values():
+            try:
+                s.close()
+            except OSError:
+                pass
+        self._socks.clear()
+        self._pool.shutdown(wait=False)
+
+
+def store_resolver(kv, timeout_s: float = 300.0):
+    def resolve(i: int):
+        t_end = time.monotonic() + timeout_s
+        while time.monotonic() < t_end:
+            a = kv.get(f"ps/addr/{i}")
+            if a:
+                a = a if isinstance(a, dict) else json.loads(a)
+                return a["host"], int(a["port"])
+            time.sleep(0.1)
+        raise TimeoutError(f"PS {i} address not published")
+
+    return resolve

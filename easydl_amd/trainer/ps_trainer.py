@@ -1,0 +1,133 @@
+"""Parameter-server mode roles: PS, worker, evaluator.
+
+Launched by the local ElasticOperator with the ``EDL_*`` environment; one
+entry point (e.g. ``python -m easydl_amd.examples.mnist``) dispatches on
+``EDL_ROLE``.  Workers pull the latest parameters from every PS shard, run
+forward/backward on a data shard claimed from the master's dispatcher and push
+gradients; PS shards apply them (async, or sync rounds over the live workers).
+The evaluator periodically pulls and scores the model (reference
+docs/design/elastic-training-operator.md:43-44,79-85).
+"""
+from __future__ import annotations
+
+import json
+import logging
+import os
+import socket
+import time
+
+import torch
+
+from easydl_amd.master.dispatcher import ShardDispatcher
+from easydl_amd.master.rendezvous import RendezvousClient
+from easydl_amd.master.store import KV, make_tcp_store
+from easydl_amd.ps.client import PSClient, shard_of, store_resolver
+from easydl_amd.ps.server import ParameterServer, PSSnapshotter
+from easydl_amd.trainer.context import TrainerContext
+from easydl_amd.utils import fault
+from easydl_amd.utils.events import EventLog
+
+log = logging.getLogger("edl.ps_trainer")
+
+
+def _kv(ctx: TrainerContext) -> KV:
+    return KV(make_tcp_store(ctx.master_addr, ctx.master_port, False), f"edl/{ctx.job}")
+
+
+def _world(kv) -> int:
+    e = kv.counter("rdzv/epoch")
+    a = kv.get(f"rdzv/assign/{e}") if e else None
+    return int(a["world"]) if a else 1
+
+
+def run_ps(model_fn, num_ps: int, ctx: TrainerContext | None = None, *, optimizer="adam", lr=1e-3, mode="async",
+           snapshot_every: int = 20, device="cpu", seed: int = 1234) -> None:
+    ctx = ctx or TrainerContext.from_env()
+    kv = _kv(ctx)
+    events = EventLog(os.path.join(ctx.run_dir, f"events-ps{ctx.index}.jsonl"), proc=f"ps{ctx.index}")
+    torch.manual_seed(seed)
+    model = model_fn(device)
+    snap = PSSnapshotter(ctx.job, ctx.index)
+    ps = ParameterServer(ctx.index, shard_of(model, num_ps, ctx.index), optimizer=optimizer, lr=lr, mode=mode,
+                         expected_workers=lambda: _world(kv), device=device, snapshot=snap,
+                         snapshot_every=snapshot_every)
+    if snap.restore(ps):
+        events.emit("ps_restored", version=ps.version)
+    ps.start()
+    kv.set(f"ps/addr/{ctx.index}", json.dumps({"host": ps.host, "port": ps.port, "pid": os.getpid(),
+                                                "gen": int(os.environ.get("EDL_GENERATION", 0))}))
+    events.emit("ps_started", port=ps.port, params=ps.state.numel)
+    try:
+        while not kv.exists("job/done") and not ps._stop.is_set():
+            time.sleep(0.2)
+    finally:
+        ps.stop()
+
+
+class PSWorker:
+    def __init__(self, model_fn, num_ps: int, ctx: TrainerContext | None = None, device="cpu", seed: int = 1234):
+        self.ctx = ctx or TrainerContext.from_env()
+        self.device = torch.device(device)
+        torch.manual_seed(seed)
+        self.model = model_fn(self.device)
+        self.kv = _kv(self.ctx)
+        self.events = EventLog(os.path.join(self.ctx.run_dir, f"events-worker{self.ctx.index}.jsonl"),
+                               proc=f"worker{self.ctx.index}")
+        self.rdzv = RendezvousClient(self.kv, self.ctx.node_id, {"index": self.ctx.index, "role": "worker"})
+        self.client = PSClient(num_ps, store_resolver(self.kv), self.ctx.node_id)
+        self.client.bind(self.model)
+        self.fault = fault.FaultInjector.from_env(self.ctx, self.events)
+        self.steps = 0
+
+    def fit(self, loss_fn, data, batch_size: int, shard_size: int, epochs: int = 1, on_step=None):
+        self.rdzv.join()
+        disp = ShardDispatcher(self.kv, len(data), shard_size, epochs)
+        self.kv.set("data/config", json.dumps({"n": len(data), "shard_size": shard_size, "epochs": epochs}))
+        try:
+            while True:
+                shard = disp.claim(self.ctx.node_id)
+                if shard is None:
+                    break
+                lo, hi = disp.shard_range(shard)
+                for b0 in range(lo, hi, batch_size):
+                    self.fault.maybe_inject("step_start", self.steps, trainer=None)
+                    self.client.pull(self.model)
+                    self.model.zero_grad(set_to_none=False)
+                    loss = loss_fn(self.model, data.batch(range(b0, min(hi, b0 + batch_size)), self.device))
+                    loss.backward()
+                    self.client.push(self.model, self.steps)
+                    self.steps += 1
+                    if on_step is not None:
+                        on_step(self, loss)
+                disp.complete(shard)
+                self.events.emit("shard_done", shard=shard, steps=self.steps)
+        finally:
+            self.rdzv.leave()
+            self.rdzv.stop_heartbeat()
+        if disp.done() >= disp.total:
+            self.kv.set("job/data_exhausted", "1")
+        return self
+
+
+def run_evaluator(model_fn, num_ps: int, eval_fn, ctx: TrainerContext | None = None, interval_s: float = 1.0,
+                  device="cpu", seed: int = 1234):
+    ctx = ctx or TrainerContext.from_env()
+    kv = _kv(ctx)
+    torch.manual_seed(seed)
+    model = model_fn(device)
+    client = PSClient(num_ps, store_resolver(kv), ctx.node_id)
+    client.bind(model)
+    events = EventLog(os.path.join(ctx.run_dir, f"events-evaluator{ctx.index}.jsonl"), proc="evaluator")
+    last = None
+    while not kv.exists("job/done"):
+        vers = client.pull(model)
+        if vers != last:
+            metrics = eval_fn(model)
+            metrics["versions"] = vers
+            kv.set("eval/latest", json.dumps(metrics))
+            events.emit("eval", **metrics)
+            last = vers
+        if kv.exists("job/data_exhausted"):
+            break
+        time.sleep(interval_s)
+    client.close()
