@@ -136,11 +136,15 @@ class LlamaBlock(nn.Module):
         self.mlp_norm = _param((d,), 0, device, dtype)
         self.w_gu = _param((2 * self.ffn, d), std, device, dtype)
         self.w_down = _param((d, self.ffn), out_std, device, dtype)
-        # tensor-parallel hooks (identity for the dense model)
+        # tensor-parallel hooks (identity for the dense model): tp_copy before the
+        # column-parallel projections, tp_reduce after the row-parallel ones
         self.tp_reduce = None
+        self.tp_copy = None
 
     def _attn(self, n1, B, S, cos, sin):
         hd = self.cfg.head_dim
+        if self.tp_copy is not None:
+            n1 = self.tp_copy(n1)
         qkv = fused.linear(n1, self.wqkv)
         q, k, v = fused.rope_qkv(qkv, cos, sin, B, S, self.n_heads, self.n_kv, hd)
         o = attention(q, k, v, causal=True)
@@ -151,6 +155,8 @@ class LlamaBlock(nn.Module):
         return a
 
     def _mlp(self, n2):
+        if self.tp_copy is not None:
+            n2 = self.tp_copy(n2)
         m = fused.linear(fused.swiglu(fused.linear(n2, self.w_gu)), self.w_down)
         if self.tp_reduce is not None:
             m = self.tp_reduce(m)

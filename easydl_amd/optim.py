@@ -47,7 +47,7 @@ class FlatAdamW:
         self.last_stats = None  # device tensor [coef, norm, nonfinite]
         self.state = []
         for g in flat.groups:
-            if weight_decay is not None and g.name == "decay":
+            if weight_decay is not None and g.name.startswith("decay"):
                 g.weight_decay = weight_decay
             has16 = g.data.dtype != torch.float32
             master = g.data.float() if has16 else g.data
@@ -100,7 +100,7 @@ class FlatSGD:
         self.step_count = 0
         self.state = []
         for g in flat.groups:
-            if g.name == "decay":
+            if g.name.startswith("decay"):
                 g.weight_decay = weight_decay
             has16 = g.data.dtype != torch.float32
             self.state.append({

@@ -64,9 +64,8 @@ class ElasticDDP:
     def _build_buckets(self) -> None:
         self.buckets: list[Bucket] = []
         self._bucket_of: dict[int, Bucket] = {}
-        esize = torch.empty((), dtype=self.flat.grad_dtype).element_size()
-        cap = max(1, int(self.bucket_mb * 2**20 / esize))
         for gi, g in enumerate(self.flat.groups):
+            cap = max(1, int(self.bucket_mb * 2**20 / g.grad.element_size()))
             cur = None
             for s in g.slots:
                 if cur is None or cur.numel >= cap:

@@ -71,24 +71,28 @@ class FlatParams:
         if not named:
             raise ValueError("module has no trainable parameters")
         named.reverse()
-        dtypes = {p.dtype for _, p in named}
         devices = {p.device for _, p in named}
-        if len(dtypes) != 1 or len(devices) != 1:
-            raise ValueError(f"FlatParams needs one dtype/device, got {dtypes} {devices}")
-        self.dtype = dtypes.pop()
+        if len(devices) != 1:
+            raise ValueError(f"FlatParams needs one device, got {devices}")
         self.device = devices.pop()
+        by_dt: dict[torch.dtype, int] = {}
+        for _, p in named:
+            by_dt[p.dtype] = by_dt.get(p.dtype, 0) + p.numel()
+        self.dtype = max(by_dt, key=by_dt.get)  # dominant parameter dtype (by elements)
         self.grad_dtype = grad_dtype or self.dtype
-        buckets = {"decay": [], "no_decay": []}
+        # one flat group per (decay class, dtype): e.g. bf16 convs + fp32 BatchNorm in ResNet
+        buckets: dict[tuple[str, torch.dtype], list] = {}
         for n, p in named:
-            buckets["no_decay" if no_decay(n, p) else "decay"].append((n, p))
+            key = ("no_decay" if no_decay(n, p) else "decay", p.dtype)
+            buckets.setdefault(key, []).append((n, p))
         self.groups: list[FlatGroup] = []
-        for gname, plist in buckets.items():
-            if not plist:
-                continue
+        for (cls, dt), plist in sorted(buckets.items(), key=lambda kv: (kv[0][0], str(kv[0][1]))):
+            gname = cls if dt == self.dtype else f"{cls}_{str(dt).split('.')[-1]}"
+            gdt = grad_dtype if (grad_dtype is not None and dt == self.dtype) else dt
             total = sum(_roundup(p.numel()) for _, p in plist)
-            data = torch.zeros(total, dtype=self.dtype, device=self.device)
-            grad = torch.zeros(total, dtype=self.grad_dtype, device=self.device)
-            grp = FlatGroup(gname, weight_decay if gname == "decay" else 0.0, data, grad)
+            data = torch.zeros(total, dtype=dt, device=self.device)
+            grad = torch.zeros(total, dtype=gdt, device=self.device)
+            grp = FlatGroup(gname, weight_decay if cls == "decay" else 0.0, data, grad)
             off = 0
             for n, p in plist:
                 k = p.numel()

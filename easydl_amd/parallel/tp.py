@@ -1,0 +1,226 @@
+"""Megatron-style tensor parallelism for the Llama family (BASELINE.json config 5:
+Llama-3 70B, TP=8 over xGMI).
+
+Per TP rank of ``tp`` ranks:
+* attention: the fused QKV weight holds H/tp query heads and KV/tp key/value
+  heads (70B: 8 q-heads + 1 kv-head per GPU), the output projection holds the
+  matching H/tp*D input columns -> its partial output is all-reduced;
+* MLP: the fused [gate | up] weight holds F/tp rows of each half (so SwiGLU
+  stays local), the down projection the matching F/tp columns -> all-reduce;
+* embedding and LM head are vocab-parallel (V/tp rows each); the cross
+  entropy combines max / sum-exp / target logit with three tiny all-reduces
+  and never materialises the full-vocab logits;
+* norms are replicated (their inputs are replicated after each all-reduce, so
+  their gradients are identical on every TP rank — no reduction needed).
+
+The conjugate operators ``copy_to_tp`` (identity fwd / all-reduce bwd) and
+``reduce_from_tp`` (all-reduce fwd / identity bwd) carry the two all-reduces
+per block in each direction: [T, d] bf16 = 64 MiB at 4k tokens x d=8192 for
+70B — large messages that keep all 7 xGMI links of a node busy.
+Sequence parallelism (P4) swaps each all-reduce for reduce-scatter +
+all-gather over the token dimension (``sequence_parallel=True``).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn as nn
+import torch.distributed as dist
+
+from easydl_amd.models.llama import Llama, LlamaBlock, LlamaConfig, _param
+from easydl_amd.ops import fused, norms
+
+
+class TPGroup:
+    """TP ranks of one model replica (wraps an epoch Communicator)."""
+
+    def __init__(self, comm, sequence_parallel: bool = False):
+        self.comm = comm
+        self.rank = comm.rank
+        self.size = comm.world_size
+        self.sequence_parallel = sequence_parallel
+
+    def all_reduce(self, x: torch.Tensor) -> torch.Tensor:
+        if self.size == 1:
+            return x
+        x = x.contiguous()
+        self.comm.all_reduce(x)
+        return x
+
+    def all_reduce_max(self, x: torch.Tensor) -> torch.Tensor:
+        if self.size == 1:
+            return x
+        x = x.contiguous()
+        self.comm.all_reduce(x, dist.ReduceOp.MAX)
+        return x
+
+    def all_gather_rows(self, x: torch.Tensor) -> torch.Tensor:
+        if self.size == 1:
+            return x
+        out = torch.empty(x.shape[0] * self.size, *x.shape[1:], dtype=x.dtype, device=x.device)
+        self.comm.all_gather_into(out, x.contiguous())
+        return out
+
+    def reduce_scatter_rows(self, x: torch.Tensor) -> torch.Tensor:
+        if self.size == 1:
+            return x
+        out = torch.empty(x.shape[0] // self.size, *x.shape[1:], dtype=x.dtype, device=x.device)
+        self.comm.reduce_scatter_into(out, x.contiguous())
+        return out
+
+
+class _CopyToTP(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, g):
+        ctx.g = g
+        return x
+
+    @staticmethod
+    def backward(ctx, dy):
+        return ctx.g.all_reduce(dy.clone()), None
+
+
+class _ReduceFromTP(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, g):
+        return g.all_reduce(x.clone())
+
+    @staticmethod
+    def backward(ctx, dy):
+        return dy, None
+
+
+class _GatherFromSP(torch.autograd.Function):
+    """SP: [T/tp, d] -> [T, d] (all-gather); backward reduce-scatter."""
+
+    @staticmethod
+    def forward(ctx, x, g):
+        ctx.g = g
+        return g.all_gather_rows(x)
+
+    @staticmethod
+    def backward(ctx, dy):
+        return ctx.g.reduce_scatter_rows(dy), None
+
+
+class _ScatterToSP(torch.autograd.Function):
+    """SP: partial [T, d] -> reduce-scatter -> [T/tp, d]; backward all-gather."""
+
+    @staticmethod
+    def forward(ctx, x, g):
+        ctx.g = g
+        return g.reduce_scatter_rows(x)
+
+    @staticmethod
+    def backward(ctx, dy):
+        return ctx.g.all_gather_rows(dy), None
+
+
+def copy_to_tp(x, g: TPGroup):
+    return _CopyToTP.apply(x, g) if g.size > 1 else x
+
+
+def reduce_from_tp(x, g: TPGroup):
+    return _ReduceFromTP.apply(x, g) if g.size > 1 else x
+
+
+class _VocabParallelXent(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, labels, vstart, g, ignore_index):
+        x = logits.float()
+        m = x.max(dim=-1).values
+        m = g.all_reduce_max(m)
+        e = torch.exp(x - m[:, None])
+        s = g.all_reduce(e.sum(-1))
+        local = (labels >= vstart) & (labels < vstart + x.shape[-1])
+        idx = (labels - vstart).clamp(0, x.shape[-1] - 1)
+        tgt = torch.where(local, x.gather(1, idx[:, None])[:, 0], torch.zeros_like(m))
+        tgt = g.all_reduce(tgt)
+        valid = labels != ignore_index
+        loss_rows = torch.where(valid, torch.log(s) + m - tgt, torch.zeros_like(m))
+        n = valid.sum().clamp_min(1).float()
+        p = e / s[:, None]
+        ctx.save_for_backward(p, idx, local & valid, valid, n)
+        ctx.dtype = logits.dtype
+        return loss_rows.sum() / n
+
+    @staticmethod
+    def backward(ctx, dl):
+        p, idx, hit, valid, n = ctx.saved_tensors
+        grad = p * valid[:, None].float()
+        grad[hit.nonzero()[:, 0], idx[hit]] -= 1.0
+        return (grad * (dl / n)).to(ctx.dtype), None, None, None, None
+
+
+def vocab_parallel_cross_entropy(logits_local, labels, vstart: int, g: TPGroup, ignore_index: int = -100):
+    return _VocabParallelXent.apply(logits_local, labels.reshape(-1), vstart, g, ignore_index)
+
+
+class LlamaTP(nn.Module):
+    """One TP rank of a Llama model (parameter names match :class:`Llama`)."""
+
+    def __init__(self, cfg: LlamaConfig, g: TPGroup, device=None, dtype=torch.bfloat16):
+        super().__init__()
+        tp = g.size
+        if cfg.n_heads % tp or cfg.n_kv_heads % tp or cfg.ffn_dim % tp or cfg.vocab_size % tp:
+            raise ValueError(f"config not divisible by tp={tp}")
+        self.cfg, self.g = cfg, g
+        self.vshard = cfg.vocab_size // tp
+        self.vstart = g.rank * self.vshard
+        d = cfg.dim
+        self.embed = _param((self.vshard, d), cfg.init_std, device, dtype)
+        self.layers = nn.ModuleList()
+        for _ in range(cfg.n_layers):
+            blk = LlamaBlock(cfg, device, dtype, n_heads=cfg.n_heads // tp, n_kv_heads=cfg.n_kv_heads // tp,
+                             ffn_dim=cfg.ffn_dim // tp)
+            blk.tp_reduce = lambda x, _g=g: reduce_from_tp(x, _g)
+            blk.tp_copy = lambda x, _g=g: copy_to_tp(x, _g)
+            self.layers.append(blk)
+        self.norm = _param((d,), 0, device, dtype)
+        self.lm_head = _param((self.vshard, d), cfg.init_std, device, dtype)
+        self._rope = {}
+
+    rope = Llama.rope
+
+    def forward(self, ids, labels=None):
+        B, S = ids.shape
+        cos, sin = self.rope(S, ids.device)
+        flat = ids.reshape(-1)
+        local = (flat >= self.vstart) & (flat < self.vstart + self.vshard)
+        x = fused.embedding((flat - self.vstart).clamp(0, self.vshard - 1), self.embed)
+        x = x * local[:, None].to(x.dtype)
+        x = reduce_from_tp(x, self.g)
+        resid, delta = x, None
+        for layer in self.layers:
+            resid, delta = layer(resid, delta, B, S, cos, sin)
+        n, _ = norms.add_rmsnorm(delta, resid, self.norm, self.cfg.norm_eps)
+        n = copy_to_tp(n, self.g)
+        logits = fused.linear(n, self.lm_head)
+        if labels is None:
+            return logits
+        return vocab_parallel_cross_entropy(logits, labels, self.vstart, self.g)
+
+
+def shard_state_dict(full: dict[str, torch.Tensor], cfg: LlamaConfig, rank: int, tp: int) -> dict[str, torch.Tensor]:
+    """Slice a dense :class:`Llama` state dict into TP rank ``rank`` of ``tp``."""
+    H, KV, D, F = cfg.n_heads, cfg.n_kv_heads, cfg.head_dim, cfg.ffn_dim
+    hs, ks, fs, vs = H // tp, KV // tp, F // tp, cfg.vocab_size // tp
+    out = {}
+    for name, w in full.items():
+        if name.endswith("wqkv"):
+            q = w[:H * D].view(H, D, -1)[rank * hs:(rank + 1) * hs].reshape(hs * D, -1)
+            k = w[H * D:(H + KV) * D].view(KV, D, -1)[rank * ks:(rank + 1) * ks].reshape(ks * D, -1)
+            v = w[(H + KV) * D:].view(KV, D, -1)[rank * ks:(rank + 1) * ks].reshape(ks * D, -1)
+            out[name] = torch.cat([q, k, v])
+        elif name.endswith("wo"):
+            out[name] = w[:, rank * hs * D:(rank + 1) * hs * D]
+        elif name.endswith("w_gu"):
+            out[name] = torch.cat([w[rank * fs:(rank + 1) * fs], w[F + rank * fs:F + (rank + 1) * fs]])
+        elif name.endswith("w_down"):
+            out[name] = w[:, rank * fs:(rank + 1) * fs]
+        elif name in ("embed", "lm_head"):
+            out[name] = w[rank * vs:(rank + 1) * vs]
+        else:
+            out[name] = w
+    return {k: v.contiguous() for k, v in out.items()}
