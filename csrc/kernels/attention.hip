@@ -118,34 +118,44 @@ __device__ __forceinline__ void store_accT(bf16_t* rowp, const f32x16 (&acc)[4],
 }
 
 // ---------------------------------------------------------------------------
-// forward
+// forward: a wave owns QG*32 queries (QG column groups); every K / V fragment
+// read from LDS feeds QG MFMAs.
 // ---------------------------------------------------------------------------
-template <bool CAUSAL>
-__global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
+template <bool CAUSAL, int QG>
+__global__ __launch_bounds__(256, QG == 1 ? 2 : 1) void attn_fwd_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
                                                           const bf16_t* __restrict__ v, bf16_t* __restrict__ o,
                                                           float* __restrict__ lse, int S, int H, int KV,
                                                           float scale_log2) {
+  constexpr int BQ = 128 * QG;
   __shared__ __attribute__((aligned(16))) char smem[2 * 32768];
   const int qb = gridDim.x - 1 - blockIdx.x;  // longest causal rows first
   const int hq = blockIdx.y, b = blockIdx.z, hk = hq / (H / KV);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, l31 = lane & 31;
-  const int q0 = qb * 128;
-  const int qrow = q0 + 32 * w + l31;
+  const int q0 = qb * BQ;
+  const int wq0 = q0 + 32 * QG * w;  // first query of this wave
   const int64_t qs = (int64_t)H * HD, ks = (int64_t)KV * HD;
   const bf16_t* qp = q + (int64_t)b * S * qs + hq * HD;
   const bf16_t* kp = k + (int64_t)b * S * ks + hk * HD;
   const bf16_t* vp = v + (int64_t)b * S * ks + hk * HD;
 
-  bf16x8 qf[8];
+  bf16x8 qf[QG][8];
 #pragma unroll
-  for (int s = 0; s < 8; ++s) qf[s] = load_frag(qp + (int64_t)qrow * qs, s, h, qrow < S);
-
-  const int kv_end = CAUSAL ? min(S, q0 + 128) : S;
+  for (int g = 0; g < QG; ++g) {
+    const int qr = wq0 + 32 * g + l31;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) qf[g][s] = load_frag(qp + (int64_t)qr * qs, s, h, qr < S);
+  }
+  const int kv_end = CAUSAL ? min(S, q0 + BQ) : S;
   const int ntiles = (kv_end + 63) / 64;
-  f32x16 oacc[4];
+  f32x16 oacc[QG][4];
+  float m[QG], lsum[QG];
 #pragma unroll
-  for (int dt = 0; dt < 4; ++dt) oacc[dt] = f32x16{};
-  float m = -1e30f, lsum = 0.f;
+  for (int g = 0; g < QG; ++g) {
+    m[g] = -1e30f;
+    lsum[g] = 0.f;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) oacc[g][dt] = f32x16{};
+  }
 
   u32x4 kreg[4], vreg[4];
   load_rows<64>(kreg, kp, ks, 0, S);
@@ -162,51 +172,79 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_t* __restri
     }
     const char* Ks = smem + (it & 1) * 32768;
     const char* Vs = Ks + 16384;
-    f32x16 sacc[2] = {f32x16{}, f32x16{}};
+    const bool wave_visible = !CAUSAL || kv0 <= wq0 + 32 * QG - 1;
+    if (wave_visible) {
+      f32x16 sacc[QG][2];
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
+      for (int g = 0; g < QG; ++g) sacc[g][0] = sacc[g][1] = f32x16{};
 #pragma unroll
-      for (int s = 0; s < 8; ++s) sacc[t] = mfma(row_read(Ks, 32 * t + l31, s, h), qf[s], sacc[t]);
-    }
-    const bool need_mask = (kv0 + 64 > S) || (CAUSAL && kv0 + 63 > q0 + 32 * w);
-    float mx = -1e30f;
+      for (int t = 0; t < 2; ++t) {
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
+        for (int s = 0; s < 8; ++s) {
+          const bf16x8 a = row_read(Ks, 32 * t + l31, s, h);
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        float x = sacc[t][i] * scale_log2;
-        if (need_mask) {
-          const int key = kv0 + 32 * t + acc_row(i, h);
-          if (key >= S || (CAUSAL && key > qrow)) x = -INFINITY;
+          for (int g = 0; g < QG; ++g) sacc[g][t] = mfma(a, qf[g][s], sacc[g][t]);
         }
-        sacc[t][i] = x;
-        mx = fmaxf(mx, x);
       }
-    }
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float mnew = fmaxf(m, mx);
-    const float alpha = exp2f(m - mnew);
-    m = mnew;
-    float ps = 0.f;
+      const bool need_mask = (kv0 + 64 > S) || (CAUSAL && kv0 + 63 > wq0);
+      bool grow = false;
+      float alpha[QG];
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
+      for (int g = 0; g < QG; ++g) {
+        const int qr = wq0 + 32 * g + l31;
+        float mx = -1e30f;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const float p = exp2f(sacc[t][i] - mnew);
-        sacc[t][i] = p;
-        ps += p;
+        for (int t = 0; t < 2; ++t) {
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            float x = sacc[g][t][i] * scale_log2;
+            if (need_mask) {
+              const int key = kv0 + 32 * t + acc_row(i, h);
+              if (key >= S || (CAUSAL && key > qr)) x = -INFINITY;
+            }
+            sacc[g][t][i] = x;
+            mx = fmaxf(mx, x);
+          }
+        }
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        const float mnew = fmaxf(m[g], mx);
+        grow |= mnew > m[g];
+        alpha[g] = exp2f(m[g] - mnew);
+        m[g] = mnew;
+        float ps = 0.f;
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const float p = exp2f(sacc[g][t][i] - mnew);
+            sacc[g][t][i] = p;
+            ps += p;
+          }
+        }
+        lsum[g] = lsum[g] * alpha[g] + ps;
       }
-    }
-    lsum = lsum * alpha + ps;
+      // exact lazy rescale: only when some row max of this wave grew
+      if (__any(grow)) {
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt) oacc[dt] *= alpha;
+        for (int g = 0; g < QG; ++g) {
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
+          for (int dt = 0; dt < 4; ++dt) oacc[g][dt] *= alpha[g];
+        }
+      }
 #pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        const bf16x8 pb = acc_to_b(sacc[t], s2);
+      for (int t = 0; t < 2; ++t) {
 #pragma unroll
-        for (int dt = 0; dt < 4; ++dt) oacc[dt] = mfma(tr_read(Vs, 32 * t + 16 * s2 + 4 * h, dt, lane), pb, oacc[dt]);
+        for (int s2 = 0; s2 < 2; ++s2) {
+          bf16x8 pb[QG];
+#pragma unroll
+          for (int g = 0; g < QG; ++g) pb[g] = acc_to_b(sacc[g][t], s2);
+#pragma unroll
+          for (int dt = 0; dt < 4; ++dt) {
+            const bf16x8 a = tr_read(Vs, 32 * t + 16 * s2 + 4 * h, dt, lane);
+#pragma unroll
+            for (int g = 0; g < QG; ++g) oacc[g][dt] = mfma(a, pb[g], oacc[g][dt]);
+          }
+        }
       }
     }
     __syncthreads();
@@ -217,10 +255,14 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_t* __restri
     }
     __syncthreads();
   }
-  const float ltot = lsum + __shfl_xor(lsum, 32, 64);
-  if (qrow < S) {
-    store_accT(o + (int64_t)b * S * qs + (int64_t)qrow * qs + hq * HD, oacc, 1.f / ltot, h);
-    if (h == 0) lse[((int64_t)b * H + hq) * S + qrow] = (m + log2f(ltot)) * LN2;
+#pragma unroll
+  for (int g = 0; g < QG; ++g) {
+    const int qr = wq0 + 32 * g + l31;
+    const float ltot = lsum[g] + __shfl_xor(lsum[g], 32, 64);
+    if (qr < S) {
+      store_accT(o + (int64_t)b * S * qs + (int64_t)qr * qs + hq * HD, oacc[g], 1.f / ltot, h);
+      if (h == 0) lse[((int64_t)b * H + hq) * S + qr] = (m[g] + log2f(ltot)) * LN2;
+    }
   }
 }
 
@@ -250,15 +292,18 @@ __global__ __launch_bounds__(256) void attn_bwd_delta_kernel(const bf16_t* __res
 }
 
 // ---------------------------------------------------------------------------
-// backward: dK, dV
+// backward: dK, dV.  A workgroup owns 128 keys of one KV head (a wave 32 keys,
+// K/V in registers, dK^T/dV^T accumulators resident) and sweeps 64-query
+// tiles (two 32-row sub-slices) of every query head of the GQA group.
 // ---------------------------------------------------------------------------
 template <bool CAUSAL>
 __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
     const bf16_t* __restrict__ dout, const float* __restrict__ lse, const float* __restrict__ delta,
     bf16_t* __restrict__ dk, bf16_t* __restrict__ dv, int S, int H, int KV, float scale_log2, float scale) {
-  // 2 stages x (Q slice 8 KB + dO slice 8 KB) + 2 x (lse2, delta) x 32 floats
-  __shared__ __attribute__((aligned(16))) char smem[2 * 16384 + 2 * 256];
+  constexpr int QT = 64;  // queries per staged tile
+  // 2 stages x (Q tile 16 KB + dO tile 16 KB) + 2 x (lse2, delta) x 64 floats
+  __shared__ __attribute__((aligned(16))) char smem[2 * 32768 + 2 * 512];
   const int kb = blockIdx.x, hk = blockIdx.y, b = blockIdx.z;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, l31 = lane & 31;
   const int group = H / KV;
@@ -278,43 +323,33 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_kernel(
     dka[dt] = f32x16{};
     dva[dt] = f32x16{};
   }
-  const int nqs = (S + 31) / 32;
-  const int qs0 = CAUSAL ? (kb * 128) / 32 : 0;
-  const int per_head = nqs - qs0;
+  const int nqt = (S + QT - 1) / QT;
+  const int qt0 = CAUSAL ? (kb * 128) / QT : 0;
+  const int per_head = nqt - qt0;
   const int total = per_head * group;
   const int wave_key_lo = kb * 128 + 32 * w;
 
-  auto q_base = [&](int j) {
-    const int hq = hk * group + j / per_head;
-    return q + (int64_t)b * S * qs + hq * HD;
-  };
-  auto do_base = [&](int j) {
-    const int hq = hk * group + j / per_head;
-    return dout + (int64_t)b * S * qs + hq * HD;
-  };
-  auto slice_q0 = [&](int j) { return (qs0 + j % per_head) * 32; };
-
-  u32x4 qreg[2], dreg[2];
+  u32x4 qreg[4], dreg[4];
   float lreg = 0.f, dlreg = 0.f;
   auto fetch = [&](int j) {
-    const int q0 = slice_q0(j);
-    load_rows<32>(qreg, q_base(j), qs, q0, S);
-    load_rows<32>(dreg, do_base(j), qs, q0, S);
-    if (threadIdx.x < 32) {
-      const int hq = hk * group + j / per_head;
+    const int hq = hk * group + j / per_head;
+    const int q0 = (qt0 + j % per_head) * QT;
+    load_rows<QT>(qreg, q + (int64_t)b * S * qs + hq * HD, qs, q0, S);
+    load_rows<QT>(dreg, dout + (int64_t)b * S * qs + hq * HD, qs, q0, S);
+    if (threadIdx.x < QT) {
       const int qq = q0 + threadIdx.x;
       lreg = qq < S ? lse[((int64_t)b * H + hq) * S + qq] * LOG2E : 0.f;
       dlreg = qq < S ? delta[((int64_t)b * H + hq) * S + qq] : 0.f;
     }
   };
   auto commit = [&](int st) {
-    char* base = smem + st * 16384;
-    store_rows<32>(base, qreg);
-    store_rows<32>(base + 8192, dreg);
-    if (threadIdx.x < 32) {
-      float* lf = reinterpret_cast<float*>(smem + 2 * 16384 + st * 256);
+    char* base = smem + st * 32768;
+    store_rows<QT>(base, qreg);
+    store_rows<QT>(base + 16384, dreg);
+    if (threadIdx.x < QT) {
+      float* lf = reinterpret_cast<float*>(smem + 2 * 32768 + st * 512);
       lf[threadIdx.x] = lreg;
-      lf[32 + threadIdx.x] = dlreg;
+      lf[QT + threadIdx.x] = dlreg;
     }
   };
   if (total > 0) {
@@ -325,44 +360,42 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_kernel(
   for (int j = 0; j < total; ++j) {
     if (j + 1 < total) fetch(j + 1);
     const int st = j & 1;
-    const char* Qs = smem + st * 16384;
-    const char* Ds = Qs + 8192;
-    const float* L2 = reinterpret_cast<const float*>(smem + 2 * 16384 + st * 256);
-    const int q0 = slice_q0(j);
-    if (!(CAUSAL && q0 + 31 < wave_key_lo)) {  // wave-uniform: some key of this wave is visible
-      // S = Q K^T  (rows q, col = my key)
+    const char* Qs = smem + st * 32768;
+    const char* Ds = Qs + 16384;
+    const float* L2 = reinterpret_cast<const float*>(smem + 2 * 32768 + st * 512);
+    const int q0 = (qt0 + j % per_head) * QT;
+#pragma unroll
+    for (int sub = 0; sub < QT / 32; ++sub) {
+      const int qs0 = q0 + 32 * sub;
+      if (CAUSAL && qs0 + 31 < wave_key_lo) continue;  // wave-uniform: all masked
+      const int rb = 32 * sub;  // row base inside the staged tile
       f32x16 sa = f32x16{};
 #pragma unroll
-      for (int s = 0; s < 8; ++s) sa = mfma(row_read(Qs, l31, s, h), kf[s], sa);
-      // P
+      for (int s = 0; s < 8; ++s) sa = mfma(row_read(Qs, rb + l31, s, h), kf[s], sa);
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int r = acc_row(i, h);
-        const int qi = q0 + r;
-        float p = exp2f(sa[i] * scale_log2 - L2[r]);
+        const int qi = qs0 + r;
+        float p = exp2f(sa[i] * scale_log2 - L2[rb + r]);
         if (qi >= S || mykey >= S || (CAUSAL && mykey > qi)) p = 0.f;
         sa[i] = p;
       }
-      // dV^T += dO^T P
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
         const bf16x8 pb = acc_to_b(sa, s2);
 #pragma unroll
-        for (int dt = 0; dt < 4; ++dt) dva[dt] = mfma(tr_read(Ds, 16 * s2 + 4 * h, dt, lane), pb, dva[dt]);
+        for (int dt = 0; dt < 4; ++dt) dva[dt] = mfma(tr_read(Ds, rb + 16 * s2 + 4 * h, dt, lane), pb, dva[dt]);
       }
-      // dP = dO V^T
       f32x16 dp = f32x16{};
 #pragma unroll
-      for (int s = 0; s < 8; ++s) dp = mfma(row_read(Ds, l31, s, h), vf[s], dp);
-      // dS = P (dP - delta)
+      for (int s = 0; s < 8; ++s) dp = mfma(row_read(Ds, rb + l31, s, h), vf[s], dp);
 #pragma unroll
-      for (int i = 0; i < 16; ++i) dp[i] = sa[i] * (dp[i] - L2[32 + acc_row(i, h)]);
-      // dK^T += Q^T dS
+      for (int i = 0; i < 16; ++i) dp[i] = sa[i] * (dp[i] - L2[QT + rb + acc_row(i, h)]);
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
         const bf16x8 db = acc_to_b(dp, s2);
 #pragma unroll
-        for (int dt = 0; dt < 4; ++dt) dka[dt] = mfma(tr_read(Qs, 16 * s2 + 4 * h, dt, lane), db, dka[dt]);
+        for (int dt = 0; dt < 4; ++dt) dka[dt] = mfma(tr_read(Qs, rb + 16 * s2 + 4 * h, dt, lane), db, dka[dt]);
       }
     }
     __syncthreads();
@@ -376,37 +409,42 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_kernel(
 }
 
 // ---------------------------------------------------------------------------
-// backward: dQ
+// backward: dQ (a wave owns QG*32 queries; K/V fragments feed QG MFMAs)
 // ---------------------------------------------------------------------------
-template <bool CAUSAL>
-__global__ __launch_bounds__(256, 1) void attn_bwd_dq_kernel(
+template <bool CAUSAL, int QG>
+__global__ __launch_bounds__(256, QG == 1 ? 2 : 1) void attn_bwd_dq_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
     const bf16_t* __restrict__ dout, const float* __restrict__ lse, const float* __restrict__ delta,
     bf16_t* __restrict__ dq, int S, int H, int KV, float scale_log2, float scale) {
+  constexpr int BQ = 128 * QG;
   __shared__ __attribute__((aligned(16))) char smem[2 * 32768];
   const int qb = gridDim.x - 1 - blockIdx.x;
   const int hq = blockIdx.y, b = blockIdx.z, hk = hq / (H / KV);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, l31 = lane & 31;
-  const int q0 = qb * 128;
-  const int myq = q0 + 32 * w + l31;
+  const int q0 = qb * BQ;
+  const int wq0 = q0 + 32 * QG * w;
   const int64_t qs = (int64_t)H * HD, ks = (int64_t)KV * HD;
   const bf16_t* kp = k + (int64_t)b * S * ks + hk * HD;
   const bf16_t* vp = v + (int64_t)b * S * ks + hk * HD;
-  bf16x8 qf[8], df[8];
-  const bf16_t* qrow = q + (int64_t)b * S * qs + (int64_t)myq * qs + hq * HD;
-  const bf16_t* drow = dout + (int64_t)b * S * qs + (int64_t)myq * qs + hq * HD;
+  bf16x8 qf[QG][8], df[QG][8];
+  float l2[QG], dl[QG];
+  f32x16 dqa[QG][4];
 #pragma unroll
-  for (int s = 0; s < 8; ++s) {
-    qf[s] = load_frag(qrow, s, h, myq < S);
-    df[s] = load_frag(drow, s, h, myq < S);
+  for (int g = 0; g < QG; ++g) {
+    const int qr = wq0 + 32 * g + l31;
+    const bf16_t* qrow = q + (int64_t)b * S * qs + (int64_t)qr * qs + hq * HD;
+    const bf16_t* drow = dout + (int64_t)b * S * qs + (int64_t)qr * qs + hq * HD;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      qf[g][s] = load_frag(qrow, s, h, qr < S);
+      df[g][s] = load_frag(drow, s, h, qr < S);
+    }
+    l2[g] = qr < S ? lse[((int64_t)b * H + hq) * S + qr] * LOG2E : 0.f;
+    dl[g] = qr < S ? delta[((int64_t)b * H + hq) * S + qr] : 0.f;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) dqa[g][dt] = f32x16{};
   }
-  const float l2 = myq < S ? lse[((int64_t)b * H + hq) * S + myq] * LOG2E : 0.f;
-  const float dl = myq < S ? delta[((int64_t)b * H + hq) * S + myq] : 0.f;
-  f32x16 dqa[4];
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt) dqa[dt] = f32x16{};
-
-  const int kv_end = CAUSAL ? min(S, q0 + 128) : S;
+  const int kv_end = CAUSAL ? min(S, q0 + BQ) : S;
   const int ntiles = (kv_end + 63) / 64;
   u32x4 kreg[4], vreg[4];
   load_rows<64>(kreg, kp, ks, 0, S);
@@ -422,30 +460,50 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dq_kernel(
     }
     const char* Ks = smem + (it & 1) * 32768;
     const char* Vs = Ks + 16384;
-    const bool visible = !(CAUSAL && kv0 > q0 + 32 * w + 31);
+    const bool visible = !(CAUSAL && kv0 > wq0 + 32 * QG - 1);
     if (visible) {
-      const bool need_mask = (kv0 + 64 > S) || (CAUSAL && kv0 + 63 > q0 + 32 * w);
+      const bool need_mask = (kv0 + 64 > S) || (CAUSAL && kv0 + 63 > wq0);
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
-        f32x16 st = f32x16{}, dpt = f32x16{};
+        f32x16 st[QG], dpt[QG];
 #pragma unroll
-        for (int s = 0; s < 8; ++s) st = mfma(row_read(Ks, 32 * t + l31, s, h), qf[s], st);
+        for (int g = 0; g < QG; ++g) st[g] = dpt[g] = f32x16{};
 #pragma unroll
-        for (int s = 0; s < 8; ++s) dpt = mfma(row_read(Vs, 32 * t + l31, s, h), df[s], dpt);
+        for (int s = 0; s < 8; ++s) {
+          const bf16x8 a = row_read(Ks, 32 * t + l31, s, h);
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          float p = exp2f(st[i] * scale_log2 - l2);
-          if (need_mask) {
-            const int key = kv0 + 32 * t + acc_row(i, h);
-            if (key >= S || (CAUSAL && key > myq)) p = 0.f;
+          for (int g = 0; g < QG; ++g) st[g] = mfma(a, qf[g][s], st[g]);
+        }
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+          const bf16x8 a = row_read(Vs, 32 * t + l31, s, h);
+#pragma unroll
+          for (int g = 0; g < QG; ++g) dpt[g] = mfma(a, df[g][s], dpt[g]);
+        }
+#pragma unroll
+        for (int g = 0; g < QG; ++g) {
+          const int qr = wq0 + 32 * g + l31;
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            float p = exp2f(st[g][i] * scale_log2 - l2[g]);
+            if (need_mask) {
+              const int key = kv0 + 32 * t + acc_row(i, h);
+              if (key >= S || (CAUSAL && key > qr)) p = 0.f;
+            }
+            dpt[g][i] = p * (dpt[g][i] - dl[g]);  // dS^T
           }
-          dpt[i] = p * (dpt[i] - dl);  // dS^T
         }
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
-          const bf16x8 db = acc_to_b(dpt, s2);
+          bf16x8 db[QG];
 #pragma unroll
-          for (int dt = 0; dt < 4; ++dt) dqa[dt] = mfma(tr_read(Ks, 32 * t + 16 * s2 + 4 * h, dt, lane), db, dqa[dt]);
+          for (int g = 0; g < QG; ++g) db[g] = acc_to_b(dpt[g], s2);
+#pragma unroll
+          for (int dt = 0; dt < 4; ++dt) {
+            const bf16x8 a = tr_read(Ks, 32 * t + 16 * s2 + 4 * h, dt, lane);
+#pragma unroll
+            for (int g = 0; g < QG; ++g) dqa[g][dt] = mfma(a, db[g], dqa[g][dt]);
+          }
         }
       }
     }
@@ -457,7 +515,11 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dq_kernel(
     }
     __syncthreads();
   }
-  if (myq < S) store_accT(dq + (int64_t)b * S * qs + (int64_t)myq * qs + hq * HD, dqa, scale, h);
+#pragma unroll
+  for (int g = 0; g < QG; ++g) {
+    const int qr = wq0 + 32 * g + l31;
+    if (qr < S) store_accT(dq + (int64_t)b * S * qs + (int64_t)qr * qs + hq * HD, dqa[g], scale, h);
+  }
 }
 
 }  // namespace
@@ -467,14 +529,17 @@ extern "C" {
 int edl_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int S, int H, int KV,
                  int D, int causal, float scale, hipStream_t s) {
   if (D != HD || H % KV != 0 || S <= 0) return (int)hipErrorInvalidValue;
-  dim3 grid((S + 127) / 128, H, B);
+  // QG = 2 (64 rows per wave) halves LDS bytes per MFMA but needs 512 registers
+  // -> 1 wave/SIMD, which measured 2.7x slower (latency exposed); keep QG = 1.
+  constexpr int QG = 1;
+  dim3 grid((S + 128 * QG - 1) / (128 * QG), H, B);
   const float sl2 = scale * LOG2E;
   if (causal)
-    attn_fwd_kernel<true><<<grid, 256, 0, s>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (bf16_t*)o,
-                                               lse, S, H, KV, sl2);
+    attn_fwd_kernel<true, QG><<<grid, 256, 0, s>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
+                                                   (bf16_t*)o, lse, S, H, KV, sl2);
   else
-    attn_fwd_kernel<false><<<grid, 256, 0, s>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (bf16_t*)o,
-                                                lse, S, H, KV, sl2);
+    attn_fwd_kernel<false, QG><<<grid, 256, 0, s>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
+                                                    (bf16_t*)o, lse, S, H, KV, sl2);
   EDL_LAUNCH_CHECK();
   return 0;
 }
@@ -489,20 +554,21 @@ int edl_attn_bwd(const void* q, const void* k, const void* v, const void* o, con
                                                                             delta, S, H, nrows);
   EDL_LAUNCH_CHECK();
   const float sl2 = scale * LOG2E;
-  dim3 gkv((S + 127) / 128, KV, B), gq((S + 127) / 128, H, B);
+  constexpr int QG = 1;
+  dim3 gkv((S + 127) / 128, KV, B), gq((S + 128 * QG - 1) / (128 * QG), H, B);
   if (causal) {
     attn_bwd_dkdv_kernel<true><<<gkv, 256, 0, s>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
                                                    (const bf16_t*)dout, lse, delta, (bf16_t*)dk, (bf16_t*)dv, S, H,
                                                    KV, sl2, scale);
     EDL_LAUNCH_CHECK();
-    attn_bwd_dq_kernel<true><<<gq, 256, 0, s>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
+    attn_bwd_dq_kernel<true, QG><<<gq, 256, 0, s>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
                                                 (const bf16_t*)dout, lse, delta, (bf16_t*)dq, S, H, KV, sl2, scale);
   } else {
     attn_bwd_dkdv_kernel<false><<<gkv, 256, 0, s>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
                                                     (const bf16_t*)dout, lse, delta, (bf16_t*)dk, (bf16_t*)dv, S, H,
                                                     KV, sl2, scale);
     EDL_LAUNCH_CHECK();
-    attn_bwd_dq_kernel<false><<<gq, 256, 0, s>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
+    attn_bwd_dq_kernel<false, QG><<<gq, 256, 0, s>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
                                                  (const bf16_t*)dout, lse, delta, (bf16_t*)dq, S, H, KV, sl2, scale);
   }
   EDL_LAUNCH_CHECK();
