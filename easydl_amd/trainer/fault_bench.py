@@ -1,0 +1,114 @@
+"""Time-to-recover benchmark (``bench.py --fault-inject``; BASELINE.json metric
+"time-to-recover ... w/ fault inject", config 3 "kill-1-worker fault inject +
+in-mem ckpt restore").
+
+Runs a real job through the local ElasticOperator on this node's GPUs (or CPU
+processes when no GPU is visible):
+
+* N workers train the model with in-memory sharded snapshots every
+  ``--ckpt-interval`` steps;
+* worker ``N-1`` SIGKILLs itself at step ``--fault-step`` (EDL_FAULT);
+* N > 1: the supervisor's pidfd exit event reaches the master in
+  microseconds, the epoch is aborted, survivors abort RCCL, rebuild an (N-1)
+  world and continue without restarting; the operator's replacement later
+  rejoins (scale-up with state broadcast);
+* N = 1: there is no survivor: the replacement process restores the newest
+  committed snapshot from /dev/shm and continues.
+
+TTR = wall time from the ``fault_injected`` event to the first committed step
+after it; the breakdown (detect / abort / new epoch / comm ready / state sync
+/ first step) comes from the merged event timeline.  Prints one JSON line.
+"""
+from __future__ import annotations
+
+import json
+import os
+import shutil
+import sys
+import tempfile
+
+from easydl_amd.utils.events import read_events, ttr_breakdown
+
+
+def _gpus() -> list[int]:
+    from easydl_amd.brain.collectors import kfd_gpus
+    return [g.index for g in kfd_gpus()]
+
+
+def main(args) -> int:
+    from easydl_amd.api.spec import ElasticJob, JobResource, Resource, RoleResource
+    from easydl_amd.ckpt.manager import unlink_job_segments
+    from easydl_amd.operator.reconciler import ElasticOperator, OperatorConfig
+
+    gpus = _gpus()
+    n = max(1, min(args.gpus, len(gpus))) if gpus else max(1, args.gpus)
+    run_dir = tempfile.mkdtemp(prefix="edl-ttr-", dir=os.environ.get("EDL_TTR_DIR", None))
+    job_name = "ttr"
+    unlink_job_segments(job_name)
+    steps = args.warmup + args.steps
+    fault_step = getattr(args, "fault_step", None) or max(2, args.warmup + 1)
+    env = {
+        "EDL_BENCH_MODEL": args.model, "EDL_BENCH_SEQ": str(args.seq), "EDL_BENCH_MBS": str(args.mbs),
+        "EDL_BENCH_ACCUM": str(args.accum), "EDL_BENCH_STEPS": str(steps),
+        "EDL_BENCH_CKPT": str(getattr(args, "ckpt_interval", 0) or 2),
+        "EDL_FAULT": f"kill@step={fault_step},index={n - 1}",
+        "EDL_PLANNED_WORKERS": str(n),
+    }
+    if args.layers:
+        env["EDL_BENCH_LAYERS"] = str(args.layers)
+    job = ElasticJob(name=job_name, command=f"{sys.executable} -m easydl_amd.trainer.fault_bench --worker",
+                     env=env, min_workers=1, max_workers=n)
+    jr = JobResource(f"{job_name}-resource", job_name,
+                     {"worker": RoleResource(n, Resource(gpu=1 if gpus else 0, cpu=4))})
+    cfg = OperatorConfig(gpus=gpus[:n], cpus=[], leave_grace_s=120.0)
+    op = ElasticOperator(job, run_dir, cfg=cfg, job_resource=jr)
+    rc = op.run(timeout_s=1000)
+    ev = read_events(run_dir)
+    ttr = ttr_breakdown(ev)
+    worlds = [e.get("world") for e in ev if e["kind"] == "step_done"]
+    restored = [e for e in ev if e["kind"] == "restored"]
+    out = {
+        "metric": "time-to-recover after SIGKILL of one worker (Llama elastic DDP, local operator)",
+        "value": None if not ttr else ttr["ttr_s"], "unit": "s", "higher_is_better": False,
+        "n_gpus": n if gpus else 0,
+        "model": (args.model if not args.layers else f"{args.model}-L{args.layers}") if gpus else "llama-tiny (CPU)",
+        "breakdown": ttr, "operator_rc": rc, "restored_from": restored[0].get("source") if restored else None,
+        "worlds_seen": sorted({w for w in worlds if w}), "run_dir": run_dir,
+    }
+    print(json.dumps(out), flush=True)
+    unlink_job_segments(job_name)
+    if os.environ.get("EDL_TTR_KEEP") != "1":
+        shutil.rmtree(run_dir, ignore_errors=True)
+    return 0 if rc == 0 and ttr else 1
+
+
+def worker() -> None:
+    """One training process of the TTR job (spawned by the operator)."""
+    import torch
+
+    from easydl_amd.ckpt.manager import CheckpointManager
+    from easydl_amd.models.llama import Llama, get_config
+    from easydl_amd.trainer.data import SyntheticTokens
+    from easydl_amd.trainer.elastic import ElasticTrainer
+
+    e = os.environ
+    over = {"n_layers": int(e["EDL_BENCH_LAYERS"])} if "EDL_BENCH_LAYERS" in e else {}
+    cfg = get_config(e.get("EDL_BENCH_MODEL", "llama3-8b"), **over)
+    cuda = torch.cuda.is_available()
+    if not cuda:
+        cfg = get_config("llama-tiny")
+    seq = int(e.get("EDL_BENCH_SEQ", 8192)) if cuda else 64
+    mbs, accum = int(e.get("EDL_BENCH_MBS", 1)), int(e.get("EDL_BENCH_ACCUM", 1))
+    ckpt = CheckpointManager(e.get("EDL_JOB", "ttr"), interval=int(e.get("EDL_BENCH_CKPT", 2)))
+    tr = ElasticTrainer(lambda d: Llama(cfg, device=d, dtype=torch.bfloat16 if cuda else torch.float32),
+                        global_batch=None, micro_batch=mbs, checkpoint=ckpt)
+    # global batch: the planned world x mbs x accum, fixed across resizes (accumulation absorbs it)
+    tr.global_batch = mbs * accum * max(1, int(e.get("EDL_PLANNED_WORKERS", 1)))
+    tr.fit(lambda m, b: m(*b), SyntheticTokens(cfg.vocab_size, seq), num_steps=int(e.get("EDL_BENCH_STEPS", 10)))
+    tr.close()
+    ckpt.close()
+
+
+if __name__ == "__main__":
+    if "--worker" in sys.argv:
+        worker()

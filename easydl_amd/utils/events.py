@@ -59,7 +59,10 @@ def read_events(run_dir: str) -> list[dict]:
 
 
 def ttr_breakdown(events: list[dict]) -> dict | None:
-    """Time-to-recover phases relative to the first injected fault."""
+    """Time-to-recover phases relative to the first injected fault.
+
+    Recovery is complete at the first committed step of an epoch formed after
+    the fault (a step finishing in the old epoch does not count)."""
     fault = next((e for e in events if e["kind"] == "fault_injected"), None)
     if fault is None:
         return None
@@ -67,16 +70,24 @@ def ttr_breakdown(events: list[dict]) -> dict | None:
     after = [e for e in events if e["ts"] >= t0]
 
     def first(kind, pred=lambda e: True):
-        r = next((e for e in after if e["kind"] == kind and pred(e)), None)
-        return None if r is None else round(r["ts"] - t0, 4)
+        return next((e for e in after if e["kind"] == kind and pred(e)), None)
 
+    def rel(e):
+        return None if e is None else round(e["ts"] - t0, 4)
+
+    formed = first("epoch_formed")
+    new_epoch = formed["epoch"] if formed else None
+    in_new = (lambda e: new_epoch is not None and e.get("epoch", -1) >= new_epoch)
+    done = first("step_done", in_new)
+    last_before = max((e.get("step", 0) for e in events if e["kind"] == "step_done" and e["ts"] < t0), default=0)
     out = {
-        "detect_s": first("node_dead"),
-        "abort_s": first("epoch_abort"),
-        "epoch_formed_s": first("epoch_formed"),
-        "comm_ready_s": first("comm_ready"),
-        "state_synced_s": first("state_synced"),
-        "first_step_s": first("step_done"),
+        "detect_s": rel(first("node_dead")),
+        "abort_s": rel(first("epoch_abort")),
+        "epoch_formed_s": rel(formed),
+        "comm_ready_s": rel(first("comm_ready", in_new)),
+        "state_synced_s": rel(first("state_synced", in_new)),
+        "first_step_s": rel(done),
+        "steps_lost": None if done is None else max(0, last_before + 1 - int(done.get("step", 0))),
     }
     out["ttr_s"] = out["first_step_s"]
     return out
