@@ -84,7 +84,7 @@ def build_runtime(force: bool = False, verbose: bool = False) -> str:
         # Host-only C++ (no device code): compiled by hipcc's clang in host mode,
         # linked against libamdhip64 for the pinned-memory / async-copy engine.
         cmd = [_hipcc(), "-O2", "-std=c++17", "-fPIC", "-shared", "-x", "c++", *srcs, "-o", tmp,
-               "-D__HIP_PLATFORM_AMD__", f"-I{ROCM}/include", f"-L{ROCM}/lib", "-lamdhip64", "-lpthread",
+               "-D__HIP_PLATFORM_AMD__", f"-I{ROCM}/include", f"-L{ROCM}/lib", "-lamdhip64", "-lpthread", "-ldl",
                "-Wl,-rpath," + f"{ROCM}/lib"]
         if verbose:
             print(" ".join(cmd))

@@ -43,4 +43,10 @@ SIGS = {
     "edl_ckpt_wait": (i32, [vp, i64, i32]),
     "edl_ckpt_restore": (i32, [vp, i32, i32, u64p, u64p, u64p, vp]),
     "edl_ckpt_engine_destroy": (None, [vp]),
+    "edl_stream_create_cumask": (vp, [i32, ctypes.POINTER(ctypes.c_uint32), i32, i32]),
+    "edl_stream_destroy": (i32, [vp]),
+    "edl_roctx_available": (i32, []),
+    "edl_roctx_push": (i32, [cp]),
+    "edl_roctx_pop": (i32, []),
+    "edl_roctx_mark": (None, [cp]),
 }

@@ -81,6 +81,31 @@ class JobMaster:
         self.events.emit("master_started", port=self.port)
         return self
 
+    def serve_metrics(self, port: int = 0) -> int:
+        """Prometheus text endpoint: per-member training metrics reported to the store."""
+        from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
+
+        from easydl_amd.utils.metrics import render_prometheus
+        master = self
+
+        class H(BaseHTTPRequestHandler):
+            def log_message(self, *a):
+                pass
+
+            def do_GET(self):
+                ms = {n: m for n in master.rdzv.members() if (m := master.kv.get(f"metrics/{n}"))}
+                body = render_prometheus(ms, master.job).encode()
+                self.send_response(200)
+                self.send_header("Content-Type", "text/plain; version=0.0.4")
+                self.send_header("Content-Length", str(len(body)))
+                self.end_headers()
+                self.wfile.write(body)
+
+        srv = ThreadingHTTPServer(("127.0.0.1", port), H)
+        threading.Thread(target=srv.serve_forever, daemon=True, name="edl-metrics").start()
+        self._metrics_srv = srv
+        return srv.server_address[1]
+
     def stop(self):
         self._stop.set()
         for t in self._threads:
@@ -111,6 +136,7 @@ def main(argv=None):
     ap.add_argument("--brain-url", default=os.environ.get("EDL_BRAIN_URL"))
     ap.add_argument("--plan-period", type=float, default=30.0)
     ap.add_argument("--job-resource", default=None, help="user JobResource JSON/YAML (Brain not consulted)")
+    ap.add_argument("--metrics-port", type=int, default=-1, help="Prometheus endpoint port (0 = any, -1 = off)")
     a = ap.parse_args(argv)
     logging.basicConfig(level=logging.INFO, format="%(asctime)s [master] %(message)s")
     cfg = RendezvousConfig(min_nodes=a.min, max_nodes=a.max, initial_nodes=a.initial, join_window_s=a.join_window,
@@ -130,6 +156,8 @@ def main(argv=None):
         doc = json.loads(txt) if txt.lstrip().startswith("{") else load_yaml_docs(txt)[0]
         m.kv.set("jobresource", json.dumps(JobResource.from_dict(doc).to_dict()))
     m.start()
+    if a.metrics_port >= 0:
+        m.events.emit("metrics_endpoint", port=m.serve_metrics(a.metrics_port))
     signal.signal(signal.SIGTERM, lambda *_: m._stop.set())
     print(json.dumps({"master_port": m.port}), flush=True)
     m.serve_forever()

@@ -225,6 +225,7 @@ class RendezvousClient:
         self._hb_stop = threading.Event()
         self._hb = None
         self.epoch = 0
+        self.plan_version = 0
 
     def join(self) -> None:
         self.kv.set(f"rdzv/info/{self.node_id}", json.dumps(dict(self.info, pid=os.getpid(),
@@ -270,33 +271,39 @@ class RendezvousClient:
         raise TimeoutError(f"no rendezvous assignment after epoch {after_epoch} within {timeout_s}s")
 
     # -- step commit -------------------------------------------------------------
+    def _decision(self, kind: str) -> str:
+        # the decider also fixes the runtime-plan version every rank switches to
+        return f"{kind}:{self.latest_epoch()}:{self.kv.counter('plan/version')}"
+
     def commit(self, epoch: int, step: int, world: int, ok: bool, timeout_s: float = 600.0,
                gc: bool = False) -> tuple[bool, int]:
         """Agree with every rank of ``epoch`` on step ``step``.
 
         Returns ``(apply, latest_epoch)``: apply the optimizer step iff True;
-        leave the epoch after this step iff ``latest_epoch > epoch``.
+        leave the epoch after this step iff ``latest_epoch > epoch``.  The
+        agreed runtime-plan version is left in ``self.plan_version``.
         """
         dkey = f"decision/{epoch}/{step}"
         if ok:
             c = self.kv.add(f"commit/{epoch}/{step}", 1)
             if c >= world:
-                self.kv.compare_set(dkey, "", f"commit:{self.latest_epoch()}")
+                self.kv.compare_set(dkey, "", self._decision("commit"))
         else:
-            self.kv.compare_set(dkey, "", f"abort:{self.latest_epoch()}")
+            self.kv.compare_set(dkey, "", self._decision("abort"))
         t_end = time.monotonic() + timeout_s
         poll = 0.0002
         while True:
             if self.kv.exists(dkey):
                 d = self.kv.get_str(dkey)
-                kind, e = d.split(":")
+                kind, e, pv = d.split(":")
+                self.plan_version = int(pv)
                 if gc and step >= 2:
                     # everyone has read decision(step-2) before anyone can decide step-1: GC
                     self.kv.delete(f"commit/{epoch}/{step - 2}")
                     self.kv.delete(f"decision/{epoch}/{step - 2}")
                 return kind == "commit", int(e)
             if self.aborted(epoch):
-                self.kv.compare_set(dkey, "", f"abort:{self.latest_epoch()}")
+                self.kv.compare_set(dkey, "", self._decision("abort"))
                 continue
             if time.monotonic() > t_end:
                 raise TimeoutError(f"commit of step {step} in epoch {epoch} timed out")

@@ -40,8 +40,10 @@ from easydl_amd.parallel.ddp import ElasticDDP
 from easydl_amd.parallel.flat import FlatParams
 from easydl_amd.trainer.context import TrainerContext
 from easydl_amd.trainer.data import ElasticBatchPlan
-from easydl_amd.utils import fault
+from easydl_amd.utils import fault, trace
 from easydl_amd.utils.events import EventLog
+from easydl_amd.utils.metrics import MetricsReporter
+from easydl_amd.utils.resources import apply_plan
 
 log = logging.getLogger(__name__)
 
@@ -65,6 +67,7 @@ class ElasticTrainer:
         self.device = torch.device(device)
         if self.device.type == "cuda":
             torch.cuda.set_device(self.device)
+        self.resources = apply_plan(self.ctx, self.device)  # Brain CU mask / HBM cap
         self.events = EventLog(os.path.join(self.ctx.run_dir, f"events-{self.ctx.role}{self.ctx.index}.jsonl"),
                                proc=f"{self.ctx.role}{self.ctx.index}")
         torch.manual_seed(seed)
@@ -95,6 +98,9 @@ class ElasticTrainer:
         self.fault = fault.FaultInjector.from_env(self.ctx, self.events)
         self.history: list[dict] = []
         self.last_loss = None
+        self.tokens_per_sample = 0
+        self.metrics = MetricsReporter(path=os.path.join(self.ctx.run_dir, f"metrics-{self.ctx.role}{self.ctx.index}.jsonl"))
+        self.plan_version = 0
 
     # ------------------------------------------------------------------ setup
     def _connect(self):
@@ -114,6 +120,7 @@ class ElasticTrainer:
             self._manager.start()
         info = {"index": self.ctx.index, "role": self.ctx.role, "gpu": self.ctx.gpu}
         self.rdzv = RendezvousClient(self.kv, self.ctx.node_id, info)
+        self.metrics.kv, self.metrics.node = self.kv, self.ctx.node_id
         self.rdzv.join()
         self.events.emit("joined", node=self.ctx.node_id)
 
@@ -266,15 +273,18 @@ class ElasticTrainer:
             batch = data.batch(idx, self.device)
             w = len(idx) / plan.global_batch
             ctxm = self.ddp.no_sync() if i < len(mbs) - 1 else _null()
-            with ctxm:
-                loss = loss_fn(self.model, batch)
-                (loss * w).backward() if w != 1.0 else loss.backward()
+            with ctxm, trace.range(f"microbatch{i}"):
+                with trace.range("fwd"):
+                    loss = loss_fn(self.model, batch)
+                with trace.range("bwd"):
+                    (loss * w).backward() if w != 1.0 else loss.backward()
             ld = loss.detach() * w
             loss_acc = ld if loss_acc is None else loss_acc + ld
             total += w
         # a rank without samples (world > batch) still joins every all-reduce with zeros:
         # finish() zero-fills untouched gradients before flushing the buckets.
-        self.ddp.finish()
+        with trace.range("grad_sync"):
+            self.ddp.finish()
         self.fault.maybe_inject("after_backward", self.step, trainer=self)
         return None if loss_acc is None else loss_acc / total
 
@@ -321,7 +331,8 @@ class ElasticTrainer:
                 if apply:
                     if self.checkpoint is not None:
                         self.checkpoint.fence()  # never update params under an in-flight snapshot
-                    self.opt.step(pre_scale=1.0)
+                    with trace.range("optimizer"):
+                        self.opt.step(pre_scale=1.0)
                     self.step += 1
                     self.last_loss = loss
                     rec = {"step": self.step, "epoch": self.comm.epoch, "world": self.comm.world_size,
@@ -329,6 +340,9 @@ class ElasticTrainer:
                     self.history.append(rec)
                     self.events.emit("step_done", step=self.step, epoch=self.comm.epoch,
                                      world=self.comm.world_size)
+                    self.metrics.record(self.step, rec["dt"], samples=self.global_batch,
+                                        tokens=self.global_batch * self.tokens_per_sample, world=self.comm.world_size,
+                                        loss=None)
                     if self.checkpoint is not None:
                         self.checkpoint.on_step(self)
                     if on_step is not None:
@@ -337,12 +351,25 @@ class ElasticTrainer:
                         log.info("step %d loss %.4f world %d", self.step, float(loss), self.comm.world_size)
                 else:
                     self.events.emit("step_dropped", step=self.step, epoch=self.comm.epoch)
+                if self.rdzv is not None and self.rdzv.plan_version != self.plan_version:
+                    self._apply_runtime_plan(self.rdzv.plan_version)
                 need_new = (not ok) or self.comm.aborted or (self.rdzv is not None and latest > self.comm.epoch)
                 if need_new:
                     self._reconfigure()
         finally:
             self._stop.set()
         return self
+
+    def _apply_runtime_plan(self, version: int) -> None:
+        """Brain runtime knobs, switched by every rank at the same committed step."""
+        self.plan_version = version
+        mb = self.kv.get("plan/bucket_mb")
+        if mb and float(mb) != self.ddp.bucket_mb:
+            self.ddp.set_bucket_mb(float(mb))
+            self.events.emit("plan_bucket_mb", mb=float(mb), step=self.step)
+        ci = self.kv.get("plan/ckpt_interval")
+        if ci and self.checkpoint is not None:
+            self.checkpoint.interval = max(1, int(ci))
 
     def _reconfigure(self):
         old = self.comm

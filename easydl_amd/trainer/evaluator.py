@@ -1,0 +1,79 @@
+"""Evaluator role for all-reduce jobs (reference docs/design/elastic-training-operator.md:43-44,79-85).
+
+The DDP workers never pause for evaluation: the evaluator process watches the
+job's in-memory snapshots (/dev/shm, format v1 slots), loads the newest
+complete step into its own copy of the model — parameters only (fp32 masters
+are converted to the model dtype; optimizer moments are skipped) — scores it
+and publishes ``eval/latest`` to the master's store + an ``eval`` event.
+(Parameter-server jobs use ``ps_trainer.run_evaluator``, which pulls from the PS.)
+"""
+from __future__ import annotations
+
+import json
+import os
+import time
+
+import torch
+
+from easydl_amd.ckpt.manager import CheckpointManager, ShmSegment, _TD
+from easydl_amd.parallel.flat import FlatParams
+from easydl_amd.utils.events import EventLog
+
+
+class SnapshotEvaluator:
+    def __init__(self, model_fn, job: str, device="cpu", kv=None, run_dir: str | None = None):
+        self.device = torch.device(device)
+        self.model = model_fn(self.device)
+        self.flat = FlatParams(self.model)
+        self.groups = {g.name: g for g in self.flat.groups}
+        self.ckpt = CheckpointManager(job)
+        self.kv = kv
+        self.events = EventLog(os.path.join(run_dir, "events-evaluator.jsonl"), proc="evaluator") if run_dir else None
+        self.step = None
+
+    def load_latest(self) -> int | None:
+        found = self.ckpt.find_latest()
+        if found is None:
+            return None
+        world, step, infos = found
+        if step == self.step:
+            return None
+        for s, info in enumerate(infos):
+            seg = ShmSegment(self.ckpt.seg_name(world, s), create=False)
+            try:
+                for name, dt, numel, lo, hi, off in info["meta"]["t"]:
+                    if name.startswith("model."):
+                        g = self.groups.get(name[len("model."):])
+                    elif name.startswith("opt.") and name.endswith(".master"):
+                        g = self.groups.get(name[len("opt."):-len(".master")])
+                    else:
+                        continue
+                    if g is None:
+                        continue
+                    nbytes = (hi - lo) * torch.empty((), dtype=_TD[dt]).element_size()
+                    src = torch.from_numpy(seg.view(info["slot"], off, nbytes)).view(_TD[dt])
+                    with torch.no_grad():
+                        g.data[lo:hi].copy_(src.to(self.device, g.data.dtype))
+            finally:
+                seg.close()
+        self.step = step
+        return step
+
+    def run(self, eval_fn, interval_s: float = 5.0, stop=lambda: False, max_evals: int | None = None) -> list[dict]:
+        out = []
+        while not stop():
+            step = self.load_latest()
+            if step is not None:
+                self.model.eval()
+                with torch.no_grad():
+                    m = dict(eval_fn(self.model))
+                m["step"] = step
+                out.append(m)
+                if self.kv is not None:
+                    self.kv.set("eval/latest", json.dumps(m))
+                if self.events is not None:
+                    self.events.emit("eval", **m)
+                if max_evals is not None and len(out) >= max_evals:
+                    break
+            time.sleep(interval_s)
+        return out

@@ -89,3 +89,22 @@ def test_snapshot_restore_resumes_bit_identically(tmp_path):
         assert c.step == 6
     finally:
         unlink_job_segments("ck")
+
+
+def test_snapshot_evaluator_reads_latest(tmp_path):
+    from easydl_amd.trainer.evaluator import SnapshotEvaluator
+    unlink_job_segments("ckev")
+    data = SyntheticTokens(CFG.vocab_size, 16, num_samples=1024)
+    ckpt = CheckpointManager("ckev", interval=2)
+    try:
+        ctx = TrainerContext(job="ckev", run_dir=str(tmp_path))
+        tr = ElasticTrainer(lambda d: Llama(CFG, device=d, dtype=torch.float32), global_batch=4, micro_batch=2,
+                            lr=1e-3, device="cpu", ctx=ctx, checkpoint=ckpt)
+        tr.fit(lambda m, b: m(*b), data, num_steps=4)
+        ev = SnapshotEvaluator(lambda d: Llama(CFG, device=d, dtype=torch.float32), "ckev", run_dir=str(tmp_path))
+        res = ev.run(lambda m: {"loss": float(m(*data.batch([1, 2], "cpu")))}, interval_s=0, max_evals=1)
+        assert res[0]["step"] == 4
+        for a, b in zip(tr.flat.groups, ev.flat.groups):
+            assert torch.equal(a.data, b.data)
+    finally:
+        unlink_job_segments("ckev")
