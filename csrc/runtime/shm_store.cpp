@@ -422,6 +422,55 @@ int edl_ckpt_restore(void* seg, int slot, int nbuf, const uint64_t* dev_ptrs, co
   return 0;
 }
 
+// Fast restore from (pageable) shm: multi-threaded memcpy into two pinned
+// staging buffers, each drained by an async H2D copy on `stream`; the CPU copy
+// of chunk i+1 overlaps the DMA of chunk i.  Blocks until done.
+int edl_ckpt_restore_pipelined(void* seg, int slot, int nbuf, const uint64_t* dev_ptrs, const uint64_t* sizes,
+                               const uint64_t* offsets, hipStream_t stream, uint64_t chunk, int threads) {
+  auto* s = static_cast<Seg*>(seg);
+  if (slot < 0) slot = edl_shm_current(s);
+  if (slot < 0) return -1;
+  if (chunk == 0) chunk = 256ull << 20;
+  if (threads <= 0) threads = 8;
+  void* stage[2] = {nullptr, nullptr};
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  hipError_t err = hipSuccess;
+  for (int i = 0; i < 2 && err == hipSuccess; ++i) {
+    err = hipHostMalloc(&stage[i], chunk, hipHostMallocDefault);
+    if (err == hipSuccess) err = hipEventCreateWithFlags(&ev[i], hipEventDisableTiming);
+  }
+  bool used[2] = {false, false};
+  int k = 0;
+  const uint8_t* base = s->data(slot);
+  for (int b = 0; b < nbuf && err == hipSuccess; ++b) {
+    for (uint64_t off = 0; off < sizes[b] && err == hipSuccess; off += chunk, k ^= 1) {
+      const uint64_t n = sizes[b] - off < chunk ? sizes[b] - off : chunk;
+      if (used[k]) err = hipEventSynchronize(ev[k]);  // staging buffer k free again
+      if (err != hipSuccess) break;
+      const uint8_t* src = base + offsets[b] + off;
+      uint8_t* dst = (uint8_t*)stage[k];
+      const uint64_t per = (n + threads - 1) / threads;
+      std::vector<std::thread> ts;
+      for (int t = 0; t < threads; ++t) {
+        const uint64_t lo = per * t;
+        if (lo >= n) break;
+        const uint64_t len = (lo + per > n) ? n - lo : per;
+        ts.emplace_back([=] { memcpy(dst + lo, src + lo, len); });
+      }
+      for (auto& th : ts) th.join();
+      err = hipMemcpyAsync((uint8_t*)dev_ptrs[b] + off, dst, n, hipMemcpyHostToDevice, stream);
+      if (err == hipSuccess) err = hipEventRecord(ev[k], stream);
+      used[k] = true;
+    }
+  }
+  if (err == hipSuccess) err = hipStreamSynchronize(stream);
+  for (int i = 0; i < 2; ++i) {
+    if (ev[i]) hipEventDestroy(ev[i]);
+    if (stage[i]) hipHostFree(stage[i]);
+  }
+  return (int)err;
+}
+
 void edl_ckpt_engine_destroy(void* eng) {
   auto* e = static_cast<Engine*>(eng);
   if (!e) return;

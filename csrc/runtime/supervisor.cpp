@@ -29,6 +29,7 @@
 #include <time.h>
 #include <unistd.h>
 
+#include <cstdio>
 #include <map>
 #include <mutex>
 #include <string>
@@ -213,6 +214,42 @@ int edl_sup_wait(void* h, int timeout_ms, EdlExitEvent* out, int max) {
     count += reap(s, it->second, &out[count]);
   }
   return count;
+}
+
+// Children that are being torn down right now (PF_EXITING set in
+// /proc/<pid>/stat flags) but not yet reaped.  A SIGKILLed process with a
+// large address space (hundreds of GB of GPU + shared memory mappings) takes
+// seconds to unmap before its pidfd becomes readable; its PF_EXITING flag is
+// set at the start of do_exit(), so this reports the death seconds earlier.
+int edl_sup_exiting(void* h, int* pids, int max) {
+  auto* s = static_cast<Supervisor*>(h);
+  std::vector<pid_t> live;
+  {
+    std::lock_guard<std::mutex> g(s->mu);
+    for (auto& kv : s->children) live.push_back(kv.first);
+  }
+  int n = 0;
+  char path[64], buf[1024];
+  for (pid_t p : live) {
+    if (n >= max) break;
+    snprintf(path, sizeof(path), "/proc/%d/stat", (int)p);
+    int fd = open(path, O_RDONLY | O_CLOEXEC);
+    if (fd < 0) continue;
+    ssize_t r = read(fd, buf, sizeof(buf) - 1);
+    close(fd);
+    if (r <= 0) continue;
+    buf[r] = 0;
+    // fields after "(comm)": state ppid pgrp session tty_nr tpgid flags ...
+    char* rp = strrchr(buf, ')');
+    if (!rp) continue;
+    char state = 0;
+    long ppid, pgrp, sess, tty, tpgid;
+    unsigned long flags = 0;
+    if (sscanf(rp + 2, "%c %ld %ld %ld %ld %ld %lu", &state, &ppid, &pgrp, &sess, &tty, &tpgid, &flags) != 7)
+      continue;
+    if ((flags & 0x4UL) || state == 'Z' || state == 'X') pids[n++] = (int)p;  // PF_EXITING
+  }
+  return n;
 }
 
 int edl_sup_kill(void* h, int pid, int sig, int group) {

@@ -22,6 +22,7 @@ SIGS = {
                             ctypes.POINTER(i32)]),
     "edl_sup_wait": (i32, [vp, i32, ctypes.POINTER(ExitEvent), i32]),
     "edl_sup_kill": (i32, [vp, i32, i32, i32]),
+    "edl_sup_exiting": (i32, [vp, ctypes.POINTER(i32), i32]),
     "edl_sup_num_children": (i32, [vp]),
     "edl_sup_destroy": (None, [vp]),
     "edl_shm_open": (vp, [cp, u64, i32, i32]),
@@ -43,6 +44,7 @@ SIGS = {
     "edl_ckpt_wait": (i32, [vp, i64, i32]),
     "edl_ckpt_restore": (i32, [vp, i32, i32, u64p, u64p, u64p, vp]),
     "edl_ckpt_engine_destroy": (None, [vp]),
+    "edl_ckpt_restore_pipelined": (i32, [vp, i32, i32, u64p, u64p, u64p, vp, u64, i32]),
     "edl_stream_create_cumask": (vp, [i32, ctypes.POINTER(ctypes.c_uint32), i32, i32]),
     "edl_stream_destroy": (i32, [vp]),
     "edl_roctx_available": (i32, []),

@@ -334,7 +334,7 @@ class CheckpointManager:
             seg = ShmSegment(self.seg_name(world, s), create=False)
             try:
                 _load_shard(lambda off, nb: seg.view(info["slot"], off, nb), info["meta"]["t"], state, dev,
-                            info["checksum"], f"shm shard {s} of step {step}")
+                            info["checksum"], f"shm shard {s} of step {step}", seg=seg, slot=info["slot"])
             finally:
                 seg.close()
         self.finish_restore(trainer)
@@ -414,10 +414,35 @@ def load_dir(d: str, trainer) -> None:
     trainer.opt.step_count = int(m["opt_step"])
 
 
-def _load_shard(read, table, state, dev, expect: int, what: str) -> None:
+def _load_shard(read, table, state, dev, expect: int, what: str, seg=None, slot=None) -> None:
     """Copy one shard's tensor slices to their device buffers and verify the checksum
-    (on the GPU for device tensors: no host pass over tens of GB)."""
+    (on the GPU for device tensors: no host pass over tens of GB).  From a shm
+    segment to a GPU the copy runs through the native pipelined restore
+    (multi-threaded memcpy into pinned staging buffers overlapped with DMA)."""
     acc = torch.zeros(1, dtype=torch.int64, device=dev) if dev.type == "cuda" else None
+    if acc is not None and seg is not None:
+        ptrs, sizes, offs, items = [], [], [], []
+        for name, dt, numel, lo, hi, off in table:
+            t = state[name]
+            nbytes = (hi - lo) * t.element_size()
+            if nbytes:
+                dst = t.view(-1)[lo:hi]
+                ptrs.append(dst.data_ptr())
+                sizes.append(nbytes)
+                offs.append(off)
+                items.append((dst, off))
+        n = len(ptrs)
+        arr = lambda v: (ctypes.c_uint64 * n)(*v)  # noqa: E731
+        rc = _native.runtime()("edl_ckpt_restore_pipelined", seg.h, slot, n, arr(ptrs), arr(sizes), arr(offs),
+                               ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream), 256 << 20, 16)
+        if rc != 0:
+            raise RuntimeError(f"pipelined restore failed: hipError {rc}")
+        for dst, off in items:
+            checksum_tensor(dst, acc, base_index=off // 4)
+        got = int(acc.item()) & ((1 << 64) - 1)
+        if got != expect:
+            raise RuntimeError(f"checksum mismatch in {what}: {got:#x} != {expect:#x}")
+        return
     total = 0
     for name, dt, numel, lo, hi, off in table:
         t = state[name]

@@ -340,7 +340,24 @@ class ElasticOperator:
         workers = [p for p in self.procs.values() if p.role == "worker"]
         return jr.replicas("worker") > 0 and bool(workers) and all(p.state == "completed" for p in workers)
 
+    def _early_exits(self) -> None:
+        """Report deaths as soon as the kernel starts tearing a worker down."""
+        if not hasattr(self.launcher, "exiting") or self.kv is None:
+            return
+        for pid in self.launcher.exiting():
+            p = next((q for q in self.procs.values() if q.pid == pid), None)
+            if p is None or p.role == "trainer" or getattr(p, "_early_reported", False):
+                continue
+            p._early_reported = True
+            if p.state == "running":
+                try:
+                    self.kv.set(f"ev/exit/{p.node_id}", json.dumps({"exiting": True, "ts": time.time()}))
+                    self.events.emit("exiting", name=p.name, pid=pid)
+                except Exception:
+                    pass
+
     def tick(self, timeout_s: float = 0.05) -> None:
+        self._early_exits()
         for ex in self.launcher.poll(timeout_s):
             self.handle_exit(ex)
         self._poll_jobresource()

@@ -78,6 +78,12 @@ class Supervisor:
             out.append(Exit(e.pid, self.names.pop(e.pid, "?"), e.exit_code, e.signal, e.ts_ns / 1e9))
         return out
 
+    def exiting(self, max_n: int = 64) -> list[int]:
+        """Children already inside exit() (PF_EXITING) but not yet reaped."""
+        buf = (ctypes.c_int * max_n)()
+        n = self.rt("edl_sup_exiting", self.h, buf, max_n)
+        return [buf[i] for i in range(max(0, n))]
+
     def kill(self, pid: int, sig: int = signal.SIGKILL, group: bool = True) -> None:
         rc = self.rt("edl_sup_kill", self.h, pid, int(sig), 1 if group else 0)
         if rc != 0 and -rc != 3:  # ESRCH: already gone
