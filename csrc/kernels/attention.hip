@@ -23,6 +23,9 @@
 //     (Q/dO slices double-buffered in LDS);
 //   * dQ kernel: the forward's structure with dP^T = V dO^T and dQ^T += K^T dS^T.
 // Capability source: Llama-3 training workloads (BASELINE.json configs 3/5).
+#include <cstdlib>
+#include <type_traits>
+
 #include "common.h"
 
 using namespace edl;
@@ -34,6 +37,7 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef short i16x4 __attribute__((ext_vector_type(4)));
 typedef short i16x8 __attribute__((ext_vector_type(8)));
 typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
+typedef __attribute__((address_space(3))) void lds_void;
 
 constexpr int HD = 128;        // head dim
 constexpr float LOG2E = 1.4426950408889634f;
@@ -77,7 +81,22 @@ __device__ __forceinline__ bf16x8 acc_to_b(const f32x16& acc, int s2) {
 // row (within a 32-row tile) of accumulator register i for lane half h
 __device__ __forceinline__ int acc_row(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }
 
-// stage `rows` x 256 B of a token-major tensor into a swizzled LDS tile
+// v_exp_f32 directly (exp2f() adds a denormal range fix-up: 3 extra VALU per call)
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// reductions across the two 32-lane halves with v_permlane32_swap (no LDS traffic)
+__device__ __forceinline__ float xhalf_max(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float xhalf_sum(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+// stage `rows` x 256 B of a token-major tensor into a swizzled LDS tile.  Rows
+// past the end are clamped to the last row (no exec-mask branches in the hot
+// loop); the score mask / zero probabilities make their contribution vanish.
 template <int ROWS>
 __device__ __forceinline__ void load_rows(u32x4 (&regs)[ROWS / 16], const bf16_t* base, int64_t stride, int row0,
                                           int S) {
@@ -85,8 +104,8 @@ __device__ __forceinline__ void load_rows(u32x4 (&regs)[ROWS / 16], const bf16_t
   for (int i = 0; i < ROWS / 16; ++i) {
     const int idx = threadIdx.x + 256 * i;
     const int r = idx >> 4, c = idx & 15;
-    const int row = row0 + r;
-    regs[i] = row < S ? *reinterpret_cast<const u32x4*>(base + (int64_t)row * stride + c * 8) : u32x4{0, 0, 0, 0};
+    const int row = min(row0 + r, S - 1);
+    regs[i] = *reinterpret_cast<const u32x4*>(base + (int64_t)row * stride + c * 8);
   }
 }
 template <int ROWS>
@@ -98,8 +117,64 @@ __device__ __forceinline__ void store_rows(char* tile, const u32x4 (&regs)[ROWS 
   }
 }
 
-__device__ __forceinline__ bf16x8 load_frag(const bf16_t* rowp, int s, int h, bool valid) {
-  if (!valid) return bf16x8{};
+// 8 bf16 of a (clamped, always valid) row pointer: k-step s, lane half h
+// LDS-DMA staging: fill ROWS x 256 B of a swizzled LDS tile straight from
+// global memory with buffer_load_dwordx4 ... lds (no staging registers, no
+// ds_write).  Each wave-instruction writes one contiguous 1-KiB piece = 4 rows,
+// lane l landing at piece + 16*l, so lane l fetches the chunk that the XOR
+// swizzle maps to that slot.  The per-lane byte offsets are loop-invariant
+// (PER_WAVE VGPRs); the tile's first row goes in the scalar offset.  The buffer
+// descriptor's range ends at row S of this (batch, head) slice, so rows past
+// the end read as zeros (and are masked).  Completion: vmcnt + barrier.
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+
+__device__ __forceinline__ rsrc_t make_rsrc(const void* base, int64_t nbytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)nbytes, 0x00020000);
+}
+
+// The LDS-DMA builtin exists only for the device target; clang's host pass
+// instantiates kernel templates too, and an (otherwise silent) deferred error
+// there drops the kernels' host launch stubs -> keep it out of the host pass.
+__device__ __forceinline__ void buffer_load_lds16(rsrc_t rs, void* lds, uint32_t voff, uint32_t soff) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)lds, 16, voff, soff, 0, 0);
+#endif
+}
+__device__ __forceinline__ void buffer_load_lds4(rsrc_t rs, void* lds, uint32_t voff, uint32_t soff) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)lds, 4, voff, soff, 0, 0);
+#endif
+}
+
+template <int ROWS, int NWAVES>
+struct DmaPlan {
+  static constexpr int PER_WAVE = ROWS / 4 / NWAVES;
+  uint32_t voff[PER_WAVE];
+  __device__ __forceinline__ DmaPlan(int64_t stride_elems, int w, int lane) {
+#pragma unroll
+    for (int i = 0; i < PER_WAVE; ++i) {
+      const int r = 4 * (w * PER_WAVE + i) + (lane >> 4);
+      const int c = (lane & 15) ^ (((r & 3) << 2) | ((r >> 2) & 3));
+      voff[i] = (uint32_t)((r * stride_elems + c * 8) * 2);
+    }
+  }
+  // rows row0 .. row0+ROWS-1 (row0 * row_bytes goes in the scalar offset)
+  __device__ __forceinline__ void issue(char* tile, rsrc_t rs, uint32_t soff, int w) const {
+#pragma unroll
+    for (int i = 0; i < PER_WAVE; ++i)
+      buffer_load_lds16(rs, tile + (w * PER_WAVE + i) * 1024, voff[i], soff);
+  }
+};
+
+// 64 consecutive fp32 -> LDS, one wave-instruction (past-the-end reads as 0)
+__device__ __forceinline__ void dma_f32x64(float* dst, rsrc_t rs, int i0, int lane) {
+  buffer_load_lds4(rs, dst, (uint32_t)lane * 4, (uint32_t)i0 * 4);
+}
+
+// all of this wave's outstanding vector-memory ops (incl. LDS-DMA) done
+__device__ __forceinline__ void wait_vm() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+
+__device__ __forceinline__ bf16x8 load_frag(const bf16_t* rowp, int s, int h) {
   return *reinterpret_cast<const bf16x8*>(rowp + (2 * s + h) * 8);
 }
 
@@ -118,151 +193,136 @@ __device__ __forceinline__ void store_accT(bf16_t* rowp, const f32x16 (&acc)[4],
 }
 
 // ---------------------------------------------------------------------------
-// forward: a wave owns QG*32 queries (QG column groups); every K / V fragment
-// read from LDS feeds QG MFMAs.
+// forward: a wave owns 32 queries; one 64-key tile = 16 MFMAs for S^T and 16
+// for O^T.  The per-tile VALU work is kept to ~4 instructions per score
+// (max3, fma+exp, add, half a cvt_pk): masks only on the diagonal / tail tile.
 // ---------------------------------------------------------------------------
-template <bool CAUSAL, int QG>
-__global__ __launch_bounds__(256, QG == 1 ? 2 : 1) void attn_fwd_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
+template <bool MASK, bool CAUSAL>
+__device__ __forceinline__ void fwd_tile(const char* Ks, const char* Vs, const bf16x8 (&qf)[8], f32x16 (&oacc)[4],
+                                         float& m, float& lsum, int kv0, int qr, int S, float sl2, int lane) {
+  const int h = lane >> 5, l31 = lane & 31;
+  f32x16 sacc[2];
+  sacc[0] = sacc[1] = f32x16{};
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+#pragma unroll
+    for (int s = 0; s < 8; ++s) sacc[t] = mfma(row_read(Ks, 32 * t + l31, s, h), qf[s], sacc[t]);
+  }
+  if (MASK) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int key = kv0 + 32 * t + acc_row(i, h);
+        if (key >= S || (CAUSAL && key > qr)) sacc[t][i] = -INFINITY;
+      }
+    }
+  }
+  float mx = sacc[0][0];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) mx = fmaxf(mx, sacc[t][i]);
+  }
+  mx = xhalf_max(mx);
+  // running max in the scaled log2 domain (sl2 > 0 commutes with max)
+  const float mnew = fmaxf(m, mx * sl2);
+  const bool grow = mnew > m;
+  const float alpha = fast_exp2(m - mnew);
+  m = mnew;
+  const float negm = -mnew;
+  float ps = 0.f;
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const float p = fast_exp2(__builtin_fmaf(sacc[t][i], sl2, negm));
+      sacc[t][i] = p;
+      ps += p;
+    }
+  }
+  lsum = lsum * alpha + ps;
+  // exact lazy rescale: only when some row max of this wave grew
+  if (__any(grow)) {
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) oacc[dt] *= alpha;
+  }
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const bf16x8 pb = acc_to_b(sacc[t], s2);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) oacc[dt] = mfma(tr_read(Vs, 32 * t + 16 * s2 + 4 * h, dt, lane), pb, oacc[dt]);
+    }
+  }
+}
+
+template <bool CAUSAL>
+__global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
                                                           const bf16_t* __restrict__ v, bf16_t* __restrict__ o,
                                                           float* __restrict__ lse, int S, int H, int KV,
                                                           float scale_log2) {
-  constexpr int BQ = 128 * QG;
+  constexpr int BQ = 128;
   __shared__ __attribute__((aligned(16))) char smem[2 * 32768];
   const int qb = gridDim.x - 1 - blockIdx.x;  // longest causal rows first
   const int hq = blockIdx.y, b = blockIdx.z, hk = hq / (H / KV);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, l31 = lane & 31;
   const int q0 = qb * BQ;
-  const int wq0 = q0 + 32 * QG * w;  // first query of this wave
+  const int wq0 = q0 + 32 * w;  // first query of this wave
   const int64_t qs = (int64_t)H * HD, ks = (int64_t)KV * HD;
   const bf16_t* qp = q + (int64_t)b * S * qs + hq * HD;
   const bf16_t* kp = k + (int64_t)b * S * ks + hk * HD;
   const bf16_t* vp = v + (int64_t)b * S * ks + hk * HD;
 
-  bf16x8 qf[QG][8];
+  const int qr = wq0 + l31;
+  bf16x8 qf[8];
 #pragma unroll
-  for (int g = 0; g < QG; ++g) {
-    const int qr = wq0 + 32 * g + l31;
-#pragma unroll
-    for (int s = 0; s < 8; ++s) qf[g][s] = load_frag(qp + (int64_t)qr * qs, s, h, qr < S);
-  }
+  for (int s = 0; s < 8; ++s) qf[s] = load_frag(qp + (int64_t)min(qr, S - 1) * qs, s, h);
   const int kv_end = CAUSAL ? min(S, q0 + BQ) : S;
   const int ntiles = (kv_end + 63) / 64;
-  f32x16 oacc[QG][4];
-  float m[QG], lsum[QG];
+  f32x16 oacc[4];
+  float m = -1e30f, lsum = 0.f;
 #pragma unroll
-  for (int g = 0; g < QG; ++g) {
-    m[g] = -1e30f;
-    lsum[g] = 0.f;
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) oacc[g][dt] = f32x16{};
-  }
+  for (int dt = 0; dt < 4; ++dt) oacc[dt] = f32x16{};
 
-  u32x4 kreg[4], vreg[4];
-  load_rows<64>(kreg, kp, ks, 0, S);
-  load_rows<64>(vreg, vp, ks, 0, S);
-  store_rows<64>(smem, kreg);
-  store_rows<64>(smem + 16384, vreg);
+  const DmaPlan<64, 4> plan(ks, w, lane);
+  const int64_t kv_bytes = ((int64_t)S * ks - hk * HD) * 2;
+  const rsrc_t krs = make_rsrc(kp, kv_bytes), vrs = make_rsrc(vp, kv_bytes);
+  const uint32_t tile_bytes = (uint32_t)(64 * ks * 2);
+  plan.issue(smem, krs, 0, w);
+  plan.issue(smem + 16384, vrs, 0, w);
+  wait_vm();
   __syncthreads();
 
-  for (int it = 0; it < ntiles; ++it) {
-    const int kv0 = it * 64;
-    if (it + 1 < ntiles) {
-      load_rows<64>(kreg, kp, ks, kv0 + 64, S);
-      load_rows<64>(vreg, vp, ks, kv0 + 64, S);
-    }
-    const char* Ks = smem + (it & 1) * 32768;
-    const char* Vs = Ks + 16384;
-    const bool wave_visible = !CAUSAL || kv0 <= wq0 + 32 * QG - 1;
-    if (wave_visible) {
-      f32x16 sacc[QG][2];
-#pragma unroll
-      for (int g = 0; g < QG; ++g) sacc[g][0] = sacc[g][1] = f32x16{};
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-#pragma unroll
-        for (int s = 0; s < 8; ++s) {
-          const bf16x8 a = row_read(Ks, 32 * t + l31, s, h);
-#pragma unroll
-          for (int g = 0; g < QG; ++g) sacc[g][t] = mfma(a, qf[g][s], sacc[g][t]);
-        }
+  // Tiles below the workgroup's first query (and inside S) need no mask for
+  // any wave: run them in a mask-free loop, the diagonal / tail tiles in a
+  // second loop (two straight-line bodies allocate registers better than one
+  // body with a masked and an unmasked branch).
+  const int nfull = CAUSAL ? min(q0, S) / 64 : S / 64;
+  auto run = [&](auto masked, int it0, int it1) {
+    constexpr bool MASK = decltype(masked)::value;
+#pragma unroll 1
+    for (int it = it0; it < it1; ++it) {
+      const int kv0 = it * 64;
+      if (it + 1 < ntiles) {  // buffer (it+1)&1 was released by the previous barrier
+        char* nxt = smem + ((it + 1) & 1) * 32768;
+        plan.issue(nxt, krs, (it + 1) * tile_bytes, w);
+        plan.issue(nxt + 16384, vrs, (it + 1) * tile_bytes, w);
       }
-      const bool need_mask = (kv0 + 64 > S) || (CAUSAL && kv0 + 63 > wq0);
-      bool grow = false;
-      float alpha[QG];
-#pragma unroll
-      for (int g = 0; g < QG; ++g) {
-        const int qr = wq0 + 32 * g + l31;
-        float mx = -1e30f;
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-#pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            float x = sacc[g][t][i] * scale_log2;
-            if (need_mask) {
-              const int key = kv0 + 32 * t + acc_row(i, h);
-              if (key >= S || (CAUSAL && key > qr)) x = -INFINITY;
-            }
-            sacc[g][t][i] = x;
-            mx = fmaxf(mx, x);
-          }
-        }
-        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-        const float mnew = fmaxf(m[g], mx);
-        grow |= mnew > m[g];
-        alpha[g] = exp2f(m[g] - mnew);
-        m[g] = mnew;
-        float ps = 0.f;
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-#pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            const float p = exp2f(sacc[g][t][i] - mnew);
-            sacc[g][t][i] = p;
-            ps += p;
-          }
-        }
-        lsum[g] = lsum[g] * alpha[g] + ps;
-      }
-      // exact lazy rescale: only when some row max of this wave grew
-      if (__any(grow)) {
-#pragma unroll
-        for (int g = 0; g < QG; ++g) {
-#pragma unroll
-          for (int dt = 0; dt < 4; ++dt) oacc[g][dt] *= alpha[g];
-        }
-      }
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          bf16x8 pb[QG];
-#pragma unroll
-          for (int g = 0; g < QG; ++g) pb[g] = acc_to_b(sacc[g][t], s2);
-#pragma unroll
-          for (int dt = 0; dt < 4; ++dt) {
-            const bf16x8 a = tr_read(Vs, 32 * t + 16 * s2 + 4 * h, dt, lane);
-#pragma unroll
-            for (int g = 0; g < QG; ++g) oacc[g][dt] = mfma(a, pb[g], oacc[g][dt]);
-          }
-        }
-      }
+      const char* Ks = smem + (it & 1) * 32768;
+      if (!MASK || !CAUSAL || kv0 <= wq0 + 31)  // wave-uniform: tile visible to this wave
+        fwd_tile<MASK, CAUSAL>(Ks, Ks + 16384, qf, oacc, m, lsum, kv0, qr, S, scale_log2, lane);
+      wait_vm();
+      __syncthreads();
     }
-    __syncthreads();
-    if (it + 1 < ntiles) {
-      char* nxt = smem + ((it + 1) & 1) * 32768;
-      store_rows<64>(nxt, kreg);
-      store_rows<64>(nxt + 16384, vreg);
-    }
-    __syncthreads();
-  }
-#pragma unroll
-  for (int g = 0; g < QG; ++g) {
-    const int qr = wq0 + 32 * g + l31;
-    const float ltot = lsum[g] + __shfl_xor(lsum[g], 32, 64);
-    if (qr < S) {
-      store_accT(o + (int64_t)b * S * qs + (int64_t)qr * qs + hq * HD, oacc[g], 1.f / ltot, h);
-      if (h == 0) lse[((int64_t)b * H + hq) * S + qr] = (m[g] + log2f(ltot)) * LN2;
-    }
+  };
+  run(std::integral_constant<bool, false>{}, 0, nfull);
+  run(std::integral_constant<bool, true>{}, nfull, ntiles);
+  const float ltot = xhalf_sum(lsum);
+  if (qr < S) {
+    store_accT(o + (int64_t)b * S * qs + (int64_t)qr * qs + hq * HD, oacc, 1.f / ltot, h);
+    if (h == 0) lse[((int64_t)b * H + hq) * S + qr] = (m + log2f(ltot)) * LN2;
   }
 }
 
@@ -271,6 +331,7 @@ __global__ __launch_bounds__(256, QG == 1 ? 2 : 1) void attn_fwd_kernel(const bf
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void attn_bwd_delta_kernel(const bf16_t* __restrict__ o,
                                                              const bf16_t* __restrict__ dout,
+                                                             const float* __restrict__ lse,
                                                              float* __restrict__ delta, int S, int H,
                                                              int64_t nrows) {
   const int64_t row = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 4;  // row = (b*S + s)*H + h
@@ -287,7 +348,9 @@ __global__ __launch_bounds__(256) void attn_bwd_delta_kernel(const bf16_t* __res
   for (int off = 8; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 16);
   if (c == 0 && row < nrows) {
     const int64_t hh = row % H, tok = row / H, s = tok % S, b = tok / S;
-    delta[(b * H + hh) * S + s] = acc;
+    const int64_t i = (b * H + hh) * S + s;
+    delta[i] = acc;
+    delta[nrows + i] = -lse[i] * LOG2E;  // row constant of the exp2 in both bwd kernels
   }
 }
 
@@ -295,27 +358,74 @@ __global__ __launch_bounds__(256) void attn_bwd_delta_kernel(const bf16_t* __res
 // backward: dK, dV.  A workgroup owns 128 keys of one KV head (a wave 32 keys,
 // K/V in registers, dK^T/dV^T accumulators resident) and sweeps 64-query
 // tiles (two 32-row sub-slices) of every query head of the GQA group.
+// LDS per stage: Q tile, dO tile, -lse*log2(e) and delta for the 64 rows.
 // ---------------------------------------------------------------------------
-template <bool CAUSAL>
-__global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_kernel(
+// Issue order S, dP (16 back-to-back MFMAs), then exp(S) under the dP MFMAs,
+// dV += dO^T P under which dS = P (dP - delta) runs, then dK += Q^T dS.
+template <bool MASK, bool CAUSAL>
+__device__ __forceinline__ void dkdv_slice(const char* Qs, const char* Ds, const float* NL, const float* DL, int rb,
+                                           const bf16x8 (&kf)[8], const bf16x8 (&vf)[8], f32x16 (&dka)[4],
+                                           f32x16 (&dva)[4], int qs0, int mykey, int S, float sl2, int lane) {
+  const int h = lane >> 5, l31 = lane & 31;
+  f32x16 sa = f32x16{}, dp = f32x16{};
+#pragma unroll
+  for (int s = 0; s < 8; ++s) sa = mfma(row_read(Qs, rb + l31, s, h), kf[s], sa);
+#pragma unroll
+  for (int s = 0; s < 8; ++s) dp = mfma(row_read(Ds, rb + l31, s, h), vf[s], dp);
+  // accumulator register i <-> query row rb + acc_row(i, h): rows 8g+4h .. +3 are contiguous
+  f32x4 nl[4], dl[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    nl[g] = *reinterpret_cast<const f32x4*>(NL + rb + 8 * g + 4 * h);
+    dl[g] = *reinterpret_cast<const f32x4*>(DL + rb + 8 * g + 4 * h);
+  }
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    float p = fast_exp2(__builtin_fmaf(sa[i], sl2, nl[i >> 2][i & 3]));
+    if (MASK) {
+      const int qi = qs0 + acc_row(i, h);
+      if (qi >= S || mykey >= S || (CAUSAL && mykey > qi)) p = 0.f;
+    }
+    sa[i] = p;
+  }
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) {
+    const bf16x8 pb = acc_to_b(sa, s2);
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) dva[dt] = mfma(tr_read(Ds, rb + 16 * s2 + 4 * h, dt, lane), pb, dva[dt]);
+  }
+#pragma unroll
+  for (int i = 0; i < 16; ++i) dp[i] = sa[i] * (dp[i] - dl[i >> 2][i & 3]);
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) {
+    const bf16x8 db = acc_to_b(dp, s2);
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) dka[dt] = mfma(tr_read(Qs, rb + 16 * s2 + 4 * h, dt, lane), db, dka[dt]);
+  }
+}
+
+// OCC = waves per SIMD the register budget is cut for: 1 keeps every K/V
+// fragment resident (no spill); 2 doubles the latency hiding but reloads six
+// fragments per slice from scratch.  Chosen at launch (EDL_ATTN_DKDV_OCC).
+template <bool CAUSAL, int OCC>
+__global__ __launch_bounds__(256, OCC) void attn_bwd_dkdv_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
     const bf16_t* __restrict__ dout, const float* __restrict__ lse, const float* __restrict__ delta,
     bf16_t* __restrict__ dk, bf16_t* __restrict__ dv, int S, int H, int KV, float scale_log2, float scale) {
   constexpr int QT = 64;  // queries per staged tile
-  // 2 stages x (Q tile 16 KB + dO tile 16 KB) + 2 x (lse2, delta) x 64 floats
+  // 2 stages x (Q tile 16 KB + dO tile 16 KB) + 2 x (-lse2, delta) x 64 floats
   __shared__ __attribute__((aligned(16))) char smem[2 * 32768 + 2 * 512];
   const int kb = blockIdx.x, hk = blockIdx.y, b = blockIdx.z;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, l31 = lane & 31;
   const int group = H / KV;
   const int64_t qs = (int64_t)H * HD, ks = (int64_t)KV * HD;
   const int mykey = kb * 128 + 32 * w + l31;
-  const bf16_t* krow = k + (int64_t)b * S * ks + (int64_t)mykey * ks + hk * HD;
-  const bf16_t* vrow = v + (int64_t)b * S * ks + (int64_t)mykey * ks + hk * HD;
+  const int64_t krow_off = (int64_t)b * S * ks + (int64_t)min(mykey, S - 1) * ks + hk * HD;
   bf16x8 kf[8], vf[8];
 #pragma unroll
   for (int s = 0; s < 8; ++s) {
-    kf[s] = load_frag(krow, s, h, mykey < S);
-    vf[s] = load_frag(vrow, s, h, mykey < S);
+    kf[s] = load_frag(k + krow_off, s, h);
+    vf[s] = load_frag(v + krow_off, s, h);
   }
   f32x16 dka[4], dva[4];
 #pragma unroll
@@ -329,77 +439,43 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_kernel(
   const int total = per_head * group;
   const int wave_key_lo = kb * 128 + 32 * w;
 
-  u32x4 qreg[4], dreg[4];
-  float lreg = 0.f, dlreg = 0.f;
-  auto fetch = [&](int j) {
+  const int64_t nBHS = (int64_t)gridDim.z * H * S;  // delta = [delta | -lse*log2e]
+  const DmaPlan<QT, 4> plan(qs, w, lane);
+  auto fetch = [&](int j, int st) {
     const int hq = hk * group + j / per_head;
     const int q0 = (qt0 + j % per_head) * QT;
-    load_rows<QT>(qreg, q + (int64_t)b * S * qs + hq * HD, qs, q0, S);
-    load_rows<QT>(dreg, dout + (int64_t)b * S * qs + hq * HD, qs, q0, S);
-    if (threadIdx.x < QT) {
-      const int qq = q0 + threadIdx.x;
-      lreg = qq < S ? lse[((int64_t)b * H + hq) * S + qq] * LOG2E : 0.f;
-      dlreg = qq < S ? delta[((int64_t)b * H + hq) * S + qq] : 0.f;
-    }
-  };
-  auto commit = [&](int st) {
     char* base = smem + st * 32768;
-    store_rows<QT>(base, qreg);
-    store_rows<QT>(base + 16384, dreg);
-    if (threadIdx.x < QT) {
-      float* lf = reinterpret_cast<float*>(smem + 2 * 32768 + st * 512);
-      lf[threadIdx.x] = lreg;
-      lf[QT + threadIdx.x] = dlreg;
-    }
+    const int64_t off = (int64_t)b * S * qs + hq * HD, nbytes = ((int64_t)S * qs - hq * HD) * 2;
+    const uint32_t soff = (uint32_t)(q0 * qs * 2);
+    plan.issue(base, make_rsrc(q + off, nbytes), soff, w);
+    plan.issue(base + 16384, make_rsrc(dout + off, nbytes), soff, w);
+    float* lf = reinterpret_cast<float*>(smem + 2 * 32768 + st * 512);
+    const int64_t row0 = ((int64_t)b * H + hq) * S;
+    if (w == 0) dma_f32x64(lf, make_rsrc(delta + nBHS + row0, (int64_t)S * 4), q0, lane);
+    if (w == 1) dma_f32x64(lf + QT, make_rsrc(delta + row0, (int64_t)S * 4), q0, lane);
   };
-  if (total > 0) {
-    fetch(0);
-    commit(0);
-  }
+  if (total > 0) fetch(0, 0);
+  wait_vm();
   __syncthreads();
+#pragma unroll 1
   for (int j = 0; j < total; ++j) {
-    if (j + 1 < total) fetch(j + 1);
+    if (j + 1 < total) fetch(j + 1, (j + 1) & 1);
     const int st = j & 1;
     const char* Qs = smem + st * 32768;
     const char* Ds = Qs + 16384;
-    const float* L2 = reinterpret_cast<const float*>(smem + 2 * 32768 + st * 512);
+    const float* NL = reinterpret_cast<const float*>(smem + 2 * 32768 + st * 512);
     const int q0 = (qt0 + j % per_head) * QT;
 #pragma unroll
     for (int sub = 0; sub < QT / 32; ++sub) {
       const int qs0 = q0 + 32 * sub;
       if (CAUSAL && qs0 + 31 < wave_key_lo) continue;  // wave-uniform: all masked
-      const int rb = 32 * sub;  // row base inside the staged tile
-      f32x16 sa = f32x16{};
-#pragma unroll
-      for (int s = 0; s < 8; ++s) sa = mfma(row_read(Qs, rb + l31, s, h), kf[s], sa);
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int r = acc_row(i, h);
-        const int qi = qs0 + r;
-        float p = exp2f(sa[i] * scale_log2 - L2[rb + r]);
-        if (qi >= S || mykey >= S || (CAUSAL && mykey > qi)) p = 0.f;
-        sa[i] = p;
-      }
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        const bf16x8 pb = acc_to_b(sa, s2);
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt) dva[dt] = mfma(tr_read(Ds, rb + 16 * s2 + 4 * h, dt, lane), pb, dva[dt]);
-      }
-      f32x16 dp = f32x16{};
-#pragma unroll
-      for (int s = 0; s < 8; ++s) dp = mfma(row_read(Ds, rb + l31, s, h), vf[s], dp);
-#pragma unroll
-      for (int i = 0; i < 16; ++i) dp[i] = sa[i] * (dp[i] - L2[QT + rb + acc_row(i, h)]);
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        const bf16x8 db = acc_to_b(dp, s2);
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt) dka[dt] = mfma(tr_read(Qs, rb + 16 * s2 + 4 * h, dt, lane), db, dka[dt]);
-      }
+      const bool mask = (qs0 + 32 > S) || (wave_key_lo + 32 > S) || (CAUSAL && wave_key_lo + 31 > qs0);
+      if (mask)
+        dkdv_slice<true, CAUSAL>(Qs, Ds, NL, NL + QT, 32 * sub, kf, vf, dka, dva, qs0, mykey, S, scale_log2, lane);
+      else
+        dkdv_slice<false, CAUSAL>(Qs, Ds, NL, NL + QT, 32 * sub, kf, vf, dka, dva, qs0, mykey, S, scale_log2, lane);
     }
-    __syncthreads();
-    if (j + 1 < total) commit((j + 1) & 1);
+    wait_vm();
     __syncthreads();
   }
   if (mykey < S) {
@@ -409,117 +485,106 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_kernel(
 }
 
 // ---------------------------------------------------------------------------
-// backward: dQ (a wave owns QG*32 queries; K/V fragments feed QG MFMAs)
+// backward: dQ (a wave owns 32 queries; the forward's structure with
+// dP^T = V dO^T and dQ^T += K^T dS^T)
 // ---------------------------------------------------------------------------
-template <bool CAUSAL, int QG>
-__global__ __launch_bounds__(256, QG == 1 ? 2 : 1) void attn_bwd_dq_kernel(
+template <bool MASK, bool CAUSAL>
+__device__ __forceinline__ void dq_tile(const char* Ks, const char* Vs, const bf16x8 (&qf)[8], const bf16x8 (&df)[8],
+                                        f32x16 (&dqa)[4], float nl2, float dl, int kv0, int qr, int S, float sl2,
+                                        int lane) {
+  const int h = lane >> 5, l31 = lane & 31;
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    f32x16 st = f32x16{}, dpt = f32x16{};
+#pragma unroll
+    for (int s = 0; s < 8; ++s) st = mfma(row_read(Ks, 32 * t + l31, s, h), qf[s], st);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int s = 0; s < 8; ++s) dpt = mfma(row_read(Vs, 32 * t + l31, s, h), df[s], dpt);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      float p = fast_exp2(__builtin_fmaf(st[i], sl2, nl2));
+      if (MASK) {
+        const int key = kv0 + 32 * t + acc_row(i, h);
+        if (key >= S || (CAUSAL && key > qr)) p = 0.f;
+      }
+      dpt[i] = p * (dpt[i] - dl);  // dS^T
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const bf16x8 db = acc_to_b(dpt, s2);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) dqa[dt] = mfma(tr_read(Ks, 32 * t + 16 * s2 + 4 * h, dt, lane), db, dqa[dt]);
+    }
+    // keep the scheduler from hoisting the next half's 32 LDS reads over this
+    // one (that overlap costs ~100 registers and spills at 2 waves/SIMD)
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+template <bool CAUSAL>
+__global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
     const bf16_t* __restrict__ dout, const float* __restrict__ lse, const float* __restrict__ delta,
     bf16_t* __restrict__ dq, int S, int H, int KV, float scale_log2, float scale) {
-  constexpr int BQ = 128 * QG;
+  constexpr int BQ = 128;
   __shared__ __attribute__((aligned(16))) char smem[2 * 32768];
   const int qb = gridDim.x - 1 - blockIdx.x;
   const int hq = blockIdx.y, b = blockIdx.z, hk = hq / (H / KV);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, l31 = lane & 31;
   const int q0 = qb * BQ;
-  const int wq0 = q0 + 32 * QG * w;
+  const int wq0 = q0 + 32 * w;
   const int64_t qs = (int64_t)H * HD, ks = (int64_t)KV * HD;
   const bf16_t* kp = k + (int64_t)b * S * ks + hk * HD;
   const bf16_t* vp = v + (int64_t)b * S * ks + hk * HD;
-  bf16x8 qf[QG][8], df[QG][8];
-  float l2[QG], dl[QG];
-  f32x16 dqa[QG][4];
-#pragma unroll
-  for (int g = 0; g < QG; ++g) {
-    const int qr = wq0 + 32 * g + l31;
-    const bf16_t* qrow = q + (int64_t)b * S * qs + (int64_t)qr * qs + hq * HD;
-    const bf16_t* drow = dout + (int64_t)b * S * qs + (int64_t)qr * qs + hq * HD;
+  const int qr = wq0 + l31, qc = min(qr, S - 1);
+  bf16x8 qf[8], df[8];
+  {
+    const bf16_t* qrow = q + (int64_t)b * S * qs + (int64_t)qc * qs + hq * HD;
+    const bf16_t* drow = dout + (int64_t)b * S * qs + (int64_t)qc * qs + hq * HD;
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
-      qf[g][s] = load_frag(qrow, s, h, qr < S);
-      df[g][s] = load_frag(drow, s, h, qr < S);
+      qf[s] = load_frag(qrow, s, h);
+      df[s] = load_frag(drow, s, h);
     }
-    l2[g] = qr < S ? lse[((int64_t)b * H + hq) * S + qr] * LOG2E : 0.f;
-    dl[g] = qr < S ? delta[((int64_t)b * H + hq) * S + qr] : 0.f;
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) dqa[g][dt] = f32x16{};
   }
+  const int64_t nBHS = (int64_t)gridDim.z * H * S;  // delta = [delta | -lse*log2e]
+  const float dl = delta[((int64_t)b * H + hq) * S + qc];
+  const float nl2 = delta[nBHS + ((int64_t)b * H + hq) * S + qc];
+  f32x16 dqa[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) dqa[dt] = f32x16{};
   const int kv_end = CAUSAL ? min(S, q0 + BQ) : S;
   const int ntiles = (kv_end + 63) / 64;
-  u32x4 kreg[4], vreg[4];
-  load_rows<64>(kreg, kp, ks, 0, S);
-  load_rows<64>(vreg, vp, ks, 0, S);
-  store_rows<64>(smem, kreg);
-  store_rows<64>(smem + 16384, vreg);
+  const DmaPlan<64, 4> plan(ks, w, lane);
+  const int64_t kv_bytes = ((int64_t)S * ks - hk * HD) * 2;
+  const rsrc_t krs = make_rsrc(kp, kv_bytes), vrs = make_rsrc(vp, kv_bytes);
+  const uint32_t tile_bytes = (uint32_t)(64 * ks * 2);
+  plan.issue(smem, krs, 0, w);
+  plan.issue(smem + 16384, vrs, 0, w);
+  wait_vm();
   __syncthreads();
-  for (int it = 0; it < ntiles; ++it) {
-    const int kv0 = it * 64;
-    if (it + 1 < ntiles) {
-      load_rows<64>(kreg, kp, ks, kv0 + 64, S);
-      load_rows<64>(vreg, vp, ks, kv0 + 64, S);
-    }
-    const char* Ks = smem + (it & 1) * 32768;
-    const char* Vs = Ks + 16384;
-    const bool visible = !(CAUSAL && kv0 > wq0 + 32 * QG - 1);
-    if (visible) {
-      const bool need_mask = (kv0 + 64 > S) || (CAUSAL && kv0 + 63 > wq0);
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        f32x16 st[QG], dpt[QG];
-#pragma unroll
-        for (int g = 0; g < QG; ++g) st[g] = dpt[g] = f32x16{};
-#pragma unroll
-        for (int s = 0; s < 8; ++s) {
-          const bf16x8 a = row_read(Ks, 32 * t + l31, s, h);
-#pragma unroll
-          for (int g = 0; g < QG; ++g) st[g] = mfma(a, qf[g][s], st[g]);
-        }
-#pragma unroll
-        for (int s = 0; s < 8; ++s) {
-          const bf16x8 a = row_read(Vs, 32 * t + l31, s, h);
-#pragma unroll
-          for (int g = 0; g < QG; ++g) dpt[g] = mfma(a, df[g][s], dpt[g]);
-        }
-#pragma unroll
-        for (int g = 0; g < QG; ++g) {
-          const int qr = wq0 + 32 * g + l31;
-#pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            float p = exp2f(st[g][i] * scale_log2 - l2[g]);
-            if (need_mask) {
-              const int key = kv0 + 32 * t + acc_row(i, h);
-              if (key >= S || (CAUSAL && key > qr)) p = 0.f;
-            }
-            dpt[g][i] = p * (dpt[g][i] - dl[g]);  // dS^T
-          }
-        }
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          bf16x8 db[QG];
-#pragma unroll
-          for (int g = 0; g < QG; ++g) db[g] = acc_to_b(dpt[g], s2);
-#pragma unroll
-          for (int dt = 0; dt < 4; ++dt) {
-            const bf16x8 a = tr_read(Ks, 32 * t + 16 * s2 + 4 * h, dt, lane);
-#pragma unroll
-            for (int g = 0; g < QG; ++g) dqa[g][dt] = mfma(a, db[g], dqa[g][dt]);
-          }
-        }
+  const int nfull = CAUSAL ? min(q0, S) / 64 : S / 64;  // see the forward
+  auto run = [&](auto masked, int it0, int it1) {
+    constexpr bool MASK = decltype(masked)::value;
+#pragma unroll 1
+    for (int it = it0; it < it1; ++it) {
+      const int kv0 = it * 64;
+      if (it + 1 < ntiles) {
+        char* nxt = smem + ((it + 1) & 1) * 32768;
+        plan.issue(nxt, krs, (it + 1) * tile_bytes, w);
+        plan.issue(nxt + 16384, vrs, (it + 1) * tile_bytes, w);
       }
+      const char* Ks = smem + (it & 1) * 32768;
+      if (!MASK || !CAUSAL || kv0 <= wq0 + 31)
+        dq_tile<MASK, CAUSAL>(Ks, Ks + 16384, qf, df, dqa, nl2, dl, kv0, qr, S, scale_log2, lane);
+      wait_vm();
+      __syncthreads();
     }
-    __syncthreads();
-    if (it + 1 < ntiles) {
-      char* nxt = smem + ((it + 1) & 1) * 32768;
-      store_rows<64>(nxt, kreg);
-      store_rows<64>(nxt + 16384, vreg);
-    }
-    __syncthreads();
-  }
-#pragma unroll
-  for (int g = 0; g < QG; ++g) {
-    const int qr = wq0 + 32 * g + l31;
-    if (qr < S) store_accT(dq + (int64_t)b * S * qs + (int64_t)qr * qs + hq * HD, dqa[g], scale, h);
-  }
+  };
+  run(std::integral_constant<bool, false>{}, 0, nfull);
+  run(std::integral_constant<bool, true>{}, nfull, ntiles);
+  if (qr < S) store_accT(dq + (int64_t)b * S * qs + (int64_t)qr * qs + hq * HD, dqa, scale, h);
 }
 
 }  // namespace
@@ -529,49 +594,52 @@ extern "C" {
 int edl_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int S, int H, int KV,
                  int D, int causal, float scale, hipStream_t s) {
   if (D != HD || H % KV != 0 || S <= 0) return (int)hipErrorInvalidValue;
-  // QG = 2 (64 rows per wave) halves LDS bytes per MFMA but needs 512 registers
-  // -> 1 wave/SIMD, which measured 2.7x slower (latency exposed); keep QG = 1.
-  constexpr int QG = 1;
-  dim3 grid((S + 128 * QG - 1) / (128 * QG), H, B);
+  // 64 rows per wave (two 32-row groups sharing each K/V fragment) needs 512
+  // registers -> 1 wave/SIMD, which measured 2.7x slower (latency exposed).
+  dim3 grid((S + 127) / 128, H, B);
   const float sl2 = scale * LOG2E;
   if (causal)
-    attn_fwd_kernel<true, QG><<<grid, 256, 0, s>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
+    attn_fwd_kernel<true><<<grid, 256, 0, s>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
                                                    (bf16_t*)o, lse, S, H, KV, sl2);
   else
-    attn_fwd_kernel<false, QG><<<grid, 256, 0, s>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
+    attn_fwd_kernel<false><<<grid, 256, 0, s>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
                                                     (bf16_t*)o, lse, S, H, KV, sl2);
   EDL_LAUNCH_CHECK();
   return 0;
 }
 
-// delta: fp32 [B,H,S] scratch filled here.
+// delta: fp32 [2,B,H,S] scratch filled here (delta, -lse*log2(e)).
 int edl_attn_bwd(const void* q, const void* k, const void* v, const void* o, const void* dout, const float* lse,
                  float* delta, void* dq, void* dk, void* dv, int B, int S, int H, int KV, int D, int causal,
                  float scale, hipStream_t s) {
   if (D != HD || H % KV != 0 || S <= 0) return (int)hipErrorInvalidValue;
   const int64_t nrows = (int64_t)B * S * H;
   attn_bwd_delta_kernel<<<(unsigned)((nrows * 16 + 255) / 256), 256, 0, s>>>((const bf16_t*)o, (const bf16_t*)dout,
-                                                                            delta, S, H, nrows);
+                                                                            lse, delta, S, H, nrows);
   EDL_LAUNCH_CHECK();
   const float sl2 = scale * LOG2E;
-  constexpr int QG = 1;
-  dim3 gkv((S + 127) / 128, KV, B), gq((S + 128 * QG - 1) / (128 * QG), H, B);
+  dim3 gkv((S + 127) / 128, KV, B), gq((S + 127) / 128, H, B);
+  static const int occ = [] {
+    const char* e = getenv("EDL_ATTN_DKDV_OCC");
+    return e && atoi(e) == 2 ? 2 : 1;
+  }();
+#define EDL_DKDV(C, O)                                                                                              \
+  attn_bwd_dkdv_kernel<C, O><<<gkv, 256, 0, s>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,               \
+                                                 (const bf16_t*)dout, lse, delta, (bf16_t*)dk, (bf16_t*)dv, S, H, KV, \
+                                                 sl2, scale)
   if (causal) {
-    attn_bwd_dkdv_kernel<true><<<gkv, 256, 0, s>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
-                                                   (const bf16_t*)dout, lse, delta, (bf16_t*)dk, (bf16_t*)dv, S, H,
-                                                   KV, sl2, scale);
+    if (occ == 2) EDL_DKDV(true, 2); else EDL_DKDV(true, 1);
     EDL_LAUNCH_CHECK();
-    attn_bwd_dq_kernel<true, QG><<<gq, 256, 0, s>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
+    attn_bwd_dq_kernel<true><<<gq, 256, 0, s>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
                                                 (const bf16_t*)dout, lse, delta, (bf16_t*)dq, S, H, KV, sl2, scale);
   } else {
-    attn_bwd_dkdv_kernel<false><<<gkv, 256, 0, s>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
-                                                    (const bf16_t*)dout, lse, delta, (bf16_t*)dk, (bf16_t*)dv, S, H,
-                                                    KV, sl2, scale);
+    if (occ == 2) EDL_DKDV(false, 2); else EDL_DKDV(false, 1);
     EDL_LAUNCH_CHECK();
-    attn_bwd_dq_kernel<false, QG><<<gq, 256, 0, s>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
+    attn_bwd_dq_kernel<false><<<gq, 256, 0, s>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
                                                  (const bf16_t*)dout, lse, delta, (bf16_t*)dq, S, H, KV, sl2, scale);
   }
   EDL_LAUNCH_CHECK();
+#undef EDL_DKDV
   return 0;
 }
 

@@ -51,6 +51,16 @@ def _run(cmd: list[str]) -> None:
         raise RuntimeError(f"build failed: {' '.join(cmd[:6])} ...")
 
 
+def _check_resolves(lib: str) -> None:
+    """Fail the build (not the first GPU run) if a kernel's host launch stub is
+    missing: clang's host pass can silently drop stubs of kernel templates whose
+    bodies use device-only builtins."""
+    r = subprocess.run(["nm", "-D", "--undefined-only", lib], capture_output=True, text=True)
+    missing = [ln.split()[-1] for ln in r.stdout.splitlines() if "__device_stub__" in ln]
+    if missing:
+        raise RuntimeError(f"{os.path.basename(lib)}: undefined kernel launch stubs: {missing}")
+
+
 def build_kernels(force: bool = False, verbose: bool = False) -> str:
     srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
     deps = srcs + glob.glob(os.path.join(CSRC, "kernels", "*.h"))
@@ -69,6 +79,7 @@ def build_kernels(force: bool = False, verbose: bool = False) -> str:
             objs.append(o)
         tmp = KERNELS_SO + ".tmp"
         _run([_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs)
+        _check_resolves(tmp)
         os.replace(tmp, KERNELS_SO)
     return KERNELS_SO
 

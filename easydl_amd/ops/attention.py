@@ -47,7 +47,7 @@ class _FlashAttnFn(torch.autograd.Function):
         KV = km.shape[2]
         dom = _bshd(do)
         dq, dk, dv = torch.empty_like(qm), torch.empty_like(km), torch.empty_like(vm)
-        delta = torch.empty(B, H, S, dtype=torch.float32, device=qm.device)
+        delta = torch.empty(2, B, H, S, dtype=torch.float32, device=qm.device)  # (delta, -lse*log2e)
         kn.check("edl_attn_bwd", qm.data_ptr(), km.data_ptr(), vm.data_ptr(), o.data_ptr(), dom.data_ptr(),
                  lse.data_ptr(), delta.data_ptr(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), B, S, H, KV, D,
                  1 if ctx.causal else 0, ctx.scale, _native.stream_of(qm))

@@ -22,7 +22,8 @@ def _err(a, b):
 
 
 @pytest.mark.parametrize("B,S,H,KV,causal", [(1, 128, 4, 4, True), (2, 256, 8, 2, True), (1, 200, 4, 1, True),
-                                             (1, 384, 8, 8, False), (1, 1024, 32, 8, True)])
+                                             (1, 384, 8, 8, False), (2, 200, 4, 2, False), (1, 1024, 32, 8, True),
+                                             (1, 2112, 8, 2, True)])
 def test_flash_attention_fwd_bwd(cuda, B, S, H, KV, causal):
     q, k, v = _mk(B, S, H, KV, cuda, S + H)
     q1, k1, v1 = (t.detach().clone().requires_grad_() for t in (q, k, v))
