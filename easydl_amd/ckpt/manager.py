@@ -32,6 +32,7 @@ import glob
 import json
 import logging
 import os
+import re
 import threading
 import time
 
@@ -175,8 +176,20 @@ class CheckpointManager:
         self.stats = {"snapshots": 0, "d2h_bytes": 0}
 
     # -- naming --------------------------------------------------------------
-    def seg_name(self, world: int, shard: int) -> str:
-        return f"/edl-{self.job}-w{world}-s{shard}"
+    # ``tag`` separates independent state sets of one job: with tensor
+    # parallelism every TP rank's parameter shard is its own set ("-t<i>of<T>"),
+    # each replicated over (and sharded across) that rank's DP group.
+    def seg_name(self, world: int, shard: int, tag: str = "") -> str:
+        return f"/edl-{self.job}{tag}-w{world}-s{shard}"
+
+    @staticmethod
+    def _tag(trainer) -> str:
+        return getattr(trainer, "ckpt_tag", "") or ""
+
+    @staticmethod
+    def _comm(trainer):
+        """The communicator the state is replicated over (DP group under TP)."""
+        return getattr(trainer, "dp_comm", None) or trainer.comm
 
     @staticmethod
     def state_of(trainer) -> list[tuple[str, torch.Tensor]]:
@@ -197,12 +210,12 @@ class CheckpointManager:
                 if mk in opt:
                     g.data.copy_(opt[mk])
 
-    def _segment(self, world, shard, need_bytes, pin=True) -> ShmSegment:
-        key = (world, shard)
+    def _segment(self, world, shard, need_bytes, pin=True, tag: str = "") -> ShmSegment:
+        key = (world, shard, tag)
         if self._seg is None or self._seg_key != key or self._seg.slot_bytes < need_bytes:
             if self._seg is not None:
                 self._seg.close()
-            self._seg = ShmSegment(self.seg_name(world, shard), need_bytes, create=True, pin=self.pin and pin)
+            self._seg = ShmSegment(self.seg_name(world, shard, tag), need_bytes, create=True, pin=self.pin and pin)
             self._seg_key = key
         return self._seg
 
@@ -213,16 +226,17 @@ class CheckpointManager:
         self.snapshot(trainer)
 
     def snapshot(self, trainer) -> None:
-        comm = trainer.comm
+        comm = self._comm(trainer)
+        tag = self._tag(trainer)
         world = comm.world_size if self.sharded else 1
         shard = comm.rank if self.sharded else 0
         if not self.sharded and comm.rank != 0:
             return
         state = self.state_of(trainer)
         layout, cs_off = shard_layout(state, shard, world)
-        seg = self._segment(world, shard, cs_off + 8, pin=state[0][1].is_cuda)
+        seg = self._segment(world, shard, cs_off + 8, pin=state[0][1].is_cuda, tag=tag)
         meta = {"format": FORMAT, "step": trainer.step, "opt_step": trainer.opt.step_count, "world": world,
-                "shard": shard, "epoch": comm.epoch,
+                "shard": shard, "epoch": comm.epoch, "tag": tag,
                 "t": [[d["name"], d["dtype"], d["numel"], d["lo"], d["hi"], d["offset"]] for d in layout]}
         dev = state[0][1].device
         self.wait()  # at most one snapshot in flight
@@ -292,17 +306,17 @@ class CheckpointManager:
             self._ticket = None
 
     # -- restore -------------------------------------------------------------
-    def find_latest(self) -> tuple[int, int, list[dict]] | None:
-        """Newest step for which every shard of some world size has a committed slot."""
+    def find_latest(self, tag: str = "", max_step: int | None = None) -> tuple[int, int, list[dict]] | None:
+        """Newest step (<= ``max_step``) for which every shard of some world size has a committed slot."""
         best = None
         worlds = {}
-        for path in glob.glob(f"/dev/shm/edl-{self.job}-w*-s*"):
+        pat = re.compile(rf"^edl-{re.escape(self.job + tag)}-w(\d+)-s(\d+)$")
+        for path in glob.glob(f"/dev/shm/edl-{self.job}{tag}-w*-s*"):
             base = os.path.basename(path)
-            try:
-                w = int(base.rsplit("-w", 1)[1].split("-s")[0])
-                s = int(base.rsplit("-s", 1)[1])
-            except (IndexError, ValueError):
+            mt = pat.match(base)
+            if mt is None:
                 continue
+            w, s = int(mt.group(1)), int(mt.group(2))
             worlds.setdefault(w, {})[s] = "/" + base
         for w, shards in worlds.items():
             if len(shards) != w:
@@ -315,14 +329,22 @@ class CheckpointManager:
             common = set(per[0])
             for p in per[1:]:
                 common &= set(p)
+            if max_step is not None:
+                common = {c for c in common if c <= max_step}
             if common:
                 st = max(common)
                 if best is None or st > best[1]:
                     best = (w, st, [p[st] for p in per])
         return best
 
-    def restore_latest(self, trainer) -> str | None:
-        found = self.find_latest()
+    def latest_step(self, trainer) -> int:
+        """Newest restorable in-memory step of this trainer's state set (-1: none)."""
+        found = self.find_latest(self._tag(trainer))
+        return -1 if found is None else found[1]
+
+    def restore_latest(self, trainer, max_step: int | None = None) -> str | None:
+        tag = self._tag(trainer)
+        found = self.find_latest(tag, max_step)
         if found is None:
             if self.persist_dir:
                 return self.load_dir_latest(trainer)
@@ -331,7 +353,7 @@ class CheckpointManager:
         state = dict(self.state_of(trainer))
         dev = next(iter(state.values())).device
         for s, info in enumerate(infos):
-            seg = ShmSegment(self.seg_name(world, s), create=False)
+            seg = ShmSegment(self.seg_name(world, s, tag), create=False)
             try:
                 _load_shard(lambda off, nb: seg.view(info["slot"], off, nb), info["meta"]["t"], state, dev,
                             info["checksum"], f"shm shard {s} of step {step}", seg=seg, slot=info["slot"])
@@ -341,7 +363,7 @@ class CheckpointManager:
         meta = infos[0]["meta"]
         trainer.step = int(meta["step"])
         trainer.opt.step_count = int(meta["opt_step"])
-        return f"shm:w{world}:step{step}"
+        return f"shm{tag}:w{world}:step{step}"
 
     # -- disk persistence (format v1) ----------------------------------------------
     def _persist_async(self, step: int) -> None:
@@ -357,33 +379,35 @@ class CheckpointManager:
         if info is None:
             return
         m = info["meta"]
+        tag = m.get("tag", "")
         d = os.path.join(self.persist_dir, f"step-{step}")
         os.makedirs(d, exist_ok=True)
-        fname = f"shard-{m['shard']}-of-{m['world']}.bin"
+        fname = f"shard{tag}-{m['shard']}-of-{m['world']}.bin"
         with open(os.path.join(d, fname + ".tmp"), "wb") as f:
             f.write(seg.view(info["slot"], 0, info["nbytes"]).tobytes())
         os.replace(os.path.join(d, fname + ".tmp"), os.path.join(d, fname))
         shard_manifest = {"file": fname, "checksum": info["checksum"], "nbytes": info["nbytes"],
                           "tensors": m["t"], "shard": m["shard"]}
-        with open(os.path.join(d, f"shard-{m['shard']}.json"), "w") as f:
+        with open(os.path.join(d, f"shard{tag}-{m['shard']}.json"), "w") as f:
             json.dump(shard_manifest, f)
         if m["shard"] == 0:
-            with open(os.path.join(d, "manifest.json"), "w") as f:
+            with open(os.path.join(d, f"manifest{tag}.json"), "w") as f:
                 json.dump({"format": FORMAT, "step": step, "opt_step": m["opt_step"], "world": m["world"],
                            "epoch": m["epoch"], "time": time.time()}, f)
 
     def load_dir_latest(self, trainer) -> str | None:
         dirs = sorted(glob.glob(os.path.join(self.persist_dir or "", "step-*")),
                       key=lambda p: int(p.rsplit("-", 1)[1]))
+        tag = self._tag(trainer)
         for d in reversed(dirs):
-            mf = os.path.join(d, "manifest.json")
+            mf = os.path.join(d, f"manifest{tag}.json")
             if not os.path.exists(mf):
                 continue
             m = json.load(open(mf))
-            shards = [os.path.join(d, f"shard-{s}.json") for s in range(m["world"])]
+            shards = [os.path.join(d, f"shard{tag}-{s}.json") for s in range(m["world"])]
             if not all(os.path.exists(p) for p in shards):
                 continue
-            load_dir(d, trainer)
+            load_dir(d, trainer, tag)
             return f"disk:{d}"
         return None
 
@@ -399,13 +423,13 @@ class CheckpointManager:
             self._engine = None
 
 
-def load_dir(d: str, trainer) -> None:
+def load_dir(d: str, trainer, tag: str = "") -> None:
     """Cold resume from a format-v1 directory (any world size -> any world size)."""
-    m = json.load(open(os.path.join(d, "manifest.json")))
+    m = json.load(open(os.path.join(d, f"manifest{tag}.json")))
     state = dict(CheckpointManager.state_of(trainer))
     dev = next(iter(state.values())).device
     for s in range(m["world"]):
-        sm = json.load(open(os.path.join(d, f"shard-{s}.json")))
+        sm = json.load(open(os.path.join(d, f"shard{tag}-{s}.json")))
         raw = np.memmap(os.path.join(d, sm["file"]), dtype=np.uint8, mode="r")
         _load_shard(lambda off, nb: np.array(raw[off:off + nb]), sm["tensors"], state, dev, sm["checksum"],
                     sm["file"])
@@ -463,7 +487,10 @@ def _load_shard(read, table, state, dev, expect: int, what: str, seg=None, slot=
 
 def unlink_job_segments(job: str) -> int:
     n = 0
-    for path in glob.glob(f"/dev/shm/edl-{job}-w*-s*"):
+    pat = re.compile(rf"^edl-{re.escape(job)}(-t\d+of\d+)?-w\d+-s\d+$")
+    for path in glob.glob(f"/dev/shm/edl-{job}-*"):
+        if not pat.match(os.path.basename(path)):
+            continue
         try:
             os.unlink(path)
             n += 1

@@ -131,6 +131,8 @@ def main(argv=None):
     ap.add_argument("--join-window", type=float, default=0.5)
     ap.add_argument("--hb-timeout", type=float, default=15.0)
     ap.add_argument("--policy", default="shrink")
+    ap.add_argument("--granule", type=int, default=int(os.environ.get("EDL_TP", 1)),
+                    help="world sizes are multiples of this (tensor-parallel degree)")
     ap.add_argument("--run-dir", default=os.environ.get("EDL_RUN_DIR"))
     ap.add_argument("--job-spec", default=None, help="ElasticJob JSON/YAML: enables the Brain plan loop")
     ap.add_argument("--brain-url", default=os.environ.get("EDL_BRAIN_URL"))
@@ -140,6 +142,7 @@ def main(argv=None):
     a = ap.parse_args(argv)
     logging.basicConfig(level=logging.INFO, format="%(asctime)s [master] %(message)s")
     cfg = RendezvousConfig(min_nodes=a.min, max_nodes=a.max, initial_nodes=a.initial, join_window_s=a.join_window,
+                           granule=a.granule,
                            heartbeat_timeout_s=a.hb_timeout, policy=a.policy)
     planner = None
     if a.job_spec:

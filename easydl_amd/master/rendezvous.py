@@ -53,6 +53,11 @@ class RendezvousConfig:
     heartbeat_timeout_s: float = 15.0
     policy: str = "shrink"          # on failure: "shrink" (continue with survivors) or "replace" (wait)
     replace_wait_s: float = 60.0    # "replace": how long to wait for a replacement before shrinking
+    granule: int = 1                # world sizes are multiples of this (the TP degree)
+
+
+class JobFinished(Exception):
+    """Training finished while this node waited for an epoch."""
 
 
 class RendezvousManager:
@@ -141,12 +146,14 @@ class RendezvousManager:
                 if e == cur:
                     self._broken_ts = now
         max_n = self.cfg.max_nodes if self.target_nodes is None else min(self.cfg.max_nodes, self.target_nodes)
+        g = max(1, self.cfg.granule)
+        max_n = max_n // g * g
         waiting = [n for n in alive if n not in members]
         survivors = [m for m in members if m in alive]
         reason = None
         if cur == 0:
             want = max(self.cfg.min_nodes, min(self.cfg.initial_nodes, max_n))
-            if len(alive) >= self.cfg.min_nodes:
+            if len(alive) // g * g >= max(self.cfg.min_nodes, g):
                 if self._first_wait_ts is None:
                     self._first_wait_ts = now
                 waited = now - self._first_wait_ts
@@ -156,14 +163,14 @@ class RendezvousManager:
         elif broken:
             replace_ok = (self.cfg.policy == "shrink" or len(survivors) + len(waiting) >= len(members)
                           or (self._broken_ts is not None and now - self._broken_ts >= self.cfg.replace_wait_s))
-            if replace_ok and len(survivors) + len(waiting) >= self.cfg.min_nodes:
+            if replace_ok and (len(survivors) + len(waiting)) // g * g >= max(self.cfg.min_nodes, g):
                 reason = "failure"
         elif any(m in leaving for m in members):
-            if len(survivors) + len(waiting) >= self.cfg.min_nodes:
+            if (len(survivors) + len(waiting)) // g * g >= max(self.cfg.min_nodes, g):
                 reason = "leave"
         elif len(members) > max_n:
             reason = "scale_down"
-        elif waiting and len(members) < max_n:
+        elif waiting and len(members) < max_n and min(max_n, len(members) + len(waiting)) // g * g > len(members):
             if self._first_wait_ts is None:
                 self._first_wait_ts = now
             if len(members) + len(waiting) >= max_n or now - self._first_wait_ts >= self.cfg.join_window_s:
@@ -175,6 +182,9 @@ class RendezvousManager:
         new_members = (survivors + waiting)[:max_n]
         if reason == "scale_down":
             new_members = survivors[:max_n]
+        if g > 1:
+            new_members = self._arrange(members, new_members if reason == "scale_down" else survivors + waiting,
+                                        min(max_n, len(new_members)) // g * g)
         e = cur + 1
         self.kv.set(f"rdzv/assign/{e}", json.dumps(
             {"members": new_members, "world": len(new_members), "reason": reason, "ts": now, "prev": cur}))
@@ -184,6 +194,28 @@ class RendezvousManager:
         self._event("epoch_formed", epoch=e, world=len(new_members), reason=reason, members=new_members)
         log.info("rendezvous: epoch %d formed (%s): %s", e, reason, new_members)
         return e
+
+    def _arrange(self, prev: list[str], cand: list[str], n: int) -> list[str]:
+        """TP-aware rank order for ``n`` of the candidates (survivors first).
+
+        A survivor keeps its TP rank (``rank % granule``) whenever a slot with
+        that TP rank is free, so it still holds the right parameter shard and
+        only the processes that change shard (or are new) need state."""
+        g = self.cfg.granule
+        slots: list[str | None] = [None] * n
+        rest = []
+        for node in cand:
+            placed = False
+            if node in prev:
+                for sl in range(prev.index(node) % g, n, g):
+                    if slots[sl] is None:
+                        slots[sl] = node
+                        placed = True
+                        break
+            if not placed:
+                rest.append(node)
+        it = iter(rest)
+        return [sl if sl is not None else next(it) for sl in slots]
 
     # -- background loop ------------------------------------------------------
     def start(self, period_s: float = 0.02) -> None:
@@ -256,9 +288,16 @@ class RendezvousClient:
         return self.kv.exists(f"rdzv/abort/{epoch}")
 
     def wait_assignment(self, after_epoch: int = 0, timeout_s: float = 600.0, poll_s: float = 0.005) -> Assignment:
-        """Block until an epoch > after_epoch that includes this node is formed."""
+        """Block until an epoch > after_epoch that includes this node is formed.
+
+        Raises :class:`JobFinished` when training completed while this node was
+        waiting (e.g. a spare worker that a TP-granular world could not use)."""
         t_end = time.monotonic() + timeout_s
+        n = 0
         while time.monotonic() < t_end:
+            n += 1
+            if n % 20 == 1 and (self.kv.exists("train/done") or self.kv.exists("job/done")):
+                raise JobFinished(self.node_id)
             e = self.latest_epoch()
             if e > after_epoch and not self.aborted(e):
                 a = self.kv.get(f"rdzv/assign/{e}")

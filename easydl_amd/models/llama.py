@@ -103,14 +103,14 @@ def _param(shape, std, device, dtype, init=True):
 def attention(q, k, v, causal=True):
     """q [B,H,S,D], k/v [B,KV,S,D] -> [B,H,S,D] (GQA).
 
-    GPU: ``EDL_ATTN=hip`` selects the hand-written kernels of
-    csrc/kernels/attention.hip, otherwise PyTorch SDPA (AOTriton flash) — the
-    default while it is the faster of the two on the 8k-context shape
-    (profiles/r01_attention_kernels.md)."""
+    GPU: the hand-written kernels of csrc/kernels/attention.hip (default;
+    1.4x / 1.8x faster than PyTorch SDPA's AOTriton forward / backward at the
+    8k-context shape, profiles/r01_attention_kernels.md); ``EDL_ATTN=sdpa``
+    selects SDPA for A/B runs."""
     H, KV = q.shape[1], k.shape[1]
     if q.is_cuda:
         import os
-        if os.environ.get("EDL_ATTN", "sdpa") == "hip":
+        if os.environ.get("EDL_ATTN", "hip") == "hip":
             from easydl_amd.ops.attention import flash_attention
             return flash_attention(q, k, v, causal=causal)
         return F.scaled_dot_product_attention(q, k, v, is_causal=causal, enable_gqa=(H != KV))

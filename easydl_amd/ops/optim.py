@@ -22,13 +22,29 @@ def _gdtype(g: torch.Tensor) -> int:
     raise TypeError(f"unsupported gradient dtype {g.dtype}")
 
 
-def grad_clip_scale(grads: list[torch.Tensor], max_norm: float, pre_scale: float = 1.0) -> torch.Tensor:
+def grad_clip_scale(grads: list[torch.Tensor], max_norm: float, pre_scale: float = 1.0, weights=None,
+                    reduce=None) -> torch.Tensor:
     """Return a device tensor [coef, norm, nonfinite] for flat gradient buffers.
 
     ``norm`` is the L2 norm of ``pre_scale * concat(grads)``; ``coef`` =
     ``pre_scale * min(1, max_norm / norm)`` (``max_norm <= 0`` disables clipping).
+    Model-parallel form: ``weights`` scales each buffer's sum of squares (1/tp
+    for buffers replicated over the TP group) and ``reduce`` all-reduces the
+    total over the group, so every rank clips by the global norm.
     """
     dev = grads[0].device
+    if weights is not None or reduce is not None:
+        weights = weights or [1.0] * len(grads)
+        terms = [grad_clip_scale([g], 0.0, 1.0)[1].double().pow(2) * w for g, w in zip(grads, weights)]
+        total = torch.stack(terms).sum().reshape(1)
+        if reduce is not None:
+            reduce(total)
+        norm = (total.sqrt() * pre_scale).float().reshape(())
+        bad = (~torch.isfinite(norm)).float()
+        coef = torch.tensor(pre_scale, dtype=torch.float32, device=dev)
+        if max_norm > 0:
+            coef = torch.where(norm > max_norm, pre_scale * (max_norm / (norm + 1e-6)), coef)
+        return torch.stack([coef, norm, bad]).float()
     if _native.use_hip(grads[0]):
         k = _native.kernels()
         nparts = [k("edl_sumsq_nparts", g.numel()) for g in grads]

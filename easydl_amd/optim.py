@@ -45,6 +45,9 @@ class FlatAdamW:
         self.schedule = schedule
         self.step_count = 0
         self.last_stats = None  # device tensor [coef, norm, nonfinite]
+        # model parallelism: per-group sum-of-squares weights + group all-reduce
+        self.norm_weights = None
+        self.norm_reduce = None
         self.state = []
         for g in flat.groups:
             if weight_decay is not None and g.name.startswith("decay"):
@@ -64,7 +67,7 @@ class FlatAdamW:
     def step(self, pre_scale: float = 1.0) -> torch.Tensor:
         """Apply one update; ``pre_scale`` multiplies the (summed) gradients, e.g. 1/world."""
         grads = [g.grad for g in self.flat.groups]
-        stats = grad_clip_scale(grads, self.max_grad_norm, pre_scale)
+        stats = grad_clip_scale(grads, self.max_grad_norm, pre_scale, self.norm_weights, self.norm_reduce)
         self.step_count += 1
         lr = self.schedule(self.step_count) if self.schedule else self.lr
         for g, st in zip(self.flat.groups, self.state):
@@ -97,6 +100,8 @@ class FlatSGD:
                  max_grad_norm: float = 0.0, schedule: LRSchedule | None = None):
         self.flat = flat
         self.lr, self.momentum, self.max_grad_norm, self.schedule = lr, momentum, max_grad_norm, schedule
+        self.norm_weights = None
+        self.norm_reduce = None
         self.step_count = 0
         self.state = []
         for g in flat.groups:
@@ -111,7 +116,7 @@ class FlatSGD:
     @torch.no_grad()
     def step(self, pre_scale: float = 1.0):
         grads = [g.grad for g in self.flat.groups]
-        stats = grad_clip_scale(grads, self.max_grad_norm, pre_scale)
+        stats = grad_clip_scale(grads, self.max_grad_norm, pre_scale, self.norm_weights, self.norm_reduce)
         self.step_count += 1
         lr = self.schedule(self.step_count) if self.schedule else self.lr
         for g, st in zip(self.flat.groups, self.state):

@@ -38,17 +38,21 @@ def _td(s: float) -> datetime.timedelta:
 class Communicator:
     def __init__(self, store: dist.Store, rank: int, world_size: int, epoch: int, *, device: torch.device,
                  job: str = "job", timeout_s: float = 120.0, control_timeout_s: float = 30.0,
-                 high_priority: bool = True):
+                 high_priority: bool = True, tag: str = "", data: bool = True):
         self.rank = rank
         self.world_size = world_size
         self.epoch = epoch
         self.device = torch.device(device)
+        self.tag = tag
         self._aborted = False
         self._lock = threading.Lock()
         t0 = time.perf_counter()
-        base = dist.PrefixStore(f"edl/{job}/e{epoch}", store)
+        base = dist.PrefixStore(f"edl/{job}/e{epoch}" + (f"/{tag}" if tag else ""), store)
         self.ctrl = dist.ProcessGroupGloo(dist.PrefixStore("ctrl", base), rank, world_size, _td(control_timeout_s))
-        if self.device.type == "cuda":
+        if not data:
+            self.data = None
+            self.backend = "none"
+        elif self.device.type == "cuda":
             opts = dist.ProcessGroupNCCL.Options()
             opts.is_high_priority_stream = high_priority
             opts._timeout = _td(timeout_s)
@@ -63,10 +67,11 @@ class Communicator:
     def warmup(self) -> float:
         """Force lazy communicator creation now (so it is not hidden in step 1)."""
         t0 = time.perf_counter()
-        x = torch.zeros(1, device=self.device)
-        self.data.allreduce([x]).wait()
-        if self.device.type == "cuda":
-            torch.cuda.synchronize(self.device)
+        if self.data is not None:
+            x = torch.zeros(1, device=self.device)
+            self.data.allreduce([x]).wait()
+            if self.device.type == "cuda":
+                torch.cuda.synchronize(self.device)
         self.ctrl.allreduce([torch.zeros(1)]).wait()
         return time.perf_counter() - t0
 
@@ -94,6 +99,8 @@ class Communicator:
         if self._aborted:
             return
         for pg in (self.data, self.ctrl):
+            if pg is None:
+                continue
             try:
                 if hasattr(pg, "shutdown"):
                     pg.shutdown()
@@ -166,6 +173,73 @@ class Communicator:
 
     def barrier(self) -> None:
         self._wait(self.ctrl.barrier())
+
+
+class MeshComm:
+    """One rank's communicators for a DP x TP epoch (Megatron ordering: the TP
+    group is ``tp`` consecutive ranks, the DP group the ranks with equal
+    ``rank % tp``).
+
+    ``world`` carries only the control plane (agreement, barriers); gradients
+    are all-reduced over ``dp``, activations over ``tp``.  On one node every
+    group is fully xGMI-connected, so consecutive-rank TP needs no topology
+    search; across nodes it keeps TP traffic inside a node.  ``abort()`` aborts
+    all three so no rank stays blocked in any of them.
+    """
+
+    def __init__(self, world, tp, dp, tp_size: int):
+        self.world, self.tp, self.dp = world, tp, dp
+        self.tp_size = tp_size
+        self.rank, self.world_size, self.epoch = world.rank, world.world_size, world.epoch
+        self.device = world.device
+        self.backend = getattr(dp, "backend", "local")
+        self.init_s = sum(getattr(c, "init_s", 0.0) for c in (world, tp, dp))
+
+    @property
+    def tp_rank(self) -> int:
+        return self.rank % self.tp_size
+
+    @property
+    def dp_rank(self) -> int:
+        return self.rank // self.tp_size
+
+    @property
+    def aborted(self) -> bool:
+        return any(c.aborted for c in (self.world, self.tp, self.dp))
+
+    def abort(self) -> None:
+        for c in (self.dp, self.tp, self.world):
+            c.abort()
+
+    def shutdown(self) -> None:
+        for c in (self.dp, self.tp, self.world):
+            c.shutdown()
+
+    def warmup(self) -> float:
+        return sum(c.warmup() for c in (self.world, self.tp, self.dp))
+
+    def ctrl_all_reduce(self, values, op=dist.ReduceOp.SUM):
+        return self.world.ctrl_all_reduce(values, op)
+
+    def ctrl_broadcast(self, values, src: int):
+        return self.world.ctrl_broadcast(values, src)
+
+    def barrier(self) -> None:
+        self.world.barrier()
+
+
+def build_mesh(store, rank: int, world: int, epoch: int, tp: int, *, device, job: str, **kw) -> MeshComm:
+    """World control plane + this rank's TP and DP groups for one epoch."""
+    if world % tp:
+        raise ValueError(f"world {world} is not a multiple of tp={tp}")
+    dp_rank, tp_rank = divmod(rank, tp)
+    w = Communicator(store, rank, world, epoch, device=device, job=job, data=False, **kw)
+    tpc = (Communicator(store, tp_rank, tp, epoch, device=device, job=job, tag=f"tp{dp_rank}", **kw)
+           if tp > 1 else LocalCommunicator(device, epoch))
+    dpn = world // tp
+    dpc = (Communicator(store, dp_rank, dpn, epoch, device=device, job=job, tag=f"dp{tp_rank}", **kw)
+           if dpn > 1 else LocalCommunicator(device, epoch))
+    return MeshComm(w, tpc, dpc, tp)
 
 
 class LocalCommunicator:

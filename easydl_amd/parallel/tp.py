@@ -33,13 +33,23 @@ from easydl_amd.ops import fused, norms
 
 
 class TPGroup:
-    """TP ranks of one model replica (wraps an epoch Communicator)."""
+    """TP ranks of one model replica (wraps an epoch Communicator).
 
-    def __init__(self, comm, sequence_parallel: bool = False):
+    Under the elastic trainer the group outlives epochs: the model is built
+    once against it and :meth:`rebind` swaps in each new epoch's TP
+    communicator (same size; the rank may change, with the state re-synced).
+    """
+
+    def __init__(self, comm=None, sequence_parallel: bool = False, size: int | None = None, rank: int = 0):
         self.comm = comm
-        self.rank = comm.rank
-        self.size = comm.world_size
+        self.rank = comm.rank if comm is not None else rank
+        self.size = comm.world_size if comm is not None else int(size or 1)
         self.sequence_parallel = sequence_parallel
+
+    def rebind(self, comm) -> None:
+        if comm.world_size != self.size:
+            raise ValueError(f"TP size is fixed at {self.size}, got a group of {comm.world_size}")
+        self.comm, self.rank = comm, comm.rank
 
     def all_reduce(self, x: torch.Tensor) -> torch.Tensor:
         if self.size == 1:
@@ -167,7 +177,6 @@ class LlamaTP(nn.Module):
             raise ValueError(f"config not divisible by tp={tp}")
         self.cfg, self.g = cfg, g
         self.vshard = cfg.vocab_size // tp
-        self.vstart = g.rank * self.vshard
         d = cfg.dim
         self.embed = _param((self.vshard, d), cfg.init_std, device, dtype)
         self.layers = nn.ModuleList()
@@ -180,8 +189,17 @@ class LlamaTP(nn.Module):
         self.norm = _param((d,), 0, device, dtype)
         self.lm_head = _param((self.vshard, d), cfg.init_std, device, dtype)
         self._rope = {}
+        # norms are replicated on every TP rank (identical values and gradients):
+        # the grad-norm counts them once (ElasticTrainer / FlatAdamW weights)
+        for n, p in self.named_parameters():
+            if p.ndim < 2:
+                p._tp_replicated = True
 
     rope = Llama.rope
+
+    @property
+    def vstart(self) -> int:  # follows the group's current rank (elastic re-ranking)
+        return self.g.rank * self.vshard
 
     def forward(self, ids, labels=None):
         B, S = ids.shape

@@ -32,10 +32,10 @@ import time
 import torch
 import torch.distributed as dist
 
-from easydl_amd.master.rendezvous import RendezvousClient, RendezvousConfig, RendezvousManager
+from easydl_amd.master.rendezvous import JobFinished, RendezvousClient, RendezvousConfig, RendezvousManager
 from easydl_amd.master.store import KV, make_tcp_store
 from easydl_amd.optim import FlatAdamW, FlatSGD, LRSchedule
-from easydl_amd.parallel.comm import CommAborted, Communicator, LocalCommunicator
+from easydl_amd.parallel.comm import CommAborted, Communicator, LocalCommunicator, build_mesh
 from easydl_amd.parallel.ddp import ElasticDDP
 from easydl_amd.parallel.flat import FlatParams
 from easydl_amd.trainer.context import TrainerContext
@@ -57,7 +57,7 @@ class ElasticTrainer:
                  micro_batch: int = 1, device=None, dtype=torch.bfloat16, bucket_mb: float | None = None,
                  grad_dtype=None, ctx: TrainerContext | None = None, seed: int = 1234, schedule: LRSchedule | None = None,
                  rdzv_config: RendezvousConfig | None = None, checkpoint=None, log_every: int = 0,
-                 store=None):
+                 store=None, tp: int | None = None):
         self.ctx = ctx or TrainerContext.from_env()
         if device is None:
             if torch.cuda.is_available():
@@ -70,18 +70,25 @@ class ElasticTrainer:
         self.resources = apply_plan(self.ctx, self.device)  # Brain CU mask / HBM cap
         self.events = EventLog(os.path.join(self.ctx.run_dir, f"events-{self.ctx.role}{self.ctx.index}.jsonl"),
                                proc=f"{self.ctx.role}{self.ctx.index}")
-        torch.manual_seed(seed)
-        self.model = model_fn(self.device)
-        self.flat = FlatParams(self.model, weight_decay=weight_decay, grad_dtype=grad_dtype)
-        if optimizer == "adamw":
-            self.opt = FlatAdamW(self.flat, lr=lr, betas=betas, weight_decay=weight_decay,
-                                 max_grad_norm=max_grad_norm, schedule=schedule)
-        elif optimizer == "sgd":
-            self.opt = FlatSGD(self.flat, lr=lr, momentum=momentum, weight_decay=weight_decay,
-                               max_grad_norm=max_grad_norm, schedule=schedule)
-        else:
+        if optimizer not in ("adamw", "sgd"):
             raise ValueError(f"unknown optimizer {optimizer}")
-        self.ddp = ElasticDDP(self.flat, None, bucket_mb=bucket_mb)
+        self._model_fn, self._seed = model_fn, seed
+        self._opt_args = dict(optimizer=optimizer, lr=lr, weight_decay=weight_decay, betas=betas, momentum=momentum,
+                              max_grad_norm=max_grad_norm, schedule=schedule, grad_dtype=grad_dtype,
+                              bucket_mb=bucket_mb)
+        # tensor parallelism (Megatron layout inside each DP replica): model_fn(device, tp_group);
+        # the model is built at the first epoch, once this process's TP rank is known
+        self.tp = int(tp if tp is not None else os.environ.get("EDL_TP", 1))
+        self.tp_group = None
+        self.held_tp = None          # TP rank whose parameter shard this process holds
+        self.ckpt_tag = ""
+        self.dp_comm = None
+        self.model = self.flat = self.opt = self.ddp = None
+        if self.tp == 1:
+            self._build_model(0)
+        else:
+            from easydl_amd.parallel.tp import TPGroup
+            self.tp_group = TPGroup(size=self.tp)
         self.global_batch = global_batch
         self.micro_batch = micro_batch
         self.step = 0                # committed optimizer steps
@@ -103,6 +110,33 @@ class ElasticTrainer:
         self.plan_version = 0
 
     # ------------------------------------------------------------------ setup
+    def _build_model(self, tp_rank: int) -> None:
+        a = self._opt_args
+        torch.manual_seed(self._seed + 1009 * tp_rank)  # DP replicas of a shard initialise identically
+        if self.tp > 1:
+            self.tp_group.rank = tp_rank
+            self.model = self._model_fn(self.device, self.tp_group)
+        else:
+            self.model = self._model_fn(self.device)
+        self.flat = FlatParams(self.model, weight_decay=a["weight_decay"], grad_dtype=a["grad_dtype"])
+        if a["optimizer"] == "adamw":
+            self.opt = FlatAdamW(self.flat, lr=a["lr"], betas=a["betas"], weight_decay=a["weight_decay"],
+                                 max_grad_norm=a["max_grad_norm"], schedule=a["schedule"])
+        else:
+            self.opt = FlatSGD(self.flat, lr=a["lr"], momentum=a["momentum"], weight_decay=a["weight_decay"],
+                               max_grad_norm=a["max_grad_norm"], schedule=a["schedule"])
+        if self.tp > 1:
+            # grad norm over the whole model: replicated groups (norms) count once
+            w = []
+            for g in self.flat.groups:
+                rep = {bool(getattr(sl.param, "_tp_replicated", False)) for sl in g.slots}
+                if len(rep) != 1:
+                    raise ValueError(f"flat group {g.name} mixes TP-replicated and sharded parameters")
+                w.append(1.0 / self.tp if rep.pop() else 1.0)
+            self.opt.norm_weights = w
+            self.opt.norm_reduce = lambda t: self.comm.tp.all_reduce(t)
+        self.ddp = ElasticDDP(self.flat, None, bucket_mb=a["bucket_mb"])
+
     def _connect(self):
         if self.ctx.standalone:
             self.kv = None
@@ -115,7 +149,7 @@ class ElasticTrainer:
         self.kv = KV(self._store, f"edl/{self.ctx.job}")
         if self.ctx.embedded_master and self.ctx.index == 0:
             cfg = self.rdzv_config or RendezvousConfig(min_nodes=self.ctx.static_world,
-                                                       max_nodes=self.ctx.static_world)
+                                                       max_nodes=self.ctx.static_world, granule=self.tp)
             self._manager = RendezvousManager(self.kv, cfg, events=self.events)
             self._manager.start()
         info = {"index": self.ctx.index, "role": self.ctx.role, "gpu": self.ctx.gpu}
@@ -151,7 +185,7 @@ class ElasticTrainer:
                 a = self.rdzv.wait_assignment(after_epoch=self.assignment.epoch if self.assignment else 0)
                 self.assignment = a
                 self.events.emit("epoch_joined", epoch=a.epoch, rank=a.rank, world=a.world, reason=a.reason)
-                if a.world == 1:
+                if a.world == 1 and self.tp == 1:
                     self.comm = LocalCommunicator(self.device, epoch=a.epoch)
                 else:
                     comm = self._build_comm(a)
@@ -161,8 +195,17 @@ class ElasticTrainer:
                     self.comm = comm
             self.events.emit("comm_ready", epoch=self.comm.epoch, world=self.comm.world_size,
                              rank=self.comm.rank, init_s=round(time.time() - t0, 4))
+            if self.tp > 1:
+                if self.rdzv is None:
+                    raise RuntimeError("tensor parallelism needs a rendezvous (tp > 1 ranks)")
+                if self.model is None:
+                    self._build_model(self.comm.tp_rank)
+                self.tp_group.rebind(self.comm.tp)
+                self.dp_comm = self.comm.dp
+            else:
+                self.dp_comm = self.comm
             try:
-                self._sync_state()
+                self._sync_state() if self.tp == 1 else self._sync_state_tp()
             except (CommAborted, RuntimeError) as e:
                 if self.rdzv is None or not (self.comm.aborted or self.rdzv.aborted(self.comm.epoch)
                                              or _is_comm_error(e)):
@@ -170,7 +213,7 @@ class ElasticTrainer:
                 self.events.emit("epoch_skipped", epoch=self.comm.epoch, during="state_sync")
                 self.comm.abort()
                 continue
-            self.ddp.set_comm(self.comm)
+            self.ddp.set_comm(self.dp_comm)
             self.events.emit("state_synced", epoch=self.comm.epoch, step=self.step)
             return
 
@@ -191,7 +234,11 @@ class ElasticTrainer:
 
         def build():
             try:
-                c = Communicator(self._store, a.rank, a.world, a.epoch, device=self.device, job=self.ctx.job)
+                if self.tp > 1:
+                    c = build_mesh(self._store, a.rank, a.world, a.epoch, self.tp, device=self.device,
+                                   job=self.ctx.job)
+                else:
+                    c = Communicator(self._store, a.rank, a.world, a.epoch, device=self.device, job=self.ctx.job)
                 c.warmup()
                 box["comm"] = c
             except Exception as e:  # noqa: BLE001 - reported through box
@@ -251,6 +298,46 @@ class ElasticTrainer:
             self.events.emit("state_broadcast", src=src_rank, bytes=nbytes, s=round(time.time() - t0, 4))
         self.needs_state = False
 
+    def _sync_state_tp(self):
+        """DP x TP state agreement.  Each TP rank's shard is replicated over its
+        DP group: if every group still has a member holding its shard at the
+        newest committed step, that member broadcasts inside the group (only
+        new or re-ranked processes receive).  If some shard has no live holder
+        (e.g. TP = world and a worker died), every rank rolls back to the
+        newest snapshot step that all shards have in memory."""
+        c = self.comm
+        t = c.tp_rank
+        valid = (not self.needs_state) and self.held_tp == t
+        max_step = int(c.ctrl_all_reduce([-1 if self.needs_state else self.step], dist.ReduceOp.MAX)[0])
+        mine_ok = 1 if (valid and self.step == max_step) else 0
+        grp_ok = int(c.dp.ctrl_all_reduce([mine_ok], dist.ReduceOp.MAX)[0]) if c.dp.world_size > 1 else mine_ok
+        all_ok = int(c.ctrl_all_reduce([grp_ok], dist.ReduceOp.MIN)[0])
+        self.ckpt_tag = f"-t{t}of{self.tp}"
+        if max_step >= 0 and all_ok:
+            if c.dp.world_size > 1 and int(c.dp.ctrl_all_reduce([1 - mine_ok], dist.ReduceOp.MAX)[0]):
+                src = int(c.dp.ctrl_all_reduce([c.dp.rank if mine_ok else 1 << 30], dist.ReduceOp.MIN)[0])
+                t0 = time.time()
+                for ten in self._state_tensors():
+                    c.dp.broadcast(ten, src)
+                scal = c.dp.ctrl_broadcast([self.step, self.opt.step_count], src)
+                self.step, self.opt.step_count = int(scal[0]), int(scal[1])
+                if self.device.type == "cuda":
+                    torch.cuda.synchronize(self.device)
+                self.events.emit("state_broadcast", src=src, group="dp", tp_rank=t, s=round(time.time() - t0, 4))
+        else:
+            mine = self.checkpoint.latest_step(self) if self.checkpoint is not None else -1
+            target = int(c.ctrl_all_reduce([mine], dist.ReduceOp.MIN)[0])
+            if target >= 0:
+                src = self.checkpoint.restore_latest(self, max_step=target)
+                if src is None or self.step != target:
+                    raise RuntimeError(f"TP shard {t}: snapshot of step {target} not restorable")
+                self.events.emit("restored", step=self.step, source=src, tp_rank=t)
+            elif max_step >= 0:
+                raise RuntimeError(f"TP shard {t} lost at step {max_step} and no in-memory snapshot covers it")
+            # else: fresh start; replicas of a shard are identical by seeding (no broadcast)
+        self.held_tp = t
+        self.needs_state = False
+
     def _maybe_restore(self):
         if self.checkpoint is None:
             return
@@ -260,9 +347,8 @@ class ElasticTrainer:
 
     # ------------------------------------------------------------------ steps
     def _micro_batches(self, data, plan: ElasticBatchPlan):
-        rank = self.comm.rank
-        world = self.comm.world_size
-        return plan.indices(self.step, rank, world)
+        c = self.dp_comm or self.comm  # TP ranks of one replica consume the same samples
+        return plan.indices(self.step, c.rank, c.world_size)
 
     def _run_step(self, loss_fn, data, plan):
         mbs = self._micro_batches(data, plan)
@@ -305,7 +391,11 @@ class ElasticTrainer:
         self._connect()
         self._start_watchdog()
         try:
-            self._enter_epoch()
+            try:
+                self._enter_epoch()
+            except JobFinished:
+                self.events.emit("finished_waiting", node=self.ctx.node_id)
+                return self
             while self.step < num_steps:
                 t0 = time.perf_counter()
                 ok = True
@@ -354,8 +444,14 @@ class ElasticTrainer:
                 if self.rdzv is not None and self.rdzv.plan_version != self.plan_version:
                     self._apply_runtime_plan(self.rdzv.plan_version)
                 need_new = (not ok) or self.comm.aborted or (self.rdzv is not None and latest > self.comm.epoch)
-                if need_new:
-                    self._reconfigure()
+                if need_new and self.step < num_steps:
+                    try:
+                        self._reconfigure()
+                    except JobFinished:
+                        self.events.emit("finished_waiting", node=self.ctx.node_id)
+                        return self
+            if self.rdzv is not None and self.comm.rank == 0:
+                self.rdzv.kv.set("train/done", str(self.step))  # releases spare waiting workers
         finally:
             self._stop.set()
         return self

@@ -21,17 +21,28 @@ torch.set_num_threads(1)
 cfg = get_config("llama-tiny", n_layers=1, dim=64, n_heads=4, n_kv_heads=2, ffn_dim=128, vocab_size=128)
 steps = int(os.environ.get("TEST_STEPS", 8))
 gb = int(os.environ.get("TEST_GB", 6))
-tr = ElasticTrainer(lambda dev: Llama(cfg, device=dev, dtype=torch.float32), global_batch=gb, micro_batch=2,
-                    lr=1e-3, device="cpu")
+if int(os.environ.get("EDL_TP", 1)) > 1:
+    from easydl_amd.parallel.tp import LlamaTP  # noqa: E402
+    model_fn = lambda dev, g: LlamaTP(cfg, g, device=dev, dtype=torch.float32)  # noqa: E731
+else:
+    model_fn = lambda dev: Llama(cfg, device=dev, dtype=torch.float32)  # noqa: E731
+ckpt = None
+if os.environ.get("TEST_CKPT"):
+    from easydl_amd.ckpt.manager import CheckpointManager  # noqa: E402
+    ckpt = CheckpointManager(os.environ["TEST_CKPT_JOB"], interval=int(os.environ["TEST_CKPT"]), pin=False)
+tr = ElasticTrainer(model_fn, global_batch=gb, micro_batch=2, lr=1e-3, device="cpu", checkpoint=ckpt)
 tr.fit(lambda m, b: m(*b), SyntheticTokens(cfg.vocab_size, 16, num_samples=4096), num_steps=steps,
        on_step=lambda t, l: time.sleep(float(os.environ.get("TEST_STEP_SLEEP", 0))))
 h = hashlib.sha256()
-for g in tr.flat.groups:
+for g in (tr.flat.groups if tr.flat is not None else []):
     h.update(g.data.numpy().tobytes())
-res = {"index": tr.ctx.index, "step": tr.step, "hash": h.hexdigest(),
+res = {"index": tr.ctx.index, "step": tr.step, "hash": h.hexdigest(), "tp_rank": tr.held_tp,
+       "dp_rank": tr.dp_comm.rank if tr.dp_comm is not None else None,
        "worlds": [r["world"] for r in tr.history], "epochs": [r["epoch"] for r in tr.history],
        "loss": float(tr.last_loss) if tr.last_loss is not None else None}
 out = os.environ.get("TEST_OUT") or os.path.join(os.environ["EDL_RUN_DIR"], f"res{tr.ctx.index}-{os.getpid()}.json")
 with open(out, "w") as f:
     json.dump(res, f)
 tr.close()
+if ckpt is not None:
+    ckpt.close()

@@ -30,10 +30,10 @@ def _env(tmp, idx, extra):
     return e
 
 
-def _start_master(tmp, port, mn, mx, window=0.3, initial=0):
+def _start_master(tmp, port, mn, mx, window=0.3, initial=0, granule=1):
     return subprocess.Popen([sys.executable, "-m", "easydl_amd.master.main", "--job", "t", "--port", str(port),
                              "--min", str(mn), "--max", str(mx), "--join-window", str(window),
-                             "--initial", str(initial),
+                             "--initial", str(initial), "--granule", str(granule),
                              "--run-dir", str(tmp)], cwd=ROOT, env=dict(os.environ, PYTHONPATH=ROOT),
                             stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
 
@@ -128,3 +128,111 @@ def test_scale_up_joiner_receives_state(tmp_path):
         assert r[2]["step"] == 30
     finally:
         m.terminate()
+
+
+def _report_exit(port, idx, rc):
+    from easydl_amd.master.store import KV, make_tcp_store
+    kv = KV(make_tcp_store("127.0.0.1", port, False), "edl/t")
+    node = [n for n in (kv.get_str("rdzv/joined") or "").split(",") if n.startswith(f"t-worker-{idx}:")][0]
+    kv.set(f"ev/exit/{node}", json.dumps({"code": rc}))
+
+
+@pytest.mark.slow
+def test_tp2_dp2_static_replicas_agree(tmp_path):
+    """DP x TP mesh (tp=2, dp=2): TP ranks of a replica see the same batch, DP
+    replicas of each shard stay bit-identical, all ranks report one loss."""
+    port = free_port()
+    m = _start_master(tmp_path, port, 2, 4, initial=4, granule=2)
+    try:
+        procs = {}
+        for i in range(4):
+            env = _env(tmp_path, i, {"EDL_MASTER_ADDR": "127.0.0.1", "EDL_MASTER_PORT": str(port),
+                                     "TEST_STEPS": "6", "TEST_GB": "4", "EDL_TP": "2"})
+            procs[i] = subprocess.Popen([sys.executable, WORKER], env=env, cwd=ROOT)
+        codes = _wait(procs)
+        assert codes == {0: 0, 1: 0, 2: 0, 3: 0}, codes
+        r = _results(tmp_path, range(4))
+        by_tp = {}
+        for x in r.values():
+            assert x["step"] == 6 and x["worlds"] == [4] * 6
+            by_tp.setdefault(x["tp_rank"], set()).add(x["hash"])
+        assert sorted(by_tp) == [0, 1] and all(len(v) == 1 for v in by_tp.values()), by_tp
+        assert by_tp[0] != by_tp[1]
+        by_dp = {}
+        for x in r.values():  # the TP ranks of one replica compute one loss
+            by_dp.setdefault(x["dp_rank"], set()).add(round(x["loss"], 6))
+        assert sorted(by_dp) == [0, 1] and all(len(v) == 1 for v in by_dp.values()), by_dp
+    finally:
+        m.terminate()
+
+
+@pytest.mark.slow
+def test_tp2_kill_worker_keeps_shards(tmp_path):
+    """tp=2 world 4 -> a worker dies -> world 2 (granule 2): the survivors that
+    keep their TP rank continue without restore; the spare exits cleanly."""
+    port = free_port()
+    m = _start_master(tmp_path, port, 2, 4, initial=4, granule=2)
+    try:
+        procs = {}
+        for i in range(4):
+            env = _env(tmp_path, i, {"EDL_MASTER_ADDR": "127.0.0.1", "EDL_MASTER_PORT": str(port),
+                                     "TEST_STEPS": "8", "TEST_GB": "4", "EDL_TP": "2",
+                                     "EDL_FAULT": "kill@step=3,index=3"})
+            procs[i] = subprocess.Popen([sys.executable, WORKER], env=env, cwd=ROOT)
+        t_end = time.time() + 240
+        while time.time() < t_end:
+            rc = procs[3].poll()
+            if rc is not None:
+                _report_exit(port, 3, rc)
+                break
+            time.sleep(0.05)
+        codes = _wait({i: procs[i] for i in range(3)})
+        assert codes == {0: 0, 1: 0, 2: 0}, codes
+        r = _results(tmp_path, range(3))
+        done = [x for x in r.values() if x["step"] == 8]
+        assert len(done) == 2 and {x["tp_rank"] for x in done} == {0, 1}, r
+        assert done[0]["worlds"][0] == 4 and done[0]["worlds"][-1] == 2
+        from easydl_amd.utils.events import read_events
+        ev = read_events(str(tmp_path))
+        assert not [e for e in ev if e["kind"] == "restored"], "no restore needed: shards survived"
+        assert [e for e in ev if e["kind"] == "finished_waiting"], "spare worker did not exit via train/done"
+    finally:
+        m.terminate()
+
+
+@pytest.mark.slow
+def test_tp_shard_lost_restores_from_snapshot(tmp_path):
+    """tp=2 = world (no DP replica): a dead worker's shard has no live holder;
+    after the operator-style replacement joins, BOTH ranks roll back to the
+    newest common in-memory snapshot and finish."""
+    from easydl_amd.ckpt.manager import unlink_job_segments
+    job = f"tpck{os.getpid()}"
+    unlink_job_segments(job)
+    port = free_port()
+    m = _start_master(tmp_path, port, 2, 2, initial=2, granule=2)
+    try:
+        procs = {}
+        base = {"EDL_MASTER_ADDR": "127.0.0.1", "EDL_MASTER_PORT": str(port), "TEST_STEPS": "8", "TEST_GB": "4",
+                "EDL_TP": "2", "TEST_CKPT": "2", "TEST_CKPT_JOB": job}
+        for i in range(2):
+            procs[i] = subprocess.Popen([sys.executable, WORKER],
+                                        env=_env(tmp_path, i, dict(base, EDL_FAULT="kill@step=5,index=1")), cwd=ROOT)
+        t_end = time.time() + 240
+        while time.time() < t_end:
+            rc = procs[1].poll()
+            if rc is not None:
+                _report_exit(port, 1, rc)
+                break
+            time.sleep(0.05)
+        env = _env(tmp_path, 1, dict(base, EDL_GENERATION="1", TEST_OUT=str(tmp_path / "res1b.json")))
+        procs["r"] = subprocess.Popen([sys.executable, WORKER], env=env, cwd=ROOT)
+        codes = _wait({0: procs[0], "r": procs["r"]})
+        assert codes == {0: 0, "r": 0}, codes
+        a, b = json.load(open(tmp_path / "res0.json")), json.load(open(tmp_path / "res1b.json"))
+        assert a["step"] == b["step"] == 8 and {a["tp_rank"], b["tp_rank"]} == {0, 1}
+        from easydl_amd.utils.events import read_events
+        rs = [e for e in read_events(str(tmp_path)) if e["kind"] == "restored"]
+        assert len(rs) == 2 and {e["step"] for e in rs} == {4}, rs
+    finally:
+        m.terminate()
+        unlink_job_segments(job)
