@@ -48,6 +48,8 @@ def parse():
     ap.add_argument("--ckpt-interval", type=int, default=0,
                     help="in-memory sharded snapshot every K steps (async D2H, overlapped)")
     ap.add_argument("--fault-inject", action="store_true", help="measure time-to-recover instead (local operator)")
+    ap.add_argument("--tp", type=int, default=1,
+                    help="tensor-parallel degree inside each DP replica (BASELINE config 5: --model llama3-70b --tp 8)")
     return ap.parse_args()
 
 
@@ -74,15 +76,24 @@ def main():
     cfg = get_config(args.model, **overrides)
     dtype = torch.bfloat16 if use_cuda else torch.float32
     S, B = args.seq, args.mbs
-    gb = world * B * args.accum
+    tp = args.tp
+    if world % tp:
+        raise SystemExit(f"WORLD_SIZE={world} is not a multiple of --tp {tp}")
+    dp = world // tp
+    gb = dp * B * args.accum
     ckpt = None
     if args.ckpt_interval > 0:
         from easydl_amd.ckpt.manager import CheckpointManager, unlink_job_segments
         unlink_job_segments("bench")
         ckpt = CheckpointManager("bench", interval=args.ckpt_interval)
-    tr = ElasticTrainer(lambda d: Llama(cfg, device=d, dtype=dtype), lr=3e-4, betas=(0.9, 0.95), weight_decay=0.1,
+    if tp > 1:
+        from easydl_amd.parallel.tp import LlamaTP
+        model_fn = lambda d, g: LlamaTP(cfg, g, device=d, dtype=dtype)  # noqa: E731
+    else:
+        model_fn = lambda d: Llama(cfg, device=d, dtype=dtype)  # noqa: E731
+    tr = ElasticTrainer(model_fn, lr=3e-4, betas=(0.9, 0.95), weight_decay=0.1,
                         max_grad_norm=1.0, global_batch=gb, micro_batch=B, device=dev, bucket_mb=args.bucket_mb,
-                        checkpoint=ckpt)
+                        checkpoint=ckpt, tp=tp)
     marks = {}
 
     def sync_barrier(t):
@@ -107,12 +118,15 @@ def main():
     if comm.world_size > 1:
         import torch.distributed as dist
         el = float(comm.ctrl_all_reduce([el], op=dist.ReduceOp.MAX)[0])
-    tokens = comm.world_size * B * S * args.accum * args.steps
+    tokens = (comm.world_size // tp) * B * S * args.accum * args.steps
     tps = tokens / el
     fpt = cfg.flops_per_token(S)
     tflops_gpu = tps / comm.world_size * fpt / 1e12
+    metric = "tokens/sec, Llama-3-8B elastic DDP (full train step: fwd+bwd+allreduce+commit+AdamW)"
+    if tp > 1:
+        metric = f"tokens/sec, {args.model} elastic DP x TP={tp} (full train step)"
     res = {
-        "metric": "tokens/sec, Llama-3-8B elastic DDP (full train step: fwd+bwd+allreduce+commit+AdamW)",
+        "metric": metric,
         "value": round(tps, 2),
         "unit": "tokens/s",
         "n_gpus": comm.world_size,
@@ -128,7 +142,7 @@ def main():
             "model": args.model if not args.layers else f"{args.model}-L{args.layers}",
             "global_batch": gb,
             "seq_len": S,
-            "parallelism": f"dp{comm.world_size}",
+            "parallelism": f"dp{comm.world_size // tp}" + (f"tp{tp}" if tp > 1 else ""),
             "micro_batch": B,
             "grad_accum": args.accum,
             "optimizer": "AdamW fp32 master/moments, clip 1.0",
