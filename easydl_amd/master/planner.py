@@ -32,13 +32,14 @@ class PlanLoop:
         self._t_start = time.time()
         self._last = 0.0
         self.started = False
+        self._features = None
 
     def features(self) -> dict:
-        f = dict(self.job.features)
-        f.setdefault("mode", self.job.mode)
-        f.setdefault("min_workers", self.job.min_workers)
-        f.setdefault("max_workers", self.job.max_workers)
-        return f
+        """Extracted job features (meta-device model analysis) + the user's hints."""
+        if self._features is None:
+            from easydl_amd.master.features import extract
+            self._features = extract(self.job)
+        return dict(self._features)
 
     def _apply(self, master, jr: JobResource):
         self.version += 1

@@ -1,0 +1,31 @@
+"""Job feature extraction (meta-device model analysis) feeding the Brain."""
+from easydl_amd.api.spec import ElasticJob
+from easydl_amd.brain.collectors import GpuInfo, NodeInventory
+from easydl_amd.brain.planner import JobFeatures, Planner
+from easydl_amd.master.features import extract
+
+
+def test_llama_features_from_env():
+    f = extract(ElasticJob(name="j", env={"EDL_MODEL": "llama3-8b", "EDL_SEQ": "8192", "EDL_MBS": "2"}))
+    assert 8.0e9 < f["params"] < 8.1e9
+    assert f["tokens_per_step_per_rank"] == 16384
+    assert abs(f["state_gb_per_rank"] - 128.5) < 1.0          # 16 B/param
+    assert 60 < f["activation_gb_per_rank"] < 90
+
+
+def test_tp_divides_state_and_hints_win():
+    f = extract(ElasticJob(name="j", env={"EDL_MODEL": "llama3-70b", "EDL_TP": "8"},
+                           features={"activation_gb_per_rank": 50}))
+    assert 7.0e10 < f["params"] < 7.1e10 and f["tp"] == 8
+    assert f["state_gb_per_rank"] < 145
+    assert f["activation_gb_per_rank"] == 50                 # user declaration overrides
+
+
+def test_unknown_model_is_harmless_and_brain_accepts():
+    f = extract(ElasticJob(name="j", features={"model": "my-net", "params": 1e6}))
+    assert f["params"] == 1e6
+    inv = NodeInventory(gpus=[GpuInfo(i, "gfx950", 256, 288.0) for i in range(8)], cpus=128, host_mem_gb=2048)
+    feat = JobFeatures.from_dict(extract(ElasticJob(name="j", env={"EDL_MODEL": "llama3-8b"})))
+    plan = Planner().startup_plan(feat, inv)
+    assert plan.roles["worker"].replicas == 8
+    assert JobFeatures.from_dict(f).params == 1e6
