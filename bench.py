@@ -43,7 +43,8 @@ def parse():
     ap.add_argument("--mbs", type=int, default=2, help="sequences per micro-batch per GPU")
     ap.add_argument("--accum", type=int, default=2, help="micro-batches per step per GPU")
     ap.add_argument("--bucket-mb", type=float, default=None)
-    ap.add_argument("--layers", type=int, default=None, help="override layer count (debug only; invalid for the metric)")
+    ap.add_argument("--layers", type=int, default=None,
+                    help="override layer count (debug only; invalid for the metric)")
     ap.add_argument("--out", default=None)
     ap.add_argument("--ckpt-interval", type=int, default=0,
                     help="in-memory sharded snapshot every K steps (async D2H, overlapped)")
@@ -154,8 +155,9 @@ def main():
         "peak_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 2**30, 1) if use_cuda else 0.0,
         "setup_and_warmup_s": round(marks["t0"] - t_start, 2),
         "time_to_recover_s": None,
-        "ckpt": None if ckpt is None else {"interval": args.ckpt_interval, "snapshots": ckpt.stats["snapshots"],
-                                           "bytes_per_snapshot": ckpt.stats["d2h_bytes"] // max(1, ckpt.stats["snapshots"])},
+        "ckpt": None if ckpt is None else {
+            "interval": args.ckpt_interval, "snapshots": ckpt.stats["snapshots"],
+            "bytes_per_snapshot": ckpt.stats["d2h_bytes"] // max(1, ckpt.stats["snapshots"])},
     }
     if comm.rank == 0:
         line = json.dumps(res)

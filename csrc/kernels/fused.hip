@@ -144,7 +144,8 @@ __global__ __launch_bounds__(256) void rope_qkv_kernel(const bf16_t* __restrict_
 // autograd wrapper applies dloss / n_valid).  ignore_index rows get loss 0 and
 // zero gradient.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void xent_fwd_bwd_kernel(bf16_t* __restrict__ logits, const int64_t* __restrict__ labels,
+__global__ __launch_bounds__(256) void xent_fwd_bwd_kernel(bf16_t* __restrict__ logits,
+                                                           const int64_t* __restrict__ labels,
                                                            float* __restrict__ loss, int V, int64_t ignore_index,
                                                            int write_grad) {
   __shared__ float sm[4], ss[4];

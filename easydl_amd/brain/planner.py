@@ -29,7 +29,7 @@ from __future__ import annotations
 
 import math
 import statistics
-from dataclasses import dataclass, field
+from dataclasses import dataclass
 
 from easydl_amd.api.spec import Resource, ResourcePlan, RoleResource
 from easydl_amd.brain.collectors import NodeInventory

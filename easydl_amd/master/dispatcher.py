@@ -12,7 +12,6 @@ instead.
 """
 from __future__ import annotations
 
-import json
 
 
 class ShardDispatcher:

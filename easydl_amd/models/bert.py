@@ -8,7 +8,6 @@ decoder).  Attention (head_dim 64, bidirectional) runs through SDPA.
 """
 from __future__ import annotations
 
-import math
 from dataclasses import dataclass
 
 import torch

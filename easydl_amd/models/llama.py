@@ -18,7 +18,7 @@ Capability source: BASELINE.json configs 3 and 5 (Llama-3 8B DDP, 70B TP=8).
 from __future__ import annotations
 
 import math
-from dataclasses import asdict, dataclass, field
+from dataclasses import asdict, dataclass
 
 import torch
 import torch.nn as nn

@@ -22,7 +22,6 @@ all-gather over the token dimension (``sequence_parallel=True``).
 """
 from __future__ import annotations
 
-import math
 
 import torch
 import torch.nn as nn

@@ -21,9 +21,7 @@ interrupt the training", README.md:28): the PS just stops hearing from it.
 """
 from __future__ import annotations
 
-import json
 import logging
-import os
 import socket
 import threading
 import time

@@ -12,7 +12,6 @@ import json
 import socket
 import struct
 
-import numpy as np
 import torch
 
 _DT = {torch.float32: "f32", torch.bfloat16: "bf16", torch.float16: "f16", torch.int64: "i64", torch.int32: "i32",

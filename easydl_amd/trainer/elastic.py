@@ -55,7 +55,8 @@ class ElasticTrainer:
     def __init__(self, model_fn, *, optimizer: str = "adamw", lr: float = 3e-4, weight_decay: float = 0.1,
                  betas=(0.9, 0.95), momentum: float = 0.9, max_grad_norm: float = 1.0, global_batch: int | None = None,
                  micro_batch: int = 1, device=None, dtype=torch.bfloat16, bucket_mb: float | None = None,
-                 grad_dtype=None, ctx: TrainerContext | None = None, seed: int = 1234, schedule: LRSchedule | None = None,
+                 grad_dtype=None, ctx: TrainerContext | None = None, seed: int = 1234,
+                 schedule: LRSchedule | None = None,
                  rdzv_config: RendezvousConfig | None = None, checkpoint=None, log_every: int = 0,
                  store=None, tp: int | None = None):
         self.ctx = ctx or TrainerContext.from_env()
@@ -106,7 +107,8 @@ class ElasticTrainer:
         self.history: list[dict] = []
         self.last_loss = None
         self.tokens_per_sample = 0
-        self.metrics = MetricsReporter(path=os.path.join(self.ctx.run_dir, f"metrics-{self.ctx.role}{self.ctx.index}.jsonl"))
+        self.metrics = MetricsReporter(
+            path=os.path.join(self.ctx.run_dir, f"metrics-{self.ctx.role}{self.ctx.index}.jsonl"))
         self.plan_version = 0
 
     # ------------------------------------------------------------------ setup

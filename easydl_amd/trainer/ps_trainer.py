@@ -13,7 +13,6 @@ from __future__ import annotations
 import json
 import logging
 import os
-import socket
 import time
 
 import torch

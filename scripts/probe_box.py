@@ -1,5 +1,7 @@
 """Probe the MI355X box: memory, GEMM rates (hipBLASLt via torch), SDPA backends/speed."""
-import json, time, os, subprocess, sys
+import json
+import os
+import time
 import torch
 import torch.nn.functional as F
 

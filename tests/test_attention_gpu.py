@@ -1,5 +1,4 @@
 """Hand-written flash attention vs an fp32 reference (GPU)."""
-import math
 
 import pytest
 import torch

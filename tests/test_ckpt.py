@@ -1,8 +1,6 @@
 """Checkpoint format v1 + shm A/B store + restore (CPU tier; GPU variant in test_ckpt_gpu)."""
-import os
 
 import numpy as np
-import pytest
 import torch
 
 from easydl_amd.ckpt.manager import CheckpointManager, ShmSegment, checksum_np, load_dir, shard_layout, \

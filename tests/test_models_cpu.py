@@ -56,7 +56,6 @@ def test_mlp_learns():
 
 
 def test_flat_params_mixed_dtypes():
-    from easydl_amd.models.resnet import resnet50
     m = ResNet(layers=(1, 1, 1, 1), num_classes=10, width=8).to(torch.bfloat16)
     for mod in m.modules():
         if isinstance(mod, torch.nn.BatchNorm2d):
