@@ -51,4 +51,19 @@ SIGS = {
     "edl_roctx_push": (i32, [cp]),
     "edl_roctx_pop": (i32, []),
     "edl_roctx_mark": (None, [cp]),
+    "edl_rccl_available": (i32, [ctypes.POINTER(i32), ctypes.POINTER(i32)]),
+    "edl_rccl_error_string": (cp, [i32]),
+    "edl_rccl_unique_id": (i32, [ctypes.c_char_p]),
+    "edl_rccl_init": (i32, [cp, i32, i32, i32, ctypes.POINTER(i32), ctypes.c_double, ctypes.POINTER(vp)]),
+    "edl_rccl_shrink": (i32, [vp, ctypes.POINTER(i32), i32, i32, ctypes.POINTER(i32), ctypes.c_double,
+                              ctypes.POINTER(vp)]),
+    "edl_rccl_abort": (i32, [vp]),
+    "edl_rccl_destroy": (i32, [vp]),
+    "edl_rccl_async_error": (i32, [vp]),
+    "edl_rccl_all_reduce": (i32, [vp, vp, vp, ctypes.c_size_t, i32, i32, vp]),
+    "edl_rccl_broadcast": (i32, [vp, vp, vp, ctypes.c_size_t, i32, i32, vp]),
+    "edl_rccl_reduce_scatter": (i32, [vp, vp, vp, ctypes.c_size_t, i32, i32, vp]),
+    "edl_rccl_all_gather": (i32, [vp, vp, vp, ctypes.c_size_t, i32, vp]),
+    "edl_rccl_sendrecv": (i32, [vp, i32, ctypes.POINTER(i32), ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_size_t),
+                                ctypes.POINTER(i32), i32, vp]),
 }

@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import datetime
 import logging
+import os
 import threading
 import time
 
@@ -38,20 +39,28 @@ def _td(s: float) -> datetime.timedelta:
 class Communicator:
     def __init__(self, store: dist.Store, rank: int, world_size: int, epoch: int, *, device: torch.device,
                  job: str = "job", timeout_s: float = 120.0, control_timeout_s: float = 30.0,
-                 high_priority: bool = True, tag: str = "", data: bool = True):
+                 high_priority: bool = True, tag: str = "", data: bool = True, data_backend: str | None = None):
         self.rank = rank
         self.world_size = world_size
         self.epoch = epoch
         self.device = torch.device(device)
         self.tag = tag
+        self.rccl = None
         self._aborted = False
         self._lock = threading.Lock()
         t0 = time.perf_counter()
         base = dist.PrefixStore(f"edl/{job}/e{epoch}" + (f"/{tag}" if tag else ""), store)
         self.ctrl = dist.ProcessGroupGloo(dist.PrefixStore("ctrl", base), rank, world_size, _td(control_timeout_s))
+        data_backend = data_backend or os.environ.get("EDL_COMM", "pg")
         if not data:
             self.data = None
             self.backend = "none"
+        elif self.device.type == "cuda" and data_backend == "native":
+            # csrc/runtime/rccl_comm.cpp: non-blocking, abortable creation; own comm stream
+            from easydl_amd.parallel.rccl import RcclComm
+            self.data = None
+            self.rccl = RcclComm(dist.PrefixStore("data", base), rank, world_size, self.device, timeout_s=timeout_s)
+            self.backend = "rccl-native"
         elif self.device.type == "cuda":
             opts = dist.ProcessGroupNCCL.Options()
             opts.is_high_priority_stream = high_priority
@@ -67,7 +76,10 @@ class Communicator:
     def warmup(self) -> float:
         """Force lazy communicator creation now (so it is not hidden in step 1)."""
         t0 = time.perf_counter()
-        if self.data is not None:
+        if self.rccl is not None:
+            self.all_reduce(torch.zeros(1, device=self.device))
+            torch.cuda.synchronize(self.device)
+        elif self.data is not None:
             x = torch.zeros(1, device=self.device)
             self.data.allreduce([x]).wait()
             if self.device.type == "cuda":
@@ -85,7 +97,9 @@ class Communicator:
         # collectives already fail as soon as a peer's sockets close, and
         # ProcessGroupGloo.abort() leaves worker threads that std::terminate the
         # process at teardown, so gloo groups are only marked, never aborted.
-        if self.backend == "rccl":
+        if self.rccl is not None:
+            self.rccl.abort()
+        elif self.backend == "rccl":
             try:
                 self.data.abort()
             except Exception as e:  # pragma: no cover - best effort
@@ -98,6 +112,8 @@ class Communicator:
     def shutdown(self) -> None:
         if self._aborted:
             return
+        if self.rccl is not None:
+            self.rccl.destroy()
         for pg in (self.data, self.ctrl):
             if pg is None:
                 continue
@@ -111,6 +127,8 @@ class Communicator:
     def all_reduce_async(self, t: torch.Tensor, op=dist.ReduceOp.SUM):
         if self._aborted:
             raise CommAborted("communicator aborted")
+        if self.rccl is not None:
+            return self._native(self.rccl.all_reduce_async, t, op)
         o = dist.AllreduceOptions()
         o.reduceOp = op
         return self.data.allreduce([t], o)
@@ -122,31 +140,60 @@ class Communicator:
     def broadcast(self, t: torch.Tensor, src: int) -> torch.Tensor:
         if self._aborted:
             raise CommAborted("communicator aborted")
+        if self.rccl is not None:
+            self._wait(self._native(self.rccl.broadcast_async, t, src))
+            return t
         o = dist.BroadcastOptions()
         o.rootRank = src
         self._wait(self.data.broadcast([t], o))
         return t
 
     def all_gather_into(self, out: torch.Tensor, inp: torch.Tensor) -> torch.Tensor:
+        if self.rccl is not None:
+            self._wait(self._native(self.rccl.all_gather_async, out, inp))
+            return out
         self._wait(self.data._allgather_base(out, inp))
         return out
 
     def reduce_scatter_into(self, out: torch.Tensor, inp: torch.Tensor, op=dist.ReduceOp.SUM) -> torch.Tensor:
+        if self.rccl is not None:
+            self._wait(self._native(self.rccl.reduce_scatter_async, out, inp, op))
+            return out
         o = dist.ReduceScatterOptions()
         o.reduceOp = op
         self._wait(self.data._reduce_scatter_base(out, inp, o))
         return out
 
     def all_to_all_single(self, out: torch.Tensor, inp: torch.Tensor):
+        if self.rccl is not None:  # equal splits as one grouped send/recv batch
+            n = self.world_size
+            src, dst = inp.reshape(n, -1), out.reshape(n, -1)
+            dst[self.rank].copy_(src[self.rank])
+            ops = [op for p in range(n) if p != self.rank for op in (("send", src[p], p), ("recv", dst[p], p))]
+            if ops:
+                self._wait(self._native(self.rccl.sendrecv_async, ops))
+            return out
         self._wait(self.data.alltoall_base(out, inp, [], [], dist.AllToAllOptions()))
         return out
 
     def send(self, t: torch.Tensor, dst: int, tag: int = 0):
+        if self.rccl is not None:
+            self._wait(self._native(self.rccl.sendrecv_async, [("send", t, dst)]))
+            return
         self._wait(self.data.send([t], dst, tag))
 
     def recv(self, t: torch.Tensor, src: int, tag: int = 0):
+        if self.rccl is not None:
+            self._wait(self._native(self.rccl.sendrecv_async, [("recv", t, src)]))
+            return t
         self._wait(self.data.recv([t], src, tag))
         return t
+
+    def _native(self, fn, *args):
+        try:
+            return fn(*args)
+        except RuntimeError as e:
+            raise CommAborted(f"native RCCL call failed in epoch {self.epoch}: {e}") from e
 
     def _wait(self, work) -> None:
         try:
