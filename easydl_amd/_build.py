@@ -63,14 +63,15 @@ def _check_resolves(lib: str) -> None:
 
 def build_kernels(force: bool = False, verbose: bool = False) -> str:
     srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
-    deps = srcs + glob.glob(os.path.join(CSRC, "kernels", "*.h"))
+    hdrs = glob.glob(os.path.join(CSRC, "kernels", "*.h")) + glob.glob(os.path.join(CSRC, "include", "*.h"))
+    deps = srcs + hdrs
     os.makedirs(LIBDIR, exist_ok=True)
     if force or _stale(KERNELS_SO, deps):
         objs = []
         for s in srcs:
             o = os.path.join(LIBDIR, "obj", os.path.basename(s) + ".o")
             os.makedirs(os.path.dirname(o), exist_ok=True)
-            if force or _stale(o, [s] + glob.glob(os.path.join(CSRC, "kernels", "*.h"))):
+            if force or _stale(o, [s] + hdrs):
                 cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-c", s, "-o", o,
                        "-Wno-unused-result"]
                 if verbose:
@@ -86,7 +87,7 @@ def build_kernels(force: bool = False, verbose: bool = False) -> str:
 
 def build_runtime(force: bool = False, verbose: bool = False) -> str:
     srcs = sorted(glob.glob(os.path.join(CSRC, "runtime", "*.cpp")))
-    deps = srcs + glob.glob(os.path.join(CSRC, "runtime", "*.h"))
+    deps = srcs + glob.glob(os.path.join(CSRC, "runtime", "*.h")) + glob.glob(os.path.join(CSRC, "include", "*.h"))
     os.makedirs(LIBDIR, exist_ok=True)
     if not srcs:
         return ""

@@ -51,6 +51,16 @@ SIGS = {
     "edl_roctx_push": (i32, [cp]),
     "edl_roctx_pop": (i32, []),
     "edl_roctx_mark": (None, [cp]),
+    "edl_xgmi_ws_create": (i32, [i32, u64, ctypes.POINTER(vp)]),
+    "edl_xgmi_ws_handles": (i32, [vp, ctypes.c_char_p]),
+    "edl_xgmi_ws_open": (i32, [vp, i32, i32, ctypes.c_char_p]),
+    "edl_xgmi_ws_ptrs": (i32, [vp, ctypes.POINTER(vp), ctypes.POINTER(vp)]),
+    "edl_xgmi_ws_bytes": (u64, [vp]),
+    "edl_xgmi_ws_abort_dev": (vp, [vp]),
+    "edl_xgmi_ws_status_dev": (vp, [vp]),
+    "edl_xgmi_ws_set_abort": (None, [vp, i32]),
+    "edl_xgmi_ws_status": (i32, [vp]),
+    "edl_xgmi_ws_destroy": (i32, [vp]),
     "edl_rccl_available": (i32, [ctypes.POINTER(i32), ctypes.POINTER(i32)]),
     "edl_rccl_error_string": (cp, [i32]),
     "edl_rccl_unique_id": (i32, [ctypes.c_char_p]),

@@ -1,0 +1,107 @@
+"""Custom xGMI all-reduce (csrc/kernels/xgmi.hip + csrc/runtime/xgmi.cpp;
+SURVEY.md N3): IPC-mapped peer buffers on one node, one-shot for small
+messages, two-shot (direct reduce-scatter + all-gather over all 7 links) for
+large ones, every wait bounded by an abort word and a deadline.
+
+Usage (one object per rank and epoch; every rank issues the same calls)::
+
+    x = XgmiComm(store, "edl/job/e3/xgmi", rank, world, device)
+    x.all_reduce(t)           # in place, on the current stream
+    x.abort()                 # watchdog thread: spinning kernels give up
+
+Limits: <= 8 ranks (one node), fp32 / bf16, sizes a multiple of 16 bytes
+(tensors are processed in workspace-sized pieces).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from easydl_amd import _native
+
+
+class XgmiError(RuntimeError):
+    pass
+
+
+class XgmiComm:
+    ONESHOT_MAX = 512 << 10      # bytes: below this latency dominates -> one-shot
+
+    def __init__(self, store, prefix: str, rank: int, world: int, device, ws_bytes: int = 64 << 20,
+                 timeout_s: float = 60.0):
+        self.rank, self.world_size = rank, world
+        self.device = torch.device(device)
+        self.timeout_s = timeout_s
+        self._rt, self._k = _native.runtime(), _native.kernels()
+        if world > self._k("edl_xgmi_max_ranks"):
+            raise XgmiError(f"xGMI all-reduce supports at most {self._k('edl_xgmi_max_ranks')} ranks")
+        h = ctypes.c_void_p()
+        rc = self._rt("edl_xgmi_ws_create", self.device.index or 0, ws_bytes, ctypes.byref(h))
+        if rc != 0:
+            raise XgmiError(f"workspace allocation failed: hipError {rc}")
+        self._ws = h
+        self.ws_bytes = self._rt("edl_xgmi_ws_bytes", h)
+        mine = ctypes.create_string_buffer(128)
+        rc = self._rt("edl_xgmi_ws_handles", h, mine)
+        if rc != 0:
+            raise XgmiError(f"hipIpcGetMemHandle failed: hipError {rc}")
+        store.set(f"{prefix}/ipc/{rank}", mine.raw)
+        allh = b"".join(mine.raw if p == rank else store.get(f"{prefix}/ipc/{p}") for p in range(world))
+        rc = self._rt("edl_xgmi_ws_open", h, world, rank, allh)
+        if rc != 0:
+            raise XgmiError(f"hipIpcOpenMemHandle failed: hipError {rc}")
+        self._data = (ctypes.c_void_p * (2 * world))()
+        self._flags = (ctypes.c_void_p * world)()
+        self._rt("edl_xgmi_ws_ptrs", h, self._data, self._flags)
+        self._abort_dev = self._rt("edl_xgmi_ws_abort_dev", h)
+        self._status_dev = self._rt("edl_xgmi_ws_status_dev", h)
+        self.round = 0
+        self.blocks = min(self._k("edl_xgmi_max_blocks"), 256)
+        self._aborted = False
+
+    def abort(self) -> None:
+        """From any thread: every spinning workgroup of every in-flight call exits."""
+        self._aborted = True
+        if self._ws is not None:
+            self._rt("edl_xgmi_ws_set_abort", self._ws, 1)
+
+    @property
+    def aborted(self) -> bool:
+        return self._aborted
+
+    def status(self) -> int:
+        """0 = every barrier so far completed; 1 = one gave up (abort / deadline). Synchronising."""
+        return self._rt("edl_xgmi_ws_status", self._ws)
+
+    def all_reduce(self, t: torch.Tensor, algo: str | None = None) -> torch.Tensor:
+        if self._aborted:
+            raise XgmiError("aborted")
+        if t.dtype not in (torch.float32, torch.bfloat16) or not t.is_contiguous():
+            raise XgmiError("xGMI all-reduce takes contiguous fp32 / bf16 tensors")
+        flat = t.view(-1)
+        es = flat.element_size()
+        if (flat.numel() * es) % 16:
+            raise XgmiError("size must be a multiple of 16 bytes")
+        piece = (self.ws_bytes // 16) * 16 // es
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        for lo in range(0, flat.numel(), piece):
+            part = flat[lo:lo + piece]
+            nbytes = part.numel() * es
+            a = (0 if nbytes <= self.ONESHOT_MAX else 1) if algo is None else (0 if algo == "oneshot" else 1)
+            nvec = nbytes // 16
+            per_block = 2048 if a == 0 else 4096  # 16-byte vectors per workgroup before adding workgroups
+            blocks = int(max(1, min(self.blocks, -(-nvec // per_block))))
+            self.round += 1
+            rc = self._k("edl_xgmi_allreduce", self._data, self._flags, self.world_size, self.rank,
+                         part.data_ptr(), part.data_ptr(), nbytes, 0 if t.dtype == torch.float32 else 1, a,
+                         self.round, blocks, self._abort_dev, float(self.timeout_s), self._status_dev, stream)
+            if rc != 0:
+                raise XgmiError(f"launch failed: hipError {rc}")
+        return t
+
+    def close(self) -> None:
+        if self._ws is not None:
+            torch.cuda.synchronize(self.device)
+            self._rt("edl_xgmi_ws_destroy", self._ws)
+            self._ws = None
