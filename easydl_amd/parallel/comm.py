@@ -59,7 +59,7 @@ class Communicator:
             # csrc/runtime/rccl_comm.cpp: non-blocking, abortable creation; own comm stream
             from easydl_amd.parallel.rccl import RcclComm
             self.data = None
-            self.rccl = RcclComm(dist.PrefixStore("data", base), rank, world_size, self.device, timeout_s=timeout_s)
+            self.rccl = RcclComm(base, "data", rank, world_size, self.device, timeout_s=timeout_s)
             self.backend = "rccl-native"
         elif self.device.type == "cuda":
             opts = dist.ProcessGroupNCCL.Options()
