@@ -49,6 +49,9 @@ def parse():
     ap.add_argument("--ckpt-interval", type=int, default=0,
                     help="in-memory sharded snapshot every K steps (async D2H, overlapped)")
     ap.add_argument("--fault-inject", action="store_true", help="measure time-to-recover instead (local operator)")
+    ap.add_argument("--comm", default=None, choices=["pg", "native", "xgmi", "auto"],
+                    help="gradient all-reduce data plane (default $EDL_COMM or pg = ProcessGroupNCCL/RCCL; "
+                         "xgmi = hand-written IPC all-reduce; auto = probe both at each epoch, keep the faster)")
     ap.add_argument("--tp", type=int, default=1,
                     help="tensor-parallel degree inside each DP replica (BASELINE config 5: --model llama3-70b --tp 8)")
     return ap.parse_args()
@@ -67,6 +70,8 @@ def main():
     use_cuda = torch.cuda.is_available()
     dev = torch.device("cuda", local) if use_cuda else torch.device("cpu")
     os.environ.setdefault("EDL_JOB", "bench")
+    if args.comm:
+        os.environ["EDL_COMM"] = args.comm
     os.environ.setdefault("EDL_RUN_DIR", os.path.join("gpurun_out", "bench_run") if use_cuda else "/tmp/edl_bench")
 
     from easydl_amd.models.llama import Llama, get_config
@@ -148,7 +153,9 @@ def main():
             "grad_accum": args.accum,
             "optimizer": "AdamW fp32 master/moments, clip 1.0",
             "bucket_mb": tr.ddp.bucket_mb,
+            "comm": getattr(getattr(comm, "dp", comm), "backend", "local"),
         },
+        "allreduce_probe": getattr(getattr(comm, "dp", comm), "xgmi_probe", None),
         "tflops_per_gpu": round(tflops_gpu, 1),
         "mfu_vs_2.5PF": round(tflops_gpu / 2500.0, 4),
         "loss": round(float(tr.last_loss), 4) if tr.last_loss is not None else None,

@@ -1,0 +1,198 @@
+// Parameter-server data-plane kernels.
+//
+// Embedding tables of CTR-style models (the reference's example job is
+// "elastic-deepctr-job", docs/design/elastic-training-operator.md:35) live on
+// the PS as fp32 [rows, dim].  Workers touch a few thousand rows per step, so
+// push/pull are row-sparse:
+//   * pull  = gather rows (edl_embed_gather): one 64-lane wave per row, 16-B
+//     loads; the table pointer may be an IPC-mapped peer pointer, then the
+//     rows stream over xGMI straight into the worker's HBM (bf16 or fp32 out);
+//   * push  = segment-sum of duplicate ids into a compact [unique, dim]
+//     gradient (edl_embed_scatter_add: fp32 atomics into an L2-resident
+//     buffer), then a lazy AdamW/Adagrad/SGD on exactly the touched rows
+//     (edl_sparse_adamw_rows) — untouched rows keep their moments, as in
+//     TF's lazy Adam, so the cost is O(touched rows), not O(table);
+//   * dense pull with cast (edl_ps_pull_cast): fp32 PS shard -> bf16 worker
+//     params, reading a peer pointer over xGMI.
+// Index validity is checked on the host side of every entry (rows bound); a
+// bad id is clamped to a zero row on gather and dropped on scatter instead of
+// faulting the device.
+#include "common.h"
+
+using namespace edl;
+
+namespace {
+
+constexpr int kRowBlock = 256;  // 4 waves, one row per wave
+
+// dim % 4 == 0; one wave per row, each lane moves 4 floats per iteration.
+template <bool OUT_BF16>
+__global__ __launch_bounds__(kRowBlock) void embed_gather_kernel(const float* __restrict__ table,
+                                                                 const int64_t* __restrict__ idx, int64_t n, int dim,
+                                                                 int64_t rows, void* __restrict__ out) {
+  const int64_t r = (int64_t)blockIdx.x * (kRowBlock / kWave) + (threadIdx.x >> 6);
+  if (r >= n) return;
+  const int lane = threadIdx.x & 63;
+  const int64_t id = idx[r];
+  const bool ok = id >= 0 && id < rows;
+  const f32x4* src = reinterpret_cast<const f32x4*>(table + (ok ? id : 0) * (int64_t)dim);
+  const int d4 = dim >> 2;
+  for (int c = lane; c < d4; c += kWave) {
+    f32x4 v = ok ? src[c] : f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (OUT_BF16) {
+      u32x2 o{pack2(v[0], v[1]), pack2(v[2], v[3])};
+      reinterpret_cast<u32x2*>(static_cast<bf16_t*>(out) + r * (int64_t)dim)[c] = o;
+    } else {
+      reinterpret_cast<f32x4*>(static_cast<float*>(out) + r * (int64_t)dim)[c] = v;
+    }
+  }
+}
+
+template <bool IN_BF16>
+__global__ __launch_bounds__(kRowBlock) void embed_scatter_add_kernel(float* __restrict__ acc,
+                                                                      const int64_t* __restrict__ idx,
+                                                                      const void* __restrict__ grad, int64_t n,
+                                                                      int dim, int64_t rows) {
+  const int64_t r = (int64_t)blockIdx.x * (kRowBlock / kWave) + (threadIdx.x >> 6);
+  if (r >= n) return;
+  const int64_t id = idx[r];
+  if (id < 0 || id >= rows) return;
+  const int lane = threadIdx.x & 63;
+  float* dst = acc + id * (int64_t)dim;
+  const int d4 = dim >> 2;
+  for (int c = lane; c < d4; c += kWave) {
+    float g[4];
+    if constexpr (IN_BF16) {
+      u32x2 w = reinterpret_cast<const u32x2*>(static_cast<const bf16_t*>(grad) + r * (int64_t)dim)[c];
+      g[0] = bflo(w[0]); g[1] = bfhi(w[0]); g[2] = bflo(w[1]); g[3] = bfhi(w[1]);
+    } else {
+      f32x4 w = reinterpret_cast<const f32x4*>(static_cast<const float*>(grad) + r * (int64_t)dim)[c];
+      g[0] = w[0]; g[1] = w[1]; g[2] = w[2]; g[3] = w[3];
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) unsafeAtomicAdd(dst + 4 * c + j, g[j]);
+  }
+}
+
+struct SparseOpt {
+  int kind;  // 0 = AdamW, 1 = Adagrad, 2 = SGD
+  float lr, beta1, beta2, eps, wd, step_size, inv_bc2_sqrt, scale;
+};
+
+// Update table rows rows[u] with compact gradient grad[u, :].
+__global__ __launch_bounds__(kRowBlock) void sparse_rows_update_kernel(float* __restrict__ w, float* __restrict__ m,
+                                                                       float* __restrict__ v,
+                                                                       const int64_t* __restrict__ rows_idx,
+                                                                       const float* __restrict__ grad, int64_t nu,
+                                                                       int dim, int64_t rows, SparseOpt o) {
+  const int64_t u = (int64_t)blockIdx.x * (kRowBlock / kWave) + (threadIdx.x >> 6);
+  if (u >= nu) return;
+  const int64_t id = rows_idx[u];
+  if (id < 0 || id >= rows) return;
+  const int lane = threadIdx.x & 63;
+  const int d4 = dim >> 2;
+  f32x4* W = reinterpret_cast<f32x4*>(w + id * (int64_t)dim);
+  f32x4* M = m ? reinterpret_cast<f32x4*>(m + id * (int64_t)dim) : nullptr;
+  f32x4* V = v ? reinterpret_cast<f32x4*>(v + id * (int64_t)dim) : nullptr;
+  const f32x4* G = reinterpret_cast<const f32x4*>(grad + u * (int64_t)dim);
+  const float decay = 1.f - o.lr * o.wd;
+  for (int c = lane; c < d4; c += kWave) {
+    f32x4 g = G[c] * o.scale, p = W[c];
+    if (o.kind == 0) {
+      f32x4 mm = M[c], vv = V[c];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        mm[j] = o.beta1 * mm[j] + (1.f - o.beta1) * g[j];
+        vv[j] = o.beta2 * vv[j] + (1.f - o.beta2) * g[j] * g[j];
+        p[j] = p[j] * decay - o.step_size * mm[j] / (sqrtf(vv[j]) * o.inv_bc2_sqrt + o.eps);
+      }
+      M[c] = mm;
+      V[c] = vv;
+    } else if (o.kind == 1) {
+      f32x4 vv = V[c];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        vv[j] += g[j] * g[j];
+        p[j] = p[j] * decay - o.lr * g[j] / (sqrtf(vv[j]) + o.eps);
+      }
+      V[c] = vv;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) p[j] = p[j] * decay - o.lr * g[j];
+    }
+    W[c] = p;
+  }
+}
+
+// fp32 src (possibly a peer's IPC-mapped shard) -> bf16 dst, 8 elements per lane-iteration.
+__global__ __launch_bounds__(256) void pull_cast_kernel(const float* __restrict__ src, bf16_t* __restrict__ dst,
+                                                        int64_t n8) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += stride) {
+    const f32x4 a = reinterpret_cast<const f32x4*>(src)[2 * i];
+    const f32x4 b = reinterpret_cast<const f32x4*>(src)[2 * i + 1];
+    reinterpret_cast<u32x4*>(dst)[i] = u32x4{pack2(a[0], a[1]), pack2(a[2], a[3]), pack2(b[0], b[1]),
+                                             pack2(b[2], b[3])};
+  }
+}
+
+inline int row_blocks(int64_t n) { return (int)((n + (kRowBlock / kWave) - 1) / (kRowBlock / kWave)); }
+
+}  // namespace
+
+extern "C" {
+
+int edl_embed_gather(const float* table, const int64_t* idx, int64_t n, int dim, int64_t rows, void* out,
+                     int out_bf16, hipStream_t s) {
+  if (dim % 4 || n < 0 || rows < 1) return (int)hipErrorInvalidValue;
+  if (n == 0) return 0;
+  if (out_bf16)
+    embed_gather_kernel<true><<<row_blocks(n), kRowBlock, 0, s>>>(table, idx, n, dim, rows, out);
+  else
+    embed_gather_kernel<false><<<row_blocks(n), kRowBlock, 0, s>>>(table, idx, n, dim, rows, out);
+  EDL_LAUNCH_CHECK();
+  return 0;
+}
+
+int edl_embed_scatter_add(float* acc, const int64_t* idx, const void* grad, int grad_bf16, int64_t n, int dim,
+                          int64_t rows, hipStream_t s) {
+  if (dim % 4 || n < 0 || rows < 1) return (int)hipErrorInvalidValue;
+  if (n == 0) return 0;
+  if (grad_bf16)
+    embed_scatter_add_kernel<true><<<row_blocks(n), kRowBlock, 0, s>>>(acc, idx, grad, n, dim, rows);
+  else
+    embed_scatter_add_kernel<false><<<row_blocks(n), kRowBlock, 0, s>>>(acc, idx, grad, n, dim, rows);
+  EDL_LAUNCH_CHECK();
+  return 0;
+}
+
+// kind: 0 AdamW (m, v required), 1 Adagrad (v required), 2 SGD.  `step` is the
+// table's update count after this update (bias correction of lazy Adam).
+int edl_sparse_rows_update(float* w, float* m, float* v, const int64_t* rows_idx, const float* grad, int64_t nu,
+                           int dim, int64_t rows, int kind, float lr, float beta1, float beta2, float eps, float wd,
+                           int64_t step, float scale, hipStream_t s) {
+  if (dim % 4 || nu < 0 || kind < 0 || kind > 2) return (int)hipErrorInvalidValue;
+  if ((kind == 0 && (!m || !v)) || (kind == 1 && !v)) return (int)hipErrorInvalidValue;
+  if (nu == 0) return 0;
+  SparseOpt o{kind, lr, beta1, beta2, eps, wd, lr, 1.f, scale};
+  if (kind == 0) {
+    o.step_size = lr / (1.f - powf(beta1, (float)step));
+    o.inv_bc2_sqrt = 1.f / sqrtf(1.f - powf(beta2, (float)step));
+  }
+  sparse_rows_update_kernel<<<row_blocks(nu), kRowBlock, 0, s>>>(w, m, v, rows_idx, grad, nu, dim, rows, o);
+  EDL_LAUNCH_CHECK();
+  return 0;
+}
+
+int edl_ps_pull_cast(const float* src, void* dst, int64_t n, hipStream_t s) {
+  if (n % 8) return (int)hipErrorInvalidValue;
+  const int64_t n8 = n / 8;
+  if (n8 == 0) return 0;
+  int64_t blocks = (n8 + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  pull_cast_kernel<<<(int)blocks, 256, 0, s>>>(src, (bf16_t*)dst, n8);
+  EDL_LAUNCH_CHECK();
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,120 @@
+"""Row-sparse parameter-server ops (csrc/kernels/ps_sparse.hip).
+
+* :func:`embed_gather`        rows of an fp32 table -> fp32/bf16 [n, dim] (PS pull)
+* :func:`segment_sum_rows`    duplicate ids -> (unique ids, compact fp32 grad) (PS push)
+* :func:`sparse_rows_update`  lazy AdamW / Adagrad / SGD on the touched rows only
+* :func:`pull_cast`           fp32 shard -> bf16 worker copy (dense pull)
+
+GPU tensors run the HIP kernels; CPU tensors run the same math in PyTorch
+(that is the CPU/gloo PS path and the numerics reference of the GPU tests).
+Out-of-range ids gather a zero row and are dropped on scatter, on both paths.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from easydl_amd import _native
+
+OPT_KIND = {"adam": 0, "adamw": 0, "adagrad": 1, "sgd": 2}
+
+
+def _check_rows(table: torch.Tensor) -> None:
+    if table.dim() != 2 or table.dtype != torch.float32 or not table.is_contiguous() or table.shape[1] % 4:
+        raise ValueError("embedding tables are contiguous fp32 [rows, dim] with dim % 4 == 0")
+
+
+def embed_gather(table: torch.Tensor, ids: torch.Tensor, out_dtype=torch.float32) -> torch.Tensor:
+    _check_rows(table)
+    ids = ids.reshape(-1).to(torch.int64)
+    rows, dim = table.shape
+    if _native.use_hip(table):
+        ids = ids.to(table.device).contiguous()
+        out = torch.empty(ids.numel(), dim, dtype=out_dtype, device=table.device)
+        _native.kernels().check("edl_embed_gather", table.data_ptr(), ids.data_ptr(), ids.numel(), dim, rows,
+                                out.data_ptr(), 1 if out_dtype == torch.bfloat16 else 0,
+                                _native.stream_of(table))
+        return out
+    ok = (ids >= 0) & (ids < rows)
+    out = table[ids.clamp(0, rows - 1)] * ok.unsqueeze(1)
+    return out.to(out_dtype)
+
+
+def scatter_add_rows(acc: torch.Tensor, ids: torch.Tensor, grad: torch.Tensor) -> torch.Tensor:
+    """acc[ids[i]] += grad[i] (duplicates accumulate; out-of-range ids are dropped)."""
+    _check_rows(acc)
+    ids = ids.reshape(-1).to(torch.int64)
+    grad = grad.reshape(ids.numel(), acc.shape[1])
+    if _native.use_hip(acc):
+        ids = ids.to(acc.device).contiguous()
+        grad = grad.to(acc.device).contiguous()
+        if grad.dtype not in (torch.float32, torch.bfloat16):
+            grad = grad.float()
+        _native.kernels().check("edl_embed_scatter_add", acc.data_ptr(), ids.data_ptr(), grad.data_ptr(),
+                                1 if grad.dtype == torch.bfloat16 else 0, ids.numel(), acc.shape[1], acc.shape[0],
+                                _native.stream_of(acc))
+        return acc
+    ok = (ids >= 0) & (ids < acc.shape[0])
+    acc.index_add_(0, ids[ok], grad[ok].float())
+    return acc
+
+
+def segment_sum_rows(ids: torch.Tensor, grad: torch.Tensor, rows: int) -> tuple[torch.Tensor, torch.Tensor]:
+    """(unique valid ids, fp32 [n_unique, dim] sums of their gradient rows)."""
+    ids = ids.reshape(-1).to(torch.int64)
+    dim = grad.shape[-1]
+    grad = grad.reshape(ids.numel(), dim)
+    ok = (ids >= 0) & (ids < rows)
+    if not bool(ok.all()):
+        ids, grad = ids[ok], grad[ok]
+    uniq, inv = torch.unique(ids, return_inverse=True)
+    compact = torch.zeros(uniq.numel(), dim, dtype=torch.float32, device=grad.device)
+    if uniq.numel():
+        scatter_add_rows(compact, inv, grad)
+    return uniq, compact
+
+
+def sparse_rows_update(w: torch.Tensor, m: torch.Tensor | None, v: torch.Tensor | None, uniq: torch.Tensor,
+                       grad: torch.Tensor, *, kind: str = "adam", lr: float, beta1: float = 0.9,
+                       beta2: float = 0.999, eps: float = 1e-8, weight_decay: float = 0.0, step: int = 1,
+                       scale: float = 1.0) -> None:
+    """Lazy optimizer update of rows ``uniq`` (unique ids) with ``grad[i]`` for ``uniq[i]``."""
+    _check_rows(w)
+    k = OPT_KIND[kind]
+    if _native.use_hip(w):
+        _native.kernels().check("edl_sparse_rows_update", w.data_ptr(), _native.ptr(m), _native.ptr(v),
+                                uniq.data_ptr(), grad.contiguous().data_ptr(), uniq.numel(), w.shape[1], w.shape[0],
+                                k, lr, beta1, beta2, eps, weight_decay, int(step), float(scale),
+                                _native.stream_of(w))
+        return
+    if uniq.numel() == 0:
+        return
+    g = grad.float() * scale
+    p = w[uniq]
+    decay = 1.0 - lr * weight_decay
+    if k == 0:
+        mm = m[uniq].mul_(beta1).add_(g, alpha=1 - beta1)
+        vv = v[uniq].mul_(beta2).addcmul_(g, g, value=1 - beta2)
+        denom = vv.sqrt() / math.sqrt(1 - beta2 ** step) + eps
+        p = p * decay - (lr / (1 - beta1 ** step)) * mm / denom
+        m[uniq], v[uniq] = mm, vv
+    elif k == 1:
+        vv = v[uniq] + g * g
+        p = p * decay - lr * g / (vv.sqrt() + eps)
+        v[uniq] = vv
+    else:
+        p = p * decay - lr * g
+    w[uniq] = p
+
+
+def pull_cast(src: torch.Tensor, dst: torch.Tensor) -> torch.Tensor:
+    """dst (bf16) <- src (fp32); the src pointer may be an IPC-mapped peer shard."""
+    if dst.is_cuda:
+        if src.numel() != dst.numel() or src.numel() % 8:
+            raise ValueError("pull_cast: equal sizes, multiple of 8 elements")
+        _native.kernels().check("edl_ps_pull_cast", src.data_ptr(), dst.data_ptr(), src.numel(),
+                                _native.stream_of(dst))
+        return dst
+    dst.copy_(src)
+    return dst

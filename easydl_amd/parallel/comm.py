@@ -46,6 +46,9 @@ class Communicator:
         self.device = torch.device(device)
         self.tag = tag
         self.rccl = None
+        self.xgmi = None
+        self.xgmi_mode = None
+        self.xgmi_probe: dict | None = None
         self._aborted = False
         self._lock = threading.Lock()
         t0 = time.perf_counter()
@@ -62,11 +65,19 @@ class Communicator:
             self.rccl = RcclComm(base, "data", rank, world_size, self.device, timeout_s=timeout_s)
             self.backend = "rccl-native"
         elif self.device.type == "cuda":
+            if data_backend in ("xgmi", "auto") and world_size > 1:
+                # csrc/kernels/xgmi.hip: abortable one-/two-shot all-reduce over IPC-mapped
+                # peer buffers; RCCL keeps the other collectives (and all-reduce in "auto"
+                # until warmup() has measured both on this node)
+                from easydl_amd.parallel.xgmi import XgmiComm
+                self.xgmi = XgmiComm(dist.PrefixStore("xgmi", base), "ws", rank, world_size, self.device,
+                                     timeout_s=timeout_s)
+                self.xgmi_mode = data_backend
             opts = dist.ProcessGroupNCCL.Options()
             opts.is_high_priority_stream = high_priority
             opts._timeout = _td(timeout_s)
             self.data = dist.ProcessGroupNCCL(dist.PrefixStore("data", base), rank, world_size, opts)
-            self.backend = "rccl"
+            self.backend = "rccl+xgmi" if self.xgmi_mode == "xgmi" else "rccl"
         else:
             self.data = dist.ProcessGroupGloo(dist.PrefixStore("data", base), rank, world_size, _td(timeout_s))
             self.backend = "gloo"
@@ -85,7 +96,54 @@ class Communicator:
             if self.device.type == "cuda":
                 torch.cuda.synchronize(self.device)
         self.ctrl.allreduce([torch.zeros(1)]).wait()
+        if self.xgmi is not None and self.xgmi_mode == "auto":
+            self._probe_xgmi()
         return time.perf_counter() - t0
+
+    def _probe_xgmi(self, mb: int = 64, iters: int = 5) -> None:
+        """Measure the xGMI engine against RCCL on a gradient-bucket-sized message on
+        THIS node and keep it only if every rank saw an exact result and it was
+        faster everywhere (integer-valued data: both sums are exact)."""
+        n = (mb << 20) // 2
+        g = torch.Generator(device="cpu").manual_seed(7 + self.rank)
+        src = torch.randint(-4, 5, (n,), generator=g, dtype=torch.int8).to(self.device, torch.bfloat16)
+        a, b = src.clone(), src.clone()
+        self.data.allreduce([a]).wait()
+        keep_timeout, self.xgmi.timeout_s = self.xgmi.timeout_s, 5.0  # a broken path gives up fast
+        self.xgmi.all_reduce(b)
+        torch.cuda.synchronize(self.device)
+        self.xgmi.timeout_s = keep_timeout
+        bad = 0.0 if (torch.equal(a, b) and self.xgmi.status() == 0) else 1.0
+
+        def timed(fn):
+            t = src.clone()
+            fn(t)
+            torch.cuda.synchronize(self.device)
+            t0 = time.perf_counter()
+            for _ in range(iters):
+                fn(t)
+            torch.cuda.synchronize(self.device)
+            return (time.perf_counter() - t0) / iters
+
+        t_rccl = timed(lambda t: self.data.allreduce([t]).wait())
+        t_xgmi = timed(self.xgmi.all_reduce) if not bad else float("inf")
+        worst = self.ctrl_all_reduce([bad, min(t_xgmi - t_rccl, 1e9)], dist.ReduceOp.MAX)
+        keep = worst[0] == 0 and worst[1] < 0
+        self.xgmi_probe = {"mb": mb, "rccl_ms": round(t_rccl * 1e3, 3), "xgmi_ms": round(t_xgmi * 1e3, 3),
+                           "exact_everywhere": bool(worst[0] == 0), "selected": "xgmi" if keep else "rccl"}
+        log.info("all-reduce probe (epoch %d, world %d): %s", self.epoch, self.world_size, self.xgmi_probe)
+        if keep:
+            self.xgmi_mode = "xgmi"
+            self.backend = "rccl+xgmi"
+        else:
+            torch.cuda.synchronize(self.device)
+            self.xgmi.close()
+            self.xgmi = None
+
+    def healthy(self) -> bool:
+        """False if a hand-written collective gave up (abort word / deadline) since the
+        epoch started; read after the step's host sync, so it costs one 4-byte copy."""
+        return self.xgmi is None or self.xgmi.status() == 0
 
     def abort(self) -> None:
         """Abort in-flight collectives (callable from a watchdog thread)."""
@@ -97,9 +155,11 @@ class Communicator:
         # collectives already fail as soon as a peer's sockets close, and
         # ProcessGroupGloo.abort() leaves worker threads that std::terminate the
         # process at teardown, so gloo groups are only marked, never aborted.
+        if self.xgmi is not None:
+            self.xgmi.abort()  # host-mapped abort word: spinning workgroups exit
         if self.rccl is not None:
             self.rccl.abort()
-        elif self.backend == "rccl":
+        elif self.backend.startswith("rccl"):
             try:
                 self.data.abort()
             except Exception as e:  # pragma: no cover - best effort
@@ -114,6 +174,9 @@ class Communicator:
             return
         if self.rccl is not None:
             self.rccl.destroy()
+        if self.xgmi is not None:
+            self.xgmi.close()
+            self.xgmi = None
         for pg in (self.data, self.ctrl):
             if pg is None:
                 continue
@@ -129,6 +192,8 @@ class Communicator:
             raise CommAborted("communicator aborted")
         if self.rccl is not None:
             return self._native(self.rccl.all_reduce_async, t, op)
+        if self.xgmi is not None and self.xgmi_mode == "xgmi" and op == dist.ReduceOp.SUM and self.xgmi.supports(t):
+            return self._native(self.xgmi.all_reduce_async, t)
         o = dist.AllreduceOptions()
         o.reduceOp = op
         return self.data.allreduce([t], o)
@@ -258,6 +323,9 @@ class MeshComm:
         for c in (self.dp, self.tp, self.world):
             c.abort()
 
+    def healthy(self) -> bool:
+        return all(c.healthy() for c in (self.world, self.tp, self.dp))
+
     def shutdown(self) -> None:
         for c in (self.dp, self.tp, self.world):
             c.shutdown()
@@ -306,6 +374,9 @@ class LocalCommunicator:
 
     def abort(self):
         self.aborted = True
+
+    def healthy(self):
+        return True
 
     def shutdown(self):
         pass

@@ -25,6 +25,19 @@ class XgmiError(RuntimeError):
     pass
 
 
+class _Work:
+    def __init__(self, event: torch.cuda.Event, keep):
+        self._event, self._keep = event, keep
+
+    def wait(self, *a, **k):
+        torch.cuda.current_stream().wait_event(self._event)
+        self._keep = None
+        return True
+
+    def is_completed(self):
+        return self._event.query()
+
+
 class XgmiComm:
     ONESHOT_MAX = 512 << 10      # bytes: below this latency dominates -> one-shot
 
@@ -59,6 +72,7 @@ class XgmiComm:
         self.round = 0
         self.blocks = min(self._k("edl_xgmi_max_blocks"), 256)
         self._aborted = False
+        self.stream = torch.cuda.Stream(self.device, priority=-1)
 
     def abort(self) -> None:
         """From any thread: every spinning workgroup of every in-flight call exits."""
@@ -99,6 +113,23 @@ class XgmiComm:
             if rc != 0:
                 raise XgmiError(f"launch failed: hipError {rc}")
         return t
+
+    def all_reduce_async(self, t: torch.Tensor) -> "_Work":
+        """In-place SUM on the engine's own high-priority stream, ordered after the
+        caller's stream; ``wait()`` orders the caller's stream after it (the
+        ``ProcessGroupNCCL`` work contract ElasticDDP overlaps with backward)."""
+        self.stream.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(self.stream):
+            self.all_reduce(t)
+        t.record_stream(self.stream)
+        ev = torch.cuda.Event()
+        ev.record(self.stream)
+        return _Work(ev, t)
+
+    @staticmethod
+    def supports(t: torch.Tensor) -> bool:
+        return (t.is_cuda and t.dtype in (torch.float32, torch.bfloat16) and t.is_contiguous()
+                and (t.numel() * t.element_size()) % 16 == 0)
 
     def close(self) -> None:
         if self._ws is not None:

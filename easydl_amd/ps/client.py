@@ -30,9 +30,17 @@ def partition(named_sizes: list[tuple[str, int]], num_ps: int) -> dict[str, int]
     return out
 
 
+def dense_params(model: torch.nn.Module) -> dict[str, torch.Tensor]:
+    """Named parameters that the PS serves densely (row-sparse PSEmbedding tables excluded)."""
+    from easydl_amd.ps.embedding import tables_of
+    skip = {f"{n}.weight" for n in tables_of(model)}
+    return {n: p for n, p in model.named_parameters() if n not in skip}
+
+
 def shard_of(model: torch.nn.Module, num_ps: int, index: int) -> dict[str, torch.Tensor]:
-    assign = partition([(n, p.numel()) for n, p in model.named_parameters()], num_ps)
-    return {n: p.detach() for n, p in model.named_parameters() if assign[n] == index}
+    params = dense_params(model)
+    assign = partition([(n, p.numel()) for n, p in params.items()], num_ps)
+    return {n: p.detach() for n, p in params.items() if assign[n] == index}
 
 
 class PSClient:
@@ -47,9 +55,47 @@ class PSClient:
         self._pool = ThreadPoolExecutor(max_workers=max(1, num_ps))
         self.versions = [0] * num_ps
         self.assign: dict[str, int] = {}
+        self.tables: dict = {}
+        self.rows_bf16 = False  # pull embedding rows as bf16 (halves the wire bytes)
 
     def bind(self, model: torch.nn.Module) -> None:
-        self.assign = partition([(n, p.numel()) for n, p in model.named_parameters()], self.num_ps)
+        from easydl_amd.ps.embedding import tables_of
+        self.assign = partition([(n, p.numel()) for n, p in dense_params(model).items()], self.num_ps)
+        self.tables = tables_of(model)
+        for n, m in self.tables.items():
+            m.attach(self, n)
+
+    # -- row-sparse tables ---------------------------------------------------------
+    def _split_rows(self, ids: torch.Tensor):
+        ids = ids.reshape(-1).to(torch.int64)
+        owner = ids % self.num_ps
+        return [(i, (owner == i).nonzero().view(-1)) for i in range(self.num_ps)], ids
+
+    def pull_rows(self, table: str, ids: torch.Tensor) -> torch.Tensor:
+        """Rows ``ids`` (global) of ``table`` from their owning shards, fp32 [n, dim] on ids' device."""
+        m = self.tables[table]
+        parts, flat = self._split_rows(ids.cpu())
+        out = torch.empty(flat.numel(), m.dim, dtype=torch.float32)
+
+        def one(arg):
+            i, pos = arg
+            if pos.numel() == 0:
+                return
+            h, ts = self._call(i, {"op": "pull_rows", "table": table, "bf16": self.rows_bf16},
+                               {"ids": flat[pos] // self.num_ps})
+            out[pos] = ts["rows"].float()
+
+        list(self._pool.map(one, parts))
+        return out.to(ids.device)
+
+    def _sparse_grads(self, i: int, grads_by_table: dict) -> dict[str, torch.Tensor]:
+        out = {}
+        for n, (parts, flat, g) in grads_by_table.items():
+            pos = parts[i][1]
+            if pos.numel():
+                out[f"sparse/{n}/ids"] = flat[pos] // self.num_ps
+                out[f"sparse/{n}/grad"] = g[pos]
+        return out
 
     def _call(self, i: int, header: dict, tensors=None):
         t_end = time.monotonic() + self.retry_s
@@ -90,9 +136,15 @@ class PSClient:
 
     def push(self, model: torch.nn.Module, step: int = 0) -> list[int]:
         params = dict(model.named_parameters())
+        sparse_grads = {}
+        for n, m in self.tables.items():
+            got = m.take_grads()
+            if got is not None:
+                parts, flat = self._split_rows(got[0].cpu())
+                sparse_grads[n] = (parts, flat, got[1].detach().cpu())
 
         def one(i):
-            grads = {}
+            grads = self._sparse_grads(i, sparse_grads)
             for n, j in self.assign.items():
                 if j == i:
                     g = params[n].grad

@@ -23,11 +23,13 @@ from __future__ import annotations
 
 import logging
 import socket
+import zlib
 import threading
 import time
 
 import torch
 
+from easydl_amd.ops import sparse
 from easydl_amd.ops.optim import adamw_flat_, sgd_flat_
 from easydl_amd.ps.wire import recv_msg, send_msg
 
@@ -66,13 +68,41 @@ class ShardState:
         return {n: self.view(buf, n) for n in (names or self.names)}
 
 
+class TableShard:
+    """This PS's stripe of a row-sparse embedding table (fp32 rows + lazy optimizer state)."""
+
+    def __init__(self, name: str, rows: int, dim: int, init_std: float, index: int, device, seed: int = 1234):
+        self.name, self.rows, self.dim = name, max(1, rows), dim
+        g = torch.Generator(device="cpu").manual_seed(seed * 1000003 + zlib.crc32(name.encode()) * 31 + index)
+        self.w = (torch.randn(self.rows, dim, generator=g) * init_std).to(device)
+        self.m = torch.zeros_like(self.w)
+        self.v = torch.zeros_like(self.w)
+        self.step = 0
+        self.pending: list[tuple[torch.Tensor, torch.Tensor]] = []  # sync mode: (ids, grads) of the round
+
+    def apply(self, ids: torch.Tensor, grads: torch.Tensor, *, kind: str, lr: float, betas, eps: float,
+              wd: float, scale: float) -> None:
+        ids = ids.to(self.w.device)
+        grads = grads.to(self.w.device)
+        uniq, comp = sparse.segment_sum_rows(ids, grads, self.rows)
+        self.step += 1
+        sparse.sparse_rows_update(self.w, self.m, self.v, uniq, comp, kind=kind, lr=lr, beta1=betas[0],
+                                  beta2=betas[1], eps=eps, weight_decay=wd, step=self.step, scale=scale)
+
+
 class ParameterServer:
     def __init__(self, index: int, tensors: dict[str, torch.Tensor], *, optimizer: str = "adam", lr: float = 1e-3,
                  betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0, momentum: float = 0.9,
                  mode: str = "async", expected_workers=None, host: str = "127.0.0.1", port: int = 0,
-                 device="cpu", snapshot=None, snapshot_every: int = 50):
+                 device="cpu", snapshot=None, snapshot_every: int = 50, tables: dict[str, dict] | None = None,
+                 sparse_optimizer: str | None = None, sparse_lr: float | None = None, seed: int = 1234):
         self.index = index
         self.state = ShardState(tensors, device)
+        # row-sparse embedding stripes (easydl_amd/ps/embedding.py), lazily updated
+        self.tables = {n: TableShard(n, t["rows"], t["dim"], t.get("init_std", 0.01), index, device, seed)
+                       for n, t in (tables or {}).items()}
+        self.sparse_optimizer = sparse_optimizer or ("adam" if optimizer == "adam" else "sgd")
+        self.sparse_lr = lr if sparse_lr is None else sparse_lr
         self.optimizer, self.lr, self.betas, self.eps = optimizer, lr, betas, eps
         self.wd, self.momentum = weight_decay, momentum
         self.mode = mode
@@ -103,17 +133,38 @@ class ParameterServer:
             sgd_flat_(None, st.w, st.m if self.momentum else None, st.g, lr=self.lr, momentum=self.momentum,
                       weight_decay=self.wd, scale=scale)
         st.g.zero_()
+        for t in self.tables.values():
+            if t.pending:
+                ids = torch.cat([i for i, _ in t.pending])
+                grads = torch.cat([g for _, g in t.pending])
+                t.pending = []
+                self._apply_table(t, ids, grads, scale)
         self.version += 1
         self.stats["applied"] += 1
         if self.snapshot is not None and self.version % self.snapshot_every == 0:
             self.snapshot(self)
         self.lock.notify_all()
 
+    def _apply_table(self, t: TableShard, ids, grads, scale: float) -> None:
+        t.apply(ids, grads, kind=self.sparse_optimizer, lr=self.sparse_lr, betas=self.betas, eps=self.eps, wd=0.0,
+                scale=scale)
+
     def _push(self, worker: str, grads: dict[str, torch.Tensor]) -> int:
         with self.lock:
             st = self.state
             for n, g in grads.items():
+                if n.startswith("sparse/"):
+                    continue
                 st.view(st.g, n).add_(g.to(st.device, torch.float32))
+            for n, t in self.tables.items():
+                ids = grads.get(f"sparse/{n}/ids")
+                if ids is None or ids.numel() == 0:
+                    continue
+                g = grads[f"sparse/{n}/grad"]
+                if self.mode == "async":
+                    self._apply_table(t, ids, g, 1.0)
+                else:
+                    t.pending.append((ids.to(t.w.device), g.to(t.w.device, torch.float32)))
             self.stats["pushes"] += 1
             self.stats["workers"].add(worker)
             if self.mode == "async":
@@ -151,18 +202,28 @@ class ParameterServer:
                         out = {n: t.clone() for n, t in self.state.tensors(names=hdr.get("names")).items()}
                         ver = self.version
                     send_msg(conn, {"ok": True, "version": ver}, out)
+                elif op == "pull_rows":
+                    t = self.tables[hdr["table"]]
+                    ids = tensors["ids"].to(t.w.device)
+                    dt = torch.bfloat16 if hdr.get("bf16") else torch.float32
+                    with self.lock:
+                        rows = sparse.embed_gather(t.w, ids, out_dtype=dt)
+                        ver = self.version
+                    self.stats["pulls"] += 1
+                    send_msg(conn, {"ok": True, "version": ver}, {"rows": rows})
                 elif op == "push":
                     ver = self._push(hdr.get("worker", "?"), tensors)
                     send_msg(conn, {"ok": True, "version": ver})
                 elif op == "state":
                     with self.lock:
-                        st = self.state
-                        out = {"w": st.w.clone(), "m": st.m.clone(), "v": st.v.clone()}
-                        meta = {"version": self.version, "step": self.step}
+                        out = {f"b{i}": b.clone() for i, b in enumerate(self.state_buffers())}
+                        meta = {"version": self.version, "step": self.step,
+                                "table_steps": [t.step for t in self.tables.values()]}
                     send_msg(conn, {"ok": True, **meta}, out)
                 elif op == "load":
                     with self.lock:
-                        self.load(tensors["w"], tensors["m"], tensors["v"], hdr["version"], hdr["step"])
+                        self.load([tensors[f"b{i}"] for i in range(len(tensors))], hdr["version"], hdr["step"],
+                                  hdr.get("table_steps"))
                     send_msg(conn, {"ok": True})
                 elif op == "stats":
                     s = dict(self.stats)
@@ -177,11 +238,19 @@ class ParameterServer:
         finally:
             conn.close()
 
-    def load(self, w, m, v, version, step):
+    def state_buffers(self) -> list[torch.Tensor]:
+        """Every fp32 state buffer in a fixed order: dense w, m, v, then per table w, m, v."""
         st = self.state
-        st.w.copy_(w)
-        st.m.copy_(m)
-        st.v.copy_(v)
+        out = [st.w, st.m, st.v]
+        for t in self.tables.values():
+            out += [t.w.view(-1), t.m.view(-1), t.v.view(-1)]
+        return out
+
+    def load(self, bufs, version, step, table_steps=None):
+        for dst, src in zip(self.state_buffers(), bufs):
+            dst.copy_(src.reshape(dst.shape))
+        for t, k in zip(self.tables.values(), table_steps or []):
+            t.step = int(k)
         self.version, self.step = int(version), int(step)
 
     def start(self) -> "ParameterServer":
@@ -226,17 +295,19 @@ class PSSnapshotter:
 
     def __call__(self, ps: ParameterServer) -> None:
         from easydl_amd.ckpt.manager import ShmSegment, checksum_np
-        st = ps.state
-        nbytes = st.w.numel() * 4
+        bufs = ps.state_buffers()
+        sizes = [b.numel() * 4 for b in bufs]
         if self.seg is None:
-            self.seg = ShmSegment(self.name, 3 * nbytes, create=True, pin=False)
+            self.seg = ShmSegment(self.name, sum(sizes), create=True, pin=False)
         slot = self.seg.begin()
-        total = 0
-        for i, buf in enumerate((st.w, st.m, st.v)):
+        total, off = 0, 0
+        for buf, nb in zip(bufs, sizes):
             arr = buf.detach().cpu().contiguous().view(torch.uint8).numpy()
-            self.seg.view(slot, i * nbytes, nbytes)[:] = arr
-            total += checksum_np(arr, i * nbytes // 4)
-        self.seg.commit(slot, ps.version, ps.step, 3 * nbytes, total, {"n": st.w.numel(), "step": ps.step})
+            self.seg.view(slot, off, nb)[:] = arr
+            total += checksum_np(arr, off // 4)
+            off += nb
+        self.seg.commit(slot, ps.version, ps.step, off, total,
+                        {"sizes": sizes, "step": ps.step, "table_steps": [t.step for t in ps.tables.values()]})
 
     def restore(self, ps: ParameterServer) -> bool:
         from easydl_amd.ckpt.manager import ShmSegment, checksum_np
@@ -249,19 +320,19 @@ class PSSnapshotter:
             if not infos:
                 return False
             info = max(infos, key=lambda i: i["step"])
-            n = info["meta"]["n"]
-            if n != ps.state.w.numel():
+            sizes = info["meta"].get("sizes")
+            if sizes != [b.numel() * 4 for b in ps.state_buffers()]:
                 return False
-            nbytes = n * 4
-            bufs, total = [], 0
-            for i in range(3):
-                raw = seg.view(info["slot"], i * nbytes, nbytes)
-                total += checksum_np(raw, i * nbytes // 4)
+            bufs, total, off = [], 0, 0
+            for nb in sizes:
+                raw = seg.view(info["slot"], off, nb)
+                total += checksum_np(raw, off // 4)
                 bufs.append(torch.from_numpy(raw.copy()).view(torch.float32))
+                off += nb
             if (total & ((1 << 64) - 1)) != info["checksum"]:
                 log.error("PS snapshot checksum mismatch: ignoring")
                 return False
-            ps.load(*bufs, info["step"], info["meta"]["step"])
+            ps.load(bufs, info["step"], info["meta"]["step"], info["meta"].get("table_steps"))
             return True
         finally:
             seg.close()

@@ -380,7 +380,13 @@ class ElasticTrainer:
         """Host-side completion of every gradient all-reduce; False if the epoch broke."""
         if self.device.type == "cuda":
             torch.cuda.current_stream(self.device).synchronize()
-        return not self.comm.aborted
+        if self.comm.aborted:
+            return False
+        if not self.comm.healthy():  # a hand-written collective hit its deadline: the grads are not a sum
+            log.warning("epoch %d: a bounded collective gave up; dropping step %d", self.comm.epoch, self.step)
+            self.comm.abort()
+            return False
+        return True
 
     def fit(self, loss_fn, data, num_steps: int, on_step=None) -> "ElasticTrainer":
         """Train until ``num_steps`` committed steps.  ``loss_fn(model, batch) -> scalar loss``."""

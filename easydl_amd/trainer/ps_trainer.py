@@ -21,6 +21,7 @@ from easydl_amd.master.dispatcher import ShardDispatcher
 from easydl_amd.master.rendezvous import RendezvousClient
 from easydl_amd.master.store import KV, make_tcp_store
 from easydl_amd.ps.client import PSClient, shard_of, store_resolver
+from easydl_amd.ps.embedding import table_shard_spec
 from easydl_amd.ps.server import ParameterServer, PSSnapshotter
 from easydl_amd.trainer.context import TrainerContext
 from easydl_amd.utils import fault
@@ -40,7 +41,8 @@ def _world(kv) -> int:
 
 
 def run_ps(model_fn, num_ps: int, ctx: TrainerContext | None = None, *, optimizer="adam", lr=1e-3, mode="async",
-           snapshot_every: int = 20, device="cpu", seed: int = 1234) -> None:
+           snapshot_every: int = 20, device="cpu", seed: int = 1234, sparse_optimizer: str | None = None,
+           sparse_lr: float | None = None) -> None:
     ctx = ctx or TrainerContext.from_env()
     kv = _kv(ctx)
     events = EventLog(os.path.join(ctx.run_dir, f"events-ps{ctx.index}.jsonl"), proc=f"ps{ctx.index}")
@@ -49,7 +51,9 @@ def run_ps(model_fn, num_ps: int, ctx: TrainerContext | None = None, *, optimize
     snap = PSSnapshotter(ctx.job, ctx.index)
     ps = ParameterServer(ctx.index, shard_of(model, num_ps, ctx.index), optimizer=optimizer, lr=lr, mode=mode,
                          expected_workers=lambda: _world(kv), device=device, snapshot=snap,
-                         snapshot_every=snapshot_every)
+                         snapshot_every=snapshot_every, tables=table_shard_spec(model, num_ps, ctx.index),
+                         sparse_optimizer=sparse_optimizer, sparse_lr=sparse_lr, seed=seed)
+    del model  # the PS keeps only its shard
     if snap.restore(ps):
         events.emit("ps_restored", version=ps.version)
     ps.start()

@@ -1,0 +1,55 @@
+"""One rank of the Communicator(data_backend="xgmi") test: ElasticDDP-style
+bucket all-reduces go through the xGMI engine's async path (its own stream,
+event-ordered), and a give-up is reported by healthy().  All ranks share one
+GPU, so no RCCL collective is issued (RCCL refuses two ranks on one device)."""
+import datetime
+import json
+import os
+import sys
+import threading
+
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+from easydl_amd.parallel.comm import Communicator  # noqa: E402
+
+rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+mode = os.environ.get("XG_MODE", "sum")
+torch.cuda.set_device(0)
+store = dist.TCPStore("127.0.0.1", int(os.environ["PORT"]), world, rank == 0,
+                      timeout=datetime.timedelta(seconds=60))
+c = Communicator(store, rank, world, 3, device=torch.device("cuda", 0), job="t", timeout_s=5.0, data_backend="xgmi")
+res = {"rank": rank, "ok": True, "errors": [], "backend": c.backend}
+if mode == "sum":
+    grads = torch.empty(3 * (1 << 20) + 4096, device="cuda", dtype=torch.bfloat16)
+    buckets = [grads[:4096], grads[4096:4096 + (1 << 20)], grads[4096 + (1 << 20):]]
+    for it in range(3):
+        g = torch.Generator(device="cpu").manual_seed(100 * it + rank)
+        grads.copy_(torch.randint(-8, 8, grads.shape, generator=g).to(torch.bfloat16))
+        exp = torch.zeros(grads.numel(), dtype=torch.float64)
+        for r in range(world):
+            exp += torch.randint(-8, 8, grads.shape, generator=torch.Generator().manual_seed(100 * it + r)).double()
+        works = [c.all_reduce_async(b) for b in buckets]  # issued in bucket order, overlapping
+        for w in works:
+            w.wait()
+        torch.cuda.current_stream().synchronize()
+        if not torch.equal(grads.double().cpu(), exp):
+            res["ok"] = False
+            res["errors"].append(f"iter {it}: max err {(grads.double().cpu() - exp).abs().max().item()}")
+    res["healthy"] = c.healthy()
+elif mode == "abort":
+    if rank == 0:  # the peer never joins: the watchdog's abort() releases the kernel, healthy() says so
+        t = torch.ones(1 << 16, device="cuda", dtype=torch.bfloat16)
+        threading.Timer(1.0, c.abort).start()
+        w = c.all_reduce_async(t)
+        w.wait()
+        torch.cuda.synchronize()
+        res["healthy"] = c.healthy()
+        res["aborted"] = c.aborted
+    store.set(f"done{rank}", "1")
+    store.wait([f"done{r}" for r in range(world)])
+print(json.dumps(res), flush=True)
+with open(os.environ["OUT"] + f".{rank}", "w") as f:
+    json.dump(res, f)
+c.xgmi.close()

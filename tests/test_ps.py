@@ -120,3 +120,52 @@ def test_mnist_ps_job_with_worker_and_ps_failures(tmp_path):
     assert done == set(range((12000 + 511) // 512)), sorted(done)   # every shard exactly covered
     evals = [e for e in ev if e["kind"] == "eval"]
     assert evals and evals[-1]["acc"] > 0.6, evals[-1:]
+
+
+@pytest.mark.parametrize("mode", ["async", "sync"])
+def test_deepfm_sparse_tables_on_ps(mode):
+    """DeepFM with row-striped embedding tables: workers hold no table, pull only the
+    rows a batch touches, push de-duplicated row grads; the PS applies lazy Adagrad."""
+    from easydl_amd.models.deepctr import DeepFM, SyntheticCTR, auc
+    from easydl_amd.ps.embedding import table_shard_spec
+    torch.manual_seed(0)
+    vocab = 500
+    data = SyntheticCTR(40000, vocab=vocab)
+    ref = DeepFM(vocab=vocab, hidden=(64, 64))
+    servers = [ParameterServer(i, shard_of(ref, 2, i), lr=2e-3, mode=mode, expected_workers=lambda: 2,
+                               tables=table_shard_spec(ref, 2, i), sparse_optimizer="adagrad",
+                               sparse_lr=0.05).start() for i in range(2)]
+    assert servers[0].tables["emb"].rows == 26 * vocab // 2
+    try:
+        addrs = {i: (s.host, s.port) for i, s in enumerate(servers)}
+        base = None
+
+        def work(wid):
+            m = DeepFM(vocab=vocab, hidden=(64, 64))
+            c = PSClient(2, lambda i: addrs[i], f"w{wid}")
+            c.bind(m)
+            assert m.emb.weight is None           # the table lives on the PS only
+            for step in range(60):
+                c.pull(m)
+                m.zero_grad()
+                b0 = (step * 2 + wid) * 256
+                m(*data.batch(range(b0, b0 + 256))).backward()
+                c.push(m, step)
+            c.close()
+
+        m = DeepFM(vocab=vocab, hidden=(64, 64))
+        c = PSClient(2, lambda i: addrs[i], "eval")
+        c.bind(m)
+        c.pull(m)
+        base = auc(m, data)
+        ts = [threading.Thread(target=work, args=(w,)) for w in range(2)]
+        [t.start() for t in ts]
+        [t.join(120) for t in ts]
+        vers = c.pull(m)
+        after = auc(m, data)
+        assert after > max(0.6, base + 0.05), (base, after)
+        assert vers == ([60, 60] if mode == "sync" else [120, 120])
+        assert servers[0].tables["emb"].step == (60 if mode == "sync" else 120)
+    finally:
+        for s in servers:
+            s.stop()

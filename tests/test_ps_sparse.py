@@ -1,0 +1,83 @@
+"""Row-sparse PS ops (easydl_amd/ops/sparse.py, csrc/kernels/ps_sparse.hip).
+
+CPU tier: the reference math equals a dense fp32 AdamW restricted to touched
+rows (lazy Adam).  GPU tier: each HIP kernel against the fp32 PyTorch
+reference of the same op, incl. duplicate and out-of-range ids."""
+import math
+
+import pytest
+import torch
+
+from easydl_amd.ops import sparse
+
+
+def _dense_lazy_adam(w, m, v, ids, grad, lr, b1, b2, eps, wd, step):
+    g = torch.zeros_like(w)
+    g.index_add_(0, ids, grad)
+    rows = torch.unique(ids)
+    for r in rows.tolist():
+        m[r] = b1 * m[r] + (1 - b1) * g[r]
+        v[r] = b2 * v[r] + (1 - b2) * g[r] * g[r]
+        denom = v[r].sqrt() / math.sqrt(1 - b2 ** step) + eps
+        w[r] = w[r] * (1 - lr * wd) - lr / (1 - b1 ** step) * m[r] / denom
+
+
+def test_segment_sum_and_lazy_adam_cpu():
+    torch.manual_seed(0)
+    rows, dim = 50, 8
+    w = torch.randn(rows, dim)
+    m, v = torch.zeros_like(w), torch.zeros_like(w)
+    w2, m2, v2 = w.clone(), m.clone(), v.clone()
+    w0 = w.clone()
+    seen = torch.zeros(rows, dtype=torch.bool)
+    for step in (1, 2, 3):
+        ids = torch.randint(0, rows - 10, (40,))  # rows >= 40 are never touched
+        seen[ids] = True
+        grad = torch.randn(40, dim)
+        uniq, comp = sparse.segment_sum_rows(ids, grad, rows)
+        assert torch.equal(uniq, torch.unique(ids))
+        sparse.sparse_rows_update(w, m, v, uniq, comp, kind="adam", lr=0.01, weight_decay=0.1, step=step)
+        _dense_lazy_adam(w2, m2, v2, ids, grad, 0.01, 0.9, 0.999, 1e-8, 0.1, step)
+    torch.testing.assert_close(w, w2, rtol=1e-5, atol=1e-6)
+    assert torch.equal(w[~seen], w0[~seen]) and not m[~seen].any()  # lazy: untouched rows keep state
+
+
+def test_gather_out_of_range_is_zero_cpu():
+    t = torch.arange(24, dtype=torch.float32).view(6, 4)
+    out = sparse.embed_gather(t, torch.tensor([1, -1, 7, 5]))
+    assert torch.equal(out[0], t[1]) and torch.equal(out[3], t[5])
+    assert not out[1].any() and not out[2].any()
+
+
+@pytest.mark.gpu
+def test_sparse_kernels_match_reference(cuda):
+    torch.manual_seed(1)
+    rows, dim, n = 1000, 128, 4096
+    table = torch.randn(rows, dim)
+    ids = torch.randint(-3, rows + 3, (n,))                  # duplicates and a few invalid ids
+    grad = torch.randn(n, dim)
+    # gather (fp32 and bf16 out)
+    g_ref = sparse.embed_gather(table, ids)
+    g_hip = sparse.embed_gather(table.cuda(), ids.cuda())
+    torch.testing.assert_close(g_hip.cpu(), g_ref, rtol=0, atol=0)
+    g16 = sparse.embed_gather(table.cuda(), ids.cuda(), out_dtype=torch.bfloat16)
+    torch.testing.assert_close(g16.float().cpu(), g_ref.bfloat16().float(), rtol=0, atol=0)
+    # segment sum (fp32 atomics: order-dependent rounding only)
+    u_ref, c_ref = sparse.segment_sum_rows(ids, grad, rows)
+    u_hip, c_hip = sparse.segment_sum_rows(ids.cuda(), grad.cuda(), rows)
+    assert torch.equal(u_hip.cpu(), u_ref)
+    torch.testing.assert_close(c_hip.cpu(), c_ref, rtol=1e-5, atol=1e-5)
+    # lazy optimizers
+    for kind in ("adam", "adagrad", "sgd"):
+        w, m, v = table.clone(), torch.rand(rows, dim) * 0.1, torch.rand(rows, dim) * 0.1
+        wg, mg, vg = w.cuda(), m.cuda(), v.cuda()
+        sparse.sparse_rows_update(w, m, v, u_ref, c_ref, kind=kind, lr=1e-2, weight_decay=0.01, step=3)
+        sparse.sparse_rows_update(wg, mg, vg, u_hip, c_hip, kind=kind, lr=1e-2, weight_decay=0.01, step=3)
+        torch.cuda.synchronize()
+        torch.testing.assert_close(wg.cpu(), w, rtol=1e-5, atol=1e-5)
+        torch.testing.assert_close(vg.cpu(), v, rtol=1e-5, atol=1e-5)
+    # dense pull with cast
+    src = torch.randn(1 << 20, device="cuda")
+    dst = torch.empty(1 << 20, device="cuda", dtype=torch.bfloat16)
+    sparse.pull_cast(src, dst)
+    assert torch.equal(dst, src.bfloat16())

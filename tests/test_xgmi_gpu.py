@@ -10,6 +10,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 WORKER = os.path.join(ROOT, "tests", "helpers", "xgmi_worker.py")
+COMM_WORKER = os.path.join(ROOT, "tests", "helpers", "xgmi_comm_worker.py")
 
 
 def _port():
@@ -20,10 +21,10 @@ def _port():
     return p
 
 
-def _run(world, tmp_path, mode="sum", timeout=120):
+def _run(world, tmp_path, mode="sum", timeout=120, worker=WORKER):
     port = _port()
     out = str(tmp_path / "xg")
-    procs = [subprocess.Popen([sys.executable, WORKER], cwd=ROOT,
+    procs = [subprocess.Popen([sys.executable, worker], cwd=ROOT,
                               env=dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), PORT=str(port), OUT=out,
                                        XG_MODE=mode, PYTHONPATH=ROOT)) for r in range(world)]
     codes = []
@@ -48,3 +49,16 @@ def test_xgmi_abort_releases_spinning_kernel(cuda, tmp_path):
     r0 = _run(2, tmp_path, mode="abort")[0]
     assert r0["status"] == 1           # the barrier gave up ...
     assert r0["elapsed"] < 4.5         # ... on the abort word, before the 5 s deadline
+
+
+def test_communicator_xgmi_bucket_allreduce(cuda, tmp_path):
+    """Communicator(data_backend="xgmi"): async bucket all-reduces on the engine's stream."""
+    for r in _run(3, tmp_path, worker=COMM_WORKER):
+        assert r["backend"] == "rccl+xgmi"
+        assert r["ok"], r["errors"]
+        assert r["healthy"]
+
+
+def test_communicator_xgmi_abort_marks_unhealthy(cuda, tmp_path):
+    r0 = _run(2, tmp_path, mode="abort", worker=COMM_WORKER)[0]
+    assert r0["aborted"] and not r0["healthy"]
