@@ -81,3 +81,49 @@ def test_sparse_kernels_match_reference(cuda):
     dst = torch.empty(1 << 20, device="cuda", dtype=torch.bfloat16)
     sparse.pull_cast(src, dst)
     assert torch.equal(dst, src.bfloat16())
+
+
+@pytest.mark.gpu
+def test_deepfm_ps_shards_on_gpu(cuda):
+    """PS shards (dense + embedding stripes) resident in HBM: pulls gather rows with
+    the HIP kernel, pushes segment-sum + lazy Adagrad on the device."""
+    import threading
+
+    from easydl_amd.models.deepctr import DeepFM, SyntheticCTR, auc
+    from easydl_amd.ps.client import PSClient, shard_of
+    from easydl_amd.ps.embedding import table_shard_spec
+    from easydl_amd.ps.server import ParameterServer
+    torch.manual_seed(0)
+    vocab = 1000
+    data = SyntheticCTR(60000, vocab=vocab)
+    ref = DeepFM(vocab=vocab, hidden=(128, 128))
+    servers = [ParameterServer(i, shard_of(ref, 2, i), lr=2e-3, device="cuda", tables=table_shard_spec(ref, 2, i),
+                               sparse_optimizer="adagrad", sparse_lr=0.05).start() for i in range(2)]
+    assert servers[0].tables["emb"].w.is_cuda
+    try:
+        addrs = {i: (s.host, s.port) for i, s in enumerate(servers)}
+
+        def work(wid):
+            m = DeepFM(vocab=vocab, hidden=(128, 128), device="cuda")
+            c = PSClient(2, lambda i: addrs[i], f"w{wid}")
+            c.bind(m)
+            for step in range(80):
+                c.pull(m)
+                m.zero_grad()
+                b0 = (step * 2 + wid) * 256
+                m(*data.batch(range(b0, b0 + 256), "cuda")).backward()
+                c.push(m, step)
+            c.close()
+
+        ts = [threading.Thread(target=work, args=(w,)) for w in range(2)]
+        [t.start() for t in ts]
+        [t.join(120) for t in ts]
+        m = DeepFM(vocab=vocab, hidden=(128, 128), device="cuda")
+        c = PSClient(2, lambda i: addrs[i], "eval")
+        c.bind(m)
+        c.pull(m)
+        assert auc(m, data, device="cuda") > 0.65
+        assert servers[1].tables["emb"].step == 160
+    finally:
+        for s in servers:
+            s.stop()
