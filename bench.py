@@ -49,6 +49,8 @@ def parse():
     ap.add_argument("--ckpt-interval", type=int, default=0,
                     help="in-memory sharded snapshot every K steps (async D2H, overlapped)")
     ap.add_argument("--fault-inject", action="store_true", help="measure time-to-recover instead (local operator)")
+    ap.add_argument("--standby", type=int, default=1,
+                    help="--fault-inject: warm spare workers kept by the operator (0 = cold respawn)")
     ap.add_argument("--comm", default=None, choices=["pg", "native", "xgmi", "auto"],
                     help="gradient all-reduce data plane (default $EDL_COMM or pg = ProcessGroupNCCL/RCCL; "
                          "xgmi = hand-written IPC all-reduce; auto = probe both at each epoch, keep the faster)")

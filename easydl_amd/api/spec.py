@@ -117,6 +117,7 @@ class ElasticJob:
     min_workers: int = 1
     max_workers: int = 8
     features: dict = field(default_factory=dict)   # hints for the Brain (model name, seq, batch...)
+    standby: int = 0    # warm spare worker processes kept parked by the operator (hot standby)
 
     @classmethod
     def from_dict(cls, d: dict) -> "ElasticJob":
@@ -140,14 +141,15 @@ class ElasticJob:
                    roles=roles, api_version=av, mode=spec.get("mode", "ps" if "parameter_server" in roles else
                                                               "allreduce"),
                    env=dict(spec.get("env") or {}), min_workers=int(spec.get("min_workers", 1)),
-                   max_workers=int(spec.get("max_workers", 8)), features=dict(spec.get("features") or {}))
+                   max_workers=int(spec.get("max_workers", 8)), features=dict(spec.get("features") or {}),
+                   standby=int(spec.get("standby", 0)))
 
     def to_dict(self) -> dict:
         spec = {"command": self.command, "image": self.image}
         for r, rs in self.roles.items():
             spec[r] = {"image": rs.image} | ({"command": rs.command} if rs.command else {})
         spec.update(mode=self.mode, env=self.env, min_workers=self.min_workers, max_workers=self.max_workers,
-                    features=self.features)
+                    features=self.features, standby=self.standby)
         return {"apiVersion": self.api_version, "kind": "ElasticJob", "metadata": {"name": self.name}, "spec": spec}
 
     def command_for(self, role: str) -> str:

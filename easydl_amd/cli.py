@@ -32,7 +32,8 @@ def cmd_submit(a):
     if job is None:
         raise SystemExit("spec has no ElasticJob")
     gpus = [int(g) for g in a.gpus.split(",")] if a.gpus else _detect_gpus()
-    cfg = OperatorConfig(gpus=gpus, cpus=list(range(os.cpu_count() or 1)), master_port=a.master_port)
+    cfg = OperatorConfig(gpus=gpus, cpus=list(range(os.cpu_count() or 1)), master_port=a.master_port,
+                         standby=a.standby)
     op = ElasticOperator(job, a.run_dir or os.path.join("runs", job.name), cfg=cfg, job_resource=jr)
     print(json.dumps({"job": job.name, "master_port": op.master_port, "run_dir": op.run_dir}), flush=True)
     return op.run(timeout_s=a.timeout)
@@ -100,6 +101,7 @@ def main(argv=None):
     s.add_argument("--run-dir", default=None)
     s.add_argument("--master-port", type=int, default=None)
     s.add_argument("--timeout", type=float, default=None)
+    s.add_argument("--standby", type=int, default=0, help="warm spare worker processes (hot standby)")
     s.set_defaults(fn=cmd_submit)
     for name, fn in (("apply", cmd_apply), ("status", cmd_status), ("scale", cmd_scale), ("kill", cmd_kill)):
         p = sub.add_parser(name)

@@ -65,6 +65,7 @@ class OperatorConfig:
     master_port: int | None = None
     python: str = sys.executable
     replace_failed: bool = True
+    standby: int = 0            # warm spare processes for the worker role (easydl_amd/operator/standby.py)
 
 
 def free_port() -> int:
@@ -113,6 +114,8 @@ class ElasticOperator:
         self.done = False
         self.failed = False
         self._free_gpus = list(self.cfg.gpus)
+        self.standbys: dict[str, Proc] = {}      # name -> parked spare
+        self._standby_seq = 0
 
     # ------------------------------------------------------------- master
     def start(self) -> None:
@@ -172,16 +175,15 @@ class ElasticOperator:
     def _completed(self, role: str) -> int:
         return sum(1 for p in self.procs.values() if p.role == role and p.state == "completed")
 
-    def _spawn_role(self, role: str, index: int, res: Resource, generation: int = 0) -> Proc:
-        short = ROLE_SHORT[role]
-        name = f"{self.job.name}-{short}-{index}"
-        env = self._base_env()
+    def _role_env(self, role: str, index: int, res: Resource, generation: int) -> tuple[dict, int | None, list]:
+        """Environment delta, GPU and CPU set of one role incarnation."""
+        env = {}
         gpu = None
         if self._needs_gpu(role, res):
             if self._free_gpus:
                 gpu = self._free_gpus.pop(0)
                 env["EDL_GPU"] = str(gpu)
-        env.update({"EDL_ROLE": short, "EDL_INDEX": str(index), "EDL_GENERATION": str(generation)})
+        env.update({"EDL_ROLE": ROLE_SHORT[role], "EDL_INDEX": str(index), "EDL_GENERATION": str(generation)})
         if res.cu:
             env["EDL_CU_MASK"] = cu_mask_hex(res.cu)
         if res.hbm_gb:
@@ -190,16 +192,30 @@ class ElasticOperator:
         if res.cpu and self.cfg.cpus:
             n = max(1, int(res.cpu))
             used = set()
-            for p in self.procs.values():
+            for p in list(self.procs.values()) + list(self.standbys.values()):
                 used |= set(getattr(p, "cpus", []))
             cpus = [c for c in self.cfg.cpus if c not in used][:n]
             env["OMP_NUM_THREADS"] = str(n)
+        return env, gpu, cpus
+
+    def _argv_for(self, role: str) -> list[str]:
         cmd = self.job.command_for(role)
         if not cmd:
             raise ValueError(f"no command for role {role}")
         argv = shlex.split(cmd)
         if argv[0] in ("python", "python3"):
             argv[0] = self.cfg.python
+        return argv
+
+    def _spawn_role(self, role: str, index: int, res: Resource, generation: int = 0) -> Proc:
+        name = f"{self.job.name}-{ROLE_SHORT[role]}-{index}"
+        delta, gpu, cpus = self._role_env(role, index, res, generation)
+        argv = self._argv_for(role)
+        taken = self._take_standby(role, name, argv, delta, gpu, cpus, res, index, generation)
+        if taken is not None:
+            return taken
+        env = self._base_env()
+        env.update(delta)
         pid = self.launcher.spawn(name, argv, env=env, cwd=REPO_ROOT,
                                   log_path=os.path.join(self.run_dir, "logs", f"{name}.log"), cpus=cpus)
         p = Proc(name, role, index, pid, gpu, res, time.time(), generation=generation)
@@ -207,6 +223,58 @@ class ElasticOperator:
         self.procs[name] = p
         self.events.emit("spawn", name=name, pid=pid, role=role, gpu=gpu, gen=generation, resource=res.to_dict())
         return p
+
+    # ------------------------------------------------------------- hot standby
+    def _maintain_standbys(self) -> None:
+        from easydl_amd.operator.standby import module_of
+        want = max(self.cfg.standby, getattr(self.job, "standby", 0))
+        if want <= 0 or self.kv is None or self.done:
+            return
+        try:
+            mod = module_of(self._argv_for("worker"))
+        except ValueError:
+            return
+        if mod is None:
+            return  # not a `python -m` entry: a standby could not run it in-process
+        while len(self.standbys) < want:
+            name = f"{self.job.name}-standby-{self._standby_seq}"
+            self._standby_seq += 1
+            env = self._base_env()
+            env.update({"EDL_STANDBY_NAME": name, "EDL_STANDBY_MODULE": mod, "EDL_ROLE": "standby"})
+            argv = [self.cfg.python, "-m", "easydl_amd.operator.standby"]
+            pid = self.launcher.spawn(name, argv, env=env, cwd=REPO_ROOT,
+                                      log_path=os.path.join(self.run_dir, "logs", f"{name}.log"))
+            self.standbys[name] = Proc(name, "standby", self._standby_seq - 1, pid, None, Resource(), time.time())
+            self.events.emit("standby_spawn", name=name, pid=pid)
+
+    def _take_standby(self, role, name, argv, delta, gpu, cpus, res, index, generation) -> Proc | None:
+        from easydl_amd.operator.standby import module_of
+        if role != "worker" or not self.standbys or self.kv is None or module_of(argv) is None:
+            return None
+        for sname, sp in list(self.standbys.items()):
+            try:
+                ready = self.kv.get(f"standby/ready/{sname}")
+            except Exception:
+                ready = None
+            if not ready:
+                continue
+            env = dict(self.job.env)
+            env.update(delta)
+            self.kv.set(f"standby/assign/{sname}", json.dumps({"env": env, "argv": argv}))
+            if cpus:
+                try:
+                    os.sched_setaffinity(sp.pid, cpus)
+                except OSError:
+                    pass
+            del self.standbys[sname]
+            p = Proc(name, role, index, sp.pid, gpu, res, time.time(), generation=generation)
+            p.cpus = cpus
+            p.standby = sname
+            self.procs[name] = p
+            self.events.emit("spawn", name=name, pid=sp.pid, role=role, gpu=gpu, gen=generation,
+                             resource=res.to_dict(), standby=sname)
+            return p
+        return None
 
     def _needs_gpu(self, role: str, res: Resource) -> bool:
         if res.gpu is not None:
@@ -280,6 +348,11 @@ class ElasticOperator:
 
     # ------------------------------------------------------------- events
     def handle_exit(self, ex) -> None:
+        sb = next((q for q in self.standbys.values() if q.pid == ex.pid), None)
+        if sb is not None:
+            del self.standbys[sb.name]
+            self.events.emit("standby_exit", name=sb.name, code=ex.exit_code, signal=ex.signal)
+            return
         p = next((q for q in list(self.procs.values()) + self.history if q.pid == ex.pid), None)
         if p is None:
             return
@@ -362,6 +435,7 @@ class ElasticOperator:
             self.handle_exit(ex)
         self._poll_jobresource()
         self.reconcile()
+        self._maintain_standbys()
         self._enforce_grace()
         if self.job_complete() and not self.done:
             self.done = True
@@ -391,6 +465,11 @@ class ElasticOperator:
                     for ex in self.launcher.poll(0.1):
                         self.handle_exit(ex)
                 self.kv.set("master/shutdown", "1")
+            except Exception:
+                pass
+        for p in list(self.standbys.values()):
+            try:
+                self.launcher.terminate(p.pid, grace_s=2.0)
             except Exception:
                 pass
         for p in list(self.procs.values()):

@@ -1,0 +1,91 @@
+"""Hot-standby role processes (SURVEY.md §5.3 "hot-standby processes ... remove
+the multi-second Python/torch import from TTR", §7.3 hard part 3).
+
+A standby is started by the local ElasticOperator ahead of any failure as
+``python -m easydl_amd.operator.standby``.  It pays every start-up cost that
+does not depend on WHICH role it will become:
+
+* imports torch and the framework (trainer, models, comm, checkpoint, PS) —
+  not the job's entry module itself, whose top level may start training;
+* loads the gfx950 kernel library (code-object registration) and initialises
+  the HIP runtime (device enumeration) without creating a context on any GPU —
+  the GPU is chosen at takeover (``EDL_GPU``), so one spare covers any rank;
+
+then parks on the job store.  When a role process dies the operator writes
+``standby/assign/<standby name>`` = ``{"env": {...}, "argv": [...]}``; the
+standby applies the environment (role, index, generation, GPU, CU/HBM plan),
+sets ``sys.argv`` and runs the role's module in-process with ``runpy`` — it
+becomes ``<job>-<role>-<index>`` without a new process (its pid is the new
+incarnation's pid, so exit events keep flowing through the supervisor).
+"""
+from __future__ import annotations
+
+import importlib
+import json
+import os
+import runpy
+import sys
+import time
+
+
+def module_of(argv: list[str]) -> str | None:
+    """The module of a ``python -m <module> ...`` command, else None (not runnable by a standby)."""
+    if len(argv) >= 3 and os.path.basename(argv[0]).startswith("python") and argv[1] == "-m":
+        return argv[2]
+    return None
+
+
+PREWARM_MODULES = ("easydl_amd.trainer.elastic", "easydl_amd.ckpt.manager", "easydl_amd.models.llama",
+                   "easydl_amd.parallel.tp", "easydl_amd.trainer.ps_trainer", "easydl_amd.trainer.data")
+
+
+def prewarm() -> dict:
+    t0 = time.perf_counter()
+    import torch  # noqa: F401
+
+    from easydl_amd import _native
+    for m in PREWARM_MODULES:
+        importlib.import_module(m)
+    out = {"import_s": round(time.perf_counter() - t0, 3)}
+    if _native.kernels_available():
+        out["kernels"] = True
+    n = torch.cuda.device_count()
+    out["gpus"] = n
+    if n:
+        torch.cuda.init()  # HIP runtime + device enumeration; contexts stay lazy (per device, at takeover)
+    out["prewarm_s"] = round(time.perf_counter() - t0, 3)
+    return out
+
+
+def main() -> int:
+    from easydl_amd.master.store import KV, make_tcp_store
+    name = os.environ["EDL_STANDBY_NAME"]
+    job = os.environ.get("EDL_JOB", "job")
+    kv = KV(make_tcp_store(os.environ.get("EDL_MASTER_ADDR", "127.0.0.1"), int(os.environ["EDL_MASTER_PORT"]),
+                           False), f"edl/{job}")
+    info = prewarm()
+    info.update(pid=os.getpid(), ts=time.time())
+    kv.set(f"standby/ready/{name}", json.dumps(info))
+    key = f"standby/assign/{name}"
+    while True:
+        a = kv.get(key)
+        if a is not None:
+            break
+        if kv.exists("job/done"):
+            return 0
+        time.sleep(0.005)
+    a = a if isinstance(a, dict) else json.loads(a)
+    os.environ.update({k: str(v) for k, v in a["env"].items()})
+    argv = a["argv"]
+    mod = module_of(argv)
+    if mod is None:
+        print(f"standby {name}: cannot run {argv!r} in-process", file=sys.stderr)
+        return 3
+    sys.argv = [mod] + argv[3:]
+    kv.set(f"standby/taken/{name}", json.dumps({"as": a["env"].get("EDL_INDEX"), "ts": time.time()}))
+    runpy.run_module(mod, run_name="__main__", alter_sys=True)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

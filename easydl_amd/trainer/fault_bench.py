@@ -56,11 +56,11 @@ def main(args) -> int:
     }
     if args.layers:
         env["EDL_BENCH_LAYERS"] = str(args.layers)
-    job = ElasticJob(name=job_name, command=f"{sys.executable} -m easydl_amd.trainer.fault_bench --worker",
+    job = ElasticJob(name=job_name, command="python -m easydl_amd.trainer.fault_bench --worker",
                      env=env, min_workers=1, max_workers=n)
     jr = JobResource(f"{job_name}-resource", job_name,
                      {"worker": RoleResource(n, Resource(gpu=1 if gpus else 0, cpu=4))})
-    cfg = OperatorConfig(gpus=gpus[:n], cpus=[], leave_grace_s=120.0)
+    cfg = OperatorConfig(gpus=gpus[:n], cpus=[], leave_grace_s=120.0, standby=getattr(args, "standby", 0))
     op = ElasticOperator(job, run_dir, cfg=cfg, job_resource=jr)
     rc = op.run(timeout_s=1000)
     ev = read_events(run_dir)
@@ -72,7 +72,8 @@ def main(args) -> int:
         "value": None if not ttr else ttr["ttr_s"], "unit": "s", "higher_is_better": False,
         "n_gpus": n if gpus else 0,
         "model": (args.model if not args.layers else f"{args.model}-L{args.layers}") if gpus else "llama-tiny (CPU)",
-        "breakdown": ttr, "operator_rc": rc, "restored_from": restored[0].get("source") if restored else None,
+        "breakdown": ttr, "operator_rc": rc, "hot_standby": getattr(args, "standby", 0),
+        "replacement_from_standby": any(e["kind"] == "spawn" and e.get("standby") for e in ev), "restored_from": restored[0].get("source") if restored else None,
         "worlds_seen": sorted({w for w in worlds if w}), "run_dir": run_dir,
     }
     print(json.dumps(out), flush=True)

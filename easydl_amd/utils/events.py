@@ -84,6 +84,8 @@ def ttr_breakdown(events: list[dict]) -> dict | None:
         "detect_s": rel(first("node_dead")),
         "abort_s": rel(first("epoch_abort")),
         "epoch_formed_s": rel(formed),
+        "replacement_spawn_s": rel(first("spawn", lambda e: e.get("role") == "worker")),
+        "replacement_joined_s": rel(first("joined")),
         "comm_ready_s": rel(first("comm_ready", in_new)),
         "state_synced_s": rel(first("state_synced", in_new)),
         "first_step_s": rel(done),

@@ -49,3 +49,41 @@ def test_submit_kill_replace_complete(tmp_path):
     spawns = [e for e in ev if e["kind"] == "spawn"]
     assert spawns[0]["name"] == "e2e-trainer-0"
     assert sum(1 for e in spawns if e["name"] == "e2e-worker-1") == 2
+
+
+@pytest.mark.slow
+def test_hot_standby_takes_over_failed_worker(tmp_path):
+    """A parked, pre-imported standby becomes the dead worker (same name, new
+    generation) without a new process: the replacement joins faster than a cold spawn."""
+    spec = tmp_path / "job.yaml"
+    spec.write_text(textwrap.dedent("""
+        apiVersion: edl.mi355x/v1
+        kind: ElasticJob
+        metadata: {name: hot}
+        spec:
+          command: "python -m tests.helpers.elastic_worker"
+          min_workers: 1
+          max_workers: 2
+          standby: 1
+          env: {TEST_STEPS: "40", TEST_GB: "4", TEST_STEP_SLEEP: "0.15", EDL_FAULT: "kill@step=12,index=1"}
+        ---
+        apiVersion: edl.mi355x/v1
+        kind: JobResource
+        metadata: {name: hot-resource}
+        spec:
+          selector: {name: hot}
+          worker: {replicas: 2, resource: {cpu: 1, gpu: 0}}
+        """))
+    run = tmp_path / "run"
+    r = subprocess.run([sys.executable, "-m", "easydl_amd.cli", "submit", str(spec), "--gpus", "",
+                        "--run-dir", str(run), "--timeout", "240"], cwd=ROOT,
+                       capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1"))
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    ev = [json.loads(l) for f in glob.glob(str(run / "events-*.jsonl")) for l in open(f)]
+    spawns = [e for e in ev if e["kind"] == "spawn" and e.get("name") == "hot-worker-1"]
+    assert len(spawns) == 2 and spawns[1].get("standby"), spawns
+    sb = [e for e in ev if e["kind"] == "standby_spawn"]
+    assert spawns[1]["pid"] in {e["pid"] for e in sb}           # no new process: the standby's pid
+    res = [json.load(open(f)) for f in glob.glob(str(run / "res*.json"))]
+    assert len({x["hash"] for x in res}) == 1 and all(x["step"] == 40 for x in res), res
