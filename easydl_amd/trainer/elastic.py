@@ -66,11 +66,14 @@ class ElasticTrainer:
             else:
                 device = torch.device("cpu")
         self.device = torch.device(device)
+        t_init = time.perf_counter()
         if self.device.type == "cuda":
             torch.cuda.set_device(self.device)
+            torch.empty(1, device=self.device)  # HIP context now, so its cost shows up in the timeline
         self.resources = apply_plan(self.ctx, self.device)  # Brain CU mask / HBM cap
         self.events = EventLog(os.path.join(self.ctx.run_dir, f"events-{self.ctx.role}{self.ctx.index}.jsonl"),
                                proc=f"{self.ctx.role}{self.ctx.index}")
+        self.events.emit("device_ready", s=round(time.perf_counter() - t_init, 4))
         if optimizer not in ("adamw", "sgd"):
             raise ValueError(f"unknown optimizer {optimizer}")
         self._model_fn, self._seed = model_fn, seed
@@ -114,12 +117,14 @@ class ElasticTrainer:
     # ------------------------------------------------------------------ setup
     def _build_model(self, tp_rank: int) -> None:
         a = self._opt_args
+        t0 = time.perf_counter()
         torch.manual_seed(self._seed + 1009 * tp_rank)  # DP replicas of a shard initialise identically
         if self.tp > 1:
             self.tp_group.rank = tp_rank
             self.model = self._model_fn(self.device, self.tp_group)
         else:
             self.model = self._model_fn(self.device)
+        t1 = time.perf_counter()
         self.flat = FlatParams(self.model, weight_decay=a["weight_decay"], grad_dtype=a["grad_dtype"])
         if a["optimizer"] == "adamw":
             self.opt = FlatAdamW(self.flat, lr=a["lr"], betas=a["betas"], weight_decay=a["weight_decay"],
@@ -138,6 +143,10 @@ class ElasticTrainer:
             self.opt.norm_weights = w
             self.opt.norm_reduce = lambda t: self.comm.tp.all_reduce(t)
         self.ddp = ElasticDDP(self.flat, None, bucket_mb=a["bucket_mb"])
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        if getattr(self, "events", None) is not None:
+            self.events.emit("model_built", model_s=round(t1 - t0, 4), flat_opt_s=round(time.perf_counter() - t1, 4))
 
     def _connect(self):
         if self.ctx.standalone:
