@@ -471,67 +471,6 @@ int edl_ckpt_restore_pipelined(void* seg, int slot, int nbuf, const uint64_t* de
   return (int)err;
 }
 
-// Zero-copy restore: the slot's pages are page-locked in place (hipHostRegister
-// on page-aligned windows of `chunk` bytes) and DMA'd straight to the device —
-// no CPU memcpy through staging buffers, so host memory sees one read per byte
-// instead of read + write + read.  Up to `depth` windows are registered and in
-// flight at once: registering window k+1 (page-table walk in the kernel)
-// overlaps the DMA of window k; a window is unregistered once its copy is done.
-int edl_ckpt_restore_registered(void* seg, int slot, int nbuf, const uint64_t* dev_ptrs, const uint64_t* sizes,
-                                const uint64_t* offsets, hipStream_t stream, uint64_t chunk, int depth) {
-  auto* s = static_cast<Seg*>(seg);
-  if (slot < 0) slot = edl_shm_current(s);
-  if (slot < 0) return -1;
-  const uint64_t page = (uint64_t)sysconf(_SC_PAGESIZE);
-  if (chunk == 0) chunk = 512ull << 20;
-  chunk = round_up(chunk, page);
-  if (depth < 2) depth = 2;
-  struct Win {
-    uint8_t* base = nullptr;
-    hipEvent_t ev = nullptr;
-  };
-  std::deque<Win> inflight;
-  hipError_t err = hipSuccess;
-  auto retire = [&](bool all) {
-    while (!inflight.empty() && (all || (int)inflight.size() >= depth)) {
-      Win w = inflight.front();
-      inflight.pop_front();
-      hipError_t e = hipEventSynchronize(w.ev);
-      if (err == hipSuccess) err = e;
-      hipEventDestroy(w.ev);
-      hipHostUnregister(w.base);
-    }
-  };
-  uint8_t* data = s->data(slot);
-  const uint8_t* seg_end = s->base + s->total;
-  for (int b = 0; b < nbuf && err == hipSuccess; ++b) {
-    for (uint64_t off = 0; off < sizes[b] && err == hipSuccess; off += chunk) {
-      const uint64_t n = sizes[b] - off < chunk ? sizes[b] - off : chunk;
-      uint8_t* src = data + offsets[b] + off;
-      uint8_t* lo = (uint8_t*)((uintptr_t)src & ~(uintptr_t)(page - 1));
-      uint8_t* hi = (uint8_t*)round_up((uint64_t)(uintptr_t)(src + n), page);
-      if (hi > seg_end) hi = (uint8_t*)seg_end;
-      retire(false);
-      Win w;
-      w.base = lo;
-      err = hipHostRegister(lo, (size_t)(hi - lo), hipHostRegisterPortable);
-      if (err != hipSuccess) break;
-      err = hipEventCreateWithFlags(&w.ev, hipEventDisableTiming);
-      if (err == hipSuccess)
-        err = hipMemcpyAsync((uint8_t*)dev_ptrs[b] + off, src, n, hipMemcpyHostToDevice, stream);
-      if (err == hipSuccess) err = hipEventRecord(w.ev, stream);
-      if (err != hipSuccess) {
-        if (w.ev) hipEventDestroy(w.ev);
-        hipHostUnregister(lo);
-        break;
-      }
-      inflight.push_back(w);
-    }
-  }
-  retire(true);
-  return (int)err;
-}
-
 void edl_ckpt_engine_destroy(void* eng) {
   auto* e = static_cast<Engine*>(eng);
   if (!e) return;

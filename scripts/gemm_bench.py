@@ -41,6 +41,7 @@ def main():
     ap.add_argument("--tune", action="store_true")
     ap.add_argument("--tune-file", default="")
     ap.add_argument("--out", default="")
+    ap.add_argument("--layouts", action="store_true", help="also time the W^T [in,out] storage variants")
     a = ap.parse_args()
     if a.tune:
         import torch.cuda.tunable as tun
@@ -59,10 +60,16 @@ def main():
         dy = torch.randn(M, n, device=dev, dtype=torch.bfloat16)
         dw = torch.empty(n, k, device=dev, dtype=torch.bfloat16)
         flops = 2.0 * M * k * n
+        wt = w.t().contiguous()          # alternative storage: W^T [in, out] row-major
+        dwt = torch.empty(k, n, device=dev, dtype=torch.bfloat16)
         ops = {"fwd": lambda: torch.nn.functional.linear(x, w),
                "dgrad": lambda: torch.mm(dy, w),
                "wgrad": lambda: torch.mm(dy.t(), x, out=dw),
                "wgrad_acc": lambda: dw.addmm_(dy.t(), x)}
+        if a.layouts:
+            ops.update({"T_fwd": lambda: torch.mm(x, wt),
+                        "T_dgrad": lambda: torch.mm(dy, wt.t()),
+                        "T_wgrad": lambda: torch.mm(x.t(), dy, out=dwt)})
         for op, fn in ops.items():
             t = timeit(fn)
             r = {"shape": name, "op": op, "M": M, "K": k, "N": n, "ms": round(t * 1e3, 3),
@@ -71,7 +78,7 @@ def main():
                 total[op] += t
             res.append(r)
             print(json.dumps(r), flush=True)
-        del x, w, dy, dw
+        del x, w, dy, dw, wt, dwt
         torch.cuda.empty_cache()
     print(json.dumps({"total_ms": {k: round(v * 1e3, 2) for k, v in total.items()}}), flush=True)
     if a.tune:
