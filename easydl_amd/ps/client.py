@@ -44,8 +44,12 @@ def shard_of(model: torch.nn.Module, num_ps: int, index: int) -> dict[str, torch
 
 
 class PSClient:
-    def __init__(self, num_ps: int, resolve, worker_id: str, retry_s: float = 120.0):
-        """``resolve(i) -> (host, port)`` returns the current address of PS i."""
+    def __init__(self, num_ps: int, resolve, worker_id: str, retry_s: float = 120.0, transport: str = "tcp"):
+        """``resolve(i) -> (host, port)`` returns the current address of PS i.
+
+        ``transport``: ``tcp`` (tensors over the socket) or ``ipc`` (GPU shards:
+        parameters / gradients move through IPC-mapped HBM, easydl_amd/ps/ipc.py;
+        TCP carries only control messages and sparse rows)."""
         self.num_ps = num_ps
         self.resolve = resolve
         self.worker_id = worker_id
@@ -57,6 +61,8 @@ class PSClient:
         self.assign: dict[str, int] = {}
         self.tables: dict = {}
         self.rows_bf16 = False  # pull embedding rows as bf16 (halves the wire bytes)
+        self.transport = transport
+        self._ipc: dict[int, dict] = {}   # PS index -> {"w", "inbox", "layout", "sock"}
 
     def bind(self, model: torch.nn.Module) -> None:
         from easydl_amd.ps.embedding import tables_of
@@ -107,6 +113,7 @@ class PSClient:
                     send_msg(self._socks[i], header, tensors)
                     return recv_msg(self._socks[i])
                 except (ConnectionError, OSError, TimeoutError):
+                    self._ipc.pop(i, None)  # a replacement PS exports new handles
                     s = self._socks.pop(i, None)
                     if s is not None:
                         try:
@@ -117,8 +124,62 @@ class PSClient:
                         raise
             time.sleep(0.2)  # PS being replaced: re-resolve and retry
 
+    # -- GPU transport ---------------------------------------------------------------
+    def _ipc_map(self, i: int) -> dict:
+        m = self._ipc.get(i)
+        if m is None or m["sock"] is not self._socks.get(i):
+            from easydl_amd.ps.ipc import import_tensor
+            h, _ = self._call(i, {"op": "ipc_open", "worker": self.worker_id})
+            if not h.get("ok"):
+                raise RuntimeError(f"PS {i}: {h.get('error')}")
+            d = h["ipc"]
+            m = {"w": import_tensor(d["w"]), "inbox": import_tensor(d["inbox"]), "layout": d["layout"],
+                 "sock": self._socks.get(i)}
+            self._ipc[i] = m
+        return m
+
+    def _pull_ipc(self, i: int, params: dict, min_version=None) -> int:
+        from easydl_amd.ops.sparse import pull_cast
+        hdr = {"op": "pull_ipc"}
+        if min_version is not None:
+            hdr["min_version"] = min_version
+        m = self._ipc_map(i)
+        h, _ = self._call(i, hdr)
+        w = m["w"]
+        with torch.no_grad():
+            for n, (off, shape) in m["layout"].items():
+                p = params[n]
+                k = p.numel()
+                src = w[off:off + k]
+                if p.dtype == torch.bfloat16 and k % 8 == 0 and p.is_contiguous():
+                    pull_cast(src, p.view(-1))   # HIP kernel on this GPU, fp32 read from the PS's HBM
+                else:
+                    p.copy_(src.view(p.shape))
+        torch.cuda.current_stream(next(iter(params.values())).device).synchronize()
+        return h["version"]
+
+    def _push_ipc(self, i: int, params: dict, extra: dict, step: int) -> int:
+        m = self._ipc_map(i)
+        inbox = m["inbox"]
+        with torch.no_grad():
+            for n, (off, shape) in m["layout"].items():
+                g = params[n].grad
+                dst = inbox[off:off + params[n].numel()]
+                if g is None:
+                    dst.zero_()
+                else:
+                    dst.copy_(g.reshape(-1))  # peer writes into the PS's HBM
+        torch.cuda.current_stream(next(iter(params.values())).device).synchronize()
+        h, _ = self._call(i, {"op": "push_ipc", "worker": self.worker_id, "step": step}, extra)
+        return h["version"]
+
     def pull(self, model: torch.nn.Module, min_versions=None) -> list[int]:
         params = dict(model.named_parameters())
+        if self.transport == "ipc":
+            self.versions = list(self._pool.map(
+                lambda i: self._pull_ipc(i, params, None if min_versions is None else min_versions[i]),
+                range(self.num_ps)))
+            return self.versions
 
         def one(i):
             names = [n for n, j in self.assign.items() if j == i]
@@ -142,6 +203,11 @@ class PSClient:
             if got is not None:
                 parts, flat = self._split_rows(got[0].cpu())
                 sparse_grads[n] = (parts, flat, got[1].detach().cpu())
+
+        if self.transport == "ipc":
+            self.versions = list(self._pool.map(
+                lambda i: self._push_ipc(i, params, self._sparse_grads(i, sparse_grads), step), range(self.num_ps)))
+            return self.versions
 
         def one(i):
             grads = self._sparse_grads(i, sparse_grads)

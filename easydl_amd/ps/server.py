@@ -101,6 +101,7 @@ class ParameterServer:
         # row-sparse embedding stripes (easydl_amd/ps/embedding.py), lazily updated
         self.tables = {n: TableShard(n, t["rows"], t["dim"], t.get("init_std", 0.01), index, device, seed)
                        for n, t in (tables or {}).items()}
+        self.inboxes: dict[str, torch.Tensor] = {}   # GPU transport: worker -> gradient inbox in this HBM
         self.sparse_optimizer = sparse_optimizer or ("adam" if optimizer == "adam" else "sgd")
         self.sparse_lr = lr if sparse_lr is None else sparse_lr
         self.optimizer, self.lr, self.betas, self.eps = optimizer, lr, betas, eps
@@ -123,16 +124,19 @@ class ParameterServer:
         self._threads = []
 
     # -- optimizer -------------------------------------------------------------
-    def _apply(self, scale: float) -> None:
+    def _apply(self, scale: float, grad: torch.Tensor | None = None) -> None:
+        """One optimizer update of the shard from ``grad`` (default: the accumulator)."""
         st = self.state
+        g = st.g if grad is None else grad
         self.step += 1
         if self.optimizer == "adam":
-            adamw_flat_(None, st.w, st.m, st.v, st.g, lr=self.lr, beta1=self.betas[0], beta2=self.betas[1],
+            adamw_flat_(None, st.w, st.m, st.v, g, lr=self.lr, beta1=self.betas[0], beta2=self.betas[1],
                         eps=self.eps, weight_decay=self.wd, step=self.step, scale=scale)
         else:
-            sgd_flat_(None, st.w, st.m if self.momentum else None, st.g, lr=self.lr, momentum=self.momentum,
+            sgd_flat_(None, st.w, st.m if self.momentum else None, g, lr=self.lr, momentum=self.momentum,
                       weight_decay=self.wd, scale=scale)
-        st.g.zero_()
+        if grad is None:
+            st.g.zero_()
         for t in self.tables.values():
             if t.pending:
                 ids = torch.cat([i for i, _ in t.pending])
@@ -149,22 +153,36 @@ class ParameterServer:
         t.apply(ids, grads, kind=self.sparse_optimizer, lr=self.sparse_lr, betas=self.betas, eps=self.eps, wd=0.0,
                 scale=scale)
 
-    def _push(self, worker: str, grads: dict[str, torch.Tensor]) -> int:
+    def _apply_sparse(self, grads: dict[str, torch.Tensor], async_mode: bool) -> None:
+        for n, t in self.tables.items():
+            ids = grads.get(f"sparse/{n}/ids")
+            if ids is None or ids.numel() == 0:
+                continue
+            g = grads[f"sparse/{n}/grad"]
+            if async_mode:
+                self._apply_table(t, ids, g, 1.0)
+            else:
+                t.pending.append((ids.to(t.w.device), g.to(t.w.device, torch.float32)))
+
+    def _push(self, worker: str, grads: dict[str, torch.Tensor], inbox: torch.Tensor | None = None) -> int:
         with self.lock:
             st = self.state
+            if inbox is not None and self.mode == "async":
+                # GPU transport: the inbox IS the gradient of this update (no accumulate pass)
+                self._apply_sparse(grads, async_mode=True)
+                self.stats["pushes"] += 1
+                self.stats["workers"].add(worker)
+                self._apply(1.0, grad=inbox)
+                torch.cuda.current_stream(st.device).synchronize()  # inbox free for the next push
+                return self.version
+            if inbox is not None:
+                st.g.add_(inbox)
+                torch.cuda.current_stream(st.device).synchronize()
             for n, g in grads.items():
                 if n.startswith("sparse/"):
                     continue
                 st.view(st.g, n).add_(g.to(st.device, torch.float32))
-            for n, t in self.tables.items():
-                ids = grads.get(f"sparse/{n}/ids")
-                if ids is None or ids.numel() == 0:
-                    continue
-                g = grads[f"sparse/{n}/grad"]
-                if self.mode == "async":
-                    self._apply_table(t, ids, g, 1.0)
-                else:
-                    t.pending.append((ids.to(t.w.device), g.to(t.w.device, torch.float32)))
+            self._apply_sparse(grads, async_mode=self.mode == "async")
             self.stats["pushes"] += 1
             self.stats["workers"].add(worker)
             if self.mode == "async":
@@ -211,6 +229,31 @@ class ParameterServer:
                         ver = self.version
                     self.stats["pulls"] += 1
                     send_msg(conn, {"ok": True, "version": ver}, {"rows": rows})
+                elif op == "ipc_open":
+                    from easydl_amd.ps.ipc import export_tensor
+                    st = self.state
+                    if not st.w.is_cuda:
+                        send_msg(conn, {"ok": False, "error": "PS shard is not on a GPU"})
+                        continue
+                    with self.lock:
+                        wid = hdr.get("worker", "?")
+                        if wid not in self.inboxes:
+                            self.inboxes[wid] = torch.zeros_like(st.w)
+                        desc = {"w": export_tensor(st.w), "inbox": export_tensor(self.inboxes[wid]),
+                                "layout": {n: [st.offsets[n], list(st.shapes[n])] for n in st.names}}
+                    send_msg(conn, {"ok": True, "ipc": desc, "version": self.version})
+                elif op == "pull_ipc":
+                    minv = int(hdr.get("min_version", 0))
+                    with self.lock:
+                        t_end = time.monotonic() + float(hdr.get("timeout", 60))
+                        while self.version < minv and time.monotonic() < t_end:
+                            self.lock.wait(timeout=0.05)
+                        self.stats["pulls"] += 1
+                        ver = self.version
+                    send_msg(conn, {"ok": True, "version": ver})
+                elif op == "push_ipc":
+                    ver = self._push(hdr.get("worker", "?"), tensors, inbox=self.inboxes[hdr["worker"]])
+                    send_msg(conn, {"ok": True, "version": ver})
                 elif op == "push":
                     ver = self._push(hdr.get("worker", "?"), tensors)
                     send_msg(conn, {"ok": True, "version": ver})

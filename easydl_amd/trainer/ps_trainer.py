@@ -67,6 +67,12 @@ def run_ps(model_fn, num_ps: int, ctx: TrainerContext | None = None, *, optimize
         ps.stop()
 
 
+def _transport(device) -> str:
+    """EDL_PS_TRANSPORT (tcp | ipc); ipc needs the worker and the PS shards on GPUs of this node."""
+    t = os.environ.get("EDL_PS_TRANSPORT", "tcp")
+    return t if torch.device(device).type == "cuda" else "tcp"
+
+
 class PSWorker:
     def __init__(self, model_fn, num_ps: int, ctx: TrainerContext | None = None, device="cpu", seed: int = 1234):
         self.ctx = ctx or TrainerContext.from_env()
@@ -77,7 +83,7 @@ class PSWorker:
         self.events = EventLog(os.path.join(self.ctx.run_dir, f"events-worker{self.ctx.index}.jsonl"),
                                proc=f"worker{self.ctx.index}")
         self.rdzv = RendezvousClient(self.kv, self.ctx.node_id, {"index": self.ctx.index, "role": "worker"})
-        self.client = PSClient(num_ps, store_resolver(self.kv), self.ctx.node_id)
+        self.client = PSClient(num_ps, store_resolver(self.kv), self.ctx.node_id, transport=_transport(self.device))
         self.client.bind(self.model)
         self.fault = fault.FaultInjector.from_env(self.ctx, self.events)
         self.steps = 0
@@ -118,7 +124,7 @@ def run_evaluator(model_fn, num_ps: int, eval_fn, ctx: TrainerContext | None = N
     kv = _kv(ctx)
     torch.manual_seed(seed)
     model = model_fn(device)
-    client = PSClient(num_ps, store_resolver(kv), ctx.node_id)
+    client = PSClient(num_ps, store_resolver(kv), ctx.node_id, transport=_transport(device))
     client.bind(model)
     events = EventLog(os.path.join(ctx.run_dir, f"events-evaluator{ctx.index}.jsonl"), proc="evaluator")
     last = None

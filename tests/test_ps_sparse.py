@@ -127,3 +127,37 @@ def test_deepfm_ps_shards_on_gpu(cuda):
     finally:
         for s in servers:
             s.stop()
+
+
+@pytest.mark.gpu
+def test_ps_gpu_ipc_transport(cuda, tmp_path):
+    """PS shard in HBM, two worker processes pulling through the mapped shard (HIP
+    pull-cast kernel) and pushing into their inboxes; async updates all applied."""
+    import json
+    import os
+    import subprocess
+    import sys
+    import time
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    helper = os.path.join(root, "tests", "helpers", "ps_ipc_proc.py")
+    pf = str(tmp_path / "port")
+    env = dict(os.environ, PYTHONPATH=root)
+    ps = subprocess.Popen([sys.executable, helper, "ps", pf], env=env)
+    try:
+        t_end = time.time() + 60
+        while not os.path.exists(pf) and time.time() < t_end:
+            time.sleep(0.1)
+        port = open(pf).read().strip()
+        ws = [subprocess.Popen([sys.executable, helper, "worker", port, str(w), "60"], env=env,
+                               stdout=subprocess.PIPE, text=True) for w in range(2)]
+        outs = [w.communicate(timeout=120)[0] for w in ws]
+        assert all(w.returncode == 0 for w in ws), outs
+        out = str(tmp_path / "check.json")
+        subprocess.run([sys.executable, helper, "check", port, out], env=env, check=True, timeout=120)
+        r = json.load(open(out))
+        assert r["same"], r          # IPC pull == TCP pull, bit for bit
+        assert r["va"] == [120] and r["vb"] == [120]
+        assert r["acc"] > 0.6, r
+    finally:
+        open(pf + ".stop", "w").close()
+        ps.wait(timeout=30)
