@@ -104,6 +104,11 @@ class Planner:
             state_gb = feat.params * 12 / 2**30  # fp32 param + m + v on the PS
             n_ps = max(1, math.ceil(state_gb / self.cfg.ps_shard_gb)) if feat.params else 1
             if ngpu:
+                # dense pushes: every worker step writes the whole gradient (4 B/param) into the
+                # PS's HBM over xGMI -> one PS per 4 GPUs keeps the PS inbound links and its
+                # HBM update below the workers' step rate (BERT-large: 2 PS + 6 workers)
+                if feat.params * 4 > 1e9:
+                    n_ps = max(n_ps, ngpu // 4)
                 n_ps = min(n_ps, max(1, ngpu // 4))
                 n_workers = max(feat.min_workers, min(feat.max_workers, ngpu - n_ps))
                 ps_res = Resource(cpu=4, memory=max(4096, state_gb / n_ps * 1024 * 2), gpu=1, cu=self.cfg.ps_cu,

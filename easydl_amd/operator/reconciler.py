@@ -184,6 +184,8 @@ class ElasticOperator:
                 gpu = self._free_gpus.pop(0)
                 env["EDL_GPU"] = str(gpu)
         env.update({"EDL_ROLE": ROLE_SHORT[role], "EDL_INDEX": str(index), "EDL_GENERATION": str(generation)})
+        if self.desired is not None and "parameter_server" in self.desired.roles:
+            env["EDL_NUM_PS"] = str(self.desired.replicas("parameter_server"))  # shard count for PS jobs
         if res.cu:
             env["EDL_CU_MASK"] = cu_mask_hex(res.cu)
         if res.hbm_gb:

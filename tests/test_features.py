@@ -29,3 +29,17 @@ def test_unknown_model_is_harmless_and_brain_accepts():
     plan = Planner().startup_plan(feat, inv)
     assert plan.roles["worker"].replicas == 8
     assert JobFeatures.from_dict(f).params == 1e6
+
+
+def test_bert_large_ps_plan_is_2ps_6workers_with_cu_hbm():
+    """BASELINE config 4: the Brain's startup plan for BERT-large async PS on 8 MI355X."""
+    from easydl_amd.api.spec import load_specs
+    job, jr = load_specs("examples/bert_ps.yaml")
+    assert jr is None and job.mode == "ps"          # no JobResource: the Brain decides
+    feat = JobFeatures.from_dict(extract(job))
+    assert 3.3e8 < feat.params < 3.5e8
+    inv = NodeInventory(gpus=[GpuInfo(i, "gfx950", 256, 288.0) for i in range(8)], cpus=128, host_mem_gb=2048)
+    plan = Planner().startup_plan(feat, inv)
+    ps, w = plan.roles["parameter_server"], plan.roles["worker"]
+    assert (ps.replicas, w.replicas) == (2, 6), plan.reason
+    assert ps.resource.gpu == 1 and 0 < ps.resource.cu < 256 and 0 < ps.resource.hbm_gb < 288
