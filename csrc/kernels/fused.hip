@@ -236,6 +236,47 @@ inline int grid_for(int64_t items, int cap = 4096) {
   return (int)(b < cap ? b : cap);
 }
 
+
+// bf16 [R, C] -> [C, R] through a padded 64x64 LDS tile: 16-B global loads along
+// C, 16-B global stores along R (both coalesced); the LDS row stride of 66
+// elements (33 banks) keeps the column reads of the transposed pass conflict-
+// free.  HBM-bound: 4 B moved per element.  Used to keep a [in, out] copy of
+// Linear weights so the input-gradient GEMM runs in hipBLASLt's fast NT form.
+__global__ __launch_bounds__(256) void transpose_bf16_kernel(const bf16_t* __restrict__ src, bf16_t* __restrict__ dst,
+                                                             int R, int C) {
+  constexpr int T = 64, P = T + 2;
+  __shared__ bf16_t tile[T * P];
+  const int r0 = blockIdx.y * T, c0 = blockIdx.x * T;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int idx = threadIdx.x + 256 * i;      // 512 chunks of 8 elements
+    const int r = idx >> 3, c8 = (idx & 7) * 8;
+    const int gr = r0 + r, gc = c0 + c8;
+    if (gr < R && gc + 8 <= C) {
+      const u32x4 v = *reinterpret_cast<const u32x4*>(src + (int64_t)gr * C + gc);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        tile[r * P + c8 + 2 * j] = (bf16_t)(v[j] & 0xffffu);
+        tile[r * P + c8 + 2 * j + 1] = (bf16_t)(v[j] >> 16);
+      }
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int idx = threadIdx.x + 256 * i;
+    const int c = idx >> 3, r8 = (idx & 7) * 8;  // output row c, columns r8..r8+7
+    const int gc = c0 + c, gr = r0 + r8;
+    if (gc < C && gr + 8 <= R) {
+      u32x4 o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        o[j] = (uint32_t)tile[(r8 + 2 * j) * P + c] | ((uint32_t)tile[(r8 + 2 * j + 1) * P + c] << 16);
+      *reinterpret_cast<u32x4*>(dst + (int64_t)gc * R + gr) = o;
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -279,6 +320,15 @@ int edl_xent_fwd_bwd(void* logits, const int64_t* labels, float* loss, int64_t r
                      int write_grad, hipStream_t s) {
   if (rows <= 0) return 0;
   xent_fwd_bwd_kernel<<<(unsigned)rows, 256, 0, s>>>((bf16_t*)logits, labels, loss, V, ignore_index, write_grad);
+  EDL_LAUNCH_CHECK();
+  return 0;
+}
+
+// dst[C, R] = src[R, C]^T (bf16, R and C multiples of 8)
+int edl_transpose_bf16(const void* src, void* dst, int R, int C, hipStream_t s) {
+  if (R % 8 || C % 8 || R <= 0 || C <= 0) return (int)hipErrorInvalidValue;
+  dim3 grid((C + 63) / 64, (R + 63) / 64);
+  transpose_bf16_kernel<<<grid, 256, 0, s>>>((const bf16_t*)src, (bf16_t*)dst, R, C);
   EDL_LAUNCH_CHECK();
   return 0;
 }

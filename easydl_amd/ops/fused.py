@@ -8,6 +8,7 @@ into the flat gradient buffer (see :mod:`easydl_amd.ops.gradsink`).
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 import torch.nn.functional as F
@@ -186,23 +187,57 @@ def cross_entropy(logits, labels, ignore_index: int = -100):
 # ----------------------------------------------------------------------------
 # Linear / Embedding with direct weight-gradient delivery
 # ----------------------------------------------------------------------------
+# Transposed weight copies.  hipBLASLt runs Y = X W^T (the forward, "NT") at
+# ~1.5 PF/s on MI355X but dX = dY W ("NN") 10-30 % slower on every Llama
+# shape (profiles/r01_gemm_layouts.jsonl); with a [in, out] copy W^T the input
+# gradient becomes dY (W^T)^T, the fast NT form again.  The copy is refreshed
+# by an LDS-tiled HIP transpose (edl_transpose_bf16) in the first forward after
+# the parameters may have changed — FlatParams.zero_grad() starts a new
+# generation, and every parameter mutation (optimizer, state sync, restore)
+# happens between steps — so it costs one 4 B/element pass per step (~6 ms for
+# Llama-3-8B) and 2 B/param of HBM.  EDL_WT_CACHE=0 disables it.
+_WT_GEN = [0]
+_WT_ON = os.environ.get("EDL_WT_CACHE", "1") != "0"
+
+
+def new_weight_generation() -> None:
+    _WT_GEN[0] += 1
+
+
+def _wt_of(w: torch.Tensor):
+    if not (_WT_ON and w.is_cuda and w.dtype == torch.bfloat16 and w.dim() == 2 and w.is_contiguous()
+            and w.shape[0] % 8 == 0 and w.shape[1] % 8 == 0):
+        return None
+    wt = getattr(w, "_edl_wt", None)
+    if wt is None:
+        wt = torch.empty(w.shape[1], w.shape[0], dtype=w.dtype, device=w.device)
+        w._edl_wt = wt
+        w._edl_wt_gen = -1
+    if w._edl_wt_gen != _WT_GEN[0]:
+        _native.kernels().check("edl_transpose_bf16", w.data_ptr(), wt.data_ptr(), w.shape[0], w.shape[1],
+                                _native.stream_of(w))
+        w._edl_wt_gen = _WT_GEN[0]
+    return wt
+
+
 class _LinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b):
         x2 = x.reshape(-1, x.shape[-1])
         y = F.linear(x2, w, b)
-        ctx.save_for_backward(x2, w)
+        wt = _wt_of(w) if ctx.needs_input_grad[0] else None
+        ctx.save_for_backward(x2, w, wt)
         ctx.has_b = b is not None
         ctx.b = b
         return y.view(*x.shape[:-1], w.shape[0])
 
     @staticmethod
     def backward(ctx, dy):
-        x2, w = ctx.saved_tensors
+        x2, w, wt = ctx.saved_tensors
         dy2 = dy.reshape(-1, dy.shape[-1])
         dx = None
         if ctx.needs_input_grad[0]:
-            dx = torch.mm(dy2, w).view(*dy.shape[:-1], w.shape[1])
+            dx = (torch.mm(dy2, wt.t()) if wt is not None else torch.mm(dy2, w)).view(*dy.shape[:-1], w.shape[1])
         dw = db = None
         if ctx.needs_input_grad[1]:
             if gradsink.is_flat(w):

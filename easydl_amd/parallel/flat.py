@@ -132,8 +132,12 @@ class FlatParams:
         """Start a new accumulation window.
 
         Direct-writing ops overwrite on their first write, so no memset is
-        needed unless an autograd-path parameter accumulated last time.
+        needed unless an autograd-path parameter accumulated last time.  Also
+        starts a new weight generation: parameters may have changed since the
+        last step, so cached transposed weight copies are refreshed on use.
         """
+        from easydl_amd.ops.fused import new_weight_generation
+        new_weight_generation()
         if self.saw_autograd:
             for g in self.groups:
                 g.grad.zero_()

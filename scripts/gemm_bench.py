@@ -42,7 +42,10 @@ def main():
     ap.add_argument("--tune-file", default="")
     ap.add_argument("--out", default="")
     ap.add_argument("--layouts", action="store_true", help="also time the W^T [in,out] storage variants")
+    ap.add_argument("--blas", default="", help="hipblaslt | rocblas (torch.backends.cuda.preferred_blas_library)")
     a = ap.parse_args()
+    if a.blas:
+        torch.backends.cuda.preferred_blas_library(a.blas)
     if a.tune:
         import torch.cuda.tunable as tun
         tun.enable(True)
@@ -73,7 +76,7 @@ def main():
         for op, fn in ops.items():
             t = timeit(fn)
             r = {"shape": name, "op": op, "M": M, "K": k, "N": n, "ms": round(t * 1e3, 3),
-                 "tflops": round(flops / t / 1e12, 1), "tuned": a.tune}
+                 "tflops": round(flops / t / 1e12, 1), "tuned": a.tune, "blas": a.blas or "default"}
             if op in total:
                 total[op] += t
             res.append(r)

@@ -167,3 +167,32 @@ def test_linear_direct_grad_into_flat(cuda):
         (x.float() @ ref_w.t()).sum().backward()
     _close(lin.weight.grad, ref_w.grad, 2e-2)
     assert lin.weight.grad.data_ptr() == flat.groups[0].grad.data_ptr() + 0
+
+
+@pytest.mark.parametrize("R,C", [(4096, 6144), (136, 72), (14336, 4096)])
+def test_transpose_bf16(cuda, R, C):
+    from easydl_amd import _native
+    x = torch.randn(R, C, device="cuda").bfloat16()
+    y = torch.empty(C, R, device="cuda", dtype=torch.bfloat16)
+    _native.kernels().check("edl_transpose_bf16", x.data_ptr(), y.data_ptr(), R, C, _native.stream_of(x))
+    assert torch.equal(y, x.t())
+
+
+def test_linear_input_grad_uses_transposed_copy(cuda):
+    """dX through the cached W^T (NT GEMM) equals dY @ W; the copy follows weight updates
+    once a new generation starts (FlatParams.zero_grad)."""
+    from easydl_amd.ops import fused
+    torch.manual_seed(0)
+    w = (torch.randn(512, 256, device="cuda") * 0.05).bfloat16().requires_grad_(True)
+    x = torch.randn(64, 256, device="cuda").bfloat16().requires_grad_(True)
+    for it in range(2):
+        fused.new_weight_generation()
+        y = fused.linear(x, w)
+        dy = torch.randn_like(y)
+        y.backward(dy)
+        ref = (dy.float() @ w.detach().float())
+        assert hasattr(w, "_edl_wt") and torch.equal(w._edl_wt, w.detach().t())
+        torch.testing.assert_close(x.grad.float(), ref, rtol=2e-2, atol=2e-2)
+        x.grad = None
+        with torch.no_grad():
+            w.mul_(0.5)   # "optimizer step" between generations
