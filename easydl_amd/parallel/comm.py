@@ -32,6 +32,16 @@ class CommAborted(RuntimeError):
     """A collective was aborted because membership changed or a peer died."""
 
 
+class CollectiveMismatch(RuntimeError):
+    """Ranks issued different collectives at the same position (EDL_CHECK_COLLECTIVES=1)."""
+
+
+def _signature(kind: str, t: torch.Tensor, extra: int = 0) -> int:
+    """31-bit fingerprint of (kind, numel, dtype, extra) — identical on every rank for the same call."""
+    import zlib
+    return zlib.crc32(f"{kind}:{t.numel()}:{t.dtype}:{extra}".encode()) & 0x7FFFFFFF
+
+
 def _td(s: float) -> datetime.timedelta:
     return datetime.timedelta(seconds=s)
 
@@ -51,6 +61,10 @@ class Communicator:
         self.xgmi_probe: dict | None = None
         self._aborted = False
         self._lock = threading.Lock()
+        # debug: verify every rank issues the same collective sequence (the classic
+        # DDP hang: one rank's bucket order or sizes differ) — SURVEY.md §5.2
+        self.check = os.environ.get("EDL_CHECK_COLLECTIVES", "0") == "1"
+        self._seq = 0
         t0 = time.perf_counter()
         base = dist.PrefixStore(f"edl/{job}/e{epoch}" + (f"/{tag}" if tag else ""), store)
         self.ctrl = dist.ProcessGroupGloo(dist.PrefixStore("ctrl", base), rank, world_size, _td(control_timeout_s))
@@ -187,9 +201,22 @@ class Communicator:
                 pass
 
     # -- data plane ------------------------------------------------------------
+    def _verify(self, kind: str, t: torch.Tensor, extra: int = 0) -> None:
+        """Agree on (sequence number, signature) over the CPU control plane before the call."""
+        if not self.check or self.world_size == 1:
+            return
+        self._seq += 1
+        sig = float(_signature(kind, t, extra))
+        v = self.ctrl_all_reduce([sig, -sig, float(self._seq), -float(self._seq)], dist.ReduceOp.MAX)
+        if v[0] != -v[1] or v[2] != -v[3]:
+            raise CollectiveMismatch(
+                f"rank {self.rank} epoch {self.epoch}: collective #{self._seq} {kind}(numel={t.numel()}, "
+                f"{t.dtype}) differs across ranks (signatures {int(v[0])}..{int(-v[1])})")
+
     def all_reduce_async(self, t: torch.Tensor, op=dist.ReduceOp.SUM):
         if self._aborted:
             raise CommAborted("communicator aborted")
+        self._verify("all_reduce", t, int(op))
         if self.rccl is not None:
             return self._native(self.rccl.all_reduce_async, t, op)
         if self.xgmi is not None and self.xgmi_mode == "xgmi" and op == dist.ReduceOp.SUM and self.xgmi.supports(t):
@@ -205,6 +232,7 @@ class Communicator:
     def broadcast(self, t: torch.Tensor, src: int) -> torch.Tensor:
         if self._aborted:
             raise CommAborted("communicator aborted")
+        self._verify("broadcast", t, src)
         if self.rccl is not None:
             self._wait(self._native(self.rccl.broadcast_async, t, src))
             return t
