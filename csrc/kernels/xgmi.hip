@@ -58,7 +58,7 @@ __device__ bool xg_barrier(const XgmiPeers& P, int rank, int nranks, int phase, 
       while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < round) {
         if (*abort_word || now_ticks() > deadline) {
           good = 0;
-          atomicOr(status, 1);
+          __hip_atomic_store(status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);  // host-mapped word
           break;
         }
         __builtin_amdgcn_s_sleep(2);

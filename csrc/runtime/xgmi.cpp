@@ -25,7 +25,8 @@ struct Workspace {
   void* flags = nullptr;
   int* abort_host = nullptr;
   int* abort_dev = nullptr;
-  int* status = nullptr;
+  int* status = nullptr;       // device view of status_host
+  int* status_host = nullptr;
   int nranks = 1, rank = 0;
   std::vector<char*> peer_data;    // nranks (own included)
   std::vector<void*> peer_flags;   // nranks
@@ -48,8 +49,14 @@ int edl_xgmi_ws_create(int device, uint64_t data_bytes, void** out) {
     *w->abort_host = 0;
     e = hipHostGetDevicePointer((void**)&w->abort_dev, w->abort_host, 0);
   }
-  if (e == hipSuccess) e = hipMalloc((void**)&w->status, sizeof(int));
-  if (e == hipSuccess) e = hipMemset(w->status, 0, sizeof(int));
+  // status word in mapped pinned host memory: readable without a hipMemcpy, which
+  // would go through the legacy NULL stream and wait for every blocking stream
+  // (e.g. a CU-masked snapshot copy in flight)
+  if (e == hipSuccess) e = hipHostMalloc((void**)&w->status_host, sizeof(int), hipHostMallocMapped);
+  if (e == hipSuccess) {
+    *w->status_host = 0;
+    e = hipHostGetDevicePointer((void**)&w->status, w->status_host, 0);
+  }
   if (e == hipSuccess) e = hipDeviceSynchronize();
   if (e != hipSuccess) {
     delete w;
@@ -120,12 +127,11 @@ void edl_xgmi_ws_set_abort(void* ws, int v) {
   __atomic_store_n(((Workspace*)ws)->abort_host, v, __ATOMIC_SEQ_CST);
 }
 
-// blocking read of the device status word (0 = ok, 1 = a barrier gave up)
+// status word (0 = ok, 1 = a barrier gave up); valid once the caller has
+// synchronised with the collectives it asks about
 int edl_xgmi_ws_status(void* ws) {
   auto* w = (Workspace*)ws;
-  int v = -1;
-  if (hipMemcpy(&v, w->status, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return -1;
-  return v;
+  return __atomic_load_n(w->status_host, __ATOMIC_ACQUIRE);
 }
 
 int edl_xgmi_ws_destroy(void* ws) {
@@ -139,7 +145,7 @@ int edl_xgmi_ws_destroy(void* ws) {
   }
   if (w->data) hipFree(w->data);
   if (w->flags) hipFree(w->flags);
-  if (w->status) hipFree(w->status);
+  if (w->status_host) hipHostFree(w->status_host);
   if (w->abort_host) hipHostFree(w->abort_host);
   delete w;
   return 0;

@@ -287,7 +287,10 @@ class CheckpointManager:
 
     @staticmethod
     def _make_engine(device: int):
-        e = _native.runtime()("edl_ckpt_engine_create", device, 256 << 20)
+        # snapshot copies run as blit kernels: confine them to EDL_CKPT_CUS CUs (default 8,
+        # one per XCD) so they barely touch the training kernels (csrc/runtime/shm_store.cpp)
+        cus = int(os.environ.get("EDL_CKPT_CUS", 8))
+        e = _native.runtime()("edl_ckpt_engine_create", device, 256 << 20, cus)
         if not e:
             raise RuntimeError("cannot create checkpoint engine")
         return e

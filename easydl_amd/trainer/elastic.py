@@ -71,6 +71,11 @@ class ElasticTrainer:
             torch.cuda.set_device(self.device)
             torch.empty(1, device=self.device)  # HIP context now, so its cost shows up in the timeline
         self.resources = apply_plan(self.ctx, self.device)  # Brain CU mask / HBM cap
+        if self.device.type == "cuda" and torch.cuda.current_stream(self.device).cuda_stream == 0:
+            # never compute on the legacy NULL stream: it implicitly serialises with every
+            # blocking stream, e.g. the CU-masked snapshot copy stream (ckpt/manager.py)
+            self.compute_stream = torch.cuda.Stream(self.device)
+            torch.cuda.set_stream(self.compute_stream)
         self.events = EventLog(os.path.join(self.ctx.run_dir, f"events-{self.ctx.role}{self.ctx.index}.jsonl"),
                                proc=f"{self.ctx.role}{self.ctx.index}")
         self.events.emit("device_ready", s=round(time.perf_counter() - t_init, 4))

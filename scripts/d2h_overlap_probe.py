@@ -38,12 +38,16 @@ def main():
     dst = torch.empty(n, dtype=torch.uint8, pin_memory=True)
     a = torch.randn(8192, 8192, device=dev, dtype=torch.bfloat16)
     b = torch.randn(8192, 8192, device=dev, dtype=torch.bfloat16)
-    iters = 60
+    iters = 200
     flop = 2 * 8192 ** 3 * iters
+    # compute on a non-blocking pool stream: a CU-masked stream is a BLOCKING stream,
+    # which the legacy default stream would implicitly serialise with
+    comp = torch.cuda.Stream(dev)
 
     def gemms():
-        for _ in range(iters):
-            torch.mm(a, b)
+        with torch.cuda.stream(comp):
+            for _ in range(iters):
+                torch.mm(a, b)
 
     gemms()
     torch.cuda.synchronize()
@@ -66,7 +70,7 @@ def main():
                 dst[o:o + chunk].copy_(src[o:o + chunk], non_blocking=True)
             copy_done.record(s)
         gemms()
-        torch.cuda.current_stream().synchronize()
+        comp.synchronize()
         t_gemm = time.perf_counter() - t0
         copy_done.synchronize()
         t_copy = time.perf_counter() - t0
