@@ -73,7 +73,8 @@ def main(args) -> int:
         "n_gpus": n if gpus else 0,
         "model": (args.model if not args.layers else f"{args.model}-L{args.layers}") if gpus else "llama-tiny (CPU)",
         "breakdown": ttr, "operator_rc": rc, "hot_standby": getattr(args, "standby", 0),
-        "replacement_from_standby": any(e["kind"] == "spawn" and e.get("standby") for e in ev), "restored_from": restored[0].get("source") if restored else None,
+        "replacement_from_standby": any(e["kind"] == "spawn" and e.get("standby") for e in ev),
+        "restored_from": restored[0].get("source") if restored else None,
         "worlds_seen": sorted({w for w in worlds if w}), "run_dir": run_dir,
     }
     print(json.dumps(out), flush=True)

@@ -11,9 +11,11 @@ P3="WRITE_SIZE GRBM_GUI_ACTIVE"
 i=0
 for P in "$P1" "$P2" "$P3"; do
   i=$((i+1))
-  timeout -s KILL 240 rocprofv3 --kernel-trace --pmc $P --output-format csv -d gpurun_out/pmc/p$i -o k -- python3 scripts/pmc_kernels.py > gpurun_out/pmc/p$i.log 2>&1
+  timeout -s KILL 240 rocprofv3 --kernel-trace --pmc $P --output-format csv \
+  -d gpurun_out/pmc/p$i -o k -- python3 scripts/pmc_kernels.py > gpurun_out/pmc/p$i.log 2>&1
   rc=$?; echo "pmc pass $i rc=$rc"; [ $rc -eq 0 ] || exit $rc
 done
-timeout -k 10 400 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d gpurun_out/pmc/ckpt -o bench -- python3 bench.py --steps 3 --warmup 1 --ckpt-interval 1 > gpurun_out/pmc/ckpt.log 2>&1
+timeout -k 10 400 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv \
+  -d gpurun_out/pmc/ckpt -o bench -- python3 bench.py --steps 3 --warmup 1 --ckpt-interval 1 > gpurun_out/pmc/ckpt.log 2>&1
 rc=$?; echo "ckpt trace rc=$rc"; grep metric gpurun_out/pmc/ckpt.log | tail -1
 exit $rc
