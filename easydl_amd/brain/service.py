@@ -61,6 +61,19 @@ class _Handler(BaseHTTPRequestHandler):
         n = int(self.headers.get("Content-Length", 0))
         body = json.loads(self.rfile.read(n).decode() or "{}")
         try:
+            from easydl_amd.api.schema import errors, SCHEMAS
+            if self.path in ("/startup_plan", "/next_plan"):
+                bad = errors(body.get("features", {}), {"type": "object"})
+                if self.path == "/next_plan":
+                    bad += errors(body.get("plan"), SCHEMAS["ResourcePlan"], "$.plan")
+                if bad:
+                    data = json.dumps({"error": "schema", "details": bad}).encode()
+                    self.send_response(400)
+                    self.send_header("Content-Type", "application/json")
+                    self.send_header("Content-Length", str(len(data)))
+                    self.end_headers()
+                    self.wfile.write(data)
+                    return
             if self.path == "/startup_plan":
                 out = self.planner.startup_plan(JobFeatures.from_dict(body.get("features")), host_inventory()).to_dict()
             elif self.path == "/next_plan":

@@ -91,6 +91,24 @@ def cmd_brain(a):
     bmain(["--port", str(a.port)])
 
 
+def cmd_schema(a):
+    from easydl_amd.api.schema import SCHEMAS, document
+    kinds = [a.kind] if a.kind else sorted(SCHEMAS)
+    print(json.dumps({k: document(k) for k in kinds} if len(kinds) > 1 else document(kinds[0]), indent=1))
+
+
+def cmd_validate(a):
+    """Schema-check every document of a spec file (exit 1 on any violation)."""
+    from easydl_amd.api.schema import validate
+    from easydl_amd.api.spec import load_yaml_docs
+    bad = 0
+    for i, d in enumerate(load_yaml_docs(a.spec)):
+        errs = validate(d)
+        print(json.dumps({"doc": i, "kind": d.get("kind"), "ok": not errs, "errors": errs}))
+        bad += bool(errs)
+    return 1 if bad else 0
+
+
 def main(argv=None):
     logging.basicConfig(level=logging.INFO, format="%(asctime)s %(name)s %(message)s")
     ap = argparse.ArgumentParser(prog="edl")
@@ -115,6 +133,12 @@ def main(argv=None):
         if name == "kill":
             p.add_argument("--node", required=True)
         p.set_defaults(fn=fn)
+    sc = sub.add_parser("schema", help="print the JSON Schema of control-plane messages")
+    sc.add_argument("kind", nargs="?", default=None)
+    sc.set_defaults(fn=cmd_schema)
+    v = sub.add_parser("validate", help="schema-check an ElasticJob / JobResource spec file")
+    v.add_argument("spec")
+    v.set_defaults(fn=cmd_validate)
     b = sub.add_parser("brain")
     b.add_argument("--port", type=int, default=8808)
     b.set_defaults(fn=cmd_brain)

@@ -398,7 +398,16 @@ class ElasticOperator:
             return
         if raw is None:
             return
-        jr = JobResource.from_dict(raw if isinstance(raw, dict) else json.loads(raw))
+        doc = raw if isinstance(raw, dict) else json.loads(raw)
+        from easydl_amd.api.schema import validate
+        errs = validate(doc, "JobResource")
+        if errs:
+            if doc.get("spec", {}).get("version") != getattr(self, "_rejected_version", None):
+                self._rejected_version = doc.get("spec", {}).get("version")
+                log.error("JobResource rejected by schema: %s", errs)
+                self.events.emit("jobresource_rejected", errors=errs[:8])
+            return
+        jr = JobResource.from_dict(doc)
         if jr.selector != self.job.name:
             log.error("JobResource selector %s does not match job %s: ignored", jr.selector, self.job.name)
             return
