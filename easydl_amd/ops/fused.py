@@ -220,6 +220,31 @@ def _wt_of(w: torch.Tensor):
     return wt
 
 
+# Weight gradients in NT form.  dW = dY^T X is a "TN" GEMM, 15-35 % slower in
+# hipBLASLt than the NT form dW = (dY^T) (X^T)^T on contiguous transposed
+# activations (profiles/r01_gemm_nt_wgrad.jsonl).  The two LDS-tiled transposes
+# cost less than that gap when the input width K is small next to the output
+# width (qkv, o, gate_up, lm_head: net -0.14 / -0.02 / -0.34 / -1.9 ms per
+# 16k-token micro-batch); for wide inputs (down-proj, K = 14336) the X
+# transpose eats the gain, so those keep the TN call.  EDL_NT_WGRAD=0 disables.
+_NT_WGRAD = os.environ.get("EDL_NT_WGRAD", "1") != "0"
+_NT_WGRAD_MAX_K = 8192
+
+
+def _transposed(t: torch.Tensor) -> torch.Tensor:
+    t = t.contiguous()
+    out = torch.empty(t.shape[1], t.shape[0], dtype=t.dtype, device=t.device)
+    _native.kernels().check("edl_transpose_bf16", t.data_ptr(), out.data_ptr(), t.shape[0], t.shape[1],
+                            _native.stream_of(t))
+    return out
+
+
+def _nt_wgrad_ok(dy2: torch.Tensor, x2: torch.Tensor) -> bool:
+    return (_NT_WGRAD and dy2.is_cuda and dy2.dtype == torch.bfloat16 and x2.dtype == torch.bfloat16
+            and x2.shape[1] <= _NT_WGRAD_MAX_K and dy2.shape[0] % 8 == 0 and dy2.shape[1] % 8 == 0
+            and x2.shape[1] % 8 == 0)
+
+
 class _LinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b):
@@ -240,10 +265,14 @@ class _LinearFn(torch.autograd.Function):
             dx = (torch.mm(dy2, wt.t()) if wt is not None else torch.mm(dy2, w)).view(*dy.shape[:-1], w.shape[1])
         dw = db = None
         if ctx.needs_input_grad[1]:
-            if gradsink.is_flat(w):
-                gradsink.write_mm(w, dy2.t(), x2)
+            if _nt_wgrad_ok(dy2, x2):
+                a, b_ = _transposed(dy2), _transposed(x2).t()   # dY^T (contiguous) @ (X^T)^T: NT GEMM
             else:
-                dw = torch.mm(dy2.t(), x2)
+                a, b_ = dy2.t(), x2
+            if gradsink.is_flat(w):
+                gradsink.write_mm(w, a, b_)
+            else:
+                dw = torch.mm(a, b_)
         if ctx.has_b and ctx.needs_input_grad[2]:
             b = ctx.b
             g = dy2.sum(0)

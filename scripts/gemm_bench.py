@@ -23,6 +23,12 @@ def shapes(model: str):
             "gate_up": (c.dim, 2 * c.ffn_dim), "down": (c.ffn_dim, c.dim), "lm_head": (c.dim, c.vocab_size)}
 
 
+def tr(src, dst):
+    from easydl_amd import _native
+    _native.kernels().check("edl_transpose_bf16", src.data_ptr(), dst.data_ptr(), src.shape[0], src.shape[1],
+                            _native.stream_of(src))
+
+
 def timeit(fn, iters=10):
     for _ in range(3):
         fn()
@@ -64,6 +70,7 @@ def main():
         dw = torch.empty(n, k, device=dev, dtype=torch.bfloat16)
         flops = 2.0 * M * k * n
         wt = w.t().contiguous()          # alternative storage: W^T [in, out] row-major
+        dyT, xT = dy.t().contiguous(), x.t().contiguous()
         dwt = torch.empty(k, n, device=dev, dtype=torch.bfloat16)
         ops = {"fwd": lambda: torch.nn.functional.linear(x, w),
                "dgrad": lambda: torch.mm(dy, w),
@@ -72,7 +79,10 @@ def main():
         if a.layouts:
             ops.update({"T_fwd": lambda: torch.mm(x, wt),
                         "T_dgrad": lambda: torch.mm(dy, wt.t()),
-                        "T_wgrad": lambda: torch.mm(x.t(), dy, out=dwt)})
+                        "T_wgrad": lambda: torch.mm(x.t(), dy, out=dwt),
+                        # wgrad in NT form from transposed activations (dY^T [N,M], X^T [K,M] contiguous)
+                        "NT_wgrad": lambda: torch.mm(dyT, xT.t(), out=dw),
+                        "transpose_dy_x": lambda: (tr(dy, dyT), tr(x, xT))})
         for op, fn in ops.items():
             t = timeit(fn)
             r = {"shape": name, "op": op, "M": M, "K": k, "N": n, "ms": round(t * 1e3, 3),
@@ -81,7 +91,7 @@ def main():
                 total[op] += t
             res.append(r)
             print(json.dumps(r), flush=True)
-        del x, w, dy, dw, wt, dwt
+        del x, w, dy, dw, wt, dwt, dyT, xT
         torch.cuda.empty_cache()
     print(json.dumps({"total_ms": {k: round(v * 1e3, 2) for k, v in total.items()}}), flush=True)
     if a.tune:

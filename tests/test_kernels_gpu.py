@@ -196,3 +196,22 @@ def test_linear_input_grad_uses_transposed_copy(cuda):
         x.grad = None
         with torch.no_grad():
             w.mul_(0.5)   # "optimizer step" between generations
+
+
+def test_linear_weight_grad_nt_form_matches(cuda):
+    """dW through transposed activations (NT GEMM) == the TN GEMM result."""
+    from easydl_amd.ops import fused
+    torch.manual_seed(1)
+    x = torch.randn(4096, 1024, device="cuda").bfloat16()
+    w = (torch.randn(3072, 1024, device="cuda") * 0.02).bfloat16()
+    dy = torch.randn(4096, 3072, device="cuda").bfloat16()
+    grads = []
+    for on in (True, False):
+        fused._NT_WGRAD = on
+        wp = w.clone().requires_grad_(True)
+        fused.linear(x, wp).backward(dy)
+        grads.append(wp.grad.float())
+    fused._NT_WGRAD = True
+    ref = dy.float().t() @ x.float()
+    torch.testing.assert_close(grads[0], ref, rtol=2e-2, atol=2e-1)
+    torch.testing.assert_close(grads[0], grads[1], rtol=2e-2, atol=2e-1)
