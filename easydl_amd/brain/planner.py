@@ -161,18 +161,20 @@ class Planner:
             t.setdefault("results", {})
             t["results"][cur] = min(st, t["results"].get(cur, float("inf")))
             choices = list(self.cfg.bucket_choices)
-            if cur in choices:
-                i = choices.index(cur)
+            # hill-climb around the best size measured so far: try its untried neighbours,
+            # settle on it once both have been measured
+            best = min(t["results"], key=t["results"].get)
+            if best in choices:
+                i = choices.index(best)
                 untried = [c for c in (choices[i - 1] if i > 0 else None, choices[i + 1] if i + 1 < len(choices)
                                        else None) if c is not None and c not in t["results"]]
                 if untried:
-                    plan.bucket_mb = untried[0]
-                    changed.append(f"bucket autotune: try {untried[0]} MB")
-                else:
-                    best = min(t["results"], key=t["results"].get)
-                    if best != cur:
-                        plan.bucket_mb = best
-                        changed.append(f"bucket autotune: best {best} MB")
+                    if untried[0] != cur:
+                        plan.bucket_mb = untried[0]
+                        changed.append(f"bucket autotune: try {untried[0]} MB (best so far {best} MB)")
+                elif best != cur:
+                    plan.bucket_mb = best
+                    changed.append(f"bucket autotune: best {best} MB")
         # grow into free GPUs
         wr = plan.roles.get("worker")
         if wr is not None and feat.mode != "ps":

@@ -1,0 +1,91 @@
+"""Unit tier: Brain periodic plans, bucket/interval sizing, and
+the elastic shard dispatcher's requeue-on-death guarantees, on an in-process store."""
+import datetime
+import socket
+
+import torch.distributed as dist
+
+from easydl_amd.api.spec import Resource, ResourcePlan, RoleResource
+from easydl_amd.brain.collectors import GpuInfo, NodeInventory
+from easydl_amd.brain.planner import JobFeatures, Planner, ckpt_interval, grad_bucket_mb, BrainConfig
+from easydl_amd.master.dispatcher import ShardDispatcher
+from easydl_amd.master.store import KV
+
+
+def _inv(n=8, busy=0.0):
+    return NodeInventory(gpus=[GpuInfo(i, "gfx950", 256, 288.0, busy_pct=busy) for i in range(n)], cpus=128,
+                         host_mem_gb=2048)
+
+
+def _plan(workers=4, bucket=128.0):
+    return ResourcePlan(roles={"worker": RoleResource(workers, Resource(gpu=1))}, bucket_mb=bucket)
+
+
+def test_straggler_is_marked_for_eviction_after_a_full_window():
+    p = Planner()
+    feat = JobFeatures(params=8e9, max_workers=4)
+    m = {f"w{i}": {"step_time": 1.0, "window": 20} for i in range(4)}
+    m["w3"]["step_time"] = 1.6
+    nxt = p.next_plan(feat, _inv(4, busy=90), _plan(), m)
+    assert nxt is not None and nxt.per_rank["w3"]["evict"] is True
+    assert "w0" not in nxt.per_rank
+    m["w3"]["window"] = 5                      # not a full window yet: no eviction
+    nxt = Planner().next_plan(feat, _inv(4, busy=90), _plan(), m)
+    assert nxt is None or "w3" not in nxt.per_rank
+
+
+def test_bucket_autotune_tries_neighbours_then_keeps_the_best():
+    p = Planner()
+    feat = JobFeatures(params=8e9, max_workers=4)
+    times = {128.0: 1.00, 64.0: 1.10, 256.0: 0.95, 512.0: 0.97}
+    plan = _plan(bucket=128.0)
+    seen = []
+    for _ in range(6):
+        m = {f"w{i}": {"step_time": times[plan.bucket_mb], "window": 20} for i in range(4)}
+        nxt = p.next_plan(feat, _inv(4, busy=90), plan, m)
+        if nxt is None:
+            break
+        plan = nxt
+        seen.append(plan.bucket_mb)
+    assert plan.bucket_mb == 256.0, seen       # fastest measured size wins
+
+
+def test_scale_up_into_free_gpus():
+    nxt = Planner().next_plan(JobFeatures(params=1e9, max_workers=8), _inv(8), _plan(workers=4),
+                              {"w0": {"step_time": 1.0}})
+    assert nxt.roles["worker"].replicas == 8
+
+
+def test_bucket_and_interval_sizing():
+    assert grad_bucket_mb(8e9, 1) == 128.0
+    b = grad_bucket_mb(8e9, 8)
+    assert 64.0 <= b <= 512.0 and (int(b) & (int(b) - 1)) == 0     # power of two
+    k1 = ckpt_interval(8e9, 1, 1.7, BrainConfig())
+    k8 = ckpt_interval(8e9, 8, 1.7, BrainConfig())
+    assert k1 > k8 >= 1                                               # sharding shortens the copy
+
+
+def _kv():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return KV(dist.TCPStore("127.0.0.1", port, 1, True, timeout=datetime.timedelta(seconds=10)), "t")
+
+
+def test_dispatcher_requeues_a_dead_workers_leases_exactly_once():
+    kv = _kv()
+    d = ShardDispatcher(kv, num_samples=1000, shard_size=100, epochs=1)
+    a = [d.claim("A") for _ in range(3)]
+    b = [d.claim("B") for _ in range(2)]
+    d.complete(a[0])
+    assert d.requeue_dead({"A"}) == [a[1], a[2]]      # completed shards are not requeued
+    got = []
+    while (s := d.claim("B")) is not None:
+        got.append(s)
+        d.complete(s)
+    for s in b:
+        d.complete(s)
+    covered = sorted([a[0]] + b + got)
+    assert covered == list(range(10)), covered         # every shard exactly once
+    assert d.done() == 10
