@@ -156,6 +156,39 @@ int edl_shm_pin(void* h) {
   return (int)e;
 }
 
+// Populate this process's page tables for every slot (MADV_POPULATE_READ, in
+// `threads` parallel ranges).  A hot standby does this ahead of any failure so
+// the restore's staging memcpy never takes a page fault.  Returns 0 or -errno.
+int edl_shm_prefault(void* h, int threads) {
+  auto* s = static_cast<Seg*>(h);
+#ifndef MADV_POPULATE_READ
+#define MADV_POPULATE_READ 22
+#endif
+  uint8_t* d0 = s->data(0);
+  const uint64_t bytes = s->hdr()->slot_bytes * s->hdr()->nslots;
+  if (threads < 1) threads = 1;
+  const uint64_t page = (uint64_t)sysconf(_SC_PAGESIZE);
+  const uint64_t per = round_up((bytes + threads - 1) / threads, page);
+  std::atomic<int> err{0};
+  std::vector<std::thread> ts;
+  for (int t = 0; t < threads; ++t) {
+    const uint64_t lo = per * t;
+    if (lo >= bytes) break;
+    const uint64_t len = lo + per > bytes ? bytes - lo : per;
+    ts.emplace_back([&, lo, len] {
+      if (madvise(d0 + lo, len, MADV_POPULATE_READ) != 0) {
+        // older kernels: touch one byte per page
+        volatile uint8_t sink = 0;
+        for (uint64_t o = 0; o < len; o += page) sink ^= d0[lo + o];
+        (void)sink;
+        err = errno;
+      }
+    });
+  }
+  for (auto& t : ts) t.join();
+  return 0;
+}
+
 void* edl_shm_data(void* h, int slot) { return static_cast<Seg*>(h)->data(slot); }
 uint64_t edl_shm_slot_bytes(void* h) { return static_cast<Seg*>(h)->hdr()->slot_bytes; }
 int edl_shm_nslots(void* h) { return (int)static_cast<Seg*>(h)->hdr()->nslots; }

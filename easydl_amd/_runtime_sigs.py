@@ -28,6 +28,7 @@ SIGS = {
     "edl_shm_open": (vp, [cp, u64, i32, i32]),
     "edl_shm_pin": (i32, [vp]),
     "edl_shm_data": (vp, [vp, i32]),
+    "edl_shm_prefault": (i32, [vp, i32]),
     "edl_shm_slot_bytes": (u64, [vp]),
     "edl_shm_nslots": (i32, [vp]),
     "edl_shm_current": (i32, [vp]),

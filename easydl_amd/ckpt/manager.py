@@ -145,6 +145,35 @@ class ShmSegment:
             self.h = None
 
 
+# Segments a hot standby mapped and pre-faulted before any failure
+# (easydl_amd/operator/standby.py); a restore in the same process reuses them.
+_PREMAPPED: dict[str, ShmSegment] = {}
+
+
+def premap_job_segments(job: str, threads: int = 8) -> list[str]:
+    """Map + pre-fault every snapshot segment of ``job`` not mapped yet (returns the new names)."""
+    new = []
+    pat = re.compile(rf"^edl-{re.escape(job)}(-t\d+of\d+)?-w\d+-s\d+$")
+    for path in sorted(glob.glob(f"/dev/shm/edl-{job}-*")):
+        base = os.path.basename(path)
+        name = "/" + base
+        if not pat.match(base) or name in _PREMAPPED:
+            continue
+        try:
+            seg = ShmSegment(name, create=False)
+        except OSError:
+            continue
+        seg.rt("edl_shm_prefault", seg.h, threads)
+        _PREMAPPED[name] = seg
+        new.append(name)
+    return new
+
+
+def _open_segment(name: str) -> ShmSegment:
+    seg = _PREMAPPED.pop(name, None)
+    return seg if seg is not None else ShmSegment(name, create=False)
+
+
 class CheckpointManager:
     """Periodic sharded in-memory snapshots (+ optional disk persistence) for a trainer.
 
@@ -356,7 +385,7 @@ class CheckpointManager:
         state = dict(self.state_of(trainer))
         dev = next(iter(state.values())).device
         for s, info in enumerate(infos):
-            seg = ShmSegment(self.seg_name(world, s, tag), create=False)
+            seg = _open_segment(self.seg_name(world, s, tag))
             try:
                 _load_shard(lambda off, nb: seg.view(info["slot"], off, nb), info["meta"]["t"], state, dev,
                             info["checksum"], f"shm shard {s} of step {step}", seg=seg, slot=info["slot"])

@@ -116,6 +116,7 @@ class ElasticOperator:
         self._free_gpus = list(self.cfg.gpus)
         self.standbys: dict[str, Proc] = {}      # name -> parked spare
         self._standby_seq = 0
+        self._last_takeover = 0.0
 
     # ------------------------------------------------------------- master
     def start(self) -> None:
@@ -238,6 +239,8 @@ class ElasticOperator:
             return
         if mod is None:
             return  # not a `python -m` entry: a standby could not run it in-process
+        if time.time() - self._last_takeover < 20.0:
+            return  # refill later: a starting spare would compete for CPUs with the replacement's restore
         while len(self.standbys) < want:
             name = f"{self.job.name}-standby-{self._standby_seq}"
             self._standby_seq += 1
@@ -269,6 +272,7 @@ class ElasticOperator:
                 except OSError:
                     pass
             del self.standbys[sname]
+            self._last_takeover = time.time()
             p = Proc(name, role, index, sp.pid, gpu, res, time.time(), generation=generation)
             p.cpus = cpus
             p.standby = sname

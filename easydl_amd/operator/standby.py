@@ -11,7 +11,9 @@ does not depend on WHICH role it will become:
   the HIP runtime (device enumeration) without creating a context on any GPU —
   the GPU is chosen at takeover (``EDL_GPU``), so one spare covers any rank;
 
-then parks on the job store.  When a role process dies the operator writes
+then parks on the job store — and, while parked, maps and pre-faults the
+job's in-memory snapshot segments (/dev/shm), so that if it becomes a
+replacement the restore's staging copy takes no page faults.  When a role process dies the operator writes
 ``standby/assign/<standby name>`` = ``{"env": {...}, "argv": [...]}``; the
 standby applies the environment (role, index, generation, GPU, CU/HBM plan),
 sets ``sys.argv`` and runs the role's module in-process with ``runpy`` — it
@@ -67,12 +69,20 @@ def main() -> int:
     info.update(pid=os.getpid(), ts=time.time())
     kv.set(f"standby/ready/{name}", json.dumps(info))
     key = f"standby/assign/{name}"
+    premap = os.environ.get("EDL_STANDBY_PREMAP", "1") != "0"
+    next_scan = 0.0
     while True:
         a = kv.get(key)
         if a is not None:
             break
         if kv.exists("job/done"):
             return 0
+        if premap and time.monotonic() > next_scan:
+            from easydl_amd.ckpt.manager import premap_job_segments
+            mapped = premap_job_segments(job)
+            if mapped:
+                kv.set(f"standby/premapped/{name}", json.dumps(mapped))
+            next_scan = time.monotonic() + 2.0
         time.sleep(0.005)
     a = a if isinstance(a, dict) else json.loads(a)
     os.environ.update({k: str(v) for k, v in a["env"].items()})

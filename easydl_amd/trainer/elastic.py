@@ -357,9 +357,10 @@ class ElasticTrainer:
     def _maybe_restore(self):
         if self.checkpoint is None:
             return
+        t0 = time.perf_counter()
         st = self.checkpoint.restore_latest(self)
         if st is not None:
-            self.events.emit("restored", step=self.step, source=st)
+            self.events.emit("restored", step=self.step, source=st, s=round(time.perf_counter() - t0, 3))
 
     # ------------------------------------------------------------------ steps
     def _micro_batches(self, data, plan: ElasticBatchPlan):

@@ -106,3 +106,21 @@ def test_snapshot_evaluator_reads_latest(tmp_path):
             assert torch.equal(a.data, b.data)
     finally:
         unlink_job_segments("ckev")
+
+
+def test_premapped_segments_are_reused_by_restore(tmp_path):
+    """A hot standby maps + pre-faults the job's segments; the restore then uses that mapping."""
+    from easydl_amd.ckpt import manager as m
+    seg = m.ShmSegment("/edl-premaptest-w1-s0", 1 << 20, create=True)
+    try:
+        slot = seg.begin()
+        seg.view(slot, 0, 16)[:] = 7
+        seg.commit(slot, 3, 1, 16, 0, {})
+        assert m.premap_job_segments("premaptest") == ["/edl-premaptest-w1-s0"]
+        assert m.premap_job_segments("premaptest") == []              # already mapped
+        s2 = m._open_segment("/edl-premaptest-w1-s0")
+        assert s2.committed()[0]["step"] == 3 and int(s2.view(slot, 0, 16)[5]) == 7
+        s2.close()
+        assert "/edl-premaptest-w1-s0" not in m._PREMAPPED
+    finally:
+        seg.close(unlink=True)
