@@ -289,6 +289,15 @@ class Communicator:
             raise CommAborted(f"native RCCL call failed in epoch {self.epoch}: {e}") from e
 
     def _wait(self, work) -> None:
+        if self.backend == "gloo":
+            # gloo collectives cannot be aborted; a rank blocked on a dead peer would sit in
+            # wait() until gloo's own error path unwinds the ring (~1.5 s measured).  Poll
+            # instead, so the watchdog's abort() releases this rank at once (the abandoned
+            # work object fails on its own when the old group's sockets close).
+            while not work.is_completed():
+                if self._aborted:
+                    raise CommAborted(f"epoch {self.epoch} aborted while waiting for a collective")
+                time.sleep(0.0002)
         try:
             work.wait()
         except Exception as e:

@@ -107,6 +107,11 @@ class ElasticDDP:
         self._works = []
 
     def _on_ready(self, p) -> None:
+        if self.comm is not None and getattr(self.comm, "aborted", False) and self.comm.world_size > 1:
+            # the epoch broke mid-backward (peer died): stop computing gradients nobody will
+            # reduce; the trainer drops the step and re-forms the world
+            from easydl_amd.parallel.comm import CommAborted
+            raise CommAborted(f"epoch {self.comm.epoch} aborted during backward")
         if not self._active():
             return
         b = self._bucket_of.get(id(p))

@@ -373,6 +373,8 @@ class ElasticTrainer:
         total = 0.0
         loss_acc = None
         for i, idx in enumerate(mbs):
+            if self.comm is not None and self.comm.aborted:  # epoch broke: do not start more work
+                raise CommAborted(f"epoch {self.comm.epoch} aborted before micro-batch {i}")
             batch = data.batch(idx, self.device)
             w = len(idx) / plan.global_batch
             ctxm = self.ddp.no_sync() if i < len(mbs) - 1 else _null()
