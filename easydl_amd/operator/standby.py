@@ -11,9 +11,10 @@ does not depend on WHICH role it will become:
   the HIP runtime (device enumeration) without creating a context on any GPU —
   the GPU is chosen at takeover (``EDL_GPU``), so one spare covers any rank;
 
-then parks on the job store — and, while parked, maps and pre-faults the
-job's in-memory snapshot segments (/dev/shm), so that if it becomes a
-replacement the restore's staging copy takes no page faults.  When a role process dies the operator writes
+then parks on the job store.  With ``EDL_STANDBY_PREMAP=1`` it also maps and
+pre-faults the job's snapshot segments while parked (restore 4.9 -> 4.0 s for
+96 GB on one MI355X), but in that run the killed worker's exit, which unpins
+the same pages, took 6.4 s instead of ~2.5 s, so it is off by default.  When a role process dies the operator writes
 ``standby/assign/<standby name>`` = ``{"env": {...}, "argv": [...]}``; the
 standby applies the environment (role, index, generation, GPU, CU/HBM plan),
 sets ``sys.argv`` and runs the role's module in-process with ``runpy`` — it
@@ -69,7 +70,7 @@ def main() -> int:
     info.update(pid=os.getpid(), ts=time.time())
     kv.set(f"standby/ready/{name}", json.dumps(info))
     key = f"standby/assign/{name}"
-    premap = os.environ.get("EDL_STANDBY_PREMAP", "1") != "0"
+    premap = os.environ.get("EDL_STANDBY_PREMAP", "0") == "1"
     next_scan = 0.0
     while True:
         a = kv.get(key)
