@@ -117,6 +117,57 @@ def host_inventory(telemetry: bool = False) -> NodeInventory:
     return NodeInventory(gpus=gpus, cpus=os.cpu_count() or 1, host_mem_gb=mem)
 
 
+# --------------------------------------------------------------------- rocprofv3
+# Kernel classes by name: matrix-core work (hipBLASLt/Tensile GEMMs, our MFMA
+# flash attention) vs. bandwidth-bound work (elementwise, norms, optimizer,
+# copies, collectives).  A role whose GPU time is mostly bandwidth-bound keeps
+# its throughput on a fraction of the 256 CUs — that is the Brain's CU signal.
+_COMPUTE_PAT = ("Cijk_", "gemm", "attn_fwd", "attn_bwd_dq", "attn_bwd_dkdv", "mfma")
+_COMM_PAT = ("ncclDevKernel", "rccl", "xgmi_")
+
+
+def rocprof_kernel_profile(path: str) -> dict | None:
+    """Summarise a ``rocprofv3 --kernel-trace --stats`` kernel-stats CSV.
+
+    Accepts rocprofv3's own ``*_kernel_stats.csv`` (Name, TotalDurationNs, ...)
+    and the trimmed copies under ``profiles/`` (kernel, total_ms, ...).  Returns
+    ``{"total_ms", "compute_frac", "comm_frac", "memory_frac", "top": [...]}``.
+    """
+    import csv
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        lines = [ln for ln in f if not ln.startswith("#")]
+    rows = list(csv.DictReader(lines))
+    if not rows:
+        return None
+    items = []
+    for r in rows:
+        name = r.get("Name") or r.get("kernel") or ""
+        if "TotalDurationNs" in r:
+            ms = float(r["TotalDurationNs"]) / 1e6
+        else:
+            ms = float(r.get("total_ms") or 0.0)
+        items.append((name, ms))
+    total = sum(ms for _, ms in items) or 1.0
+    comp = sum(ms for n, ms in items if any(p in n for p in _COMPUTE_PAT))
+    comm = sum(ms for n, ms in items if any(p in n for p in _COMM_PAT))
+    top = sorted(items, key=lambda x: -x[1])[:5]
+    return {"total_ms": round(total, 3), "compute_frac": round(comp / total, 4), "comm_frac": round(comm / total, 4),
+            "memory_frac": round(max(0.0, 1 - (comp + comm) / total), 4),
+            "top": [{"kernel": n[:80], "ms": round(ms, 3)} for n, ms in top]}
+
+
+def rocprof_rank_profiles(run_dir: str) -> dict[str, dict]:
+    """Per-process kernel profiles a job left under ``<run_dir>/rocprof/<process>/*kernel_stats.csv``."""
+    out = {}
+    for p in glob.glob(os.path.join(run_dir, "rocprof", "*", "*kernel_stats.csv")):
+        prof = rocprof_kernel_profile(p)
+        if prof is not None:
+            out[os.path.basename(os.path.dirname(p))] = prof
+    return out
+
+
 def collect_worker_metrics(kv, nodes: list[str]) -> dict[str, dict]:
     out = {}
     for n in nodes:

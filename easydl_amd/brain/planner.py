@@ -138,6 +138,17 @@ class Planner:
         plan.ckpt_interval = ckpt_interval(feat.params, world, feat.step_time_s, self.cfg)
         return plan
 
+    @staticmethod
+    def cu_for_profile(prof: dict, total_cus: int = 256) -> int | None:
+        """CUs for a rank from its kernel mix: matrix-core heavy ranks keep every CU;
+        bandwidth-bound ranks need only enough CUs to saturate HBM (~1/4 of the chip
+        drives 6 TB/s with 16-byte accesses), scaled by their compute share."""
+        comp = prof.get("compute_frac", 1.0)
+        if comp >= 0.5:
+            return None
+        frac = max(0.25, min(1.0, 0.25 + comp))
+        return int(round(total_cus * frac / 8)) * 8   # whole CUs per XCD
+
     # ------------------------------------------------------------------ periodic
     def next_plan(self, feat: JobFeatures, inv: NodeInventory, current: ResourcePlan,
                   metrics: dict[str, dict]) -> ResourcePlan | None:
@@ -175,6 +186,17 @@ class Planner:
                 elif best != cur:
                     plan.bucket_mb = best
                     changed.append(f"bucket autotune: best {best} MB")
+        # per-rank CU plan from rocprofv3 kernel profiles (metrics[n]["rocprof"], see
+        # collectors.rocprof_kernel_profile): a rank whose GPU time is mostly bandwidth-bound
+        # work (a PS applying AdamW, an evaluator) keeps its speed on a slice of the CUs
+        for n, m in metrics.items():
+            prof = m.get("rocprof")
+            if not prof:
+                continue
+            cu = self.cu_for_profile(prof)
+            if cu is not None and plan.per_rank.get(n, {}).get("cu") != cu:
+                plan.per_rank.setdefault(n, {})["cu"] = cu
+                changed.append(f"{n}: {cu} CUs ({100 * prof['memory_frac']:.0f}% of kernel time bandwidth-bound)")
         # grow into free GPUs
         wr = plan.roles.get("worker")
         if wr is not None and feat.mode != "ps":

@@ -85,15 +85,25 @@ class PlanLoop:
         metrics = {n: m for n in members if (m := master.kv.get(f"metrics/{n}"))}
         if not metrics:
             return
+        # rocprofv3 kernel profiles the roles left under <run_dir>/rocprof/<process>/ (Brain CU signal)
+        from easydl_amd.brain.collectors import rocprof_rank_profiles
+        profs = rocprof_rank_profiles(getattr(master, "run_dir", "") or "")
+        for n in list(metrics):
+            prof = profs.get(n.split(":")[0])
+            if prof is not None:
+                metrics[n] = dict(metrics[n], rocprof=prof)
         newp = self.brain.next_plan(self.features(), self.plan, metrics)
         if newp is None:
             return
         master.events.emit("replan", reason=newp.reason)
         jr = newp.to_job_resource(self.job.name)
         for node, d in newp.per_rank.items():
+            name = node.split(":")[0]
             if d.get("evict"):
-                name = node.split(":")[0]
                 jr.resource_updation.append(ResourceUpdation(name=name, resource=Resource()))
+            elif d.get("cu") and d.get("cu") != (self.plan.per_rank.get(node) or {}).get("cu"):
+                # CU plan from the rank's kernel mix: re-create it with a CU-masked stream
+                jr.resource_updation.append(ResourceUpdation(name=name, resource=Resource(cu=int(d["cu"]))))
         for d in newp.per_rank.values():
             d.pop("evict", None)
         self.plan = newp

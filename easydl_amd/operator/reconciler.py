@@ -219,6 +219,12 @@ class ElasticOperator:
             return taken
         env = self._base_env()
         env.update(delta)
+        if role in [r.strip() for r in env.get("EDL_ROCPROF_ROLES", "").split(",") if r.strip()]:
+            # kernel-stats profile of this incarnation for the Brain's CU plan
+            # (brain/collectors.py::rocprof_rank_profiles reads <run_dir>/rocprof/<name>/)
+            out = os.path.join(self.run_dir, "rocprof", name)
+            argv = ["rocprofv3", "--kernel-trace", "--stats", "--output-format", "csv", "-d", out, "-o", "k",
+                    "--", *argv]
         pid = self.launcher.spawn(name, argv, env=env, cwd=REPO_ROOT,
                                   log_path=os.path.join(self.run_dir, "logs", f"{name}.log"), cpus=cpus)
         p = Proc(name, role, index, pid, gpu, res, time.time(), generation=generation)

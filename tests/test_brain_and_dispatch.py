@@ -1,6 +1,7 @@
 """Unit tier: Brain periodic plans, bucket/interval sizing, and
 the elastic shard dispatcher's requeue-on-death guarantees, on an in-process store."""
 import datetime
+import os
 import socket
 
 import torch.distributed as dist
@@ -10,6 +11,9 @@ from easydl_amd.brain.collectors import GpuInfo, NodeInventory
 from easydl_amd.brain.planner import JobFeatures, Planner, ckpt_interval, grad_bucket_mb, BrainConfig
 from easydl_amd.master.dispatcher import ShardDispatcher
 from easydl_amd.master.store import KV
+
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _inv(n=8, busy=0.0):
@@ -89,3 +93,21 @@ def test_dispatcher_requeues_a_dead_workers_leases_exactly_once():
     covered = sorted([a[0]] + b + got)
     assert covered == list(range(10)), covered         # every shard exactly once
     assert d.done() == 10
+
+
+def test_rocprof_profile_drives_per_rank_cu_plan(tmp_path):
+    """The Brain reads rocprofv3 kernel stats: a bandwidth-bound rank gets a CU share,
+    a matrix-core-bound rank keeps the whole GPU."""
+    from easydl_amd.brain.collectors import rocprof_kernel_profile
+    ps = tmp_path / "ps_kernel_stats.csv"
+    ps.write_text('"Name","Calls","TotalDurationNs","AverageNs","Percentage"\n'
+                  '"void adamw_flat_kernel<float>",100,900000000,9000000,90\n'
+                  '"Cijk_Ailk_Bljk_BBS_BH",10,100000000,10000000,10\n')
+    prof = rocprof_kernel_profile(str(ps))
+    assert prof["memory_frac"] == 0.9 and prof["compute_frac"] == 0.1
+    train = rocprof_kernel_profile(os.path.join(ROOT, "profiles", "r01_bench_kernel_stats_hipattn.csv"))
+    assert train["compute_frac"] > 0.85
+    metrics = {"ps0": {"rocprof": prof}, "w0": {"step_time": 1.0, "rocprof": train}}
+    nxt = Planner().next_plan(JobFeatures(mode="ps", params=3.3e8), _inv(8, busy=90), _plan(), metrics)
+    assert nxt is not None and 0 < nxt.per_rank["ps0"]["cu"] < 256 and nxt.per_rank["ps0"]["cu"] % 8 == 0
+    assert "cu" not in nxt.per_rank.get("w0", {})
