@@ -15,11 +15,19 @@ from easydl_amd.master.features import extract
 job, _ = load_specs("examples/bert_ps.yaml")
 inv = NodeInventory(gpus=[GpuInfo(i, "gfx950", 256, 288.0) for i in range(8)], cpus=128, host_mem_gb=2048)
 plan = Planner().startup_plan(JobFeatures.from_dict(extract(job)), inv)
-job.env.update({"EDL_SAMPLES": "3072", "EDL_SHARD": "64"})
+job.env.update({"EDL_SAMPLES": "3072", "EDL_SHARD": "64", "EDL_ROCPROF_ROLES": "parameter_server"})
 jr = JobResource(f"{job.name}-resource", job.name, plan.roles)
 print(yaml.safe_dump_all([job.to_dict(), jr.to_dict()]))
 PY
 timeout -k 10 500 python -m easydl_amd.cli submit /tmp/bert_ps_1gpu.yaml --gpus 0,0,0,0,0,0,0,0 --run-dir $OUT --timeout 450 > $OUT.log 2>&1
 rc=$?
 grep -h '"worker_done"\|"startup_plan"\|"eval"' $OUT/events-*.jsonl | tail -12
+python -c "
+import json, sys
+from easydl_amd.brain.collectors import rocprof_rank_profiles
+from easydl_amd.brain.planner import Planner
+p = rocprof_rank_profiles('$OUT')
+print(json.dumps({k: dict(v, planned_cu=Planner.cu_for_profile(v)) for k, v in p.items()}))
+" > $OUT/rocprof_profiles.json
+cat $OUT/rocprof_profiles.json
 exit $rc
