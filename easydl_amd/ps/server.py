@@ -128,6 +128,8 @@ class ParameterServer:
         """One optimizer update of the shard from ``grad`` (default: the accumulator)."""
         st = self.state
         g = st.g if grad is None else grad
+        if st.w.is_cuda and hasattr(self.snapshot, "fence"):
+            self.snapshot.fence(st.w.device)  # never update under an in-flight snapshot copy
         self.step += 1
         if self.optimizer == "adam":
             adamw_flat_(None, st.w, st.m, st.v, g, lr=self.lr, beta1=self.betas[0], beta2=self.betas[1],
@@ -335,13 +337,21 @@ class PSSnapshotter:
     def __init__(self, job: str, index: int):
         self.name = f"/edl-{job}-ps{index}"
         self.seg = None
+        self.engine = None
+        self.ticket = None
+        self._keep = None
 
     def __call__(self, ps: ParameterServer) -> None:
         from easydl_amd.ckpt.manager import ShmSegment, checksum_np
         bufs = ps.state_buffers()
         sizes = [b.numel() * 4 for b in bufs]
+        total_bytes = sum(sizes)
+        meta = {"sizes": sizes, "step": ps.step, "table_steps": [t.step for t in ps.tables.values()]}
+        if bufs[0].is_cuda:
+            self._snapshot_async(ps, bufs, sizes, meta)
+            return
         if self.seg is None:
-            self.seg = ShmSegment(self.name, sum(sizes), create=True, pin=False)
+            self.seg = ShmSegment(self.name, total_bytes, create=True, pin=False)
         slot = self.seg.begin()
         total, off = 0, 0
         for buf, nb in zip(bufs, sizes):
@@ -349,8 +359,53 @@ class PSSnapshotter:
             self.seg.view(slot, off, nb)[:] = arr
             total += checksum_np(arr, off // 4)
             off += nb
-        self.seg.commit(slot, ps.version, ps.step, off, total,
-                        {"sizes": sizes, "step": ps.step, "table_steps": [t.step for t in ps.tables.values()]})
+        self.seg.commit(slot, ps.version, ps.step, off, total, meta)
+
+    def _snapshot_async(self, ps: ParameterServer, bufs, sizes, meta) -> None:
+        """HBM-resident shard: checksum on the GPU, D2H through the snapshot engine
+        (CU-masked side stream, pinned segment, commit thread) — the PS keeps
+        serving while the copy runs; the next update waits for it (fence)."""
+        import ctypes
+        import json
+
+        from easydl_amd import _native
+        from easydl_amd.ckpt.manager import CheckpointManager, ShmSegment, checksum_tensor
+        rt = _native.runtime()
+        dev = bufs[0].device
+        cs_off = sum(sizes)
+        if self.seg is None:
+            self.seg = ShmSegment(self.name, cs_off + 8, create=True, pin=True)
+        if self.engine is None:
+            self.engine = CheckpointManager._make_engine(dev.index or 0)
+        if self.ticket is not None:
+            rt("edl_ckpt_wait", self.engine, self.ticket, 600000)  # at most one snapshot in flight
+        csum = torch.zeros(1, dtype=torch.int64, device=dev)
+        ptrs, offs, off = [], [], 0
+        for b, nb in zip(bufs, sizes):
+            checksum_tensor(b.view(-1), csum, base_index=off // 4)
+            ptrs.append(b.data_ptr())
+            offs.append(off)
+            off += nb
+        ptrs.append(csum.data_ptr())
+        offs.append(cs_off)
+        szs = list(sizes) + [8]
+        n = len(ptrs)
+        arr = lambda v: (ctypes.c_uint64 * n)(*v)  # noqa: E731
+        t = rt("edl_ckpt_snapshot", self.engine, self.seg.h, n, arr(ptrs), arr(szs), arr(offs),
+               ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream), ps.version, ps.step, cs_off,
+               json.dumps(meta, separators=(",", ":")).encode())
+        if t < 0:
+            raise RuntimeError(f"PS snapshot enqueue failed: hipError {-t}")
+        self.ticket, self._keep = t, csum
+
+    def fence(self, device) -> None:
+        """The next update of the shard waits (on the GPU) for the in-flight copy."""
+        if self.ticket is not None and self.engine is not None:
+            import ctypes
+
+            from easydl_amd import _native
+            _native.runtime()("edl_ckpt_fence", self.engine, self.ticket,
+                              ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream))
 
     def restore(self, ps: ParameterServer) -> bool:
         from easydl_amd.ckpt.manager import ShmSegment, checksum_np

@@ -161,3 +161,43 @@ def test_ps_gpu_ipc_transport(cuda, tmp_path):
     finally:
         open(pf + ".stop", "w").close()
         ps.wait(timeout=30)
+
+
+@pytest.mark.gpu
+def test_ps_gpu_async_snapshot_restores_exactly(cuda):
+    """HBM-resident PS shard snapshotted through the async engine (CU-masked copy stream,
+    GPU checksum, fenced updates); a replacement PS restores it bit-exactly."""
+    import os
+
+    from easydl_amd import _native
+    from easydl_amd.models.deepctr import DeepFM
+    from easydl_amd.ps.client import shard_of
+    from easydl_amd.ps.embedding import table_shard_spec
+    from easydl_amd.ps.server import ParameterServer, PSSnapshotter
+    torch.manual_seed(0)
+    ref = DeepFM(vocab=200, hidden=(64, 64))
+    snap = PSSnapshotter("snaptest", 0)
+    ps = ParameterServer(0, shard_of(ref, 1, 0), lr=1e-2, device="cuda", tables=table_shard_spec(ref, 1, 0),
+                         snapshot=snap, snapshot_every=3)
+
+    def push():
+        g = {n: torch.randn(ps.state.shapes[n]) for n in ps.state.names}
+        g["sparse/emb/ids"] = torch.randint(0, 200 * 26, (64,))
+        g["sparse/emb/grad"] = torch.randn(64, 16)
+        ps._push("w", g)
+
+    try:
+        for _ in range(6):            # snapshots taken after versions 3 and 6
+            push()
+        expect = [b.clone() for b in ps.state_buffers()]
+        push()                        # version 7: fenced behind the v6 copy
+        assert _native.runtime()("edl_ckpt_wait", snap.engine, snap.ticket, 60000) == 1
+        fresh = ParameterServer(0, shard_of(ref, 1, 0), lr=1e-2, device="cuda", tables=table_shard_spec(ref, 1, 0))
+        assert PSSnapshotter("snaptest", 0).restore(fresh)
+        assert fresh.version == 6
+        assert all(torch.equal(a, b) for a, b in zip(fresh.state_buffers(), expect))
+        assert not torch.equal(ps.state_buffers()[0], expect[0])   # the live shard moved on
+    finally:
+        for f in os.listdir("/dev/shm"):
+            if f.startswith("edl-snaptest-ps"):
+                os.unlink("/dev/shm/" + f)
