@@ -198,6 +198,7 @@ def cross_entropy(logits, labels, ignore_index: int = -100):
 # Llama-3-8B) and 2 B/param of HBM.  EDL_WT_CACHE=0 disables it.
 _WT_GEN = [0]
 _WT_ON = os.environ.get("EDL_WT_CACHE", "1") != "0"
+_WT_BUDGET: list = [None]   # bytes the transposed copies may still take (set at first use)
 
 
 def new_weight_generation() -> None:
@@ -210,6 +211,18 @@ def _wt_of(w: torch.Tensor):
         return None
     wt = getattr(w, "_edl_wt", None)
     if wt is None:
+        if getattr(w, "_edl_wt_skip", False):
+            return None
+        # HBM budget: the copies never take the last EDL_WT_RESERVE_GB (default 48) of free memory
+        # (activations of the first step still have to fit); weights beyond it keep the NN dgrad
+        if _WT_BUDGET[0] is None:
+            free, _ = torch.cuda.mem_get_info(w.device)
+            _WT_BUDGET[0] = free - float(os.environ.get("EDL_WT_RESERVE_GB", 48)) * 2**30
+        need = w.numel() * w.element_size()
+        if need > _WT_BUDGET[0]:
+            w._edl_wt_skip = True
+            return None
+        _WT_BUDGET[0] -= need
         wt = torch.empty(w.shape[1], w.shape[0], dtype=w.dtype, device=w.device)
         w._edl_wt = wt
         w._edl_wt_gen = -1

@@ -1,0 +1,52 @@
+"""Offline-tuned hipBLASLt / rocBLAS GEMM selections (PyTorch TunableOp).
+
+hipBLASLt's heuristic picks a good kernel for most Llama shapes but not all
+(the qkv projection forward gained 18 % from a tuned solution,
+profiles/r01_gemm_shapes_hipblaslt.jsonl).  The framework ships the TunableOp
+results for its own GEMM call forms on gfx950 (`easydl_amd/tuned/`), made by
+one tuning run of the training step (``EDL_GEMM_TUNING=tune``); every later
+run only reads the file (no tuning time, no GPU search).  GEMMs absent from
+the file fall back to the library heuristic.
+
+EDL_GEMM_TUNING: ``use`` (default: read the shipped file if present),
+``tune`` (search every GEMM met and write the file at exit), ``off``.
+"""
+from __future__ import annotations
+
+import atexit
+import logging
+import os
+
+log = logging.getLogger(__name__)
+TUNED_FILE = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tuned",
+                          "tunableop_gfx950.csv")
+
+
+def apply(mode: str | None = None, path: str | None = None) -> str:
+    """Configure TunableOp for this process; returns the mode in effect."""
+    import torch
+    mode = mode or os.environ.get("EDL_GEMM_TUNING", "use")
+    path = path or TUNED_FILE
+    if mode == "off" or not torch.cuda.is_available():
+        return "off"
+    import torch.cuda.tunable as tun
+    if mode == "tune":
+        tun.enable(True)
+        tun.tuning_enable(True)
+        tun.set_max_tuning_iterations(30)
+        tun.set_max_tuning_duration(30)
+        tun.set_filename(path)
+        if hasattr(tun, "write_file"):
+            atexit.register(tun.write_file)   # else TunableOp writes the file at process exit itself
+        return "tune"
+    if not os.path.exists(path):
+        return "off"
+    tun.enable(True)
+    tun.tuning_enable(False)
+    tun.set_filename(path)
+    ok = tun.read_file(path)
+    if not ok:
+        log.warning("TunableOp results %s not loaded (validator mismatch?): library heuristics", path)
+        tun.enable(False)
+        return "off"
+    return "use"

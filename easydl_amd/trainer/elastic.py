@@ -71,6 +71,9 @@ class ElasticTrainer:
             torch.cuda.set_device(self.device)
             torch.empty(1, device=self.device)  # HIP context now, so its cost shows up in the timeline
         self.resources = apply_plan(self.ctx, self.device)  # Brain CU mask / HBM cap
+        if self.device.type == "cuda":
+            from easydl_amd.ops import gemm_tuning
+            self.gemm_tuning = gemm_tuning.apply()  # shipped TunableOp selections (or tune / off)
         if self.device.type == "cuda" and torch.cuda.current_stream(self.device).cuda_stream == 0:
             # never compute on the legacy NULL stream: it implicitly serialises with every
             # blocking stream, e.g. the CU-masked snapshot copy stream (ckpt/manager.py)

@@ -43,3 +43,10 @@ def test_bert_large_ps_plan_is_2ps_6workers_with_cu_hbm():
     ps, w = plan.roles["parameter_server"], plan.roles["worker"]
     assert (ps.replicas, w.replicas) == (2, 6), plan.reason
     assert ps.resource.gpu == 1 and 0 < ps.resource.cu < 256 and 0 < ps.resource.hbm_gb < 288
+
+
+def test_gemm_tuning_is_off_without_a_gpu(monkeypatch):
+    from easydl_amd.ops import gemm_tuning
+    monkeypatch.setenv("EDL_GEMM_TUNING", "use")
+    assert gemm_tuning.apply() == "off"          # CPU tier: no TunableOp, no file needed
+    assert gemm_tuning.TUNED_FILE.endswith("tunableop_gfx950.csv")
