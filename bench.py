@@ -49,6 +49,8 @@ def parse():
     ap.add_argument("--ckpt-interval", type=int, default=0,
                     help="in-memory sharded snapshot every K steps (async D2H, overlapped)")
     ap.add_argument("--fault-inject", action="store_true", help="measure time-to-recover instead (local operator)")
+    ap.add_argument("--scale-up", default=None, metavar="START:END",
+                    help="measure an elastic scale-up mid-run instead (BASELINE config 2, ResNet-50)")
     ap.add_argument("--standby", type=int, default=1,
                     help="--fault-inject: warm spare workers kept by the operator (0 = cold respawn)")
     ap.add_argument("--comm", default=None, choices=["pg", "native", "xgmi", "auto"],
@@ -64,6 +66,10 @@ def main():
     if args.fault_inject:
         from easydl_amd.trainer import fault_bench
         return fault_bench.main(args)
+    if args.scale_up:
+        from easydl_amd.trainer import scale_bench
+        start, end = args.scale_up.split(":")
+        return scale_bench.main(["--start", start, "--end", end, "--steps", str(args.warmup + args.steps)])
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))

@@ -56,6 +56,26 @@ class PlanLoop:
         master.events.emit("plan_applied", version=self.version, replicas={r: v.replicas for r, v in
                                                                              jr.roles.items()})
 
+    def _adopt_external(self, master) -> None:
+        """A JobResource written by someone else (``edl scale`` / ``edl apply`` / a user
+        tool) supersedes the plan: follow its worker target so the rendezvous grows or
+        shrinks the world to it (the operator already reconciles the processes)."""
+        raw = master.kv.get("jobresource")
+        if raw is None:
+            return
+        doc = raw if isinstance(raw, dict) else json.loads(raw)
+        ver = int((doc.get("spec") or {}).get("version", 0))
+        if ver == self.version:
+            return
+        jr = JobResource.from_dict(doc)
+        self.version = ver
+        if self.plan is not None:
+            self.plan.roles = jr.roles
+        wr = jr.roles.get("worker")
+        if wr is not None and self.job.mode == "allreduce":
+            master.rdzv.target_nodes = wr.replicas
+        master.events.emit("jobresource_adopted", version=ver, replicas={r: v.replicas for r, v in jr.roles.items()})
+
     def maybe_replan(self, master) -> None:
         now = time.time()
         if not self.started:
@@ -78,6 +98,7 @@ class PlanLoop:
             self.started = True
             self._last = now
             return
+        self._adopt_external(master)
         if self.period_s <= 0 or now - self._last < self.period_s:
             return
         self._last = now

@@ -192,13 +192,17 @@ class ElasticOperator:
         if res.hbm_gb:
             env["EDL_HBM_GB"] = str(res.hbm_gb)
         cpus = []
-        if res.cpu and self.cfg.cpus:
+        if res.cpu:
+            # the role's CPU share bounds its intra-op threads even without pinning: N
+            # processes x all-core OpenMP pools oversubscribe the host (measured: a 3-worker
+            # CPU job ran 4.8 s steps instead of 8 ms)
             n = max(1, int(res.cpu))
-            used = set()
-            for p in list(self.procs.values()) + list(self.standbys.values()):
-                used |= set(getattr(p, "cpus", []))
-            cpus = [c for c in self.cfg.cpus if c not in used][:n]
             env["OMP_NUM_THREADS"] = str(n)
+            if self.cfg.cpus:
+                used = set()
+                for p in list(self.procs.values()) + list(self.standbys.values()):
+                    used |= set(getattr(p, "cpus", []))
+                cpus = [c for c in self.cfg.cpus if c not in used][:n]
         return env, gpu, cpus
 
     def _argv_for(self, role: str) -> list[str]:

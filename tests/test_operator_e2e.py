@@ -87,3 +87,17 @@ def test_hot_standby_takes_over_failed_worker(tmp_path):
     assert spawns[1]["pid"] in {e["pid"] for e in sb}           # no new process: the standby's pid
     res = [json.load(open(f)) for f in glob.glob(str(run / "res*.json"))]
     assert len({x["hash"] for x in res}) == 1 and all(x["step"] == 40 for x in res), res
+
+
+@pytest.mark.slow
+def test_scale_up_mid_run_through_jobresource():
+    """BASELINE config 2 path on CPU: a JobResource update mid-run (what `edl scale` writes)
+    grows the world 1 -> 3 without restarting the running worker."""
+    r = subprocess.run([sys.executable, "-m", "easydl_amd.trainer.scale_bench", "--start", "1", "--end", "3",
+                        "--steps", "300", "--scale-step", "5"], cwd=ROOT, capture_output=True, text=True,
+                       timeout=400, env=dict(os.environ, PYTHONPATH=ROOT))
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert set(out["images_per_s_by_world"]) == {"1", "3"}, out
+    s = out["scale_up_s"]
+    assert s["epoch_formed"] is not None and s["first_step"] is not None and s["first_step"] < 30, s
