@@ -33,8 +33,8 @@ def apply(mode: str | None = None, path: str | None = None) -> str:
     if mode == "tune":
         tun.enable(True)
         tun.tuning_enable(True)
-        tun.set_max_tuning_iterations(30)
-        tun.set_max_tuning_duration(30)
+        tun.set_max_tuning_iterations(int(os.environ.get("EDL_GEMM_TUNING_ITERS", 10)))
+        tun.set_max_tuning_duration(int(os.environ.get("EDL_GEMM_TUNING_MS", 10)))
         tun.set_filename(path)
         if hasattr(tun, "write_file"):
             atexit.register(tun.write_file)   # else TunableOp writes the file at process exit itself
