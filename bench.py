@@ -56,6 +56,7 @@ def parse():
     ap.add_argument("--comm", default=None, choices=["pg", "native", "xgmi", "auto"],
                     help="gradient all-reduce data plane (default $EDL_COMM or pg = ProcessGroupNCCL/RCCL; "
                          "xgmi = hand-written IPC all-reduce; auto = probe both at each epoch, keep the faster)")
+    ap.add_argument("--sp", action="store_true", help="Megatron sequence parallelism inside the TP group")
     ap.add_argument("--tp", type=int, default=1,
                     help="tensor-parallel degree inside each DP replica (BASELINE config 5: --model llama3-70b --tp 8)")
     return ap.parse_args()
@@ -80,6 +81,8 @@ def main():
     os.environ.setdefault("EDL_JOB", "bench")
     if args.comm:
         os.environ["EDL_COMM"] = args.comm
+    if args.sp:
+        os.environ["EDL_SP"] = "1"
     os.environ.setdefault("EDL_RUN_DIR", os.path.join("gpurun_out", "bench_run") if use_cuda else "/tmp/edl_bench")
 
     from easydl_amd.models.llama import Llama, get_config
@@ -156,7 +159,7 @@ def main():
             "model": args.model if not args.layers else f"{args.model}-L{args.layers}",
             "global_batch": gb,
             "seq_len": S,
-            "parallelism": f"dp{comm.world_size // tp}" + (f"tp{tp}" if tp > 1 else ""),
+            "parallelism": f"dp{comm.world_size // tp}" + (f"tp{tp}" if tp > 1 else "") + ("sp" if args.sp else ""),
             "micro_batch": B,
             "grad_accum": args.accum,
             "optimizer": "AdamW fp32 master/moments, clip 1.0",

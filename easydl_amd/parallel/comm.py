@@ -226,7 +226,7 @@ class Communicator:
         return self.data.allreduce([t], o)
 
     def all_reduce(self, t: torch.Tensor, op=dist.ReduceOp.SUM) -> torch.Tensor:
-        self._wait(self.all_reduce_async(t, op))
+        self._wait(self.all_reduce_async(t, op), poll=True)
         return t
 
     def broadcast(self, t: torch.Tensor, src: int) -> torch.Tensor:
@@ -238,7 +238,7 @@ class Communicator:
             return t
         o = dist.BroadcastOptions()
         o.rootRank = src
-        self._wait(self.data.broadcast([t], o))
+        self._wait(self.data.broadcast([t], o), poll=True)
         return t
 
     def all_gather_into(self, out: torch.Tensor, inp: torch.Tensor) -> torch.Tensor:
@@ -288,8 +288,15 @@ class Communicator:
         except RuntimeError as e:
             raise CommAborted(f"native RCCL call failed in epoch {self.epoch}: {e}") from e
 
-    def _wait(self, work) -> None:
-        if self.backend == "gloo":
+    def wait_work(self, work) -> None:
+        """Wait for an all-reduce work object (DDP buckets): abortable on gloo."""
+        self._wait(work, poll=True)
+
+    def _wait(self, work, poll: bool = False) -> None:
+        # poll only for collectives whose gloo work progresses on its own thread
+        # (allreduce / broadcast / allgather); gloo's _reduce_scatter_base runs inside
+        # wait() and would never report completion to a poller
+        if poll and self.backend == "gloo":
             # gloo collectives cannot be aborted; a rank blocked on a dead peer would sit in
             # wait() until gloo's own error path unwinds the ring (~1.5 s measured).  Poll
             # instead, so the watchdog's abort() releases this rank at once (the abandoned
@@ -310,7 +317,7 @@ class Communicator:
         t = torch.as_tensor(values, dtype=torch.float64).clone().reshape(-1)
         o = dist.AllreduceOptions()
         o.reduceOp = op
-        self._wait(self.ctrl.allreduce([t], o))
+        self._wait(self.ctrl.allreduce([t], o), poll=True)
         return t
 
     def ctrl_broadcast(self, values, src: int) -> torch.Tensor:

@@ -139,8 +139,9 @@ class ElasticDDP:
                 b.ready = True
             self._launch_ready()
             t0 = time.perf_counter()
+            wait = getattr(self.comm, "wait_work", None)
             for w in self._works:
-                w.wait()
+                wait(w) if wait is not None else w.wait()
             self.stats["wait_s"] += time.perf_counter() - t0
         self._works = []
         self.prepare()

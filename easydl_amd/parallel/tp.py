@@ -130,6 +130,14 @@ def copy_to_tp(x, g: TPGroup):
     return _CopyToTP.apply(x, g) if g.size > 1 else x
 
 
+def gather_from_sp(x, g: TPGroup):
+    return _GatherFromSP.apply(x, g) if g.size > 1 else x
+
+
+def scatter_to_sp(x, g: TPGroup):
+    return _ScatterToSP.apply(x, g) if g.size > 1 else x
+
+
 def reduce_from_tp(x, g: TPGroup):
     return _ReduceFromTP.apply(x, g) if g.size > 1 else x
 
@@ -182,8 +190,15 @@ class LlamaTP(nn.Module):
         for _ in range(cfg.n_layers):
             blk = LlamaBlock(cfg, device, dtype, n_heads=cfg.n_heads // tp, n_kv_heads=cfg.n_kv_heads // tp,
                              ffn_dim=cfg.ffn_dim // tp)
-            blk.tp_reduce = lambda x, _g=g: reduce_from_tp(x, _g)
-            blk.tp_copy = lambda x, _g=g: copy_to_tp(x, _g)
+            if g.sequence_parallel:
+                # Megatron-SP: the residual stream and norms live on a 1/tp token shard;
+                # all-gather before the column-parallel GEMMs, reduce-scatter after the
+                # row-parallel ones (same bytes as the all-reduce, 1/tp the activations)
+                blk.tp_reduce = lambda x, _g=g: scatter_to_sp(x, _g)
+                blk.tp_copy = lambda x, _g=g: gather_from_sp(x, _g)
+            else:
+                blk.tp_reduce = lambda x, _g=g: reduce_from_tp(x, _g)
+                blk.tp_copy = lambda x, _g=g: copy_to_tp(x, _g)
             self.layers.append(blk)
         self.norm = _param((d,), 0, device, dtype)
         self.lm_head = _param((self.vshard, d), cfg.init_std, device, dtype)
@@ -196,6 +211,22 @@ class LlamaTP(nn.Module):
 
     rope = Llama.rope
 
+    def sync_sp_grads(self, flat=None) -> None:
+        """Sequence parallelism: each TP rank's norm weights saw only its token shard,
+        so their gradients are partial — sum them over the TP group (after backward,
+        before clipping).  ``flat``: a FlatParams whose groups hold these parameters
+        (one all-reduce per group) — else per parameter."""
+        if not self.g.sequence_parallel or self.g.size == 1:
+            return
+        if flat is not None:
+            for grp in flat.groups:
+                if grp.slots and all(getattr(sl.param, "_tp_replicated", False) for sl in grp.slots):
+                    self.g.all_reduce(grp.grad)
+            return
+        for p in self.parameters():
+            if getattr(p, "_tp_replicated", False) and p.grad is not None:
+                p.grad.copy_(self.g.all_reduce(p.grad))
+
     @property
     def vstart(self) -> int:  # follows the group's current rank (elastic re-ranking)
         return self.g.rank * self.vshard
@@ -207,12 +238,15 @@ class LlamaTP(nn.Module):
         local = (flat >= self.vstart) & (flat < self.vstart + self.vshard)
         x = fused.embedding((flat - self.vstart).clamp(0, self.vshard - 1), self.embed)
         x = x * local[:, None].to(x.dtype)
-        x = reduce_from_tp(x, self.g)
+        sp = self.g.sequence_parallel and self.g.size > 1
+        if sp and flat.numel() % self.g.size:
+            raise ValueError(f"sequence parallelism needs B*S ({flat.numel()}) divisible by tp={self.g.size}")
+        x = scatter_to_sp(x, self.g) if sp else reduce_from_tp(x, self.g)
         resid, delta = x, None
         for layer in self.layers:
             resid, delta = layer(resid, delta, B, S, cos, sin)
         n, _ = norms.add_rmsnorm(delta, resid, self.norm, self.cfg.norm_eps)
-        n = copy_to_tp(n, self.g)
+        n = gather_from_sp(n, self.g) if sp else copy_to_tp(n, self.g)
         logits = fused.linear(n, self.lm_head)
         if labels is None:
             return logits

@@ -100,7 +100,7 @@ class ElasticTrainer:
             self._build_model(0)
         else:
             from easydl_amd.parallel.tp import TPGroup
-            self.tp_group = TPGroup(size=self.tp)
+            self.tp_group = TPGroup(size=self.tp, sequence_parallel=os.environ.get("EDL_SP", "0") == "1")
         self.global_batch = global_batch
         self.micro_batch = micro_batch
         self.step = 0                # committed optimizer steps
@@ -393,6 +393,8 @@ class ElasticTrainer:
         # finish() zero-fills untouched gradients before flushing the buckets.
         with trace.range("grad_sync"):
             self.ddp.finish()
+            if hasattr(self.model, "sync_sp_grads"):
+                self.model.sync_sp_grads(self.flat)   # sequence-parallel norm grads: sum over TP
         self.fault.maybe_inject("after_backward", self.step, trainer=self)
         return None if loss_acc is None else loss_acc / total
 

@@ -23,7 +23,7 @@ ids = torch.randint(0, 128, (2, 16))
 labels = torch.randint(0, 128, (2, 16))
 loss_d = dense(ids, labels)
 loss_d.backward()
-g = TPGroup(comm)
+g = TPGroup(comm, sequence_parallel=os.environ.get("SP") == "1")
 tp = LlamaTP(cfg, g, dtype=torch.float32)
 sd = shard_state_dict({k: v.detach() for k, v in dense.named_parameters()}, cfg, rank, world)
 with torch.no_grad():
@@ -31,6 +31,7 @@ with torch.no_grad():
         p.copy_(sd[n])
 loss_t = tp(ids, labels)
 loss_t.backward()
+tp.sync_sp_grads()
 dgrads = shard_state_dict({k: v.grad for k, v in dense.named_parameters()}, cfg, rank, world)
 err = max((p.grad - dgrads[n]).abs().max().item() / (dgrads[n].abs().max().item() + 1e-9)
           for n, p in tp.named_parameters())

@@ -5,17 +5,21 @@ import socket
 import subprocess
 import sys
 
+import pytest
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def test_tp2_matches_dense(tmp_path):
+@pytest.mark.parametrize("sp", ["0", "1"])
+def test_tp2_matches_dense(tmp_path, sp):
+    """sp=1: Megatron sequence parallelism (token-sharded residual stream and norms)."""
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
     procs = [subprocess.Popen([sys.executable, os.path.join(ROOT, "tests/helpers/tp_worker.py")],
                               env=dict(os.environ, RANK=str(r), WORLD_SIZE="2", PORT=str(port),
-                                       OUT=str(tmp_path / "r"), PYTHONPATH=ROOT)) for r in range(2)]
+                                       OUT=str(tmp_path / "r"), PYTHONPATH=ROOT, SP=sp)) for r in range(2)]
     assert [p.wait(timeout=120) for p in procs] == [0, 0]
     for r in range(2):
         res = json.load(open(tmp_path / f"r.{r}"))
