@@ -91,6 +91,25 @@ def cmd_brain(a):
     bmain(["--port", str(a.port)])
 
 
+def cmd_logs(a):
+    """Tail the logs of a job's processes (``<run_dir>/logs/<job>-<role>-<i>.log``) and,
+    with --events, its merged event timeline."""
+    import glob
+    logs = sorted(glob.glob(os.path.join(a.run_dir, "logs", "*.log")))
+    if a.name:
+        logs = [p for p in logs if os.path.basename(p).startswith(a.name)]
+    for p in logs:
+        with open(p, errors="replace") as f:
+            lines = f.readlines()[-a.tail:]
+        print(f"==> {os.path.basename(p)} <==")
+        print("".join(lines), end="" if lines and lines[-1].endswith("\n") else "\n")
+    if a.events:
+        from easydl_amd.utils.events import read_events
+        for e in read_events(a.run_dir)[-a.tail:]:
+            print(json.dumps(e))
+    return 0 if logs or a.events else 1
+
+
 def cmd_schema(a):
     from easydl_amd.api.schema import SCHEMAS, document
     kinds = [a.kind] if a.kind else sorted(SCHEMAS)
@@ -133,6 +152,12 @@ def main(argv=None):
         if name == "kill":
             p.add_argument("--node", required=True)
         p.set_defaults(fn=fn)
+    lg = sub.add_parser("logs", help="tail process logs (and events) of a job's run directory")
+    lg.add_argument("--run-dir", required=True)
+    lg.add_argument("--name", default=None, help="process name prefix, e.g. myjob-worker-1")
+    lg.add_argument("--tail", type=int, default=50)
+    lg.add_argument("--events", action="store_true")
+    lg.set_defaults(fn=cmd_logs)
     sc = sub.add_parser("schema", help="print the JSON Schema of control-plane messages")
     sc.add_argument("kind", nargs="?", default=None)
     sc.set_defaults(fn=cmd_schema)

@@ -74,3 +74,13 @@ def test_cli_schema_and_validate(tmp_path):
     assert json.loads(r.stdout)["title"] == "ResourcePlan"
     assert set(SCHEMAS) >= {"ElasticJob", "JobResource", "ResourcePlan", "PlanRequest", "PlanResponse"}
     assert document("ElasticJob")["$id"].endswith("/ElasticJob")
+
+
+def test_cli_logs(tmp_path):
+    (tmp_path / "logs").mkdir()
+    (tmp_path / "logs" / "j-worker-0.log").write_text("a\nb\nc\n")
+    (tmp_path / "events-worker0.jsonl").write_text('{"ts": 1.0, "mono": 1.0, "proc": "w", "kind": "joined"}\n')
+    r = subprocess.run([sys.executable, "-m", "easydl_amd.cli", "logs", "--run-dir", str(tmp_path), "--tail", "2",
+                        "--events"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    assert "==> j-worker-0.log <==" in r.stdout and "b\nc" in r.stdout and '"joined"' in r.stdout
