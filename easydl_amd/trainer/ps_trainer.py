@@ -87,6 +87,7 @@ class PSWorker:
         self.client.bind(self.model)
         self.fault = fault.FaultInjector.from_env(self.ctx, self.events)
         self.steps = 0
+        self._phase = [0.0, 0.0, 0.0]
 
     def fit(self, loss_fn, data, batch_size: int, shard_size: int, epochs: int = 1, on_step=None):
         self.rdzv.join()
@@ -100,12 +101,24 @@ class PSWorker:
                 lo, hi = disp.shard_range(shard)
                 for b0 in range(lo, hi, batch_size):
                     self.fault.maybe_inject("step_start", self.steps, trainer=None)
+                    t0 = time.perf_counter()
                     self.client.pull(self.model)
+                    t1 = time.perf_counter()
                     self.model.zero_grad(set_to_none=False)
                     loss = loss_fn(self.model, data.batch(range(b0, min(hi, b0 + batch_size)), self.device))
                     loss.backward()
+                    if self.device.type == "cuda":
+                        torch.cuda.current_stream(self.device).synchronize()
+                    t2 = time.perf_counter()
                     self.client.push(self.model, self.steps)
+                    t3 = time.perf_counter()
                     self.steps += 1
+                    self._phase = [a + b for a, b in zip(self._phase, (t1 - t0, t2 - t1, t3 - t2))]
+                    if self.steps % 16 == 0:  # where a PS step's time goes (pull / compute / push)
+                        self.events.emit("ps_step_phases", steps=16, pull_s=round(self._phase[0] / 16, 4),
+                                         compute_s=round(self._phase[1] / 16, 4),
+                                         push_s=round(self._phase[2] / 16, 4), transport=self.client.transport)
+                        self._phase = [0.0, 0.0, 0.0]
                     if on_step is not None:
                         on_step(self, loss)
                 disp.complete(shard)

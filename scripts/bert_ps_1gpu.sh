@@ -21,7 +21,7 @@ print(yaml.safe_dump_all([job.to_dict(), jr.to_dict()]))
 PY
 timeout -k 10 500 python -m easydl_amd.cli submit /tmp/bert_ps_1gpu.yaml --gpus 0,0,0,0,0,0,0,0 --run-dir $OUT --timeout 450 > $OUT.log 2>&1
 rc=$?
-grep -h '"worker_done"\|"startup_plan"\|"eval"' $OUT/events-*.jsonl | tail -12
+grep -h '"worker_done"\|"startup_plan"\|"ps_step_phases"' $OUT/events-*.jsonl | tail -14
 python -c "
 import json, sys
 from easydl_amd.brain.collectors import rocprof_rank_profiles
