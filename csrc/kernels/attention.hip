@@ -360,18 +360,41 @@ __global__ __launch_bounds__(256) void attn_bwd_delta_kernel(const bf16_t* __res
 // tiles (two 32-row sub-slices) of every query head of the GQA group.
 // LDS per stage: Q tile, dO tile, -lse*log2(e) and delta for the 64 rows.
 // ---------------------------------------------------------------------------
-// Issue order S, dP (16 back-to-back MFMAs), then exp(S) under the dP MFMAs,
-// dV += dO^T P under which dS = P (dP - delta) runs, then dK += Q^T dS.
+// Issue order: all 16 LDS operand reads, S and dP (16 back-to-back MFMAs), the
+// 16 transposed reads for dV / dK under them, exp(S), dV += dO^T P under which
+// dS = P (dP - delta) runs, then dK += Q^T dS.
 template <bool MASK, bool CAUSAL>
 __device__ __forceinline__ void dkdv_slice(const char* Qs, const char* Ds, const float* NL, const float* DL, int rb,
                                            const bf16x8 (&kf)[8], const bf16x8 (&vf)[8], f32x16 (&dka)[4],
                                            f32x16 (&dva)[4], int qs0, int mykey, int S, float sl2, int lane) {
   const int h = lane >> 5, l31 = lane & 31;
+  // This kernel runs one wave per SIMD (the K/V fragments and dK/dV accumulators
+  // are register-resident), so no other wave hides LDS latency: issue every LDS
+  // operand read of the S / dP GEMMs before their MFMAs (64 VGPRs in flight)
+  // instead of one read just ahead of each MFMA, and the transposed dO / Q reads
+  // of the dV / dK GEMMs while the S / dP MFMAs and the softmax run.
+  bf16x8 qa[8], da[8];
+#pragma unroll
+  for (int s = 0; s < 8; ++s) qa[s] = row_read(Qs, rb + l31, s, h);
+#pragma unroll
+  for (int s = 0; s < 8; ++s) da[s] = row_read(Ds, rb + l31, s, h);
+  __builtin_amdgcn_sched_barrier(0);
   f32x16 sa = f32x16{}, dp = f32x16{};
 #pragma unroll
-  for (int s = 0; s < 8; ++s) sa = mfma(row_read(Qs, rb + l31, s, h), kf[s], sa);
+  for (int s = 0; s < 8; ++s) sa = mfma(qa[s], kf[s], sa);
 #pragma unroll
-  for (int s = 0; s < 8; ++s) dp = mfma(row_read(Ds, rb + l31, s, h), vf[s], dp);
+  for (int s = 0; s < 8; ++s) dp = mfma(da[s], vf[s], dp);
+  bf16x8 tv[2][4], tq[2][4];
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) {
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) tv[s2][dt] = tr_read(Ds, rb + 16 * s2 + 4 * h, dt, lane);
+  }
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) {
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) tq[s2][dt] = tr_read(Qs, rb + 16 * s2 + 4 * h, dt, lane);
+  }
   // accumulator register i <-> query row rb + acc_row(i, h): rows 8g+4h .. +3 are contiguous
   f32x4 nl[4], dl[4];
 #pragma unroll
@@ -379,6 +402,7 @@ __device__ __forceinline__ void dkdv_slice(const char* Qs, const char* Ds, const
     nl[g] = *reinterpret_cast<const f32x4*>(NL + rb + 8 * g + 4 * h);
     dl[g] = *reinterpret_cast<const f32x4*>(DL + rb + 8 * g + 4 * h);
   }
+  __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     float p = fast_exp2(__builtin_fmaf(sa[i], sl2, nl[i >> 2][i & 3]));
@@ -392,7 +416,7 @@ __device__ __forceinline__ void dkdv_slice(const char* Qs, const char* Ds, const
   for (int s2 = 0; s2 < 2; ++s2) {
     const bf16x8 pb = acc_to_b(sa, s2);
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt) dva[dt] = mfma(tr_read(Ds, rb + 16 * s2 + 4 * h, dt, lane), pb, dva[dt]);
+    for (int dt = 0; dt < 4; ++dt) dva[dt] = mfma(tv[s2][dt], pb, dva[dt]);
   }
 #pragma unroll
   for (int i = 0; i < 16; ++i) dp[i] = sa[i] * (dp[i] - dl[i >> 2][i & 3]);
@@ -400,7 +424,7 @@ __device__ __forceinline__ void dkdv_slice(const char* Qs, const char* Ds, const
   for (int s2 = 0; s2 < 2; ++s2) {
     const bf16x8 db = acc_to_b(dp, s2);
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt) dka[dt] = mfma(tr_read(Qs, rb + 16 * s2 + 4 * h, dt, lane), db, dka[dt]);
+    for (int dt = 0; dt < 4; ++dt) dka[dt] = mfma(tq[s2][dt], db, dka[dt]);
   }
 }
 
