@@ -38,6 +38,8 @@ typedef short i16x4 __attribute__((ext_vector_type(4)));
 typedef short i16x8 __attribute__((ext_vector_type(8)));
 typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
 typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(3))) char lds_char;
+typedef __attribute__((address_space(3))) const bf16x8 lds_bf16x8;
 
 constexpr int HD = 128;        // head dim
 constexpr float LOG2E = 1.4426950408889634f;
@@ -360,41 +362,18 @@ __global__ __launch_bounds__(256) void attn_bwd_delta_kernel(const bf16_t* __res
 // tiles (two 32-row sub-slices) of every query head of the GQA group.
 // LDS per stage: Q tile, dO tile, -lse*log2(e) and delta for the 64 rows.
 // ---------------------------------------------------------------------------
-// Issue order: all 16 LDS operand reads, S and dP (16 back-to-back MFMAs), the
-// 16 transposed reads for dV / dK under them, exp(S), dV += dO^T P under which
-// dS = P (dP - delta) runs, then dK += Q^T dS.
+// Issue order S, dP (16 back-to-back MFMAs), then exp(S) under the dP MFMAs,
+// dV += dO^T P under which dS = P (dP - delta) runs, then dK += Q^T dS.
 template <bool MASK, bool CAUSAL>
 __device__ __forceinline__ void dkdv_slice(const char* Qs, const char* Ds, const float* NL, const float* DL, int rb,
                                            const bf16x8 (&kf)[8], const bf16x8 (&vf)[8], f32x16 (&dka)[4],
                                            f32x16 (&dva)[4], int qs0, int mykey, int S, float sl2, int lane) {
   const int h = lane >> 5, l31 = lane & 31;
-  // This kernel runs one wave per SIMD (the K/V fragments and dK/dV accumulators
-  // are register-resident), so no other wave hides LDS latency: issue every LDS
-  // operand read of the S / dP GEMMs before their MFMAs (64 VGPRs in flight)
-  // instead of one read just ahead of each MFMA, and the transposed dO / Q reads
-  // of the dV / dK GEMMs while the S / dP MFMAs and the softmax run.
-  bf16x8 qa[8], da[8];
-#pragma unroll
-  for (int s = 0; s < 8; ++s) qa[s] = row_read(Qs, rb + l31, s, h);
-#pragma unroll
-  for (int s = 0; s < 8; ++s) da[s] = row_read(Ds, rb + l31, s, h);
-  __builtin_amdgcn_sched_barrier(0);
   f32x16 sa = f32x16{}, dp = f32x16{};
 #pragma unroll
-  for (int s = 0; s < 8; ++s) sa = mfma(qa[s], kf[s], sa);
+  for (int s = 0; s < 8; ++s) sa = mfma(row_read(Qs, rb + l31, s, h), kf[s], sa);
 #pragma unroll
-  for (int s = 0; s < 8; ++s) dp = mfma(da[s], vf[s], dp);
-  bf16x8 tv[2][4], tq[2][4];
-#pragma unroll
-  for (int s2 = 0; s2 < 2; ++s2) {
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) tv[s2][dt] = tr_read(Ds, rb + 16 * s2 + 4 * h, dt, lane);
-  }
-#pragma unroll
-  for (int s2 = 0; s2 < 2; ++s2) {
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) tq[s2][dt] = tr_read(Qs, rb + 16 * s2 + 4 * h, dt, lane);
-  }
+  for (int s = 0; s < 8; ++s) dp = mfma(row_read(Ds, rb + l31, s, h), vf[s], dp);
   // accumulator register i <-> query row rb + acc_row(i, h): rows 8g+4h .. +3 are contiguous
   f32x4 nl[4], dl[4];
 #pragma unroll
@@ -402,7 +381,6 @@ __device__ __forceinline__ void dkdv_slice(const char* Qs, const char* Ds, const
     nl[g] = *reinterpret_cast<const f32x4*>(NL + rb + 8 * g + 4 * h);
     dl[g] = *reinterpret_cast<const f32x4*>(DL + rb + 8 * g + 4 * h);
   }
-  __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     float p = fast_exp2(__builtin_fmaf(sa[i], sl2, nl[i >> 2][i & 3]));
@@ -416,7 +394,7 @@ __device__ __forceinline__ void dkdv_slice(const char* Qs, const char* Ds, const
   for (int s2 = 0; s2 < 2; ++s2) {
     const bf16x8 pb = acc_to_b(sa, s2);
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt) dva[dt] = mfma(tv[s2][dt], pb, dva[dt]);
+    for (int dt = 0; dt < 4; ++dt) dva[dt] = mfma(tr_read(Ds, rb + 16 * s2 + 4 * h, dt, lane), pb, dva[dt]);
   }
 #pragma unroll
   for (int i = 0; i < 16; ++i) dp[i] = sa[i] * (dp[i] - dl[i >> 2][i & 3]);
@@ -424,7 +402,7 @@ __device__ __forceinline__ void dkdv_slice(const char* Qs, const char* Ds, const
   for (int s2 = 0; s2 < 2; ++s2) {
     const bf16x8 db = acc_to_b(dp, s2);
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt) dka[dt] = mfma(tq[s2][dt], db, dka[dt]);
+    for (int dt = 0; dt < 4; ++dt) dka[dt] = mfma(tr_read(Qs, rb + 16 * s2 + 4 * h, dt, lane), db, dka[dt]);
   }
 }
 
@@ -506,6 +484,258 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dkdv_kernel(
     store_accT(dk + (int64_t)b * S * ks + (int64_t)mykey * ks + hk * HD, dka, scale, h);
     store_accT(dv + (int64_t)b * S * ks + (int64_t)mykey * ks + hk * HD, dva, 1.f, h);
   }
+}
+
+// ---------------------------------------------------------------------------
+// backward: dK, dV with 64 keys per wave.  The 32-key kernel above is LDS-
+// bandwidth-bound: every 32x32x16 MFMA consumes one 1-KiB LDS fragment, which
+// is exactly the CU's LDS rate at full MFMA rate (prefetching the fragments
+// earlier measured 4.5 % SLOWER, profiles/r01_attn_dkdv_ab.txt).  Here a wave
+// owns two 32-key blocks, so every Q / dO fragment read from LDS feeds two
+// MFMAs.  Registers: K fragments 64 VGPRs, dK/dV accumulators 256 (AGPRs),
+// S/dP 64; V is read from LDS -> one wave per SIMD, as before.  A
+// workgroup (4 waves) owns 256 keys of one KV head.  Measured at the 8k causal
+// Llama shape: 1.35 ms (incl. the partial-sum reduce) vs 2.25 ms for the
+// 32-key kernel (profiles/r01_attn_dkdv_ab.txt); EDL_ATTN_DKDV=32 selects it.
+// ---------------------------------------------------------------------------
+template <bool MASK, bool CAUSAL>
+__device__ __forceinline__ void dkdv64_slice(const char* Qs, const char* Ds, const float* NL,
+                                             const float* DL, int rb, const bf16x8 (&kf)[2][8],
+                                             const char* Vw, f32x16 (&dka)[2][4], f32x16 (&dva)[2][4],
+                                             int qs0, int key0, int S,
+                                             float sl2, int lane) {
+  const int h = lane >> 5, l31 = lane & 31;
+  f32x16 sa[2], dp[2];
+  sa[0] = sa[1] = dp[0] = dp[1] = f32x16{};
+  // V is read from LDS in every slice: the opaque offset stops the compiler from hoisting
+  // the loop-invariant reads into (64 more) registers
+  uint32_t vo = (uint32_t)(uintptr_t)(lds_char*)Vw;
+  asm volatile("" : "+v"(vo));
+  const lds_char* Vl = (const lds_char*)(uintptr_t)vo;
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    const bf16x8 a = row_read(Qs, rb + l31, s, h);
+    sa[0] = mfma(a, kf[0][s], sa[0]);
+    sa[1] = mfma(a, kf[1][s], sa[1]);
+  }
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    const bf16x8 a = row_read(Ds, rb + l31, s, h);
+    const bf16x8 v0 = *(lds_bf16x8*)(Vl + swz(l31, 2 * s + h));
+    const bf16x8 v1 = *(lds_bf16x8*)(Vl + swz(32 + l31, 2 * s + h));
+    dp[0] = mfma(a, v0, dp[0]);
+    dp[1] = mfma(a, v1, dp[1]);
+  }
+  // per-row softmax terms are read from LDS right where they are used (no 32-VGPR arrays)
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const f32x4 nl = *reinterpret_cast<const f32x4*>(NL + rb + 8 * g + 4 * h);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) sa[t][4 * g + e] = fast_exp2(__builtin_fmaf(sa[t][4 * g + e], sl2, nl[e]));
+    }
+  }
+  if (MASK) {  // diagonal / tail slices only
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int mykey = key0 + 32 * t + l31;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int qi = qs0 + acc_row(i, h);
+        if (qi >= S || mykey >= S || (CAUSAL && mykey > qi)) sa[t][i] = 0.f;
+      }
+    }
+  }
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) {
+    const bf16x8 p0 = acc_to_b(sa[0], s2), p1 = acc_to_b(sa[1], s2);
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const bf16x8 a = tr_read(Ds, rb + 16 * s2 + 4 * h, dt, lane);
+      dva[0][dt] = mfma(a, p0, dva[0][dt]);
+      dva[1][dt] = mfma(a, p1, dva[1][dt]);
+    }
+  }
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const f32x4 dl = *reinterpret_cast<const f32x4*>(DL + rb + 8 * g + 4 * h);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) dp[t][4 * g + e] = sa[t][4 * g + e] * (dp[t][4 * g + e] - dl[e]);
+    }
+  }
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) {
+    const bf16x8 d0 = acc_to_b(dp[0], s2), d1 = acc_to_b(dp[1], s2);
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const bf16x8 a = tr_read(Qs, rb + 16 * s2 + 4 * h, dt, lane);
+      dka[0][dt] = mfma(a, d0, dka[0][dt]);
+      dka[1][dt] = mfma(a, d1, dka[1][dt]);
+    }
+  }
+}
+
+// fp32 variant of store_accT for the head-split partial sums
+__device__ __forceinline__ void store_accT_f32(float* rowp, const f32x16 (&acc)[4], float mul, int h) {
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      f32x4 w;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) w[e] = acc[dt][4 * g + e] * mul;
+      *reinterpret_cast<f32x4*>(rowp + dt * 32 + 8 * g + 4 * h) = w;
+    }
+  }
+}
+
+// Work balance.  A causal key block kb sees (nkb - kb) query tiles, so with one
+// 256-key block per workgroup the first workgroup does twice the average work
+// and sets the kernel time (measured: 2.97 ms vs 1.5 ms of balanced work at the
+// 8k Llama shape).  Causal workgroups therefore process the pair of blocks
+// {p, nkb-1-p} back to back (equal work per workgroup), and when that leaves
+// fewer than ~2 workgroups per CU the GQA group's query heads are split over
+// `gsplit` workgroups that write fp32 partials to `ws`, summed by
+// attn_dkdv_reduce_kernel.
+template <bool CAUSAL>
+__global__ __launch_bounds__(256, 1) void attn_bwd_dkdv64_kernel(
+    const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
+    const bf16_t* __restrict__ dout, const float* __restrict__ lse, const float* __restrict__ delta,
+    bf16_t* __restrict__ dk, bf16_t* __restrict__ dv, float* __restrict__ ws, int S, int H, int KV, int gsplit,
+    float scale_log2, float scale) {
+  constexpr int QT = 64;   // queries per staged tile
+  constexpr int KW = 64;   // keys per wave
+  constexpr int KB = 4 * KW;
+  // [Q|dO] x 2 stages (64 KiB), softmax row terms (1 KiB), this block's V rows per wave (4 x 16 KiB)
+  __shared__ __attribute__((aligned(16))) char smem[2 * 32768 + 2 * 512 + 4 * 16384];
+  const int hk = blockIdx.y / gsplit, gs = blockIdx.y % gsplit, b = blockIdx.z;
+  const int lane = threadIdx.x & 63, h = lane >> 5, l31 = lane & 31;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // provably wave-uniform
+  const int heads = (H / KV) / gsplit, hq0 = hk * (H / KV) + gs * heads;
+  const int64_t qs = (int64_t)H * HD, ks = (int64_t)KV * HD;
+  const int nkb = (S + KB - 1) / KB, nqt = (S + QT - 1) / QT;
+  const int64_t nBHS = (int64_t)gridDim.z * H * S;  // delta = [delta | -lse*log2e]
+  const DmaPlan<QT, 4> plan(qs, w, lane);
+  const int blocks[2] = {(int)blockIdx.x, nkb - 1 - (int)blockIdx.x};
+  const int nblocks = CAUSAL && blocks[1] != blocks[0] ? 2 : 1;
+#pragma unroll 1
+  for (int bi = 0; bi < nblocks; ++bi) {
+    const int kb = blocks[bi];
+    const int key0 = kb * KB + KW * w;   // first key of this wave
+    // K stays in registers (B operand of S = Q K^T); V, the B operand of dP = dO V^T, goes to this
+    // wave's LDS rows in the row_read layout: 64 fewer VGPRs for 16 more fragment reads per slice.
+    char* Vw = smem + 2 * 32768 + 2 * 512 + w * 16384;
+    bf16x8 kf[2][8];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int64_t off = (int64_t)b * S * ks + (int64_t)min(key0 + 32 * t + l31, S - 1) * ks + hk * HD;
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        kf[t][s] = load_frag(k + off, s, h);
+        *reinterpret_cast<bf16x8*>(Vw + swz(32 * t + l31, 2 * s + h)) = load_frag(v + off, s, h);
+      }
+    }
+    f32x16 dka[2][4], dva[2][4];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        dka[t][dt] = f32x16{};
+        dva[t][dt] = f32x16{};
+      }
+    }
+    const int qt0 = CAUSAL ? (kb * KB) / QT : 0;
+    const int per_head = nqt - qt0;
+    const int total = per_head * heads;
+    auto fetch = [&](int j, int st) {
+      const int hq = hq0 + j / per_head;
+      const int q0 = (qt0 + j % per_head) * QT;
+      char* base = smem + st * 32768;
+      const int64_t off = (int64_t)b * S * qs + hq * HD, nbytes = ((int64_t)S * qs - hq * HD) * 2;
+      const uint32_t soff = (uint32_t)(q0 * qs * 2);
+      plan.issue(base, make_rsrc(q + off, nbytes), soff, w);
+      plan.issue(base + 16384, make_rsrc(dout + off, nbytes), soff, w);
+      float* lf = reinterpret_cast<float*>(smem + 2 * 32768 + st * 512);
+      const int64_t row0 = ((int64_t)b * H + hq) * S;
+      if (w == 0) dma_f32x64(lf, make_rsrc(delta + nBHS + row0, (int64_t)S * 4), q0, lane);
+      if (w == 1) dma_f32x64(lf + QT, make_rsrc(delta + row0, (int64_t)S * 4), q0, lane);
+    };
+    if (total > 0) fetch(0, 0);
+    wait_vm();
+    __syncthreads();
+    // Separate loops for the diagonal / tail tiles (masked body) and the rest (mask-free body):
+    // one straight-line body per loop allocates registers far better than a branch per slice.
+    auto run = [&](auto masked, int j0, int j1) {
+      constexpr bool MASK = decltype(masked)::value;
+#pragma unroll 1
+      for (int j = j0; j < j1; ++j) {
+        if (j + 1 < total) fetch(j + 1, (j + 1) & 1);
+        const int st = j & 1;
+        const char* Qs = smem + st * 32768;
+        const char* Ds = Qs + 16384;
+        const float* NL = reinterpret_cast<const float*>(smem + 2 * 32768 + st * 512);
+        const int q0 = (qt0 + j % per_head) * QT;
+#pragma unroll 1
+        for (int sub = 0; sub < QT / 32; ++sub) {
+          const int qs0 = q0 + 32 * sub;
+          if (CAUSAL && qs0 + 31 < key0) continue;  // wave-uniform: every key of the wave is after every query
+          dkdv64_slice<MASK, CAUSAL>(Qs, Ds, NL, NL + QT, 32 * sub, kf, Vw, dka, dva, qs0, key0, S, scale_log2, lane);
+        }
+        wait_vm();
+        __syncthreads();   // also fences the LDS buffers before the next block's first fetch
+      }
+    };
+    // tiles [lo, hi) of every head need no mask for any wave of this workgroup
+    int lo = CAUSAL ? min(KB / QT, per_head) : 0;
+    int hi = max(lo, min(per_head, S / QT - qt0));
+    if (kb * KB + KB > S) lo = hi = per_head;   // the block's keys run past S
+#pragma unroll 1
+    for (int hh = 0; hh < heads; ++hh) {
+      const int base = hh * per_head;
+      run(std::integral_constant<bool, true>{}, base, base + lo);
+      run(std::integral_constant<bool, false>{}, base + lo, base + hi);
+      run(std::integral_constant<bool, true>{}, base + hi, base + per_head);
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int mykey = key0 + 32 * t + l31;
+      if (mykey >= S) continue;
+      if (gsplit == 1) {
+        store_accT(dk + (int64_t)b * S * ks + (int64_t)mykey * ks + hk * HD, dka[t], scale, h);
+        store_accT(dv + (int64_t)b * S * ks + (int64_t)mykey * ks + hk * HD, dva[t], 1.f, h);
+      } else {  // ws[gs][b][key][hk][dk|dv][HD]
+        float* row = ws + ((((int64_t)gs * gridDim.z + b) * S + mykey) * KV + hk) * 2 * HD;
+        store_accT_f32(row, dka[t], scale, h);
+        store_accT_f32(row + HD, dva[t], 1.f, h);
+      }
+    }
+  }
+}
+
+// sum the head-split partials: ws[g][b][key][kv][2][HD] fp32 -> dk, dv bf16 (8 elements per thread)
+__global__ __launch_bounds__(256) void attn_dkdv_reduce_kernel(const float* __restrict__ ws, bf16_t* __restrict__ dk,
+                                                               bf16_t* __restrict__ dv, int64_t nrows, int gsplit) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;   // one 8-element chunk of a [2*HD] row
+  constexpr int CH = 2 * HD / 8;
+  if (i >= nrows * CH) return;
+  const int64_t row = i / CH;
+  const int c = (int)(i % CH);
+  f32x4 a = {}, bq = {};
+  for (int g = 0; g < gsplit; ++g) {
+    const float* src = ws + ((int64_t)g * nrows + row) * 2 * HD + 8 * c;
+    a += *reinterpret_cast<const f32x4*>(src);
+    bq += *reinterpret_cast<const f32x4*>(src + 4);
+  }
+  u32x4 o;
+  o[0] = pack2(a[0], a[1]);
+  o[1] = pack2(a[2], a[3]);
+  o[2] = pack2(bq[0], bq[1]);
+  o[3] = pack2(bq[2], bq[3]);
+  bf16_t* dst = (8 * c < HD ? dk : dv) + row * HD + (8 * c) % HD;
+  *reinterpret_cast<u32x4*>(dst) = o;
 }
 
 // ---------------------------------------------------------------------------
@@ -633,10 +863,36 @@ int edl_attn_fwd(const void* q, const void* k, const void* v, void* o, float* ls
 }
 
 // delta: fp32 [2,B,H,S] scratch filled here (delta, -lse*log2(e)).
+// dK/dV-64 work decomposition (see attn_bwd_dkdv64_kernel): returns gsplit, fills the grid
+static int dkdv64_plan(int B, int S, int H, int KV, int causal, dim3* grid) {
+  constexpr int kCUs = 256;   // MI355X: 8 XCDs x 32 CUs
+  const int nkb = (S + 255) / 256, nx = causal ? (nkb + 1) / 2 : nkb, group = H / KV;
+  int gsplit = 1;
+  while ((int64_t)nx * KV * B * gsplit < kCUs && group % (2 * gsplit) == 0) gsplit *= 2;
+  if (grid) *grid = dim3(nx, KV * gsplit, B);
+  return gsplit;
+}
+
+static int dkdv_keys_per_wave() {
+  static const int kpw = [] {
+    const char* e = getenv("EDL_ATTN_DKDV");
+    return e && atoi(e) == 32 ? 32 : 64;
+  }();
+  return kpw;
+}
+
+// fp32 workspace the backward needs for the head-split dK/dV partials (0 = none)
+int64_t edl_attn_bwd_ws_bytes(int B, int S, int H, int KV, int causal) {
+  if (dkdv_keys_per_wave() != 64 || KV <= 0 || H % KV != 0) return 0;
+  const int g = dkdv64_plan(B, S, H, KV, causal, nullptr);
+  return g == 1 ? 0 : (int64_t)g * B * S * KV * 2 * HD * 4;
+}
+
 int edl_attn_bwd(const void* q, const void* k, const void* v, const void* o, const void* dout, const float* lse,
-                 float* delta, void* dq, void* dk, void* dv, int B, int S, int H, int KV, int D, int causal,
-                 float scale, hipStream_t s) {
+                 float* delta, void* dq, void* dk, void* dv, float* ws, int B, int S, int H, int KV, int D,
+                 int causal, float scale, hipStream_t s) {
   if (D != HD || H % KV != 0 || S <= 0) return (int)hipErrorInvalidValue;
+  if (edl_attn_bwd_ws_bytes(B, S, H, KV, causal) > 0 && ws == nullptr) return (int)hipErrorInvalidValue;
   const int64_t nrows = (int64_t)B * S * H;
   attn_bwd_delta_kernel<<<(unsigned)((nrows * 16 + 255) / 256), 256, 0, s>>>((const bf16_t*)o, (const bf16_t*)dout,
                                                                             lse, delta, S, H, nrows);
@@ -647,23 +903,49 @@ int edl_attn_bwd(const void* q, const void* k, const void* v, const void* o, con
     const char* e = getenv("EDL_ATTN_DKDV_OCC");
     return e && atoi(e) == 2 ? 2 : 1;
   }();
+  const int keys_per_wave = dkdv_keys_per_wave();
+  dim3 gkv64;
+  const int gsplit = dkdv64_plan(B, S, H, KV, causal, &gkv64);
 #define EDL_DKDV(C, O)                                                                                              \
   attn_bwd_dkdv_kernel<C, O><<<gkv, 256, 0, s>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,               \
                                                  (const bf16_t*)dout, lse, delta, (bf16_t*)dk, (bf16_t*)dv, S, H, KV, \
                                                  sl2, scale)
+#define EDL_DKDV64(C)                                                                                                \
+  attn_bwd_dkdv64_kernel<C><<<gkv64, 256, 0, s>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,              \
+                                                  (const bf16_t*)dout, lse, delta, (bf16_t*)dk, (bf16_t*)dv, ws, S, H, \
+                                                  KV, gsplit, sl2, scale);                                             \
+  if (gsplit > 1) {                                                                                            \
+    EDL_LAUNCH_CHECK();                                                                                        \
+    const int64_t rows = (int64_t)B * S * KV;                                                                  \
+    attn_dkdv_reduce_kernel<<<(unsigned)((rows * (2 * HD / 8) + 255) / 256), 256, 0, s>>>(ws, (bf16_t*)dk,     \
+                                                                                         (bf16_t*)dv, rows, gsplit); \
+  }
   if (causal) {
-    if (occ == 2) EDL_DKDV(true, 2); else EDL_DKDV(true, 1);
+    if (keys_per_wave == 64) {
+      EDL_DKDV64(true);
+    } else if (occ == 2) {
+      EDL_DKDV(true, 2);
+    } else {
+      EDL_DKDV(true, 1);
+    }
     EDL_LAUNCH_CHECK();
     attn_bwd_dq_kernel<true><<<gq, 256, 0, s>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
                                                 (const bf16_t*)dout, lse, delta, (bf16_t*)dq, S, H, KV, sl2, scale);
   } else {
-    if (occ == 2) EDL_DKDV(false, 2); else EDL_DKDV(false, 1);
+    if (keys_per_wave == 64) {
+      EDL_DKDV64(false);
+    } else if (occ == 2) {
+      EDL_DKDV(false, 2);
+    } else {
+      EDL_DKDV(false, 1);
+    }
     EDL_LAUNCH_CHECK();
     attn_bwd_dq_kernel<false><<<gq, 256, 0, s>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
                                                  (const bf16_t*)dout, lse, delta, (bf16_t*)dq, S, H, KV, sl2, scale);
   }
   EDL_LAUNCH_CHECK();
 #undef EDL_DKDV
+#undef EDL_DKDV64
   return 0;
 }
 

@@ -18,7 +18,7 @@ import threading
 
 import torch
 
-_LIBDIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
+_LIBDIR = os.environ.get("EDL_LIBDIR") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 _lock = threading.Lock()
 _kern = None
 _rt = None
@@ -60,7 +60,8 @@ _KERNEL_SIGS = {
     "edl_attn_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
                      c_float, c_void_p],
     "edl_attn_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                     c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_void_p],
+                     c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_void_p],
+    "edl_attn_bwd_ws_bytes": (c_i64, [c_int, c_int, c_int, c_int, c_int]),
     "edl_xgmi_allreduce": [ctypes.POINTER(c_void_p), ctypes.POINTER(c_void_p), c_int, c_int, c_void_p, c_void_p,
                            c_i64, c_int, c_int, ctypes.c_uint32, c_int, c_void_p, ctypes.c_double, c_void_p,
                            c_void_p],

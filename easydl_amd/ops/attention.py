@@ -48,9 +48,14 @@ class _FlashAttnFn(torch.autograd.Function):
         dom = _bshd(do)
         dq, dk, dv = torch.empty_like(qm), torch.empty_like(km), torch.empty_like(vm)
         delta = torch.empty(2, B, H, S, dtype=torch.float32, device=qm.device)  # (delta, -lse*log2e)
+        causal = 1 if ctx.causal else 0
+        # fp32 partials when the GQA group is split over workgroups (csrc/kernels/attention.hip dkdv64_plan)
+        nws = kn.raw("edl_attn_bwd_ws_bytes")(B, S, H, KV, causal)
+        ws = torch.empty(nws // 4, dtype=torch.float32, device=qm.device) if nws else None
         kn.check("edl_attn_bwd", qm.data_ptr(), km.data_ptr(), vm.data_ptr(), o.data_ptr(), dom.data_ptr(),
-                 lse.data_ptr(), delta.data_ptr(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), B, S, H, KV, D,
-                 1 if ctx.causal else 0, ctx.scale, _native.stream_of(qm))
+                 lse.data_ptr(), delta.data_ptr(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(),
+                 ws.data_ptr() if ws is not None else None, B, S, H, KV, D, causal, ctx.scale,
+                 _native.stream_of(qm))
         return dq.transpose(1, 2), dk.transpose(1, 2), dv.transpose(1, 2), None, None
 
 
