@@ -227,12 +227,21 @@ __device__ __forceinline__ void fwd_tile(const char* Ks, const char* Vs, const b
     for (int i = 0; i < 16; ++i) mx = fmaxf(mx, sacc[t][i]);
   }
   mx = xhalf_max(mx);
-  // running max in the scaled log2 domain (sl2 > 0 commutes with max)
-  const float mnew = fmaxf(m, mx * sl2);
-  const bool grow = mnew > m;
-  const float alpha = fast_exp2(m - mnew);
-  m = mnew;
-  const float negm = -mnew;
+  // Running max in the scaled log2 domain (sl2 > 0 commutes with max).  Thresholded
+  // lazy rescale: the reference max m only moves when some row of the wave grew by
+  // more than 2^8; otherwise p = exp2(s - m) <= 256 is used as is (fp32 sums, bf16 P
+  // keeps its 8 exponent bits), and O, l stay consistent with the stale m.  This
+  // skips the 64-register O rescale on almost every tile after the first few.
+  const float mxs = mx * sl2;
+  if (__any(mxs > m + 8.f)) {
+    const float mnew = fmaxf(m, mxs);
+    const float alpha = fast_exp2(m - mnew);
+    m = mnew;
+    lsum *= alpha;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) oacc[dt] *= alpha;
+  }
+  const float negm = -m;
   float ps = 0.f;
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
@@ -243,12 +252,7 @@ __device__ __forceinline__ void fwd_tile(const char* Ks, const char* Vs, const b
       ps += p;
     }
   }
-  lsum = lsum * alpha + ps;
-  // exact lazy rescale: only when some row max of this wave grew
-  if (__any(grow)) {
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) oacc[dt] *= alpha;
-  }
+  lsum += ps;
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
 #pragma unroll
@@ -269,7 +273,8 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_t* __restri
   __shared__ __attribute__((aligned(16))) char smem[2 * 32768];
   const int qb = gridDim.x - 1 - blockIdx.x;  // longest causal rows first
   const int hq = blockIdx.y, b = blockIdx.z, hk = hq / (H / KV);
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, l31 = lane & 31;
+  const int lane = threadIdx.x & 63, h = lane >> 5, l31 = lane & 31;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // provably wave-uniform
   const int q0 = qb * BQ;
   const int wq0 = q0 + 32 * w;  // first query of this wave
   const int64_t qs = (int64_t)H * HD, ks = (int64_t)KV * HD;
@@ -302,22 +307,31 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_t* __restri
   // second loop (two straight-line bodies allocate registers better than one
   // body with a masked and an unmasked branch).
   const int nfull = CAUSAL ? min(q0, S) / 64 : S / 64;
+  // The loop body is unrolled over the two LDS stages so every LDS address is a
+  // loop-invariant register plus an immediate (no per-read address VALU).
   auto run = [&](auto masked, int it0, int it1) {
     constexpr bool MASK = decltype(masked)::value;
-#pragma unroll 1
-    for (int it = it0; it < it1; ++it) {
+    auto step = [&](int it, auto stage) {
+      constexpr int ST = decltype(stage)::value;   // == it & 1
       const int kv0 = it * 64;
-      if (it + 1 < ntiles) {  // buffer (it+1)&1 was released by the previous barrier
-        char* nxt = smem + ((it + 1) & 1) * 32768;
-        plan.issue(nxt, krs, (it + 1) * tile_bytes, w);
-        plan.issue(nxt + 16384, vrs, (it + 1) * tile_bytes, w);
+      if (it + 1 < ntiles) {  // stage 1-ST was released by the previous barrier
+        plan.issue(smem + (1 - ST) * 32768, krs, (it + 1) * tile_bytes, w);
+        plan.issue(smem + (1 - ST) * 32768 + 16384, vrs, (it + 1) * tile_bytes, w);
       }
-      const char* Ks = smem + (it & 1) * 32768;
+      const char* Ks = smem + ST * 32768;
       if (!MASK || !CAUSAL || kv0 <= wq0 + 31)  // wave-uniform: tile visible to this wave
         fwd_tile<MASK, CAUSAL>(Ks, Ks + 16384, qf, oacc, m, lsum, kv0, qr, S, scale_log2, lane);
       wait_vm();
       __syncthreads();
+    };
+    int it = it0;
+    if (it < it1 && (it & 1)) step(it++, std::integral_constant<int, 1>{});
+#pragma unroll 1
+    for (; it + 1 < it1; it += 2) {
+      step(it, std::integral_constant<int, 0>{});
+      step(it + 1, std::integral_constant<int, 1>{});
     }
+    if (it < it1) step(it, std::integral_constant<int, 0>{});
   };
   run(std::integral_constant<bool, false>{}, 0, nfull);
   run(std::integral_constant<bool, true>{}, nfull, ntiles);
@@ -418,7 +432,8 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dkdv_kernel(
   // 2 stages x (Q tile 16 KB + dO tile 16 KB) + 2 x (-lse2, delta) x 64 floats
   __shared__ __attribute__((aligned(16))) char smem[2 * 32768 + 2 * 512];
   const int kb = blockIdx.x, hk = blockIdx.y, b = blockIdx.z;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, l31 = lane & 31;
+  const int lane = threadIdx.x & 63, h = lane >> 5, l31 = lane & 31;
+  const int w = threadIdx.x >> 6;
   const int group = H / KV;
   const int64_t qs = (int64_t)H * HD, ks = (int64_t)KV * HD;
   const int mykey = kb * 128 + 32 * w + l31;
@@ -673,7 +688,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv64_kernel(
 #pragma unroll 1
       for (int j = j0; j < j1; ++j) {
         if (j + 1 < total) fetch(j + 1, (j + 1) & 1);
-        const int st = j & 1;
+        const int st = j & 1;   // (unrolling over the stages as in fwd/dQ measured 2 % slower here: more spills)
         const char* Qs = smem + st * 32768;
         const char* Ds = Qs + 16384;
         const float* NL = reinterpret_cast<const float*>(smem + 2 * 32768 + st * 512);
@@ -785,7 +800,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(
   __shared__ __attribute__((aligned(16))) char smem[2 * 32768];
   const int qb = gridDim.x - 1 - blockIdx.x;
   const int hq = blockIdx.y, b = blockIdx.z, hk = hq / (H / KV);
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, l31 = lane & 31;
+  const int lane = threadIdx.x & 63, h = lane >> 5, l31 = lane & 31;
+  const int w = threadIdx.x >> 6;
   const int q0 = qb * BQ;
   const int wq0 = q0 + 32 * w;
   const int64_t qs = (int64_t)H * HD, ks = (int64_t)KV * HD;
@@ -819,22 +835,29 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(
   wait_vm();
   __syncthreads();
   const int nfull = CAUSAL ? min(q0, S) / 64 : S / 64;  // see the forward
-  auto run = [&](auto masked, int it0, int it1) {
+  auto run = [&](auto masked, int it0, int it1) {  // unrolled over the two stages, as in the forward
     constexpr bool MASK = decltype(masked)::value;
-#pragma unroll 1
-    for (int it = it0; it < it1; ++it) {
+    auto step = [&](int it, auto stage) {
+      constexpr int ST = decltype(stage)::value;   // == it & 1
       const int kv0 = it * 64;
       if (it + 1 < ntiles) {
-        char* nxt = smem + ((it + 1) & 1) * 32768;
-        plan.issue(nxt, krs, (it + 1) * tile_bytes, w);
-        plan.issue(nxt + 16384, vrs, (it + 1) * tile_bytes, w);
+        plan.issue(smem + (1 - ST) * 32768, krs, (it + 1) * tile_bytes, w);
+        plan.issue(smem + (1 - ST) * 32768 + 16384, vrs, (it + 1) * tile_bytes, w);
       }
-      const char* Ks = smem + (it & 1) * 32768;
+      const char* Ks = smem + ST * 32768;
       if (!MASK || !CAUSAL || kv0 <= wq0 + 31)
         dq_tile<MASK, CAUSAL>(Ks, Ks + 16384, qf, df, dqa, nl2, dl, kv0, qr, S, scale_log2, lane);
       wait_vm();
       __syncthreads();
+    };
+    int it = it0;
+    if (it < it1 && (it & 1)) step(it++, std::integral_constant<int, 1>{});
+#pragma unroll 1
+    for (; it + 1 < it1; it += 2) {
+      step(it, std::integral_constant<int, 0>{});
+      step(it + 1, std::integral_constant<int, 1>{});
     }
+    if (it < it1) step(it, std::integral_constant<int, 0>{});
   };
   run(std::integral_constant<bool, false>{}, 0, nfull);
   run(std::integral_constant<bool, true>{}, nfull, ntiles);

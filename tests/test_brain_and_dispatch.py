@@ -105,7 +105,7 @@ def test_rocprof_profile_drives_per_rank_cu_plan(tmp_path):
                   '"Cijk_Ailk_Bljk_BBS_BH",10,100000000,10000000,10\n')
     prof = rocprof_kernel_profile(str(ps))
     assert prof["memory_frac"] == 0.9 and prof["compute_frac"] == 0.1
-    train = rocprof_kernel_profile(os.path.join(ROOT, "profiles", "r01_bench_kernel_stats_hipattn.csv"))
+    train = rocprof_kernel_profile(os.path.join(ROOT, "profiles", "r01_bench_kernel_stats_latest.csv"))
     assert train["compute_frac"] > 0.85
     metrics = {"ps0": {"rocprof": prof}, "w0": {"step_time": 1.0, "rocprof": train}}
     nxt = Planner().next_plan(JobFeatures(mode="ps", params=3.3e8), _inv(8, busy=90), _plan(), metrics)
