@@ -277,6 +277,110 @@ __global__ __launch_bounds__(256) void transpose_bf16_kernel(const bf16_t* __res
   }
 }
 
+// ---------------------------------------------------------------------------
+// SwiGLU with a transposed copy of its output, for the NT-form weight gradients
+// of the MLP (ops/fused.py::swiglu_mlp).  One workgroup = a 64-row x 64-column
+// tile of h (fwd) or of d_gate/d_up (bwd).  The row-major result is written as
+// usual; the same tile also goes through a padded LDS tile and out transposed
+// (16-B stores along the token axis).  Writing the transposed copy here costs
+// one extra write; a separate transpose kernel would read it back and write it.
+// ---------------------------------------------------------------------------
+constexpr int TT = 64, TP = TT + 2;
+
+// column c of the tile, rows r8..r8+7, as one 16-B chunk
+__device__ __forceinline__ u32x4 tile_col8(const bf16_t* tile, int c, int r8) {
+  u32x4 o;
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    o[j] = (uint32_t)tile[(r8 + 2 * j) * TP + c] | ((uint32_t)tile[(r8 + 2 * j + 1) * TP + c] << 16);
+  return o;
+}
+
+// gu [M, 2F] -> h [M, F] and hT [F, M]
+__global__ __launch_bounds__(256) void swiglu_fwd_t_kernel(const bf16_t* __restrict__ gu, bf16_t* __restrict__ h,
+                                                           bf16_t* __restrict__ hT, int M, int F) {
+  __shared__ bf16_t tile[TT * TP];
+  const int r0 = blockIdx.y * TT, c0 = blockIdx.x * TT;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int idx = threadIdx.x + 256 * i;
+    const int r = idx >> 3, c8 = (idx & 7) * 8;
+    const int gr = r0 + r, gc = c0 + c8;
+    if (gr < M && gc + 8 <= F) {
+      const bf16_t* row = gu + (int64_t)gr * 2 * F;
+      float g[8], u[8], o[8];
+      unpack8(*reinterpret_cast<const u32x4*>(row + gc), g);
+      unpack8(*reinterpret_cast<const u32x4*>(row + F + gc), u);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) o[k] = g[k] * sigmoidf_(g[k]) * u[k];
+      const u32x4 packed = pack8(o);
+      *reinterpret_cast<u32x4*>(h + (int64_t)gr * F + gc) = packed;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {   // the bf16 values exactly as stored in h
+        tile[r * TP + c8 + 2 * j] = (bf16_t)(packed[j] & 0xffffu);
+        tile[r * TP + c8 + 2 * j + 1] = (bf16_t)(packed[j] >> 16);
+      }
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int idx = threadIdx.x + 256 * i;
+    const int c = idx >> 3, r8 = (idx & 7) * 8;
+    const int gc = c0 + c, gr = r0 + r8;
+    if (gc < F && gr + 8 <= M) *reinterpret_cast<u32x4*>(hT + (int64_t)gc * M + gr) = tile_col8(tile, c, r8);
+  }
+}
+
+// dh [M, F], gu [M, 2F] -> dgu [M, 2F] and dguT [2F, M]
+__global__ __launch_bounds__(256) void swiglu_bwd_t_kernel(const bf16_t* __restrict__ dh,
+                                                           const bf16_t* __restrict__ gu, bf16_t* __restrict__ dgu,
+                                                           bf16_t* __restrict__ dguT, int M, int F) {
+  __shared__ bf16_t tg[TT * TP], tu[TT * TP];
+  const int r0 = blockIdx.y * TT, c0 = blockIdx.x * TT;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int idx = threadIdx.x + 256 * i;
+    const int r = idx >> 3, c8 = (idx & 7) * 8;
+    const int gr = r0 + r, gc = c0 + c8;
+    if (gr < M && gc + 8 <= F) {
+      const bf16_t* row = gu + (int64_t)gr * 2 * F;
+      float g[8], u[8], d[8], dg[8], du[8];
+      unpack8(*reinterpret_cast<const u32x4*>(row + gc), g);
+      unpack8(*reinterpret_cast<const u32x4*>(row + F + gc), u);
+      unpack8(*reinterpret_cast<const u32x4*>(dh + (int64_t)gr * F + gc), d);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float sg = sigmoidf_(g[k]);
+        du[k] = d[k] * g[k] * sg;
+        dg[k] = d[k] * u[k] * sg * (1.f + g[k] * (1.f - sg));
+      }
+      const u32x4 pg = pack8(dg), pu = pack8(du);
+      bf16_t* orow = dgu + (int64_t)gr * 2 * F;
+      *reinterpret_cast<u32x4*>(orow + gc) = pg;
+      *reinterpret_cast<u32x4*>(orow + F + gc) = pu;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        tg[r * TP + c8 + 2 * j] = (bf16_t)(pg[j] & 0xffffu);
+        tg[r * TP + c8 + 2 * j + 1] = (bf16_t)(pg[j] >> 16);
+        tu[r * TP + c8 + 2 * j] = (bf16_t)(pu[j] & 0xffffu);
+        tu[r * TP + c8 + 2 * j + 1] = (bf16_t)(pu[j] >> 16);
+      }
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int idx = threadIdx.x + 256 * i;
+    const int c = idx >> 3, r8 = (idx & 7) * 8;
+    const int gc = c0 + c, gr = r0 + r8;
+    if (gc < F && gr + 8 <= M) {
+      *reinterpret_cast<u32x4*>(dguT + (int64_t)gc * M + gr) = tile_col8(tg, c, r8);
+      *reinterpret_cast<u32x4*>(dguT + (int64_t)(F + gc) * M + gr) = tile_col8(tu, c, r8);
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -292,6 +396,25 @@ int edl_swiglu_bwd(const void* dout, const void* gu, void* dgu, int64_t rows, in
   if (F % 8) return (int)hipErrorInvalidValue;
   swiglu_bwd_kernel<<<grid_for(rows * (F / 8)), 256, 0, s>>>((const bf16_t*)dout, (const bf16_t*)gu,
                                                              (bf16_t*)dgu, rows, F);
+  EDL_LAUNCH_CHECK();
+  return 0;
+}
+
+// h = swiglu(gu) and hT = h^T (M, F multiples of 8)
+int edl_swiglu_fwd_t(const void* gu, void* h, void* hT, int M, int F, hipStream_t s) {
+  if (F % 8 || M % 8 || M <= 0 || F <= 0) return (int)hipErrorInvalidValue;
+  dim3 grid((F + TT - 1) / TT, (M + TT - 1) / TT);
+  swiglu_fwd_t_kernel<<<grid, 256, 0, s>>>((const bf16_t*)gu, (bf16_t*)h, (bf16_t*)hT, M, F);
+  EDL_LAUNCH_CHECK();
+  return 0;
+}
+
+// dgu = swiglu'(gu) * dh and dguT = dgu^T
+int edl_swiglu_bwd_t(const void* dh, const void* gu, void* dgu, void* dguT, int M, int F, hipStream_t s) {
+  if (F % 8 || M % 8 || M <= 0 || F <= 0) return (int)hipErrorInvalidValue;
+  dim3 grid((F + TT - 1) / TT, (M + TT - 1) / TT);
+  swiglu_bwd_t_kernel<<<grid, 256, 0, s>>>((const bf16_t*)dh, (const bf16_t*)gu, (bf16_t*)dgu, (bf16_t*)dguT, M,
+                                           F);
   EDL_LAUNCH_CHECK();
   return 0;
 }

@@ -49,6 +49,8 @@ _KERNEL_SIGS = {
     "edl_colsum": [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p],
     "edl_swiglu_fwd": [c_void_p, c_void_p, c_i64, c_int, c_void_p],
     "edl_swiglu_bwd": [c_void_p, c_void_p, c_void_p, c_i64, c_int, c_void_p],
+    "edl_swiglu_fwd_t": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],
+    "edl_swiglu_bwd_t": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],
     "edl_rope_qkv_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_i64, c_int, c_int, c_int,
                          c_int, c_void_p],
     "edl_rope_qkv_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_i64, c_int, c_int, c_int,

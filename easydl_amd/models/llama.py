@@ -157,7 +157,7 @@ class LlamaBlock(nn.Module):
     def _mlp(self, n2):
         if self.tp_copy is not None:
             n2 = self.tp_copy(n2)
-        m = fused.linear(fused.swiglu(fused.linear(n2, self.w_gu)), self.w_down)
+        m = fused.swiglu_mlp(n2, self.w_gu, self.w_down)
         if self.tp_reduce is not None:
             m = self.tp_reduce(m)
         return m

@@ -215,3 +215,50 @@ def test_linear_weight_grad_nt_form_matches(cuda):
     ref = dy.float().t() @ x.float()
     torch.testing.assert_close(grads[0], ref, rtol=2e-2, atol=2e-1)
     torch.testing.assert_close(grads[0], grads[1], rtol=2e-2, atol=2e-1)
+
+
+@pytest.mark.parametrize("M,D,Fh", [(128, 256, 384), (200, 128, 200)])
+def test_swiglu_transposed_kernels(cuda, M, D, Fh):
+    """h / hT and dgu / dguT of the transposed-output SwiGLU kernels: the row-major
+    outputs match the plain kernels bit for bit and the transposed ones are exact
+    transposes (shapes include partial 64-tiles)."""
+    from easydl_amd import _native
+    k = _native.kernels()
+    st = _native.stream_of
+    torch.manual_seed(1)
+    gu = torch.randn(M, 2 * Fh, device="cuda").bfloat16()
+    dh = torch.randn(M, Fh, device="cuda").bfloat16()
+    h_ref = torch.empty(M, Fh, device="cuda", dtype=torch.bfloat16)
+    k.check("edl_swiglu_fwd", gu.data_ptr(), h_ref.data_ptr(), M, Fh, st(gu))
+    h, hT = torch.empty_like(h_ref), torch.empty(Fh, M, device="cuda", dtype=torch.bfloat16)
+    k.check("edl_swiglu_fwd_t", gu.data_ptr(), h.data_ptr(), hT.data_ptr(), M, Fh, st(gu))
+    assert torch.equal(h, h_ref) and torch.equal(hT, h_ref.t())
+    dgu_ref = torch.empty_like(gu)
+    k.check("edl_swiglu_bwd", dh.data_ptr(), gu.data_ptr(), dgu_ref.data_ptr(), M, Fh, st(gu))
+    dgu, dguT = torch.empty_like(gu), torch.empty(2 * Fh, M, device="cuda", dtype=torch.bfloat16)
+    k.check("edl_swiglu_bwd_t", dh.data_ptr(), gu.data_ptr(), dgu.data_ptr(), dguT.data_ptr(), M, Fh, st(gu))
+    torch.testing.assert_close(dgu.float(), dgu_ref.float(), rtol=1e-2, atol=1e-2)
+    assert torch.equal(dguT, dgu.t())
+
+
+def test_fused_swiglu_mlp_matches_fp32_reference(cuda):
+    """swiglu_mlp (NT-form weight gradients from the transposed SwiGLU outputs) vs an
+    fp32 PyTorch MLP: output, input gradient and both weight gradients."""
+    from easydl_amd.ops import fused
+    torch.manual_seed(2)
+    M, D, Fh = 256, 256, 512
+    x = torch.randn(M, D, device="cuda").bfloat16().requires_grad_(True)
+    w_gu = (torch.randn(2 * Fh, D, device="cuda") * 0.05).bfloat16().requires_grad_(True)
+    w_dn = (torch.randn(D, Fh, device="cuda") * 0.05).bfloat16().requires_grad_(True)
+    fused.new_weight_generation()
+    y = fused.swiglu_mlp(x, w_gu, w_dn)
+    assert y.grad_fn is not None and "SwiGLUMLP" in type(y.grad_fn).__name__
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    xr, gr, dr = (t.detach().float().requires_grad_(True) for t in (x, w_gu, w_dn))
+    g, u = (xr @ gr.t()).chunk(2, dim=-1)
+    yr = (torch.nn.functional.silu(g) * u) @ dr.t()
+    yr.backward(dy.float())
+    for a, b in ((y, yr), (x.grad, xr.grad), (w_gu.grad, gr.grad), (w_dn.grad, dr.grad)):
+        err = ((a.float() - b).abs().max() / (b.abs().max() + 1e-6)).item()
+        assert err < 3e-2, err
