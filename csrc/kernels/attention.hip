@@ -513,6 +513,22 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dkdv_kernel(
 // Llama shape: 1.35 ms (incl. the partial-sum reduce) vs 2.25 ms for the
 // 32-key kernel (profiles/r01_attn_dkdv_ab.txt); EDL_ATTN_DKDV=32 selects it.
 // ---------------------------------------------------------------------------
+// S / dP MFMAs of the dK/dV-64 kernel with their results pinned to VGPRs.  With the
+// builtin, the compiler puts every MFMA result in AGPRs, and S/dP (64) plus the dK/dV
+// accumulators (256) do not fit the 256 AGPRs: it shuffled 64 accumulators through
+// ~200 v_accvgpr moves per slice.  hipcc pads nothing inside asm: the first MFMA of a
+// chain takes C = 0 (no VALU-written C), chained MFMAs read C = their own D (0 wait
+// states), and mfma_d_fence pads the MFMA D -> VALU read once after both chains.
+__device__ __forceinline__ void mfma_v_first(f32x16& d, const bf16x8& a, const bf16x8& b) {
+  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(d) : "v"(a), "v"(b));
+}
+__device__ __forceinline__ void mfma_v(f32x16& d, const bf16x8& a, const bf16x8& b) {
+  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(d) : "v"(a), "v"(b));
+}
+__device__ __forceinline__ void mfma_d_fence(f32x16 (&x)[2], f32x16 (&y)[2]) {
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 4" : "+v"(x[0]), "+v"(x[1]), "+v"(y[0]), "+v"(y[1]));
+}
+
 template <bool MASK, bool CAUSAL>
 __device__ __forceinline__ void dkdv64_slice(const char* Qs, const char* Ds, const float* NL,
                                              const float* DL, int rb, const bf16x8 (&kf)[2][8],
@@ -521,7 +537,6 @@ __device__ __forceinline__ void dkdv64_slice(const char* Qs, const char* Ds, con
                                              float sl2, int lane) {
   const int h = lane >> 5, l31 = lane & 31;
   f32x16 sa[2], dp[2];
-  sa[0] = sa[1] = dp[0] = dp[1] = f32x16{};
   // V is read from LDS in every slice: the opaque offset stops the compiler from hoisting
   // the loop-invariant reads into (64 more) registers
   uint32_t vo = (uint32_t)(uintptr_t)(lds_char*)Vw;
@@ -530,17 +545,28 @@ __device__ __forceinline__ void dkdv64_slice(const char* Qs, const char* Ds, con
 #pragma unroll
   for (int s = 0; s < 8; ++s) {
     const bf16x8 a = row_read(Qs, rb + l31, s, h);
-    sa[0] = mfma(a, kf[0][s], sa[0]);
-    sa[1] = mfma(a, kf[1][s], sa[1]);
+    if (s == 0) {
+      mfma_v_first(sa[0], a, kf[0][s]);
+      mfma_v_first(sa[1], a, kf[1][s]);
+    } else {
+      mfma_v(sa[0], a, kf[0][s]);
+      mfma_v(sa[1], a, kf[1][s]);
+    }
   }
 #pragma unroll
   for (int s = 0; s < 8; ++s) {
     const bf16x8 a = row_read(Ds, rb + l31, s, h);
     const bf16x8 v0 = *(lds_bf16x8*)(Vl + swz(l31, 2 * s + h));
     const bf16x8 v1 = *(lds_bf16x8*)(Vl + swz(32 + l31, 2 * s + h));
-    dp[0] = mfma(a, v0, dp[0]);
-    dp[1] = mfma(a, v1, dp[1]);
+    if (s == 0) {
+      mfma_v_first(dp[0], a, v0);
+      mfma_v_first(dp[1], a, v1);
+    } else {
+      mfma_v(dp[0], a, v0);
+      mfma_v(dp[1], a, v1);
+    }
   }
+  mfma_d_fence(sa, dp);
   // per-row softmax terms are read from LDS right where they are used (no 32-VGPR arrays)
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
