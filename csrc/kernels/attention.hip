@@ -709,15 +709,14 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv64_kernel(
     __syncthreads();
     // Separate loops for the diagonal / tail tiles (masked body) and the rest (mask-free body):
     // one straight-line body per loop allocates registers far better than a branch per slice.
-    auto run = [&](auto masked, int j0, int j1) {
+    auto run = [&](auto masked, int j0, int j1) {  // unrolled over the two stages (constant LDS offsets)
       constexpr bool MASK = decltype(masked)::value;
-#pragma unroll 1
-      for (int j = j0; j < j1; ++j) {
-        if (j + 1 < total) fetch(j + 1, (j + 1) & 1);
-        const int st = j & 1;   // (unrolling over the stages as in fwd/dQ measured 2 % slower here: more spills)
-        const char* Qs = smem + st * 32768;
+      auto step = [&](int j, auto stage) {
+        constexpr int ST = decltype(stage)::value;   // == j & 1
+        if (j + 1 < total) fetch(j + 1, 1 - ST);
+        const char* Qs = smem + ST * 32768;
         const char* Ds = Qs + 16384;
-        const float* NL = reinterpret_cast<const float*>(smem + 2 * 32768 + st * 512);
+        const float* NL = reinterpret_cast<const float*>(smem + 2 * 32768 + ST * 512);
         const int q0 = (qt0 + j % per_head) * QT;
 #pragma unroll 1
         for (int sub = 0; sub < QT / 32; ++sub) {
@@ -727,7 +726,15 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv64_kernel(
         }
         wait_vm();
         __syncthreads();   // also fences the LDS buffers before the next block's first fetch
+      };
+      int j = j0;
+      if (j < j1 && (j & 1)) step(j++, std::integral_constant<int, 1>{});
+#pragma unroll 1
+      for (; j + 1 < j1; j += 2) {
+        step(j, std::integral_constant<int, 0>{});
+        step(j + 1, std::integral_constant<int, 1>{});
       }
+      if (j < j1) step(j, std::integral_constant<int, 0>{});
     };
     // tiles [lo, hi) of every head need no mask for any wave of this workgroup
     int lo = CAUSAL ? min(KB / QT, per_head) : 0;
