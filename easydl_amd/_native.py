@@ -68,6 +68,9 @@ _KERNEL_SIGS = {
                            c_i64, c_int, c_int, ctypes.c_uint32, c_int, c_void_p, ctypes.c_double, c_void_p,
                            c_void_p],
     "edl_xgmi_max_ranks": [],
+    "edl_xgmi_collective": [ctypes.POINTER(c_void_p), ctypes.POINTER(c_void_p), c_int, c_int, c_void_p, c_void_p,
+                            c_i64, c_i64, c_int, c_int, ctypes.c_uint32, c_int, c_void_p, ctypes.c_double, c_void_p,
+                            c_void_p],
     "edl_embed_gather": [c_void_p, c_void_p, c_i64, c_int, c_i64, c_void_p, c_int, c_void_p],
     "edl_embed_scatter_add": [c_void_p, c_void_p, c_void_p, c_int, c_i64, c_int, c_i64, c_void_p],
     "edl_sparse_rows_update": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_i64, c_int, c_i64, c_int, c_float,

@@ -219,8 +219,11 @@ class Communicator:
         self._verify("all_reduce", t, int(op))
         if self.rccl is not None:
             return self._native(self.rccl.all_reduce_async, t, op)
-        if self.xgmi is not None and self.xgmi_mode == "xgmi" and op == dist.ReduceOp.SUM and self.xgmi.supports(t):
-            return self._native(self.xgmi.all_reduce_async, t)
+        if self._use_xgmi(t):
+            if op == dist.ReduceOp.SUM:
+                return self._native(self.xgmi.all_reduce_async, t)
+            if op == dist.ReduceOp.MAX:
+                return self._native(self._xgmi_sync, self.xgmi.all_reduce_max, t)
         o = dist.AllreduceOptions()
         o.reduceOp = op
         return self.data.allreduce([t], o)
@@ -241,7 +244,18 @@ class Communicator:
         self._wait(self.data.broadcast([t], o), poll=True)
         return t
 
+    def _use_xgmi(self, *ts) -> bool:
+        return self.xgmi is not None and self.xgmi_mode == "xgmi" and all(self.xgmi.supports(t) for t in ts)
+
+    def _xgmi_sync(self, fn, *args):
+        """Run an xGMI collective on the caller's stream (TP/SP: the consumer is next)."""
+        fn(*args)
+        return _DoneWork()
+
     def all_gather_into(self, out: torch.Tensor, inp: torch.Tensor) -> torch.Tensor:
+        if self._use_xgmi(out, inp):
+            self._native(self.xgmi.all_gather, out, inp)
+            return out
         if self.rccl is not None:
             self._wait(self._native(self.rccl.all_gather_async, out, inp))
             return out
@@ -249,6 +263,9 @@ class Communicator:
         return out
 
     def reduce_scatter_into(self, out: torch.Tensor, inp: torch.Tensor, op=dist.ReduceOp.SUM) -> torch.Tensor:
+        if op == dist.ReduceOp.SUM and self._use_xgmi(out, inp):
+            self._native(self.xgmi.reduce_scatter, out, inp)
+            return out
         if self.rccl is not None:
             self._wait(self._native(self.rccl.reduce_scatter_async, out, inp, op))
             return out

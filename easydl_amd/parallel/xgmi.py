@@ -9,6 +9,9 @@ Usage (one object per rank and epoch; every rank issues the same calls)::
     x.all_reduce(t)           # in place, on the current stream
     x.abort()                 # watchdog thread: spinning kernels give up
 
+Also ``all_reduce_max``, ``all_gather`` and ``reduce_scatter`` (the TP / SP
+collectives; ``Communicator(data_backend="xgmi")`` routes them here).
+
 Limits: <= 8 ranks (one node), fp32 / bf16, sizes a multiple of 16 bytes
 (tensors are processed in workspace-sized pieces).
 """
@@ -113,6 +116,67 @@ class XgmiComm:
             if rc != 0:
                 raise XgmiError(f"launch failed: hipError {rc}")
         return t
+
+    # -- TP / SP collectives (one-shot MAX, all-gather, reduce-scatter) --------------
+    def _launch(self, kind: int, inp_ptr: int, out_ptr: int, nvec: int, stride: int, dtype, nblocks_hint: int):
+        blocks = int(max(1, min(self.blocks, -(-nblocks_hint // 2048))))
+        self.round += 1
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        rc = self._k("edl_xgmi_collective", self._data, self._flags, self.world_size, self.rank, inp_ptr, out_ptr,
+                     nvec, stride, 0 if dtype == torch.float32 else 1, kind, self.round, blocks, self._abort_dev,
+                     float(self.timeout_s), self._status_dev, stream)
+        if rc != 0:
+            raise XgmiError(f"launch failed: hipError {rc}")
+
+    def _check(self, *ts):
+        if self._aborted:
+            raise XgmiError("aborted")
+        for t in ts:
+            if t.dtype not in (torch.float32, torch.bfloat16) or not t.is_contiguous() or \
+                    (t.numel() * t.element_size()) % 16:
+                raise XgmiError("xGMI collectives take contiguous fp32 / bf16 tensors of 16-byte multiples")
+
+    def all_reduce_max(self, t: torch.Tensor) -> torch.Tensor:
+        """In-place element-wise MAX over ranks (one-shot)."""
+        self._check(t)
+        flat = t.view(-1)
+        es = flat.element_size()
+        piece = self.ws_bytes // es
+        for lo in range(0, flat.numel(), piece):
+            part = flat[lo:lo + piece]
+            nvec = part.numel() * es // 16
+            self._launch(0, part.data_ptr(), part.data_ptr(), nvec, 0, t.dtype, nvec)
+        return t
+
+    def all_gather(self, out: torch.Tensor, inp: torch.Tensor) -> torch.Tensor:
+        """out = concat over ranks of inp (rank-major), read directly from every peer."""
+        self._check(out, inp)
+        if out.dtype != inp.dtype or out.numel() != inp.numel() * self.world_size:
+            raise XgmiError("all_gather: out must hold world_size x inp")
+        es = inp.element_size()
+        n = inp.numel()
+        stride = n * es // 16
+        piece = (self.ws_bytes // 16) * 16 // es
+        src, dst = inp.view(-1), out.view(-1)
+        for lo in range(0, n, piece):
+            m = min(piece, n - lo)
+            self._launch(1, src[lo:].data_ptr(), dst[lo:].data_ptr(), m * es // 16, stride, inp.dtype, m * es // 16)
+        return out
+
+    def reduce_scatter(self, out: torch.Tensor, inp: torch.Tensor) -> torch.Tensor:
+        """out = SUM over ranks of this rank's slice of inp (inp = world_size slices, rank-major)."""
+        self._check(out, inp)
+        if out.dtype != inp.dtype or inp.numel() != out.numel() * self.world_size:
+            raise XgmiError("reduce_scatter: inp must hold world_size x out")
+        es = out.element_size()
+        n = out.numel()
+        stride = n * es // 16
+        piece = (self.ws_bytes // self.world_size // 16) * 16 // es   # all slices are staged
+        src, dst = inp.view(-1), out.view(-1)
+        for lo in range(0, n, piece):
+            m = min(piece, n - lo)
+            self._launch(2, src[lo:].data_ptr(), dst[lo:].data_ptr(), m * es // 16, stride, out.dtype, m * es // 16)
+        return out
 
     def all_reduce_async(self, t: torch.Tensor) -> "_Work":
         """In-place SUM on the engine's own high-priority stream, ordered after the

@@ -38,6 +38,36 @@ if mode == "sum":
             res["ok"] = False
             res["errors"].append(f"iter {it}: max err {(grads.double().cpu() - exp).abs().max().item()}")
     res["healthy"] = c.healthy()
+elif mode == "coll":
+    # TP / SP collectives on the engine: integer-valued data, so results are exact
+    def ints(shape, seed, dtype):
+        return torch.randint(-64, 64, shape, generator=torch.Generator().manual_seed(seed)).to(dtype)
+    for dtype in (torch.float32, torch.bfloat16):
+        n = 3 * 4096 + 64
+        t = ints((n,), 7 + rank, dtype).cuda()
+        exp = torch.stack([ints((n,), 7 + r, dtype) for r in range(world)]).float().amax(0)
+        c.all_reduce(t, dist.ReduceOp.MAX)
+        if not torch.equal(t.float().cpu(), exp):
+            res["ok"] = False
+            res["errors"].append(f"max {dtype}")
+        # all-gather / reduce-scatter, one message that needs several workspace pieces (64 MiB)
+        m = (24 << 20) // torch.tensor([], dtype=dtype).element_size() + 256
+        inp = ints((m,), 11 + rank, dtype).cuda()
+        out = torch.empty(world * m, dtype=dtype, device="cuda")
+        c.all_gather_into(out, inp)
+        exp = torch.cat([ints((m,), 11 + r, dtype) for r in range(world)])
+        if not torch.equal(out.cpu(), exp):
+            res["ok"] = False
+            res["errors"].append(f"all_gather {dtype}")
+        big = ints((world * m,), 13 + rank, dtype).cuda()
+        part = torch.empty(m, dtype=dtype, device="cuda")
+        c.reduce_scatter_into(part, big)
+        exp = sum(ints((world * m,), 13 + r, dtype).double() for r in range(world))[rank * m:(rank + 1) * m]
+        if not torch.equal(part.double().cpu(), exp):
+            res["ok"] = False
+            res["errors"].append(f"reduce_scatter {dtype}: max err {(part.double().cpu() - exp).abs().max().item()}")
+    torch.cuda.synchronize()
+    res["healthy"] = c.healthy()
 elif mode == "abort":
     if rank == 0:  # the peer never joins: the watchdog's abort() releases the kernel, healthy() says so
         t = torch.ones(1 << 16, device="cuda", dtype=torch.bfloat16)

@@ -62,3 +62,23 @@ def test_communicator_xgmi_bucket_allreduce(cuda, tmp_path):
 def test_communicator_xgmi_abort_marks_unhealthy(cuda, tmp_path):
     r0 = _run(2, tmp_path, mode="abort", worker=COMM_WORKER)[0]
     assert r0["aborted"] and not r0["healthy"]
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_communicator_xgmi_tp_collectives_exact(cuda, tmp_path, world):
+    """MAX all-reduce, all-gather and reduce-scatter on the engine (multi-piece messages)."""
+    for r in _run(world, tmp_path, mode="coll", worker=COMM_WORKER):
+        assert r["ok"], r["errors"]
+        assert r["healthy"]
+
+
+@pytest.mark.parametrize("sp", ["0", "1"])
+def test_llama_tp2_over_xgmi_matches_dense(cuda, tmp_path, sp, monkeypatch):
+    """TP=2 Llama (bf16 HIP kernels) with every TP/SP collective on the xGMI engine
+    matches the dense fp32 model's loss and sharded gradients."""
+    monkeypatch.setenv("SP", sp)
+    rs = _run(2, tmp_path, worker=os.path.join(ROOT, "tests", "helpers", "xgmi_tp_worker.py"), timeout=240)
+    for r in rs:
+        assert r["healthy"]
+        assert abs(r["loss_t"] - r["loss_d"]) < 2e-2 * max(1.0, abs(r["loss_d"])), r
+        assert r["grad_rel_err"] < 5e-2, r
