@@ -381,6 +381,124 @@ __global__ __launch_bounds__(256) void swiglu_bwd_t_kernel(const bf16_t* __restr
   }
 }
 
+// ---------------------------------------------------------------------------
+// Register-transposed forms (no LDS, no barrier).  Each lane owns an 8x8 bf16
+// block: 8 row loads of 16 B, an in-register transpose (v_perm), 8 stores of
+// 16 B along the other axis.  Lane = cb + 8 * rb inside a wave's 64x64 tile, so
+// every load and every store instruction of a wave covers 8 full 128-B lines;
+// a 256-thread block is a 128x128 tile (2x2 waves: 256 contiguous bytes per
+// row on both sides).  8-24 independent 16-B loads in flight per lane instead
+// of 2-6, and no 2-byte LDS traffic: the LDS versions above were
+// instruction-bound at ~4.1-4.7 TB/s.
+// ---------------------------------------------------------------------------
+constexpr int RT = 128;  // block tile (rows and columns)
+
+// out[j] = column j of the 8x8 block whose rows are in[0..7]
+__device__ __forceinline__ void transpose8x8(const u32x4 (&in)[8], u32x4 (&out)[8]) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t a = in[2 * k][j >> 1], b = in[2 * k + 1][j >> 1];
+      out[j][k] = (j & 1) ? ((a >> 16) | (b & 0xffff0000u)) : ((a & 0xffffu) | (b << 16));
+    }
+}
+
+// this lane's 8x8 block origin (row, column) inside the grid's 128x128 tiles.
+// Tiles are visited in diagonal order: consecutive (co-resident) workgroups
+// step BOTH the row and the column tile, so neither their loads nor their
+// transposed stores all sit at one power-of-two pitch (M = 16384 tokens is a
+// 32 KB row pitch on the transposed side: row-major order camps on a few
+// HBM channels).
+__device__ __forceinline__ void block8_origin(int& r, int& c) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int gx = gridDim.x, gy = gridDim.y;
+  const int b = blockIdx.x + gx * blockIdx.y;
+  const int ty = b % gy, tx = (b / gy + ty) % gx;
+  r = ty * RT + (w >> 1) * 64 + (lane >> 3) * 8;
+  c = tx * RT + (w & 1) * 64 + (lane & 7) * 8;
+}
+
+__global__ __launch_bounds__(256) void transpose_bf16_reg_kernel(const bf16_t* __restrict__ src,
+                                                                 bf16_t* __restrict__ dst, int R, int C) {
+  int r, c;
+  block8_origin(r, c);
+  if (r >= R || c >= C) return;  // R, C multiples of 8: a block is all in or all out
+  u32x4 in[8], out[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) in[i] = *reinterpret_cast<const u32x4*>(src + (int64_t)(r + i) * C + c);
+  transpose8x8(in, out);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) *reinterpret_cast<u32x4*>(dst + (int64_t)(c + j) * R + r) = out[j];
+}
+
+__global__ __launch_bounds__(256) void swiglu_fwd_t_reg_kernel(const bf16_t* __restrict__ gu, bf16_t* __restrict__ h,
+                                                               bf16_t* __restrict__ hT, int M, int F) {
+  int r, c;
+  block8_origin(r, c);
+  if (r >= M || c >= F) return;
+  u32x4 g8[8], u8[8], o8[8], t8[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const bf16_t* row = gu + (int64_t)(r + i) * 2 * F;
+    g8[i] = *reinterpret_cast<const u32x4*>(row + c);
+    u8[i] = *reinterpret_cast<const u32x4*>(row + F + c);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    float g[8], u[8], o[8];
+    unpack8(g8[i], g);
+    unpack8(u8[i], u);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o[k] = g[k] * sigmoidf_(g[k]) * u[k];
+    o8[i] = pack8(o);
+    *reinterpret_cast<u32x4*>(h + (int64_t)(r + i) * F + c) = o8[i];
+  }
+  transpose8x8(o8, t8);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) *reinterpret_cast<u32x4*>(hT + (int64_t)(c + j) * M + r) = t8[j];
+}
+
+__global__ __launch_bounds__(256) void swiglu_bwd_t_reg_kernel(const bf16_t* __restrict__ dh,
+                                                               const bf16_t* __restrict__ gu, bf16_t* __restrict__ dgu,
+                                                               bf16_t* __restrict__ dguT, int M, int F) {
+  int r, c;
+  block8_origin(r, c);
+  if (r >= M || c >= F) return;
+  u32x4 a8[8], b8[8], d8[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const bf16_t* row = gu + (int64_t)(r + i) * 2 * F;
+    a8[i] = *reinterpret_cast<const u32x4*>(row + c);
+    b8[i] = *reinterpret_cast<const u32x4*>(row + F + c);
+    d8[i] = *reinterpret_cast<const u32x4*>(dh + (int64_t)(r + i) * F + c);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {   // a8 <- d_gate, b8 <- d_up (same math as swiglu_bwd_t_kernel)
+    float g[8], u[8], d[8], dg[8], du[8];
+    unpack8(a8[i], g);
+    unpack8(b8[i], u);
+    unpack8(d8[i], d);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float sg = sigmoidf_(g[k]);
+      du[k] = d[k] * g[k] * sg;
+      dg[k] = d[k] * u[k] * sg * (1.f + g[k] * (1.f - sg));
+    }
+    a8[i] = pack8(dg);
+    b8[i] = pack8(du);
+    bf16_t* orow = dgu + (int64_t)(r + i) * 2 * F;
+    *reinterpret_cast<u32x4*>(orow + c) = a8[i];
+    *reinterpret_cast<u32x4*>(orow + F + c) = b8[i];
+  }
+  transpose8x8(a8, d8);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) *reinterpret_cast<u32x4*>(dguT + (int64_t)(c + j) * M + r) = d8[j];
+  transpose8x8(b8, d8);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) *reinterpret_cast<u32x4*>(dguT + (int64_t)(F + c + j) * M + r) = d8[j];
+}
+
 }  // namespace
 
 extern "C" {
@@ -403,6 +521,15 @@ int edl_swiglu_bwd(const void* dout, const void* gu, void* dgu, int64_t rows, in
 // h = swiglu(gu) and hT = h^T (M, F multiples of 8)
 int edl_swiglu_fwd_t(const void* gu, void* h, void* hT, int M, int F, hipStream_t s) {
   if (F % 8 || M % 8 || M <= 0 || F <= 0) return (int)hipErrorInvalidValue;
+  dim3 grid((F + RT - 1) / RT, (M + RT - 1) / RT);
+  swiglu_fwd_t_reg_kernel<<<grid, 256, 0, s>>>((const bf16_t*)gu, (bf16_t*)h, (bf16_t*)hT, M, F);
+  EDL_LAUNCH_CHECK();
+  return 0;
+}
+
+// LDS-tile version (kept for A/B measurement: scripts/transpose_ab.py)
+int edl_swiglu_fwd_t_lds(const void* gu, void* h, void* hT, int M, int F, hipStream_t s) {
+  if (F % 8 || M % 8 || M <= 0 || F <= 0) return (int)hipErrorInvalidValue;
   dim3 grid((F + TT - 1) / TT, (M + TT - 1) / TT);
   swiglu_fwd_t_kernel<<<grid, 256, 0, s>>>((const bf16_t*)gu, (bf16_t*)h, (bf16_t*)hT, M, F);
   EDL_LAUNCH_CHECK();
@@ -411,6 +538,15 @@ int edl_swiglu_fwd_t(const void* gu, void* h, void* hT, int M, int F, hipStream_
 
 // dgu = swiglu'(gu) * dh and dguT = dgu^T
 int edl_swiglu_bwd_t(const void* dh, const void* gu, void* dgu, void* dguT, int M, int F, hipStream_t s) {
+  if (F % 8 || M % 8 || M <= 0 || F <= 0) return (int)hipErrorInvalidValue;
+  dim3 grid((F + RT - 1) / RT, (M + RT - 1) / RT);
+  swiglu_bwd_t_reg_kernel<<<grid, 256, 0, s>>>((const bf16_t*)dh, (const bf16_t*)gu, (bf16_t*)dgu,
+                                               (bf16_t*)dguT, M, F);
+  EDL_LAUNCH_CHECK();
+  return 0;
+}
+
+int edl_swiglu_bwd_t_lds(const void* dh, const void* gu, void* dgu, void* dguT, int M, int F, hipStream_t s) {
   if (F % 8 || M % 8 || M <= 0 || F <= 0) return (int)hipErrorInvalidValue;
   dim3 grid((F + TT - 1) / TT, (M + TT - 1) / TT);
   swiglu_bwd_t_kernel<<<grid, 256, 0, s>>>((const bf16_t*)dh, (const bf16_t*)gu, (bf16_t*)dgu, (bf16_t*)dguT, M,
@@ -449,6 +585,14 @@ int edl_xent_fwd_bwd(void* logits, const int64_t* labels, float* loss, int64_t r
 
 // dst[C, R] = src[R, C]^T (bf16, R and C multiples of 8)
 int edl_transpose_bf16(const void* src, void* dst, int R, int C, hipStream_t s) {
+  if (R % 8 || C % 8 || R <= 0 || C <= 0) return (int)hipErrorInvalidValue;
+  dim3 grid((C + RT - 1) / RT, (R + RT - 1) / RT);
+  transpose_bf16_reg_kernel<<<grid, 256, 0, s>>>((const bf16_t*)src, (bf16_t*)dst, R, C);
+  EDL_LAUNCH_CHECK();
+  return 0;
+}
+
+int edl_transpose_bf16_lds(const void* src, void* dst, int R, int C, hipStream_t s) {
   if (R % 8 || C % 8 || R <= 0 || C <= 0) return (int)hipErrorInvalidValue;
   dim3 grid((C + 63) / 64, (R + 63) / 64);
   transpose_bf16_kernel<<<grid, 256, 0, s>>>((const bf16_t*)src, (bf16_t*)dst, R, C);

@@ -58,6 +58,9 @@ _KERNEL_SIGS = {
     "edl_xent_fwd_bwd": [c_void_p, c_void_p, c_void_p, c_i64, c_int, c_i64, c_int, c_void_p],
     "edl_scale_bf16": [c_void_p, c_i64, c_void_p, c_float, c_void_p],
     "edl_transpose_bf16": [c_void_p, c_void_p, c_int, c_int, c_void_p],
+    "edl_transpose_bf16_lds": [c_void_p, c_void_p, c_int, c_int, c_void_p],
+    "edl_swiglu_fwd_t_lds": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],
+    "edl_swiglu_bwd_t_lds": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],
     "edl_checksum": [c_void_p, c_i64, c_void_p, ctypes.c_uint64, c_void_p],
     "edl_attn_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
                      c_float, c_void_p],

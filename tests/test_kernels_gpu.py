@@ -169,7 +169,7 @@ def test_linear_direct_grad_into_flat(cuda):
     assert lin.weight.grad.data_ptr() == flat.groups[0].grad.data_ptr() + 0
 
 
-@pytest.mark.parametrize("R,C", [(4096, 6144), (136, 72), (14336, 4096)])
+@pytest.mark.parametrize("R,C", [(4096, 6144), (136, 72), (14336, 4096), (8, 200), (1000, 8)])
 def test_transpose_bf16(cuda, R, C):
     from easydl_amd import _native
     x = torch.randn(R, C, device="cuda").bfloat16()
