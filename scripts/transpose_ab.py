@@ -54,8 +54,10 @@ def main():
     dh = torch.randn(M, F, device=dev, dtype=torch.bfloat16)
     outs = {}
     for v, sfx in (("reg", ""), ("lds", "_lds")):
-        h, hT = torch.empty(M, F, device=dev, dtype=torch.bfloat16), torch.empty(F, M, device=dev, dtype=torch.bfloat16)
-        ms = timeit(lambda: k.check("edl_swiglu_fwd_t" + sfx, gu.data_ptr(), h.data_ptr(), hT.data_ptr(), M, F, st)) * 1e3
+        h = torch.empty(M, F, device=dev, dtype=torch.bfloat16)
+        hT = torch.empty(F, M, device=dev, dtype=torch.bfloat16)
+        ms = timeit(lambda: k.check("edl_swiglu_fwd_t" + sfx, gu.data_ptr(), h.data_ptr(), hT.data_ptr(),
+                                    M, F, st)) * 1e3
         rows.append({"kernel": "swiglu_fwd_t", "variant": v, "shape": [M, F], "ms": round(ms, 4),
                      "tb_s": round(2 * M * F * 4 / ms / 1e9, 3)})
         dgu, dguT = torch.empty_like(gu), torch.empty(2 * F, M, device=dev, dtype=torch.bfloat16)
