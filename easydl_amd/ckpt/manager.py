@@ -201,6 +201,8 @@ class CheckpointManager:
         self._ticket = None
         self._n = 0
         self._persist_thread = None
+        self._persist_slot = None   # slot the persist thread is reading (None: idle)
+        self._last_slot = None      # slot of the newest snapshot
         self.last_snapshot_step = None
         self.stats = {"snapshots": 0, "d2h_bytes": 0}
 
@@ -243,6 +245,10 @@ class CheckpointManager:
         key = (world, shard, tag)
         if self._seg is None or self._seg_key != key or self._seg.slot_bytes < need_bytes:
             if self._seg is not None:
+                # nothing may still read or write the mapping we are about to unmap:
+                # the in-flight D2H / committer (wait) and a disk persist (join)
+                self.wait()
+                self._join_persist()
                 self._seg.close()
             self._seg = ShmSegment(self.seg_name(world, shard, tag), need_bytes, create=True, pin=self.pin and pin)
             self._seg_key = key
@@ -263,12 +269,17 @@ class CheckpointManager:
             return
         state = self.state_of(trainer)
         layout, cs_off = shard_layout(state, shard, world)
+        self.wait()  # at most one snapshot in flight (and never one across a segment change)
         seg = self._segment(world, shard, cs_off + 8, pin=state[0][1].is_cuda, tag=tag)
+        if self._persist_busy_slot(seg):
+            # A/B slots: the slot this snapshot would overwrite is still being written to
+            # disk (persisting takes longer than two intervals) -> skip rather than tear it
+            self.stats["skipped"] = self.stats.get("skipped", 0) + 1
+            return
         meta = {"format": FORMAT, "step": trainer.step, "opt_step": trainer.opt.step_count, "world": world,
                 "shard": shard, "epoch": comm.epoch, "tag": tag,
                 "t": [[d["name"], d["dtype"], d["numel"], d["lo"], d["hi"], d["offset"]] for d in layout]}
         dev = state[0][1].device
-        self.wait()  # at most one snapshot in flight
         if dev.type == "cuda":
             if self._engine is None or self._engine_dev != dev.index:
                 self._engine = self.__class__._make_engine(dev.index)
@@ -290,6 +301,9 @@ class CheckpointManager:
             n = len(ptrs)
             arr = lambda v: (ctypes.c_uint64 * n)(*v)  # noqa: E731
             rt = _native.runtime()
+            # the engine claims the non-current slot (edl_shm_begin); the previous
+            # snapshot has been waited for, so "current" cannot move before it does
+            self._last_slot = self._next_slot(seg)
             t = rt("edl_ckpt_snapshot", self._engine, seg.h, n, arr(ptrs), arr(sizes), arr(offs),
                    ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream), trainer.step, comm.epoch, cs_off,
                    json.dumps(meta, separators=(",", ":")).encode())
@@ -299,6 +313,7 @@ class CheckpointManager:
             self._keep_alive = csum
         else:
             slot = seg.begin()
+            self._last_slot = slot
             total = 0
             for (name, t), d in zip(state, layout):
                 if d["nbytes"] == 0:
@@ -331,11 +346,27 @@ class CheckpointManager:
                               ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
 
     def wait(self, timeout_s: float = 600.0) -> None:
+        """Block until the in-flight snapshot is committed (main thread only)."""
         if self._ticket is not None and self._engine is not None:
             st = _native.runtime()("edl_ckpt_wait", self._engine, self._ticket, int(timeout_s * 1000))
             if st < 0:
                 raise RuntimeError(f"snapshot failed: {st}")
             self._ticket = None
+
+    @staticmethod
+    def _next_slot(seg: ShmSegment) -> int:
+        cur = seg.rt("edl_shm_current", seg.h)
+        return max(0, (cur + 1) % seg.rt("edl_shm_nslots", seg.h))
+
+    def _persist_busy_slot(self, seg: ShmSegment) -> bool:
+        th = self._persist_thread
+        return (th is not None and th.is_alive() and self._persist_slot is not None
+                and self._persist_slot == self._next_slot(seg))
+
+    def _join_persist(self, timeout_s: float | None = None) -> None:
+        th = self._persist_thread
+        if th is not None and th is not threading.current_thread():
+            th.join(timeout_s)
 
     # -- restore -------------------------------------------------------------
     def find_latest(self, tag: str = "", max_step: int | None = None) -> tuple[int, int, list[dict]] | None:
@@ -371,10 +402,15 @@ class CheckpointManager:
 
     def latest_step(self, trainer) -> int:
         """Newest restorable in-memory step of this trainer's state set (-1: none)."""
+        self.wait()  # this rank's own in-flight snapshot counts once it is committed
         found = self.find_latest(self._tag(trainer))
         return -1 if found is None else found[1]
 
     def restore_latest(self, trainer, max_step: int | None = None) -> str | None:
+        # Drain this rank's in-flight snapshot first: its D2H reads the very buffers the
+        # restore is about to overwrite, and its commit must not publish a slot that
+        # mixes pre- and post-rollback bytes under a pre-restore checksum.
+        self.wait()
         tag = self._tag(trainer)
         found = self.find_latest(tag, max_step)
         if found is None:
@@ -401,23 +437,47 @@ class CheckpointManager:
     def _persist_async(self, step: int) -> None:
         if self._persist_thread is not None and self._persist_thread.is_alive():
             return
-        self._persist_thread = threading.Thread(target=self._persist, args=(step,), daemon=True)
+        # The thread owns (seg, slot) until it ends: snapshot() skips rather than reuse
+        # that slot (_persist_busy_slot) and _segment() joins it before unmapping.
+        self._persist_slot = self._last_slot
+        args = (step, self._seg, self._engine, self._ticket, self._persist_slot)
+        self._persist_thread = threading.Thread(target=self._persist, args=args, daemon=True)
         self._persist_thread.start()
 
-    def _persist(self, step: int) -> None:
-        self.wait()
-        seg = self._seg
-        info = next((i for i in seg.committed() if i["step"] == step), None)
-        if info is None:
+    PERSIST_CHUNK = 64 << 20
+
+    def _persist(self, step: int, seg: ShmSegment, engine, ticket, slot: int) -> None:
+        try:
+            if ticket is not None and engine is not None:
+                # wait on the captured ticket: self._ticket belongs to the training thread
+                if _native.runtime()("edl_ckpt_wait", engine, ticket, 600000) < 0:
+                    return
+            self._persist_slot_to_disk(step, seg, slot)
+        except Exception:  # noqa: BLE001 - a failed persist must never kill training
+            log.exception("persisting step %d failed", step)
+        finally:
+            self._persist_slot = None
+
+    def _persist_slot_to_disk(self, step: int, seg: ShmSegment, slot: int) -> None:
+        info = seg.slot_info(slot)
+        if info is None or info["step"] != step:
             return
         m = info["meta"]
         tag = m.get("tag", "")
         d = os.path.join(self.persist_dir, f"step-{step}")
         os.makedirs(d, exist_ok=True)
         fname = f"shard{tag}-{m['shard']}-of-{m['world']}.bin"
-        with open(os.path.join(d, fname + ".tmp"), "wb") as f:
-            f.write(seg.view(info["slot"], 0, info["nbytes"]).tobytes())
-        os.replace(os.path.join(d, fname + ".tmp"), os.path.join(d, fname))
+        tmp = os.path.join(d, fname + ".tmp")
+        src = seg.view(slot, 0, info["nbytes"])
+        with open(tmp, "wb") as f:  # streamed from the mapping: no full-size host copy
+            for o in range(0, info["nbytes"], self.PERSIST_CHUNK):
+                f.write(src[o:o + self.PERSIST_CHUNK])
+        after = seg.slot_info(slot)
+        if after is None or any(after[k] != info[k] for k in ("step", "checksum", "nbytes")):
+            os.unlink(tmp)  # the slot was rewritten under us: never publish a torn file
+            log.warning("slot %d changed while persisting step %d: discarded", slot, step)
+            return
+        os.replace(tmp, os.path.join(d, fname))
         shard_manifest = {"file": fname, "checksum": info["checksum"], "nbytes": info["nbytes"],
                           "tensors": m["t"], "shard": m["shard"]}
         with open(os.path.join(d, f"shard{tag}-{m['shard']}.json"), "w") as f:
@@ -439,14 +499,19 @@ class CheckpointManager:
             shards = [os.path.join(d, f"shard{tag}-{s}.json") for s in range(m["world"])]
             if not all(os.path.exists(p) for p in shards):
                 continue
-            load_dir(d, trainer, tag)
+            try:
+                load_dir(d, trainer, tag)
+            except (RuntimeError, OSError, ValueError, KeyError) as e:
+                # torn / truncated shard: fall back to the next older complete directory
+                # (a later full load overwrites whatever this attempt already copied)
+                log.warning("checkpoint %s unusable (%s): trying an older one", d, e)
+                continue
             return f"disk:{d}"
         return None
 
     def close(self, unlink: bool = False) -> None:
         self.wait()
-        if self._persist_thread is not None:
-            self._persist_thread.join(timeout=60)
+        self._join_persist(60)
         if self._seg is not None:
             self._seg.close(unlink)
             self._seg = None

@@ -91,7 +91,24 @@ class XgmiComm:
         """0 = every barrier so far completed; 1 = one gave up (abort / deadline). Synchronising."""
         return self._rt("edl_xgmi_ws_status", self._ws)
 
+    # Every kernel of this comm runs on ONE stream (self.stream).  The workspace's
+    # round-parity buffers are only safe if a rank's rounds execute one after
+    # another: a sync collective issued while async bucket all-reduces are still
+    # pending must queue behind them, never run beside them.
+    def _serialized(self, fn, *args):
+        caller = torch.cuda.current_stream(self.device)
+        if caller == self.stream:
+            return fn(*args)
+        self.stream.wait_stream(caller)
+        with torch.cuda.stream(self.stream):
+            out = fn(*args)
+        caller.wait_stream(self.stream)
+        return out
+
     def all_reduce(self, t: torch.Tensor, algo: str | None = None) -> torch.Tensor:
+        return self._serialized(self._all_reduce, t, algo)
+
+    def _all_reduce(self, t: torch.Tensor, algo: str | None = None) -> torch.Tensor:
         if self._aborted:
             raise XgmiError("aborted")
         if t.dtype not in (torch.float32, torch.bfloat16) or not t.is_contiguous():
@@ -138,6 +155,17 @@ class XgmiComm:
 
     def all_reduce_max(self, t: torch.Tensor) -> torch.Tensor:
         """In-place element-wise MAX over ranks (one-shot)."""
+        return self._serialized(self._all_reduce_max, t)
+
+    def all_gather(self, out: torch.Tensor, inp: torch.Tensor) -> torch.Tensor:
+        """out = concat over ranks of inp (rank-major), read directly from every peer."""
+        return self._serialized(self._all_gather, out, inp)
+
+    def reduce_scatter(self, out: torch.Tensor, inp: torch.Tensor) -> torch.Tensor:
+        """out = SUM over ranks of this rank's slice of inp (inp = world_size slices, rank-major)."""
+        return self._serialized(self._reduce_scatter, out, inp)
+
+    def _all_reduce_max(self, t: torch.Tensor) -> torch.Tensor:
         self._check(t)
         flat = t.view(-1)
         es = flat.element_size()
@@ -148,8 +176,7 @@ class XgmiComm:
             self._launch(0, part.data_ptr(), part.data_ptr(), nvec, 0, t.dtype, nvec)
         return t
 
-    def all_gather(self, out: torch.Tensor, inp: torch.Tensor) -> torch.Tensor:
-        """out = concat over ranks of inp (rank-major), read directly from every peer."""
+    def _all_gather(self, out: torch.Tensor, inp: torch.Tensor) -> torch.Tensor:
         self._check(out, inp)
         if out.dtype != inp.dtype or out.numel() != inp.numel() * self.world_size:
             raise XgmiError("all_gather: out must hold world_size x inp")
@@ -163,8 +190,7 @@ class XgmiComm:
             self._launch(1, src[lo:].data_ptr(), dst[lo:].data_ptr(), m * es // 16, stride, inp.dtype, m * es // 16)
         return out
 
-    def reduce_scatter(self, out: torch.Tensor, inp: torch.Tensor) -> torch.Tensor:
-        """out = SUM over ranks of this rank's slice of inp (inp = world_size slices, rank-major)."""
+    def _reduce_scatter(self, out: torch.Tensor, inp: torch.Tensor) -> torch.Tensor:
         self._check(out, inp)
         if out.dtype != inp.dtype or inp.numel() != out.numel() * self.world_size:
             raise XgmiError("reduce_scatter: inp must hold world_size x out")
@@ -184,7 +210,7 @@ class XgmiComm:
         ``ProcessGroupNCCL`` work contract ElasticDDP overlaps with backward)."""
         self.stream.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(self.stream):
-            self.all_reduce(t)
+            self._all_reduce(t)
         t.record_stream(self.stream)
         ev = torch.cuda.Event()
         ev.record(self.stream)

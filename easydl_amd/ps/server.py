@@ -124,12 +124,18 @@ class ParameterServer:
         self._threads = []
 
     # -- optimizer -------------------------------------------------------------
+    def _fence_snapshot(self) -> None:
+        """Order every later write of a snapshotted buffer (dense shard, sparse
+        table rows, a restore) after the in-flight D2H copy of the snapshot."""
+        st = self.state
+        if st.w.is_cuda and hasattr(self.snapshot, "fence"):
+            self.snapshot.fence(st.w.device)
+
     def _apply(self, scale: float, grad: torch.Tensor | None = None) -> None:
         """One optimizer update of the shard from ``grad`` (default: the accumulator)."""
         st = self.state
         g = st.g if grad is None else grad
-        if st.w.is_cuda and hasattr(self.snapshot, "fence"):
-            self.snapshot.fence(st.w.device)  # never update under an in-flight snapshot copy
+        self._fence_snapshot()  # never update under an in-flight snapshot copy
         self.step += 1
         if self.optimizer == "adam":
             adamw_flat_(None, st.w, st.m, st.v, g, lr=self.lr, beta1=self.betas[0], beta2=self.betas[1],
@@ -169,6 +175,9 @@ class ParameterServer:
     def _push(self, worker: str, grads: dict[str, torch.Tensor], inbox: torch.Tensor | None = None) -> int:
         with self.lock:
             st = self.state
+            # sparse-table rows are updated below, before _apply: they are part of the
+            # snapshot too, so the fence must come first
+            self._fence_snapshot()
             if inbox is not None and self.mode == "async":
                 # GPU transport: the inbox IS the gradient of this update (no accumulate pass)
                 self._apply_sparse(grads, async_mode=True)
@@ -267,6 +276,7 @@ class ParameterServer:
                     send_msg(conn, {"ok": True, **meta}, out)
                 elif op == "load":
                     with self.lock:
+                        self._fence_snapshot()
                         self.load([tensors[f"b{i}"] for i in range(len(tensors))], hdr["version"], hdr["step"],
                                   hdr.get("table_steps"))
                     send_msg(conn, {"ok": True})

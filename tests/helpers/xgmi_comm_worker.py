@@ -68,6 +68,34 @@ elif mode == "coll":
             res["errors"].append(f"reduce_scatter {dtype}: max err {(part.double().cpu() - exp).abs().max().item()}")
     torch.cuda.synchronize()
     res["healthy"] = c.healthy()
+elif mode == "mixed":
+    # async bucket all-reduces still pending on the engine stream while sync collectives
+    # are issued on the SAME comm from the caller's stream: they must queue behind them
+    x = c.xgmi
+    for it in range(3):
+        def ints(n, seed):
+            return torch.randint(-32, 32, (n,), generator=torch.Generator().manual_seed(seed)).float()
+        big = [ints(6 << 20, 1000 * it + 10 * k + rank).cuda() for k in range(3)]
+        works = [x.all_reduce_async(b) for b in big]
+        m = 5 << 20
+        inp = ints(world * m, 2000 * it + rank).cuda()
+        part = torch.empty(m, device="cuda")
+        x.reduce_scatter(part, inp)
+        gat = torch.empty(world * m, device="cuda")
+        x.all_gather(gat, part)
+        for w in works:
+            w.wait()
+        torch.cuda.synchronize()
+        for k, b in enumerate(big):
+            exp = sum(ints(6 << 20, 1000 * it + 10 * k + r) for r in range(world))
+            if not torch.equal(b.cpu(), exp):
+                res["ok"] = False
+                res["errors"].append(f"iter {it} bucket {k}")
+        red = sum(ints(world * m, 2000 * it + r) for r in range(world))
+        if not torch.equal(part.cpu(), red[rank * m:(rank + 1) * m]) or not torch.equal(gat.cpu(), red):
+            res["ok"] = False
+            res["errors"].append(f"iter {it} rs/ag")
+    res["healthy"] = c.healthy()
 elif mode == "abort":
     if rank == 0:  # the peer never joins: the watchdog's abort() releases the kernel, healthy() says so
         t = torch.ones(1 << 16, device="cuda", dtype=torch.bfloat16)

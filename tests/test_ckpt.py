@@ -124,3 +124,52 @@ def test_premapped_segments_are_reused_by_restore(tmp_path):
         assert "/edl-premaptest-w1-s0" not in m._PREMAPPED
     finally:
         seg.close(unlink=True)
+
+
+def test_load_dir_latest_falls_back_past_a_torn_shard(tmp_path):
+    """A corrupted newest step-* directory is skipped: cold resume uses the next older one."""
+    unlink_job_segments("ck")
+    data = SyntheticTokens(CFG.vocab_size, 16, num_samples=1024)
+    disk = tmp_path / "disk"
+    ckpt = CheckpointManager("ck", interval=2, persist_dir=str(disk), persist_every=1)
+    try:
+        a = _trainer(tmp_path, ckpt)
+        a.fit(lambda m, b: m(*b), data, num_steps=6, on_step=lambda t, loss: ckpt._join_persist())
+        ckpt.close()
+        assert sorted(p.name for p in disk.iterdir()) == ["step-2", "step-4", "step-6"]
+        shard = next((disk / "step-6").glob("*.bin"))
+        raw = bytearray(shard.read_bytes())
+        raw[100] ^= 0xFF
+        shard.write_bytes(bytes(raw))
+        unlink_job_segments("ck")           # no in-memory copy left: the disk path is taken
+        b = _trainer(tmp_path, None, seed=77)
+        src = CheckpointManager("ck", persist_dir=str(disk)).restore_latest(b)
+        assert src == f"disk:{disk / 'step-4'}" and b.step == 4
+    finally:
+        unlink_job_segments("ck")
+
+
+def test_snapshot_skips_the_slot_a_persist_is_reading(tmp_path):
+    """A/B slots: while the disk writer still reads slot X, the snapshot that would
+    reuse X is skipped instead of tearing the file being written."""
+    import threading
+    unlink_job_segments("ck")
+    data = SyntheticTokens(CFG.vocab_size, 16, num_samples=1024)
+    ckpt = CheckpointManager("ck", interval=1)
+    try:
+        a = _trainer(tmp_path, ckpt)
+        a.fit(lambda m, b: m(*b), data, num_steps=1)          # snapshot of step 1 -> slot s1
+        release = threading.Event()
+        ckpt._persist_thread = threading.Thread(target=release.wait, daemon=True)
+        ckpt._persist_thread.start()
+        ckpt._persist_slot = ckpt._last_slot                  # "persisting step 1"
+        a.fit(lambda m, b: m(*b), data, num_steps=3)          # step 2 -> other slot; step 3 would reuse s1
+        assert ckpt.stats.get("skipped", 0) == 1 and ckpt.last_snapshot_step == 2
+        release.set()
+        ckpt._join_persist()
+        ckpt._persist_slot = None
+        a.fit(lambda m, b: m(*b), data, num_steps=4)
+        assert ckpt.last_snapshot_step == 4
+    finally:
+        ckpt.close()
+        unlink_job_segments("ck")

@@ -48,3 +48,26 @@ def test_async_snapshot_and_restore(cuda, tmp_path):
     finally:
         ckpt.close()
         unlink_job_segments("ckg")
+
+
+def test_restore_right_after_enqueue_drains_the_inflight_snapshot(cuda, tmp_path):
+    """restore_latest() right after a snapshot was enqueued (the DP x TP rollback path):
+    the in-flight D2H is drained first, so the slot it commits is consistent and a
+    second restore of the same step still verifies."""
+    unlink_job_segments("ckg")
+    data = SyntheticTokens(CFG.vocab_size, 64, num_samples=4096)
+    ckpt = CheckpointManager("ckg", interval=2)
+    try:
+        a = _trainer(tmp_path, ckpt, 1, cuda)
+        a.fit(lambda m, b: m(*b), data, num_steps=4)     # snapshot of step 4 still in flight
+        assert ckpt._ticket is not None
+        expect = _flat(a).clone()
+        assert ckpt.restore_latest(a) is not None and a.step == 4
+        assert torch.equal(_flat(a), expect)
+        a.fit(lambda m, b: m(*b), data, num_steps=6)     # step 6 enqueued ...
+        assert ckpt.restore_latest(a, max_step=4) is not None and a.step == 4   # ... roll back to 4
+        assert torch.equal(_flat(a), expect)
+        assert ckpt.latest_step(a) == 6
+    finally:
+        ckpt.close()
+        unlink_job_segments("ckg")

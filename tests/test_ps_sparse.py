@@ -201,3 +201,43 @@ def test_ps_gpu_async_snapshot_restores_exactly(cuda):
         for f in os.listdir("/dev/shm"):
             if f.startswith("edl-snaptest-ps"):
                 os.unlink("/dev/shm/" + f)
+
+
+@pytest.mark.gpu
+def test_ps_sparse_push_during_inflight_snapshot(cuda):
+    """Sparse-table rows pushed while a large snapshot is still copying are fenced
+    behind it: the committed slot is the pre-push state and restores exactly."""
+    import os
+
+    from easydl_amd import _native
+    from easydl_amd.models.deepctr import DeepFM
+    from easydl_amd.ps.client import shard_of
+    from easydl_amd.ps.embedding import table_shard_spec
+    from easydl_amd.ps.server import ParameterServer, PSSnapshotter
+    torch.manual_seed(0)
+    vocab = 40000                      # 26 x 40k rows x 16 x fp32 x {w, m, v}: ~200 MB to copy
+    ref = DeepFM(vocab=vocab, hidden=(64, 64))
+    snap = PSSnapshotter("snapsp", 0)
+    ps = ParameterServer(0, shard_of(ref, 1, 0), lr=1e-2, device="cuda", tables=table_shard_spec(ref, 1, 0),
+                         snapshot=snap, snapshot_every=2)
+
+    def push(n_ids):
+        g = {n: torch.randn(ps.state.shapes[n]) for n in ps.state.names}
+        g["sparse/emb/ids"] = torch.randint(0, vocab * 26, (n_ids,))
+        g["sparse/emb/grad"] = torch.randn(n_ids, 16)
+        ps._push("w", g)
+
+    try:
+        push(64)
+        push(64)                      # version 2: snapshot enqueued, copy in flight
+        expect = [b.clone() for b in ps.state_buffers()]
+        push(1 << 16)                 # touches rows all over the table right away
+        assert _native.runtime()("edl_ckpt_wait", snap.engine, snap.ticket, 60000) == 1
+        fresh = ParameterServer(0, shard_of(ref, 1, 0), lr=1e-2, device="cuda", tables=table_shard_spec(ref, 1, 0))
+        assert PSSnapshotter("snapsp", 0).restore(fresh)
+        assert fresh.version == 2
+        assert all(torch.equal(a, b) for a, b in zip(fresh.state_buffers(), expect))
+    finally:
+        for f in os.listdir("/dev/shm"):
+            if f.startswith("edl-snapsp-ps"):
+                os.unlink("/dev/shm/" + f)

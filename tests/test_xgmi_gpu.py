@@ -72,6 +72,14 @@ def test_communicator_xgmi_tp_collectives_exact(cuda, tmp_path, world):
         assert r["healthy"]
 
 
+def test_xgmi_sync_collectives_queue_behind_pending_async(cuda, tmp_path):
+    """Sync reduce-scatter / all-gather issued while async all-reduces are pending on
+    the same comm: one stream orders every round, all results exact."""
+    for r in _run(2, tmp_path, mode="mixed", worker=COMM_WORKER):
+        assert r["ok"], r["errors"]
+        assert r["healthy"]
+
+
 @pytest.mark.parametrize("sp", ["0", "1"])
 def test_llama_tp2_over_xgmi_matches_dense(cuda, tmp_path, sp, monkeypatch):
     """TP=2 Llama (bf16 HIP kernels) with every TP/SP collective on the xGMI engine
