@@ -343,6 +343,446 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_t* __restri
 }
 
 // ---------------------------------------------------------------------------
+// forward, software-pipelined (cdna_hip_programming.md "4-wave, one-wave-per-
+// SIMD" structure).  A workgroup = 4 waves = 256 queries of one head; a wave
+// owns 64 queries as two 32-query column blocks (qb) that share every K and V
+// fragment, so each LDS read feeds two MFMAs.  One wave per SIMD: the wave
+// hides its own latency by running the softmax of one tile beside the matrix
+// products of its neighbours.  Per 64-key tile j:
+//   phase 1: S(j+1) = K(j+1) Q^T   (32 MFMAs) || exp / row-sum / bf16-pack of S(j), qb 1
+//   phase 2: O^T += V(j)^T P(j)^T  (32 MFMAs) || row max of S(j+1), running-max update,
+//                                                exp / row-sum / pack of S(j+1), qb 0
+// so every MFMA gap carries <= ~5 VALU issues (cdna_hip_programming.md
+// Appendix B 'Fused attention prefill'), and at most one S tile plus half of
+// the next is live in fp32.  Register placement is pinned with asm MFMAs:
+// S in VGPRs (softmax works in place), O and Q in AGPRs (only MFMAs touch them
+// in the loop); each step is a sched_barrier region, so LDS reads are issued
+// one (V) or two (K) steps ahead of their MFMAs.  K/V tiles stream through
+// 4-slot LDS rings by LDS-DMA (K three tiles ahead, V two), one barrier per
+// tile; the body is unrolled over the ring slots so every LDS address is a
+// register plus an immediate.  Lazy rescale: the running max moves only when
+// a row grew by > 2^8 (then O is rescaled after the tile's PV, l at once).
+// ---------------------------------------------------------------------------
+namespace fwd64 {
+constexpr int NS = 4;         // ring slots
+constexpr int TB = 16384;     // one 64-row x 256-B tile
+
+// hipcc pads nothing inside asm: MFMA D -> VALU read needs 18 wait states
+// (fence_d), a VALU / v_accvgpr_write result -> MFMA operand 2 (fence_op);
+// chained MFMAs that take their own D whole as C need none.
+// MODE (debug bisect of register placement): bit0 Q operand in VGPRs instead of
+// AGPRs, bit1 S MFMAs by builtin, bit2 O MFMAs by builtin
+template <int MODE>
+__device__ __forceinline__ void mfma_s0(f32x16& d, const bf16x8& kf, const bf16x8& qf) {
+  if constexpr (MODE & 2) {
+    d = mfma(kf, qf, f32x16{});
+  } else if constexpr (MODE & 1) {
+    asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(d) : "v"(kf), "v"(qf));
+  } else {
+    asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(d) : "v"(kf), "a"(qf));
+  }
+}
+template <int MODE>
+__device__ __forceinline__ void mfma_s(f32x16& d, const bf16x8& kf, const bf16x8& qf) {
+  if constexpr (MODE & 2) {
+    d = mfma(kf, qf, d);
+  } else if constexpr (MODE & 1) {
+    asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(d) : "v"(kf), "v"(qf));
+  } else {
+    asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(d) : "v"(kf), "a"(qf));
+  }
+}
+template <int MODE>
+__device__ __forceinline__ void mfma_o(f32x16& acc, const bf16x8& vf, const bf16x8& pb) {
+  if constexpr (MODE & 4) {
+    acc = mfma(vf, pb, acc);
+  } else {
+    asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(vf), "v"(pb));
+  }
+}
+template <int MODE>
+__device__ __forceinline__ void fence_d(f32x16 (&x)[2][2]) {
+  if constexpr (!(MODE & 2))
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 4" : "+v"(x[0][0]), "+v"(x[0][1]), "+v"(x[1][0]), "+v"(x[1][1]));
+}
+template <int MODE>
+__device__ __forceinline__ void fence_d_acc(f32x16 (&o)[4]) {
+  if constexpr (!(MODE & 4))
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 4" : "+a"(o[0]), "+a"(o[1]), "+a"(o[2]), "+a"(o[3]));
+}
+template <int MODE>
+__device__ __forceinline__ void fence_acc(f32x16 (&o)[4]) {
+  if constexpr (MODE & 16)
+    asm volatile("s_nop 7\n\ts_nop 7" : "+a"(o[0]), "+a"(o[1]), "+a"(o[2]), "+a"(o[3]));
+  else if constexpr (!(MODE & 4))
+    asm volatile("s_nop 1" : "+a"(o[0]), "+a"(o[1]), "+a"(o[2]), "+a"(o[3]));
+}
+// keep the P operands of the PV MFMAs allocated until `point` (asm MFMAs are opaque:
+// hipcc would hand their source registers to VALU right after issue)
+template <int MODE>
+__device__ __forceinline__ void keep_pb(bf16x8 (&p)[2][2][2]) {
+  if constexpr ((MODE & 32) != 0)
+    asm volatile("" ::"v"(p[0][0][0]), "v"(p[0][0][1]), "v"(p[0][1][0]), "v"(p[0][1][1]), "v"(p[1][0][0]),
+                 "v"(p[1][0][1]), "v"(p[1][1][0]), "v"(p[1][1][1]));
+}
+template <int MODE>
+__device__ __forceinline__ void fence_op(bf16x8 (&p)[2][2][2]) {
+  if constexpr (!(MODE & 4))
+    asm volatile("s_nop 1" : "+v"(p[0][0][0]), "+v"(p[0][0][1]), "+v"(p[0][1][0]), "+v"(p[0][1][1]),
+                 "+v"(p[1][0][0]), "+v"(p[1][0][1]), "+v"(p[1][1][0]), "+v"(p[1][1][1]));
+}
+// v_max3 beside MFMA results (asm: hipcc otherwise inserts canonicalising v_max
+// before fmaxf on them).  Its inputs are MFMA results behind fence_d and
+// plain VALU (mask) values -- never a transcendental result: a trans -> VALU
+// read needs a wait state that hipcc does not pad for an asm consumer (an asm
+// v_add after v_exp read the pre-exp value).  Row sums are plain adds; this
+// file is built with -fno-slp-vectorize so they stay scalar (v_pk_add_f32
+// costs ~+22 cycles each beside MFMAs, MI355X_MICROARCH.md).
+__device__ __forceinline__ float max3(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
+struct State {
+  bf16x8 qf[2][8];            // Q fragments of the two 32-query blocks (AGPRs)
+  f32x16 o[2][4];             // O^T accumulators (d = 32*dt + row, query = lane & 31; AGPRs)
+  f32x16 s[2][2][2];          // S tiles by tile parity: [buf][qb][key half t]
+  bf16x8 pb[2][2][2][2];      // P tiles as bf16 B operands: [buf][qb][t][s2]
+  bf16x8 kf[3];               // K fragment ring (read two steps ahead)
+  bf16x8 vf[2];               // V fragment ring (read one step ahead)
+  float m[2], ls[2], al[2];   // running max (scaled log2), row sums, pending O rescale
+};
+
+#define EDL_SB() __builtin_amdgcn_sched_barrier(0)
+
+// LDS addressing: V ring at [0, 64K), K ring at [64K, 128K).  Every read is a
+// per-lane base register plus a compile-time immediate (slot, key half, s2)
+// that stays below the 16-bit ds offset limit: K bases hold 64K + the lane's
+// swizzled row/chunk for each k-step s (8 registers), V bases the lane's
+// transposed-read piece for each (dt, lo/hi) (8 registers).
+struct Lds {
+  uint32_t k[8];
+  uint32_t v[4][2];
+};
+
+__device__ __forceinline__ Lds lds_bases(const char* smem, int lane) {
+  Lds a;
+  const uint32_t base = (uint32_t)(uintptr_t)(const lds_char*)smem;
+  const int h = lane >> 5, l31 = lane & 31;
+#pragma unroll
+  for (int s = 0; s < 8; ++s) a.k[s] = base + NS * TB + swz(l31, 2 * s + h);
+  const int i = lane & 15, qq = i >> 2, p = i & 3;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) {
+    const int col = dt * 32 + ((lane >> 4) & 1) * 16 + 4 * p;
+    const int c = col >> 3, half = (col >> 2) & 1;
+    a.v[dt][0] = base + swz(4 * h + qq, c) + half * 8;
+    a.v[dt][1] = base + swz(4 * h + 8 + qq, c) + half * 8;
+  }
+#pragma unroll
+  for (int s = 0; s < 8; ++s) asm volatile("" : "+v"(a.k[s]));   // keep them plain registers
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) asm volatile("" : "+v"(a.v[dt][0]), "+v"(a.v[dt][1]));
+  return a;
+}
+
+// K fragment of step k (key half k>>3, k-step k&7) of ring slot `slot`
+__device__ __forceinline__ void kread(State& st, const Lds& a, int slot, int k) {
+  st.kf[k % 3] = *(const lds_bf16x8*)(uintptr_t)(a.k[k & 7] + slot * TB + (k >> 3) * 8192);
+}
+// V^T fragment of PV step k (key half k>>3, s2 = (k>>2)&1, dt = k&3) of ring slot `slot`
+__device__ __forceinline__ void vread(State& st, const Lds& a, int slot, int k) {
+  const uint32_t off = slot * TB + (32 * (k >> 3) + 16 * ((k >> 2) & 1)) * 256;
+  const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(uintptr_t)(a.v[k & 3][0] + off));
+  const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(uintptr_t)(a.v[k & 3][1] + off));
+  st.vf[k & 1] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+
+// exp / row sum of scores f (0..31, = 16 t + i) of query block qb of S(buf); packs
+// every completed group of 8 into pb[buf][qb]
+__device__ __forceinline__ void soft(State& st, int buf, int qb, int f0, int f1, float sl2, float negm) {
+#pragma unroll
+  for (int f = f0; f < f1; ++f) {
+    const int t = f >> 4, i = f & 15;
+    const float p = fast_exp2(__builtin_fmaf(st.s[buf][qb][t][i], sl2, negm));
+    st.s[buf][qb][t][i] = p;
+    st.ls[qb] += p;
+    if ((f & 7) == 7) st.pb[buf][qb][t][(f >> 3) & 1] = acc_to_b(st.s[buf][qb][t], (f >> 3) & 1);
+  }
+  // pin the sum here: otherwise hipcc sinks the add chain to the loop latch and keeps
+  // every p alive (spilled) until then
+  asm volatile("" : "+v"(st.ls[qb]));
+}
+
+// phase 1: S(nb) = K Q^T (K fragments 0, 1 already read) || softmax of S(cb), qb 1
+template <int MODE>
+__device__ __forceinline__ void phase1(State& st, int nb, int cb, const Lds& a, int kslot, float sl2,
+                                       bool soft1) {
+  const float negm = -st.m[1];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    if (k + 2 < 16) kread(st, a, kslot, k + 2);
+    const int t = k >> 3, s = k & 7;
+    if (s == 0) {
+      mfma_s0<MODE>(st.s[nb][0][t], st.kf[k % 3], st.qf[0][s]);
+      mfma_s0<MODE>(st.s[nb][1][t], st.kf[k % 3], st.qf[1][s]);
+    } else {
+      mfma_s<MODE>(st.s[nb][0][t], st.kf[k % 3], st.qf[0][s]);
+      mfma_s<MODE>(st.s[nb][1][t], st.kf[k % 3], st.qf[1][s]);
+    }
+    if (soft1) soft(st, cb, 1, 2 * k, 2 * k + 2, sl2, negm);
+    EDL_SB();
+  }
+}
+
+// phase 2: O += V^T P(cb)^T (V fragment 0 already read) || max of S(nb) (steps 0-3),
+// running-max update, softmax of S(nb), qb 0 (steps 4-15).  S(nb) is fenced.
+template <int MODE>
+__device__ __forceinline__ void phase2(State& st, int nb, int cb, const Lds& a, int vslot, float sl2, bool next) {
+  float mx[2][2];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    if (k + 1 < 16) vread(st, a, vslot, k + 1);
+    const int t = k >> 3, s2 = (k >> 2) & 1, dt = k & 3;
+    mfma_o<MODE>(st.o[0][dt], st.vf[k & 1], st.pb[cb][0][t][s2]);
+    mfma_o<MODE>(st.o[1][dt], st.vf[k & 1], st.pb[cb][1][t][s2]);
+    if (next) {
+      if (k < 4) {   // 4 registers per (qb, t) per step
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+          for (int tt = 0; tt < 2; ++tt) {
+            const f32x16& x = st.s[nb][qb][tt];
+            mx[qb][tt] = k == 0 ? max3(max3(x[0], x[1], x[2]), x[3], x[3])
+                                : max3(max3(mx[qb][tt], x[4 * k], x[4 * k + 1]), x[4 * k + 2], x[4 * k + 3]);
+          }
+      }
+      if (k == 3) {  // running-max update (per row; l at once, O after this tile's PV)
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb) {
+          const float mxs = xhalf_max(fmaxf(mx[qb][0], mx[qb][1])) * sl2;
+          const float mnew = mxs > st.m[qb] + 8.f ? fmaxf(st.m[qb], mxs) : st.m[qb];
+          const float alpha = fast_exp2(st.m[qb] - mnew);
+          st.m[qb] = mnew;
+          st.ls[qb] *= alpha;
+          st.al[qb] *= alpha;
+        }
+      }
+      if (k >= 4) soft(st, nb, 0, (32 * (k - 4)) / 12, (32 * (k - 3)) / 12, sl2, -st.m[0]);
+    }
+    EDL_SB();
+  }
+  keep_pb<MODE>(st.pb[cb]);
+}
+
+// pending O rescale (rare: only when some row's max moved)
+template <int MODE>
+__device__ __forceinline__ void apply_rescale(State& st) {
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    if (__any(st.al[qb] != 1.f)) {
+      fence_d_acc<MODE>(st.o[qb]);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) st.o[qb][dt] *= st.al[qb];
+      fence_acc<MODE>(st.o[qb]);
+    }
+    st.al[qb] = 1.f;
+  }
+}
+
+// scores of keys past min(query, S-1) -> -inf (diagonal / tail tiles only)
+template <bool CAUSAL>
+__device__ __forceinline__ void mask(State& st, int buf, int kv0, int wq0, int S, int h) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    const int lim = CAUSAL ? min(wq0 + 32 * qb + (lane & 31), S - 1) : S - 1;
+    const int rel = lim - kv0 - 4 * h;   // key - kv0 - 4h = 32t + (i&3) + 8(i>>2)
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int i = 0; i < 16; ++i)
+        if (32 * t + (i & 3) + 8 * (i >> 2) > rel) st.s[buf][qb][t][i] = -INFINITY;
+  }
+}
+
+// s_waitcnt vmcnt(N) for the LDS-DMA pieces still allowed in flight
+__device__ __forceinline__ void wait_vm_n(int n) {
+  if (n >= 8)
+    __builtin_amdgcn_s_waitcnt(0x0F78);
+  else if (n >= 4)
+    __builtin_amdgcn_s_waitcnt(0x0F74);
+  else
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+}
+}  // namespace fwd64
+
+template <bool CAUSAL, int MODE>
+__global__ __launch_bounds__(256, 1) void attn_fwd64_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
+                                                            const bf16_t* __restrict__ v, bf16_t* __restrict__ o,
+                                                            float* __restrict__ lse, int S, int H, int KV,
+                                                            float sl2) {
+  using namespace fwd64;
+  constexpr int BQ = 256;
+  __shared__ __attribute__((aligned(16))) char smem[2 * NS * TB];   // K ring, then V ring (one array)
+  const int qblk = gridDim.x - 1 - blockIdx.x;  // longest causal rows first
+  const int hq = blockIdx.y, b = blockIdx.z, hk = hq / (H / KV);
+  const int lane = threadIdx.x & 63, h = lane >> 5, l31 = lane & 31;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int q0 = qblk * BQ, wq0 = q0 + 64 * w;
+  const int64_t qs = (int64_t)H * HD, ks = (int64_t)KV * HD;
+  const bf16_t* qp = q + (int64_t)b * S * qs + hq * HD;
+  const bf16_t* kp = k + (int64_t)b * S * ks + hk * HD;
+  const bf16_t* vp = v + (int64_t)b * S * ks + hk * HD;
+
+  State st;
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    const bf16_t* rowp = qp + (int64_t)min(wq0 + 32 * qb + l31, S - 1) * qs;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) st.qf[qb][s] = load_frag(rowp, s, h);
+    st.m[qb] = -1e30f;
+    st.ls[qb] = 0.f;
+    st.al[qb] = 1.f;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) st.o[qb][dt] = f32x16{};
+  }
+  const int kv_end = CAUSAL ? min(S, q0 + BQ) : S;
+  const int nt = (kv_end + 63) / 64;
+  const int nfull = CAUSAL ? min(q0, S) / 64 : S / 64;   // tiles that need no mask for any wave
+
+  const DmaPlan<64, 4> plan(ks, w, lane);
+  const int64_t kv_bytes = ((int64_t)S * ks - hk * HD) * 2;
+  const rsrc_t krs = make_rsrc(kp, kv_bytes), vrs = make_rsrc(vp, kv_bytes);
+  const uint32_t tile_bytes = (uint32_t)(64 * ks * 2);
+  char* const Vr = smem;             // V ring [0, 64K)
+  char* const Kr = smem + NS * TB;   // K ring [64K, 128K)
+  // K(i) -> K slot i%4, three tiles ahead; V(i) -> V slot i%4, two tiles ahead
+  plan.issue(Kr, krs, 0, w);
+  if (nt > 1) plan.issue(Kr + TB, krs, tile_bytes, w);
+  if (nt > 2) plan.issue(Kr + 2 * TB, krs, 2 * tile_bytes, w);
+  plan.issue(Vr, vrs, 0, w);
+  if (nt > 1) plan.issue(Vr + TB, vrs, tile_bytes, w);
+  wait_vm();
+  __syncthreads();
+  // Q fragments and the zeroed O -> AGPRs (v_accvgpr_write -> MFMA operand: 2 wait states)
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+#pragma unroll
+    for (int s = 0; s < 8; s += 4)
+      if constexpr (!(MODE & 3))
+        asm volatile("s_nop 1" : "+a"(st.qf[qb][s]), "+a"(st.qf[qb][s + 1]), "+a"(st.qf[qb][s + 2]),
+                     "+a"(st.qf[qb][s + 3]));
+    fence_acc<MODE>(st.o[qb]);
+  }
+
+  const Lds la = lds_bases(smem, lane);
+  // prologue: S(0), its row max, the running max, softmax of S(0) qb 0
+  kread(st, la, 0, 0);
+  kread(st, la, 0, 1);
+  phase1<MODE>(st, 0, 1, la, 0, sl2, false);
+  fence_d<MODE>(st.s[0]);
+  if (0 >= nfull) mask<CAUSAL>(st, 0, 0, wq0, S, h);
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    float a = st.s[0][qb][0][0];
+#pragma unroll
+    for (int f = 1; f < 32; ++f) a = fmaxf(a, st.s[0][qb][f >> 4][f & 15]);
+    st.m[qb] = xhalf_max(a) * sl2;   // O = 0, l = 0: nothing to rescale
+  }
+  soft(st, 0, 0, 0, 32, sl2, -st.m[0]);
+  if constexpr ((MODE & 8) != 0) {   // debug dump of wave 0 after the prologue (lse = scratch buffer)
+    if (w == 0 && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0) {
+      float* d = lse + lane * 64;
+      d[0] = st.m[0];
+      d[1] = st.ls[0];
+      d[2] = st.m[1];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        d[8 + i] = st.s[0][0][0][i];
+        d[24 + i] = st.s[0][0][1][i];
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) d[40 + j] = (float)st.pb[0][0][0][0][j];
+    }
+    return;
+  }
+
+  // iteration j (ring slot ST = j % 4, tile parity B = j % 2): K(j+1), V(j) resident
+  auto iter = [&](int j, auto stage) {
+    constexpr int ST = decltype(stage)::value;
+    constexpr int B = ST & 1;
+    int issued = 0;
+    kread(st, la, (ST + 1) % NS, 0);
+    kread(st, la, (ST + 1) % NS, 1);
+    if (j + 3 < nt) {
+      plan.issue(Kr + ((ST + 3) % NS) * TB, krs, (uint32_t)(j + 3) * tile_bytes, w);
+      issued += 4;
+    }
+    EDL_SB();
+    phase1<MODE>(st, B ^ 1, B, la, (ST + 1) % NS, sl2, true);
+    if (j + 2 < nt) {
+      plan.issue(Vr + ((ST + 2) % NS) * TB, vrs, (uint32_t)(j + 2) * tile_bytes, w);
+      issued += 4;
+    }
+    vread(st, la, ST, 0);
+    fence_op<MODE>(st.pb[B]);
+    fence_d<MODE>(st.s[B ^ 1]);
+    EDL_SB();
+#ifndef EDL_ISA_HOTPATH  // (ISA audits of the steady-state body compile the rare paths out)
+    if (j + 1 >= nfull) mask<CAUSAL>(st, B ^ 1, (j + 1) * 64, wq0, S, h);
+#endif
+    phase2<MODE>(st, B ^ 1, B, la, ST, sl2, true);
+#ifndef EDL_ISA_HOTPATH
+    apply_rescale<MODE>(st);
+#endif
+    wait_vm_n(issued);
+    __builtin_amdgcn_s_barrier();
+  };
+  int j = 0;
+#pragma unroll 1
+  for (; j + 4 <= nt - 1; j += 4) {
+    iter(j, std::integral_constant<int, 0>{});
+    iter(j + 1, std::integral_constant<int, 1>{});
+    iter(j + 2, std::integral_constant<int, 2>{});
+    iter(j + 3, std::integral_constant<int, 3>{});
+  }
+  if (j < nt - 1) iter(j++, std::integral_constant<int, 0>{});
+  if (j < nt - 1) iter(j++, std::integral_constant<int, 1>{});
+  if (j < nt - 1) iter(j++, std::integral_constant<int, 2>{});
+  // drain: softmax of the last tile's qb 1, its PV (runtime slot; once per workgroup),
+  // epilogue.  Each parity branch ends with its own fence + stores so that no O value
+  // is live across the join: hipcc would otherwise insert v_accvgpr_mov phi copies
+  // right behind the last (asm, opaque) MFMA and read its result before it lands.
+  {
+    const int vslot = (nt - 1) % NS;
+    auto fin = [&](auto bufc) {
+      constexpr int CB = decltype(bufc)::value;
+      soft(st, CB, 1, 0, 32, sl2, -st.m[1]);
+      fence_op<MODE>(st.pb[CB]);
+      vread(st, la, vslot, 0);
+      phase2<MODE>(st, CB ^ 1, CB, la, vslot, sl2, false);
+      fence_d_acc<MODE>(st.o[0]);
+      fence_d_acc<MODE>(st.o[1]);
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) {
+        const int qr = wq0 + 32 * qb + l31;
+        const float ltot = xhalf_sum(st.ls[qb]);
+        if (qr < S) {
+          store_accT(o + (int64_t)b * S * qs + (int64_t)qr * qs + hq * HD, st.o[qb], 1.f / ltot, h);
+          if (h == 0) lse[((int64_t)b * H + hq) * S + qr] = (st.m[qb] + log2f(ltot)) * LN2;
+        }
+      }
+    };
+    if ((nt - 1) & 1)
+      fin(std::integral_constant<int, 1>{});
+    else
+      fin(std::integral_constant<int, 0>{});
+  }
+}
+
+// ---------------------------------------------------------------------------
 // backward preprocess: delta = rowsum(dO * O)   (16 lanes per row, 16 B each)
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void attn_bwd_delta_kernel(const bf16_t* __restrict__ o,
@@ -904,10 +1344,48 @@ extern "C" {
 int edl_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int S, int H, int KV,
                  int D, int causal, float scale, hipStream_t s) {
   if (D != HD || H % KV != 0 || S <= 0) return (int)hipErrorInvalidValue;
-  // 64 rows per wave (two 32-row groups sharing each K/V fragment) needs 512
-  // registers -> 1 wave/SIMD, which measured 2.7x slower (latency exposed).
-  dim3 grid((S + 127) / 128, H, B);
   const float sl2 = scale * LOG2E;
+  // EDL_ATTN_FWD=64: the software-pipelined 64-queries-per-wave kernel
+  const char* sel = getenv("EDL_ATTN_FWD");
+  if (sel && atoi(sel) == 64) {
+    dim3 g64((S + 255) / 256, H, B);
+    const char* me = getenv("EDL_ATTN_FWD_MODE");
+    const int mode = me ? atoi(me) : 0;
+#define EDL_FWD64(C, M)                                                                                         \
+  attn_fwd64_kernel<C, M><<<g64, 256, 0, s>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (bf16_t*)o, \
+                                              lse, S, H, KV, sl2)
+    if (causal) {
+      switch (mode) {
+        case 1: EDL_FWD64(true, 1); break;
+        case 2: EDL_FWD64(true, 2); break;
+        case 4: EDL_FWD64(true, 4); break;
+        case 16: EDL_FWD64(true, 16); break;
+        case 32: EDL_FWD64(true, 32); break;
+        case 48: EDL_FWD64(true, 48); break;
+        case 8: EDL_FWD64(true, 8); break;
+        case 14: EDL_FWD64(true, 14); break;
+        case 6: EDL_FWD64(true, 6); break;
+        case 7: EDL_FWD64(true, 7); break;
+        default: EDL_FWD64(true, 0);
+      }
+    } else {
+      switch (mode) {
+        case 1: EDL_FWD64(false, 1); break;
+        case 2: EDL_FWD64(false, 2); break;
+        case 4: EDL_FWD64(false, 4); break;
+        case 16: EDL_FWD64(false, 16); break;
+        case 32: EDL_FWD64(false, 32); break;
+        case 48: EDL_FWD64(false, 48); break;
+        case 6: EDL_FWD64(false, 6); break;
+        case 7: EDL_FWD64(false, 7); break;
+        default: EDL_FWD64(false, 0);
+      }
+    }
+#undef EDL_FWD64
+    EDL_LAUNCH_CHECK();
+    return 0;
+  }
+  dim3 grid((S + 127) / 128, H, B);
   if (causal)
     attn_fwd_kernel<true><<<grid, 256, 0, s>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
                                                    (bf16_t*)o, lse, S, H, KV, sl2);

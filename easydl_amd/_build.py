@@ -61,6 +61,11 @@ def _check_resolves(lib: str) -> None:
         raise RuntimeError(f"{os.path.basename(lib)}: undefined kernel launch stubs: {missing}")
 
 
+# per-source flags: the attention kernels keep f32 softmax adds scalar beside MFMAs
+# (packed v_pk_add_f32 is an anti-lever there, MI355X_MICROARCH.md cycle constants)
+_EXTRA_FLAGS = {"attention.hip": ["-fno-slp-vectorize"]}
+
+
 def build_kernels(force: bool = False, verbose: bool = False) -> str:
     srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
     hdrs = glob.glob(os.path.join(CSRC, "kernels", "*.h")) + glob.glob(os.path.join(CSRC, "include", "*.h"))
@@ -73,7 +78,7 @@ def build_kernels(force: bool = False, verbose: bool = False) -> str:
             os.makedirs(os.path.dirname(o), exist_ok=True)
             if force or _stale(o, [s] + hdrs):
                 cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-c", s, "-o", o,
-                       "-Wno-unused-result"]
+                       "-Wno-unused-result"] + _EXTRA_FLAGS.get(os.path.basename(s), [])
                 if verbose:
                     print(" ".join(cmd))
                 _run(cmd)

@@ -80,6 +80,7 @@ _KERNEL_SIGS = {
                                c_float, c_float, c_float, c_float, c_i64, c_float, c_void_p],
     "edl_ps_pull_cast": [c_void_p, c_void_p, c_i64, c_void_p],
     "edl_xgmi_max_blocks": [],
+    "edl_diag_lds_dma": [c_void_p, c_void_p, c_int, c_void_p],
 }
 
 

@@ -23,7 +23,10 @@ def _err(a, b):
 @pytest.mark.parametrize("B,S,H,KV,causal", [(1, 128, 4, 4, True), (2, 256, 8, 2, True), (1, 200, 4, 1, True),
                                              (1, 384, 8, 8, False), (2, 200, 4, 2, False), (1, 1024, 32, 8, True),
                                              (1, 2112, 8, 2, True)])
-def test_flash_attention_fwd_bwd(cuda, B, S, H, KV, causal):
+@pytest.mark.parametrize("fwd", ["0", "64"])
+def test_flash_attention_fwd_bwd(cuda, B, S, H, KV, causal, fwd, monkeypatch):
+    """Both forward kernels (EDL_ATTN_FWD=0: 32 queries/wave; 64: software-pipelined)."""
+    monkeypatch.setenv("EDL_ATTN_FWD", fwd)
     q, k, v = _mk(B, S, H, KV, cuda, S + H)
     q1, k1, v1 = (t.detach().clone().requires_grad_() for t in (q, k, v))
     o = flash_attention(q1, k1, v1, causal=causal)
@@ -36,6 +39,19 @@ def test_flash_attention_fwd_bwd(cuda, B, S, H, KV, causal):
     assert _err(q1.grad, q2.grad) < 3e-2, "dq"
     assert _err(k1.grad, k2.grad) < 3e-2, "dk"
     assert _err(v1.grad, v2.grad) < 3e-2, "dv"
+
+
+@pytest.mark.parametrize("fwd", ["0", "64"])
+def test_flash_attention_forces_lazy_rescale(cuda, fwd, monkeypatch):
+    """A late key that every query scores highly moves the running max mid-row
+    (the lazy-rescale branch of both forward kernels) -- cdna_hip_programming.md rule 26."""
+    monkeypatch.setenv("EDL_ATTN_FWD", fwd)
+    q, k, v = _mk(1, 1000, 8, 2, cuda, 7)
+    k = k.clone()
+    k[:, :, 500] = q[:, 0:1, 500].expand(-1, 2, -1) * 3.0
+    o = flash_attention(q, k, v, causal=True)
+    ref = attention_ref(q.float(), k.float(), v.float(), causal=True)
+    assert _err(o, ref) < 2e-2
 
 
 def test_flash_attention_speed_report(cuda):
