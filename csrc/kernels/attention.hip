@@ -370,66 +370,27 @@ constexpr int TB = 16384;     // one 64-row x 256-B tile
 // hipcc pads nothing inside asm: MFMA D -> VALU read needs 18 wait states
 // (fence_d), a VALU / v_accvgpr_write result -> MFMA operand 2 (fence_op);
 // chained MFMAs that take their own D whole as C need none.
-// MODE (debug bisect of register placement): bit0 Q operand in VGPRs instead of
-// AGPRs, bit1 S MFMAs by builtin, bit2 O MFMAs by builtin
-template <int MODE>
 __device__ __forceinline__ void mfma_s0(f32x16& d, const bf16x8& kf, const bf16x8& qf) {
-  if constexpr (MODE & 2) {
-    d = mfma(kf, qf, f32x16{});
-  } else if constexpr (MODE & 1) {
-    asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(d) : "v"(kf), "v"(qf));
-  } else {
-    asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(d) : "v"(kf), "a"(qf));
-  }
+  asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(d) : "v"(kf), "a"(qf));
 }
-template <int MODE>
 __device__ __forceinline__ void mfma_s(f32x16& d, const bf16x8& kf, const bf16x8& qf) {
-  if constexpr (MODE & 2) {
-    d = mfma(kf, qf, d);
-  } else if constexpr (MODE & 1) {
-    asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(d) : "v"(kf), "v"(qf));
-  } else {
-    asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(d) : "v"(kf), "a"(qf));
-  }
+  asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(d) : "v"(kf), "a"(qf));
 }
-template <int MODE>
 __device__ __forceinline__ void mfma_o(f32x16& acc, const bf16x8& vf, const bf16x8& pb) {
-  if constexpr (MODE & 4) {
-    acc = mfma(vf, pb, acc);
-  } else {
-    asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(vf), "v"(pb));
-  }
+  asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(vf), "v"(pb));
 }
-template <int MODE>
 __device__ __forceinline__ void fence_d(f32x16 (&x)[2][2]) {
-  if constexpr (!(MODE & 2))
-    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 4" : "+v"(x[0][0]), "+v"(x[0][1]), "+v"(x[1][0]), "+v"(x[1][1]));
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 4" : "+v"(x[0][0]), "+v"(x[0][1]), "+v"(x[1][0]), "+v"(x[1][1]));
 }
-template <int MODE>
 __device__ __forceinline__ void fence_d_acc(f32x16 (&o)[4]) {
-  if constexpr (!(MODE & 4))
-    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 4" : "+a"(o[0]), "+a"(o[1]), "+a"(o[2]), "+a"(o[3]));
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 4" : "+a"(o[0]), "+a"(o[1]), "+a"(o[2]), "+a"(o[3]));
 }
-template <int MODE>
 __device__ __forceinline__ void fence_acc(f32x16 (&o)[4]) {
-  if constexpr (MODE & 16)
-    asm volatile("s_nop 7\n\ts_nop 7" : "+a"(o[0]), "+a"(o[1]), "+a"(o[2]), "+a"(o[3]));
-  else if constexpr (!(MODE & 4))
-    asm volatile("s_nop 1" : "+a"(o[0]), "+a"(o[1]), "+a"(o[2]), "+a"(o[3]));
+  asm volatile("s_nop 1" : "+a"(o[0]), "+a"(o[1]), "+a"(o[2]), "+a"(o[3]));
 }
-// keep the P operands of the PV MFMAs allocated until `point` (asm MFMAs are opaque:
-// hipcc would hand their source registers to VALU right after issue)
-template <int MODE>
-__device__ __forceinline__ void keep_pb(bf16x8 (&p)[2][2][2]) {
-  if constexpr ((MODE & 32) != 0)
-    asm volatile("" ::"v"(p[0][0][0]), "v"(p[0][0][1]), "v"(p[0][1][0]), "v"(p[0][1][1]), "v"(p[1][0][0]),
-                 "v"(p[1][0][1]), "v"(p[1][1][0]), "v"(p[1][1][1]));
-}
-template <int MODE>
 __device__ __forceinline__ void fence_op(bf16x8 (&p)[2][2][2]) {
-  if constexpr (!(MODE & 4))
-    asm volatile("s_nop 1" : "+v"(p[0][0][0]), "+v"(p[0][0][1]), "+v"(p[0][1][0]), "+v"(p[0][1][1]),
-                 "+v"(p[1][0][0]), "+v"(p[1][0][1]), "+v"(p[1][1][0]), "+v"(p[1][1][1]));
+  asm volatile("s_nop 1" : "+v"(p[0][0][0]), "+v"(p[0][0][1]), "+v"(p[0][1][0]), "+v"(p[0][1][1]),
+               "+v"(p[1][0][0]), "+v"(p[1][0][1]), "+v"(p[1][1][0]), "+v"(p[1][1][1]));
 }
 // v_max3 beside MFMA results (asm: hipcc otherwise inserts canonicalising v_max
 // before fmaxf on them).  Its inputs are MFMA results behind fence_d and
@@ -516,7 +477,6 @@ __device__ __forceinline__ void soft(State& st, int buf, int qb, int f0, int f1,
 }
 
 // phase 1: S(nb) = K Q^T (K fragments 0, 1 already read) || softmax of S(cb), qb 1
-template <int MODE>
 __device__ __forceinline__ void phase1(State& st, int nb, int cb, const Lds& a, int kslot, float sl2,
                                        bool soft1) {
   const float negm = -st.m[1];
@@ -525,11 +485,11 @@ __device__ __forceinline__ void phase1(State& st, int nb, int cb, const Lds& a, 
     if (k + 2 < 16) kread(st, a, kslot, k + 2);
     const int t = k >> 3, s = k & 7;
     if (s == 0) {
-      mfma_s0<MODE>(st.s[nb][0][t], st.kf[k % 3], st.qf[0][s]);
-      mfma_s0<MODE>(st.s[nb][1][t], st.kf[k % 3], st.qf[1][s]);
+      mfma_s0(st.s[nb][0][t], st.kf[k % 3], st.qf[0][s]);
+      mfma_s0(st.s[nb][1][t], st.kf[k % 3], st.qf[1][s]);
     } else {
-      mfma_s<MODE>(st.s[nb][0][t], st.kf[k % 3], st.qf[0][s]);
-      mfma_s<MODE>(st.s[nb][1][t], st.kf[k % 3], st.qf[1][s]);
+      mfma_s(st.s[nb][0][t], st.kf[k % 3], st.qf[0][s]);
+      mfma_s(st.s[nb][1][t], st.kf[k % 3], st.qf[1][s]);
     }
     if (soft1) soft(st, cb, 1, 2 * k, 2 * k + 2, sl2, negm);
     EDL_SB();
@@ -538,15 +498,14 @@ __device__ __forceinline__ void phase1(State& st, int nb, int cb, const Lds& a, 
 
 // phase 2: O += V^T P(cb)^T (V fragment 0 already read) || max of S(nb) (steps 0-3),
 // running-max update, softmax of S(nb), qb 0 (steps 4-15).  S(nb) is fenced.
-template <int MODE>
 __device__ __forceinline__ void phase2(State& st, int nb, int cb, const Lds& a, int vslot, float sl2, bool next) {
   float mx[2][2];
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
     if (k + 1 < 16) vread(st, a, vslot, k + 1);
     const int t = k >> 3, s2 = (k >> 2) & 1, dt = k & 3;
-    mfma_o<MODE>(st.o[0][dt], st.vf[k & 1], st.pb[cb][0][t][s2]);
-    mfma_o<MODE>(st.o[1][dt], st.vf[k & 1], st.pb[cb][1][t][s2]);
+    mfma_o(st.o[0][dt], st.vf[k & 1], st.pb[cb][0][t][s2]);
+    mfma_o(st.o[1][dt], st.vf[k & 1], st.pb[cb][1][t][s2]);
     if (next) {
       if (k < 4) {   // 4 registers per (qb, t) per step
 #pragma unroll
@@ -573,19 +532,17 @@ __device__ __forceinline__ void phase2(State& st, int nb, int cb, const Lds& a, 
     }
     EDL_SB();
   }
-  keep_pb<MODE>(st.pb[cb]);
 }
 
 // pending O rescale (rare: only when some row's max moved)
-template <int MODE>
 __device__ __forceinline__ void apply_rescale(State& st) {
 #pragma unroll
   for (int qb = 0; qb < 2; ++qb) {
     if (__any(st.al[qb] != 1.f)) {
-      fence_d_acc<MODE>(st.o[qb]);
+      fence_d_acc(st.o[qb]);
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) st.o[qb][dt] *= st.al[qb];
-      fence_acc<MODE>(st.o[qb]);
+      fence_acc(st.o[qb]);
     }
     st.al[qb] = 1.f;
   }
@@ -618,7 +575,7 @@ __device__ __forceinline__ void wait_vm_n(int n) {
 }
 }  // namespace fwd64
 
-template <bool CAUSAL, int MODE>
+template <bool CAUSAL>
 __global__ __launch_bounds__(256, 1) void attn_fwd64_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
                                                             const bf16_t* __restrict__ v, bf16_t* __restrict__ o,
                                                             float* __restrict__ lse, int S, int H, int KV,
@@ -671,18 +628,17 @@ __global__ __launch_bounds__(256, 1) void attn_fwd64_kernel(const bf16_t* __rest
   for (int qb = 0; qb < 2; ++qb) {
 #pragma unroll
     for (int s = 0; s < 8; s += 4)
-      if constexpr (!(MODE & 3))
-        asm volatile("s_nop 1" : "+a"(st.qf[qb][s]), "+a"(st.qf[qb][s + 1]), "+a"(st.qf[qb][s + 2]),
-                     "+a"(st.qf[qb][s + 3]));
-    fence_acc<MODE>(st.o[qb]);
+      asm volatile("s_nop 1" : "+a"(st.qf[qb][s]), "+a"(st.qf[qb][s + 1]), "+a"(st.qf[qb][s + 2]),
+                   "+a"(st.qf[qb][s + 3]));
+    fence_acc(st.o[qb]);
   }
 
   const Lds la = lds_bases(smem, lane);
   // prologue: S(0), its row max, the running max, softmax of S(0) qb 0
   kread(st, la, 0, 0);
   kread(st, la, 0, 1);
-  phase1<MODE>(st, 0, 1, la, 0, sl2, false);
-  fence_d<MODE>(st.s[0]);
+  phase1(st, 0, 1, la, 0, sl2, false);
+  fence_d(st.s[0]);
   if (0 >= nfull) mask<CAUSAL>(st, 0, 0, wq0, S, h);
 #pragma unroll
   for (int qb = 0; qb < 2; ++qb) {
@@ -692,22 +648,6 @@ __global__ __launch_bounds__(256, 1) void attn_fwd64_kernel(const bf16_t* __rest
     st.m[qb] = xhalf_max(a) * sl2;   // O = 0, l = 0: nothing to rescale
   }
   soft(st, 0, 0, 0, 32, sl2, -st.m[0]);
-  if constexpr ((MODE & 8) != 0) {   // debug dump of wave 0 after the prologue (lse = scratch buffer)
-    if (w == 0 && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0) {
-      float* d = lse + lane * 64;
-      d[0] = st.m[0];
-      d[1] = st.ls[0];
-      d[2] = st.m[1];
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        d[8 + i] = st.s[0][0][0][i];
-        d[24 + i] = st.s[0][0][1][i];
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) d[40 + j] = (float)st.pb[0][0][0][0][j];
-    }
-    return;
-  }
 
   // iteration j (ring slot ST = j % 4, tile parity B = j % 2): K(j+1), V(j) resident
   auto iter = [&](int j, auto stage) {
@@ -721,21 +661,21 @@ __global__ __launch_bounds__(256, 1) void attn_fwd64_kernel(const bf16_t* __rest
       issued += 4;
     }
     EDL_SB();
-    phase1<MODE>(st, B ^ 1, B, la, (ST + 1) % NS, sl2, true);
+    phase1(st, B ^ 1, B, la, (ST + 1) % NS, sl2, true);
     if (j + 2 < nt) {
       plan.issue(Vr + ((ST + 2) % NS) * TB, vrs, (uint32_t)(j + 2) * tile_bytes, w);
       issued += 4;
     }
     vread(st, la, ST, 0);
-    fence_op<MODE>(st.pb[B]);
-    fence_d<MODE>(st.s[B ^ 1]);
+    fence_op(st.pb[B]);
+    fence_d(st.s[B ^ 1]);
     EDL_SB();
 #ifndef EDL_ISA_HOTPATH  // (ISA audits of the steady-state body compile the rare paths out)
     if (j + 1 >= nfull) mask<CAUSAL>(st, B ^ 1, (j + 1) * 64, wq0, S, h);
 #endif
-    phase2<MODE>(st, B ^ 1, B, la, ST, sl2, true);
+    phase2(st, B ^ 1, B, la, ST, sl2, true);
 #ifndef EDL_ISA_HOTPATH
-    apply_rescale<MODE>(st);
+    apply_rescale(st);
 #endif
     wait_vm_n(issued);
     __builtin_amdgcn_s_barrier();
@@ -760,11 +700,11 @@ __global__ __launch_bounds__(256, 1) void attn_fwd64_kernel(const bf16_t* __rest
     auto fin = [&](auto bufc) {
       constexpr int CB = decltype(bufc)::value;
       soft(st, CB, 1, 0, 32, sl2, -st.m[1]);
-      fence_op<MODE>(st.pb[CB]);
+      fence_op(st.pb[CB]);
       vread(st, la, vslot, 0);
-      phase2<MODE>(st, CB ^ 1, CB, la, vslot, sl2, false);
-      fence_d_acc<MODE>(st.o[0]);
-      fence_d_acc<MODE>(st.o[1]);
+      phase2(st, CB ^ 1, CB, la, vslot, sl2, false);
+      fence_d_acc(st.o[0]);
+      fence_d_acc(st.o[1]);
 #pragma unroll
       for (int qb = 0; qb < 2; ++qb) {
         const int qr = wq0 + 32 * qb + l31;
@@ -1349,39 +1289,12 @@ int edl_attn_fwd(const void* q, const void* k, const void* v, void* o, float* ls
   const char* sel = getenv("EDL_ATTN_FWD");
   if (sel && atoi(sel) == 64) {
     dim3 g64((S + 255) / 256, H, B);
-    const char* me = getenv("EDL_ATTN_FWD_MODE");
-    const int mode = me ? atoi(me) : 0;
-#define EDL_FWD64(C, M)                                                                                         \
-  attn_fwd64_kernel<C, M><<<g64, 256, 0, s>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (bf16_t*)o, \
-                                              lse, S, H, KV, sl2)
-    if (causal) {
-      switch (mode) {
-        case 1: EDL_FWD64(true, 1); break;
-        case 2: EDL_FWD64(true, 2); break;
-        case 4: EDL_FWD64(true, 4); break;
-        case 16: EDL_FWD64(true, 16); break;
-        case 32: EDL_FWD64(true, 32); break;
-        case 48: EDL_FWD64(true, 48); break;
-        case 8: EDL_FWD64(true, 8); break;
-        case 14: EDL_FWD64(true, 14); break;
-        case 6: EDL_FWD64(true, 6); break;
-        case 7: EDL_FWD64(true, 7); break;
-        default: EDL_FWD64(true, 0);
-      }
-    } else {
-      switch (mode) {
-        case 1: EDL_FWD64(false, 1); break;
-        case 2: EDL_FWD64(false, 2); break;
-        case 4: EDL_FWD64(false, 4); break;
-        case 16: EDL_FWD64(false, 16); break;
-        case 32: EDL_FWD64(false, 32); break;
-        case 48: EDL_FWD64(false, 48); break;
-        case 6: EDL_FWD64(false, 6); break;
-        case 7: EDL_FWD64(false, 7); break;
-        default: EDL_FWD64(false, 0);
-      }
-    }
-#undef EDL_FWD64
+    if (causal)
+      attn_fwd64_kernel<true><<<g64, 256, 0, s>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
+                                                     (bf16_t*)o, lse, S, H, KV, sl2);
+    else
+      attn_fwd64_kernel<false><<<g64, 256, 0, s>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
+                                                      (bf16_t*)o, lse, S, H, KV, sl2);
     EDL_LAUNCH_CHECK();
     return 0;
   }

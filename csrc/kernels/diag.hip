@@ -30,7 +30,8 @@ __global__ __launch_bounds__(64) void diag_lds_dma_kernel(const uint32_t* __rest
   // and what landed at off - 64 KiB (a wrapped 16-bit address would land there)
   if (off >= 65536) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) out[256 + lane * 4 + i] = reinterpret_cast<const uint32_t*>(smem + off - 65536)[lane * 4 + i];
+    for (int i = 0; i < 4; ++i)
+      out[256 + lane * 4 + i] = reinterpret_cast<const uint32_t*>(smem + off - 65536)[lane * 4 + i];
   }
 }
 }  // namespace

@@ -11,7 +11,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from easydl_amd.ops.attention import attention_ref, flash_attention  # noqa: E402
 
-VARIANTS = ["0", "64", "64m2", "64m4"]
+VARIANTS = ["0", "64"]
 
 
 def mk(B, S, H, KV, seed, spike=False):
@@ -40,8 +40,7 @@ def numerics():
         ref = attention_ref(q.float(), k.float(), v.float(), causal=causal)
         row = {"shape": [B, S, H, KV, causal, spike]}
         for var in VARIANTS:
-            os.environ["EDL_ATTN_FWD"], _, mode = var.partition("m")
-            os.environ["EDL_ATTN_FWD_MODE"] = mode or "0"
+            os.environ["EDL_ATTN_FWD"] = var
             row[var] = round(err(flash_attention(q, k, v, causal=causal), ref), 5)
         out.append(row)
     return out
@@ -53,15 +52,13 @@ def timing(rounds=5, iters=10):
     flops = 4 * B * H * S * S * 128 / 2
     res = {var: [] for var in VARIANTS}
     for var in VARIANTS:
-        os.environ["EDL_ATTN_FWD"], _, mode = var.partition("m")
-        os.environ["EDL_ATTN_FWD_MODE"] = mode or "0"
+        os.environ["EDL_ATTN_FWD"] = var
         for _ in range(3):
             flash_attention(q, k, v)
     torch.cuda.synchronize()
     for _ in range(rounds):
         for var in VARIANTS:
-            os.environ["EDL_ATTN_FWD"], _, mode = var.partition("m")
-            os.environ["EDL_ATTN_FWD_MODE"] = mode or "0"
+            os.environ["EDL_ATTN_FWD"] = var
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(iters):

@@ -56,7 +56,8 @@ def main():
                 c[classify(x.split()[0])] += 1
             mf = max(1, c["mfma"])
             if "--hist" in sys.argv:
-                h = Counter(x.split()[0] for x in (y.strip() for y in body[lo:i + 1])
+                lines_ = (y.strip() for y in body[lo:i + 1])
+                h = Counter(x.split()[0] for x in lines_
                             if x and not x.startswith((";", ".")) and not x.endswith(":"))
                 print("   ", ", ".join(f"{k} {v}" for k, v in h.most_common(40)))
             print(f"loop {m.group(1)} lines {start + lo + 1}-{start + i + 1}: " + " ".join(f"{k}={v}" for k, v in sorted(c.items()))
