@@ -60,8 +60,8 @@ def main():
                 h = Counter(x.split()[0] for x in lines_
                             if x and not x.startswith((";", ".")) and not x.endswith(":"))
                 print("   ", ", ".join(f"{k} {v}" for k, v in h.most_common(40)))
-            print(f"loop {m.group(1)} lines {start + lo + 1}-{start + i + 1}: " + " ".join(f"{k}={v}" for k, v in sorted(c.items()))
-                  + f"  valu/mfma={c['valu'] / mf:.2f}")
+            mix = " ".join(f"{k}={v}" for k, v in sorted(c.items()))
+            print(f"loop {m.group(1)} lines {start + lo + 1}-{start + i + 1}: {mix}  valu/mfma={c['valu'] / mf:.2f}")
 
 
 if __name__ == "__main__":
