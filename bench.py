@@ -51,9 +51,12 @@ def parse():
     ap.add_argument("--fault-inject", action="store_true", help="measure time-to-recover instead (local operator)")
     ap.add_argument("--scale-up", default=None, metavar="START:END",
                     help="measure an elastic scale-up mid-run instead (BASELINE config 2, ResNet-50)")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="--fault-inject: all --gpus workers on GPU 0 over the xGMI engine (shrink on one GPU)")
+    ap.add_argument("--fault-step", type=int, default=None, help="--fault-inject: step at which the worker dies")
     ap.add_argument("--standby", type=int, default=1,
                     help="--fault-inject: warm spare workers kept by the operator (0 = cold respawn)")
-    ap.add_argument("--comm", default=None, choices=["pg", "native", "xgmi", "auto"],
+    ap.add_argument("--comm", default=None, choices=["pg", "native", "xgmi", "auto", "xgmi-only"],
                     help="gradient all-reduce data plane (default $EDL_COMM or pg = ProcessGroupNCCL/RCCL; "
                          "xgmi = hand-written IPC all-reduce; auto = probe both at each epoch, keep the faster)")
     ap.add_argument("--sp", action="store_true", help="Megatron sequence parallelism inside the TP group")

@@ -58,7 +58,7 @@ class Proc:
 
 @dataclass
 class OperatorConfig:
-    gpus: list[int] = field(default_factory=list)       # GPU ordinals this operator may hand out
+    gpus: list[int] = field(default_factory=list)       # GPU ordinals to hand out (repeat = shared slots)
     cpus: list[int] = field(default_factory=list)       # host CPUs to partition (affinity)
     max_restarts: int = 100
     leave_grace_s: float = 30.0
@@ -348,7 +348,9 @@ class ElasticOperator:
         self.events.emit("leave", name=p.name, replaced=replaced)
 
     def _release_gpu(self, p: Proc) -> None:
-        if p.gpu is not None and p.gpu not in self._free_gpus:
+        # cfg.gpus may list an ordinal several times (slots of one shared GPU); a process
+        # gives its slot back once (p.gpu is cleared)
+        if p.gpu is not None:
             self._free_gpus.append(p.gpu)
             self._free_gpus.sort()
             p.gpu = None

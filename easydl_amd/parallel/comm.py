@@ -78,6 +78,17 @@ class Communicator:
             self.data = None
             self.rccl = RcclComm(base, "data", rank, world_size, self.device, timeout_s=timeout_s)
             self.backend = "rccl-native"
+        elif self.device.type == "cuda" and data_backend == "xgmi-only":
+            # the hand-written engine is the ONLY data plane (no RCCL communicator): several
+            # ranks may then share one GPU (RCCL refuses duplicate devices), e.g. to exercise
+            # worker death + shrink on a single MI355X.  broadcast = all-reduce of a buffer
+            # that only the source holds; unsupported dtypes go through the CPU control plane.
+            from easydl_amd.parallel.xgmi import XgmiComm
+            self.data = None
+            self.xgmi = XgmiComm(dist.PrefixStore("xgmi", base), "ws", rank, world_size, self.device,
+                                 timeout_s=timeout_s)
+            self.xgmi_mode = "xgmi"
+            self.backend = "xgmi"
         elif self.device.type == "cuda":
             if data_backend in ("xgmi", "auto") and world_size > 1:
                 # csrc/kernels/xgmi.hip: abortable one-/two-shot all-reduce over IPC-mapped
@@ -103,6 +114,9 @@ class Communicator:
         t0 = time.perf_counter()
         if self.rccl is not None:
             self.all_reduce(torch.zeros(1, device=self.device))
+            torch.cuda.synchronize(self.device)
+        elif self.backend == "xgmi":
+            self.xgmi.all_reduce(torch.zeros(64, device=self.device))
             torch.cuda.synchronize(self.device)
         elif self.data is not None:
             x = torch.zeros(1, device=self.device)
@@ -224,6 +238,8 @@ class Communicator:
                 return self._native(self.xgmi.all_reduce_async, t)
             if op == dist.ReduceOp.MAX:
                 return self._native(self._xgmi_sync, self.xgmi.all_reduce_max, t)
+        if self.backend == "xgmi":
+            return self._xgmi_only_fallback(t, op)
         o = dist.AllreduceOptions()
         o.reduceOp = op
         return self.data.allreduce([t], o)
@@ -239,10 +255,43 @@ class Communicator:
         if self.rccl is not None:
             self._wait(self._native(self.rccl.broadcast_async, t, src))
             return t
+        if self.backend == "xgmi":
+            if self._use_xgmi(t):
+                if self.rank != src:
+                    t.zero_()
+                self._native(self.xgmi.all_reduce, t)   # x + 0 + ... + 0 == x exactly
+                torch.cuda.current_stream(self.device).synchronize()
+                if self.xgmi.status() != 0:
+                    raise CommAborted(f"xGMI broadcast gave up in epoch {self.epoch}")
+                return t
+            h = t.detach().cpu().contiguous()
+            o = dist.BroadcastOptions()
+            o.rootRank = src
+            self._wait(self.ctrl.broadcast([h], o), poll=True)
+            t.copy_(h)
+            return t
         o = dist.BroadcastOptions()
         o.rootRank = src
         self._wait(self.data.broadcast([t], o), poll=True)
         return t
+
+    def _xgmi_only_fallback(self, t: torch.Tensor, op):
+        """xgmi-only data plane, tensor the engine cannot take: pad fp32/bf16 to 16 bytes,
+        anything else through the CPU control plane."""
+        if t.dtype in (torch.float32, torch.bfloat16) and t.is_contiguous() and op == dist.ReduceOp.SUM:
+            n = t.numel()
+            per = 16 // t.element_size()
+            tmp = torch.zeros(-(-n // per) * per, dtype=t.dtype, device=t.device)
+            tmp[:n].copy_(t.view(-1))
+            self._native(self.xgmi.all_reduce, tmp)
+            t.view(-1).copy_(tmp[:n])
+            return _DoneWork()
+        h = t.detach().cpu().contiguous()
+        o = dist.AllreduceOptions()
+        o.reduceOp = op
+        self._wait(self.ctrl.allreduce([h], o), poll=True)
+        t.copy_(h)
+        return _DoneWork()
 
     def _use_xgmi(self, *ts) -> bool:
         return self.xgmi is not None and self.xgmi_mode == "xgmi" and all(self.xgmi.supports(t) for t in ts)

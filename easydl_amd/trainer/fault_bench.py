@@ -41,7 +41,14 @@ def main(args) -> int:
     from easydl_amd.operator.reconciler import ElasticOperator, OperatorConfig
 
     gpus = _gpus()
-    n = max(1, min(args.gpus, len(gpus))) if gpus else max(1, args.gpus)
+    share = bool(getattr(args, "share_gpu", False)) and bool(gpus)
+    if share:
+        # N workers on ONE GPU, the xGMI engine as the only data plane (RCCL refuses two
+        # ranks on one device): worker death -> shrink measured on a single MI355X
+        n = max(1, args.gpus)
+        gpus = [gpus[0]] * n
+    else:
+        n = max(1, min(args.gpus, len(gpus))) if gpus else max(1, args.gpus)
     run_dir = tempfile.mkdtemp(prefix="edl-ttr-", dir=os.environ.get("EDL_TTR_DIR", None))
     job_name = "ttr"
     unlink_job_segments(job_name)
@@ -56,6 +63,10 @@ def main(args) -> int:
     }
     if args.layers:
         env["EDL_BENCH_LAYERS"] = str(args.layers)
+    if share:
+        env["EDL_COMM"] = "xgmi-only"
+    elif getattr(args, "comm", None):
+        env["EDL_COMM"] = args.comm
     job = ElasticJob(name=job_name, command="python -m easydl_amd.trainer.fault_bench --worker",
                      env=env, min_workers=1, max_workers=n)
     jr = JobResource(f"{job_name}-resource", job_name,
@@ -70,9 +81,10 @@ def main(args) -> int:
     out = {
         "metric": "time-to-recover after SIGKILL of one worker (Llama elastic DDP, local operator)",
         "value": None if not ttr else ttr["ttr_s"], "unit": "s", "higher_is_better": False,
-        "n_gpus": n if gpus else 0,
+        "n_gpus": (1 if share else n) if gpus else 0,
         "model": (args.model if not args.layers else f"{args.model}-L{args.layers}") if gpus else "llama-tiny (CPU)",
         "breakdown": ttr, "operator_rc": rc, "hot_standby": getattr(args, "standby", 0),
+        "shared_gpu": share, "comm": env.get("EDL_COMM", "pg"), "workers": n,
         "replacement_from_standby": any(e["kind"] == "spawn" and e.get("standby") for e in ev),
         "restored_from": restored[0].get("source") if restored else None,
         "worlds_seen": sorted({w for w in worlds if w}), "run_dir": run_dir,
