@@ -80,7 +80,12 @@ def main():
     if world != args.gpus and rank == 0:
         print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
     use_cuda = torch.cuda.is_available()
-    dev = torch.device("cuda", local) if use_cuda else torch.device("cpu")
+    dev = torch.device("cuda", 0 if args.share_gpu else local) if use_cuda else torch.device("cpu")
+    if args.share_gpu and use_cuda:
+        # every rank on GPU 0, the xGMI engine as the only data plane (test / fault drills
+        # on a one-GPU box; not the headline configuration)
+        os.environ["EDL_COMM"] = "xgmi-only"
+        os.environ.setdefault("EDL_XGMI_MAX_BLOCKS", "16")   # co-residency of all ranks' grids
     os.environ.setdefault("EDL_JOB", "bench")
     if args.comm:
         os.environ["EDL_COMM"] = args.comm

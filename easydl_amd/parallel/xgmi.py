@@ -18,6 +18,7 @@ Limits: <= 8 ranks (one node), fp32 / bf16, sizes a multiple of 16 bytes
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 
@@ -73,7 +74,13 @@ class XgmiComm:
         self._abort_dev = self._rt("edl_xgmi_ws_abort_dev", h)
         self._status_dev = self._rt("edl_xgmi_ws_status_dev", h)
         self.round = 0
-        self.blocks = min(self._k("edl_xgmi_max_blocks"), 256)
+        # Workgroup b of every rank meets workgroup b of every peer (per-block barrier), so
+        # all ranks' workgroups must be resident together.  One rank per GPU: always true.
+        # Ranks SHARING a GPU (EDL_XGMI_MAX_BLOCKS set by the shared-GPU drills): 4 ranks x
+        # 256 x 512 threads would fill every thread slot of the chip and a late rank's
+        # workgroups could never be dispatched, so the grid is capped.
+        cap = int(os.environ.get("EDL_XGMI_MAX_BLOCKS", 256))
+        self.blocks = max(1, min(self._k("edl_xgmi_max_blocks"), 256, cap))
         self._aborted = False
         self.stream = torch.cuda.Stream(self.device, priority=-1)
 

@@ -65,6 +65,7 @@ def main(args) -> int:
         env["EDL_BENCH_LAYERS"] = str(args.layers)
     if share:
         env["EDL_COMM"] = "xgmi-only"
+        env["EDL_XGMI_MAX_BLOCKS"] = "16"   # all ranks' grids must be co-resident on the one GPU
     elif getattr(args, "comm", None):
         env["EDL_COMM"] = args.comm
     job = ElasticJob(name=job_name, command="python -m easydl_amd.trainer.fault_bench --worker",

@@ -173,3 +173,30 @@ def test_snapshot_skips_the_slot_a_persist_is_reading(tmp_path):
     finally:
         ckpt.close()
         unlink_job_segments("ck")
+
+
+def test_new_layout_segment_is_prepared_off_the_step_path(tmp_path):
+    """After a world change the new shard layout's segment is created (and page-locked
+    on GPU) by a background thread; the snapshot that finds it unprepared is skipped,
+    the next one lands in it."""
+    import types
+    unlink_job_segments("ck")
+    ckpt = CheckpointManager("ck", interval=1)
+    try:
+        a = _trainer(tmp_path, None)
+        a.comm = types.SimpleNamespace(world_size=2, rank=0, epoch=1)
+        a.step = 1
+        ckpt.snapshot(a)                                   # first segment: synchronous
+        assert ckpt.last_snapshot_step == 1 and ckpt._seg_key[0] == 2
+        a.comm = types.SimpleNamespace(world_size=3, rank=0, epoch=2)
+        a.step = 2
+        ckpt.snapshot(a)                                   # w3 segment not ready: skipped
+        assert ckpt.stats.get("skipped") == 1 and ckpt.last_snapshot_step == 1
+        ckpt._prep[2].join(30)
+        a.step = 3
+        ckpt.snapshot(a)
+        assert ckpt.last_snapshot_step == 3 and ckpt._seg_key[0] == 3
+        assert [i["step"] for i in ckpt._seg.committed()] == [3]    # shard 0 of world 3
+    finally:
+        ckpt.close()
+        unlink_job_segments("ck")

@@ -90,3 +90,16 @@ def test_llama_tp2_over_xgmi_matches_dense(cuda, tmp_path, sp, monkeypatch):
         assert r["healthy"]
         assert abs(r["loss_t"] - r["loss_d"]) < 2e-2 * max(1.0, abs(r["loss_d"])), r
         assert r["grad_rel_err"] < 5e-2, r
+
+
+def test_ddp_step_xgmi_only_ranks_sharing_one_gpu(cuda, tmp_path):
+    """bench.py --share-gpu: 2 ranks on GPU 0, the xGMI engine as the only data plane
+    (state broadcast + bucketed gradient all-reduce overlapped with backward)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--share-gpu", "--gpus", "2",
+           "--model", "llama-tiny", "--seq", "256", "--mbs", "1", "--accum", "1", "--steps", "3", "--warmup", "1"]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=240,
+                       env=dict(os.environ, EDL_RUN_DIR=str(tmp_path)))
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert d["n_gpus"] == 2 and d["config"]["comm"] == "xgmi" and d["loss"] == d["loss"]
