@@ -276,6 +276,23 @@ int edl_shm_close(void* h, int unlink_seg) {
 
 int edl_shm_unlink(const char* name) { return shm_unlink(name) == 0 ? 0 : -errno; }
 
+// Re-use an already mapped (and page-locked) segment for another shard layout
+// after a world change: invalidate both slots FIRST (no reader may take the old
+// layout's bytes for the new name), then atomically rename the /dev/shm file
+// (replacing a stale one of that name).  Mappings stay valid across the rename,
+// so the multi-GB hipHostRegister is not repeated.  Returns 0 or -errno.
+int edl_shm_reassign(void* h, const char* new_name) {
+  auto* s = static_cast<Seg*>(h);
+  if (!s || !new_name || new_name[0] != '/') return -EINVAL;
+  for (uint32_t i = 0; i < s->hdr()->nslots; ++i) __atomic_store_n(&s->slot(i)->state, kEmpty, __ATOMIC_RELEASE);
+  __atomic_store_n(&s->hdr()->current, -1, __ATOMIC_RELEASE);
+  msync(s->base, kHdr * (1 + s->hdr()->nslots), MS_SYNC);
+  const std::string from = "/dev/shm" + s->name, to = std::string("/dev/shm") + new_name;
+  if (from != to && rename(from.c_str(), to.c_str()) != 0) return -errno;
+  s->name = new_name;
+  return 0;
+}
+
 }  // extern "C"
 
 // ---------------------------------------------------------------------------

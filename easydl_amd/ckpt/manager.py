@@ -202,7 +202,6 @@ class CheckpointManager:
         self._n = 0
         self._persist_thread = None
         self._persist_slot = None   # slot the persist thread is reading (None: idle)
-        self._prep = None           # (key, bytes, thread, box): segment being prepared off-path
         self._last_slot = None      # slot of the newest snapshot
         self.last_snapshot_step = None
         self.stats = {"snapshots": 0, "d2h_bytes": 0}
@@ -242,45 +241,35 @@ class CheckpointManager:
                 if mk in opt:
                     g.data.copy_(opt[mk])
 
-    def _segment(self, world, shard, need_bytes, pin=True, tag: str = "") -> ShmSegment | None:
-        """The shm segment for this (world, shard, tag) layout, or None while it is being
-        prepared.  The first segment of the process is created synchronously (start-up);
-        after a world change the new one is created and page-locked on a background
-        thread -- hipHostRegister of a multi-GB slot takes seconds, which would otherwise
-        land on the first step after a recovery -- and that one snapshot is skipped."""
+    def _segment(self, world, shard, need_bytes, pin=True, tag: str = "", alloc_bytes: int = 0) -> ShmSegment:
+        """The shm segment for this (world, shard, tag) layout.
+
+        Page-locking a multi-GB slot (hipHostRegister) takes seconds and serialises
+        with the training thread's HIP calls, so after a world change the mapped,
+        pinned segment is re-used whenever it is big enough: its slots are
+        invalidated and the file renamed to the new layout's name
+        (edl_shm_reassign).  The first segment is sized for ``alloc_bytes`` (>= the
+        shard of a world one rank smaller), so a shrink by one rank never re-pins."""
         key = (world, shard, tag)
         if self._seg is not None and self._seg_key == key and self._seg.slot_bytes >= need_bytes:
             return self._seg
         name = self.seg_name(world, shard, tag)
-        if self._seg is None:
-            self._seg = ShmSegment(name, need_bytes, create=True, pin=self.pin and pin)
-            self._seg_key = key
-            return self._seg
-        prep = self._prep
-        if prep is None or prep[0] != key or prep[1] < need_bytes:
-            box: dict = {}
-
-            def make():
-                try:
-                    box["seg"] = ShmSegment(name, need_bytes, create=True, pin=self.pin and pin)
-                except Exception as e:  # noqa: BLE001 - reported when swapped in
-                    box["err"] = e
-            th = threading.Thread(target=make, name=f"edl-shm-prep-{world}-{shard}", daemon=True)
-            th.start()
-            self._prep = (key, need_bytes, th, box)
-            return None
-        key_, _, th, box = prep
-        if th.is_alive():
-            return None
-        self._prep = None
-        if "err" in box:
-            raise box["err"]
-        # nothing may still read or write the mapping we are about to unmap:
-        # the in-flight D2H / committer (wait) and a disk persist (join)
-        self.wait()
-        self._join_persist()
-        self._seg.close()
-        self._seg, self._seg_key = box["seg"], key
+        if self._seg is not None:
+            # nothing may still read or write the mapping while it changes hands:
+            # the in-flight D2H / committer (wait) and a disk persist (join)
+            self.wait()
+            self._join_persist()
+            if self._seg.slot_bytes >= need_bytes:
+                rc = self._seg.rt("edl_shm_reassign", self._seg.h, name.encode())
+                if rc == 0:
+                    self._seg.name, self._seg_key = name, key
+                    self.stats["reassigned"] = self.stats.get("reassigned", 0) + 1
+                    return self._seg
+                log.warning("re-using snapshot segment as %s failed (%d): new segment", name, rc)
+            self._seg.close()
+            self._seg = None
+        self._seg = ShmSegment(name, max(need_bytes, alloc_bytes), create=True, pin=self.pin and pin)
+        self._seg_key = key
         return self._seg
 
     # -- snapshot ------------------------------------------------------------
@@ -299,10 +288,11 @@ class CheckpointManager:
         state = self.state_of(trainer)
         layout, cs_off = shard_layout(state, shard, world)
         self.wait()  # at most one snapshot in flight (and never one across a segment change)
-        seg = self._segment(world, shard, cs_off + 8, pin=state[0][1].is_cuda, tag=tag)
-        if seg is None:   # new layout's segment still being prepared in the background
-            self.stats["skipped"] = self.stats.get("skipped", 0) + 1
-            return
+        alloc = 0
+        if world > 1 and self._seg is None:
+            # headroom: the largest shard of a world one rank smaller (+ alignment slack)
+            alloc = max(shard_layout(state, s, world - 1)[1] for s in range(world - 1)) + 8
+        seg = self._segment(world, shard, cs_off + 8, pin=state[0][1].is_cuda, tag=tag, alloc_bytes=alloc)
         if self._persist_busy_slot(seg):
             # A/B slots: the slot this snapshot would overwrite is still being written to
             # disk (persisting takes longer than two intervals) -> skip rather than tear it
@@ -544,12 +534,6 @@ class CheckpointManager:
     def close(self, unlink: bool = False) -> None:
         self.wait()
         self._join_persist(60)
-        if self._prep is not None:
-            _, _, th, box = self._prep
-            th.join(120)
-            if "seg" in box:
-                box["seg"].close(unlink)
-            self._prep = None
         if self._seg is not None:
             self._seg.close(unlink)
             self._seg = None

@@ -175,28 +175,29 @@ def test_snapshot_skips_the_slot_a_persist_is_reading(tmp_path):
         unlink_job_segments("ck")
 
 
-def test_new_layout_segment_is_prepared_off_the_step_path(tmp_path):
-    """After a world change the new shard layout's segment is created (and page-locked
-    on GPU) by a background thread; the snapshot that finds it unprepared is skipped,
-    the next one lands in it."""
+def test_world_change_reuses_the_pinned_segment(tmp_path):
+    """A shrink by one rank re-uses the (headroom-sized, page-locked) segment under the
+    new layout's name with its slots invalidated: no new mapping, no re-pinning, and
+    no stale old-layout slot visible under the new name."""
+    import os
     import types
     unlink_job_segments("ck")
     ckpt = CheckpointManager("ck", interval=1)
     try:
         a = _trainer(tmp_path, None)
-        a.comm = types.SimpleNamespace(world_size=2, rank=0, epoch=1)
+        a.comm = types.SimpleNamespace(world_size=4, rank=1, epoch=1)
         a.step = 1
-        ckpt.snapshot(a)                                   # first segment: synchronous
-        assert ckpt.last_snapshot_step == 1 and ckpt._seg_key[0] == 2
-        a.comm = types.SimpleNamespace(world_size=3, rank=0, epoch=2)
-        a.step = 2
-        ckpt.snapshot(a)                                   # w3 segment not ready: skipped
-        assert ckpt.stats.get("skipped") == 1 and ckpt.last_snapshot_step == 1
-        ckpt._prep[2].join(30)
-        a.step = 3
         ckpt.snapshot(a)
-        assert ckpt.last_snapshot_step == 3 and ckpt._seg_key[0] == 3
-        assert [i["step"] for i in ckpt._seg.committed()] == [3]    # shard 0 of world 3
+        h0 = ckpt._seg.h
+        assert os.path.exists("/dev/shm/edl-ck-w4-s1")
+        a.comm = types.SimpleNamespace(world_size=3, rank=2, epoch=2)     # renumbered survivor
+        a.step = 2
+        seg = ckpt._segment(3, 2, shard_layout(CheckpointManager.state_of(a), 2, 3)[1] + 8)
+        assert seg.h == h0 and ckpt.stats["reassigned"] == 1
+        assert not os.path.exists("/dev/shm/edl-ck-w4-s1") and os.path.exists("/dev/shm/edl-ck-w3-s2")
+        assert seg.committed() == []                                       # old layout invalidated
+        ckpt.snapshot(a)
+        assert [i["step"] for i in ckpt._seg.committed()] == [2] and ckpt._seg.h == h0
     finally:
         ckpt.close()
         unlink_job_segments("ck")
