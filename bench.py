@@ -146,7 +146,7 @@ def main():
     tokens = (comm.world_size // tp) * B * S * args.accum * args.steps
     tps = tokens / el
     fpt = cfg.flops_per_token(S)
-    tflops_gpu = tps / comm.world_size * fpt / 1e12
+    tflops_gpu = tps / (1 if (args.share_gpu and use_cuda) else comm.world_size) * fpt / 1e12
     metric = "tokens/sec, Llama-3-8B elastic DDP (full train step: fwd+bwd+allreduce+commit+AdamW)"
     if tp > 1:
         metric = f"tokens/sec, {args.model} elastic DP x TP={tp} (full train step)"
@@ -154,7 +154,7 @@ def main():
         "metric": metric,
         "value": round(tps, 2),
         "unit": "tokens/s",
-        "n_gpus": comm.world_size,
+        "n_gpus": 1 if (args.share_gpu and use_cuda) else comm.world_size,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(el / args.steps * 1e3, 3),
@@ -174,6 +174,8 @@ def main():
             "bucket_mb": tr.ddp.bucket_mb,
             "comm": getattr(getattr(comm, "dp", comm), "backend", "local"),
         },
+        "ranks": comm.world_size,
+        "shared_gpu": bool(args.share_gpu and use_cuda),   # functional drill, not a throughput figure
         "allreduce_probe": getattr(getattr(comm, "dp", comm), "xgmi_probe", None),
         "tflops_per_gpu": round(tflops_gpu, 1),
         "mfu_vs_2.5PF": round(tflops_gpu / 2500.0, 4),

@@ -102,4 +102,5 @@ def test_ddp_step_xgmi_only_ranks_sharing_one_gpu(cuda, tmp_path):
                        env=dict(os.environ, EDL_RUN_DIR=str(tmp_path)))
     assert r.returncode == 0, r.stderr[-3000:]
     d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
-    assert d["n_gpus"] == 2 and d["config"]["comm"] == "xgmi" and d["loss"] == d["loss"]
+    assert d["ranks"] == 2 and d["n_gpus"] == 1 and d["shared_gpu"]
+    assert d["config"]["comm"] == "xgmi" and d["loss"] == d["loss"]
