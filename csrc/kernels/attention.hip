@@ -396,9 +396,9 @@ __device__ __forceinline__ void fence_op(bf16x8 (&p)[2][2][2]) {
 // before fmaxf on them).  Its inputs are MFMA results behind fence_d and
 // plain VALU (mask) values -- never a transcendental result: a trans -> VALU
 // read needs a wait state that hipcc does not pad for an asm consumer (an asm
-// v_add after v_exp read the pre-exp value).  Row sums are plain adds; this
-// file is built with -fno-slp-vectorize so they stay scalar (v_pk_add_f32
-// costs ~+22 cycles each beside MFMAs, MI355X_MICROARCH.md).
+// v_add after v_exp read the pre-exp value).  Row sums are plain adds, one
+// query block per soft() call, pinned after it (no adjacent independent chains
+// for hipcc to SLP-pack into v_pk_add_f32, ~+22 cycles each beside MFMAs).
 __device__ __forceinline__ float max3(float a, float b, float c) {
   float r;
   asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));

@@ -61,9 +61,9 @@ def _check_resolves(lib: str) -> None:
         raise RuntimeError(f"{os.path.basename(lib)}: undefined kernel launch stubs: {missing}")
 
 
-# per-source flags: the attention kernels keep f32 softmax adds scalar beside MFMAs
-# (packed v_pk_add_f32 is an anti-lever there, MI355X_MICROARCH.md cycle constants)
-_EXTRA_FLAGS = {"attention.hip": ["-fno-slp-vectorize"]}
+# per-source extra hipcc flags (none at present: -fno-slp-vectorize on attention.hip
+# measured the dK/dV kernel 12 % slower in the bench, profiles/r02_bench_kernel_stats_*)
+_EXTRA_FLAGS: dict[str, list[str]] = {}
 
 
 def build_kernels(force: bool = False, verbose: bool = False) -> str:
