@@ -173,6 +173,7 @@ def main():
             "optimizer": "AdamW fp32 master/moments, clip 1.0",
             "bucket_mb": tr.ddp.bucket_mb,
             "comm": getattr(getattr(comm, "dp", comm), "backend", "local"),
+            "gemm_tuning": getattr(tr, "gemm_tuning", "off"),
         },
         "ranks": comm.world_size,
         "shared_gpu": bool(args.share_gpu and use_cuda),   # functional drill, not a throughput figure

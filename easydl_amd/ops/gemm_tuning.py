@@ -8,30 +8,37 @@ one tuning run of the training step (``EDL_GEMM_TUNING=tune``); every later
 run only reads the file (no tuning time, no GPU search).  GEMMs absent from
 the file fall back to the library heuristic.
 
-EDL_GEMM_TUNING: ``off`` (default), ``use`` (read the shipped file),
-``tune`` (search every GEMM met and write the file at exit).
+EDL_GEMM_TUNING: ``select`` (default: read the curated file, the
+selections verified to speed up the whole step), ``use`` (read the full
+round-1 file), ``tune`` (search every GEMM met and write the file at exit),
+``off`` (library heuristics only).
 
-Measured (profiles/r01_gemm_tuning_ab.jsonl): per GEMM the tuned selections
-are faster in TunableOp's isolated timing (lm_head 11.2 -> 8.5-9.1 ms, qkv
-0.65 -> 0.53 ms), yet the full Llama-3-8B step ran 19,295 tokens/s with them
-vs 19,496 without — so the library heuristics stay the default.
+Measured (profiles/r01_gemm_tuning_ab.jsonl): per GEMM the full set of tuned
+selections is faster in TunableOp's isolated timing (lm_head 11.2 -> 8.5-9.1
+ms, qkv 0.65 -> 0.53 ms), yet the full Llama-3-8B step ran 19,295 tokens/s
+with them vs 19,496 without.  The curated file holds only the down-projection
+weight gradient (dY^T [4096, M] @ h [M, 14336], M = 16384), the one GEMM the
+heuristic runs at 1.13 PF/s: hipBLASLt solution 618613 takes it from 1.71 to
+1.31 ms (scripts/gemm_wgrad_probe.py, profiles/r02_gemm_wgrad_probe.jsonl).
 """
 from __future__ import annotations
 
 import atexit
 import logging
 import os
+import tempfile
 
 log = logging.getLogger(__name__)
-TUNED_FILE = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tuned",
-                          "tunableop_gfx950.csv")
+_TUNED_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tuned")
+TUNED_FILE = os.path.join(_TUNED_DIR, "tunableop_gfx950.csv")
+SELECT_FILE = os.path.join(_TUNED_DIR, "tunableop_gfx950_select.csv")
 
 
 def apply(mode: str | None = None, path: str | None = None) -> str:
     """Configure TunableOp for this process; returns the mode in effect."""
     import torch
-    mode = mode or os.environ.get("EDL_GEMM_TUNING", "off")
-    path = path or TUNED_FILE
+    mode = mode or os.environ.get("EDL_GEMM_TUNING", "select")
+    path = path or (SELECT_FILE if mode == "select" else TUNED_FILE)
     if mode == "off" or not torch.cuda.is_available():
         return "off"
     import torch.cuda.tunable as tun
@@ -48,10 +55,12 @@ def apply(mode: str | None = None, path: str | None = None) -> str:
         return "off"
     tun.enable(True)
     tun.tuning_enable(False)
-    tun.set_filename(path)
+    # TunableOp writes its results at exit even with tuning off: point that at a
+    # scratch file, never at the shipped one (or the working directory's default)
+    tun.set_filename(os.path.join(tempfile.gettempdir(), f"edl_tunableop_{os.getpid()}_%d.csv"))
     ok = tun.read_file(path)
     if not ok:
         log.warning("TunableOp results %s not loaded (validator mismatch?): library heuristics", path)
         tun.enable(False)
         return "off"
-    return "use"
+    return mode

@@ -50,3 +50,18 @@ def test_gemm_tuning_is_off_without_a_gpu(monkeypatch):
     monkeypatch.setenv("EDL_GEMM_TUNING", "use")
     assert gemm_tuning.apply() == "off"          # CPU tier: no TunableOp, no file needed
     assert gemm_tuning.TUNED_FILE.endswith("tunableop_gfx950.csv")
+
+
+def test_gemm_tuning_select_file_is_curated(monkeypatch):
+    """The default mode reads the curated selections: validators of this image plus only
+    hipBLASLt entries (each one vetted end to end, profiles/r02_gemm_select_ab.txt)."""
+    from easydl_amd.ops import gemm_tuning
+    monkeypatch.delenv("EDL_GEMM_TUNING", raising=False)
+    assert gemm_tuning.apply() == "off"          # no GPU here
+    lines = open(gemm_tuning.SELECT_FILE).read().splitlines()
+    vals = {ln.split(",")[1]: ln.split(",")[2] for ln in lines if ln.startswith("Validator,")}
+    assert vals["GCN_ARCH_NAME"].startswith("gfx950") and "PT_VERSION" in vals
+    entries = [ln.split(",") for ln in lines if not ln.startswith("Validator,")]
+    assert entries and all(e[0].startswith("GemmTunableOp_BFloat16") and e[2].startswith("Gemm_Hipblaslt")
+                           for e in entries)
+    assert any(e[1] == "tn_14336_4096_16384_ld_16384_16384_14336" for e in entries)   # down-proj wgrad
