@@ -38,7 +38,7 @@ def apply(mode: str | None = None, path: str | None = None) -> str:
     """Configure TunableOp for this process; returns the mode in effect."""
     import torch
     mode = mode or os.environ.get("EDL_GEMM_TUNING", "select")
-    path = path or (SELECT_FILE if mode == "select" else TUNED_FILE)
+    path = path or os.environ.get("EDL_GEMM_TUNING_FILE") or (SELECT_FILE if mode == "select" else TUNED_FILE)
     if mode == "off" or not torch.cuda.is_available():
         return "off"
     import torch.cuda.tunable as tun
