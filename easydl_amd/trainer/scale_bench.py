@@ -41,16 +41,25 @@ def main(argv=None) -> int:
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--scale-step", type=int, default=10)
     ap.add_argument("--batch", type=int, default=256, help="per-worker images per step")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="every worker on GPU 0 with the xGMI engine as the only data plane (RCCL refuses "
+                         "two ranks on one device): the scale-up path measured on a single MI355X")
     a = ap.parse_args(argv)
     from easydl_amd.api.spec import ElasticJob, JobResource, Resource, RoleResource
     from easydl_amd.operator.reconciler import ElasticOperator, OperatorConfig
     gpus = _gpus()
+    share = a.share_gpu and bool(gpus)
+    if share:
+        gpus = [gpus[0]] * a.end
     end = min(a.end, len(gpus)) if gpus else a.end
     run_dir = tempfile.mkdtemp(prefix="edl-scale-", dir=os.environ.get("EDL_SCALE_DIR", None))
     cpu_batch = 4
     per = a.batch if gpus else cpu_batch
     gb = per * end   # global batch fixed across the resize: 1 worker accumulates end micro-batches
     env = {"EDL_SCALE_STEPS": str(a.steps), "EDL_SCALE_BATCH": str(per), "EDL_SCALE_GB": str(gb)}
+    if share:
+        env["EDL_COMM"] = "xgmi-only"
+        env["EDL_XGMI_MAX_BLOCKS"] = "16"   # all ranks' engine grids must be co-resident on the one GPU
     job = ElasticJob(name="scale", command="python -m easydl_amd.trainer.scale_bench --worker", env=env,
                      min_workers=1, max_workers=end)
     jr = JobResource("scale-resource", "scale", {"worker": RoleResource(a.start, Resource(gpu=1 if gpus else 0,
@@ -92,6 +101,8 @@ def main(argv=None) -> int:
     new_world = lambda e: e.get("world") == end  # noqa: E731
     out = {"metric": "elastic scale-up mid-run (ResNet-50 bf16 DDP)" if gpus else "elastic scale-up (CPU ResNet)",
            "start": a.start, "end": end, "global_batch": gb, "images_per_s_by_world": ips, "operator_rc": rc,
+           "n_gpus": (1 if share else end) if gpus else 0, "shared_gpu": share,
+           "comm": env.get("EDL_COMM", os.environ.get("EDL_COMM", "pg")),
            "scale_up_s": {"spawn": first("spawn", lambda e: e.get("role") == "worker"), "joined": first("joined"),
                           "epoch_formed": first("epoch_formed", new_world),
                           "comm_ready": first("comm_ready", new_world),
