@@ -113,6 +113,7 @@ class ElasticTrainer:
         self._store = store
         self._manager = None
         self._watchdog = None
+        self._prejoin = None   # fit(): warm-up run by a process joining a running job
         self._stop = threading.Event()
         self.fault = fault.FaultInjector.from_env(self.ctx, self.events)
         self.history: list[dict] = []
@@ -174,8 +175,38 @@ class ElasticTrainer:
         info = {"index": self.ctx.index, "role": self.ctx.role, "gpu": self.ctx.gpu}
         self.rdzv = RendezvousClient(self.kv, self.ctx.node_id, info)
         self.metrics.kv, self.metrics.node = self.kv, self.ctx.node_id
+        if self._prejoin is not None and self._job_is_running():
+            self._prejoin()
         self.rdzv.join()
         self.events.emit("joined", node=self.ctx.node_id)
+
+    def _job_is_running(self) -> bool:
+        """A live epoch exists: this process is a scale-up joiner or a replacement beside
+        survivors (not part of the initial cohort, not a restore with nobody left)."""
+        e = self.rdzv.latest_epoch()
+        return e > 0 and not self.rdzv.aborted(e) and not self.kv.exists("train/done")
+
+    def _prejoin_warmup(self, loss_fn, data, plan) -> None:
+        """One local forward + backward on this process's own (not yet synced) weights
+        BEFORE it announces itself.  A fresh process's first iteration loads every
+        kernel (MIOpen convolutions, hipBLASLt, our extensions) and grows the caching
+        allocator: measured 1.5 s for ResNet-50 joiners, during which the running world
+        stalled in its first collective with them (profiles/r02_scale_up_resnet50_*).
+        Here the running world keeps training meanwhile.  No communicator exists yet,
+        so no collective is issued; the gradients are discarded."""
+        if self.model is None or self.tp > 1:
+            return
+        t0 = time.perf_counter()
+        idx = plan.indices(0, 0, 1)[0]
+        self.flat.zero_grad()
+        loss = loss_fn(self.model, data.batch(idx, self.device))
+        loss.backward()
+        # every real step starts with zero_grad(): fresh gradient window and a new weight
+        # generation, so transposed-weight caches built from these random weights are dropped
+        self.flat.zero_grad()
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        self.events.emit("prejoin_warmup", s=round(time.perf_counter() - t0, 4))
 
     def _start_watchdog(self):
         def loop():
@@ -418,6 +449,8 @@ class ElasticTrainer:
             gb = w * self.micro_batch
             self.global_batch = gb
         plan = ElasticBatchPlan(len(data), gb, self.micro_batch, seed=17)
+        if os.environ.get("EDL_PREJOIN_WARMUP", "1") != "0":
+            self._prejoin = lambda: self._prejoin_warmup(loss_fn, data, plan)
         self._connect()
         self._start_watchdog()
         try:

@@ -126,6 +126,10 @@ def test_scale_up_joiner_receives_state(tmp_path):
         assert r[0]["hash"] == r[1]["hash"] == r[2]["hash"]
         assert 3 in r[0]["worlds"], r[0]["worlds"]
         assert r[2]["step"] == 30
+        # only the process joining a running job warms up before announcing itself
+        from easydl_amd.utils.events import read_events
+        warm = {e.get("proc") for e in read_events(str(tmp_path)) if e["kind"] == "prejoin_warmup"}
+        assert warm == {"worker2"}, warm
     finally:
         m.terminate()
 
