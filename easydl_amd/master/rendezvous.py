@@ -54,6 +54,7 @@ class RendezvousConfig:
     policy: str = "shrink"          # on failure: "shrink" (continue with survivors) or "replace" (wait)
     replace_wait_s: float = 60.0    # "replace": how long to wait for a replacement before shrinking
     granule: int = 1                # world sizes are multiples of this (the TP degree)
+    arrive_timeout_s: float = 30.0  # scale-up waits this long at most for processes still warming up
 
 
 class JobFinished(Exception):
@@ -95,6 +96,19 @@ class RendezvousManager:
     def members(self) -> list[str]:
         a = self.assignment(self.epoch())
         return list(a["members"]) if a else []
+
+    def arriving(self, joined: list[str], now: float) -> list[str]:
+        """Processes that announced themselves (RendezvousClient.arriving) and are still
+        warming up: not joined, not dead, announced less than arrive_timeout_s ago."""
+        raw = self.kv.get_str("rdzv/arriving", "") or ""
+        out = []
+        for n in dict.fromkeys(x for x in raw.split(",") if x):
+            if n in joined or self.kv.exists(f"ev/dead/{n}") or self.kv.exists(f"ev/exit/{n}"):
+                continue   # joined already, or died while starting (supervisor exit event)
+            ts = self.kv.get(f"rdzv/arrive_ts/{n}")
+            if ts is not None and now - float(ts) < self.cfg.arrive_timeout_s:
+                out.append(n)
+        return out
 
     def mark_dead(self, node: str, reason: str) -> None:
         if not self.kv.exists(f"ev/dead/{node}"):
@@ -173,7 +187,12 @@ class RendezvousManager:
         elif waiting and len(members) < max_n and min(max_n, len(members) + len(waiting)) // g * g > len(members):
             if self._first_wait_ts is None:
                 self._first_wait_ts = now
-            if len(members) + len(waiting) >= max_n or now - self._first_wait_ts >= self.cfg.join_window_s:
+            # Every re-formation pauses the running world, so joiners of one scale event
+            # are admitted together: hold while announced processes are still warming up
+            # (they keep their arrive_ts fresh only until arrive_timeout_s).
+            coming = len(self.arriving(joined, now)) if len(members) + len(waiting) < max_n else 0
+            if len(members) + len(waiting) >= max_n or (now - self._first_wait_ts >= self.cfg.join_window_s
+                                                        and not coming):
                 reason = "scale_up"
         else:
             self._first_wait_ts = None
@@ -258,6 +277,12 @@ class RendezvousClient:
         self._hb = None
         self.epoch = 0
         self.plan_version = 0
+
+    def arriving(self) -> None:
+        """Announce this process before its pre-join warm-up: the master then admits it
+        together with the other joiners of the same scale event (one re-formation)."""
+        self.kv.set(f"rdzv/arrive_ts/{self.node_id}", str(time.time()))
+        self.kv.append("rdzv/arriving", self.node_id + ",")
 
     def join(self) -> None:
         self.kv.set(f"rdzv/info/{self.node_id}", json.dumps(dict(self.info, pid=os.getpid(),

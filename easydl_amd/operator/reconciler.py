@@ -235,7 +235,20 @@ class ElasticOperator:
         p.cpus = cpus
         self.procs[name] = p
         self.events.emit("spawn", name=name, pid=pid, role=role, gpu=gpu, gen=generation, resource=res.to_dict())
+        self._announce_arrival(p)
         return p
+
+    def _announce_arrival(self, p: Proc) -> None:
+        """Tell the rendezvous that a worker is starting (RendezvousManager.arriving): the
+        master then admits all joiners of one scale event in ONE re-formation, even when
+        their start-up and pre-join warm-up finish at different times."""
+        if p.role != "worker" or self.kv is None:
+            return
+        try:
+            self.kv.set(f"rdzv/arrive_ts/{p.node_id}", str(time.time()))
+            self.kv.append("rdzv/arriving", p.node_id + ",")
+        except Exception as e:  # the store is best effort here: the join window still applies
+            log.debug("arrival announcement for %s failed: %s", p.node_id, e)
 
     # ------------------------------------------------------------- hot standby
     def _maintain_standbys(self) -> None:
@@ -289,6 +302,7 @@ class ElasticOperator:
             self.procs[name] = p
             self.events.emit("spawn", name=name, pid=sp.pid, role=role, gpu=gpu, gen=generation,
                              resource=res.to_dict(), standby=sname)
+            self._announce_arrival(p)
             return p
         return None
 

@@ -109,20 +109,26 @@ class Communicator:
         self.init_s = time.perf_counter() - t0
 
     # -- lifecycle -----------------------------------------------------------
+    def _sync_stream(self) -> None:
+        """Host-wait for this rank's compute stream, which every collective is ordered
+        into.  Never torch.cuda.synchronize(): that also waits for an in-flight snapshot
+        copy on the checkpoint engine's stream, on the recovery path."""
+        torch.cuda.current_stream(self.device).synchronize()
+
     def warmup(self) -> float:
         """Force lazy communicator creation now (so it is not hidden in step 1)."""
         t0 = time.perf_counter()
         if self.rccl is not None:
             self.all_reduce(torch.zeros(1, device=self.device))
-            torch.cuda.synchronize(self.device)
+            self._sync_stream()
         elif self.backend == "xgmi":
             self.xgmi.all_reduce(torch.zeros(64, device=self.device))
-            torch.cuda.synchronize(self.device)
+            self._sync_stream()
         elif self.data is not None:
             x = torch.zeros(1, device=self.device)
             self.data.allreduce([x]).wait()
             if self.device.type == "cuda":
-                torch.cuda.synchronize(self.device)
+                self._sync_stream()
         self.ctrl.allreduce([torch.zeros(1)]).wait()
         if self.xgmi is not None and self.xgmi_mode == "auto":
             self._probe_xgmi()
@@ -139,18 +145,18 @@ class Communicator:
         self.data.allreduce([a]).wait()
         keep_timeout, self.xgmi.timeout_s = self.xgmi.timeout_s, 5.0  # a broken path gives up fast
         self.xgmi.all_reduce(b)
-        torch.cuda.synchronize(self.device)
+        self._sync_stream()
         self.xgmi.timeout_s = keep_timeout
         bad = 0.0 if (torch.equal(a, b) and self.xgmi.status() == 0) else 1.0
 
         def timed(fn):
             t = src.clone()
             fn(t)
-            torch.cuda.synchronize(self.device)
+            self._sync_stream()
             t0 = time.perf_counter()
             for _ in range(iters):
                 fn(t)
-            torch.cuda.synchronize(self.device)
+            self._sync_stream()
             return (time.perf_counter() - t0) / iters
 
         t_rccl = timed(lambda t: self.data.allreduce([t]).wait())
@@ -164,7 +170,7 @@ class Communicator:
             self.xgmi_mode = "xgmi"
             self.backend = "rccl+xgmi"
         else:
-            torch.cuda.synchronize(self.device)
+            self._sync_stream()
             self.xgmi.close()
             self.xgmi = None
 

@@ -229,7 +229,12 @@ class XgmiComm:
                 and (t.numel() * t.element_size()) % 16 == 0)
 
     def close(self) -> None:
+        """Free the workspace.  Called after a committed step, when every rank has synced its
+        streams, so no engine kernel is in flight anywhere.  Only this engine's stream is
+        drained: a device-wide sync would also wait for an in-flight snapshot copy (up to
+        ~0.5 s at a world change, profiles/r02_ttr_rejoin_*)."""
         if self._ws is not None:
-            torch.cuda.synchronize(self.device)
+            torch.cuda.current_stream(self.device).synchronize()
+            self.stream.synchronize()
             self._rt("edl_xgmi_ws_destroy", self._ws)
             self._ws = None

@@ -176,6 +176,7 @@ class ElasticTrainer:
         self.rdzv = RendezvousClient(self.kv, self.ctx.node_id, info)
         self.metrics.kv, self.metrics.node = self.kv, self.ctx.node_id
         if self._prejoin is not None and self._job_is_running():
+            self.rdzv.arriving()
             self._prejoin()
         self.rdzv.join()
         self.events.emit("joined", node=self.ctx.node_id)
@@ -337,16 +338,30 @@ class ElasticTrainer:
         need = int(c.ctrl_all_reduce([differ], dist.ReduceOp.MAX)[0])
         if need or max_step < 0:
             t0 = time.time()
+            holder = not self.needs_state and self.step == max_step
+            self._fence_snapshot_before_overwrite(c, src_rank, holder)
             for t in self._state_tensors():
                 c.broadcast(t, src_rank)
             scal = c.ctrl_broadcast([self.step, self.opt.step_count], src_rank)
             self.step = int(scal[0])
             self.opt.step_count = int(scal[1])
             if self.device.type == "cuda":
-                torch.cuda.synchronize(self.device)
+                torch.cuda.current_stream(self.device).synchronize()
             nbytes = sum(t.numel() * t.element_size() for t in self._state_tensors())
             self.events.emit("state_broadcast", src=src_rank, bytes=nbytes, s=round(time.time() - t0, 4))
         self.needs_state = False
+
+    def _fence_snapshot_before_overwrite(self, c, src: int, holder: bool) -> None:
+        """A state broadcast rewrites this rank's buffers unless it is the source, or a
+        holder of the same step receiving identical bytes over RCCL.  The xGMI-only
+        broadcast zero-fills non-source ranks first.  If the buffers will change, the
+        in-flight snapshot D2H (which reads them on the checkpoint engine's stream) must
+        finish first, or its slot would mix old and new bytes under the old checksum.
+        The fence is a stream wait, not a host block."""
+        if self.checkpoint is None or self.device.type != "cuda" or c.rank == src:
+            return
+        if not holder or getattr(c, "backend", "") == "xgmi":
+            self.checkpoint.fence()
 
     def _sync_state_tp(self):
         """DP x TP state agreement.  Each TP rank's shard is replicated over its
@@ -367,12 +382,13 @@ class ElasticTrainer:
             if c.dp.world_size > 1 and int(c.dp.ctrl_all_reduce([1 - mine_ok], dist.ReduceOp.MAX)[0]):
                 src = int(c.dp.ctrl_all_reduce([c.dp.rank if mine_ok else 1 << 30], dist.ReduceOp.MIN)[0])
                 t0 = time.time()
+                self._fence_snapshot_before_overwrite(c.dp, src, bool(mine_ok))
                 for ten in self._state_tensors():
                     c.dp.broadcast(ten, src)
                 scal = c.dp.ctrl_broadcast([self.step, self.opt.step_count], src)
                 self.step, self.opt.step_count = int(scal[0]), int(scal[1])
                 if self.device.type == "cuda":
-                    torch.cuda.synchronize(self.device)
+                    torch.cuda.current_stream(self.device).synchronize()
                 self.events.emit("state_broadcast", src=src, group="dp", tp_rank=t, s=round(time.time() - t0, 4))
         else:
             mine = self.checkpoint.latest_step(self) if self.checkpoint is not None else -1

@@ -1,5 +1,6 @@
-"""Training pause of the running world across a scale-up, from an event timeline:
-last step at the old world size -> first step at the new one (worker0's view)."""
+"""Training pauses of the running world across world-size changes, from an event
+timeline: last step at the old size -> first step at the new one (worker0's view).
+Prints the first change (``pause``) and every change (``changes``)."""
 import glob
 import json
 import os
@@ -16,14 +17,15 @@ def pause(run_dir: str) -> dict:
                 pass
     ev.sort(key=lambda e: e["ts"])
     done = [e for e in ev if e["kind"] == "step_done" and e.get("proc") == "worker0"]
+    warm = [e.get("s") for e in ev if e["kind"] == "prejoin_warmup"]
+    out = []
     for a, b in zip(done, done[1:]):
         if b.get("world") != a.get("world"):
-            steady = [y["ts"] - x["ts"] for x, y in zip(done, done[1:]) if x.get("world") == y.get("world") == b["world"]]
-            warm = [e.get("s") for e in ev if e["kind"] == "prejoin_warmup"]
-            return {"from_world": a["world"], "to_world": b["world"], "pause_s": round(b["ts"] - a["ts"], 3),
-                    "steady_step_s_new_world": round(sorted(steady)[len(steady) // 2], 3) if steady else None,
-                    "prejoin_warmup_s": warm}
-    return {}
+            steady = [y["ts"] - x["ts"] for x, y in zip(done, done[1:])
+                      if x.get("world") == y.get("world") == b["world"]]
+            out.append({"from_world": a["world"], "to_world": b["world"], "pause_s": round(b["ts"] - a["ts"], 3),
+                        "steady_step_s_new_world": round(sorted(steady)[len(steady) // 2], 3) if steady else None})
+    return dict(out[0], prejoin_warmup_s=warm, changes=out) if out else {}
 
 
 if __name__ == "__main__":

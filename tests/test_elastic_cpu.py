@@ -126,10 +126,12 @@ def test_scale_up_joiner_receives_state(tmp_path):
         assert r[0]["hash"] == r[1]["hash"] == r[2]["hash"]
         assert 3 in r[0]["worlds"], r[0]["worlds"]
         assert r[2]["step"] == 30
-        # only the process joining a running job warms up before announcing itself
+        # a process joining a running job warms up before announcing itself; whichever of
+        # the two initial workers formed the first (world-1) epoch never does (the other
+        # may have found that epoch running, depending on start-up timing)
         from easydl_amd.utils.events import read_events
         warm = {e.get("proc") for e in read_events(str(tmp_path)) if e["kind"] == "prejoin_warmup"}
-        assert warm == {"worker2"}, warm
+        assert "worker2" in warm and len(warm & {"worker0", "worker1"}) <= 1, warm
     finally:
         m.terminate()
 
