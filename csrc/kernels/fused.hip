@@ -432,6 +432,53 @@ __global__ __launch_bounds__(256) void transpose_bf16_reg_kernel(const bf16_t* _
   for (int j = 0; j < 8; ++j) *reinterpret_cast<u32x4*>(dst + (int64_t)(c + j) * R + r) = out[j];
 }
 
+// Transpose + column sums of src (the bias gradient of a linear layer is the column
+// sum of dY, whose transpose the NT weight-gradient GEMM needs anyway): each thread
+// sums its 8x8 block's columns, the 16 row groups of a 128x128 tile meet in LDS, and
+// the tile writes one row of a [R/128, C] fp32 slab that edl_colsum reduces
+// (deterministic, no float atomics).
+__global__ __launch_bounds__(256) void transpose_colsum_bf16_kernel(const bf16_t* __restrict__ src,
+                                                                    bf16_t* __restrict__ dst,
+                                                                    float* __restrict__ partial, int R, int C) {
+  __shared__ float red[16][RT + 4];
+  int r, c;
+  block8_origin(r, c);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int rg = (w >> 1) * 8 + (lane >> 3), c0 = ((w & 1) * 8 + (lane & 7)) * 8;
+  const bool live = r < R && c < C;   // R, C multiples of 8: a block is all in or all out
+  float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (live) {
+    u32x4 in[8], out[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      in[i] = *reinterpret_cast<const u32x4*>(src + (int64_t)(r + i) * C + c);
+      float f[8];
+      unpack8(in[i], f);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) cs[k] += f[k];
+    }
+    transpose8x8(in, out);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) *reinterpret_cast<u32x4*>(dst + (int64_t)(c + j) * R + r) = out[j];
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) red[rg][c0 + k] = cs[k];
+  __syncthreads();
+  if (threadIdx.x < RT) {
+    // this tile's column origin and row-tile index (block8_origin's mapping, lane-independent part)
+    const int gx = gridDim.x, gy = gridDim.y;
+    const int b = blockIdx.x + gx * blockIdx.y;
+    const int ty = b % gy, tx = (b / gy + ty) % gx;
+    const int col = tx * RT + threadIdx.x;
+    if (col < C) {
+      float t = 0.f;
+#pragma unroll
+      for (int g = 0; g < 16; ++g) t += red[g][threadIdx.x];
+      partial[(int64_t)ty * C + col] = t;
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void swiglu_fwd_t_reg_kernel(const bf16_t* __restrict__ gu, bf16_t* __restrict__ h,
                                                                bf16_t* __restrict__ hT, int M, int F) {
   int r, c;
@@ -591,6 +638,17 @@ int edl_transpose_bf16(const void* src, void* dst, int R, int C, hipStream_t s) 
   EDL_LAUNCH_CHECK();
   return 0;
 }
+
+// dst = src^T and partial[R/128 (rounded up), C] = per-row-tile column sums of src (fp32)
+int edl_transpose_colsum_bf16(const void* src, void* dst, float* partial, int R, int C, hipStream_t s) {
+  if (R % 8 || C % 8 || R <= 0 || C <= 0) return (int)hipErrorInvalidValue;
+  dim3 grid((C + RT - 1) / RT, (R + RT - 1) / RT);
+  transpose_colsum_bf16_kernel<<<grid, 256, 0, s>>>((const bf16_t*)src, (bf16_t*)dst, partial, R, C);
+  EDL_LAUNCH_CHECK();
+  return 0;
+}
+
+int edl_transpose_tiles(int R) { return (R + RT - 1) / RT; }
 
 int edl_transpose_bf16_lds(const void* src, void* dst, int R, int C, hipStream_t s) {
   if (R % 8 || C % 8 || R <= 0 || C <= 0) return (int)hipErrorInvalidValue;

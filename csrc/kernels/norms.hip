@@ -122,7 +122,27 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(const bf16_t* __restrict_
     for (int k = 0; k < 8; ++k) { accw[c][k] = 0.f; accb[c][k] = 0.f; wf[c][k] = 0.f; }
     if (ch < nchunk) unpack8(reinterpret_cast<const u32x4*>(w)[ch], wf[c]);
   }
+  // Each workgroup sweeps rows with two block reductions per row: the next row's
+  // dy / x / dres are loaded into registers before the current row's reductions, so
+  // the HBM latency overlaps them (the sweep was latency-bound at ~2-4 TB/s).
+  u32x4 nd[NC], nx[NC], nr[NC];
+  auto fetch = [&](int r) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int ch = threadIdx.x + c * blockDim.x;
+      if (ch < nchunk) {
+        nd[c] = reinterpret_cast<const u32x4*>(dy + (int64_t)r * cols)[ch];
+        nx[c] = reinterpret_cast<const u32x4*>(x + (int64_t)r * cols)[ch];
+        if (dres) nr[c] = reinterpret_cast<const u32x4*>(dres + (int64_t)r * cols)[ch];
+      }
+    }
+  };
+  if (blockIdx.x < rows) fetch(blockIdx.x);
   for (int row = blockIdx.x; row < rows; row += gridDim.x) {
+    u32x4 cd[NC], cx[NC], cr[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) { cd[c] = nd[c]; cx[c] = nx[c]; cr[c] = nr[c]; }
+    if (row + (int)gridDim.x < rows) fetch(row + gridDim.x);
     const float rstd = rstd_in[row];
     const float mean = LN ? mean_in[row] : 0.f;
     float xh[NC][8], g[NC][8];
@@ -132,8 +152,8 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(const bf16_t* __restrict_
       const int ch = threadIdx.x + c * blockDim.x;
       if (ch < nchunk) {
         float d[8];
-        unpack8(reinterpret_cast<const u32x4*>(dy + (int64_t)row * cols)[ch], d);
-        unpack8(reinterpret_cast<const u32x4*>(x + (int64_t)row * cols)[ch], xh[c]);
+        unpack8(cd[c], d);
+        unpack8(cx[c], xh[c]);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           xh[c][k] = (xh[c][k] - mean) * rstd;
@@ -159,7 +179,7 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(const bf16_t* __restrict_
         for (int k = 0; k < 8; ++k) o[k] = rstd * (g[c][k] - m_g - xh[c][k] * m_gx);
         if (dres) {
           float r[8];
-          unpack8(reinterpret_cast<const u32x4*>(dres + (int64_t)row * cols)[ch], r);
+          unpack8(cr[c], r);
 #pragma unroll
           for (int k = 0; k < 8; ++k) o[k] += r[k];
         }
@@ -257,7 +277,14 @@ extern "C" {
 int edl_norm_max_cols() { return 256 * 8 * kMaxNC; }
 
 // Number of row-sweeping workgroups the backward uses (size of the partial slab).
-int edl_norm_bwd_groups(int rows) { return rows < 512 ? (rows > 0 ? rows : 1) : 512; }
+// Sweeping workgroups: 1024 for rows narrower than 4096 (BERT-large d = 1024: 2 waves
+// per workgroup, 512 left the sweep latency-bound: 73 -> 40 us), 512 at d >= 4096 where
+// the sweep is already 4 waves wide and a bigger [G, cols] slab costs colsum more than
+// it saves (profiles/r02_norm_kernels.txt).
+int edl_norm_bwd_groups(int rows, int cols) {
+  const int g = cols >= 4096 ? 512 : 1024;
+  return rows < g ? (rows > 0 ? rows : 1) : g;
+}
 
 int edl_rmsnorm_fwd(const void* x, const void* res, void* sum_out, const void* w, void* y, float* rstd, int rows,
                     int cols, float eps, hipStream_t s) {
@@ -275,7 +302,7 @@ int edl_layernorm_fwd(const void* x, const void* res, void* sum_out, const void*
 int edl_rmsnorm_bwd(const void* dy, const void* x, const void* w, const float* rstd, const void* dres, void* dx,
                     float* partial_w, int rows, int cols, hipStream_t s) {
   return launch_bwd<false>((const bf16_t*)dy, (const bf16_t*)x, (const bf16_t*)w, nullptr, rstd,
-                           (const bf16_t*)dres, (bf16_t*)dx, partial_w, nullptr, edl_norm_bwd_groups(rows), rows,
+                           (const bf16_t*)dres, (bf16_t*)dx, partial_w, nullptr, edl_norm_bwd_groups(rows, cols), rows,
                            cols, s);
 }
 
@@ -283,7 +310,7 @@ int edl_layernorm_bwd(const void* dy, const void* x, const void* w, const float*
                       const void* dres, void* dx, float* partial_w, float* partial_b, int rows, int cols,
                       hipStream_t s) {
   return launch_bwd<true>((const bf16_t*)dy, (const bf16_t*)x, (const bf16_t*)w, mean, rstd, (const bf16_t*)dres,
-                          (bf16_t*)dx, partial_w, partial_b, edl_norm_bwd_groups(rows), rows, cols, s);
+                          (bf16_t*)dx, partial_w, partial_b, edl_norm_bwd_groups(rows, cols), rows, cols, s);
 }
 
 int edl_colsum(const float* partial, int G, int cols, void* out, int odt, int accumulate, hipStream_t s) {

@@ -39,7 +39,7 @@ _KERNEL_SIGS = {
     "edl_sumsq_partial": [c_void_p, c_int, c_i64, c_void_p, c_void_p],
     "edl_clip_finalize": [c_void_p, c_int, c_float, c_float, c_void_p, c_void_p],
     "edl_norm_max_cols": [],
-    "edl_norm_bwd_groups": [c_int],
+    "edl_norm_bwd_groups": [c_int, c_int],
     "edl_rmsnorm_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_void_p],
     "edl_layernorm_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                           c_int, c_float, c_void_p],
@@ -58,6 +58,8 @@ _KERNEL_SIGS = {
     "edl_xent_fwd_bwd": [c_void_p, c_void_p, c_void_p, c_i64, c_int, c_i64, c_int, c_void_p],
     "edl_scale_bf16": [c_void_p, c_i64, c_void_p, c_float, c_void_p],
     "edl_transpose_bf16": [c_void_p, c_void_p, c_int, c_int, c_void_p],
+    "edl_transpose_colsum_bf16": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],
+    "edl_transpose_tiles": [c_int],
     "edl_transpose_bf16_lds": [c_void_p, c_void_p, c_int, c_int, c_void_p],
     "edl_swiglu_fwd_t_lds": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],
     "edl_swiglu_bwd_t_lds": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],

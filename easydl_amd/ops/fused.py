@@ -254,6 +254,19 @@ def _transposed(t: torch.Tensor) -> torch.Tensor:
     return out
 
 
+def _transposed_colsum(t: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor, int]:
+    """(t^T, [G, cols] fp32 column-sum partials, G) in one pass over t: the bias gradient
+    rides on the transpose the NT weight-gradient GEMM needs anyway."""
+    t = t.contiguous()
+    k = _native.kernels()
+    out = torch.empty(t.shape[1], t.shape[0], dtype=t.dtype, device=t.device)
+    G = k("edl_transpose_tiles", t.shape[0])
+    partial = torch.empty(G, t.shape[1], dtype=torch.float32, device=t.device)
+    k.check("edl_transpose_colsum_bf16", t.data_ptr(), out.data_ptr(), partial.data_ptr(), t.shape[0], t.shape[1],
+            _native.stream_of(t))
+    return out, partial, G
+
+
 def _nt_wgrad_ok(dy2: torch.Tensor, x2: torch.Tensor) -> bool:
     return (_NT_WGRAD and dy2.is_cuda and dy2.dtype == torch.bfloat16 and x2.dtype == torch.bfloat16
             and x2.shape[1] <= _NT_WGRAD_MAX_K and dy2.shape[0] % 8 == 0 and dy2.shape[1] % 8 == 0
@@ -279,22 +292,36 @@ class _LinearFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = (torch.mm(dy2, wt.t()) if wt is not None else torch.mm(dy2, w)).view(*dy.shape[:-1], w.shape[1])
         dw = db = None
+        bias_partial = None   # (partial slab, G): bias gradient computed by the dY transpose
+        want_db = ctx.has_b and ctx.needs_input_grad[2]
         if ctx.needs_input_grad[1]:
             if _nt_wgrad_ok(dy2, x2):
-                a, b_ = _transposed(dy2), _transposed(x2).t()   # dY^T (contiguous) @ (X^T)^T: NT GEMM
+                if want_db:
+                    dyT, part, G = _transposed_colsum(dy2)
+                    bias_partial = (part, G)
+                else:
+                    dyT = _transposed(dy2)
+                a, b_ = dyT, _transposed(x2).t()   # dY^T (contiguous) @ (X^T)^T: NT GEMM
             else:
                 a, b_ = dy2.t(), x2
             if gradsink.is_flat(w):
                 gradsink.write_mm(w, a, b_)
             else:
                 dw = torch.mm(a, b_)
-        if ctx.has_b and ctx.needs_input_grad[2]:
+        if want_db:
             b = ctx.b
-            g = dy2.sum(0)
-            if gradsink.is_flat(b):
-                gradsink.write(b, g)
+            if bias_partial is not None:
+                from easydl_amd.ops.norms import _deliver_colsum
+                part, G = bias_partial
+                g = _deliver_colsum(_native.kernels(), b, part, G, dy2.shape[1], _native.stream_of(dy2))
+                if g is not None:
+                    db = g.to(b.dtype)
             else:
-                db = g.to(b.dtype)
+                g = dy2.sum(0)
+                if gradsink.is_flat(b):
+                    gradsink.write(b, g)
+                else:
+                    db = g.to(b.dtype)
         return dx, dw, db
 
 

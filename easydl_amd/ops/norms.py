@@ -91,7 +91,7 @@ class _NormFn(torch.autograd.Function):
         if ds is not None:
             ds = ds.contiguous()
         dx = torch.empty_like(src)
-        G = k("edl_norm_bwd_groups", rows)
+        G = k("edl_norm_bwd_groups", rows, cols)
         pw = torch.empty(G, cols, dtype=torch.float32, device=src.device)
         pb = torch.empty(G, cols, dtype=torch.float32, device=src.device) if ctx.ln else None
         st = _native.stream_of(src)

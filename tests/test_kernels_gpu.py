@@ -178,6 +178,36 @@ def test_transpose_bf16(cuda, R, C):
     assert torch.equal(y, x.t())
 
 
+@pytest.mark.parametrize("R,C", [(4096, 1024), (136, 72), (1000, 8), (16, 4104)])
+def test_transpose_colsum_bf16(cuda, R, C):
+    """dY^T plus fp32 column sums (the bias gradient) in one pass, vs torch."""
+    from easydl_amd.ops.fused import _transposed_colsum
+    x = torch.randn(R, C, device="cuda").bfloat16()
+    y, part, G = _transposed_colsum(x)
+    assert torch.equal(y, x.t())
+    torch.testing.assert_close(part.sum(0), x.float().sum(0), rtol=1e-5, atol=1e-3)
+
+
+@pytest.mark.parametrize("flat", [False, True])
+def test_linear_bias_grad_from_transpose(cuda, flat):
+    """Linear with bias: weight and bias gradients (NT path, bias from the fused
+    transpose + column sums) match fp32, accumulated over two micro-batches."""
+    from easydl_amd.parallel.flat import FlatParams
+    torch.manual_seed(3)
+    lin = torch.nn.Linear(1024, 3072).to(cuda, torch.bfloat16)
+    rw = lin.weight.detach().float().clone().requires_grad_()
+    rb = lin.bias.detach().float().clone().requires_grad_()
+    if flat:
+        FlatParams(lin)
+    x = torch.randn(512, 1024, device=cuda, dtype=torch.bfloat16)
+    for mb in range(2):
+        dy = torch.randn(512, 3072, device=cuda, dtype=torch.bfloat16)
+        fused.linear(x, lin.weight, lin.bias).backward(dy)
+        (x.float() @ rw.t() + rb).backward(dy.float())
+    _close(lin.weight.grad, rw.grad, 2e-2)
+    _close(lin.bias.grad, rb.grad, 2e-2)
+
+
 def test_linear_input_grad_uses_transposed_copy(cuda):
     """dX through the cached W^T (NT GEMM) equals dY @ W; the copy follows weight updates
     once a new generation starts (FlatParams.zero_grad)."""
