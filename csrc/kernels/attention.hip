@@ -83,6 +83,29 @@ __device__ __forceinline__ bf16x8 acc_to_b(const f32x16& acc, int s2) {
 // row (within a 32-row tile) of accumulator register i for lane half h
 __device__ __forceinline__ int acc_row(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }
 
+// Work decode of the (query block, query head, batch) grids of the forward and dQ
+// kernels.  xcd = 0: blockIdx as launched (query block reversed: longest causal rows
+// first).  xcd = 1 (needs B*KV % 8 == 0): workgroups are dealt round-robin over the 8
+// XCDs (blocks b and b+8 share one, MI355X_MICROARCH.md 'Workgroup dispatch'), so block
+// b is given K/V group (b % 8) + 8 j: every XCD serves whole GQA groups and one group's
+// K and V (4 MiB at S = 8192) stay in that XCD's L2 instead of all groups thrashing
+// every L2; query blocks still run longest first within each XCD.
+__device__ __forceinline__ void grid_decode(int xcd, int H, int KV, int& qb, int& hq, int& b) {
+  if (!xcd) {
+    qb = gridDim.x - 1 - blockIdx.x;
+    hq = blockIdx.y;
+    b = blockIdx.z;
+    return;
+  }
+  const int id = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+  const int gsz = H / KV, per = (int)gridDim.z * KV / 8;   // q heads per group, groups per XCD
+  const int slot = id >> 3, rank = slot / (per * gsz), rem = slot % (per * gsz);
+  const int g = (id & 7) + 8 * (rem / gsz);
+  qb = gridDim.x - 1 - rank;
+  b = g / KV;
+  hq = (g % KV) * gsz + rem % gsz;
+}
+
 // v_exp_f32 directly (exp2f() adds a denormal range fix-up: 3 extra VALU per call)
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
@@ -268,11 +291,12 @@ template <bool CAUSAL>
 __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
                                                           const bf16_t* __restrict__ v, bf16_t* __restrict__ o,
                                                           float* __restrict__ lse, int S, int H, int KV,
-                                                          float scale_log2) {
+                                                          float scale_log2, int xcd) {
   constexpr int BQ = 128;
   __shared__ __attribute__((aligned(16))) char smem[2 * 32768];
-  const int qb = gridDim.x - 1 - blockIdx.x;  // longest causal rows first
-  const int hq = blockIdx.y, b = blockIdx.z, hk = hq / (H / KV);
+  int qb, hq, b;
+  grid_decode(xcd, H, KV, qb, hq, b);  // longest causal rows first
+  const int hk = hq / (H / KV);
   const int lane = threadIdx.x & 63, h = lane >> 5, l31 = lane & 31;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // provably wave-uniform
   const int q0 = qb * BQ;
@@ -1208,11 +1232,12 @@ template <bool CAUSAL>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
     const bf16_t* __restrict__ dout, const float* __restrict__ lse, const float* __restrict__ delta,
-    bf16_t* __restrict__ dq, int S, int H, int KV, float scale_log2, float scale) {
+    bf16_t* __restrict__ dq, int S, int H, int KV, float scale_log2, float scale, int xcd) {
   constexpr int BQ = 128;
   __shared__ __attribute__((aligned(16))) char smem[2 * 32768];
-  const int qb = gridDim.x - 1 - blockIdx.x;
-  const int hq = blockIdx.y, b = blockIdx.z, hk = hq / (H / KV);
+  int qb, hq, b;
+  grid_decode(xcd, H, KV, qb, hq, b);
+  const int hk = hq / (H / KV);
   const int lane = threadIdx.x & 63, h = lane >> 5, l31 = lane & 31;
   const int w = threadIdx.x >> 6;
   const int q0 = qb * BQ;
@@ -1279,6 +1304,16 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(
 
 }  // namespace
 
+// XCD-aware work decode (grid_decode) for the forward and dQ kernels whenever every XCD
+// can take whole K/V groups: -21 % kernel time each at B 2, S 8192, H 32, KV 8
+// (profiles/r02_attn_xcd_ab.txt; the dK/dV kernel measured no gain from the same
+// grouping and keeps its launch order).  EDL_ATTN_XCD=0 restores the launch order.
+static int attn_xcd_map(int B, int KV) {
+  const char* e = getenv("EDL_ATTN_XCD");
+  const bool on = e == nullptr || atoi(e) != 0;
+  return on && (B * KV) % 8 == 0 ? 1 : 0;
+}
+
 extern "C" {
 
 int edl_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int S, int H, int KV,
@@ -1299,12 +1334,13 @@ int edl_attn_fwd(const void* q, const void* k, const void* v, void* o, float* ls
     return 0;
   }
   dim3 grid((S + 127) / 128, H, B);
+  const int xcd = attn_xcd_map(B, KV);
   if (causal)
     attn_fwd_kernel<true><<<grid, 256, 0, s>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
-                                                   (bf16_t*)o, lse, S, H, KV, sl2);
+                                                   (bf16_t*)o, lse, S, H, KV, sl2, xcd);
   else
     attn_fwd_kernel<false><<<grid, 256, 0, s>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
-                                                    (bf16_t*)o, lse, S, H, KV, sl2);
+                                                    (bf16_t*)o, lse, S, H, KV, sl2, xcd);
   EDL_LAUNCH_CHECK();
   return 0;
 }
@@ -1377,7 +1413,8 @@ int edl_attn_bwd(const void* q, const void* k, const void* v, const void* o, con
     }
     EDL_LAUNCH_CHECK();
     attn_bwd_dq_kernel<true><<<gq, 256, 0, s>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
-                                                (const bf16_t*)dout, lse, delta, (bf16_t*)dq, S, H, KV, sl2, scale);
+                                                (const bf16_t*)dout, lse, delta, (bf16_t*)dq, S, H, KV, sl2, scale,
+                                                attn_xcd_map(B, KV));
   } else {
     if (keys_per_wave == 64) {
       EDL_DKDV64(false);
@@ -1388,7 +1425,8 @@ int edl_attn_bwd(const void* q, const void* k, const void* v, const void* o, con
     }
     EDL_LAUNCH_CHECK();
     attn_bwd_dq_kernel<false><<<gq, 256, 0, s>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
-                                                 (const bf16_t*)dout, lse, delta, (bf16_t*)dq, S, H, KV, sl2, scale);
+                                                 (const bf16_t*)dout, lse, delta, (bf16_t*)dq, S, H, KV, sl2, scale,
+                                                 attn_xcd_map(B, KV));
   }
   EDL_LAUNCH_CHECK();
 #undef EDL_DKDV

@@ -22,7 +22,7 @@ def _err(a, b):
 
 @pytest.mark.parametrize("B,S,H,KV,causal", [(1, 128, 4, 4, True), (2, 256, 8, 2, True), (1, 200, 4, 1, True),
                                              (1, 384, 8, 8, False), (2, 200, 4, 2, False), (1, 1024, 32, 8, True),
-                                             (1, 2112, 8, 2, True)])
+                                             (1, 2112, 8, 2, True), (2, 200, 8, 4, False), (2, 1000, 16, 8, True)])
 @pytest.mark.parametrize("fwd", ["0", "64"])
 def test_flash_attention_fwd_bwd(cuda, B, S, H, KV, causal, fwd, monkeypatch):
     """Both forward kernels (EDL_ATTN_FWD=0: 32 queries/wave; 64: software-pipelined)."""
@@ -52,6 +52,23 @@ def test_flash_attention_forces_lazy_rescale(cuda, fwd, monkeypatch):
     o = flash_attention(q, k, v, causal=True)
     ref = attention_ref(q.float(), k.float(), v.float(), causal=True)
     assert _err(o, ref) < 2e-2
+
+
+@pytest.mark.parametrize("causal", [True, False])
+def test_xcd_work_decode_is_bitwise_identical(cuda, causal, monkeypatch):
+    """B*KV % 8 == 0: the forward and dQ kernels deal whole K/V groups to XCDs
+    (EDL_ATTN_XCD, default on).  Same per-workgroup arithmetic -> identical bits."""
+    q, k, v = _mk(2, 1152, 16, 4, cuda, 5)
+    do = torch.randn(2, 16, 1152, 128, device=cuda).to(torch.bfloat16)
+    outs = []
+    for mode in ("0", "1"):
+        monkeypatch.setenv("EDL_ATTN_XCD", mode)
+        q1, k1, v1 = (t.detach().clone().requires_grad_() for t in (q, k, v))
+        o = flash_attention(q1, k1, v1, causal=causal)
+        o.backward(do)
+        outs.append((o, q1.grad, k1.grad, v1.grad))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
 
 
 def test_flash_attention_speed_report(cuda):
