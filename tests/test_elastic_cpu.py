@@ -242,3 +242,35 @@ def test_tp_shard_lost_restores_from_snapshot(tmp_path):
     finally:
         m.terminate()
         unlink_job_segments(job)
+
+
+def test_snapshot_fenced_before_a_broadcast_rewrites_state():
+    """_fence_snapshot_before_overwrite: the in-flight snapshot D2H is fenced exactly when
+    this rank's buffers are about to change (receiver, or any non-source rank of the
+    xGMI-only broadcast, which zero-fills), never on the source or an RCCL holder."""
+    from types import SimpleNamespace
+
+    import torch
+
+    from easydl_amd.trainer.elastic import ElasticTrainer
+
+    calls = []
+    ck = SimpleNamespace(fence=lambda: calls.append(1))
+    me = SimpleNamespace(checkpoint=ck, device=torch.device("cuda", 0))
+    fn = ElasticTrainer._fence_snapshot_before_overwrite
+    cases = [  # (rank, src, holder, backend) -> fenced?
+        (0, 0, True, "rccl", False),    # the source
+        (1, 0, True, "rccl", False),    # holder receiving identical bytes
+        (1, 0, False, "rccl", True),    # receiver: buffers change
+        (1, 0, True, "xgmi", True),     # xGMI-only broadcast zero-fills non-source ranks
+        (0, 0, True, "xgmi", False),
+    ]
+    for rank, src, holder, backend, want in cases:
+        calls.clear()
+        fn(me, SimpleNamespace(rank=rank, backend=backend), src, holder)
+        assert bool(calls) == want, (rank, src, holder, backend)
+    calls.clear()
+    fn(SimpleNamespace(checkpoint=None, device=torch.device("cuda", 0)), SimpleNamespace(rank=1, backend="xgmi"), 0,
+       False)
+    fn(SimpleNamespace(checkpoint=ck, device=torch.device("cpu")), SimpleNamespace(rank=1, backend="xgmi"), 0, False)
+    assert not calls   # no checkpoint manager / CPU state: nothing to fence
