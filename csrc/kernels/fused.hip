@@ -147,7 +147,7 @@ __global__ __launch_bounds__(256) void rope_qkv_kernel(const bf16_t* __restrict_
 __global__ __launch_bounds__(256) void xent_fwd_bwd_kernel(bf16_t* __restrict__ logits,
                                                            const int64_t* __restrict__ labels,
                                                            float* __restrict__ loss, int V, int64_t ignore_index,
-                                                           int write_grad) {
+                                                           int write_grad, const float* __restrict__ gscale) {
   __shared__ float sm[4], ss[4];
   __shared__ float s_tgt;
   const int64_t row = blockIdx.x;
@@ -195,7 +195,10 @@ __global__ __launch_bounds__(256) void xent_fwd_bwd_kernel(bf16_t* __restrict__ 
   const float lse = M + __logf(Ssum);
   if (threadIdx.x == 0) loss[row] = ignored ? 0.f : (lse - s_tgt);
   if (!write_grad) return;
-  const float inv = 1.f / Ssum;
+  // gradient multiplier (device scalar, e.g. dloss / n_valid): the backward writes the
+  // final gradient in one pass instead of a separate scaling pass over V x rows
+  const float g = gscale ? *gscale : 1.f;
+  const float inv = g / Ssum;
   u32x4* lw = reinterpret_cast<u32x4*>(lr);
   for (int c = threadIdx.x; c < nchunk; c += blockDim.x) {
     float f[8];
@@ -203,14 +206,14 @@ __global__ __launch_bounds__(256) void xent_fwd_bwd_kernel(bf16_t* __restrict__ 
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       float p = ignored ? 0.f : __expf(f[i] - M) * inv;
-      if (!ignored && (int64_t)(c * 8 + i) == lab) p -= 1.f;
+      if (!ignored && (int64_t)(c * 8 + i) == lab) p -= g;
       f[i] = p;
     }
     lw[c] = pack8(f);
   }
   for (int c = (nchunk << 3) + threadIdx.x; c < V; c += blockDim.x) {
     float p = ignored ? 0.f : __expf(bf2f(lr[c]) - M) * inv;
-    if (!ignored && (int64_t)c == lab) p -= 1.f;
+    if (!ignored && (int64_t)c == lab) p -= g;
     lr[c] = f2bf(p);
   }
 }
@@ -622,10 +625,12 @@ int edl_rope_qkv_bwd(const void* dq, const void* dk, const void* dv, void* dqkv,
   return 0;
 }
 
+// write_grad: overwrite logits with (softmax - onehot) * (*gscale) (gscale may be null = 1)
 int edl_xent_fwd_bwd(void* logits, const int64_t* labels, float* loss, int64_t rows, int V, int64_t ignore_index,
-                     int write_grad, hipStream_t s) {
+                     int write_grad, const float* gscale, hipStream_t s) {
   if (rows <= 0) return 0;
-  xent_fwd_bwd_kernel<<<(unsigned)rows, 256, 0, s>>>((bf16_t*)logits, labels, loss, V, ignore_index, write_grad);
+  xent_fwd_bwd_kernel<<<(unsigned)rows, 256, 0, s>>>((bf16_t*)logits, labels, loss, V, ignore_index, write_grad,
+                                                     gscale);
   EDL_LAUNCH_CHECK();
   return 0;
 }
