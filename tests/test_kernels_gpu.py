@@ -154,6 +154,20 @@ def test_grad_clip(cuda):
     assert out[2].item() == 1
 
 
+@pytest.mark.parametrize("n,off", [(1 << 20, 0), (1 << 20, 4), (4 * 1001, 0), (4 * 1001, 8)])
+def test_sumsq_partial_matches_torch(cuda, n, off):
+    """Global grad-norm partials: 16-byte path (aligned, any 4-element count) and the
+    8-byte fallback (base not 16-byte aligned) both match an fp64 sum of squares."""
+    from easydl_amd import _native
+    k = _native.kernels()
+    buf = torch.randn(n + off, device=cuda).to(torch.bfloat16)
+    g = buf[off:]
+    parts = torch.zeros(k("edl_sumsq_nparts", n), device=cuda)
+    k.check("edl_sumsq_partial", g.data_ptr(), 0, n, parts.data_ptr(), _native.stream_of(g))
+    ref = g.double().pow(2).sum().item()
+    assert abs(parts.double().sum().item() - ref) <= 1e-4 * ref
+
+
 def test_linear_direct_grad_into_flat(cuda):
     from easydl_amd.parallel.flat import FlatParams
     torch.manual_seed(7)
