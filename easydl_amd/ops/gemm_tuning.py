@@ -55,9 +55,10 @@ def apply(mode: str | None = None, path: str | None = None) -> str:
         return "off"
     tun.enable(True)
     tun.tuning_enable(False)
-    # TunableOp writes its results at exit even with tuning off: point that at a
-    # scratch file, never at the shipped one (or the working directory's default)
-    tun.set_filename(os.path.join(tempfile.gettempdir(), f"edl_tunableop_{os.getpid()}_%d.csv"))
+    # TunableOp writes its results at exit even with tuning off: point that at ONE scratch
+    # file per user (never the shipped file or the working directory's default; a
+    # per-process name would pile up).  Ranks may overwrite it concurrently: nothing reads it.
+    tun.set_filename(os.path.join(tempfile.gettempdir(), f"edl_tunableop_scratch_{os.getuid()}.csv"))
     ok = tun.read_file(path)
     if not ok:
         log.warning("TunableOp results %s not loaded (validator mismatch?): library heuristics", path)
