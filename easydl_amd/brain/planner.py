@@ -200,7 +200,7 @@ class Planner:
         # grow into free GPUs
         wr = plan.roles.get("worker")
         if wr is not None and feat.mode != "ps":
-            busy = sum(1 for g in inv.gpus if (g.busy_pct or 0) > 50)
+            busy = sum(1 for g in inv.gpus if g.is_busy())
             free = len(inv.gpus) - max(busy, wr.replicas)
             if free > 0 and wr.replicas < feat.max_workers:
                 wr.replicas = min(feat.max_workers, wr.replicas + free)

@@ -111,3 +111,36 @@ def test_rocprof_profile_drives_per_rank_cu_plan(tmp_path):
     nxt = Planner().next_plan(JobFeatures(mode="ps", params=3.3e8), _inv(8, busy=90), _plan(), metrics)
     assert nxt is not None and 0 < nxt.per_rank["ps0"]["cu"] < 256 and nxt.per_rank["ps0"]["cu"] % 8 == 0
     assert "cu" not in nxt.per_rank.get("w0", {})
+
+
+def test_amdsmi_samples_give_link_rates_throttle_share_and_busy_by_hbm():
+    from easydl_amd.brain.collectors import amdsmi_record, merge_amdsmi
+    na = "N/A"
+
+    def raw(rd, wr, ppt, acc):
+        return {"average_gfx_activity": 97, "average_umc_activity": 41, "current_socket_power": na,
+                "average_socket_power": 1350, "current_gfxclks": [2100, 2000, na, 2100, 2000, 2100, 2000, 2100],
+                "ppt_residency_acc": ppt, "accumulation_counter": acc,
+                "xgmi_read_data_acc": rd, "xgmi_write_data_acc": wr}
+
+    a = amdsmi_record(raw([0] * 7 + [na], [0] * 8, 100, 1000), {"vram_used": 210 * 1024}, "0000:75:00.0")
+    b = amdsmi_record(raw([50_000_000] * 7 + [na], [25_000_000] * 8, 350, 2000), {"vram_used": 210 * 1024},
+                      "0000:75:00.0")
+    a["t"], b["t"] = 10.0, 10.5
+    gpus = [GpuInfo(0, "gfx950", 256, 288.0, bdf="0000:05:00.0"), GpuInfo(1, "gfx950", 256, 288.0,
+                                                                          bdf="0000:75:00.0")]
+    merge_amdsmi(gpus, [a], [b])
+    g = gpus[1]                                          # matched by PCI address, not by order
+    assert gpus[0].power_w is None and g.power_w == 1350 and g.busy_pct == 97 and g.umc_pct == 41
+    assert g.xgmi_read_gbps[:7] == [100.0] * 7 and g.xgmi_read_gbps[7] is None   # 50 GB in 0.5 s
+    assert g.xgmi_write_gbps == [50.0] * 8
+    assert g.throttle_pct == 25.0 and abs(g.gfxclk_mhz - 2057.1) < 0.1
+    assert g.mem_used_gb == 210.0 and g.is_busy()
+    assert not GpuInfo(2, "gfx950", 256, 288.0, busy_pct=3, mem_used_gb=0.3).is_busy()
+    # a GPU someone holds (HBM in use) is not "free" for a scale-up, even while idle: the
+    # job's 4 workers hold GPUs 0-3, another process holds 6-7 -> room for 2 more workers
+    inv = NodeInventory(gpus=[GpuInfo(i, "gfx950", 256, 288.0, busy_pct=0,
+                                      mem_used_gb=0.2 if i in (4, 5) else 100.0) for i in range(8)],
+                        cpus=128, host_mem_gb=2048)
+    nxt = Planner().next_plan(JobFeatures(params=8e9, max_workers=8), inv, _plan(workers=4), {})
+    assert nxt is not None and nxt.roles["worker"].replicas == 6

@@ -45,3 +45,21 @@ def test_roctx_ranges_do_not_fail(cuda):
             torch.ones(4, device=cuda).sum().item()
     trace.mark("done")
     trace.enable(False)
+
+
+def test_amdsmi_telemetry_sees_this_process_hbm_and_power(cuda):
+    """Brain telemetry: amd-smi in a child process, matched to the KFD
+    inventory by PCI address; the 20 GiB this test holds shows up as HBM in use."""
+    import json
+    from easydl_amd.brain.collectors import amdsmi_telemetry, kfd_gpus
+    assert kfd_gpus(), "KFD topology lists no GPU"
+    before = amdsmi_telemetry(kfd_gpus(), window_s=0.0)
+    assert before is not None, "amd-smi child failed"
+    hold = torch.empty(20 << 30, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    got = amdsmi_telemetry(kfd_gpus(), window_s=0.3)
+    print(json.dumps({"before": [g.__dict__ for g in before], "holding_20GiB": [g.__dict__ for g in got]}))
+    assert any((g.mem_used_gb or 0) - (b.mem_used_gb or 0) >= 19 for g, b in zip(got, before))
+    assert any(g.power_w for g in got)
+    assert all(g.xgmi_read_gbps is None or len(g.xgmi_read_gbps) == 8 for g in got)
+    del hold
