@@ -1,0 +1,385 @@
+// Training-mode BatchNorm over channels-last (NHWC) bf16 activations with the
+// ReLU and the residual add of a ResNet bottleneck fused in:
+//
+//     z = relu?( (x - mean_c) * rstd_c * w_c + b_c  [+ r] )
+//
+// The activation is a row-major [M = N*H*W, C] matrix.  MIOpen's NHWC batch
+// norm plus PyTorch's bf16<->fp32 casts, residual add and ReLU took 44 of the
+// 63 ms of a ResNet-50 step at batch 256 on one MI355X (13 kernels per block);
+// this is 2 passes forward (statistics; normalise+add+ReLU) and 2 backward
+// (dbias/dweight reductions; dx [+ d residual]), each one streaming read of the
+// bf16 tensors at 16 B per lane.
+//
+// Work split: a thread owns 8 consecutive channels (one 16-B vector) of a row;
+// ROWS_PER_ITER = 256 / (C/8) rows of a block are read at once, so a block
+// keeps its per-channel coefficients in registers for its whole row range.
+// Statistics are shifted by the running mean (sum (x - k), sum (x - k)^2 in
+// fp32 per thread, fp64 across threads and blocks), so E[x^2] - E[x]^2 does not
+// cancel once the running mean tracks the batch mean.  The backward sums
+// dp * (x - mean) with the batch mean itself.
+// Capability source: ResNet-50 bf16 elastic DDP (BASELINE.json config 2).
+#include "common.h"
+
+using namespace edl;
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kUnroll = 4;
+
+struct Geo {
+  int tpr, rpi, col8, r0;
+  bool active;
+  __device__ __forceinline__ Geo(int C) {
+    tpr = C >> 3;
+    rpi = kThreads / tpr;
+    col8 = threadIdx.x % tpr;
+    r0 = threadIdx.x / tpr;
+    active = r0 < rpi;
+  }
+};
+
+__device__ __forceinline__ void row_range(int64_t M, int rpi, int64_t& r, int64_t& end) {
+  const int64_t per = ((M + gridDim.x - 1) / gridDim.x + rpi - 1) / rpi * rpi;
+  r = (int64_t)blockIdx.x * per;
+  end = min(M, r + per);
+}
+
+// Per-block column sums of two [rpi][C] fp32 register sets -> part[block][2][C].
+__device__ __forceinline__ void block_colsum2(const float (&a)[8], const float (&b)[8], const Geo& g, int C,
+                                              float* part) {
+  __shared__ float red[2][kThreads * 8];
+  if (g.active) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      red[0][g.r0 * C + g.col8 * 8 + j] = a[j];
+      red[1][g.r0 * C + g.col8 * 8 + j] = b[j];
+    }
+  }
+  __syncthreads();
+  float* out = part + (int64_t)blockIdx.x * 2 * C;
+  for (int c = threadIdx.x; c < C; c += kThreads) {
+    float s = 0.f, q = 0.f;
+    for (int r = 0; r < g.rpi; ++r) {
+      s += red[0][r * C + c];
+      q += red[1][r * C + c];
+    }
+    out[c] = s;
+    out[C + c] = q;
+  }
+}
+
+__device__ __forceinline__ void load8f(const float* p, float (&f)[8]) {
+  const f32x4 a = *reinterpret_cast<const f32x4*>(p), b = *reinterpret_cast<const f32x4*>(p + 4);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    f[j] = a[j];
+    f[4 + j] = b[j];
+  }
+}
+
+// ---------------------------------------------------------------------------- forward
+__global__ __launch_bounds__(kThreads) void bn_stats_kernel(const bf16_t* __restrict__ x,
+                                                            const float* __restrict__ shift, int64_t M, int C,
+                                                            float* __restrict__ part) {
+  const Geo g(C);
+  float s[8] = {}, q[8] = {};
+  if (g.active) {
+    float k[8];
+    load8f(shift + g.col8 * 8, k);
+    int64_t r, end;
+    row_range(M, g.rpi, r, end);
+    r += g.r0;
+    const bf16_t* px = x + g.col8 * 8;
+    for (; r + (kUnroll - 1) * g.rpi < end; r += kUnroll * g.rpi) {
+      u32x4 v[kUnroll];
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) v[u] = *reinterpret_cast<const u32x4*>(px + (r + u * g.rpi) * C);
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) {
+        float f[8];
+        unpack8(v[u], f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float d = f[j] - k[j];
+          s[j] += d;
+          q[j] = __builtin_fmaf(d, d, q[j]);
+        }
+      }
+    }
+    for (; r < end; r += g.rpi) {
+      float f[8];
+      unpack8(*reinterpret_cast<const u32x4*>(px + r * C), f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d = f[j] - k[j];
+        s[j] += d;
+        q[j] = __builtin_fmaf(d, d, q[j]);
+      }
+    }
+  }
+  block_colsum2(s, q, g, C, part);
+}
+
+// one thread per channel per quarter of the partials; fp64 accumulation
+__global__ __launch_bounds__(kThreads) void bn_stats_finalize_kernel(
+    const float* __restrict__ part, int G, int C, int64_t M, const float* __restrict__ w,
+    const float* __restrict__ b, float* __restrict__ run_mean, float* __restrict__ run_var, float momentum,
+    float eps, float* __restrict__ mean_out, float* __restrict__ rstd_out, float* __restrict__ coef) {
+  __shared__ double red[2][kThreads];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63), gl = threadIdx.x >> 6;
+  double s = 0.0, q = 0.0;
+  if (c < C) {
+    for (int i = gl; i < G; i += 4) {
+      s += (double)part[(int64_t)i * 2 * C + c];
+      q += (double)part[(int64_t)i * 2 * C + C + c];
+    }
+  }
+  red[0][threadIdx.x] = s;
+  red[1][threadIdx.x] = q;
+  __syncthreads();
+  if (gl != 0 || c >= C) return;
+  for (int i = 1; i < 4; ++i) {
+    s += red[0][threadIdx.x + 64 * i];
+    q += red[1][threadIdx.x + 64 * i];
+  }
+  const double k = (double)run_mean[c];
+  const double dm = s / (double)M;
+  const double var = fmax(q / (double)M - dm * dm, 0.0);
+  const float mean = (float)(k + dm);
+  const float rstd = (float)(1.0 / sqrt(var + (double)eps));
+  mean_out[c] = mean;
+  rstd_out[c] = rstd;
+  const float sc = w[c] * rstd;
+  coef[c] = sc;                 // z = x * sc + sh
+  coef[C + c] = b[c] - mean * sc;
+  run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * mean;
+  const double unbiased = M > 1 ? var * (double)M / (double)(M - 1) : var;
+  run_var[c] = (1.f - momentum) * run_var[c] + momentum * (float)unbiased;
+}
+
+template <bool RES, bool RELU>
+__global__ __launch_bounds__(kThreads) void bn_apply_kernel(const bf16_t* __restrict__ x,
+                                                            const bf16_t* __restrict__ res,
+                                                            const float* __restrict__ coef, int64_t M, int C,
+                                                            bf16_t* __restrict__ z) {
+  const Geo g(C);
+  if (!g.active) return;
+  float sc[8], sh[8];
+  load8f(coef + g.col8 * 8, sc);
+  load8f(coef + C + g.col8 * 8, sh);
+  int64_t r, end;
+  row_range(M, g.rpi, r, end);
+  const int64_t o0 = g.col8 * 8;
+  for (r += g.r0; r < end; r += g.rpi) {
+    const int64_t o = r * C + o0;
+    float f[8];
+    unpack8(*reinterpret_cast<const u32x4*>(x + o), f);
+    float e[8];
+    if (RES) unpack8(*reinterpret_cast<const u32x4*>(res + o), e);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float v = __builtin_fmaf(f[j], sc[j], sh[j]);
+      if (RES) v += e[j];
+      if (RELU) v = fmaxf(v, 0.f);
+      f[j] = v;
+    }
+    *reinterpret_cast<u32x4*>(z + o) = pack8(f);
+  }
+}
+
+// ---------------------------------------------------------------------------- backward
+// dp = relu ? (z > 0 ? dz : 0) : dz;   partials of sum dp and sum dp * (x - mean)
+template <bool RELU>
+__global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(const bf16_t* __restrict__ dz,
+                                                                 const bf16_t* __restrict__ z,
+                                                                 const bf16_t* __restrict__ x,
+                                                                 const float* __restrict__ mean, int64_t M, int C,
+                                                                 float* __restrict__ part) {
+  const Geo g(C);
+  float s[8] = {}, q[8] = {};
+  if (g.active) {
+    float mu[8];
+    load8f(mean + g.col8 * 8, mu);
+    int64_t r, end;
+    row_range(M, g.rpi, r, end);
+    const int64_t o0 = g.col8 * 8;
+    for (r += g.r0; r < end; r += g.rpi) {
+      const int64_t o = r * C + o0;
+      float d[8], f[8], y[8];
+      unpack8(*reinterpret_cast<const u32x4*>(dz + o), d);
+      unpack8(*reinterpret_cast<const u32x4*>(x + o), f);
+      if (RELU) unpack8(*reinterpret_cast<const u32x4*>(z + o), y);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float dp = RELU ? (y[j] > 0.f ? d[j] : 0.f) : d[j];
+        s[j] += dp;
+        q[j] = __builtin_fmaf(dp, f[j] - mu[j], q[j]);
+      }
+    }
+  }
+  block_colsum2(s, q, g, C, part);
+}
+
+// dbias = sum dp, dweight = rstd * sum dp (x - mean); dx = A dp - K1 x + K2 with
+// A = w rstd, K1 = w rstd^2 dweight / M, K2 = K1 mean - A dbias / M
+__global__ __launch_bounds__(kThreads) void bn_bwd_finalize_kernel(const float* __restrict__ part, int G, int C,
+                                                                   int64_t M, const float* __restrict__ w,
+                                                                   const float* __restrict__ mean,
+                                                                   const float* __restrict__ rstd,
+                                                                   float* __restrict__ dw, float* __restrict__ db,
+                                                                   float* __restrict__ coef) {
+  __shared__ double red[2][kThreads];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63), gl = threadIdx.x >> 6;
+  double s = 0.0, q = 0.0;
+  if (c < C) {
+    for (int i = gl; i < G; i += 4) {
+      s += (double)part[(int64_t)i * 2 * C + c];
+      q += (double)part[(int64_t)i * 2 * C + C + c];
+    }
+  }
+  red[0][threadIdx.x] = s;
+  red[1][threadIdx.x] = q;
+  __syncthreads();
+  if (gl != 0 || c >= C) return;
+  for (int i = 1; i < 4; ++i) {
+    s += red[0][threadIdx.x + 64 * i];
+    q += red[1][threadIdx.x + 64 * i];
+  }
+  const double rs = (double)rstd[c];
+  const double gw = q * rs, gb = s;
+  dw[c] = (float)gw;
+  db[c] = (float)gb;
+  const double A = (double)w[c] * rs;
+  const double K1 = A * rs * gw / (double)M;
+  coef[c] = (float)A;
+  coef[C + c] = (float)K1;
+  coef[2 * C + c] = (float)(K1 * (double)mean[c] - A * gb / (double)M);
+}
+
+template <bool RELU, bool DRES>
+__global__ __launch_bounds__(kThreads) void bn_bwd_dx_kernel(const bf16_t* __restrict__ dz,
+                                                             const bf16_t* __restrict__ z,
+                                                             const bf16_t* __restrict__ x,
+                                                             const float* __restrict__ coef, int64_t M, int C,
+                                                             bf16_t* __restrict__ dx, bf16_t* __restrict__ dres) {
+  const Geo g(C);
+  if (!g.active) return;
+  float A[8], K1[8], K2[8];
+  load8f(coef + g.col8 * 8, A);
+  load8f(coef + C + g.col8 * 8, K1);
+  load8f(coef + 2 * C + g.col8 * 8, K2);
+  int64_t r, end;
+  row_range(M, g.rpi, r, end);
+  const int64_t o0 = g.col8 * 8;
+  for (r += g.r0; r < end; r += g.rpi) {
+    const int64_t o = r * C + o0;
+    float d[8], f[8], y[8];
+    unpack8(*reinterpret_cast<const u32x4*>(dz + o), d);
+    unpack8(*reinterpret_cast<const u32x4*>(x + o), f);
+    if (RELU) unpack8(*reinterpret_cast<const u32x4*>(z + o), y);
+    float gx[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float dp = RELU ? (y[j] > 0.f ? d[j] : 0.f) : d[j];
+      d[j] = dp;
+      gx[j] = __builtin_fmaf(A[j], dp, __builtin_fmaf(-K1[j], f[j], K2[j]));
+    }
+    *reinterpret_cast<u32x4*>(dx + o) = pack8(gx);
+    if (DRES) *reinterpret_cast<u32x4*>(dres + o) = pack8(d);
+  }
+}
+
+int blocks_for(int64_t M, int C, int min_rows_per_thread, int cap) {
+  const int rpi = kThreads / (C >> 3);
+  const int64_t want = (M + (int64_t)rpi * min_rows_per_thread - 1) / ((int64_t)rpi * min_rows_per_thread);
+  return (int)(want < 1 ? 1 : want > cap ? cap : want);
+}
+
+bool shape_ok(int64_t M, int C) { return M > 0 && C >= 8 && C % 8 == 0 && C <= 8 * kThreads; }
+
+}  // namespace
+
+extern "C" {
+
+// partial-sum slab size of the reductions: floats = 2 * C * edl_bn_groups(M, C)
+int edl_bn_groups(int64_t M, int C) { return shape_ok(M, C) ? blocks_for(M, C, 16, 1024) : 0; }
+
+// statistics + normalise (+ residual) (+ ReLU).  mean/rstd: fp32 [C] saved for the backward;
+// coef: fp32 [2C] scratch; part: fp32 [2C * edl_bn_groups].  running_mean is also the shift.
+int edl_bn_fwd_train(const void* x, const void* res, void* z, const float* w, const float* b, float* run_mean,
+                     float* run_var, float* mean, float* rstd, float* coef, float* part, int64_t M, int C,
+                     float momentum, float eps, int relu, hipStream_t s) {
+  if (!shape_ok(M, C)) return (int)hipErrorInvalidValue;
+  const int G = edl_bn_groups(M, C);
+  bn_stats_kernel<<<G, kThreads, 0, s>>>((const bf16_t*)x, run_mean, M, C, part);
+  EDL_LAUNCH_CHECK();
+  bn_stats_finalize_kernel<<<(C + 63) / 64, kThreads, 0, s>>>(part, G, C, M, w, b, run_mean, run_var, momentum,
+                                                               eps, mean, rstd, coef);
+  EDL_LAUNCH_CHECK();
+  const int GA = blocks_for(M, C, 4, 2048);
+#define EDL_BN_APPLY(R, L)                                                                               \
+  bn_apply_kernel<R, L><<<GA, kThreads, 0, s>>>((const bf16_t*)x, (const bf16_t*)res, coef, M, C, (bf16_t*)z)
+  if (res) {
+    if (relu) EDL_BN_APPLY(true, true); else EDL_BN_APPLY(true, false);
+  } else {
+    if (relu) EDL_BN_APPLY(false, true); else EDL_BN_APPLY(false, false);
+  }
+#undef EDL_BN_APPLY
+  EDL_LAUNCH_CHECK();
+  return 0;
+}
+
+// z = x * coef[c] + coef[C + c] (+ res) (+ ReLU): eval mode, coef from the running statistics
+int edl_bn_apply(const void* x, const void* res, void* z, const float* coef, int64_t M, int C, int relu,
+                 hipStream_t s) {
+  if (!shape_ok(M, C)) return (int)hipErrorInvalidValue;
+  const int GA = blocks_for(M, C, 4, 2048);
+  if (res) {
+    if (relu)
+      bn_apply_kernel<true, true><<<GA, kThreads, 0, s>>>((const bf16_t*)x, (const bf16_t*)res, coef, M, C,
+                                                          (bf16_t*)z);
+    else
+      bn_apply_kernel<true, false><<<GA, kThreads, 0, s>>>((const bf16_t*)x, (const bf16_t*)res, coef, M, C,
+                                                           (bf16_t*)z);
+  } else {
+    if (relu)
+      bn_apply_kernel<false, true><<<GA, kThreads, 0, s>>>((const bf16_t*)x, nullptr, coef, M, C, (bf16_t*)z);
+    else
+      bn_apply_kernel<false, false><<<GA, kThreads, 0, s>>>((const bf16_t*)x, nullptr, coef, M, C, (bf16_t*)z);
+  }
+  EDL_LAUNCH_CHECK();
+  return 0;
+}
+
+// dz (and z for the ReLU mask), x, saved mean/rstd -> dx, optional d residual, dw, db (fp32 [C]).
+// coef: fp32 [3C] scratch; part as in the forward.
+int edl_bn_bwd(const void* dz, const void* z, const void* x, const float* w, const float* mean, const float* rstd,
+               void* dx, void* dres, float* dw, float* db, float* coef, float* part, int64_t M, int C, int relu,
+               hipStream_t s) {
+  if (!shape_ok(M, C) || (relu && z == nullptr)) return (int)hipErrorInvalidValue;
+  const int G = edl_bn_groups(M, C);
+  if (relu)
+    bn_bwd_reduce_kernel<true><<<G, kThreads, 0, s>>>((const bf16_t*)dz, (const bf16_t*)z, (const bf16_t*)x, mean,
+                                                      M, C, part);
+  else
+    bn_bwd_reduce_kernel<false><<<G, kThreads, 0, s>>>((const bf16_t*)dz, nullptr, (const bf16_t*)x, mean, M, C,
+                                                       part);
+  EDL_LAUNCH_CHECK();
+  bn_bwd_finalize_kernel<<<(C + 63) / 64, kThreads, 0, s>>>(part, G, C, M, w, mean, rstd, dw, db, coef);
+  EDL_LAUNCH_CHECK();
+  const int GA = blocks_for(M, C, 4, 2048);
+#define EDL_BN_DX(L, D)                                                                                        \
+  bn_bwd_dx_kernel<L, D><<<GA, kThreads, 0, s>>>((const bf16_t*)dz, (const bf16_t*)z, (const bf16_t*)x, coef, M, \
+                                                 C, (bf16_t*)dx, (bf16_t*)dres)
+  if (dres) {
+    if (relu) EDL_BN_DX(true, true); else EDL_BN_DX(false, true);
+  } else {
+    if (relu) EDL_BN_DX(true, false); else EDL_BN_DX(false, false);
+  }
+#undef EDL_BN_DX
+  EDL_LAUNCH_CHECK();
+  return 0;
+}
+
+}  // extern "C"

@@ -1,15 +1,19 @@
 """ResNet-50 (BASELINE.json config 2: "ResNet-50 bf16 elastic DDP, scale 1->8").
 
 Written here (torchvision is not installed).  bf16 weights in channels-last
-memory format so MIOpen picks its NHWC implicit-GEMM (MFMA) convolutions;
-BatchNorm keeps fp32 statistics.  Synthetic ImageNet-shaped data
-(:class:`SyntheticImages`) since no dataset can be downloaded.
+memory format so MIOpen picks its NHWC implicit-GEMM (MFMA) convolutions.
+Every BatchNorm (fp32 weight and statistics) runs with its ReLU and, at the end
+of a bottleneck, the residual add fused in (:func:`easydl_amd.ops.batchnorm.bn_act`,
+HIP kernels on the GPU).  Synthetic ImageNet-shaped data (:class:`SyntheticImages`)
+since no dataset can be downloaded.
 """
 from __future__ import annotations
 
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
+
+from easydl_amd.ops.batchnorm import bn_act
 
 
 class Bottleneck(nn.Module):
@@ -27,11 +31,14 @@ class Bottleneck(nn.Module):
         self.downsample = downsample
 
     def forward(self, x):
-        idt = x if self.downsample is None else self.downsample(x)
-        y = F.relu(self.bn1(self.conv1(x)))
-        y = F.relu(self.bn2(self.conv2(y)))
-        y = self.bn3(self.conv3(y))
-        return F.relu(y + idt)
+        if self.downsample is None:
+            idt = x
+        else:
+            conv, bn = self.downsample
+            idt = bn_act(conv(x), bn, relu=False)
+        y = bn_act(self.conv1(x), self.bn1)
+        y = bn_act(self.conv2(y), self.bn2)
+        return bn_act(self.conv3(y), self.bn3, residual=idt)
 
 
 class ResNet(nn.Module):
@@ -56,7 +63,7 @@ class ResNet(nn.Module):
         self.fc = nn.Linear(cin, num_classes)
 
     def forward(self, x, y=None):
-        x = F.relu(self.bn1(self.conv1(x)))
+        x = bn_act(self.conv1(x), self.bn1)
         x = F.max_pool2d(x, 3, 2, 1)
         x = self.stages(x)
         x = torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)
@@ -71,20 +78,10 @@ def resnet50(device=None, dtype=torch.bfloat16, num_classes=1000) -> ResNet:
     m = m.to(device=device, dtype=dtype)
     if device is not None and torch.device(device).type == "cuda":
         m = m.to(memory_format=torch.channels_last)
-    for mod in m.modules():  # fp32 batch statistics
+    for mod in m.modules():  # fp32 weight, bias and batch statistics
         if isinstance(mod, nn.BatchNorm2d):
             mod.float()
-            mod.forward = _bn_fp32(mod)
     return m
-
-
-def _bn_fp32(bn):
-    orig = nn.BatchNorm2d.forward
-
-    def fwd(x):
-        return orig(bn, x.float()).to(x.dtype)
-
-    return fwd
 
 
 class SyntheticImages:

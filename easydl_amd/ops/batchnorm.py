@@ -1,0 +1,125 @@
+"""BatchNorm (+ residual add) (+ ReLU) for channels-last bf16 activations
+(HIP kernels in csrc/kernels/batchnorm.hip).
+
+``bn_act(x, bn, residual=None, relu=True)`` computes
+``relu(bn(x) + residual)`` with the statistics, running-average update and
+affine of the ``nn.BatchNorm2d`` module ``bn`` (fp32 weight, bias and running
+buffers; bf16 activations).  On the GPU this is two passes over the activation
+forward and two backward; the ResNet bottleneck's separate BatchNorm, casts,
+residual add and ReLU kernels disappear.  CPU tensors run the fp32 PyTorch
+reference :func:`bn_act_ref` (the CPU test tier and the numerics oracle).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from easydl_amd import _native
+
+
+def bn_act_ref(x, bn, residual=None, relu=True):
+    y = F.batch_norm(x.float(), bn.running_mean, bn.running_var, bn.weight, bn.bias,
+                     bn.training, bn.momentum, bn.eps)
+    if residual is not None:
+        y = y + residual.float()
+    if relu:
+        y = F.relu(y)
+    return y.to(x.dtype)
+
+
+def _nhwc(t):
+    """[N, C, H, W] channels-last (or [M, C]) tensor -> (t, its [M, C] row-major storage view)."""
+    if t.dim() == 4:
+        if not t.is_contiguous(memory_format=torch.channels_last):
+            t = t.contiguous(memory_format=torch.channels_last)
+        t2 = t.permute(0, 2, 3, 1).reshape(-1, t.shape[1])
+    else:
+        t = t2 = t.contiguous()
+    if t2.data_ptr() % 16:
+        t = t.clone(memory_format=torch.channels_last) if t.dim() == 4 else t.clone()
+        return _nhwc(t)
+    return t, t2
+
+
+class _BNActFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, res, w, b, run_mean, run_var, momentum, eps, relu):
+        k = _native.kernels()
+        x, x2 = _nhwc(x)
+        M, C = x2.shape
+        G = k("edl_bn_groups", M, C)
+        if G <= 0:
+            raise ValueError(f"batchnorm kernel: unsupported channel count {C} (needs C % 8 == 0, C <= 2048)")
+        if x.dtype != torch.bfloat16 or w.dtype != torch.float32:
+            raise TypeError("batchnorm kernel expects bf16 activations and fp32 weight / statistics")
+        r2 = None
+        if res is not None:
+            res, r2 = _nhwc(res)
+        z = torch.empty_like(x)
+        dev = x.device
+        mean = torch.empty(C, dtype=torch.float32, device=dev)
+        rstd = torch.empty(C, dtype=torch.float32, device=dev)
+        coef = torch.empty(2 * C, dtype=torch.float32, device=dev)
+        part = torch.empty(2 * C * G, dtype=torch.float32, device=dev)
+        k.check("edl_bn_fwd_train", x.data_ptr(), _native.ptr(r2), z.data_ptr(), w.data_ptr(), b.data_ptr(),
+                run_mean.data_ptr(), run_var.data_ptr(), mean.data_ptr(), rstd.data_ptr(), coef.data_ptr(),
+                part.data_ptr(), M, C, momentum, eps, int(relu), _native.stream_of(x))
+        ctx.save_for_backward(x, z if relu else None, w, mean, rstd)
+        ctx.relu, ctx.has_res = relu, res is not None
+        return z
+
+    @staticmethod
+    def backward(ctx, dz):
+        k = _native.kernels()
+        x, z, w, mean, rstd = ctx.saved_tensors
+        dz, dz2 = _nhwc(dz)
+        x2 = _nhwc(x)[1]
+        M, C = x2.shape
+        G = k("edl_bn_groups", M, C)
+        dev = x.device
+        dx = torch.empty_like(x)
+        dres = torch.empty_like(x) if ctx.has_res and ctx.needs_input_grad[1] else None
+        dw = torch.empty(C, dtype=torch.float32, device=dev)
+        db = torch.empty(C, dtype=torch.float32, device=dev)
+        coef = torch.empty(3 * C, dtype=torch.float32, device=dev)
+        part = torch.empty(2 * C * G, dtype=torch.float32, device=dev)
+        k.check("edl_bn_bwd", dz2.data_ptr(), _native.ptr(z), x.data_ptr(), w.data_ptr(), mean.data_ptr(),
+                rstd.data_ptr(), dx.data_ptr(), _native.ptr(dres), dw.data_ptr(), db.data_ptr(), coef.data_ptr(),
+                part.data_ptr(), M, C, int(ctx.relu), _native.stream_of(x))
+        return (dx, dres, dw if ctx.needs_input_grad[2] else None, db if ctx.needs_input_grad[3] else None,
+                None, None, None, None, None)
+
+
+def _eval_coef(bn):
+    scale = bn.weight.float() * torch.rsqrt(bn.running_var.float() + bn.eps)
+    return torch.cat([scale, bn.bias.float() - bn.running_mean.float() * scale]).contiguous()
+
+
+def bn_act(x, bn: torch.nn.BatchNorm2d, residual=None, relu: bool = True):
+    """``relu(bn(x) + residual)`` (residual / relu optional) with ``bn``'s parameters and buffers."""
+    if not _native.use_hip(x):
+        return bn_act_ref(x, bn, residual, relu)
+    if bn.training:
+        if bn.momentum is None:
+            raise ValueError("bn_act: cumulative moving average (momentum=None) is not supported")
+        bn.num_batches_tracked.add_(1)
+        return _BNActFn.apply(x, residual, bn.weight, bn.bias, bn.running_mean, bn.running_var,
+                              float(bn.momentum), float(bn.eps), relu)
+    if torch.is_grad_enabled() and (x.requires_grad or (residual is not None and residual.requires_grad)
+                                    or bn.weight.requires_grad):
+        # frozen statistics but gradients wanted: differentiable torch ops
+        c = _eval_coef(bn)
+        C = x.shape[1]
+        shape = (1, C, 1, 1) if x.dim() == 4 else (1, C)
+        y = x.float() * c[:C].view(shape) + c[C:].view(shape)
+        if residual is not None:
+            y = y + residual.float()
+        return (F.relu(y) if relu else y).to(x.dtype)
+    k = _native.kernels()
+    x, x2 = _nhwc(x)
+    M, C = x2.shape
+    r2 = _nhwc(residual)[1] if residual is not None else None
+    z = torch.empty_like(x)
+    k.check("edl_bn_apply", x.data_ptr(), _native.ptr(r2), z.data_ptr(), _eval_coef(bn).data_ptr(), M, C,
+            int(relu), _native.stream_of(x))
+    return z
