@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     a = ap.parse_args()
+    t_start = time.perf_counter()
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
     dev = torch.device("cuda", local) if torch.cuda.is_available() else torch.device("cpu")
@@ -77,6 +78,7 @@ def main():
                           "ms_per_step": round(el / a.steps * 1e3, 2), "per_gpu_batch": a.batch, "micro": micro,
                           "seq": a.seq if a.model != "resnet50" else None, "dtype": "bf16",
                           "loss": round(float(tr.last_loss), 4),
+                          "setup_and_warmup_s": round(marks[a.warmup] - t_start, 2),
                           "peak_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 2**30, 1)
                           if dev.type == "cuda" else 0}), flush=True)
     tr.close()

@@ -11,8 +11,10 @@
 // bf16 tensors at 16 B per lane.
 //
 // Work split: a thread owns 8 consecutive channels (one 16-B vector) of a row;
-// ROWS_PER_ITER = 256 / (C/8) rows of a block are read at once, so a block
-// keeps its per-channel coefficients in registers for its whole row range.
+// 256 / (C/8) rows of a block are read at once, so a block keeps its
+// per-channel coefficients in registers for its whole row range.  The two
+// reductions run on a (row block, channel chunk <= 256) grid, >= 256 rows per
+// block, and a 1024-thread finalize sums the per-block partials per channel.
 // Statistics are shifted by the running mean (sum (x - k), sum (x - k)^2 in
 // fp32 per thread, fp64 across threads and blocks), so E[x^2] - E[x]^2 does not
 // cancel once the running mean tracks the batch mean.  The backward sums
@@ -25,15 +27,18 @@ using namespace edl;
 namespace {
 
 constexpr int kThreads = 256;
+constexpr int kFinThreads = 1024;
 constexpr int kUnroll = 4;
 
+// thread -> (8-channel group, row lane) inside a chunk of Cb channels; the chunk is
+// blockIdx.y for the reductions (Cb = C for the elementwise kernels)
 struct Geo {
   int tpr, rpi, col8, r0;
   bool active;
-  __device__ __forceinline__ Geo(int C) {
-    tpr = C >> 3;
+  __device__ __forceinline__ Geo(int Cb, int chunk) {
+    tpr = Cb >> 3;
     rpi = kThreads / tpr;
-    col8 = threadIdx.x % tpr;
+    col8 = chunk * tpr + threadIdx.x % tpr;
     r0 = threadIdx.x / tpr;
     active = r0 < rpi;
   }
@@ -45,28 +50,64 @@ __device__ __forceinline__ void row_range(int64_t M, int rpi, int64_t& r, int64_
   end = min(M, r + per);
 }
 
-// Per-block column sums of two [rpi][C] fp32 register sets -> part[block][2][C].
-__device__ __forceinline__ void block_colsum2(const float (&a)[8], const float (&b)[8], const Geo& g, int C,
-                                              float* part) {
+// Per-block column sums of two [rpi][Cb] fp32 register sets -> part[blockIdx.x][2][C]
+// (this block's Cb channels)
+__device__ __forceinline__ void block_colsum2(const float (&a)[8], const float (&b)[8], const Geo& g, int Cb,
+                                              int C, float* part) {
   __shared__ float red[2][kThreads * 8];
+  const int lc = (threadIdx.x % g.tpr) * 8;
   if (g.active) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      red[0][g.r0 * C + g.col8 * 8 + j] = a[j];
-      red[1][g.r0 * C + g.col8 * 8 + j] = b[j];
+      red[0][g.r0 * Cb + lc + j] = a[j];
+      red[1][g.r0 * Cb + lc + j] = b[j];
     }
   }
   __syncthreads();
-  float* out = part + (int64_t)blockIdx.x * 2 * C;
-  for (int c = threadIdx.x; c < C; c += kThreads) {
+  float* out = part + (int64_t)blockIdx.x * 2 * C + blockIdx.y * Cb;
+  for (int c = threadIdx.x; c < Cb; c += kThreads) {
     float s = 0.f, q = 0.f;
     for (int r = 0; r < g.rpi; ++r) {
-      s += red[0][r * C + c];
-      q += red[1][r * C + c];
+      s += red[0][r * Cb + c];
+      q += red[1][r * Cb + c];
     }
     out[c] = s;
     out[C + c] = q;
   }
+}
+
+// sum over the G row-block partials of channel c: 16 lanes of a 1024-thread block per
+// channel, 4 independent fp64 chains per lane, then an LDS tree
+__device__ __forceinline__ void sum_partials(const float* __restrict__ part, int G, int C, double& s, double& q) {
+  __shared__ double red[2][kFinThreads];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63), gl = threadIdx.x >> 6;
+  double s4[4] = {}, q4[4] = {};
+  if (c < C) {
+    int i = gl;
+    for (; i + 48 < G; i += 64) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        s4[u] += (double)part[(int64_t)(i + 16 * u) * 2 * C + c];
+        q4[u] += (double)part[(int64_t)(i + 16 * u) * 2 * C + C + c];
+      }
+    }
+    for (; i < G; i += 16) {
+      s4[0] += (double)part[(int64_t)i * 2 * C + c];
+      q4[0] += (double)part[(int64_t)i * 2 * C + C + c];
+    }
+  }
+  red[0][threadIdx.x] = (s4[0] + s4[1]) + (s4[2] + s4[3]);
+  red[1][threadIdx.x] = (q4[0] + q4[1]) + (q4[2] + q4[3]);
+  __syncthreads();
+  for (int w = kFinThreads / 2; w >= 64; w >>= 1) {
+    if (threadIdx.x < w) {
+      red[0][threadIdx.x] += red[0][threadIdx.x + w];
+      red[1][threadIdx.x] += red[1][threadIdx.x + w];
+    }
+    __syncthreads();
+  }
+  s = red[0][threadIdx.x & 63];
+  q = red[1][threadIdx.x & 63];
 }
 
 __device__ __forceinline__ void load8f(const float* p, float (&f)[8]) {
@@ -81,8 +122,8 @@ __device__ __forceinline__ void load8f(const float* p, float (&f)[8]) {
 // ---------------------------------------------------------------------------- forward
 __global__ __launch_bounds__(kThreads) void bn_stats_kernel(const bf16_t* __restrict__ x,
                                                             const float* __restrict__ shift, int64_t M, int C,
-                                                            float* __restrict__ part) {
-  const Geo g(C);
+                                                            int Cb, float* __restrict__ part) {
+  const Geo g(Cb, blockIdx.y);
   float s[8] = {}, q[8] = {};
   if (g.active) {
     float k[8];
@@ -118,31 +159,18 @@ __global__ __launch_bounds__(kThreads) void bn_stats_kernel(const bf16_t* __rest
       }
     }
   }
-  block_colsum2(s, q, g, C, part);
+  block_colsum2(s, q, g, Cb, C, part);
 }
 
-// one thread per channel per quarter of the partials; fp64 accumulation
-__global__ __launch_bounds__(kThreads) void bn_stats_finalize_kernel(
+// per channel: fp64 sum of the partials -> mean, rstd, affine coefficients, running stats
+__global__ __launch_bounds__(kFinThreads) void bn_stats_finalize_kernel(
     const float* __restrict__ part, int G, int C, int64_t M, const float* __restrict__ w,
     const float* __restrict__ b, float* __restrict__ run_mean, float* __restrict__ run_var, float momentum,
     float eps, float* __restrict__ mean_out, float* __restrict__ rstd_out, float* __restrict__ coef) {
-  __shared__ double red[2][kThreads];
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63), gl = threadIdx.x >> 6;
-  double s = 0.0, q = 0.0;
-  if (c < C) {
-    for (int i = gl; i < G; i += 4) {
-      s += (double)part[(int64_t)i * 2 * C + c];
-      q += (double)part[(int64_t)i * 2 * C + C + c];
-    }
-  }
-  red[0][threadIdx.x] = s;
-  red[1][threadIdx.x] = q;
-  __syncthreads();
-  if (gl != 0 || c >= C) return;
-  for (int i = 1; i < 4; ++i) {
-    s += red[0][threadIdx.x + 64 * i];
-    q += red[1][threadIdx.x + 64 * i];
-  }
+  double s, q;
+  sum_partials(part, G, C, s, q);
+  const int c = blockIdx.x * 64 + threadIdx.x;
+  if (threadIdx.x >= 64 || c >= C) return;
   const double k = (double)run_mean[c];
   const double dm = s / (double)M;
   const double var = fmax(q / (double)M - dm * dm, 0.0);
@@ -163,7 +191,7 @@ __global__ __launch_bounds__(kThreads) void bn_apply_kernel(const bf16_t* __rest
                                                             const bf16_t* __restrict__ res,
                                                             const float* __restrict__ coef, int64_t M, int C,
                                                             bf16_t* __restrict__ z) {
-  const Geo g(C);
+  const Geo g(C, 0);
   if (!g.active) return;
   float sc[8], sh[8];
   load8f(coef + g.col8 * 8, sc);
@@ -195,8 +223,8 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(const bf16_t* _
                                                                  const bf16_t* __restrict__ z,
                                                                  const bf16_t* __restrict__ x,
                                                                  const float* __restrict__ mean, int64_t M, int C,
-                                                                 float* __restrict__ part) {
-  const Geo g(C);
+                                                                 int Cb, float* __restrict__ part) {
+  const Geo g(Cb, blockIdx.y);
   float s[8] = {}, q[8] = {};
   if (g.active) {
     float mu[8];
@@ -218,34 +246,21 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(const bf16_t* _
       }
     }
   }
-  block_colsum2(s, q, g, C, part);
+  block_colsum2(s, q, g, Cb, C, part);
 }
 
 // dbias = sum dp, dweight = rstd * sum dp (x - mean); dx = A dp - K1 x + K2 with
 // A = w rstd, K1 = w rstd^2 dweight / M, K2 = K1 mean - A dbias / M
-__global__ __launch_bounds__(kThreads) void bn_bwd_finalize_kernel(const float* __restrict__ part, int G, int C,
-                                                                   int64_t M, const float* __restrict__ w,
-                                                                   const float* __restrict__ mean,
-                                                                   const float* __restrict__ rstd,
-                                                                   float* __restrict__ dw, float* __restrict__ db,
-                                                                   float* __restrict__ coef) {
-  __shared__ double red[2][kThreads];
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63), gl = threadIdx.x >> 6;
-  double s = 0.0, q = 0.0;
-  if (c < C) {
-    for (int i = gl; i < G; i += 4) {
-      s += (double)part[(int64_t)i * 2 * C + c];
-      q += (double)part[(int64_t)i * 2 * C + C + c];
-    }
-  }
-  red[0][threadIdx.x] = s;
-  red[1][threadIdx.x] = q;
-  __syncthreads();
-  if (gl != 0 || c >= C) return;
-  for (int i = 1; i < 4; ++i) {
-    s += red[0][threadIdx.x + 64 * i];
-    q += red[1][threadIdx.x + 64 * i];
-  }
+__global__ __launch_bounds__(kFinThreads) void bn_bwd_finalize_kernel(const float* __restrict__ part, int G, int C,
+                                                                      int64_t M, const float* __restrict__ w,
+                                                                      const float* __restrict__ mean,
+                                                                      const float* __restrict__ rstd,
+                                                                      float* __restrict__ dw, float* __restrict__ db,
+                                                                      float* __restrict__ coef) {
+  double s, q;
+  sum_partials(part, G, C, s, q);
+  const int c = blockIdx.x * 64 + threadIdx.x;
+  if (threadIdx.x >= 64 || c >= C) return;
   const double rs = (double)rstd[c];
   const double gw = q * rs, gb = s;
   dw[c] = (float)gw;
@@ -263,7 +278,7 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_dx_kernel(const bf16_t* __res
                                                              const bf16_t* __restrict__ x,
                                                              const float* __restrict__ coef, int64_t M, int C,
                                                              bf16_t* __restrict__ dx, bf16_t* __restrict__ dres) {
-  const Geo g(C);
+  const Geo g(C, 0);
   if (!g.active) return;
   float A[8], K1[8], K2[8];
   load8f(coef + g.col8 * 8, A);
@@ -298,12 +313,29 @@ int blocks_for(int64_t M, int C, int min_rows_per_thread, int cap) {
 
 bool shape_ok(int64_t M, int C) { return M > 0 && C >= 8 && C % 8 == 0 && C <= 8 * kThreads; }
 
+// channel chunk of a reduction block: at most 32 8-channel groups (>= 8 rows per pass)
+int chunk_of(int C) {
+  const int t = C >> 3;
+  int d = t <= 32 ? t : 32;
+  while (t % d) --d;
+  return 8 * d;
+}
+
+// row blocks of a reduction: >= 256 rows each (the [2][C] partial stays < 1 % of the
+// data), <= ~1024 blocks over all channel chunks
+int row_blocks(int64_t M, int C) {
+  const int cc = C / chunk_of(C);
+  const int64_t cap = 1024 / cc > 0 ? 1024 / cc : 1;
+  const int64_t want = (M + 255) / 256;
+  return (int)(want < 1 ? 1 : want > cap ? cap : want);
+}
+
 }  // namespace
 
 extern "C" {
 
 // partial-sum slab size of the reductions: floats = 2 * C * edl_bn_groups(M, C)
-int edl_bn_groups(int64_t M, int C) { return shape_ok(M, C) ? blocks_for(M, C, 16, 1024) : 0; }
+int edl_bn_groups(int64_t M, int C) { return shape_ok(M, C) ? row_blocks(M, C) : 0; }
 
 // statistics + normalise (+ residual) (+ ReLU).  mean/rstd: fp32 [C] saved for the backward;
 // coef: fp32 [2C] scratch; part: fp32 [2C * edl_bn_groups].  running_mean is also the shift.
@@ -311,11 +343,11 @@ int edl_bn_fwd_train(const void* x, const void* res, void* z, const float* w, co
                      float* run_var, float* mean, float* rstd, float* coef, float* part, int64_t M, int C,
                      float momentum, float eps, int relu, hipStream_t s) {
   if (!shape_ok(M, C)) return (int)hipErrorInvalidValue;
-  const int G = edl_bn_groups(M, C);
-  bn_stats_kernel<<<G, kThreads, 0, s>>>((const bf16_t*)x, run_mean, M, C, part);
+  const int G = row_blocks(M, C), Cb = chunk_of(C);
+  bn_stats_kernel<<<dim3(G, C / Cb), kThreads, 0, s>>>((const bf16_t*)x, run_mean, M, C, Cb, part);
   EDL_LAUNCH_CHECK();
-  bn_stats_finalize_kernel<<<(C + 63) / 64, kThreads, 0, s>>>(part, G, C, M, w, b, run_mean, run_var, momentum,
-                                                               eps, mean, rstd, coef);
+  bn_stats_finalize_kernel<<<(C + 63) / 64, kFinThreads, 0, s>>>(part, G, C, M, w, b, run_mean, run_var,
+                                                                  momentum, eps, mean, rstd, coef);
   EDL_LAUNCH_CHECK();
   const int GA = blocks_for(M, C, 4, 2048);
 #define EDL_BN_APPLY(R, L)                                                                               \
@@ -358,15 +390,16 @@ int edl_bn_bwd(const void* dz, const void* z, const void* x, const float* w, con
                void* dx, void* dres, float* dw, float* db, float* coef, float* part, int64_t M, int C, int relu,
                hipStream_t s) {
   if (!shape_ok(M, C) || (relu && z == nullptr)) return (int)hipErrorInvalidValue;
-  const int G = edl_bn_groups(M, C);
+  const int G = row_blocks(M, C), Cb = chunk_of(C);
+  const dim3 grid(G, C / Cb);
   if (relu)
-    bn_bwd_reduce_kernel<true><<<G, kThreads, 0, s>>>((const bf16_t*)dz, (const bf16_t*)z, (const bf16_t*)x, mean,
-                                                      M, C, part);
+    bn_bwd_reduce_kernel<true><<<grid, kThreads, 0, s>>>((const bf16_t*)dz, (const bf16_t*)z, (const bf16_t*)x,
+                                                         mean, M, C, Cb, part);
   else
-    bn_bwd_reduce_kernel<false><<<G, kThreads, 0, s>>>((const bf16_t*)dz, nullptr, (const bf16_t*)x, mean, M, C,
-                                                       part);
+    bn_bwd_reduce_kernel<false><<<grid, kThreads, 0, s>>>((const bf16_t*)dz, nullptr, (const bf16_t*)x, mean, M,
+                                                          C, Cb, part);
   EDL_LAUNCH_CHECK();
-  bn_bwd_finalize_kernel<<<(C + 63) / 64, kThreads, 0, s>>>(part, G, C, M, w, mean, rstd, dw, db, coef);
+  bn_bwd_finalize_kernel<<<(C + 63) / 64, kFinThreads, 0, s>>>(part, G, C, M, w, mean, rstd, dw, db, coef);
   EDL_LAUNCH_CHECK();
   const int GA = blocks_for(M, C, 4, 2048);
 #define EDL_BN_DX(L, D)                                                                                        \

@@ -74,6 +74,9 @@ class ResNet(nn.Module):
 
 
 def resnet50(device=None, dtype=torch.bfloat16, num_classes=1000) -> ResNet:
+    if device is not None and torch.device(device).type == "cuda":
+        from easydl_amd.ops import conv_tuning
+        conv_tuning.install()   # MIOpen's solver search for these shapes, done once on gfx950
     m = ResNet(num_classes=num_classes)
     m = m.to(device=device, dtype=dtype)
     if device is not None and torch.device(device).type == "cuda":

@@ -1,4 +1,6 @@
-"""Job feature extraction (meta-device model analysis) feeding the Brain."""
+"""Job feature extraction (meta-device model analysis) feeding the Brain; shipped tuning files."""
+import os
+
 from easydl_amd.api.spec import ElasticJob
 from easydl_amd.brain.collectors import GpuInfo, NodeInventory
 from easydl_amd.brain.planner import JobFeatures, Planner
@@ -65,3 +67,19 @@ def test_gemm_tuning_select_file_is_curated(monkeypatch):
     assert entries and all(e[0].startswith("GemmTunableOp_BFloat16") and e[2].startswith("Gemm_Hipblaslt")
                            for e in entries)
     assert any(e[1] == "tn_14336_4096_16384_ld_16384_16384_14336" for e in entries)   # down-proj wgrad
+
+
+def test_shipped_miopen_find_db_installs_into_a_scratch_copy(monkeypatch, tmp_path):
+    import tempfile
+    from easydl_amd.ops import conv_tuning
+    monkeypatch.delenv("MIOPEN_USER_DB_PATH", raising=False)
+    monkeypatch.delenv("EDL_MIOPEN_DB", raising=False)
+    monkeypatch.setattr(tempfile, "tempdir", str(tmp_path))
+    d = conv_tuning.install()
+    assert d is not None and os.environ["MIOPEN_USER_DB_PATH"] == d and d.startswith(str(tmp_path))
+    assert any(f.endswith(".ufdb.txt") for f in os.listdir(d))
+    monkeypatch.setenv("MIOPEN_USER_DB_PATH", "/elsewhere")            # a user's own db wins
+    assert conv_tuning.install() is None and os.environ["MIOPEN_USER_DB_PATH"] == "/elsewhere"
+    monkeypatch.delenv("MIOPEN_USER_DB_PATH")
+    monkeypatch.setenv("EDL_MIOPEN_DB", "0")
+    assert conv_tuning.install() is None and "MIOPEN_USER_DB_PATH" not in os.environ
