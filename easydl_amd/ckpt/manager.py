@@ -230,6 +230,9 @@ class CheckpointManager:
         opt = trainer.opt.state_tensors()
         out = [(f"model.{g.name}", g.data) for g in trainer.flat.groups if f"opt.{g.name}.master" not in opt]
         out += list(opt.items())
+        bufs = getattr(trainer, "bufs", None)
+        if bufs is not None:
+            out += [(f"model.buffers.{k}", t) for k, t in bufs.tensors.items()]
         return out
 
     @staticmethod

@@ -174,3 +174,38 @@ class FlatParams:
 
     def num_params(self) -> int:
         return sum(s.numel for _, s in self.named_slots())
+
+
+class FlatBuffers:
+    """Persistent module buffers (BatchNorm running statistics and batch counters)
+    re-homed into one flat tensor per dtype, the way :class:`FlatParams` does for
+    parameters.  The trainer adds these tensors to the training state, so they
+    reach joiners in the state broadcast and go into in-memory snapshots and
+    persisted checkpoints.  The reference leaves the checkpoint contents undefined
+    (SURVEY.md §5.4); without this a replacement worker would restart its running
+    statistics from their initial values.  Non-persistent buffers (derived tables)
+    stay where they are."""
+
+    def __init__(self, module: torch.nn.Module):
+        by_dtype: dict[torch.dtype, list] = {}
+        seen = set()
+        for mod in module.modules():
+            skip = getattr(mod, "_non_persistent_buffers_set", set())
+            for name, b in mod._buffers.items():
+                if b is None or name in skip:
+                    continue
+                if id(b) in seen:
+                    raise ValueError(f"buffer {name} is registered by more than one module")
+                seen.add(id(b))
+                by_dtype.setdefault(b.dtype, []).append((mod, name, b))
+        self.tensors: dict[str, torch.Tensor] = {}
+        for dt, items in by_dtype.items():
+            flat = torch.empty(sum(b.numel() for _, _, b in items), dtype=dt, device=items[0][2].device)
+            off = 0
+            with torch.no_grad():
+                for mod, name, b in items:
+                    view = flat[off:off + b.numel()].view(b.shape)
+                    view.copy_(b)
+                    mod._buffers[name] = view
+                    off += b.numel()
+            self.tensors[str(dt).replace("torch.", "")] = flat

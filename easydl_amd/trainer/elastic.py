@@ -37,7 +37,7 @@ from easydl_amd.master.store import KV, make_tcp_store
 from easydl_amd.optim import FlatAdamW, FlatSGD, LRSchedule
 from easydl_amd.parallel.comm import CommAborted, Communicator, LocalCommunicator, build_mesh
 from easydl_amd.parallel.ddp import ElasticDDP
-from easydl_amd.parallel.flat import FlatParams
+from easydl_amd.parallel.flat import FlatBuffers, FlatParams
 from easydl_amd.trainer.context import TrainerContext
 from easydl_amd.trainer.data import ElasticBatchPlan
 from easydl_amd.utils import fault, trace
@@ -95,7 +95,7 @@ class ElasticTrainer:
         self.held_tp = None          # TP rank whose parameter shard this process holds
         self.ckpt_tag = ""
         self.dp_comm = None
-        self.model = self.flat = self.opt = self.ddp = None
+        self.model = self.flat = self.bufs = self.opt = self.ddp = None
         if self.tp == 1:
             self._build_model(0)
         else:
@@ -135,6 +135,7 @@ class ElasticTrainer:
             self.model = self._model_fn(self.device)
         t1 = time.perf_counter()
         self.flat = FlatParams(self.model, weight_decay=a["weight_decay"], grad_dtype=a["grad_dtype"])
+        self.bufs = FlatBuffers(self.model)
         if a["optimizer"] == "adamw":
             self.opt = FlatAdamW(self.flat, lr=a["lr"], betas=a["betas"], weight_decay=a["weight_decay"],
                                  max_grad_norm=a["max_grad_norm"], schedule=a["schedule"])
@@ -314,6 +315,7 @@ class ElasticTrainer:
     def _state_tensors(self) -> list[torch.Tensor]:
         ts = [g.data for g in self.flat.groups]
         ts += list(self.opt.state_tensors().values())
+        ts += list(self.bufs.tensors.values())
         return ts
 
     def _sync_state(self):

@@ -201,3 +201,54 @@ def test_world_change_reuses_the_pinned_segment(tmp_path):
     finally:
         ckpt.close()
         unlink_job_segments("ck")
+
+
+class _BNNet(torch.nn.Module):
+    def __init__(self, device=None):
+        super().__init__()
+        self.conv = torch.nn.Conv2d(3, 8, 3, padding=1, device=device)
+        self.bn = torch.nn.BatchNorm2d(8, device=device)
+        self.fc = torch.nn.Linear(8, 5, device=device)
+
+    def forward(self, x, y):
+        h = torch.relu(self.bn(self.conv(x))).mean((2, 3))
+        return torch.nn.functional.cross_entropy(self.fc(h), y)
+
+
+class _Images:
+    def __len__(self):
+        return 4096
+
+    def batch(self, idx, device="cpu"):
+        idx = list(idx)
+        g = torch.Generator().manual_seed(int(idx[0]))
+        return torch.randn(len(idx), 3, 6, 6, generator=g) * 3 + 1, torch.tensor([i % 5 for i in idx])
+
+
+def test_module_buffers_are_training_state(tmp_path):
+    """BatchNorm running statistics live in the flat buffer tensors that the snapshot,
+    the persisted checkpoint and the joiner state broadcast carry."""
+    unlink_job_segments("ckbn")
+
+    def mk(ck, seed):
+        ctx = TrainerContext(job="ckbn", run_dir=str(tmp_path))
+        return ElasticTrainer(lambda d: _BNNet(d), global_batch=8, micro_batch=4, lr=1e-2, device="cpu", ctx=ctx,
+                              checkpoint=ck, seed=seed)
+
+    ckpt = CheckpointManager("ckbn", interval=3, persist_dir=str(tmp_path / "disk"), persist_every=1)
+    try:
+        a = mk(ckpt, 1)
+        assert a.model.bn.running_mean.data_ptr() == a.bufs.tensors["float32"].data_ptr()
+        a.fit(lambda m, b: m(*b), _Images(), num_steps=6)
+        ckpt.wait()
+        rm, rv, nb = (a.model.bn.running_mean.clone(), a.model.bn.running_var.clone(),
+                      int(a.model.bn.num_batches_tracked))
+        assert nb == 12 and not torch.allclose(rm, torch.zeros_like(rm))
+        assert "model.buffers.float32" in dict(CheckpointManager.state_of(a))
+        ckpt._persist_thread.join()
+        c = mk(None, 7)
+        load_dir(str(tmp_path / "disk" / "step-6"), c)
+        assert torch.equal(c.model.bn.running_mean, rm) and torch.equal(c.model.bn.running_var, rv)
+        assert int(c.model.bn.num_batches_tracked) == nb
+    finally:
+        unlink_job_segments("ckbn")
