@@ -5,7 +5,7 @@ solver (Find), including its naive reference kernels. For ResNet-50 at batch 256
 on one MI355X that is 62 s before the first step (`profiles/r02_resnet50_miopen_db.txt`).
 That delays every elastic joiner and every replacement worker by the same amount.
 The search's winners are recorded in MIOpen's text find-db. With that file in
-place, MIOpen goes straight to the recorded solver: 1.85 s to the first timed step.
+place, MIOpen goes straight to the recorded solver: 3.4 s to the first timed step on a fresh box.
 
 MIOpen also writes to its user db, so :func:`install` copies the shipped file
 into a per-user scratch directory and points ``MIOPEN_USER_DB_PATH`` there. It
