@@ -45,29 +45,49 @@ constexpr int HD = 128;        // head dim
 constexpr float LOG2E = 1.4426950408889634f;
 constexpr float LN2 = 0.6931471805599453f;
 
-// byte offset of 16-B chunk c of row r in a [rows][256 B] LDS tile
-__device__ __forceinline__ int swz(int r, int c) {
-  return (r << 8) + ((c ^ (((r & 3) << 2) | ((r >> 2) & 3))) << 4);
+// byte offset of 16-B chunk c of row r in a [rows][2*D B] LDS tile.  D = 128: 256-B
+// rows, XOR-swizzled so the 32x32x16 fragments' ds_read_b128 row reads and
+// ds_read_b64_tr_b16 transposed reads are both conflict-free (guide §5.5 T10 (b)).
+// D = 64: 128-B rows, two per 256-B bank window; x(r) = ((r>>2)&3) | (((r>>1)&1)<<2)
+// gives every 16-lane b128 pass (rows l&31 of one chunk) and every 32-lane tr_b16
+// pass (4 rows x 4 chunks) 16 distinct 16-B bank groups (MI355X_MICROARCH.md LDS table).
+template <int D>
+__device__ __forceinline__ int swzd(int r, int c) {
+  if constexpr (D == 128)
+    return (r << 8) + ((c ^ (((r & 3) << 2) | ((r >> 2) & 3))) << 4);
+  else
+    return (r << 7) + ((c ^ (((r >> 2) & 3) | (((r >> 1) & 1) << 2))) << 4);
 }
+template <int D>
+__device__ __forceinline__ int swz_x(int r) {   // the XOR of row r (LDS-DMA lane -> chunk)
+  if constexpr (D == 128)
+    return ((r & 3) << 2) | ((r >> 2) & 3);
+  else
+    return ((r >> 2) & 3) | (((r >> 1) & 1) << 2);
+}
+__device__ __forceinline__ int swz(int r, int c) { return swzd<128>(r, c); }
 
 __device__ __forceinline__ f32x16 mfma(const bf16x8& a, const bf16x8& b, const f32x16& c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
 
 // A/B operand "row read": 8 bf16 of row r, k-step s (16 elements), lane half h
+template <int D = 128>
 __device__ __forceinline__ bf16x8 row_read(const char* tile, int r, int s, int h) {
-  return *reinterpret_cast<const bf16x8*>(tile + swz(r, 2 * s + h));
+  return *reinterpret_cast<const bf16x8*>(tile + swzd<D>(r, 2 * s + h));
 }
 
 // A operand with rows = d (32*dt + lane&31) and k = rows kb.. of a row-major
 // [k][d] tile in the permuted order of an accumulator-as-B operand:
 // element j <-> k row kb + 8*(j>>2) + (j&3).
+template <int D = 128>
 __device__ __forceinline__ bf16x8 tr_read(const char* tile, int kb, int dt, int lane) {
   const int i = lane & 15, qq = i >> 2, p = i & 3;
   const int col = dt * 32 + ((lane >> 4) & 1) * 16 + 4 * p;
   const int c = col >> 3, half = (col >> 2) & 1;
-  const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(tile + swz(kb + qq, c) + half * 8));
-  const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(tile + swz(kb + 8 + qq, c) + half * 8));
+  const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(tile + swzd<D>(kb + qq, c) + half * 8));
+  const i16x4 hi =
+      __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(tile + swzd<D>(kb + 8 + qq, c) + half * 8));
   const i16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
   return __builtin_bit_cast(bf16x8, v);
 }
@@ -171,15 +191,17 @@ __device__ __forceinline__ void buffer_load_lds4(rsrc_t rs, void* lds, uint32_t 
 #endif
 }
 
-template <int ROWS, int NWAVES>
+template <int ROWS, int NWAVES, int D = 128>
 struct DmaPlan {
-  static constexpr int PER_WAVE = ROWS / 4 / NWAVES;
+  static constexpr int LPR = D / 8;                  // lanes (16-B chunks) per row
+  static constexpr int RPP = 64 / LPR;               // rows per 1-KiB piece
+  static constexpr int PER_WAVE = ROWS / RPP / NWAVES;
   uint32_t voff[PER_WAVE];
   __device__ __forceinline__ DmaPlan(int64_t stride_elems, int w, int lane) {
 #pragma unroll
     for (int i = 0; i < PER_WAVE; ++i) {
-      const int r = 4 * (w * PER_WAVE + i) + (lane >> 4);
-      const int c = (lane & 15) ^ (((r & 3) << 2) | ((r >> 2) & 3));
+      const int r = RPP * (w * PER_WAVE + i) + lane / LPR;
+      const int c = (lane % LPR) ^ swz_x<D>(r);
       voff[i] = (uint32_t)((r * stride_elems + c * 8) * 2);
     }
   }
@@ -204,9 +226,10 @@ __device__ __forceinline__ bf16x8 load_frag(const bf16_t* rowp, int s, int h) {
 }
 
 // write an O^T-style accumulator set (rows d, col = this lane's token) as 4-element runs
-__device__ __forceinline__ void store_accT(bf16_t* rowp, const f32x16 (&acc)[4], float mul, int h) {
+template <int ND>
+__device__ __forceinline__ void store_accT(bf16_t* rowp, const f32x16 (&acc)[ND], float mul, int h) {
 #pragma unroll
-  for (int dt = 0; dt < 4; ++dt) {
+  for (int dt = 0; dt < ND; ++dt) {
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       u32x2 w;
@@ -222,16 +245,17 @@ __device__ __forceinline__ void store_accT(bf16_t* rowp, const f32x16 (&acc)[4],
 // for O^T.  The per-tile VALU work is kept to ~4 instructions per score
 // (max3, fma+exp, add, half a cvt_pk): masks only on the diagonal / tail tile.
 // ---------------------------------------------------------------------------
-template <bool MASK, bool CAUSAL>
-__device__ __forceinline__ void fwd_tile(const char* Ks, const char* Vs, const bf16x8 (&qf)[8], f32x16 (&oacc)[4],
-                                         float& m, float& lsum, int kv0, int qr, int S, float sl2, int lane) {
+template <bool MASK, bool CAUSAL, int D>
+__device__ __forceinline__ void fwd_tile(const char* Ks, const char* Vs, const bf16x8 (&qf)[D / 16],
+                                         f32x16 (&oacc)[D / 32], float& m, float& lsum, int kv0, int qr, int S,
+                                         float sl2, int lane) {
   const int h = lane >> 5, l31 = lane & 31;
   f32x16 sacc[2];
   sacc[0] = sacc[1] = f32x16{};
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
 #pragma unroll
-    for (int s = 0; s < 8; ++s) sacc[t] = mfma(row_read(Ks, 32 * t + l31, s, h), qf[s], sacc[t]);
+    for (int s = 0; s < D / 16; ++s) sacc[t] = mfma(row_read<D>(Ks, 32 * t + l31, s, h), qf[s], sacc[t]);
   }
   if (MASK) {
 #pragma unroll
@@ -262,7 +286,7 @@ __device__ __forceinline__ void fwd_tile(const char* Ks, const char* Vs, const b
     m = mnew;
     lsum *= alpha;
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt) oacc[dt] *= alpha;
+    for (int dt = 0; dt < D / 32; ++dt) oacc[dt] *= alpha;
   }
   const float negm = -m;
   float ps = 0.f;
@@ -282,18 +306,20 @@ __device__ __forceinline__ void fwd_tile(const char* Ks, const char* Vs, const b
     for (int s2 = 0; s2 < 2; ++s2) {
       const bf16x8 pb = acc_to_b(sacc[t], s2);
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) oacc[dt] = mfma(tr_read(Vs, 32 * t + 16 * s2 + 4 * h, dt, lane), pb, oacc[dt]);
+      for (int dt = 0; dt < D / 32; ++dt)
+        oacc[dt] = mfma(tr_read<D>(Vs, 32 * t + 16 * s2 + 4 * h, dt, lane), pb, oacc[dt]);
     }
   }
 }
 
-template <bool CAUSAL>
+template <bool CAUSAL, int D>
 __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
                                                           const bf16_t* __restrict__ v, bf16_t* __restrict__ o,
                                                           float* __restrict__ lse, int S, int H, int KV,
                                                           float scale_log2, int xcd) {
   constexpr int BQ = 128;
-  __shared__ __attribute__((aligned(16))) char smem[2 * 32768];
+  constexpr int TILE = 64 * 2 * D, STAGE = 2 * TILE;   // one 64-row K (or V) tile; K + V
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
   int qb, hq, b;
   grid_decode(xcd, H, KV, qb, hq, b);  // longest causal rows first
   const int hk = hq / (H / KV);
@@ -301,28 +327,28 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_t* __restri
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // provably wave-uniform
   const int q0 = qb * BQ;
   const int wq0 = q0 + 32 * w;  // first query of this wave
-  const int64_t qs = (int64_t)H * HD, ks = (int64_t)KV * HD;
-  const bf16_t* qp = q + (int64_t)b * S * qs + hq * HD;
-  const bf16_t* kp = k + (int64_t)b * S * ks + hk * HD;
-  const bf16_t* vp = v + (int64_t)b * S * ks + hk * HD;
+  const int64_t qs = (int64_t)H * D, ks = (int64_t)KV * D;
+  const bf16_t* qp = q + (int64_t)b * S * qs + hq * D;
+  const bf16_t* kp = k + (int64_t)b * S * ks + hk * D;
+  const bf16_t* vp = v + (int64_t)b * S * ks + hk * D;
 
   const int qr = wq0 + l31;
-  bf16x8 qf[8];
+  bf16x8 qf[D / 16];
 #pragma unroll
-  for (int s = 0; s < 8; ++s) qf[s] = load_frag(qp + (int64_t)min(qr, S - 1) * qs, s, h);
+  for (int s = 0; s < D / 16; ++s) qf[s] = load_frag(qp + (int64_t)min(qr, S - 1) * qs, s, h);
   const int kv_end = CAUSAL ? min(S, q0 + BQ) : S;
   const int ntiles = (kv_end + 63) / 64;
-  f32x16 oacc[4];
+  f32x16 oacc[D / 32];
   float m = -1e30f, lsum = 0.f;
 #pragma unroll
-  for (int dt = 0; dt < 4; ++dt) oacc[dt] = f32x16{};
+  for (int dt = 0; dt < D / 32; ++dt) oacc[dt] = f32x16{};
 
-  const DmaPlan<64, 4> plan(ks, w, lane);
-  const int64_t kv_bytes = ((int64_t)S * ks - hk * HD) * 2;
+  const DmaPlan<64, 4, D> plan(ks, w, lane);
+  const int64_t kv_bytes = ((int64_t)S * ks - hk * D) * 2;
   const rsrc_t krs = make_rsrc(kp, kv_bytes), vrs = make_rsrc(vp, kv_bytes);
   const uint32_t tile_bytes = (uint32_t)(64 * ks * 2);
   plan.issue(smem, krs, 0, w);
-  plan.issue(smem + 16384, vrs, 0, w);
+  plan.issue(smem + TILE, vrs, 0, w);
   wait_vm();
   __syncthreads();
 
@@ -339,12 +365,12 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_t* __restri
       constexpr int ST = decltype(stage)::value;   // == it & 1
       const int kv0 = it * 64;
       if (it + 1 < ntiles) {  // stage 1-ST was released by the previous barrier
-        plan.issue(smem + (1 - ST) * 32768, krs, (it + 1) * tile_bytes, w);
-        plan.issue(smem + (1 - ST) * 32768 + 16384, vrs, (it + 1) * tile_bytes, w);
+        plan.issue(smem + (1 - ST) * STAGE, krs, (it + 1) * tile_bytes, w);
+        plan.issue(smem + (1 - ST) * STAGE + TILE, vrs, (it + 1) * tile_bytes, w);
       }
-      const char* Ks = smem + ST * 32768;
+      const char* Ks = smem + ST * STAGE;
       if (!MASK || !CAUSAL || kv0 <= wq0 + 31)  // wave-uniform: tile visible to this wave
-        fwd_tile<MASK, CAUSAL>(Ks, Ks + 16384, qf, oacc, m, lsum, kv0, qr, S, scale_log2, lane);
+        fwd_tile<MASK, CAUSAL, D>(Ks, Ks + TILE, qf, oacc, m, lsum, kv0, qr, S, scale_log2, lane);
       wait_vm();
       __syncthreads();
     };
@@ -361,7 +387,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_t* __restri
   run(std::integral_constant<bool, true>{}, nfull, ntiles);
   const float ltot = xhalf_sum(lsum);
   if (qr < S) {
-    store_accT(o + (int64_t)b * S * qs + (int64_t)qr * qs + hq * HD, oacc, 1.f / ltot, h);
+    store_accT(o + (int64_t)b * S * qs + (int64_t)qr * qs + hq * D, oacc, 1.f / ltot, h);
     if (h == 0) lse[((int64_t)b * H + hq) * S + qr] = (m + log2f(ltot)) * LN2;
   }
 }
@@ -747,25 +773,27 @@ __global__ __launch_bounds__(256, 1) void attn_fwd64_kernel(const bf16_t* __rest
 }
 
 // ---------------------------------------------------------------------------
-// backward preprocess: delta = rowsum(dO * O)   (16 lanes per row, 16 B each)
+// backward preprocess: delta = rowsum(dO * O)   (D/8 lanes per row, 16 B each)
 // ---------------------------------------------------------------------------
+template <int D>
 __global__ __launch_bounds__(256) void attn_bwd_delta_kernel(const bf16_t* __restrict__ o,
                                                              const bf16_t* __restrict__ dout,
                                                              const float* __restrict__ lse,
                                                              float* __restrict__ delta, int S, int H,
                                                              int64_t nrows) {
-  const int64_t row = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 4;  // row = (b*S + s)*H + h
-  const int c = threadIdx.x & 15;
+  constexpr int LPR = D / 8;
+  const int64_t row = ((int64_t)blockIdx.x * 256 + threadIdx.x) / LPR;  // row = (b*S + s)*H + h
+  const int c = threadIdx.x % LPR;
   float acc = 0.f;
   if (row < nrows) {
     float a[8], d[8];
-    unpack8(reinterpret_cast<const u32x4*>(o + row * HD)[c], a);
-    unpack8(reinterpret_cast<const u32x4*>(dout + row * HD)[c], d);
+    unpack8(reinterpret_cast<const u32x4*>(o + row * D)[c], a);
+    unpack8(reinterpret_cast<const u32x4*>(dout + row * D)[c], d);
 #pragma unroll
     for (int i = 0; i < 8; ++i) acc += a[i] * d[i];
   }
 #pragma unroll
-  for (int off = 8; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 16);
+  for (int off = LPR / 2; off > 0; off >>= 1) acc += __shfl_xor(acc, off, LPR);
   if (c == 0 && row < nrows) {
     const int64_t hh = row % H, tok = row / H, s = tok % S, b = tok / S;
     const int64_t i = (b * H + hh) * S + s;
@@ -933,10 +961,10 @@ __device__ __forceinline__ void mfma_d_fence(f32x16 (&x)[2], f32x16 (&y)[2]) {
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 4" : "+v"(x[0]), "+v"(x[1]), "+v"(y[0]), "+v"(y[1]));
 }
 
-template <bool MASK, bool CAUSAL>
+template <bool MASK, bool CAUSAL, int D>
 __device__ __forceinline__ void dkdv64_slice(const char* Qs, const char* Ds, const float* NL,
-                                             const float* DL, int rb, const bf16x8 (&kf)[2][8],
-                                             const char* Vw, f32x16 (&dka)[2][4], f32x16 (&dva)[2][4],
+                                             const float* DL, int rb, const bf16x8 (&kf)[2][D / 16],
+                                             const char* Vw, f32x16 (&dka)[2][D / 32], f32x16 (&dva)[2][D / 32],
                                              int qs0, int key0, int S,
                                              float sl2, int lane) {
   const int h = lane >> 5, l31 = lane & 31;
@@ -947,8 +975,8 @@ __device__ __forceinline__ void dkdv64_slice(const char* Qs, const char* Ds, con
   asm volatile("" : "+v"(vo));
   const lds_char* Vl = (const lds_char*)(uintptr_t)vo;
 #pragma unroll
-  for (int s = 0; s < 8; ++s) {
-    const bf16x8 a = row_read(Qs, rb + l31, s, h);
+  for (int s = 0; s < D / 16; ++s) {
+    const bf16x8 a = row_read<D>(Qs, rb + l31, s, h);
     if (s == 0) {
       mfma_v_first(sa[0], a, kf[0][s]);
       mfma_v_first(sa[1], a, kf[1][s]);
@@ -958,10 +986,10 @@ __device__ __forceinline__ void dkdv64_slice(const char* Qs, const char* Ds, con
     }
   }
 #pragma unroll
-  for (int s = 0; s < 8; ++s) {
-    const bf16x8 a = row_read(Ds, rb + l31, s, h);
-    const bf16x8 v0 = *(lds_bf16x8*)(Vl + swz(l31, 2 * s + h));
-    const bf16x8 v1 = *(lds_bf16x8*)(Vl + swz(32 + l31, 2 * s + h));
+  for (int s = 0; s < D / 16; ++s) {
+    const bf16x8 a = row_read<D>(Ds, rb + l31, s, h);
+    const bf16x8 v0 = *(lds_bf16x8*)(Vl + swzd<D>(l31, 2 * s + h));
+    const bf16x8 v1 = *(lds_bf16x8*)(Vl + swzd<D>(32 + l31, 2 * s + h));
     if (s == 0) {
       mfma_v_first(dp[0], a, v0);
       mfma_v_first(dp[1], a, v1);
@@ -996,8 +1024,8 @@ __device__ __forceinline__ void dkdv64_slice(const char* Qs, const char* Ds, con
   for (int s2 = 0; s2 < 2; ++s2) {
     const bf16x8 p0 = acc_to_b(sa[0], s2), p1 = acc_to_b(sa[1], s2);
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt) {
-      const bf16x8 a = tr_read(Ds, rb + 16 * s2 + 4 * h, dt, lane);
+    for (int dt = 0; dt < D / 32; ++dt) {
+      const bf16x8 a = tr_read<D>(Ds, rb + 16 * s2 + 4 * h, dt, lane);
       dva[0][dt] = mfma(a, p0, dva[0][dt]);
       dva[1][dt] = mfma(a, p1, dva[1][dt]);
     }
@@ -1015,8 +1043,8 @@ __device__ __forceinline__ void dkdv64_slice(const char* Qs, const char* Ds, con
   for (int s2 = 0; s2 < 2; ++s2) {
     const bf16x8 d0 = acc_to_b(dp[0], s2), d1 = acc_to_b(dp[1], s2);
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt) {
-      const bf16x8 a = tr_read(Qs, rb + 16 * s2 + 4 * h, dt, lane);
+    for (int dt = 0; dt < D / 32; ++dt) {
+      const bf16x8 a = tr_read<D>(Qs, rb + 16 * s2 + 4 * h, dt, lane);
       dka[0][dt] = mfma(a, d0, dka[0][dt]);
       dka[1][dt] = mfma(a, d1, dka[1][dt]);
     }
@@ -1024,9 +1052,10 @@ __device__ __forceinline__ void dkdv64_slice(const char* Qs, const char* Ds, con
 }
 
 // fp32 variant of store_accT for the head-split partial sums
-__device__ __forceinline__ void store_accT_f32(float* rowp, const f32x16 (&acc)[4], float mul, int h) {
+template <int ND>
+__device__ __forceinline__ void store_accT_f32(float* rowp, const f32x16 (&acc)[ND], float mul, int h) {
 #pragma unroll
-  for (int dt = 0; dt < 4; ++dt) {
+  for (int dt = 0; dt < ND; ++dt) {
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       f32x4 w;
@@ -1045,7 +1074,7 @@ __device__ __forceinline__ void store_accT_f32(float* rowp, const f32x16 (&acc)[
 // fewer than ~2 workgroups per CU the GQA group's query heads are split over
 // `gsplit` workgroups that write fp32 partials to `ws`, summed by
 // attn_dkdv_reduce_kernel.
-template <bool CAUSAL>
+template <bool CAUSAL, int D>
 __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv64_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
     const bf16_t* __restrict__ dout, const float* __restrict__ lse, const float* __restrict__ delta,
@@ -1054,16 +1083,17 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv64_kernel(
   constexpr int QT = 64;   // queries per staged tile
   constexpr int KW = 64;   // keys per wave
   constexpr int KB = 4 * KW;
-  // [Q|dO] x 2 stages (64 KiB), softmax row terms (1 KiB), this block's V rows per wave (4 x 16 KiB)
-  __shared__ __attribute__((aligned(16))) char smem[2 * 32768 + 2 * 512 + 4 * 16384];
+  constexpr int TILE = 64 * 2 * D, STAGE = 2 * TILE;   // one 64-row Q (or dO, or V) tile; Q + dO
+  // [Q|dO] x 2 stages (64 KiB at D 128), softmax row terms (1 KiB), this block's V rows per wave (4 tiles)
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE + 2 * 512 + 4 * TILE];
   const int hk = blockIdx.y / gsplit, gs = blockIdx.y % gsplit, b = blockIdx.z;
   const int lane = threadIdx.x & 63, h = lane >> 5, l31 = lane & 31;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // provably wave-uniform
   const int heads = (H / KV) / gsplit, hq0 = hk * (H / KV) + gs * heads;
-  const int64_t qs = (int64_t)H * HD, ks = (int64_t)KV * HD;
+  const int64_t qs = (int64_t)H * D, ks = (int64_t)KV * D;
   const int nkb = (S + KB - 1) / KB, nqt = (S + QT - 1) / QT;
   const int64_t nBHS = (int64_t)gridDim.z * H * S;  // delta = [delta | -lse*log2e]
-  const DmaPlan<QT, 4> plan(qs, w, lane);
+  const DmaPlan<QT, 4, D> plan(qs, w, lane);
   const int blocks[2] = {(int)blockIdx.x, nkb - 1 - (int)blockIdx.x};
   const int nblocks = CAUSAL && blocks[1] != blocks[0] ? 2 : 1;
 #pragma unroll 1
@@ -1072,22 +1102,22 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv64_kernel(
     const int key0 = kb * KB + KW * w;   // first key of this wave
     // K stays in registers (B operand of S = Q K^T); V, the B operand of dP = dO V^T, goes to this
     // wave's LDS rows in the row_read layout: 64 fewer VGPRs for 16 more fragment reads per slice.
-    char* Vw = smem + 2 * 32768 + 2 * 512 + w * 16384;
-    bf16x8 kf[2][8];
+    char* Vw = smem + 2 * STAGE + 2 * 512 + w * TILE;
+    bf16x8 kf[2][D / 16];
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
-      const int64_t off = (int64_t)b * S * ks + (int64_t)min(key0 + 32 * t + l31, S - 1) * ks + hk * HD;
+      const int64_t off = (int64_t)b * S * ks + (int64_t)min(key0 + 32 * t + l31, S - 1) * ks + hk * D;
 #pragma unroll
-      for (int s = 0; s < 8; ++s) {
+      for (int s = 0; s < D / 16; ++s) {
         kf[t][s] = load_frag(k + off, s, h);
-        *reinterpret_cast<bf16x8*>(Vw + swz(32 * t + l31, 2 * s + h)) = load_frag(v + off, s, h);
+        *reinterpret_cast<bf16x8*>(Vw + swzd<D>(32 * t + l31, 2 * s + h)) = load_frag(v + off, s, h);
       }
     }
-    f32x16 dka[2][4], dva[2][4];
+    f32x16 dka[2][D / 32], dva[2][D / 32];
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
+      for (int dt = 0; dt < D / 32; ++dt) {
         dka[t][dt] = f32x16{};
         dva[t][dt] = f32x16{};
       }
@@ -1098,12 +1128,12 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv64_kernel(
     auto fetch = [&](int j, int st) {
       const int hq = hq0 + j / per_head;
       const int q0 = (qt0 + j % per_head) * QT;
-      char* base = smem + st * 32768;
-      const int64_t off = (int64_t)b * S * qs + hq * HD, nbytes = ((int64_t)S * qs - hq * HD) * 2;
+      char* base = smem + st * STAGE;
+      const int64_t off = (int64_t)b * S * qs + hq * D, nbytes = ((int64_t)S * qs - hq * D) * 2;
       const uint32_t soff = (uint32_t)(q0 * qs * 2);
       plan.issue(base, make_rsrc(q + off, nbytes), soff, w);
-      plan.issue(base + 16384, make_rsrc(dout + off, nbytes), soff, w);
-      float* lf = reinterpret_cast<float*>(smem + 2 * 32768 + st * 512);
+      plan.issue(base + TILE, make_rsrc(dout + off, nbytes), soff, w);
+      float* lf = reinterpret_cast<float*>(smem + 2 * STAGE + st * 512);
       const int64_t row0 = ((int64_t)b * H + hq) * S;
       if (w == 0) dma_f32x64(lf, make_rsrc(delta + nBHS + row0, (int64_t)S * 4), q0, lane);
       if (w == 1) dma_f32x64(lf + QT, make_rsrc(delta + row0, (int64_t)S * 4), q0, lane);
@@ -1118,15 +1148,16 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv64_kernel(
       auto step = [&](int j, auto stage) {
         constexpr int ST = decltype(stage)::value;   // == j & 1
         if (j + 1 < total) fetch(j + 1, 1 - ST);
-        const char* Qs = smem + ST * 32768;
-        const char* Ds = Qs + 16384;
-        const float* NL = reinterpret_cast<const float*>(smem + 2 * 32768 + ST * 512);
+        const char* Qs = smem + ST * STAGE;
+        const char* Ds = Qs + TILE;
+        const float* NL = reinterpret_cast<const float*>(smem + 2 * STAGE + ST * 512);
         const int q0 = (qt0 + j % per_head) * QT;
 #pragma unroll 1
         for (int sub = 0; sub < QT / 32; ++sub) {
           const int qs0 = q0 + 32 * sub;
           if (CAUSAL && qs0 + 31 < key0) continue;  // wave-uniform: every key of the wave is after every query
-          dkdv64_slice<MASK, CAUSAL>(Qs, Ds, NL, NL + QT, 32 * sub, kf, Vw, dka, dva, qs0, key0, S, scale_log2, lane);
+          dkdv64_slice<MASK, CAUSAL, D>(Qs, Ds, NL, NL + QT, 32 * sub, kf, Vw, dka, dva, qs0, key0, S, scale_log2,
+                                        lane);
         }
         wait_vm();
         __syncthreads();   // also fences the LDS buffers before the next block's first fetch
@@ -1156,28 +1187,29 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv64_kernel(
       const int mykey = key0 + 32 * t + l31;
       if (mykey >= S) continue;
       if (gsplit == 1) {
-        store_accT(dk + (int64_t)b * S * ks + (int64_t)mykey * ks + hk * HD, dka[t], scale, h);
-        store_accT(dv + (int64_t)b * S * ks + (int64_t)mykey * ks + hk * HD, dva[t], 1.f, h);
-      } else {  // ws[gs][b][key][hk][dk|dv][HD]
-        float* row = ws + ((((int64_t)gs * gridDim.z + b) * S + mykey) * KV + hk) * 2 * HD;
+        store_accT(dk + (int64_t)b * S * ks + (int64_t)mykey * ks + hk * D, dka[t], scale, h);
+        store_accT(dv + (int64_t)b * S * ks + (int64_t)mykey * ks + hk * D, dva[t], 1.f, h);
+      } else {  // ws[gs][b][key][hk][dk|dv][D]
+        float* row = ws + ((((int64_t)gs * gridDim.z + b) * S + mykey) * KV + hk) * 2 * D;
         store_accT_f32(row, dka[t], scale, h);
-        store_accT_f32(row + HD, dva[t], 1.f, h);
+        store_accT_f32(row + D, dva[t], 1.f, h);
       }
     }
   }
 }
 
 // sum the head-split partials: ws[g][b][key][kv][2][HD] fp32 -> dk, dv bf16 (8 elements per thread)
+template <int D>
 __global__ __launch_bounds__(256) void attn_dkdv_reduce_kernel(const float* __restrict__ ws, bf16_t* __restrict__ dk,
                                                                bf16_t* __restrict__ dv, int64_t nrows, int gsplit) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;   // one 8-element chunk of a [2*HD] row
-  constexpr int CH = 2 * HD / 8;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;   // one 8-element chunk of a [2*D] row
+  constexpr int CH = 2 * D / 8;
   if (i >= nrows * CH) return;
   const int64_t row = i / CH;
   const int c = (int)(i % CH);
   f32x4 a = {}, bq = {};
   for (int g = 0; g < gsplit; ++g) {
-    const float* src = ws + ((int64_t)g * nrows + row) * 2 * HD + 8 * c;
+    const float* src = ws + ((int64_t)g * nrows + row) * 2 * D + 8 * c;
     a += *reinterpret_cast<const f32x4*>(src);
     bq += *reinterpret_cast<const f32x4*>(src + 4);
   }
@@ -1186,7 +1218,7 @@ __global__ __launch_bounds__(256) void attn_dkdv_reduce_kernel(const float* __re
   o[1] = pack2(a[2], a[3]);
   o[2] = pack2(bq[0], bq[1]);
   o[3] = pack2(bq[2], bq[3]);
-  bf16_t* dst = (8 * c < HD ? dk : dv) + row * HD + (8 * c) % HD;
+  bf16_t* dst = (8 * c < D ? dk : dv) + row * D + (8 * c) % D;
   *reinterpret_cast<u32x4*>(dst) = o;
 }
 
@@ -1194,19 +1226,19 @@ __global__ __launch_bounds__(256) void attn_dkdv_reduce_kernel(const float* __re
 // backward: dQ (a wave owns 32 queries; the forward's structure with
 // dP^T = V dO^T and dQ^T += K^T dS^T)
 // ---------------------------------------------------------------------------
-template <bool MASK, bool CAUSAL>
-__device__ __forceinline__ void dq_tile(const char* Ks, const char* Vs, const bf16x8 (&qf)[8], const bf16x8 (&df)[8],
-                                        f32x16 (&dqa)[4], float nl2, float dl, int kv0, int qr, int S, float sl2,
-                                        int lane) {
+template <bool MASK, bool CAUSAL, int D>
+__device__ __forceinline__ void dq_tile(const char* Ks, const char* Vs, const bf16x8 (&qf)[D / 16],
+                                        const bf16x8 (&df)[D / 16], f32x16 (&dqa)[D / 32], float nl2, float dl,
+                                        int kv0, int qr, int S, float sl2, int lane) {
   const int h = lane >> 5, l31 = lane & 31;
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
     f32x16 st = f32x16{}, dpt = f32x16{};
 #pragma unroll
-    for (int s = 0; s < 8; ++s) st = mfma(row_read(Ks, 32 * t + l31, s, h), qf[s], st);
+    for (int s = 0; s < D / 16; ++s) st = mfma(row_read<D>(Ks, 32 * t + l31, s, h), qf[s], st);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int s = 0; s < 8; ++s) dpt = mfma(row_read(Vs, 32 * t + l31, s, h), df[s], dpt);
+    for (int s = 0; s < D / 16; ++s) dpt = mfma(row_read<D>(Vs, 32 * t + l31, s, h), df[s], dpt);
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       float p = fast_exp2(__builtin_fmaf(st[i], sl2, nl2));
@@ -1220,7 +1252,8 @@ __device__ __forceinline__ void dq_tile(const char* Ks, const char* Vs, const bf
     for (int s2 = 0; s2 < 2; ++s2) {
       const bf16x8 db = acc_to_b(dpt, s2);
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) dqa[dt] = mfma(tr_read(Ks, 32 * t + 16 * s2 + 4 * h, dt, lane), db, dqa[dt]);
+      for (int dt = 0; dt < D / 32; ++dt)
+        dqa[dt] = mfma(tr_read<D>(Ks, 32 * t + 16 * s2 + 4 * h, dt, lane), db, dqa[dt]);
     }
     // keep the scheduler from hoisting the next half's 32 LDS reads over this
     // one (that overlap costs ~100 registers and spills at 2 waves/SIMD)
@@ -1228,13 +1261,14 @@ __device__ __forceinline__ void dq_tile(const char* Ks, const char* Vs, const bf
   }
 }
 
-template <bool CAUSAL>
+template <bool CAUSAL, int D>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
     const bf16_t* __restrict__ dout, const float* __restrict__ lse, const float* __restrict__ delta,
     bf16_t* __restrict__ dq, int S, int H, int KV, float scale_log2, float scale, int xcd) {
   constexpr int BQ = 128;
-  __shared__ __attribute__((aligned(16))) char smem[2 * 32768];
+  constexpr int TILE = 64 * 2 * D, STAGE = 2 * TILE;
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
   int qb, hq, b;
   grid_decode(xcd, H, KV, qb, hq, b);
   const int hk = hq / (H / KV);
@@ -1242,16 +1276,16 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(
   const int w = threadIdx.x >> 6;
   const int q0 = qb * BQ;
   const int wq0 = q0 + 32 * w;
-  const int64_t qs = (int64_t)H * HD, ks = (int64_t)KV * HD;
-  const bf16_t* kp = k + (int64_t)b * S * ks + hk * HD;
-  const bf16_t* vp = v + (int64_t)b * S * ks + hk * HD;
+  const int64_t qs = (int64_t)H * D, ks = (int64_t)KV * D;
+  const bf16_t* kp = k + (int64_t)b * S * ks + hk * D;
+  const bf16_t* vp = v + (int64_t)b * S * ks + hk * D;
   const int qr = wq0 + l31, qc = min(qr, S - 1);
-  bf16x8 qf[8], df[8];
+  bf16x8 qf[D / 16], df[D / 16];
   {
-    const bf16_t* qrow = q + (int64_t)b * S * qs + (int64_t)qc * qs + hq * HD;
-    const bf16_t* drow = dout + (int64_t)b * S * qs + (int64_t)qc * qs + hq * HD;
+    const bf16_t* qrow = q + (int64_t)b * S * qs + (int64_t)qc * qs + hq * D;
+    const bf16_t* drow = dout + (int64_t)b * S * qs + (int64_t)qc * qs + hq * D;
 #pragma unroll
-    for (int s = 0; s < 8; ++s) {
+    for (int s = 0; s < D / 16; ++s) {
       qf[s] = load_frag(qrow, s, h);
       df[s] = load_frag(drow, s, h);
     }
@@ -1259,17 +1293,17 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(
   const int64_t nBHS = (int64_t)gridDim.z * H * S;  // delta = [delta | -lse*log2e]
   const float dl = delta[((int64_t)b * H + hq) * S + qc];
   const float nl2 = delta[nBHS + ((int64_t)b * H + hq) * S + qc];
-  f32x16 dqa[4];
+  f32x16 dqa[D / 32];
 #pragma unroll
-  for (int dt = 0; dt < 4; ++dt) dqa[dt] = f32x16{};
+  for (int dt = 0; dt < D / 32; ++dt) dqa[dt] = f32x16{};
   const int kv_end = CAUSAL ? min(S, q0 + BQ) : S;
   const int ntiles = (kv_end + 63) / 64;
-  const DmaPlan<64, 4> plan(ks, w, lane);
-  const int64_t kv_bytes = ((int64_t)S * ks - hk * HD) * 2;
+  const DmaPlan<64, 4, D> plan(ks, w, lane);
+  const int64_t kv_bytes = ((int64_t)S * ks - hk * D) * 2;
   const rsrc_t krs = make_rsrc(kp, kv_bytes), vrs = make_rsrc(vp, kv_bytes);
   const uint32_t tile_bytes = (uint32_t)(64 * ks * 2);
   plan.issue(smem, krs, 0, w);
-  plan.issue(smem + 16384, vrs, 0, w);
+  plan.issue(smem + TILE, vrs, 0, w);
   wait_vm();
   __syncthreads();
   const int nfull = CAUSAL ? min(q0, S) / 64 : S / 64;  // see the forward
@@ -1279,12 +1313,12 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(
       constexpr int ST = decltype(stage)::value;   // == it & 1
       const int kv0 = it * 64;
       if (it + 1 < ntiles) {
-        plan.issue(smem + (1 - ST) * 32768, krs, (it + 1) * tile_bytes, w);
-        plan.issue(smem + (1 - ST) * 32768 + 16384, vrs, (it + 1) * tile_bytes, w);
+        plan.issue(smem + (1 - ST) * STAGE, krs, (it + 1) * tile_bytes, w);
+        plan.issue(smem + (1 - ST) * STAGE + TILE, vrs, (it + 1) * tile_bytes, w);
       }
-      const char* Ks = smem + ST * 32768;
+      const char* Ks = smem + ST * STAGE;
       if (!MASK || !CAUSAL || kv0 <= wq0 + 31)
-        dq_tile<MASK, CAUSAL>(Ks, Ks + 16384, qf, df, dqa, nl2, dl, kv0, qr, S, scale_log2, lane);
+        dq_tile<MASK, CAUSAL, D>(Ks, Ks + TILE, qf, df, dqa, nl2, dl, kv0, qr, S, scale_log2, lane);
       wait_vm();
       __syncthreads();
     };
@@ -1299,7 +1333,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(
   };
   run(std::integral_constant<bool, false>{}, 0, nfull);
   run(std::integral_constant<bool, true>{}, nfull, ntiles);
-  if (qr < S) store_accT(dq + (int64_t)b * S * qs + (int64_t)qr * qs + hq * HD, dqa, scale, h);
+  if (qr < S) store_accT(dq + (int64_t)b * S * qs + (int64_t)qr * qs + hq * D, dqa, scale, h);
 }
 
 }  // namespace
@@ -1314,38 +1348,19 @@ static int attn_xcd_map(int B, int KV) {
   return on && (B * KV) % 8 == 0 ? 1 : 0;
 }
 
-extern "C" {
-
-int edl_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int S, int H, int KV,
-                 int D, int causal, float scale, hipStream_t s) {
-  if (D != HD || H % KV != 0 || S <= 0) return (int)hipErrorInvalidValue;
-  const float sl2 = scale * LOG2E;
-  // EDL_ATTN_FWD=64: the software-pipelined 64-queries-per-wave kernel
-  const char* sel = getenv("EDL_ATTN_FWD");
-  if (sel && atoi(sel) == 64) {
-    dim3 g64((S + 255) / 256, H, B);
-    if (causal)
-      attn_fwd64_kernel<true><<<g64, 256, 0, s>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
-                                                     (bf16_t*)o, lse, S, H, KV, sl2);
-    else
-      attn_fwd64_kernel<false><<<g64, 256, 0, s>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
-                                                      (bf16_t*)o, lse, S, H, KV, sl2);
-    EDL_LAUNCH_CHECK();
-    return 0;
-  }
+template <int D>
+static void attn_fwd_launch(const void* q, const void* k, const void* v, void* o, float* lse, int B, int S, int H,
+                            int KV, int causal, float sl2, hipStream_t s) {
   dim3 grid((S + 127) / 128, H, B);
   const int xcd = attn_xcd_map(B, KV);
   if (causal)
-    attn_fwd_kernel<true><<<grid, 256, 0, s>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
-                                                   (bf16_t*)o, lse, S, H, KV, sl2, xcd);
+    attn_fwd_kernel<true, D><<<grid, 256, 0, s>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
+                                                      (bf16_t*)o, lse, S, H, KV, sl2, xcd);
   else
-    attn_fwd_kernel<false><<<grid, 256, 0, s>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
-                                                    (bf16_t*)o, lse, S, H, KV, sl2, xcd);
-  EDL_LAUNCH_CHECK();
-  return 0;
+    attn_fwd_kernel<false, D><<<grid, 256, 0, s>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
+                                                       (bf16_t*)o, lse, S, H, KV, sl2, xcd);
 }
 
-// delta: fp32 [2,B,H,S] scratch filled here (delta, -lse*log2(e)).
 // dK/dV-64 work decomposition (see attn_bwd_dkdv64_kernel): returns gsplit, fills the grid
 static int dkdv64_plan(int B, int S, int H, int KV, int causal, dim3* grid) {
   constexpr int kCUs = 256;   // MI355X: 8 XCDs x 32 CUs
@@ -1364,21 +1379,14 @@ static int dkdv_keys_per_wave() {
   return kpw;
 }
 
-// fp32 workspace the backward needs for the head-split dK/dV partials (0 = none)
-int64_t edl_attn_bwd_ws_bytes(int B, int S, int H, int KV, int causal) {
-  if (dkdv_keys_per_wave() != 64 || KV <= 0 || H % KV != 0) return 0;
-  const int g = dkdv64_plan(B, S, H, KV, causal, nullptr);
-  return g == 1 ? 0 : (int64_t)g * B * S * KV * 2 * HD * 4;
-}
-
-int edl_attn_bwd(const void* q, const void* k, const void* v, const void* o, const void* dout, const float* lse,
-                 float* delta, void* dq, void* dk, void* dv, float* ws, int B, int S, int H, int KV, int D,
-                 int causal, float scale, hipStream_t s) {
-  if (D != HD || H % KV != 0 || S <= 0) return (int)hipErrorInvalidValue;
-  if (edl_attn_bwd_ws_bytes(B, S, H, KV, causal) > 0 && ws == nullptr) return (int)hipErrorInvalidValue;
+// delta: fp32 [2,B,H,S] scratch filled here (delta, -lse*log2(e)).
+template <int D>
+static int attn_bwd_impl(const void* q, const void* k, const void* v, const void* o, const void* dout,
+                         const float* lse, float* delta, void* dq, void* dk, void* dv, float* ws, int B, int S, int H,
+                         int KV, int causal, float scale, hipStream_t s) {
   const int64_t nrows = (int64_t)B * S * H;
-  attn_bwd_delta_kernel<<<(unsigned)((nrows * 16 + 255) / 256), 256, 0, s>>>((const bf16_t*)o, (const bf16_t*)dout,
-                                                                            lse, delta, S, H, nrows);
+  attn_bwd_delta_kernel<D><<<(unsigned)((nrows * (D / 8) + 255) / 256), 256, 0, s>>>(
+      (const bf16_t*)o, (const bf16_t*)dout, lse, delta, S, H, nrows);
   EDL_LAUNCH_CHECK();
   const float sl2 = scale * LOG2E;
   dim3 gkv((S + 127) / 128, KV, B), gq((S + 127) / 128, H, B);
@@ -1386,52 +1394,92 @@ int edl_attn_bwd(const void* q, const void* k, const void* v, const void* o, con
     const char* e = getenv("EDL_ATTN_DKDV_OCC");
     return e && atoi(e) == 2 ? 2 : 1;
   }();
-  const int keys_per_wave = dkdv_keys_per_wave();
+  // the 32-keys-per-wave kernel (EDL_ATTN_DKDV=32) exists for head dim 128 only
+  const int keys_per_wave = D == 128 ? dkdv_keys_per_wave() : 64;
   dim3 gkv64;
   const int gsplit = dkdv64_plan(B, S, H, KV, causal, &gkv64);
-#define EDL_DKDV(C, O)                                                                                              \
-  attn_bwd_dkdv_kernel<C, O><<<gkv, 256, 0, s>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,               \
-                                                 (const bf16_t*)dout, lse, delta, (bf16_t*)dk, (bf16_t*)dv, S, H, KV, \
-                                                 sl2, scale)
-#define EDL_DKDV64(C)                                                                                                \
-  attn_bwd_dkdv64_kernel<C><<<gkv64, 256, 0, s>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,              \
-                                                  (const bf16_t*)dout, lse, delta, (bf16_t*)dk, (bf16_t*)dv, ws, S, H, \
-                                                  KV, gsplit, sl2, scale);                                             \
-  if (gsplit > 1) {                                                                                            \
-    EDL_LAUNCH_CHECK();                                                                                        \
-    const int64_t rows = (int64_t)B * S * KV;                                                                  \
-    attn_dkdv_reduce_kernel<<<(unsigned)((rows * (2 * HD / 8) + 255) / 256), 256, 0, s>>>(ws, (bf16_t*)dk,     \
-                                                                                         (bf16_t*)dv, rows, gsplit); \
-  }
-  if (causal) {
-    if (keys_per_wave == 64) {
-      EDL_DKDV64(true);
-    } else if (occ == 2) {
-      EDL_DKDV(true, 2);
-    } else {
-      EDL_DKDV(true, 1);
+  const bf16_t *bq = (const bf16_t*)q, *bk = (const bf16_t*)k, *bv = (const bf16_t*)v, *bdo = (const bf16_t*)dout;
+  if (keys_per_wave == 64) {
+    if (causal)
+      attn_bwd_dkdv64_kernel<true, D><<<gkv64, 256, 0, s>>>(bq, bk, bv, bdo, lse, delta, (bf16_t*)dk, (bf16_t*)dv,
+                                                            ws, S, H, KV, gsplit, sl2, scale);
+    else
+      attn_bwd_dkdv64_kernel<false, D><<<gkv64, 256, 0, s>>>(bq, bk, bv, bdo, lse, delta, (bf16_t*)dk, (bf16_t*)dv,
+                                                             ws, S, H, KV, gsplit, sl2, scale);
+    if (gsplit > 1) {
+      EDL_LAUNCH_CHECK();
+      const int64_t rows = (int64_t)B * S * KV;
+      attn_dkdv_reduce_kernel<D><<<(unsigned)((rows * (2 * D / 8) + 255) / 256), 256, 0, s>>>(
+          ws, (bf16_t*)dk, (bf16_t*)dv, rows, gsplit);
     }
-    EDL_LAUNCH_CHECK();
-    attn_bwd_dq_kernel<true><<<gq, 256, 0, s>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
-                                                (const bf16_t*)dout, lse, delta, (bf16_t*)dq, S, H, KV, sl2, scale,
-                                                attn_xcd_map(B, KV));
   } else {
-    if (keys_per_wave == 64) {
-      EDL_DKDV64(false);
-    } else if (occ == 2) {
-      EDL_DKDV(false, 2);
-    } else {
-      EDL_DKDV(false, 1);
+    if constexpr (D == 128) {
+#define EDL_DKDV(C, O)                                                                                    \
+  attn_bwd_dkdv_kernel<C, O><<<gkv, 256, 0, s>>>(bq, bk, bv, bdo, lse, delta, (bf16_t*)dk, (bf16_t*)dv, S, H, KV, \
+                                                 sl2, scale)
+      if (causal) {
+        if (occ == 2) EDL_DKDV(true, 2); else EDL_DKDV(true, 1);
+      } else {
+        if (occ == 2) EDL_DKDV(false, 2); else EDL_DKDV(false, 1);
+      }
+#undef EDL_DKDV
     }
-    EDL_LAUNCH_CHECK();
-    attn_bwd_dq_kernel<false><<<gq, 256, 0, s>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
-                                                 (const bf16_t*)dout, lse, delta, (bf16_t*)dq, S, H, KV, sl2, scale,
-                                                 attn_xcd_map(B, KV));
   }
   EDL_LAUNCH_CHECK();
-#undef EDL_DKDV
-#undef EDL_DKDV64
+  if (causal)
+    attn_bwd_dq_kernel<true, D><<<gq, 256, 0, s>>>(bq, bk, bv, bdo, lse, delta, (bf16_t*)dq, S, H, KV, sl2, scale,
+                                                   attn_xcd_map(B, KV));
+  else
+    attn_bwd_dq_kernel<false, D><<<gq, 256, 0, s>>>(bq, bk, bv, bdo, lse, delta, (bf16_t*)dq, S, H, KV, sl2, scale,
+                                                    attn_xcd_map(B, KV));
+  EDL_LAUNCH_CHECK();
   return 0;
+}
+
+extern "C" {
+
+// head dim D = 64 or 128 (bf16, any S, GQA with H % KV == 0)
+int edl_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int S, int H, int KV,
+                 int D, int causal, float scale, hipStream_t s) {
+  if ((D != 64 && D != 128) || H % KV != 0 || S <= 0) return (int)hipErrorInvalidValue;
+  const float sl2 = scale * LOG2E;
+  // EDL_ATTN_FWD=64: the software-pipelined 64-queries-per-wave kernel (head dim 128)
+  const char* sel = getenv("EDL_ATTN_FWD");
+  if (D == 128 && sel && atoi(sel) == 64) {
+    dim3 g64((S + 255) / 256, H, B);
+    if (causal)
+      attn_fwd64_kernel<true><<<g64, 256, 0, s>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
+                                                     (bf16_t*)o, lse, S, H, KV, sl2);
+    else
+      attn_fwd64_kernel<false><<<g64, 256, 0, s>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
+                                                      (bf16_t*)o, lse, S, H, KV, sl2);
+    EDL_LAUNCH_CHECK();
+    return 0;
+  }
+  if (D == 128)
+    attn_fwd_launch<128>(q, k, v, o, lse, B, S, H, KV, causal, sl2, s);
+  else
+    attn_fwd_launch<64>(q, k, v, o, lse, B, S, H, KV, causal, sl2, s);
+  EDL_LAUNCH_CHECK();
+  return 0;
+}
+
+// fp32 workspace the backward needs for the head-split dK/dV partials (0 = none); sized
+// for head dim 128 (an upper bound for 64)
+int64_t edl_attn_bwd_ws_bytes(int B, int S, int H, int KV, int causal) {
+  if (KV <= 0 || H % KV != 0) return 0;
+  const int g = dkdv64_plan(B, S, H, KV, causal, nullptr);
+  return g == 1 ? 0 : (int64_t)g * B * S * KV * 2 * HD * 4;
+}
+
+int edl_attn_bwd(const void* q, const void* k, const void* v, const void* o, const void* dout, const float* lse,
+                 float* delta, void* dq, void* dk, void* dv, float* ws, int B, int S, int H, int KV, int D,
+                 int causal, float scale, hipStream_t s) {
+  if ((D != 64 && D != 128) || H % KV != 0 || S <= 0) return (int)hipErrorInvalidValue;
+  if (edl_attn_bwd_ws_bytes(B, S, H, KV, causal) > 0 && ws == nullptr) return (int)hipErrorInvalidValue;
+  if (D == 128)
+    return attn_bwd_impl<128>(q, k, v, o, dout, lse, delta, dq, dk, dv, ws, B, S, H, KV, causal, scale, s);
+  return attn_bwd_impl<64>(q, k, v, o, dout, lse, delta, dq, dk, dv, ws, B, S, H, KV, causal, scale, s);
 }
 
 }  // extern "C"

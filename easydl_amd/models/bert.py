@@ -15,6 +15,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from easydl_amd.ops import fused, norms
+from easydl_amd.ops.attention import flash_attention
 
 
 @dataclass
@@ -72,7 +73,9 @@ class BertLayer(nn.Module):
         qkv = fused.linear(x, self.wqkv, self.bqkv).view(B, S, 3, H, hd)
         q, k, v = qkv.unbind(2)
         q, k, v = (t.transpose(1, 2) for t in (q, k, v))
-        if q.is_cuda:
+        if q.is_cuda and mask is None:
+            o = flash_attention(q, k, v, causal=False)   # HIP kernels, head dim 64
+        elif q.is_cuda:
             o = F.scaled_dot_product_attention(q, k, v, attn_mask=mask)
         else:
             o = F.scaled_dot_product_attention(q.float(), k.float(), v.float(), attn_mask=mask).to(q.dtype)

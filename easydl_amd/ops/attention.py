@@ -1,4 +1,4 @@
-"""Flash attention (csrc/kernels/attention.hip): causal GQA, head_dim 128, bf16.
+"""Flash attention (csrc/kernels/attention.hip): causal or full, GQA, head_dim 64 or 128, bf16.
 
 Inputs are the ``[B, H, S, D]``-shaped views of token-major ``[B, S, H, D]``
 memory that the fused RoPE+QKV kernel produces; the output is returned the
@@ -6,7 +6,8 @@ same way, so ``o.transpose(1, 2).reshape(B*S, H*D)`` feeding the output
 projection is free.  The forward saves only O and the log-sum-exp (fp32
 [B,H,S]); the backward recomputes P tile by tile (dK/dV kernel + dQ kernel,
 no float atomics).  ``EDL_ATTN=sdpa`` falls back to PyTorch SDPA (used for
-A/B comparisons); other head dims also use SDPA.
+A/B comparisons); other head dims also use SDPA.  Head dim 64 (BERT-large,
+Llama-3.2-1B/3B) runs the same kernels instantiated for 128-byte rows.
 """
 from __future__ import annotations
 
@@ -74,7 +75,7 @@ def flash_attention(q, k, v, causal: bool = True, scale: float | None = None):
     D = q.shape[-1]
     scale = 1.0 / math.sqrt(D) if scale is None else scale
     if q.is_cuda:
-        if D == 128 and q.dtype == torch.bfloat16 and os.environ.get("EDL_ATTN", "hip") != "sdpa":
+        if D in (64, 128) and q.dtype == torch.bfloat16 and os.environ.get("EDL_ATTN", "hip") != "sdpa":
             return _FlashAttnFn.apply(q, k, v, causal, scale)
         return F.scaled_dot_product_attention(q, k, v, is_causal=causal, scale=scale,
                                               enable_gqa=q.shape[1] != k.shape[1])

@@ -8,11 +8,11 @@ from easydl_amd.ops.attention import attention_ref, flash_attention
 pytestmark = pytest.mark.gpu
 
 
-def _mk(B, S, H, KV, dev, seed):
+def _mk(B, S, H, KV, dev, seed, D=128):
     g = torch.Generator(device=dev).manual_seed(seed)
-    q = torch.randn(B, S, H, 128, device=dev, generator=g).to(torch.bfloat16).transpose(1, 2)
-    k = torch.randn(B, S, KV, 128, device=dev, generator=g).to(torch.bfloat16).transpose(1, 2)
-    v = torch.randn(B, S, KV, 128, device=dev, generator=g).to(torch.bfloat16).transpose(1, 2)
+    q = torch.randn(B, S, H, D, device=dev, generator=g).to(torch.bfloat16).transpose(1, 2)
+    k = torch.randn(B, S, KV, D, device=dev, generator=g).to(torch.bfloat16).transpose(1, 2)
+    v = torch.randn(B, S, KV, D, device=dev, generator=g).to(torch.bfloat16).transpose(1, 2)
     return q, k, v
 
 
@@ -35,6 +35,25 @@ def test_flash_attention_fwd_bwd(cuda, B, S, H, KV, causal, fwd, monkeypatch):
     q2, k2, v2 = (t.detach().float().requires_grad_() for t in (q, k, v))
     o2 = attention_ref(q2, k2, v2, causal=causal)
     o2.backward(do.float())
+    assert _err(o, o2) < 2e-2, "forward"
+    assert _err(q1.grad, q2.grad) < 3e-2, "dq"
+    assert _err(k1.grad, k2.grad) < 3e-2, "dk"
+    assert _err(v1.grad, v2.grad) < 3e-2, "dv"
+
+
+@pytest.mark.parametrize("B,S,H,KV,causal", [(2, 512, 16, 16, False), (1, 200, 4, 1, True), (2, 256, 8, 2, True),
+                                             (1, 1000, 8, 8, False), (1, 2112, 8, 2, True), (2, 100, 4, 4, False)])
+def test_flash_attention_head_dim_64(cuda, B, S, H, KV, causal):
+    """The same kernels instantiated for head dim 64 (BERT-large: 16 heads x 64, no mask)."""
+    q, k, v = _mk(B, S, H, KV, cuda, S + 7 * H, D=64)
+    q1, k1, v1 = (t.detach().clone().requires_grad_() for t in (q, k, v))
+    o = flash_attention(q1, k1, v1, causal=causal)
+    do = torch.randn_like(o)
+    o.backward(do)
+    q2, k2, v2 = (t.detach().float().requires_grad_() for t in (q, k, v))
+    o2 = attention_ref(q2, k2, v2, causal=causal)
+    o2.backward(do.float())
+    assert o.shape == (B, H, S, 64)
     assert _err(o, o2) < 2e-2, "forward"
     assert _err(q1.grad, q2.grad) < 3e-2, "dq"
     assert _err(k1.grad, k2.grad) < 3e-2, "dk"
