@@ -164,7 +164,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "bf16",
+        "dtype": "bf16" if use_cuda else "fp32",
         "data": "synthetic (random token ids), random-init weights",
         "config": {
             "model": args.model if not args.layers else f"{args.model}-L{args.layers}",
