@@ -810,16 +810,17 @@ __global__ __launch_bounds__(256) void attn_bwd_delta_kernel(const bf16_t* __res
 // ---------------------------------------------------------------------------
 // Issue order S, dP (16 back-to-back MFMAs), then exp(S) under the dP MFMAs,
 // dV += dO^T P under which dS = P (dP - delta) runs, then dK += Q^T dS.
-template <bool MASK, bool CAUSAL>
+template <bool MASK, bool CAUSAL, int D>
 __device__ __forceinline__ void dkdv_slice(const char* Qs, const char* Ds, const float* NL, const float* DL, int rb,
-                                           const bf16x8 (&kf)[8], const bf16x8 (&vf)[8], f32x16 (&dka)[4],
-                                           f32x16 (&dva)[4], int qs0, int mykey, int S, float sl2, int lane) {
+                                           const bf16x8 (&kf)[D / 16], const bf16x8 (&vf)[D / 16],
+                                           f32x16 (&dka)[D / 32], f32x16 (&dva)[D / 32], int qs0, int mykey, int S,
+                                           float sl2, int lane) {
   const int h = lane >> 5, l31 = lane & 31;
   f32x16 sa = f32x16{}, dp = f32x16{};
 #pragma unroll
-  for (int s = 0; s < 8; ++s) sa = mfma(row_read(Qs, rb + l31, s, h), kf[s], sa);
+  for (int s = 0; s < D / 16; ++s) sa = mfma(row_read<D>(Qs, rb + l31, s, h), kf[s], sa);
 #pragma unroll
-  for (int s = 0; s < 8; ++s) dp = mfma(row_read(Ds, rb + l31, s, h), vf[s], dp);
+  for (int s = 0; s < D / 16; ++s) dp = mfma(row_read<D>(Ds, rb + l31, s, h), vf[s], dp);
   // accumulator register i <-> query row rb + acc_row(i, h): rows 8g+4h .. +3 are contiguous
   f32x4 nl[4], dl[4];
 #pragma unroll
@@ -840,7 +841,7 @@ __device__ __forceinline__ void dkdv_slice(const char* Qs, const char* Ds, const
   for (int s2 = 0; s2 < 2; ++s2) {
     const bf16x8 pb = acc_to_b(sa, s2);
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt) dva[dt] = mfma(tr_read(Ds, rb + 16 * s2 + 4 * h, dt, lane), pb, dva[dt]);
+    for (int dt = 0; dt < D / 32; ++dt) dva[dt] = mfma(tr_read<D>(Ds, rb + 16 * s2 + 4 * h, dt, lane), pb, dva[dt]);
   }
 #pragma unroll
   for (int i = 0; i < 16; ++i) dp[i] = sa[i] * (dp[i] - dl[i >> 2][i & 3]);
@@ -848,37 +849,38 @@ __device__ __forceinline__ void dkdv_slice(const char* Qs, const char* Ds, const
   for (int s2 = 0; s2 < 2; ++s2) {
     const bf16x8 db = acc_to_b(dp, s2);
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt) dka[dt] = mfma(tr_read(Qs, rb + 16 * s2 + 4 * h, dt, lane), db, dka[dt]);
+    for (int dt = 0; dt < D / 32; ++dt) dka[dt] = mfma(tr_read<D>(Qs, rb + 16 * s2 + 4 * h, dt, lane), db, dka[dt]);
   }
 }
 
 // OCC = waves per SIMD the register budget is cut for: 1 keeps every K/V
 // fragment resident (no spill); 2 doubles the latency hiding but reloads six
 // fragments per slice from scratch.  Chosen at launch (EDL_ATTN_DKDV_OCC).
-template <bool CAUSAL, int OCC>
+template <bool CAUSAL, int OCC, int D = 128>
 __global__ __launch_bounds__(256, OCC) void attn_bwd_dkdv_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
     const bf16_t* __restrict__ dout, const float* __restrict__ lse, const float* __restrict__ delta,
     bf16_t* __restrict__ dk, bf16_t* __restrict__ dv, int S, int H, int KV, float scale_log2, float scale) {
   constexpr int QT = 64;  // queries per staged tile
-  // 2 stages x (Q tile 16 KB + dO tile 16 KB) + 2 x (-lse2, delta) x 64 floats
-  __shared__ __attribute__((aligned(16))) char smem[2 * 32768 + 2 * 512];
+  constexpr int TILE = QT * 2 * D, STAGE = 2 * TILE;
+  // 2 stages x (Q tile + dO tile) + 2 x (-lse2, delta) x 64 floats
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE + 2 * 512];
   const int kb = blockIdx.x, hk = blockIdx.y, b = blockIdx.z;
   const int lane = threadIdx.x & 63, h = lane >> 5, l31 = lane & 31;
   const int w = threadIdx.x >> 6;
   const int group = H / KV;
-  const int64_t qs = (int64_t)H * HD, ks = (int64_t)KV * HD;
+  const int64_t qs = (int64_t)H * D, ks = (int64_t)KV * D;
   const int mykey = kb * 128 + 32 * w + l31;
-  const int64_t krow_off = (int64_t)b * S * ks + (int64_t)min(mykey, S - 1) * ks + hk * HD;
-  bf16x8 kf[8], vf[8];
+  const int64_t krow_off = (int64_t)b * S * ks + (int64_t)min(mykey, S - 1) * ks + hk * D;
+  bf16x8 kf[D / 16], vf[D / 16];
 #pragma unroll
-  for (int s = 0; s < 8; ++s) {
+  for (int s = 0; s < D / 16; ++s) {
     kf[s] = load_frag(k + krow_off, s, h);
     vf[s] = load_frag(v + krow_off, s, h);
   }
-  f32x16 dka[4], dva[4];
+  f32x16 dka[D / 32], dva[D / 32];
 #pragma unroll
-  for (int dt = 0; dt < 4; ++dt) {
+  for (int dt = 0; dt < D / 32; ++dt) {
     dka[dt] = f32x16{};
     dva[dt] = f32x16{};
   }
@@ -889,16 +891,16 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dkdv_kernel(
   const int wave_key_lo = kb * 128 + 32 * w;
 
   const int64_t nBHS = (int64_t)gridDim.z * H * S;  // delta = [delta | -lse*log2e]
-  const DmaPlan<QT, 4> plan(qs, w, lane);
+  const DmaPlan<QT, 4, D> plan(qs, w, lane);
   auto fetch = [&](int j, int st) {
     const int hq = hk * group + j / per_head;
     const int q0 = (qt0 + j % per_head) * QT;
-    char* base = smem + st * 32768;
-    const int64_t off = (int64_t)b * S * qs + hq * HD, nbytes = ((int64_t)S * qs - hq * HD) * 2;
+    char* base = smem + st * STAGE;
+    const int64_t off = (int64_t)b * S * qs + hq * D, nbytes = ((int64_t)S * qs - hq * D) * 2;
     const uint32_t soff = (uint32_t)(q0 * qs * 2);
     plan.issue(base, make_rsrc(q + off, nbytes), soff, w);
-    plan.issue(base + 16384, make_rsrc(dout + off, nbytes), soff, w);
-    float* lf = reinterpret_cast<float*>(smem + 2 * 32768 + st * 512);
+    plan.issue(base + TILE, make_rsrc(dout + off, nbytes), soff, w);
+    float* lf = reinterpret_cast<float*>(smem + 2 * STAGE + st * 512);
     const int64_t row0 = ((int64_t)b * H + hq) * S;
     if (w == 0) dma_f32x64(lf, make_rsrc(delta + nBHS + row0, (int64_t)S * 4), q0, lane);
     if (w == 1) dma_f32x64(lf + QT, make_rsrc(delta + row0, (int64_t)S * 4), q0, lane);
@@ -910,9 +912,9 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dkdv_kernel(
   for (int j = 0; j < total; ++j) {
     if (j + 1 < total) fetch(j + 1, (j + 1) & 1);
     const int st = j & 1;
-    const char* Qs = smem + st * 32768;
-    const char* Ds = Qs + 16384;
-    const float* NL = reinterpret_cast<const float*>(smem + 2 * 32768 + st * 512);
+    const char* Qs = smem + st * STAGE;
+    const char* Ds = Qs + TILE;
+    const float* NL = reinterpret_cast<const float*>(smem + 2 * STAGE + st * 512);
     const int q0 = (qt0 + j % per_head) * QT;
 #pragma unroll
     for (int sub = 0; sub < QT / 32; ++sub) {
@@ -920,16 +922,18 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dkdv_kernel(
       if (CAUSAL && qs0 + 31 < wave_key_lo) continue;  // wave-uniform: all masked
       const bool mask = (qs0 + 32 > S) || (wave_key_lo + 32 > S) || (CAUSAL && wave_key_lo + 31 > qs0);
       if (mask)
-        dkdv_slice<true, CAUSAL>(Qs, Ds, NL, NL + QT, 32 * sub, kf, vf, dka, dva, qs0, mykey, S, scale_log2, lane);
+        dkdv_slice<true, CAUSAL, D>(Qs, Ds, NL, NL + QT, 32 * sub, kf, vf, dka, dva, qs0, mykey, S, scale_log2,
+                                    lane);
       else
-        dkdv_slice<false, CAUSAL>(Qs, Ds, NL, NL + QT, 32 * sub, kf, vf, dka, dva, qs0, mykey, S, scale_log2, lane);
+        dkdv_slice<false, CAUSAL, D>(Qs, Ds, NL, NL + QT, 32 * sub, kf, vf, dka, dva, qs0, mykey, S, scale_log2,
+                                     lane);
     }
     wait_vm();
     __syncthreads();
   }
   if (mykey < S) {
-    store_accT(dk + (int64_t)b * S * ks + (int64_t)mykey * ks + hk * HD, dka, scale, h);
-    store_accT(dv + (int64_t)b * S * ks + (int64_t)mykey * ks + hk * HD, dva, 1.f, h);
+    store_accT(dk + (int64_t)b * S * ks + (int64_t)mykey * ks + hk * D, dka, scale, h);
+    store_accT(dv + (int64_t)b * S * ks + (int64_t)mykey * ks + hk * D, dva, 1.f, h);
   }
 }
 
@@ -1394,8 +1398,13 @@ static int attn_bwd_impl(const void* q, const void* k, const void* v, const void
     const char* e = getenv("EDL_ATTN_DKDV_OCC");
     return e && atoi(e) == 2 ? 2 : 1;
   }();
-  // the 32-keys-per-wave kernel (EDL_ATTN_DKDV=32) exists for head dim 128 only
-  const int keys_per_wave = D == 128 ? dkdv_keys_per_wave() : 64;
+  // head dim 64: the 32-keys-per-wave kernel fits two waves per SIMD and measured +7 % over the
+  // 64-key one at the BERT-large shape (profiles/r02_attn_hd64_bert.txt); EDL_ATTN_DKDV=64 overrides
+  static const bool force64 = [] {
+    const char* e = getenv("EDL_ATTN_DKDV");
+    return e && atoi(e) == 64;
+  }();
+  const int keys_per_wave = D == 128 ? dkdv_keys_per_wave() : (force64 ? 64 : 32);
   dim3 gkv64;
   const int gsplit = dkdv64_plan(B, S, H, KV, causal, &gkv64);
   const bf16_t *bq = (const bf16_t*)q, *bk = (const bf16_t*)k, *bv = (const bf16_t*)v, *bdo = (const bf16_t*)dout;
@@ -1413,17 +1422,15 @@ static int attn_bwd_impl(const void* q, const void* k, const void* v, const void
           ws, (bf16_t*)dk, (bf16_t*)dv, rows, gsplit);
     }
   } else {
-    if constexpr (D == 128) {
-#define EDL_DKDV(C, O)                                                                                    \
-  attn_bwd_dkdv_kernel<C, O><<<gkv, 256, 0, s>>>(bq, bk, bv, bdo, lse, delta, (bf16_t*)dk, (bf16_t*)dv, S, H, KV, \
-                                                 sl2, scale)
-      if (causal) {
-        if (occ == 2) EDL_DKDV(true, 2); else EDL_DKDV(true, 1);
-      } else {
-        if (occ == 2) EDL_DKDV(false, 2); else EDL_DKDV(false, 1);
-      }
-#undef EDL_DKDV
+#define EDL_DKDV(C, O)                                                                                       \
+  attn_bwd_dkdv_kernel<C, O, D><<<gkv, 256, 0, s>>>(bq, bk, bv, bdo, lse, delta, (bf16_t*)dk, (bf16_t*)dv, S, H, \
+                                                    KV, sl2, scale)
+    if (causal) {
+      if (occ == 2 || D == 64) EDL_DKDV(true, 2); else EDL_DKDV(true, 1);
+    } else {
+      if (occ == 2 || D == 64) EDL_DKDV(false, 2); else EDL_DKDV(false, 1);
     }
+#undef EDL_DKDV
   }
   EDL_LAUNCH_CHECK();
   if (causal)
