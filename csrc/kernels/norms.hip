@@ -206,18 +206,32 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(const bf16_t* __restrict_
 // out[c] (+)= sum_g partial[g][c]; out dtype bf16 (odt=0) or fp32 (odt=1).
 // Workgroup = 16 column groups (4 columns each, f32x4 loads) x 16 row slices;
 // slices are combined through LDS.  cols % 4 == 0.
-__global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ partial, int G, int cols,
-                                                     void* __restrict__ out, int odt, int accumulate) {
-  __shared__ f32x4 red[16][16];
+// Column sums of a [G, cols] fp32 partial slab.  A 1024-thread block owns 64 columns
+// (16 groups of 4) and splits the G rows over 64 slices: at G = 1024 each thread adds 16
+// independent 16-B loads (4 chains) instead of 64 serial ones, then an LDS tree.  The
+// 256-thread version was latency-bound: 13.5 us per call, 197 calls per BERT-large step.
+__global__ __launch_bounds__(1024) void colsum_kernel(const float* __restrict__ partial, int G, int cols,
+                                                      void* __restrict__ out, int odt, int accumulate) {
+  __shared__ f32x4 red[64][16];
   const int cg = threadIdx.x & 15, sl = threadIdx.x >> 4;
   const int c = (blockIdx.x * 16 + cg) * 4;
-  f32x4 s = {0.f, 0.f, 0.f, 0.f};
-  if (c < cols)
-    for (int g = sl; g < G; g += 16) s += *reinterpret_cast<const f32x4*>(partial + (int64_t)g * cols + c);
-  red[sl][cg] = s;
+  f32x4 s4[4] = {};
+  if (c < cols) {
+    int g = sl;
+    for (; g + 192 < G; g += 256) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) s4[u] += *reinterpret_cast<const f32x4*>(partial + (int64_t)(g + 64 * u) * cols + c);
+    }
+    for (; g < G; g += 64) s4[0] += *reinterpret_cast<const f32x4*>(partial + (int64_t)g * cols + c);
+  }
+  red[sl][cg] = (s4[0] + s4[1]) + (s4[2] + s4[3]);
   __syncthreads();
+  for (int w = 32; w >= 1; w >>= 1) {
+    if (sl < w) red[sl][cg] += red[sl + w][cg];
+    __syncthreads();
+  }
   if (sl != 0 || c >= cols) return;
-  for (int i = 1; i < 16; ++i) s += red[i][cg];
+  const f32x4 s = red[0][cg];
   if (odt == 0) {
     bf16_t* o = reinterpret_cast<bf16_t*>(out) + c;
 #pragma unroll
@@ -315,7 +329,7 @@ int edl_layernorm_bwd(const void* dy, const void* x, const void* w, const float*
 
 int edl_colsum(const float* partial, int G, int cols, void* out, int odt, int accumulate, hipStream_t s) {
   if (cols % 4) return (int)hipErrorInvalidValue;
-  colsum_kernel<<<(cols + 63) / 64, 256, 0, s>>>(partial, G, cols, out, odt, accumulate);
+  colsum_kernel<<<(cols + 63) / 64, 1024, 0, s>>>(partial, G, cols, out, odt, accumulate);
   EDL_LAUNCH_CHECK();
   return 0;
 }

@@ -306,3 +306,19 @@ def test_fused_swiglu_mlp_matches_fp32_reference(cuda):
     for a, b in ((y, yr), (x.grad, xr.grad), (w_gu.grad, gr.grad), (w_dn.grad, dr.grad)):
         err = ((a.float() - b).abs().max() / (b.abs().max() + 1e-6)).item()
         assert err < 3e-2, err
+
+
+@pytest.mark.parametrize("G,cols", [(1, 4), (63, 64), (65, 1000), (1024, 1024), (1100, 4096), (512, 28)])
+@pytest.mark.parametrize("odt,acc", [(1, 0), (1, 1), (0, 1)])
+def test_colsum_partials(cuda, G, cols, odt, acc):
+    """edl_colsum (bias / norm-weight gradient from per-block partials) vs torch, every
+    tail of the 64-slice x 4-chain row split, fp32 and bf16 outputs, overwrite and accumulate."""
+    from easydl_amd import _native
+    part = torch.randn(G, cols, device=cuda)
+    dt = torch.float32 if odt == 1 else torch.bfloat16
+    out = torch.randn(cols, device=cuda).to(dt)
+    ref = part.double().sum(0) + (out.double() if acc else 0)
+    _native.kernels().check("edl_colsum", part.data_ptr(), G, cols, out.data_ptr(), odt, acc,
+                            _native.stream_of(part))
+    tol = 1e-5 if odt == 1 else 1e-2
+    assert ((out.double() - ref).abs().max() / ref.abs().max()).item() < tol
