@@ -1,5 +1,7 @@
 """Checkpoint format v1 + shm A/B store + restore (CPU tier; GPU variant in test_ckpt_gpu)."""
 
+import os
+
 import numpy as np
 import torch
 
@@ -10,11 +12,14 @@ from easydl_amd.trainer.context import TrainerContext
 from easydl_amd.trainer.data import SyntheticTokens
 from easydl_amd.trainer.elastic import ElasticTrainer
 
+# Per-process job name: under pytest-xdist the tests of this file run in several
+# workers at once, and a shared name would let one test unlink another's shm slots.
+JOB = f"ck{os.getpid()}"
 CFG = get_config("llama-tiny", n_layers=1, dim=64, n_heads=4, n_kv_heads=2, ffn_dim=128, vocab_size=128)
 
 
 def _trainer(tmp, ckpt, seed=1234):
-    ctx = TrainerContext(job="ck", run_dir=str(tmp))
+    ctx = TrainerContext(job=JOB, run_dir=str(tmp))
     return ElasticTrainer(lambda d: Llama(CFG, device=d, dtype=torch.float32), global_batch=4, micro_batch=2,
                           lr=1e-3, device="cpu", ctx=ctx, checkpoint=ckpt, seed=seed)
 
@@ -64,18 +69,18 @@ def test_shm_ab_slots_survive_torn_write():
 
 
 def test_snapshot_restore_resumes_bit_identically(tmp_path):
-    unlink_job_segments("ck")
+    unlink_job_segments(JOB)
     data = SyntheticTokens(CFG.vocab_size, 16, num_samples=1024)
     ref = _trainer(tmp_path, None)
     ref.fit(lambda m, b: m(*b), data, num_steps=10)
-    ckpt = CheckpointManager("ck", interval=3, persist_dir=str(tmp_path / "disk"), persist_every=1)
+    ckpt = CheckpointManager(JOB, interval=3, persist_dir=str(tmp_path / "disk"), persist_every=1)
     try:
         a = _trainer(tmp_path, ckpt)
         a.fit(lambda m, b: m(*b), data, num_steps=7)
         ckpt.wait()
         assert ckpt.last_snapshot_step == 6
         # a brand-new process (different init) restores step 6 from /dev/shm and continues
-        ckpt2 = CheckpointManager("ck", interval=100)
+        ckpt2 = CheckpointManager(JOB, interval=100)
         b = _trainer(tmp_path, ckpt2, seed=999)
         b.fit(lambda m, b_: m(*b_), data, num_steps=10)
         assert b.history[0]["step"] == 7  # resumed after step 6
@@ -86,7 +91,7 @@ def test_snapshot_restore_resumes_bit_identically(tmp_path):
         load_dir(str(tmp_path / "disk" / "step-6"), c)
         assert c.step == 6
     finally:
-        unlink_job_segments("ck")
+        unlink_job_segments(JOB)
 
 
 def test_snapshot_evaluator_reads_latest(tmp_path):
@@ -128,10 +133,10 @@ def test_premapped_segments_are_reused_by_restore(tmp_path):
 
 def test_load_dir_latest_falls_back_past_a_torn_shard(tmp_path):
     """A corrupted newest step-* directory is skipped: cold resume uses the next older one."""
-    unlink_job_segments("ck")
+    unlink_job_segments(JOB)
     data = SyntheticTokens(CFG.vocab_size, 16, num_samples=1024)
     disk = tmp_path / "disk"
-    ckpt = CheckpointManager("ck", interval=2, persist_dir=str(disk), persist_every=1)
+    ckpt = CheckpointManager(JOB, interval=2, persist_dir=str(disk), persist_every=1)
     try:
         a = _trainer(tmp_path, ckpt)
         a.fit(lambda m, b: m(*b), data, num_steps=6, on_step=lambda t, loss: ckpt._join_persist())
@@ -141,21 +146,21 @@ def test_load_dir_latest_falls_back_past_a_torn_shard(tmp_path):
         raw = bytearray(shard.read_bytes())
         raw[100] ^= 0xFF
         shard.write_bytes(bytes(raw))
-        unlink_job_segments("ck")           # no in-memory copy left: the disk path is taken
+        unlink_job_segments(JOB)           # no in-memory copy left: the disk path is taken
         b = _trainer(tmp_path, None, seed=77)
-        src = CheckpointManager("ck", persist_dir=str(disk)).restore_latest(b)
+        src = CheckpointManager(JOB, persist_dir=str(disk)).restore_latest(b)
         assert src == f"disk:{disk / 'step-4'}" and b.step == 4
     finally:
-        unlink_job_segments("ck")
+        unlink_job_segments(JOB)
 
 
 def test_snapshot_skips_the_slot_a_persist_is_reading(tmp_path):
     """A/B slots: while the disk writer still reads slot X, the snapshot that would
     reuse X is skipped instead of tearing the file being written."""
     import threading
-    unlink_job_segments("ck")
+    unlink_job_segments(JOB)
     data = SyntheticTokens(CFG.vocab_size, 16, num_samples=1024)
-    ckpt = CheckpointManager("ck", interval=1)
+    ckpt = CheckpointManager(JOB, interval=1)
     try:
         a = _trainer(tmp_path, ckpt)
         a.fit(lambda m, b: m(*b), data, num_steps=1)          # snapshot of step 1 -> slot s1
@@ -172,7 +177,7 @@ def test_snapshot_skips_the_slot_a_persist_is_reading(tmp_path):
         assert ckpt.last_snapshot_step == 4
     finally:
         ckpt.close()
-        unlink_job_segments("ck")
+        unlink_job_segments(JOB)
 
 
 def test_world_change_reuses_the_pinned_segment(tmp_path):
@@ -181,26 +186,26 @@ def test_world_change_reuses_the_pinned_segment(tmp_path):
     no stale old-layout slot visible under the new name."""
     import os
     import types
-    unlink_job_segments("ck")
-    ckpt = CheckpointManager("ck", interval=1)
+    unlink_job_segments(JOB)
+    ckpt = CheckpointManager(JOB, interval=1)
     try:
         a = _trainer(tmp_path, None)
         a.comm = types.SimpleNamespace(world_size=4, rank=1, epoch=1)
         a.step = 1
         ckpt.snapshot(a)
         h0 = ckpt._seg.h
-        assert os.path.exists("/dev/shm/edl-ck-w4-s1")
+        assert os.path.exists(f"/dev/shm/edl-{JOB}-w4-s1")
         a.comm = types.SimpleNamespace(world_size=3, rank=2, epoch=2)     # renumbered survivor
         a.step = 2
         seg = ckpt._segment(3, 2, shard_layout(CheckpointManager.state_of(a), 2, 3)[1] + 8)
         assert seg.h == h0 and ckpt.stats["reassigned"] == 1
-        assert not os.path.exists("/dev/shm/edl-ck-w4-s1") and os.path.exists("/dev/shm/edl-ck-w3-s2")
+        assert not os.path.exists(f"/dev/shm/edl-{JOB}-w4-s1") and os.path.exists(f"/dev/shm/edl-{JOB}-w3-s2")
         assert seg.committed() == []                                       # old layout invalidated
         ckpt.snapshot(a)
         assert [i["step"] for i in ckpt._seg.committed()] == [2] and ckpt._seg.h == h0
     finally:
         ckpt.close()
-        unlink_job_segments("ck")
+        unlink_job_segments(JOB)
 
 
 class _BNNet(torch.nn.Module):
