@@ -860,7 +860,8 @@ template <bool CAUSAL, int OCC, int D = 128>
 __global__ __launch_bounds__(256, OCC) void attn_bwd_dkdv_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
     const bf16_t* __restrict__ dout, const float* __restrict__ lse, const float* __restrict__ delta,
-    bf16_t* __restrict__ dk, bf16_t* __restrict__ dv, int S, int H, int KV, float scale_log2, float scale) {
+    bf16_t* __restrict__ dk, bf16_t* __restrict__ dv, int S, int H, int KV, float scale_log2, float scale,
+    int64_t dkvs) {
   constexpr int QT = 64;  // queries per staged tile
   constexpr int TILE = QT * 2 * D, STAGE = 2 * TILE;
   // 2 stages x (Q tile + dO tile) + 2 x (-lse2, delta) x 64 floats
@@ -932,8 +933,8 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dkdv_kernel(
     __syncthreads();
   }
   if (mykey < S) {
-    store_accT(dk + (int64_t)b * S * ks + (int64_t)mykey * ks + hk * D, dka, scale, h);
-    store_accT(dv + (int64_t)b * S * ks + (int64_t)mykey * ks + hk * D, dva, 1.f, h);
+    store_accT(dk + ((int64_t)b * S + mykey) * dkvs + hk * D, dka, scale, h);
+    store_accT(dv + ((int64_t)b * S + mykey) * dkvs + hk * D, dva, 1.f, h);
   }
 }
 
@@ -1083,7 +1084,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv64_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
     const bf16_t* __restrict__ dout, const float* __restrict__ lse, const float* __restrict__ delta,
     bf16_t* __restrict__ dk, bf16_t* __restrict__ dv, float* __restrict__ ws, int S, int H, int KV, int gsplit,
-    float scale_log2, float scale) {
+    float scale_log2, float scale, int64_t dkvs) {
   constexpr int QT = 64;   // queries per staged tile
   constexpr int KW = 64;   // keys per wave
   constexpr int KB = 4 * KW;
@@ -1191,8 +1192,8 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv64_kernel(
       const int mykey = key0 + 32 * t + l31;
       if (mykey >= S) continue;
       if (gsplit == 1) {
-        store_accT(dk + (int64_t)b * S * ks + (int64_t)mykey * ks + hk * D, dka[t], scale, h);
-        store_accT(dv + (int64_t)b * S * ks + (int64_t)mykey * ks + hk * D, dva[t], 1.f, h);
+        store_accT(dk + ((int64_t)b * S + mykey) * dkvs + hk * D, dka[t], scale, h);
+        store_accT(dv + ((int64_t)b * S + mykey) * dkvs + hk * D, dva[t], 1.f, h);
       } else {  // ws[gs][b][key][hk][dk|dv][D]
         float* row = ws + ((((int64_t)gs * gridDim.z + b) * S + mykey) * KV + hk) * 2 * D;
         store_accT_f32(row, dka[t], scale, h);
@@ -1205,7 +1206,8 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv64_kernel(
 // sum the head-split partials: ws[g][b][key][kv][2][HD] fp32 -> dk, dv bf16 (8 elements per thread)
 template <int D>
 __global__ __launch_bounds__(256) void attn_dkdv_reduce_kernel(const float* __restrict__ ws, bf16_t* __restrict__ dk,
-                                                               bf16_t* __restrict__ dv, int64_t nrows, int gsplit) {
+                                                               bf16_t* __restrict__ dv, int64_t nrows, int gsplit,
+                                                               int KV, int64_t dkvs) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;   // one 8-element chunk of a [2*D] row
   constexpr int CH = 2 * D / 8;
   if (i >= nrows * CH) return;
@@ -1222,7 +1224,8 @@ __global__ __launch_bounds__(256) void attn_dkdv_reduce_kernel(const float* __re
   o[1] = pack2(a[2], a[3]);
   o[2] = pack2(bq[0], bq[1]);
   o[3] = pack2(bq[2], bq[3]);
-  bf16_t* dst = (8 * c < D ? dk : dv) + row * D + (8 * c) % D;
+  // row = token * KV + kv head; dK / dV rows of a token are dkvs elements apart
+  bf16_t* dst = (8 * c < D ? dk : dv) + (row / KV) * dkvs + (row % KV) * D + (8 * c) % D;
   *reinterpret_cast<u32x4*>(dst) = o;
 }
 
@@ -1269,7 +1272,7 @@ template <bool CAUSAL, int D>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
     const bf16_t* __restrict__ dout, const float* __restrict__ lse, const float* __restrict__ delta,
-    bf16_t* __restrict__ dq, int S, int H, int KV, float scale_log2, float scale, int xcd) {
+    bf16_t* __restrict__ dq, int S, int H, int KV, float scale_log2, float scale, int xcd, int64_t dqs) {
   constexpr int BQ = 128;
   constexpr int TILE = 64 * 2 * D, STAGE = 2 * TILE;
   __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
@@ -1337,7 +1340,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(
   };
   run(std::integral_constant<bool, false>{}, 0, nfull);
   run(std::integral_constant<bool, true>{}, nfull, ntiles);
-  if (qr < S) store_accT(dq + (int64_t)b * S * qs + (int64_t)qr * qs + hq * D, dqa, scale, h);
+  if (qr < S) store_accT(dq + ((int64_t)b * S + qr) * dqs + hq * D, dqa, scale, h);
 }
 
 }  // namespace
@@ -1387,7 +1390,7 @@ static int dkdv_keys_per_wave() {
 template <int D>
 static int attn_bwd_impl(const void* q, const void* k, const void* v, const void* o, const void* dout,
                          const float* lse, float* delta, void* dq, void* dk, void* dv, float* ws, int B, int S, int H,
-                         int KV, int causal, float scale, hipStream_t s) {
+                         int KV, int causal, float scale, int64_t dqs, int64_t dkvs, hipStream_t s) {
   const int64_t nrows = (int64_t)B * S * H;
   attn_bwd_delta_kernel<D><<<(unsigned)((nrows * (D / 8) + 255) / 256), 256, 0, s>>>(
       (const bf16_t*)o, (const bf16_t*)dout, lse, delta, S, H, nrows);
@@ -1411,20 +1414,20 @@ static int attn_bwd_impl(const void* q, const void* k, const void* v, const void
   if (keys_per_wave == 64) {
     if (causal)
       attn_bwd_dkdv64_kernel<true, D><<<gkv64, 256, 0, s>>>(bq, bk, bv, bdo, lse, delta, (bf16_t*)dk, (bf16_t*)dv,
-                                                            ws, S, H, KV, gsplit, sl2, scale);
+                                                            ws, S, H, KV, gsplit, sl2, scale, dkvs);
     else
       attn_bwd_dkdv64_kernel<false, D><<<gkv64, 256, 0, s>>>(bq, bk, bv, bdo, lse, delta, (bf16_t*)dk, (bf16_t*)dv,
-                                                             ws, S, H, KV, gsplit, sl2, scale);
+                                                             ws, S, H, KV, gsplit, sl2, scale, dkvs);
     if (gsplit > 1) {
       EDL_LAUNCH_CHECK();
       const int64_t rows = (int64_t)B * S * KV;
       attn_dkdv_reduce_kernel<D><<<(unsigned)((rows * (2 * D / 8) + 255) / 256), 256, 0, s>>>(
-          ws, (bf16_t*)dk, (bf16_t*)dv, rows, gsplit);
+          ws, (bf16_t*)dk, (bf16_t*)dv, rows, gsplit, KV, dkvs);
     }
   } else {
 #define EDL_DKDV(C, O)                                                                                       \
   attn_bwd_dkdv_kernel<C, O, D><<<gkv, 256, 0, s>>>(bq, bk, bv, bdo, lse, delta, (bf16_t*)dk, (bf16_t*)dv, S, H, \
-                                                    KV, sl2, scale)
+                                                    KV, sl2, scale, dkvs)
     if (causal) {
       if (occ == 2 || D == 64) EDL_DKDV(true, 2); else EDL_DKDV(true, 1);
     } else {
@@ -1435,10 +1438,10 @@ static int attn_bwd_impl(const void* q, const void* k, const void* v, const void
   EDL_LAUNCH_CHECK();
   if (causal)
     attn_bwd_dq_kernel<true, D><<<gq, 256, 0, s>>>(bq, bk, bv, bdo, lse, delta, (bf16_t*)dq, S, H, KV, sl2, scale,
-                                                   attn_xcd_map(B, KV));
+                                                   attn_xcd_map(B, KV), dqs);
   else
     attn_bwd_dq_kernel<false, D><<<gq, 256, 0, s>>>(bq, bk, bv, bdo, lse, delta, (bf16_t*)dq, S, H, KV, sl2, scale,
-                                                    attn_xcd_map(B, KV));
+                                                    attn_xcd_map(B, KV), dqs);
   EDL_LAUNCH_CHECK();
   return 0;
 }
@@ -1479,14 +1482,26 @@ int64_t edl_attn_bwd_ws_bytes(int B, int S, int H, int KV, int causal) {
   return g == 1 ? 0 : (int64_t)g * B * S * KV * 2 * HD * 4;
 }
 
+// dq / dk / dv may be row-strided views: token rows dqs (>= H*D) and dkvs (>= KV*D) elements
+// apart, e.g. the q / k / v slices of one packed [B, S, 3, H, D] gradient (BERT's fused
+// qkv projection takes it without a concatenation pass)
+int edl_attn_bwd_strided(const void* q, const void* k, const void* v, const void* o, const void* dout,
+                         const float* lse, float* delta, void* dq, void* dk, void* dv, float* ws, int B, int S, int H,
+                         int KV, int D, int causal, float scale, int64_t dqs, int64_t dkvs, hipStream_t s) {
+  if ((D != 64 && D != 128) || H % KV != 0 || S <= 0) return (int)hipErrorInvalidValue;
+  if (dqs < (int64_t)H * D || dkvs < (int64_t)KV * D || dqs % 8 || dkvs % 8) return (int)hipErrorInvalidValue;
+  if (edl_attn_bwd_ws_bytes(B, S, H, KV, causal) > 0 && ws == nullptr) return (int)hipErrorInvalidValue;
+  if (D == 128)
+    return attn_bwd_impl<128>(q, k, v, o, dout, lse, delta, dq, dk, dv, ws, B, S, H, KV, causal, scale, dqs, dkvs,
+                              s);
+  return attn_bwd_impl<64>(q, k, v, o, dout, lse, delta, dq, dk, dv, ws, B, S, H, KV, causal, scale, dqs, dkvs, s);
+}
+
 int edl_attn_bwd(const void* q, const void* k, const void* v, const void* o, const void* dout, const float* lse,
                  float* delta, void* dq, void* dk, void* dv, float* ws, int B, int S, int H, int KV, int D,
                  int causal, float scale, hipStream_t s) {
-  if ((D != 64 && D != 128) || H % KV != 0 || S <= 0) return (int)hipErrorInvalidValue;
-  if (edl_attn_bwd_ws_bytes(B, S, H, KV, causal) > 0 && ws == nullptr) return (int)hipErrorInvalidValue;
-  if (D == 128)
-    return attn_bwd_impl<128>(q, k, v, o, dout, lse, delta, dq, dk, dv, ws, B, S, H, KV, causal, scale, s);
-  return attn_bwd_impl<64>(q, k, v, o, dout, lse, delta, dq, dk, dv, ws, B, S, H, KV, causal, scale, s);
+  return edl_attn_bwd_strided(q, k, v, o, dout, lse, delta, dq, dk, dv, ws, B, S, H, KV, D, causal, scale,
+                              (int64_t)H * D, (int64_t)KV * D, s);
 }
 
 }  // extern "C"

@@ -549,6 +549,103 @@ __global__ __launch_bounds__(256) void swiglu_bwd_t_reg_kernel(const bf16_t* __r
   for (int j = 0; j < 8; ++j) *reinterpret_cast<u32x4*>(dguT + (int64_t)(F + c + j) * M + r) = d8[j];
 }
 
+// ---------------------------------------------------------------------------
+// tanh-approximated GELU (BERT MLP) with the transposed operand the NT weight-
+// gradient GEMM needs, same register-transposed 8x8 blocks as the SwiGLU pair.
+// forward: h = gelu(u), hT = h^T.  backward: du = gelu'(u) * dh, duT = du^T and
+// per-128-row-tile column sums of du (the fc1 bias gradient, reduced by
+// edl_colsum) -- one pass replaces PyTorch's GELU kernels plus a separate
+// transpose of h and a transpose + column sum of du.
+// ---------------------------------------------------------------------------
+constexpr float kGeluC = 0.7978845608028654f;   // sqrt(2 / pi)
+constexpr float kGeluA = 0.044715f;
+
+__device__ __forceinline__ float gelu_tanh_(float u) {
+  const float z = kGeluC * (u + kGeluA * u * u * u);
+  const float t = 1.f - 2.f / (__expf(2.f * z) + 1.f);   // tanh(z), saturates cleanly at +-inf
+  return 0.5f * u * (1.f + t);
+}
+
+__device__ __forceinline__ float gelu_tanh_grad_(float u) {
+  const float z = kGeluC * (u + kGeluA * u * u * u);
+  const float t = 1.f - 2.f / (__expf(2.f * z) + 1.f);
+  return 0.5f * (1.f + t) + 0.5f * u * (1.f - t * t) * kGeluC * (1.f + 3.f * kGeluA * u * u);
+}
+
+__global__ __launch_bounds__(256) void gelu_fwd_t_reg_kernel(const bf16_t* __restrict__ u, bf16_t* __restrict__ h,
+                                                             bf16_t* __restrict__ hT, int M, int F) {
+  int r, c;
+  block8_origin(r, c);
+  if (r >= M || c >= F) return;
+  u32x4 o8[8], t8[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) o8[i] = *reinterpret_cast<const u32x4*>(u + (int64_t)(r + i) * F + c);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    float x[8];
+    unpack8(o8[i], x);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) x[k] = gelu_tanh_(x[k]);
+    o8[i] = pack8(x);
+    *reinterpret_cast<u32x4*>(h + (int64_t)(r + i) * F + c) = o8[i];
+  }
+  transpose8x8(o8, t8);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) *reinterpret_cast<u32x4*>(hT + (int64_t)(c + j) * M + r) = t8[j];
+}
+
+__global__ __launch_bounds__(256) void gelu_bwd_t_reg_kernel(const bf16_t* __restrict__ dh,
+                                                             const bf16_t* __restrict__ u, bf16_t* __restrict__ du,
+                                                             bf16_t* __restrict__ duT, float* __restrict__ partial,
+                                                             int M, int F) {
+  __shared__ float red[16][RT + 4];
+  int r, c;
+  block8_origin(r, c);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int rg = (w >> 1) * 8 + (lane >> 3), c0 = ((w & 1) * 8 + (lane & 7)) * 8;
+  const bool live = r < M && c < F;   // M, F multiples of 8: a block is all in or all out
+  float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (live) {
+    u32x4 a8[8], d8[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      a8[i] = *reinterpret_cast<const u32x4*>(u + (int64_t)(r + i) * F + c);
+      d8[i] = *reinterpret_cast<const u32x4*>(dh + (int64_t)(r + i) * F + c);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float x[8], d[8];
+      unpack8(a8[i], x);
+      unpack8(d8[i], d);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        x[k] = d[k] * gelu_tanh_grad_(x[k]);
+        cs[k] += x[k];
+      }
+      a8[i] = pack8(x);
+      *reinterpret_cast<u32x4*>(du + (int64_t)(r + i) * F + c) = a8[i];
+    }
+    transpose8x8(a8, d8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) *reinterpret_cast<u32x4*>(duT + (int64_t)(c + j) * M + r) = d8[j];
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) red[rg][c0 + k] = cs[k];
+  __syncthreads();
+  if (threadIdx.x < RT) {   // this tile's column origin / row-tile index (block8_origin's mapping)
+    const int gx = gridDim.x, gy = gridDim.y;
+    const int b = blockIdx.x + gx * blockIdx.y;
+    const int ty = b % gy, tx = (b / gy + ty) % gx;
+    const int col = tx * RT + threadIdx.x;
+    if (col < F) {
+      float t = 0.f;
+#pragma unroll
+      for (int g = 0; g < 16; ++g) t += red[g][threadIdx.x];
+      partial[(int64_t)ty * F + col] = t;
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -601,6 +698,26 @@ int edl_swiglu_bwd_t_lds(const void* dh, const void* gu, void* dgu, void* dguT, 
   dim3 grid((F + TT - 1) / TT, (M + TT - 1) / TT);
   swiglu_bwd_t_kernel<<<grid, 256, 0, s>>>((const bf16_t*)dh, (const bf16_t*)gu, (bf16_t*)dgu, (bf16_t*)dguT, M,
                                            F);
+  EDL_LAUNCH_CHECK();
+  return 0;
+}
+
+// h = gelu_tanh(u) and hT = h^T (M, F multiples of 8)
+int edl_gelu_fwd_t(const void* u, void* h, void* hT, int M, int F, hipStream_t s) {
+  if (F % 8 || M % 8 || M <= 0 || F <= 0) return (int)hipErrorInvalidValue;
+  dim3 grid((F + RT - 1) / RT, (M + RT - 1) / RT);
+  gelu_fwd_t_reg_kernel<<<grid, 256, 0, s>>>((const bf16_t*)u, (bf16_t*)h, (bf16_t*)hT, M, F);
+  EDL_LAUNCH_CHECK();
+  return 0;
+}
+
+// du = gelu_tanh'(u) * dh, duT = du^T, partial[edl_transpose_tiles(M), F] = column sums of du
+int edl_gelu_bwd_t(const void* dh, const void* u, void* du, void* duT, float* partial, int M, int F,
+                   hipStream_t s) {
+  if (F % 8 || M % 8 || M <= 0 || F <= 0) return (int)hipErrorInvalidValue;
+  dim3 grid((F + RT - 1) / RT, (M + RT - 1) / RT);
+  gelu_bwd_t_reg_kernel<<<grid, 256, 0, s>>>((const bf16_t*)dh, (const bf16_t*)u, (bf16_t*)du, (bf16_t*)duT,
+                                             partial, M, F);
   EDL_LAUNCH_CHECK();
   return 0;
 }

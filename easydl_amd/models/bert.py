@@ -15,7 +15,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from easydl_amd.ops import fused, norms
-from easydl_amd.ops.attention import flash_attention
+from easydl_amd.ops.attention import packed_qkv_attention
 
 
 @dataclass
@@ -70,20 +70,20 @@ class BertLayer(nn.Module):
     def forward(self, x, B, S, mask=None):
         c = self.c
         H, hd = c.n_heads, c.dim // c.n_heads
-        qkv = fused.linear(x, self.wqkv, self.bqkv).view(B, S, 3, H, hd)
-        q, k, v = qkv.unbind(2)
-        q, k, v = (t.transpose(1, 2) for t in (q, k, v))
-        if q.is_cuda and mask is None:
-            o = flash_attention(q, k, v, causal=False)   # HIP kernels, head dim 64
-        elif q.is_cuda:
-            o = F.scaled_dot_product_attention(q, k, v, attn_mask=mask)
+        qkv = fused.linear(x, self.wqkv, self.bqkv)
+        if qkv.is_cuda and mask is None:
+            # HIP kernels, head dim 64; dq / dk / dv land in one packed qkv gradient
+            o = packed_qkv_attention(qkv, B, S, H, causal=False)
         else:
-            o = F.scaled_dot_product_attention(q.float(), k.float(), v.float(), attn_mask=mask).to(q.dtype)
-        o = o.transpose(1, 2).reshape(B * S, c.dim)
+            q, k, v = (t.transpose(1, 2) for t in qkv.view(B, S, 3, H, hd).unbind(2))
+            if q.is_cuda:
+                o = F.scaled_dot_product_attention(q, k, v, attn_mask=mask)
+            else:
+                o = F.scaled_dot_product_attention(q.float(), k.float(), v.float(), attn_mask=mask).to(q.dtype)
+            o = o.transpose(1, 2).reshape(B * S, c.dim)
         a = fused.linear(o, self.wo, self.bo)
         x, _ = norms.add_layernorm(a, x, self.ln1_w, self.ln1_b, c.eps)
-        h = F.gelu(fused.linear(x, self.w1, self.b1), approximate="tanh")
-        m = fused.linear(h, self.w2, self.b2)
+        m = fused.gelu_mlp(x, self.w1, self.b1, self.w2, self.b2)
         x, _ = norms.add_layernorm(m, x, self.ln2_w, self.ln2_b, c.eps)
         return x
 

@@ -60,6 +60,57 @@ class _FlashAttnFn(torch.autograd.Function):
         return dq.transpose(1, 2), dk.transpose(1, 2), dv.transpose(1, 2), None, None
 
 
+class _PackedQKVAttnFn(torch.autograd.Function):
+    """Attention over one packed ``[B*S, 3*H*D]`` q|k|v projection (BERT's fused qkv
+    Linear).  The backward kernels write dq / dk / dv straight into the slices of one
+    packed gradient (row stride 3*H*D), so the qkv projection's backward gets its input
+    gradient without the concatenation pass autograd's unbind would run."""
+
+    @staticmethod
+    def forward(ctx, qkv, B, S, H, causal, scale):
+        kn = _native.kernels()
+        D = qkv.shape[-1] // (3 * H)
+        qkv5 = qkv.view(B, S, 3, H, D)
+        qm, km, vm = (qkv5[:, :, i].contiguous() for i in range(3))
+        o = torch.empty_like(qm)
+        lse = torch.empty(B, H, S, dtype=torch.float32, device=qkv.device)
+        kn.check("edl_attn_fwd", qm.data_ptr(), km.data_ptr(), vm.data_ptr(), o.data_ptr(), lse.data_ptr(), B, S, H,
+                 H, D, 1 if causal else 0, scale, _native.stream_of(qkv))
+        ctx.save_for_backward(qm, km, vm, o, lse)
+        ctx.causal, ctx.scale = causal, scale
+        return o.view(B * S, H * D)
+
+    @staticmethod
+    def backward(ctx, do):
+        kn = _native.kernels()
+        qm, km, vm, o, lse = ctx.saved_tensors
+        B, S, H, D = qm.shape
+        dom = do.reshape(B, S, H, D).contiguous()
+        dqkv = torch.empty(B * S, 3 * H * D, dtype=qm.dtype, device=qm.device)
+        delta = torch.empty(2, B, H, S, dtype=torch.float32, device=qm.device)
+        causal = 1 if ctx.causal else 0
+        nws = kn.raw("edl_attn_bwd_ws_bytes")(B, S, H, H, causal)
+        ws = torch.empty(nws // 4, dtype=torch.float32, device=qm.device) if nws else None
+        base, row = dqkv.data_ptr(), H * D
+        kn.check("edl_attn_bwd_strided", qm.data_ptr(), km.data_ptr(), vm.data_ptr(), o.data_ptr(), dom.data_ptr(),
+                 lse.data_ptr(), delta.data_ptr(), base, base + 2 * row, base + 4 * row,
+                 ws.data_ptr() if ws is not None else None, B, S, H, H, D, causal, ctx.scale, 3 * row, 3 * row,
+                 _native.stream_of(qm))
+        return dqkv, None, None, None, None, None
+
+
+def packed_qkv_attention(qkv: torch.Tensor, B: int, S: int, H: int, causal: bool = False,
+                         scale: float | None = None) -> torch.Tensor:
+    """``qkv`` [B*S, 3*H*D] (q | k | v per token, multi-head) -> attention output [B*S, H*D]."""
+    D = qkv.shape[-1] // (3 * H)
+    scale = 1.0 / math.sqrt(D) if scale is None else scale
+    if (qkv.is_cuda and D in (64, 128) and qkv.dtype == torch.bfloat16 and qkv.is_contiguous()
+            and os.environ.get("EDL_ATTN", "hip") != "sdpa"):
+        return _PackedQKVAttnFn.apply(qkv, B, S, H, causal, scale)
+    q, k, v = (t.transpose(1, 2) for t in qkv.view(B, S, 3, H, D).unbind(2))
+    return flash_attention(q, k, v, causal, scale).transpose(1, 2).reshape(B * S, H * D)
+
+
 def attention_ref(q, k, v, causal=True, scale=None):
     """fp32 reference (GQA by head repetition)."""
     H, KV = q.shape[1], k.shape[1]

@@ -405,6 +405,75 @@ def swiglu_mlp(x, w_gu, w_down):
     return linear(swiglu(linear(x, w_gu)), w_down)
 
 
+def _bias_grad(k, b, partial, G, cols, stream):
+    """Bias gradient from [G, cols] column-sum partials (into the flat buffer, or returned)."""
+    from easydl_amd.ops.norms import _deliver_colsum
+    g = _deliver_colsum(k, b, partial, G, cols, stream)
+    return None if g is None else g.to(b.dtype)
+
+
+class _GeluMLPFn(torch.autograd.Function):
+    """``fc2(gelu_tanh(fc1(x)))`` -- the BERT MLP, biases on both layers -- with both
+    weight gradients in hipBLASLt's NT form.  The GELU kernels write the transposed
+    operands: the forward writes h^T beside h and saves only h^T (plus fc1's output);
+    the backward writes du^T beside du, with the per-tile column sums that make fc1's
+    bias gradient in the same pass.  That replaces PyTorch's GELU forward/backward
+    kernels, the transpose of h and the transpose + column sum of du."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2):
+        k = _native.kernels()
+        x2 = x.reshape(-1, x.shape[-1])
+        u = F.linear(x2, w1, b1)
+        M, Fd = u.shape
+        h = torch.empty_like(u)
+        hT = torch.empty(Fd, M, dtype=u.dtype, device=u.device)
+        st = _native.stream_of(u)
+        k.check("edl_gelu_fwd_t", u.data_ptr(), h.data_ptr(), hT.data_ptr(), M, Fd, st)
+        y = F.linear(h, w2, b2)
+        del h
+        wt1 = _wt_of(w1) if ctx.needs_input_grad[0] else None
+        ctx.save_for_backward(x2, u, hT, w1, w2, wt1, _wt_of(w2))
+        ctx.b1, ctx.b2 = b1, b2
+        return y.view(*x.shape[:-1], w2.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        k = _native.kernels()
+        x2, u, hT, w1, w2, wt1, wt2 = ctx.saved_tensors
+        dy2 = dy.reshape(-1, dy.shape[-1]).contiguous()
+        M, Fd = u.shape
+        st = _native.stream_of(u)
+        dh = torch.mm(dy2, wt2.t()) if wt2 is not None else torch.mm(dy2, w2)
+        dyT, part2, G = _transposed_colsum(dy2)
+        dw2 = _deliver_wgrad(w2, dyT, hT.t())
+        del hT, dyT
+        db2 = _bias_grad(k, ctx.b2, part2, G, dy2.shape[1], st) if ctx.needs_input_grad[4] else None
+        du = torch.empty_like(u)
+        duT = torch.empty(Fd, M, dtype=u.dtype, device=u.device)
+        part1 = torch.empty(G, Fd, dtype=torch.float32, device=u.device)
+        k.check("edl_gelu_bwd_t", dh.data_ptr(), u.data_ptr(), du.data_ptr(), duT.data_ptr(), part1.data_ptr(),
+                M, Fd, st)
+        del dh
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.mm(du, wt1.t()) if wt1 is not None else torch.mm(du, w1)
+            dx = dx.view(*dy.shape[:-1], w1.shape[1])
+        del du
+        dw1 = _deliver_wgrad(w1, duT, _transposed(x2).t())
+        db1 = _bias_grad(k, ctx.b1, part1, G, Fd, st) if ctx.needs_input_grad[2] else None
+        return dx, dw1, db1, dw2, db2
+
+
+def gelu_mlp(x, w1, b1, w2, b2):
+    """BERT MLP ``fc2(gelu_tanh(fc1(x)))`` (biases ``b1``, ``b2``)."""
+    x2 = x.reshape(-1, x.shape[-1])
+    if (_MLP_FUSED and _native.use_hip(x) and x.dtype == torch.bfloat16 and _nt_wgrad_ok(x2, x2)
+            and x2.shape[0] % 8 == 0 and w1.shape[0] % 8 == 0 and b1 is not None and b2 is not None):
+        return _GeluMLPFn.apply(x, w1, b1, w2, b2)
+    return linear(F.gelu(linear(x, w1, b1), approximate="tanh"), w2, b2)
+
+
 class _EmbeddingFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, ids, w):

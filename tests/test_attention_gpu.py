@@ -144,3 +144,34 @@ def test_llama_on_hip_kernels_matches_fp32_cpu_model(cuda, hd):
     for (n, p), (_, p2) in zip(ref.named_parameters(), m.named_parameters()):
         err = ((p2.grad.float().cpu() - p.grad).norm() / p.grad.norm().clamp_min(1e-12)).item()
         assert err < 5e-2, (n, err)
+
+
+@pytest.mark.parametrize("B,S,H,D,causal", [(2, 512, 16, 64, False), (1, 200, 4, 64, True), (2, 384, 8, 128, False),
+                                           (1, 1000, 4, 128, True)])
+def test_packed_qkv_attention_writes_strided_gradients(cuda, B, S, H, D, causal):
+    """packed_qkv_attention (BERT: one [B*S, 3*H*D] projection in, dq/dk/dv written by the
+    kernels straight into one packed gradient at row stride 3*H*D) is bitwise identical to
+    flash_attention on the unpacked views, and within tolerance of the fp32 reference."""
+    from easydl_amd.ops.attention import packed_qkv_attention
+    g = torch.Generator(device=cuda).manual_seed(S + H)
+    qkv = torch.randn(B * S, 3 * H * D, device=cuda, generator=g).to(torch.bfloat16)
+    do = torch.randn(B * S, H * D, device=cuda, generator=g).to(torch.bfloat16)
+    p = qkv.clone().requires_grad_()
+    o = packed_qkv_attention(p, B, S, H, causal=causal)
+    assert o.shape == (B * S, H * D) and "PackedQKV" in type(o.grad_fn).__name__
+    o.backward(do)
+    u = qkv.clone().requires_grad_()
+    q, k, v = (t.transpose(1, 2) for t in u.view(B, S, 3, H, D).unbind(2))
+    ou = flash_attention(q, k, v, causal=causal).transpose(1, 2).reshape(B * S, H * D)
+    ou.backward(do)
+    assert torch.equal(o, ou)
+    assert torch.equal(p.grad, u.grad)
+    r = qkv.float().requires_grad_()
+    q, k, v = (t.transpose(1, 2) for t in r.view(B, S, 3, H, D).unbind(2))
+    orf = attention_ref(q, k, v, causal=causal).transpose(1, 2).reshape(B * S, H * D)
+    orf.backward(do.float())
+    assert _err(o, orf) < 2e-2
+    for i, n in enumerate("qkv"):
+        a = p.grad.view(B, S, 3, H, D)[:, :, i]
+        b = r.grad.view(B, S, 3, H, D)[:, :, i]
+        assert _err(a, b) < 3e-2, n

@@ -308,6 +308,66 @@ def test_fused_swiglu_mlp_matches_fp32_reference(cuda):
         assert err < 3e-2, err
 
 
+@pytest.mark.parametrize("M,Fd", [(128, 256), (200, 136), (16, 4096)])
+def test_gelu_transposed_kernels(cuda, M, Fd):
+    """edl_gelu_fwd_t / edl_gelu_bwd_t vs fp32 torch GELU (tanh): h and du within bf16
+    rounding, hT / duT exact transposes, column-sum partials = fp32 column sums of du."""
+    from easydl_amd import _native
+    k = _native.kernels()
+    st = _native.stream_of
+    torch.manual_seed(3)
+    u = (3 * torch.randn(M, Fd, device=cuda)).bfloat16()
+    dh = torch.randn(M, Fd, device=cuda).bfloat16()
+    h, hT = torch.empty_like(u), torch.empty(Fd, M, device=cuda, dtype=torch.bfloat16)
+    k.check("edl_gelu_fwd_t", u.data_ptr(), h.data_ptr(), hT.data_ptr(), M, Fd, st(u))
+    uf = u.float().requires_grad_(True)
+    hr = F.gelu(uf, approximate="tanh")
+    hr.backward(dh.float())
+    _close(h, hr, 1e-2)
+    assert torch.equal(hT, h.t())
+    G = k("edl_transpose_tiles", M)
+    du, duT = torch.empty_like(u), torch.empty(Fd, M, device=cuda, dtype=torch.bfloat16)
+    part = torch.empty(G, Fd, device=cuda)
+    k.check("edl_gelu_bwd_t", dh.data_ptr(), u.data_ptr(), du.data_ptr(), duT.data_ptr(), part.data_ptr(), M, Fd,
+            st(u))
+    _close(du, uf.grad, 1e-2)
+    assert torch.equal(duT, du.t())
+    torch.testing.assert_close(part.sum(0), uf.grad.sum(0), rtol=1e-3, atol=1e-3 * M ** 0.5)
+
+
+@pytest.mark.parametrize("flat", [False, True])
+def test_fused_gelu_mlp_matches_fp32_reference(cuda, flat):
+    """gelu_mlp (BERT MLP: GELU kernels emit h^T / du^T and fc1's bias column sums) vs an
+    fp32 PyTorch MLP: output, input gradient, both weight and both bias gradients, with
+    gradients returned to autograd or written into a flat gradient buffer (accumulated
+    over two micro-batches)."""
+    from easydl_amd.parallel.flat import FlatParams
+    torch.manual_seed(4)
+    M, D, Fd = 256, 256, 512
+    mod = torch.nn.ParameterList([torch.nn.Parameter(t.bfloat16()) for t in (
+        torch.randn(Fd, D, device=cuda) * 0.05, torch.randn(Fd, device=cuda) * 0.1,
+        torch.randn(D, Fd, device=cuda) * 0.05, torch.randn(D, device=cuda) * 0.1)])
+    pr = [p.detach().float().requires_grad_(True) for p in mod]
+    if flat:
+        FlatParams(mod)
+    fused.new_weight_generation()
+    for mb in range(2):
+        x = torch.randn(M, D, device=cuda).bfloat16().requires_grad_(True)
+        y = fused.gelu_mlp(x, *mod)
+        assert y.grad_fn is not None and "GeluMLP" in type(y.grad_fn).__name__
+        dy = torch.randn_like(y)
+        y.backward(dy)
+        xr = x.detach().float().requires_grad_(True)
+        yr = F.linear(F.gelu(F.linear(xr, pr[0], pr[1]), approximate="tanh"), pr[2], pr[3])
+        yr.backward(dy.float())
+        for a, b in ((y, yr), (x.grad, xr.grad)):
+            err = ((a.float() - b).abs().max() / (b.abs().max() + 1e-6)).item()
+            assert err < 3e-2, err
+    for p, r in zip(mod, pr):
+        err = ((p.grad.float() - r.grad).abs().max() / (r.grad.abs().max() + 1e-6)).item()
+        assert err < 3e-2, (tuple(p.shape), err)
+
+
 @pytest.mark.parametrize("G,cols", [(1, 4), (63, 64), (65, 1000), (1024, 1024), (1100, 4096), (512, 28)])
 @pytest.mark.parametrize("odt,acc", [(1, 0), (1, 1), (0, 1)])
 def test_colsum_partials(cuda, G, cols, odt, acc):
