@@ -67,6 +67,8 @@ class _NormFn(torch.autograd.Function):
             res = res.contiguous()
             s = torch.empty_like(x)
         st = _native.stream_of(x)
+        # an unused sum output (post-LN BERT drops it) arrives as ds=None instead of a zero-filled tensor
+        ctx.set_materialize_grads(False)
         if ln:
             k.check("edl_layernorm_fwd", x.data_ptr(), _native.ptr(res), _native.ptr(s), w.data_ptr(),
                     b.data_ptr(), y.data_ptr(), mean.data_ptr(), rstd.data_ptr(), rows, cols, eps, st)
@@ -87,7 +89,7 @@ class _NormFn(torch.autograd.Function):
         src, w, b, mean, rstd = ctx.saved_tensors
         cols = src.shape[-1]
         rows = src.numel() // cols
-        dy = dy.contiguous()
+        dy = torch.zeros_like(src) if dy is None else dy.contiguous()
         if ds is not None:
             ds = ds.contiguous()
         dx = torch.empty_like(src)
