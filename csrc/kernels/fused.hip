@@ -549,6 +549,24 @@ __global__ __launch_bounds__(256) void swiglu_bwd_t_reg_kernel(const bf16_t* __r
   for (int j = 0; j < 8; ++j) *reinterpret_cast<u32x4*>(dguT + (int64_t)(F + c + j) * M + r) = d8[j];
 }
 
+// packed [T, 3, HD] q|k|v rows -> contiguous q, k, v [T, HD] in one pass (BERT: one
+// launch instead of three strided copies); 8 bf16 per chunk, a chunk of each of q, k, v per iteration
+__global__ __launch_bounds__(256) void qkv_split_kernel(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ q,
+                                                        bf16_t* __restrict__ k, bf16_t* __restrict__ v, int64_t T,
+                                                        int hd8) {
+  const int64_t n = T * hd8;   // chunks per output tensor
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const int64_t t = i / hd8;
+    const int c = (int)(i - t * hd8);
+    const u32x4* src = reinterpret_cast<const u32x4*>(qkv) + t * 3 * hd8 + c;
+    const u32x4 a = src[0], b = src[hd8], d = src[2 * hd8];
+    reinterpret_cast<u32x4*>(q)[i] = a;
+    reinterpret_cast<u32x4*>(k)[i] = b;
+    reinterpret_cast<u32x4*>(v)[i] = d;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // tanh-approximated GELU (BERT MLP) with the transposed operand the NT weight-
 // gradient GEMM needs, same register-transposed 8x8 blocks as the SwiGLU pair.
@@ -698,6 +716,15 @@ int edl_swiglu_bwd_t_lds(const void* dh, const void* gu, void* dgu, void* dguT, 
   dim3 grid((F + TT - 1) / TT, (M + TT - 1) / TT);
   swiglu_bwd_t_kernel<<<grid, 256, 0, s>>>((const bf16_t*)dh, (const bf16_t*)gu, (bf16_t*)dgu, (bf16_t*)dguT, M,
                                            F);
+  EDL_LAUNCH_CHECK();
+  return 0;
+}
+
+// q / k / v [T, HD] = slices of packed qkv [T, 3 * HD] (HD multiple of 8)
+int edl_qkv_split(const void* qkv, void* q, void* k, void* v, int64_t T, int HD, hipStream_t s) {
+  if (HD % 8 || T <= 0) return (int)hipErrorInvalidValue;
+  qkv_split_kernel<<<grid_for(T * (HD / 8)), 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)q, (bf16_t*)k, (bf16_t*)v, T,
+                                                          HD / 8);
   EDL_LAUNCH_CHECK();
   return 0;
 }

@@ -52,6 +52,7 @@ _KERNEL_SIGS = {
     "edl_swiglu_fwd_t": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],
     "edl_swiglu_bwd_t": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],
     "edl_gelu_fwd_t": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],
+    "edl_qkv_split": [c_void_p, c_void_p, c_void_p, c_void_p, c_i64, c_int, c_void_p],
     "edl_gelu_bwd_t": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],
     "edl_rope_qkv_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_i64, c_int, c_int, c_int,
                          c_int, c_void_p],

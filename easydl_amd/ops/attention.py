@@ -70,8 +70,9 @@ class _PackedQKVAttnFn(torch.autograd.Function):
     def forward(ctx, qkv, B, S, H, causal, scale):
         kn = _native.kernels()
         D = qkv.shape[-1] // (3 * H)
-        qkv5 = qkv.view(B, S, 3, H, D)
-        qm, km, vm = (qkv5[:, :, i].contiguous() for i in range(3))
+        qm, km, vm = (torch.empty(B, S, H, D, dtype=qkv.dtype, device=qkv.device) for _ in range(3))
+        kn.check("edl_qkv_split", qkv.data_ptr(), qm.data_ptr(), km.data_ptr(), vm.data_ptr(), B * S, H * D,
+                 _native.stream_of(qkv))
         o = torch.empty_like(qm)
         lse = torch.empty(B, H, S, dtype=torch.float32, device=qkv.device)
         kn.check("edl_attn_fwd", qm.data_ptr(), km.data_ptr(), vm.data_ptr(), o.data_ptr(), lse.data_ptr(), B, S, H,
