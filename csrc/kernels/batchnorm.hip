@@ -256,15 +256,17 @@ __global__ __launch_bounds__(kFinThreads) void bn_bwd_finalize_kernel(const floa
                                                                       const float* __restrict__ mean,
                                                                       const float* __restrict__ rstd,
                                                                       float* __restrict__ dw, float* __restrict__ db,
-                                                                      float* __restrict__ coef) {
+                                                                      float* __restrict__ coef, int acc) {
   double s, q;
   sum_partials(part, G, C, s, q);
   const int c = blockIdx.x * 64 + threadIdx.x;
   if (threadIdx.x >= 64 || c >= C) return;
   const double rs = (double)rstd[c];
   const double gw = q * rs, gb = s;
-  dw[c] = (float)gw;
-  db[c] = (float)gb;
+  // acc: dw / db are views of a flat gradient buffer that already holds earlier
+  // micro-batches' gradients (no separate autograd accumulate launch per parameter)
+  dw[c] = acc ? dw[c] + (float)gw : (float)gw;
+  db[c] = acc ? db[c] + (float)gb : (float)gb;
   const double A = (double)w[c] * rs;
   const double K1 = A * rs * gw / (double)M;
   coef[c] = (float)A;
@@ -388,7 +390,7 @@ int edl_bn_apply(const void* x, const void* res, void* z, const float* coef, int
 // coef: fp32 [3C] scratch; part as in the forward.
 int edl_bn_bwd(const void* dz, const void* z, const void* x, const float* w, const float* mean, const float* rstd,
                void* dx, void* dres, float* dw, float* db, float* coef, float* part, int64_t M, int C, int relu,
-               hipStream_t s) {
+               int acc, hipStream_t s) {
   if (!shape_ok(M, C) || (relu && z == nullptr)) return (int)hipErrorInvalidValue;
   const int G = row_blocks(M, C), Cb = chunk_of(C);
   const dim3 grid(G, C / Cb);
@@ -399,7 +401,7 @@ int edl_bn_bwd(const void* dz, const void* z, const void* x, const float* w, con
     bn_bwd_reduce_kernel<false><<<grid, kThreads, 0, s>>>((const bf16_t*)dz, nullptr, (const bf16_t*)x, mean, M,
                                                           C, Cb, part);
   EDL_LAUNCH_CHECK();
-  bn_bwd_finalize_kernel<<<(C + 63) / 64, kFinThreads, 0, s>>>(part, G, C, M, w, mean, rstd, dw, db, coef);
+  bn_bwd_finalize_kernel<<<(C + 63) / 64, kFinThreads, 0, s>>>(part, G, C, M, w, mean, rstd, dw, db, coef, acc);
   EDL_LAUNCH_CHECK();
   const int GA = blocks_for(M, C, 4, 2048);
 #define EDL_BN_DX(L, D)                                                                                        \

@@ -15,6 +15,7 @@ import torch
 import torch.nn.functional as F
 
 from easydl_amd import _native
+from easydl_amd.ops import gradsink
 
 
 def bn_act_ref(x, bn, residual=None, relu=True):
@@ -66,6 +67,7 @@ class _BNActFn(torch.autograd.Function):
                 part.data_ptr(), M, C, momentum, eps, int(relu), _native.stream_of(x))
         ctx.save_for_backward(x, z if relu else None, w, mean, rstd)
         ctx.relu, ctx.has_res = relu, res is not None
+        ctx.bn_b = b
         return z
 
     @staticmethod
@@ -79,13 +81,27 @@ class _BNActFn(torch.autograd.Function):
         dev = x.device
         dx = torch.empty_like(x)
         dres = torch.empty_like(x) if ctx.has_res and ctx.needs_input_grad[1] else None
-        dw = torch.empty(C, dtype=torch.float32, device=dev)
-        db = torch.empty(C, dtype=torch.float32, device=dev)
+        # weight / bias gradients go straight into flat fp32 gradient views when both are
+        # flat-managed (written on the first micro-batch, accumulated after): no per-parameter
+        # autograd accumulate launch.  Otherwise they are returned to autograd.
+        b = ctx.bn_b
+        direct = (gradsink.is_flat(w) and gradsink.is_flat(b) and w.grad.dtype == torch.float32
+                  and b.grad.dtype == torch.float32 and gradsink.is_fresh(w) == gradsink.is_fresh(b))
+        if direct:
+            dw, db, acc = w.grad, b.grad, 0 if gradsink.is_fresh(w) else 1
+        else:
+            dw = torch.empty(C, dtype=torch.float32, device=dev)
+            db = torch.empty(C, dtype=torch.float32, device=dev)
+            acc = 0
         coef = torch.empty(3 * C, dtype=torch.float32, device=dev)
         part = torch.empty(2 * C * G, dtype=torch.float32, device=dev)
         k.check("edl_bn_bwd", dz2.data_ptr(), _native.ptr(z), x.data_ptr(), w.data_ptr(), mean.data_ptr(),
                 rstd.data_ptr(), dx.data_ptr(), _native.ptr(dres), dw.data_ptr(), db.data_ptr(), coef.data_ptr(),
-                part.data_ptr(), M, C, int(ctx.relu), _native.stream_of(x))
+                part.data_ptr(), M, C, int(ctx.relu), acc, _native.stream_of(x))
+        if direct:
+            gradsink.commit(w)
+            gradsink.commit(b)
+            return dx, dres, None, None, None, None, None, None, None
         return (dx, dres, dw if ctx.needs_input_grad[2] else None, db if ctx.needs_input_grad[3] else None,
                 None, None, None, None, None)
 

@@ -6,7 +6,7 @@ import sys
 
 rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-key = sys.argv[2] if len(sys.argv) > 2 else "adamw"
+key = sys.argv[2] if len(sys.argv) > 2 else "clip_finalize"   # one launch per optimizer step (AdamW or SGD)
 opt = [r for r in rows if key in r["Kernel_Name"]]
 n = min(3, len(opt) - 1)
 a, b = int(opt[-1 - n]["End_Timestamp"]), int(opt[-1]["End_Timestamp"])

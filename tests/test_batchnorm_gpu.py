@@ -86,3 +86,27 @@ def test_resnet50_step_runs_on_fused_batchnorm(cuda):
     loss.backward()
     assert torch.isfinite(loss)
     assert all(p.grad is not None and torch.isfinite(p.grad).all() for p in m.parameters())
+
+
+def test_bn_param_grads_go_straight_into_flat_buffer(cuda):
+    """With FlatParams managing the BatchNorm weight / bias, the backward kernel writes their
+    gradients into the flat fp32 buffer (first micro-batch) and accumulates (second one);
+    the result matches the autograd-returned gradients, and the ready callback fires."""
+    from easydl_amd.parallel.flat import FlatParams
+    C = 64
+    bn_a, bn_b = _bn(C, 7), _bn(C, 7)
+    FlatParams(bn_b)
+    fired = []
+    for p in (bn_b.weight, bn_b.bias):
+        p._edl_ready_cb = fired.append
+    xs = [torch.randn(4, C, 14, 14, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+          for _ in range(2)]
+    dzs = [torch.randn_like(x) for x in xs]
+    for x, dz in zip(xs, dzs):
+        bn_act(x, bn_a).backward(dz)
+        z = bn_act(x, bn_b)
+        assert "BNAct" in type(z.grad_fn).__name__
+        z.backward(dz)
+    assert len(fired) == 4
+    for pa, pb in ((bn_a.weight, bn_b.weight), (bn_a.bias, bn_b.bias)):
+        assert _rel(pb.grad, pa.grad) < 1e-5
