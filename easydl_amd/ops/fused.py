@@ -312,10 +312,7 @@ class _LinearFn(torch.autograd.Function):
                 a, b_ = dyT, _transposed(x2).t()   # dY^T (contiguous) @ (X^T)^T: NT GEMM
             else:
                 a, b_ = dy2.t(), x2
-            if gradsink.is_flat(w):
-                gradsink.write_mm(w, a, b_)
-            else:
-                dw = torch.mm(a, b_)
+            dw = _deliver_wgrad(w, a, b_)
         if want_db:
             b = ctx.b
             if bias_partial is not None:
@@ -339,9 +336,71 @@ def linear(x, w, b=None):
     return F.linear(x, w, b)
 
 
+# Weight-gradient GEMMs on a side stream.  dW = dY^T X feeds nothing else in the
+# backward, so it can run beside the input-gradient chain: hipBLASLt's Stream-K
+# kernels hold every CU with one 256-VGPR / 130 KB-LDS workgroup, which leaves room
+# on each SIMD for the chain's memory-bound kernels (transposes, SwiGLU, norms,
+# RoPE; <= 84 VGPRs, <= 512 B LDS) to co-run.  The side stream waits for the main
+# stream before each GEMM; its operands are record_stream'ed so the allocator does
+# not hand their memory back to the main stream early; ElasticDDP launches bucket
+# all-reduces behind both streams and joins them in finish().  Opt-in
+# (EDL_WGRAD_STREAM=1): measured on MI355X it slows the Llama-3-8B step 2.79 ->
+# 3.6-4.1 s (two GEMMs co-running thrash each other) and ties on BERT-large
+# (profiles/r02_wgrad_stream_ab.txt), so by default every GEMM stays on the compute stream.
+_WGRAD_STREAM = os.environ.get("EDL_WGRAD_STREAM", "0") == "1"
+_SIDE: dict = {}    # device index -> side stream
+_MAIN: dict = {}    # device index -> the compute stream the side stream last forked from
+_JOIN_QUEUED: dict = {}   # device index -> end-of-backward join already queued
+
+
+def _dev_index(dev: torch.device) -> int:
+    return dev.index if dev.index is not None else torch.cuda.current_device()
+
+
+def pending_streams(device) -> list:
+    """Streams besides the current one whose queued work writes gradients (for DDP)."""
+    if device is None or torch.device(device).type != "cuda":
+        return []
+    i = _dev_index(torch.device(device))
+    return [s for s in (_MAIN.get(i), _SIDE.get(i)) if s is not None]
+
+
+def join_side_streams(device) -> None:
+    """Make the current stream wait for every queued side-stream weight gradient."""
+    if device is None or torch.device(device).type != "cuda":
+        return
+    i = _dev_index(torch.device(device))
+    _JOIN_QUEUED[i] = False   # re-arm the end-of-backward join even if a failed pass dropped it
+    side = _SIDE.get(i)
+    if side is not None:
+        torch.cuda.current_stream(device).wait_stream(side)
+
+
 def _deliver_wgrad(w, a, b_):
     """dW = a @ b_ into the flat gradient buffer (or returned)."""
     if gradsink.is_flat(w):
+        if _WGRAD_STREAM and a.is_cuda:
+            i = _dev_index(a.device)
+            main = torch.cuda.current_stream(a.device)
+            side = _SIDE.get(i)
+            if side is None:
+                side = _SIDE[i] = torch.cuda.Stream(device=a.device)
+            _MAIN[i] = main
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                gradsink.write_mm(w, a, b_)
+            a.record_stream(side)
+            b_.record_stream(side)
+            if not _JOIN_QUEUED.get(i):
+                # the compute stream waits for the side stream once this backward pass ends, so
+                # whatever reads the gradients next (optimizer, clip, tests) is ordered after them
+                _JOIN_QUEUED[i] = True
+
+                def _join(i=i, main=main, side=side):
+                    _JOIN_QUEUED[i] = False
+                    main.wait_stream(side)
+                torch.autograd.Variable._execution_engine.queue_callback(_join)
+            return None
         gradsink.write_mm(w, a, b_)
         return None
     return torch.mm(a, b_)

@@ -55,6 +55,7 @@ class ElasticDDP:
         self.sync_enabled = True
         self._works = []
         self._next = 0
+        self._launch_stream = None   # collectives launched behind the side-stream weight gradients
         self.stats = {"buckets": 0, "bytes": 0, "wait_s": 0.0}
         self._build_buckets()
         flat.set_ready_callback(self._on_ready)
@@ -91,6 +92,10 @@ class ElasticDDP:
         self.prepare()
 
     @property
+    def device(self):
+        return self.flat.groups[0].grad.device if self.flat.groups else None
+
+    @property
     def world_size(self) -> int:
         return 1 if self.comm is None else self.comm.world_size
 
@@ -124,6 +129,23 @@ class ElasticDDP:
             self._launch_ready()
 
     def _launch_ready(self) -> None:
+        from easydl_amd.ops import fused
+        others = fused.pending_streams(self.device) if self._next < len(self.buckets) else []
+        ctx = contextlib.nullcontext()
+        if others and self.buckets[self._next].ready:
+            # weight gradients may still be queued on the fused ops' side stream: launch the
+            # collectives from a stream that waits for the caller's stream and for those
+            if self._launch_stream is None:
+                self._launch_stream = torch.cuda.Stream(device=self.device)
+            ls = self._launch_stream
+            ls.wait_stream(torch.cuda.current_stream(self.device))
+            for st in others:
+                ls.wait_stream(st)
+            ctx = torch.cuda.stream(ls)
+        with ctx:
+            self._launch_buckets()
+
+    def _launch_buckets(self) -> None:
         while self._next < len(self.buckets) and self.buckets[self._next].ready:
             b = self.buckets[self._next]
             self._works.append(self.comm.all_reduce_async(b.view))
@@ -133,6 +155,8 @@ class ElasticDDP:
 
     def finish(self) -> None:
         """Flush every bucket (zeroing grads of unused params) and wait for the all-reduces."""
+        from easydl_amd.ops import fused
+        fused.join_side_streams(self.device)   # side-stream weight gradients are complete from here on
         self.flat.finalize_untouched()
         if self._active():
             for b in self.buckets:
