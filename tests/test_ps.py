@@ -169,3 +169,53 @@ def test_deepfm_sparse_tables_on_ps(mode):
     finally:
         for s in servers:
             s.stop()
+
+
+def test_reference_example_job_runs_verbatim(tmp_path):
+    """The reference's example ElasticJob (docs/design/elastic-training-operator.md:31-45) with its
+    own command line, ``python -m model_zoo.iris.dnn_estimator``, and image names, under the
+    local operator: 2 PS + 2 workers + 1 evaluator train the Iris DNN to high accuracy."""
+    spec = tmp_path / "job.yaml"
+    spec.write_text(textwrap.dedent("""
+        apiVersion: elastic.easydl.org/v1alpha1
+        kind: ElasticJob
+        metadata:
+          name: elastic-deepctr-job
+        spec:
+          command: "python -m model_zoo.iris.dnn_estimator"
+          image:
+          parameter_server:
+            image: elasticdl:iris_estimator
+          worker:
+            image: elasticdl:iris_estimator
+          evaluator:
+            image: elasticdl:iris_estimator
+          env: {EDL_NUM_PS: "2", EDL_SAMPLES: "16000"}
+        ---
+        apiVersion: elastic.easydl.org/v1alpha1
+        kind: JobResource
+        metadata:
+          name: "elastic-training-resource"
+        spec:
+          selector:
+            name: elastic-deepctr-job
+          parameter_server:
+            replicas: 2
+            resource: {cpu: 1, memory: 1024, gpu: 0}
+          worker:
+            replicas: 2
+            resource: {cpu: 1, memory: 1024, gpu: 0}
+          evaluator:
+            replicas: 1
+            resource: {cpu: 1, memory: 1024, gpu: 0}
+        """))
+    run = tmp_path / "run"
+    out = subprocess.run([sys.executable, "-m", "easydl_amd.cli", "submit", str(spec), "--gpus", "",
+                          "--run-dir", str(run), "--timeout", "240"], cwd=ROOT, capture_output=True, text=True,
+                         env=dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1"), timeout=300)
+    assert out.returncode == 0, (out.stdout + out.stderr)[-4000:]
+    ev = [json.loads(l) for f in glob.glob(str(run / "events-*.jsonl")) for l in open(f)]
+    names = {e.get("proc") for e in ev}
+    assert {"worker0", "worker1"} <= names, sorted(n for n in names if n)
+    evals = [e for e in ev if e["kind"] == "eval"]
+    assert evals and evals[-1]["acc"] > 0.85, evals[-1:]
