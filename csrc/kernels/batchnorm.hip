@@ -218,17 +218,24 @@ __global__ __launch_bounds__(kThreads) void bn_apply_kernel(const bf16_t* __rest
 
 // ---------------------------------------------------------------------------- backward
 // dp = relu ? (z > 0 ? dz : 0) : dz;   partials of sum dp and sum dp * (x - mean)
-template <bool RELU>
+// MX: no residual was added, so the ReLU mask is recomputed from x with the forward's
+// own coefficients (z > 0  <=>  fma(x, sc, sh) > 0) instead of reading z back from HBM
+template <bool RELU, bool MX>
 __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(const bf16_t* __restrict__ dz,
                                                                  const bf16_t* __restrict__ z,
                                                                  const bf16_t* __restrict__ x,
-                                                                 const float* __restrict__ mean, int64_t M, int C,
+                                                                 const float* __restrict__ mean,
+                                                                 const float* __restrict__ fcoef, int64_t M, int C,
                                                                  int Cb, float* __restrict__ part) {
   const Geo g(Cb, blockIdx.y);
   float s[8] = {}, q[8] = {};
   if (g.active) {
-    float mu[8];
+    float mu[8], sc[8], sh[8];
     load8f(mean + g.col8 * 8, mu);
+    if (MX) {
+      load8f(fcoef + g.col8 * 8, sc);
+      load8f(fcoef + C + g.col8 * 8, sh);
+    }
     int64_t r, end;
     row_range(M, g.rpi, r, end);
     const int64_t o0 = g.col8 * 8;
@@ -237,9 +244,10 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(const bf16_t* _
       float d[8], f[8], y[8];
       unpack8(*reinterpret_cast<const u32x4*>(dz + o), d);
       unpack8(*reinterpret_cast<const u32x4*>(x + o), f);
-      if (RELU) unpack8(*reinterpret_cast<const u32x4*>(z + o), y);
+      if (RELU && !MX) unpack8(*reinterpret_cast<const u32x4*>(z + o), y);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
+        if (MX) y[j] = __builtin_fmaf(f[j], sc[j], sh[j]);
         const float dp = RELU ? (y[j] > 0.f ? d[j] : 0.f) : d[j];
         s[j] += dp;
         q[j] = __builtin_fmaf(dp, f[j] - mu[j], q[j]);
@@ -274,18 +282,23 @@ __global__ __launch_bounds__(kFinThreads) void bn_bwd_finalize_kernel(const floa
   coef[2 * C + c] = (float)(K1 * (double)mean[c] - A * gb / (double)M);
 }
 
-template <bool RELU, bool DRES>
+template <bool RELU, bool DRES, bool MX>
 __global__ __launch_bounds__(kThreads) void bn_bwd_dx_kernel(const bf16_t* __restrict__ dz,
                                                              const bf16_t* __restrict__ z,
                                                              const bf16_t* __restrict__ x,
-                                                             const float* __restrict__ coef, int64_t M, int C,
+                                                             const float* __restrict__ coef,
+                                                             const float* __restrict__ fcoef, int64_t M, int C,
                                                              bf16_t* __restrict__ dx, bf16_t* __restrict__ dres) {
   const Geo g(C, 0);
   if (!g.active) return;
-  float A[8], K1[8], K2[8];
+  float A[8], K1[8], K2[8], sc[8], sh[8];
   load8f(coef + g.col8 * 8, A);
   load8f(coef + C + g.col8 * 8, K1);
   load8f(coef + 2 * C + g.col8 * 8, K2);
+  if (MX) {
+    load8f(fcoef + g.col8 * 8, sc);
+    load8f(fcoef + C + g.col8 * 8, sh);
+  }
   int64_t r, end;
   row_range(M, g.rpi, r, end);
   const int64_t o0 = g.col8 * 8;
@@ -294,10 +307,11 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_dx_kernel(const bf16_t* __res
     float d[8], f[8], y[8];
     unpack8(*reinterpret_cast<const u32x4*>(dz + o), d);
     unpack8(*reinterpret_cast<const u32x4*>(x + o), f);
-    if (RELU) unpack8(*reinterpret_cast<const u32x4*>(z + o), y);
+    if (RELU && !MX) unpack8(*reinterpret_cast<const u32x4*>(z + o), y);
     float gx[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
+      if (MX) y[j] = __builtin_fmaf(f[j], sc[j], sh[j]);
       const float dp = RELU ? (y[j] > 0.f ? d[j] : 0.f) : d[j];
       d[j] = dp;
       gx[j] = __builtin_fmaf(A[j], dp, __builtin_fmaf(-K1[j], f[j], K2[j]));
@@ -388,29 +402,37 @@ int edl_bn_apply(const void* x, const void* res, void* z, const float* coef, int
 
 // dz (and z for the ReLU mask), x, saved mean/rstd -> dx, optional d residual, dw, db (fp32 [C]).
 // coef: fp32 [3C] scratch; part as in the forward.
+// fcoef: the forward's (scale, shift) coefficients [2C]; with relu and z == nullptr the
+// ReLU mask is recomputed from x (forward without a residual), saving a read of z per pass
 int edl_bn_bwd(const void* dz, const void* z, const void* x, const float* w, const float* mean, const float* rstd,
-               void* dx, void* dres, float* dw, float* db, float* coef, float* part, int64_t M, int C, int relu,
-               int acc, hipStream_t s) {
-  if (!shape_ok(M, C) || (relu && z == nullptr)) return (int)hipErrorInvalidValue;
+               const float* fcoef, void* dx, void* dres, float* dw, float* db, float* coef, float* part, int64_t M,
+               int C, int relu, int acc, hipStream_t s) {
+  if (!shape_ok(M, C) || (relu && z == nullptr && fcoef == nullptr)) return (int)hipErrorInvalidValue;
+  const bool mx = relu && z == nullptr;
   const int G = row_blocks(M, C), Cb = chunk_of(C);
   const dim3 grid(G, C / Cb);
-  if (relu)
-    bn_bwd_reduce_kernel<true><<<grid, kThreads, 0, s>>>((const bf16_t*)dz, (const bf16_t*)z, (const bf16_t*)x,
-                                                         mean, M, C, Cb, part);
+  if (mx)
+    bn_bwd_reduce_kernel<true, true><<<grid, kThreads, 0, s>>>((const bf16_t*)dz, nullptr, (const bf16_t*)x, mean,
+                                                               fcoef, M, C, Cb, part);
+  else if (relu)
+    bn_bwd_reduce_kernel<true, false><<<grid, kThreads, 0, s>>>((const bf16_t*)dz, (const bf16_t*)z,
+                                                                (const bf16_t*)x, mean, nullptr, M, C, Cb, part);
   else
-    bn_bwd_reduce_kernel<false><<<grid, kThreads, 0, s>>>((const bf16_t*)dz, nullptr, (const bf16_t*)x, mean, M,
-                                                          C, Cb, part);
+    bn_bwd_reduce_kernel<false, false><<<grid, kThreads, 0, s>>>((const bf16_t*)dz, nullptr, (const bf16_t*)x, mean,
+                                                                 nullptr, M, C, Cb, part);
   EDL_LAUNCH_CHECK();
   bn_bwd_finalize_kernel<<<(C + 63) / 64, kFinThreads, 0, s>>>(part, G, C, M, w, mean, rstd, dw, db, coef, acc);
   EDL_LAUNCH_CHECK();
   const int GA = blocks_for(M, C, 4, 2048);
-#define EDL_BN_DX(L, D)                                                                                        \
-  bn_bwd_dx_kernel<L, D><<<GA, kThreads, 0, s>>>((const bf16_t*)dz, (const bf16_t*)z, (const bf16_t*)x, coef, M, \
-                                                 C, (bf16_t*)dx, (bf16_t*)dres)
+#define EDL_BN_DX(L, D, X)                                                                                    \
+  bn_bwd_dx_kernel<L, D, X><<<GA, kThreads, 0, s>>>((const bf16_t*)dz, (const bf16_t*)z, (const bf16_t*)x, coef, \
+                                                    fcoef, M, C, (bf16_t*)dx, (bf16_t*)dres)
   if (dres) {
-    if (relu) EDL_BN_DX(true, true); else EDL_BN_DX(false, true);
+    if (mx) EDL_BN_DX(true, true, true); else if (relu) EDL_BN_DX(true, true, false);
+    else EDL_BN_DX(false, true, false);
   } else {
-    if (relu) EDL_BN_DX(true, false); else EDL_BN_DX(false, false);
+    if (mx) EDL_BN_DX(true, false, true); else if (relu) EDL_BN_DX(true, false, false);
+    else EDL_BN_DX(false, false, false);
   }
 #undef EDL_BN_DX
   EDL_LAUNCH_CHECK();

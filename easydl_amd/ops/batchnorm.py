@@ -65,7 +65,11 @@ class _BNActFn(torch.autograd.Function):
         k.check("edl_bn_fwd_train", x.data_ptr(), _native.ptr(r2), z.data_ptr(), w.data_ptr(), b.data_ptr(),
                 run_mean.data_ptr(), run_var.data_ptr(), mean.data_ptr(), rstd.data_ptr(), coef.data_ptr(),
                 part.data_ptr(), M, C, momentum, eps, int(relu), _native.stream_of(x))
-        ctx.save_for_backward(x, z if relu else None, w, mean, rstd)
+        # ReLU without a residual: the backward recomputes the mask from x and these
+        # coefficients (2C floats) instead of keeping and re-reading z
+        mx = relu and res is None
+        ctx.save_for_backward(x, z if relu and not mx else None, w, mean, rstd,
+                              coef if mx else None)
         ctx.relu, ctx.has_res = relu, res is not None
         ctx.bn_b = b
         return z
@@ -73,7 +77,7 @@ class _BNActFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dz):
         k = _native.kernels()
-        x, z, w, mean, rstd = ctx.saved_tensors
+        x, z, w, mean, rstd, fcoef = ctx.saved_tensors
         dz, dz2 = _nhwc(dz)
         x2 = _nhwc(x)[1]
         M, C = x2.shape
@@ -96,7 +100,7 @@ class _BNActFn(torch.autograd.Function):
         coef = torch.empty(3 * C, dtype=torch.float32, device=dev)
         part = torch.empty(2 * C * G, dtype=torch.float32, device=dev)
         k.check("edl_bn_bwd", dz2.data_ptr(), _native.ptr(z), x.data_ptr(), w.data_ptr(), mean.data_ptr(),
-                rstd.data_ptr(), dx.data_ptr(), _native.ptr(dres), dw.data_ptr(), db.data_ptr(), coef.data_ptr(),
+                rstd.data_ptr(), _native.ptr(fcoef), dx.data_ptr(), _native.ptr(dres), dw.data_ptr(), db.data_ptr(), coef.data_ptr(),
                 part.data_ptr(), M, C, int(ctx.relu), acc, _native.stream_of(x))
         if direct:
             gradsink.commit(w)
