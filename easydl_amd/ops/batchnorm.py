@@ -100,8 +100,8 @@ class _BNActFn(torch.autograd.Function):
         coef = torch.empty(3 * C, dtype=torch.float32, device=dev)
         part = torch.empty(2 * C * G, dtype=torch.float32, device=dev)
         k.check("edl_bn_bwd", dz2.data_ptr(), _native.ptr(z), x.data_ptr(), w.data_ptr(), mean.data_ptr(),
-                rstd.data_ptr(), _native.ptr(fcoef), dx.data_ptr(), _native.ptr(dres), dw.data_ptr(), db.data_ptr(), coef.data_ptr(),
-                part.data_ptr(), M, C, int(ctx.relu), acc, _native.stream_of(x))
+                rstd.data_ptr(), _native.ptr(fcoef), dx.data_ptr(), _native.ptr(dres), dw.data_ptr(), db.data_ptr(),
+                coef.data_ptr(), part.data_ptr(), M, C, int(ctx.relu), acc, _native.stream_of(x))
         if direct:
             gradsink.commit(w)
             gradsink.commit(b)
