@@ -166,10 +166,12 @@ __global__ __launch_bounds__(kThreads) void bn_stats_kernel(const bf16_t* __rest
 __global__ __launch_bounds__(kFinThreads) void bn_stats_finalize_kernel(
     const float* __restrict__ part, int G, int C, int64_t M, const float* __restrict__ w,
     const float* __restrict__ b, float* __restrict__ run_mean, float* __restrict__ run_var, float momentum,
-    float eps, float* __restrict__ mean_out, float* __restrict__ rstd_out, float* __restrict__ coef) {
+    float eps, float* __restrict__ mean_out, float* __restrict__ rstd_out, float* __restrict__ coef,
+    int64_t* __restrict__ nbt) {
   double s, q;
   sum_partials(part, G, C, s, q);
   const int c = blockIdx.x * 64 + threadIdx.x;
+  if (nbt != nullptr && c == 0) nbt[0] += 1;   // the module's num_batches_tracked (no separate launch)
   if (threadIdx.x >= 64 || c >= C) return;
   const double k = (double)run_mean[c];
   const double dm = s / (double)M;
@@ -357,13 +359,13 @@ int edl_bn_groups(int64_t M, int C) { return shape_ok(M, C) ? row_blocks(M, C) :
 // coef: fp32 [2C] scratch; part: fp32 [2C * edl_bn_groups].  running_mean is also the shift.
 int edl_bn_fwd_train(const void* x, const void* res, void* z, const float* w, const float* b, float* run_mean,
                      float* run_var, float* mean, float* rstd, float* coef, float* part, int64_t M, int C,
-                     float momentum, float eps, int relu, hipStream_t s) {
+                     float momentum, float eps, int relu, int64_t* nbt, hipStream_t s) {
   if (!shape_ok(M, C)) return (int)hipErrorInvalidValue;
   const int G = row_blocks(M, C), Cb = chunk_of(C);
   bn_stats_kernel<<<dim3(G, C / Cb), kThreads, 0, s>>>((const bf16_t*)x, run_mean, M, C, Cb, part);
   EDL_LAUNCH_CHECK();
   bn_stats_finalize_kernel<<<(C + 63) / 64, kFinThreads, 0, s>>>(part, G, C, M, w, b, run_mean, run_var,
-                                                                  momentum, eps, mean, rstd, coef);
+                                                                  momentum, eps, mean, rstd, coef, nbt);
   EDL_LAUNCH_CHECK();
   const int GA = blocks_for(M, C, 4, 2048);
 #define EDL_BN_APPLY(R, L)                                                                               \

@@ -44,7 +44,7 @@ def _nhwc(t):
 
 class _BNActFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, res, w, b, run_mean, run_var, momentum, eps, relu):
+    def forward(ctx, x, res, w, b, run_mean, run_var, momentum, eps, relu, nbt=None):
         k = _native.kernels()
         x, x2 = _nhwc(x)
         M, C = x2.shape
@@ -64,7 +64,7 @@ class _BNActFn(torch.autograd.Function):
         part = torch.empty(2 * C * G, dtype=torch.float32, device=dev)
         k.check("edl_bn_fwd_train", x.data_ptr(), _native.ptr(r2), z.data_ptr(), w.data_ptr(), b.data_ptr(),
                 run_mean.data_ptr(), run_var.data_ptr(), mean.data_ptr(), rstd.data_ptr(), coef.data_ptr(),
-                part.data_ptr(), M, C, momentum, eps, int(relu), _native.stream_of(x))
+                part.data_ptr(), M, C, momentum, eps, int(relu), _native.ptr(nbt), _native.stream_of(x))
         # ReLU without a residual: the backward recomputes the mask from x and these
         # coefficients (2C floats) instead of keeping and re-reading z
         mx = relu and res is None
@@ -105,9 +105,9 @@ class _BNActFn(torch.autograd.Function):
         if direct:
             gradsink.commit(w)
             gradsink.commit(b)
-            return dx, dres, None, None, None, None, None, None, None
+            return dx, dres, None, None, None, None, None, None, None, None
         return (dx, dres, dw if ctx.needs_input_grad[2] else None, db if ctx.needs_input_grad[3] else None,
-                None, None, None, None, None)
+                None, None, None, None, None, None)
 
 
 def _eval_coef(bn):
@@ -122,9 +122,12 @@ def bn_act(x, bn: torch.nn.BatchNorm2d, residual=None, relu: bool = True):
     if bn.training:
         if bn.momentum is None:
             raise ValueError("bn_act: cumulative moving average (momentum=None) is not supported")
-        bn.num_batches_tracked.add_(1)
+        nbt = bn.num_batches_tracked
+        if nbt.device != x.device or nbt.dtype != torch.int64:
+            nbt.add_(1)
+            nbt = None   # else the statistics kernel counts the batch (no separate launch)
         return _BNActFn.apply(x, residual, bn.weight, bn.bias, bn.running_mean, bn.running_var,
-                              float(bn.momentum), float(bn.eps), relu)
+                              float(bn.momentum), float(bn.eps), relu, nbt)
     if torch.is_grad_enabled() and (x.requires_grad or (residual is not None and residual.requires_grad)
                                     or bn.weight.requires_grad):
         # frozen statistics but gradients wanted: differentiable torch ops
