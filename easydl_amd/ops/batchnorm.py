@@ -11,6 +11,8 @@ reference :func:`bn_act_ref` (the CPU test tier and the numerics oracle).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn.functional as F
 
@@ -42,6 +44,13 @@ def _nhwc(t):
     return t, t2
 
 
+# A/B switches for the backward's two launch / traffic savings (both on by default):
+# EDL_BN_DIRECT_GRADS=0 returns dgamma / dbeta to autograd instead of writing the flat
+# buffer; EDL_BN_MASK_FROM_X=0 keeps z and reads it back for the ReLU mask.
+_DIRECT_GRADS = os.environ.get("EDL_BN_DIRECT_GRADS", "1") != "0"
+_MASK_FROM_X = os.environ.get("EDL_BN_MASK_FROM_X", "1") != "0"
+
+
 class _BNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, res, w, b, run_mean, run_var, momentum, eps, relu, nbt=None):
@@ -67,7 +76,7 @@ class _BNActFn(torch.autograd.Function):
                 part.data_ptr(), M, C, momentum, eps, int(relu), _native.ptr(nbt), _native.stream_of(x))
         # ReLU without a residual: the backward recomputes the mask from x and these
         # coefficients (2C floats) instead of keeping and re-reading z
-        mx = relu and res is None
+        mx = relu and res is None and _MASK_FROM_X
         ctx.save_for_backward(x, z if relu and not mx else None, w, mean, rstd,
                               coef if mx else None)
         ctx.relu, ctx.has_res = relu, res is not None
@@ -89,7 +98,7 @@ class _BNActFn(torch.autograd.Function):
         # flat-managed (written on the first micro-batch, accumulated after): no per-parameter
         # autograd accumulate launch.  Otherwise they are returned to autograd.
         b = ctx.bn_b
-        direct = (gradsink.is_flat(w) and gradsink.is_flat(b) and w.grad.dtype == torch.float32
+        direct = (_DIRECT_GRADS and gradsink.is_flat(w) and gradsink.is_flat(b) and w.grad.dtype == torch.float32
                   and b.grad.dtype == torch.float32 and gradsink.is_fresh(w) == gradsink.is_fresh(b))
         if direct:
             dw, db, acc = w.grad, b.grad, 0 if gradsink.is_fresh(w) else 1

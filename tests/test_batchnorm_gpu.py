@@ -92,7 +92,10 @@ def test_bn_param_grads_go_straight_into_flat_buffer(cuda):
     """With FlatParams managing the BatchNorm weight / bias, the backward kernel writes their
     gradients into the flat fp32 buffer (first micro-batch) and accumulates (second one);
     the result matches the autograd-returned gradients, and the ready callback fires."""
+    from easydl_amd.ops import batchnorm
     from easydl_amd.parallel.flat import FlatParams
+    if not batchnorm._DIRECT_GRADS:
+        pytest.skip("EDL_BN_DIRECT_GRADS=0")
     C = 64
     bn_a, bn_b = _bn(C, 7), _bn(C, 7)
     FlatParams(bn_b)
