@@ -106,7 +106,7 @@ def packed_qkv_attention(qkv: torch.Tensor, B: int, S: int, H: int, causal: bool
     D = qkv.shape[-1] // (3 * H)
     scale = 1.0 / math.sqrt(D) if scale is None else scale
     if (qkv.is_cuda and D in (64, 128) and qkv.dtype == torch.bfloat16 and qkv.is_contiguous()
-            and os.environ.get("EDL_ATTN", "hip") != "sdpa"):
+            and os.environ.get("EDL_ATTN", "hip") != "sdpa" and os.environ.get("EDL_ATTN_PACKED", "1") != "0"):
         return _PackedQKVAttnFn.apply(qkv, B, S, H, causal, scale)
     q, k, v = (t.transpose(1, 2) for t in qkv.view(B, S, 3, H, D).unbind(2))
     return flash_attention(q, k, v, causal, scale).transpose(1, 2).reshape(B * S, H * D)
