@@ -15,6 +15,7 @@
 
 using edl_xgmi::kFlagBytes;
 using edl_xgmi::kMaxRanks;
+using edl_xgmi::kStatusWords;
 
 namespace {
 
@@ -25,7 +26,7 @@ struct Workspace {
   void* flags = nullptr;
   int* abort_host = nullptr;
   int* abort_dev = nullptr;
-  int* status = nullptr;       // device view of status_host
+  int* status = nullptr;       // device view of status_host (kStatusWords ints)
   int* status_host = nullptr;
   int nranks = 1, rank = 0;
   std::vector<char*> peer_data;    // nranks (own included)
@@ -52,9 +53,9 @@ int edl_xgmi_ws_create(int device, uint64_t data_bytes, void** out) {
   // status word in mapped pinned host memory: readable without a hipMemcpy, which
   // would go through the legacy NULL stream and wait for every blocking stream
   // (e.g. a CU-masked snapshot copy in flight)
-  if (e == hipSuccess) e = hipHostMalloc((void**)&w->status_host, sizeof(int), hipHostMallocMapped);
+  if (e == hipSuccess) e = hipHostMalloc((void**)&w->status_host, kStatusWords * sizeof(int), hipHostMallocMapped);
   if (e == hipSuccess) {
-    *w->status_host = 0;
+    memset(w->status_host, 0, kStatusWords * sizeof(int));
     e = hipHostGetDevicePointer((void**)&w->status, w->status_host, 0);
   }
   if (e == hipSuccess) e = hipDeviceSynchronize();
@@ -134,6 +135,17 @@ int edl_xgmi_ws_status(void* ws) {
   return __atomic_load_n(w->status_host, __ATOMIC_ACQUIRE);
 }
 
+// the whole status record (kStatusWords ints, layout in xgmi_layout.h)
+int edl_xgmi_ws_status_detail(void* ws, int* out) {
+  auto* w = (Workspace*)ws;
+  if (__atomic_load_n(w->status_host, __ATOMIC_ACQUIRE) == 0) {
+    memset(out, 0, kStatusWords * sizeof(int));
+    return 0;
+  }
+  for (int i = 0; i < kStatusWords; ++i) out[i] = __atomic_load_n(w->status_host + i, __ATOMIC_RELAXED);
+  return out[0];
+}
+
 int edl_xgmi_ws_destroy(void* ws) {
   auto* w = (Workspace*)ws;
   if (!w) return 0;
@@ -149,6 +161,34 @@ int edl_xgmi_ws_destroy(void* ws) {
   if (w->abort_host) hipHostFree(w->abort_host);
   delete w;
   return 0;
+}
+
+// ---- registered buffers (e.g. the flat gradient buffer, mapped by every peer) ----
+// IPC handles name whole allocations, so a tensor inside a caching-allocator
+// segment is exported as (handle of its segment, byte offset).
+int edl_xgmi_buf_handle(void* ptr, char* out_handle, uint64_t* out_offset) {
+  hipDeviceptr_t base = nullptr;
+  size_t size = 0;
+  hipError_t e = hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)ptr);
+  if (e != hipSuccess) return (int)e;
+  hipIpcMemHandle_t h;
+  e = hipIpcGetMemHandle(&h, (void*)base);
+  if (e != hipSuccess) return (int)e;
+  memcpy(out_handle, &h, sizeof(h));
+  *out_offset = (uint64_t)((char*)ptr - (char*)base);
+  return 0;
+}
+
+int edl_xgmi_buf_open(int device, const char* handle, void** out) {
+  hipSetDevice(device);
+  hipIpcMemHandle_t h;
+  memcpy(&h, handle, sizeof(h));
+  return (int)hipIpcOpenMemHandle(out, h, hipIpcMemLazyEnablePeerAccess);
+}
+
+int edl_xgmi_buf_close(int device, void* p) {
+  hipSetDevice(device);
+  return (int)hipIpcCloseMemHandle(p);
 }
 
 }  // extern "C"

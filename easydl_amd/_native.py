@@ -79,6 +79,13 @@ _KERNEL_SIGS = {
                            c_i64, c_int, c_int, ctypes.c_uint32, c_int, c_void_p, ctypes.c_double, c_void_p,
                            c_void_p],
     "edl_xgmi_max_ranks": [],
+    "edl_xgmi_allreduce_inplace": [ctypes.POINTER(c_void_p), ctypes.POINTER(c_void_p), c_int, c_int, c_i64, c_int,
+                                   ctypes.c_uint32, c_int, c_void_p, ctypes.c_double, c_void_p, c_void_p],
+    "edl_xgmi_barrier": [ctypes.POINTER(c_void_p), c_int, c_int, ctypes.c_uint32, c_void_p, ctypes.c_double, c_void_p,
+                         c_void_p],
+    "edl_xgmi_wallclock_hz": (c_i64, []),
+    "edl_xgmi_pull": [ctypes.POINTER(c_void_p), ctypes.POINTER(c_void_p), c_int, c_int, c_i64, ctypes.c_uint32,
+                      ctypes.c_uint32, c_int, c_void_p, ctypes.c_double, c_void_p, c_void_p],
     "edl_xgmi_collective": [ctypes.POINTER(c_void_p), ctypes.POINTER(c_void_p), c_int, c_int, c_void_p, c_void_p,
                             c_i64, c_i64, c_int, c_int, ctypes.c_uint32, c_int, c_void_p, ctypes.c_double, c_void_p,
                             c_void_p],

@@ -302,7 +302,7 @@ class CheckpointManager:
             self.stats["skipped"] = self.stats.get("skipped", 0) + 1
             return
         meta = {"format": FORMAT, "step": trainer.step, "opt_step": trainer.opt.step_count, "world": world,
-                "shard": shard, "epoch": comm.epoch, "tag": tag,
+                "shard": shard, "epoch": comm.epoch, "tag": tag, "host": _host_state(trainer),
                 "t": [[d["name"], d["dtype"], d["numel"], d["lo"], d["hi"], d["offset"]] for d in layout]}
         dev = state[0][1].device
         if dev.type == "cuda":
@@ -456,6 +456,7 @@ class CheckpointManager:
         meta = infos[0]["meta"]
         trainer.step = int(meta["step"])
         trainer.opt.step_count = int(meta["opt_step"])
+        _load_host_state(trainer, meta.get("host"))
         return f"shm{tag}:w{world}:step{step}"
 
     # -- disk persistence (format v1) ----------------------------------------------
@@ -510,7 +511,7 @@ class CheckpointManager:
         if m["shard"] == 0:
             with open(os.path.join(d, f"manifest{tag}.json"), "w") as f:
                 json.dump({"format": FORMAT, "step": step, "opt_step": m["opt_step"], "world": m["world"],
-                           "epoch": m["epoch"], "time": time.time()}, f)
+                           "epoch": m["epoch"], "host": m.get("host"), "time": time.time()}, f)
 
     def load_dir_latest(self, trainer) -> str | None:
         dirs = sorted(glob.glob(os.path.join(self.persist_dir or "", "step-*")),
@@ -558,6 +559,18 @@ def load_dir(d: str, trainer, tag: str = "") -> None:
     CheckpointManager.finish_restore(trainer)
     trainer.step = int(m["step"])
     trainer.opt.step_count = int(m["opt_step"])
+    _load_host_state(trainer, m.get("host"))
+
+
+def _host_state(trainer) -> dict | None:
+    fn = getattr(trainer, "host_state", None)
+    return fn() if fn is not None else None
+
+
+def _load_host_state(trainer, h) -> None:
+    fn = getattr(trainer, "load_host_state", None)
+    if fn is not None:
+        fn(h)
 
 
 def _load_shard(read, table, state, dev, expect: int, what: str, seg=None, slot=None) -> None:

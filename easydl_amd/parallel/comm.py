@@ -49,7 +49,8 @@ def _td(s: float) -> datetime.timedelta:
 class Communicator:
     def __init__(self, store: dist.Store, rank: int, world_size: int, epoch: int, *, device: torch.device,
                  job: str = "job", timeout_s: float = 120.0, control_timeout_s: float = 30.0,
-                 high_priority: bool = True, tag: str = "", data: bool = True, data_backend: str | None = None):
+                 high_priority: bool = True, tag: str = "", data: bool = True, data_backend: str | None = None,
+                 xgmi_factory=None):
         self.rank = rank
         self.world_size = world_size
         self.epoch = epoch
@@ -68,7 +69,10 @@ class Communicator:
         t0 = time.perf_counter()
         base = dist.PrefixStore(f"edl/{job}/e{epoch}" + (f"/{tag}" if tag else ""), store)
         self.ctrl = dist.ProcessGroupGloo(dist.PrefixStore("ctrl", base), rank, world_size, _td(control_timeout_s))
-        data_backend = data_backend or os.environ.get("EDL_COMM", "pg")
+        # default "auto": at world > 1 the hand-written xGMI engine is measured against
+        # RCCL at the start of every epoch and kept for the message sizes where it wins
+        data_backend = data_backend or os.environ.get("EDL_COMM", "auto")
+        self.xgmi_min_bytes = 0      # all-reduces at least this large go to the engine
         if not data:
             self.data = None
             self.backend = "none"
@@ -91,13 +95,22 @@ class Communicator:
             self.backend = "xgmi"
         elif self.device.type == "cuda":
             if data_backend in ("xgmi", "auto") and world_size > 1:
-                # csrc/kernels/xgmi.hip: abortable one-/two-shot all-reduce over IPC-mapped
-                # peer buffers; RCCL keeps the other collectives (and all-reduce in "auto"
-                # until warmup() has measured both on this node)
-                from easydl_amd.parallel.xgmi import XgmiComm
-                self.xgmi = XgmiComm(dist.PrefixStore("xgmi", base), "ws", rank, world_size, self.device,
-                                     timeout_s=timeout_s)
-                self.xgmi_mode = data_backend
+                # csrc/kernels/xgmi.hip: abortable direct all-reduce over IPC-mapped peer
+                # memory; RCCL keeps the other collectives (and all-reduce in "auto" until
+                # warmup() has measured both on this node and per message size)
+                if xgmi_factory is None:
+                    from easydl_amd.parallel.xgmi import XgmiComm as xgmi_factory
+                try:
+                    self.xgmi = xgmi_factory(dist.PrefixStore("xgmi", base), "ws", rank, world_size, self.device,
+                                             timeout_s=timeout_s)
+                    self.xgmi_mode = data_backend
+                except Exception as e:  # noqa: BLE001
+                    if data_backend == "xgmi":
+                        raise
+                    # auto: the engine is an optimisation; RCCL alone is always correct
+                    log.warning("xGMI engine unavailable (%s); RCCL only", e)
+                    self.xgmi_probe = {"selected": "rccl", "error": str(e)[:200]}
+                    self.xgmi = None
             opts = dist.ProcessGroupNCCL.Options()
             opts.is_high_priority_stream = high_priority
             opts._timeout = _td(timeout_s)
@@ -113,7 +126,8 @@ class Communicator:
         """Host-wait for this rank's compute stream, which every collective is ordered
         into.  Never torch.cuda.synchronize(): that also waits for an in-flight snapshot
         copy on the checkpoint engine's stream, on the recovery path."""
-        torch.cuda.current_stream(self.device).synchronize()
+        if self.device.type == "cuda":
+            torch.cuda.current_stream(self.device).synchronize()
 
     def warmup(self) -> float:
         """Force lazy communicator creation now (so it is not hidden in step 1)."""
@@ -134,45 +148,178 @@ class Communicator:
             self._probe_xgmi()
         return time.perf_counter() - t0
 
-    def _probe_xgmi(self, mb: int = 64, iters: int = 5) -> None:
-        """Measure the xGMI engine against RCCL on a gradient-bucket-sized message on
-        THIS node and keep it only if every rank saw an exact result and it was
-        faster everywhere (integer-valued data: both sums are exact)."""
-        n = (mb << 20) // 2
+    PROBE_MB = (4, 32, 128)
+
+    def _probe_xgmi(self, sizes_mb=None, iters: int = 3) -> None:
+        """Measure the xGMI engine against RCCL on THIS node at gradient-bucket sizes
+        (in place on a registered buffer, as ElasticDDP uses it) and keep it for the
+        sizes where every rank saw an exact result and it was faster everywhere
+        (integer-valued data: both sums are exact).  The per-size table is the
+        communication policy: all-reduces >= ``xgmi_min_bytes`` use the engine."""
+        sizes_mb = tuple(sizes_mb or self.PROBE_MB)
+        n = (max(sizes_mb) << 20) // 2
         g = torch.Generator(device="cpu").manual_seed(7 + self.rank)
         src = torch.randint(-4, 5, (n,), generator=g, dtype=torch.int8).to(self.device, torch.bfloat16)
         a, b = src.clone(), src.clone()
-        self.data.allreduce([a]).wait()
+        reg = None
         keep_timeout, self.xgmi.timeout_s = self.xgmi.timeout_s, 5.0  # a broken path gives up fast
-        self.xgmi.all_reduce(b)
-        self._sync_stream()
-        self.xgmi.timeout_s = keep_timeout
-        bad = 0.0 if (torch.equal(a, b) and self.xgmi.status() == 0) else 1.0
-
-        def timed(fn):
-            t = src.clone()
-            fn(t)
-            self._sync_stream()
-            t0 = time.perf_counter()
-            for _ in range(iters):
+        # every decision point is agreed over the control plane, so a rank whose engine
+        # fails locally never leaves its peers waiting inside a data-plane collective
+        try:
+            reg = self.xgmi.register(b)
+            bad = 0.0
+        except Exception as e:  # noqa: BLE001
+            log.warning("xGMI probe: registration failed: %s", e)
+            bad = 1.0
+        bad = float(self.ctrl_all_reduce([bad], dist.ReduceOp.MAX)[0])
+        if not bad:
+            try:
+                self.data.allreduce([a]).wait()
+                self.xgmi.all_reduce(b)
+                self._sync_stream()
+                bad = 0.0 if (torch.equal(a, b) and self.xgmi.status() == 0) else 1.0
+            except Exception as e:  # noqa: BLE001
+                log.warning("xGMI probe: exactness check failed: %s", e)
+                bad = 1.0
+            bad = float(self.ctrl_all_reduce([bad], dist.ReduceOp.MAX)[0])
+        table = []
+        if not bad:
+            def timed(fn, t):
                 fn(t)
-            self._sync_stream()
-            return (time.perf_counter() - t0) / iters
+                self._sync_stream()
+                t0 = time.perf_counter()
+                for _ in range(iters):
+                    fn(t)
+                self._sync_stream()
+                return (time.perf_counter() - t0) / iters
 
-        t_rccl = timed(lambda t: self.data.allreduce([t]).wait())
-        t_xgmi = timed(self.xgmi.all_reduce) if not bad else float("inf")
-        worst = self.ctrl_all_reduce([bad, min(t_xgmi - t_rccl, 1e9)], dist.ReduceOp.MAX)
-        keep = worst[0] == 0 and worst[1] < 0
-        self.xgmi_probe = {"mb": mb, "rccl_ms": round(t_rccl * 1e3, 3), "xgmi_ms": round(t_xgmi * 1e3, 3),
-                           "exact_everywhere": bool(worst[0] == 0), "selected": "xgmi" if keep else "rccl"}
+            for mb in sizes_mb:
+                view = b[:(mb << 20) // 2]
+                try:
+                    t_r = timed(lambda t: self.data.allreduce([t]).wait(), view)
+                    t_x = timed(self.xgmi.all_reduce, view)
+                except Exception as e:  # noqa: BLE001
+                    log.warning("xGMI probe: timing at %d MB failed: %s", mb, e)
+                    t_r, t_x = 1.0, float("inf")
+                table.append((mb, t_r, t_x))
+            try:
+                bad = 0.0 if self.xgmi.status() == 0 else 1.0
+            except Exception:  # noqa: BLE001
+                bad = 1.0
+        self.xgmi.timeout_s = keep_timeout
+        diffs = [min(tx - tr, 1e9) for _, tr, tx in table] or [0.0] * len(sizes_mb)
+        worst = self.ctrl_all_reduce([bad] + diffs, dist.ReduceOp.MAX)
+        exact = worst[0] == 0
+        # smallest probed size from which the engine wins at every larger probed size
+        min_mb = None
+        if exact:
+            for i in range(len(table) - 1, -1, -1):
+                if worst[1 + i] < 0:
+                    min_mb = table[i][0]
+                else:
+                    break
+        keep = min_mb is not None
+        self.xgmi_probe = {
+            "sizes_mb": [m for m, _, _ in table],
+            "rccl_ms": [round(tr * 1e3, 3) for _, tr, _ in table],
+            "xgmi_ms": [round(tx * 1e3, 3) for _, _, tx in table],
+            "rccl_busbw_gbs": [round(2 * (self.world_size - 1) / self.world_size * (m << 20) / tr / 1e9, 1)
+                               for m, tr, _ in table],
+            "xgmi_busbw_gbs": [round(2 * (self.world_size - 1) / self.world_size * (m << 20) / tx / 1e9, 1)
+                               for m, _, tx in table],   # inf time -> 0.0
+            "exact_everywhere": bool(exact), "xgmi_min_mb": min_mb,
+            "selected": "xgmi" if keep else "rccl"}
         log.info("all-reduce probe (epoch %d, world %d): %s", self.epoch, self.world_size, self.xgmi_probe)
+        if reg is not None:
+            self._sync_stream()
+            self.xgmi.unregister(reg)
         if keep:
             self.xgmi_mode = "xgmi"
             self.backend = "rccl+xgmi"
+            # winning from the smallest probed size on: every size goes to the engine;
+            # otherwise only messages at least as large as the first winning size
+            self.xgmi_min_bytes = (min_mb << 20) if min_mb != sizes_mb[0] else 0
         else:
             self._sync_stream()
             self.xgmi.close()
             self.xgmi = None
+            self.xgmi_mode = None
+
+    def register_buffers(self, tensors) -> None:
+        """Long-lived buffers every rank registers in the same order (ElasticDDP's flat
+        gradient groups): the engine then all-reduces their slices in place."""
+        if self.xgmi is None or self.xgmi_mode != "xgmi":
+            return
+        for t in tensors:
+            if self.xgmi.supports(t):
+                self.xgmi.register(t)
+
+    def transfer_state(self, tensors, holders) -> None:
+        """State transfer to joiners / replacements: every rank not in ``holders``
+        receives each tensor, slice k from holder k, all holders sending at once over
+        distinct links (SURVEY.md §2.8 "multi-source scatter").  Holders are identical
+        by construction (same committed step).  Collective."""
+        holders = sorted(set(int(h) for h in holders))
+        if self._aborted:
+            raise CommAborted("communicator aborted")
+        if not holders:
+            raise ValueError("transfer_state: no holder")
+        if len(holders) == self.world_size:
+            return
+        if len(holders) == 1:   # one source: the collective broadcast is already link-optimal
+            for t in tensors:
+                self.broadcast(t, holders[0])
+            return
+        if self.xgmi is not None and self.device.type == "cuda":
+            big = [t for t in tensors if self.xgmi.pullable(t)]
+            rest = [t for t in tensors if not self.xgmi.pullable(t)]
+            if big:
+                self._native(self.xgmi.pull, big, holders)
+                if self.xgmi.status() != 0:
+                    raise CommAborted(f"xGMI state transfer gave up in epoch {self.epoch}: "
+                                      f"{self.xgmi.status_detail()}")
+            for t in rest:
+                self.broadcast(t, holders[0])
+            return
+        receivers = [r for r in range(self.world_size) if r not in holders]
+        me_holds = self.rank in holders
+        ops = []   # (kind, tensor slice, peer, tag)
+        for ti, t in enumerate(tensors):
+            flat = t.reshape(-1)
+            n = flat.numel()
+            nh = len(holders)
+            per = -(-n // nh)
+            for k, h in enumerate(holders):
+                sl = flat[k * per:min(n, (k + 1) * per)]
+                if sl.numel() == 0:
+                    continue
+                if me_holds and self.rank == h:
+                    ops += [("send", sl, r, ti) for r in receivers]
+                elif not me_holds:
+                    ops.append(("recv", sl, h, ti))
+        if not ops:
+            self._p2p_batch([])   # still take part in the group call on RCCL
+            return
+        self._p2p_batch(ops)
+
+    def _p2p_batch(self, ops) -> None:
+        """Concurrent point-to-point transfers (one grouped launch on RCCL)."""
+        if self.rccl is not None:
+            if ops:
+                self._wait(self._native(self.rccl.sendrecv_async, [o[:3] for o in ops]))
+            return
+        if not ops:
+            return
+        if self.backend.startswith("rccl") and hasattr(self.data, "_start_coalescing"):
+            self.data._start_coalescing(self.device)
+            for kind, t, peer, tag in ops:
+                (self.data.send if kind == "send" else self.data.recv)([t], peer, tag)
+            self._wait(self.data._end_coalescing(self.device))
+            return
+        # gloo: every transfer in flight at once; (peer, tag) pairs match sends to receives
+        works = [(self.data.send if kind == "send" else self.data.recv)([t], peer, tag) for kind, t, peer, tag in ops]
+        for w in works:
+            self._wait(w)
 
     def healthy(self) -> bool:
         """False if a hand-written collective gave up (abort word / deadline) since the
@@ -239,7 +386,7 @@ class Communicator:
         self._verify("all_reduce", t, int(op))
         if self.rccl is not None:
             return self._native(self.rccl.all_reduce_async, t, op)
-        if self._use_xgmi(t):
+        if self._use_xgmi_allreduce(t):
             if op == dist.ReduceOp.SUM:
                 return self._native(self.xgmi.all_reduce_async, t)
             if op == dist.ReduceOp.MAX:
@@ -301,6 +448,9 @@ class Communicator:
 
     def _use_xgmi(self, *ts) -> bool:
         return self.xgmi is not None and self.xgmi_mode == "xgmi" and all(self.xgmi.supports(t) for t in ts)
+
+    def _use_xgmi_allreduce(self, t) -> bool:
+        return self._use_xgmi(t) and (self.backend == "xgmi" or t.numel() * t.element_size() >= self.xgmi_min_bytes)
 
     def _xgmi_sync(self, fn, *args):
         """Run an xGMI collective on the caller's stream (TP/SP: the consumer is next)."""

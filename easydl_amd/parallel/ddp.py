@@ -89,6 +89,11 @@ class ElasticDDP:
         """Swap in the communicator of a new rendezvous epoch."""
         self._works = []
         self.comm = comm
+        reg = getattr(comm, "register_buffers", None)
+        if reg is not None and comm.world_size > 1:
+            # the xGMI engine maps every rank's flat gradient buffers once per epoch and
+            # then all-reduces each bucket in place (no staging copy)
+            reg([g.grad for g in self.flat.groups])
         self.prepare()
 
     @property

@@ -1,19 +1,30 @@
-"""Custom xGMI all-reduce (csrc/kernels/xgmi.hip + csrc/runtime/xgmi.cpp;
-SURVEY.md N3): IPC-mapped peer buffers on one node, one-shot for small
-messages, two-shot (direct reduce-scatter + all-gather over all 7 links) for
-large ones, every wait bounded by an abort word and a deadline.
+"""Custom xGMI collective engine (csrc/kernels/xgmi.hip + csrc/runtime/xgmi.cpp;
+SURVEY.md N3): IPC-mapped peer memory on one node, every wait bounded by an
+abort word and a deadline.
+
+* **staged** collectives (any tensor): one-shot all-reduce for small messages,
+  two-shot (direct reduce-scatter + all-gather over all 7 links) for large
+  ones, MAX all-reduce, all-gather, reduce-scatter — through a per-rank
+  workspace with two buffers by round parity;
+* **in-place** all-reduce on *registered* buffers: ElasticDDP registers the
+  flat gradient buffers once per epoch (:meth:`register`), after which every
+  bucket all-reduce is ONE launch that reads the peers' gradient slices where
+  they are (no staging copy, no workspace-size split).
 
 Usage (one object per rank and epoch; every rank issues the same calls)::
 
     x = XgmiComm(store, "edl/job/e3/xgmi", rank, world, device)
+    x.register(flat_grad)     # optional, collective
     x.all_reduce(t)           # in place, on the current stream
     x.abort()                 # watchdog thread: spinning kernels give up
+    x.status_detail()         # which round / phase / workgroup / peer gave up
 
-Also ``all_reduce_max``, ``all_gather`` and ``reduce_scatter`` (the TP / SP
-collectives; ``Communicator(data_backend="xgmi")`` routes them here).
+Ranks that share one GPU (single-GPU drills) are detected through the store
+(device UUIDs) and the grid is capped so every rank's workgroups can be
+resident together — the per-workgroup barrier needs workgroup b of every rank
+running at once.
 
-Limits: <= 8 ranks (one node), fp32 / bf16, sizes a multiple of 16 bytes
-(tensors are processed in workspace-sized pieces).
+Limits: <= 8 ranks (one node), fp32 / bf16, sizes a multiple of 16 bytes.
 """
 from __future__ import annotations
 
@@ -23,6 +34,9 @@ import os
 import torch
 
 from easydl_amd import _native
+
+STATUS_FIELDS = ("gave_up", "round", "phase", "block", "peer", "peer_flag", "waited_ms", "reason")
+REASONS = {0: "", 1: "abort", 2: "deadline"}
 
 
 class XgmiError(RuntimeError):
@@ -42,17 +56,31 @@ class _Work:
         return self._event.query()
 
 
+class _Registered:
+    """One registered tensor: its base pointer as mapped on every rank."""
+
+    def __init__(self, tensor: torch.Tensor, peers: list[int], opened: list[int]):
+        self.tensor = tensor
+        self.lo = tensor.data_ptr()
+        self.hi = self.lo + tensor.numel() * tensor.element_size()
+        self.peers = peers          # rank q's copy of tensor[0], valid in this process
+        self.opened = opened        # (peer, handle) keys of the IPC mappings it holds a reference on
+
+
 class XgmiComm:
     ONESHOT_MAX = 512 << 10      # bytes: below this latency dominates -> one-shot
+    DEFAULT_WS = 128 << 20       # per parity: one 128 MiB bucket / TP message per launch
 
-    def __init__(self, store, prefix: str, rank: int, world: int, device, ws_bytes: int = 64 << 20,
+    def __init__(self, store, prefix: str, rank: int, world: int, device, ws_bytes: int | None = None,
                  timeout_s: float = 60.0):
         self.rank, self.world_size = rank, world
         self.device = torch.device(device)
         self.timeout_s = timeout_s
+        self._store, self._prefix = store, prefix
         self._rt, self._k = _native.runtime(), _native.kernels()
         if world > self._k("edl_xgmi_max_ranks"):
-            raise XgmiError(f"xGMI all-reduce supports at most {self._k('edl_xgmi_max_ranks')} ranks")
+            raise XgmiError(f"xGMI engine supports at most {self._k('edl_xgmi_max_ranks')} ranks")
+        ws_bytes = int(ws_bytes or int(os.environ.get("EDL_XGMI_WS_MB", 0)) << 20 or self.DEFAULT_WS)
         h = ctypes.c_void_p()
         rc = self._rt("edl_xgmi_ws_create", self.device.index or 0, ws_bytes, ctypes.byref(h))
         if rc != 0:
@@ -63,8 +91,12 @@ class XgmiComm:
         rc = self._rt("edl_xgmi_ws_handles", h, mine)
         if rc != 0:
             raise XgmiError(f"hipIpcGetMemHandle failed: hipError {rc}")
-        store.set(f"{prefix}/ipc/{rank}", mine.raw)
-        allh = b"".join(mine.raw if p == rank else store.get(f"{prefix}/ipc/{p}") for p in range(world))
+        # device identity travels with the handles: ranks on the SAME GPU are counted
+        uuid = str(torch.cuda.get_device_properties(self.device).uuid).encode()[:64].ljust(64, b" ")
+        store.set(f"{prefix}/ipc/{rank}", mine.raw + uuid)
+        entries = [mine.raw + uuid if p == rank else store.get(f"{prefix}/ipc/{p}") for p in range(world)]
+        allh = b"".join(e[:128] for e in entries)
+        self.ranks_per_device = sum(1 for e in entries if e[128:] == uuid)
         rc = self._rt("edl_xgmi_ws_open", h, world, rank, allh)
         if rc != 0:
             raise XgmiError(f"hipIpcOpenMemHandle failed: hipError {rc}")
@@ -74,16 +106,24 @@ class XgmiComm:
         self._abort_dev = self._rt("edl_xgmi_ws_abort_dev", h)
         self._status_dev = self._rt("edl_xgmi_ws_status_dev", h)
         self.round = 0
-        # Workgroup b of every rank meets workgroup b of every peer (per-block barrier), so
-        # all ranks' workgroups must be resident together.  One rank per GPU: always true.
-        # Ranks SHARING a GPU (EDL_XGMI_MAX_BLOCKS set by the shared-GPU drills): 4 ranks x
-        # 256 x 512 threads would fill every thread slot of the chip and a late rank's
-        # workgroups could never be dispatched, so the grid is capped.
-        cap = int(os.environ.get("EDL_XGMI_MAX_BLOCKS", 256))
-        self.blocks = max(1, min(self._k("edl_xgmi_max_blocks"), 256, cap))
+        # Workgroup b of every rank meets workgroup b of every peer (per-workgroup barrier),
+        # so all ranks' grids must be resident together.  One rank per GPU: 256 workgroups
+        # of 512 threads use at most half the chip.  Ranks SHARING a GPU split the chip and
+        # also leave room for the compute kernels running beside the engine.
+        hw = min(self._k("edl_xgmi_max_blocks"), 256)
+        cap = int(os.environ.get("EDL_XGMI_MAX_BLOCKS", hw))
+        if self.ranks_per_device > 1:
+            cap = min(cap, max(4, 128 // self.ranks_per_device))
+        self.blocks = max(1, min(hw, cap))
+        # bucket all-reduces overlap backward: a bounded share of CUs (Brain-tunable)
+        self.async_blocks = max(1, min(self.blocks, int(os.environ.get("EDL_XGMI_ASYNC_BLOCKS", 64))))
         self._aborted = False
+        self._registered: list[_Registered] = []
+        self._opened: dict[tuple[int, bytes], list] = {}   # (peer, handle) -> [mapped base, refcount]
+        self._reg_seq = 0
         self.stream = torch.cuda.Stream(self.device, priority=-1)
 
+    # -- health -----------------------------------------------------------------
     def abort(self) -> None:
         """From any thread: every spinning workgroup of every in-flight call exits."""
         self._aborted = True
@@ -95,9 +135,108 @@ class XgmiComm:
         return self._aborted
 
     def status(self) -> int:
-        """0 = every barrier so far completed; 1 = one gave up (abort / deadline). Synchronising."""
+        """0 = every barrier so far completed; 1 = one gave up (abort / deadline).
+        Valid once the caller has synchronised with the collectives it asks about."""
         return self._rt("edl_xgmi_ws_status", self._ws)
 
+    def status_detail(self) -> dict:
+        """The give-up record: round, phase, workgroup, missing peer, its last flag, waited ms, reason."""
+        out = (ctypes.c_int * 8)()
+        self._rt("edl_xgmi_ws_status_detail", self._ws, out)
+        d = dict(zip(STATUS_FIELDS, list(out)))
+        d["reason"] = REASONS.get(d["reason"], str(d["reason"]))
+        return d
+
+    # -- registered buffers ------------------------------------------------------
+    def register(self, t: torch.Tensor, any_dtype: bool = False) -> "_Registered":
+        """Map ``t`` (this rank's copy of a buffer every rank registers in the same
+        order, e.g. a flat gradient group) on every peer.  Collective.  Later
+        all-reduces of any 16-byte-aligned slice of it run in place."""
+        if not (self.pullable(t) if any_dtype else self.supports(t)):
+            raise XgmiError("register: contiguous fp32 / bf16 tensor of 16-byte multiple expected")
+        self._reg_seq += 1
+        h = ctypes.create_string_buffer(64)
+        off = ctypes.c_uint64()
+        rc = self._rt("edl_xgmi_buf_handle", t.data_ptr(), h, ctypes.byref(off))
+        if rc != 0:
+            raise XgmiError(f"register: hipIpcGetMemHandle failed: hipError {rc}")
+        key = f"{self._prefix}/reg/{self._reg_seq}"
+        self._store.set(f"{key}/{self.rank}", h.raw + int(off.value).to_bytes(8, "little"))
+        peers, opened = [], []
+        for p in range(self.world_size):
+            if p == self.rank:
+                peers.append(t.data_ptr())
+                continue
+            e = self._store.get(f"{key}/{p}")
+            hp, op = e[:64], int.from_bytes(e[64:72], "little")
+            ent = self._opened.get((p, hp))
+            if ent is None:   # segments shared by several registrations are mapped once
+                ptr = ctypes.c_void_p()
+                rc = self._rt("edl_xgmi_buf_open", self.device.index or 0, hp, ctypes.byref(ptr))
+                if rc != 0:
+                    raise XgmiError(f"register: hipIpcOpenMemHandle failed: hipError {rc}")
+                ent = self._opened[(p, hp)] = [ptr.value, 0]
+            ent[1] += 1
+            opened.append((p, hp))
+            peers.append(ent[0] + op)
+        r = _Registered(t, peers, opened)
+        self._registered.append(r)
+        return r
+
+    def unregister(self, r: "_Registered") -> None:
+        """Drop a registration (after this rank's stream has passed every kernel using it)."""
+        if r in self._registered:
+            self._registered.remove(r)
+        for key in r.opened:
+            ent = self._opened.get(key)
+            if ent is None:
+                continue
+            ent[1] -= 1
+            if ent[1] == 0:
+                self._rt("edl_xgmi_buf_close", self.device.index or 0, ent[0])
+                del self._opened[key]
+        r.opened = []
+
+    def pull(self, tensors, holders) -> None:
+        """State transfer: every rank not in ``holders`` copies each tensor from the
+        holders (slice k from holder k, all holders at once over distinct links);
+        holders only take part in the entry / exit barriers.  Collective; runs on
+        the caller's stream, returns after the launches (sync the stream, then
+        check :meth:`status`)."""
+        holders = sorted(set(int(h) for h in holders))
+        if not holders or holders[0] < 0 or holders[-1] >= self.world_size:
+            raise XgmiError(f"pull: bad holder set {holders}")
+        mask = sum(1 << h for h in holders)
+        stream = torch.cuda.current_stream(self.device)
+        regs = []
+        try:
+            for t in tensors:
+                if not self.pullable(t):
+                    raise XgmiError("pull: contiguous tensors of 16-byte multiples expected")
+                regs.append(self.register(t, any_dtype=True))
+            nb = int(max(len(holders), min(self.blocks, 256) // len(holders) * len(holders)))
+            for t, r in zip(tensors, regs):
+                bufs = (ctypes.c_void_p * self.world_size)(*r.peers)
+                self.round += 1
+                rc = self._k("edl_xgmi_pull", bufs, self._flags, self.world_size, self.rank,
+                             t.numel() * t.element_size(), mask, self.round, nb, self._abort_dev,
+                             float(self.timeout_s), self._status_dev, stream.cuda_stream)
+                if rc != 0:
+                    raise XgmiError(f"launch failed: hipError {rc}")
+        finally:
+            stream.synchronize()
+            for r in regs:
+                self.unregister(r)
+
+    def _find_registered(self, t: torch.Tensor):
+        lo = t.data_ptr()
+        hi = lo + t.numel() * t.element_size()
+        for r in self._registered:
+            if r.lo <= lo and hi <= r.hi and r.tensor.dtype == t.dtype:
+                return r, lo - r.lo
+        return None, 0
+
+    # -- launches ----------------------------------------------------------------
     # Every kernel of this comm runs on ONE stream (self.stream).  The workspace's
     # round-parity buffers are only safe if a rank's rounds execute one after
     # another: a sync collective issued while async bucket all-reduces are still
@@ -113,29 +252,45 @@ class XgmiComm:
         return out
 
     def all_reduce(self, t: torch.Tensor, algo: str | None = None) -> torch.Tensor:
-        return self._serialized(self._all_reduce, t, algo)
+        return self._serialized(self._all_reduce, t, algo, self.blocks)
 
-    def _all_reduce(self, t: torch.Tensor, algo: str | None = None) -> torch.Tensor:
+    def _dtype_code(self, t) -> int:
+        return 0 if t.dtype == torch.float32 else 1
+
+    def _all_reduce(self, t: torch.Tensor, algo: str | None = None, max_blocks: int | None = None) -> torch.Tensor:
         if self._aborted:
             raise XgmiError("aborted")
-        if t.dtype not in (torch.float32, torch.bfloat16) or not t.is_contiguous():
-            raise XgmiError("xGMI all-reduce takes contiguous fp32 / bf16 tensors")
+        if not self.supports(t):
+            raise XgmiError("xGMI all-reduce takes contiguous fp32 / bf16 tensors of 16-byte multiples")
+        max_blocks = max_blocks or self.blocks
         flat = t.view(-1)
         es = flat.element_size()
-        if (flat.numel() * es) % 16:
-            raise XgmiError("size must be a multiple of 16 bytes")
-        piece = (self.ws_bytes // 16) * 16 // es
         stream = torch.cuda.current_stream(self.device).cuda_stream
+        nbytes_all = flat.numel() * es
+        reg, off = self._find_registered(t) if algo in (None, "inplace") else (None, 0)
+        if reg is not None and (nbytes_all > self.ONESHOT_MAX or algo == "inplace"):
+            bufs = (ctypes.c_void_p * self.world_size)(*[p + off for p in reg.peers])
+            nvec = nbytes_all // 16
+            blocks = int(max(1, min(max_blocks, -(-nvec // (self.world_size * 1024)))))
+            self.round += 1
+            rc = self._k("edl_xgmi_allreduce_inplace", bufs, self._flags, self.world_size, self.rank, nbytes_all,
+                         self._dtype_code(t), self.round, blocks, self._abort_dev, float(self.timeout_s),
+                         self._status_dev, stream)
+            if rc != 0:
+                raise XgmiError(f"launch failed: hipError {rc}")
+            return t
+        piece = (self.ws_bytes // 16) * 16 // es
         for lo in range(0, flat.numel(), piece):
             part = flat[lo:lo + piece]
             nbytes = part.numel() * es
-            a = (0 if nbytes <= self.ONESHOT_MAX else 1) if algo is None else (0 if algo == "oneshot" else 1)
+            a = (0 if nbytes <= self.ONESHOT_MAX else 1) if algo in (None, "inplace") else \
+                (0 if algo == "oneshot" else 1)
             nvec = nbytes // 16
             per_block = 2048 if a == 0 else 4096  # 16-byte vectors per workgroup before adding workgroups
-            blocks = int(max(1, min(self.blocks, -(-nvec // per_block))))
+            blocks = int(max(1, min(max_blocks, -(-nvec // per_block))))
             self.round += 1
             rc = self._k("edl_xgmi_allreduce", self._data, self._flags, self.world_size, self.rank,
-                         part.data_ptr(), part.data_ptr(), nbytes, 0 if t.dtype == torch.float32 else 1, a,
+                         part.data_ptr(), part.data_ptr(), nbytes, self._dtype_code(t), a,
                          self.round, blocks, self._abort_dev, float(self.timeout_s), self._status_dev, stream)
             if rc != 0:
                 raise XgmiError(f"launch failed: hipError {rc}")
@@ -156,8 +311,7 @@ class XgmiComm:
         if self._aborted:
             raise XgmiError("aborted")
         for t in ts:
-            if t.dtype not in (torch.float32, torch.bfloat16) or not t.is_contiguous() or \
-                    (t.numel() * t.element_size()) % 16:
+            if not self.supports(t):
                 raise XgmiError("xGMI collectives take contiguous fp32 / bf16 tensors of 16-byte multiples")
 
     def all_reduce_max(self, t: torch.Tensor) -> torch.Tensor:
@@ -171,6 +325,16 @@ class XgmiComm:
     def reduce_scatter(self, out: torch.Tensor, inp: torch.Tensor) -> torch.Tensor:
         """out = SUM over ranks of this rank's slice of inp (inp = world_size slices, rank-major)."""
         return self._serialized(self._reduce_scatter, out, inp)
+
+    def barrier(self) -> None:
+        """Device-side barrier of every rank's engine stream (flags only)."""
+        def run():
+            self.round += 1
+            rc = self._k("edl_xgmi_barrier", self._flags, self.world_size, self.rank, self.round, self._abort_dev,
+                         float(self.timeout_s), self._status_dev, torch.cuda.current_stream(self.device).cuda_stream)
+            if rc != 0:
+                raise XgmiError(f"launch failed: hipError {rc}")
+        self._serialized(run)
 
     def _all_reduce_max(self, t: torch.Tensor) -> torch.Tensor:
         self._check(t)
@@ -214,27 +378,38 @@ class XgmiComm:
     def all_reduce_async(self, t: torch.Tensor) -> "_Work":
         """In-place SUM on the engine's own high-priority stream, ordered after the
         caller's stream; ``wait()`` orders the caller's stream after it (the
-        ``ProcessGroupNCCL`` work contract ElasticDDP overlaps with backward)."""
+        ``ProcessGroupNCCL`` work contract ElasticDDP overlaps with backward).
+        Uses at most ``async_blocks`` workgroups so backward keeps most CUs."""
         self.stream.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(self.stream):
-            self._all_reduce(t)
+            self._all_reduce(t, None, self.async_blocks)
         t.record_stream(self.stream)
         ev = torch.cuda.Event()
         ev.record(self.stream)
         return _Work(ev, t)
 
     @staticmethod
+    def pullable(t: torch.Tensor) -> bool:
+        """Byte copies (state transfer) take any dtype."""
+        return (t.is_cuda and t.is_contiguous() and (t.numel() * t.element_size()) % 16 == 0
+                and t.data_ptr() % 16 == 0 and t.numel() > 0)
+
+    @staticmethod
     def supports(t: torch.Tensor) -> bool:
         return (t.is_cuda and t.dtype in (torch.float32, torch.bfloat16) and t.is_contiguous()
-                and (t.numel() * t.element_size()) % 16 == 0)
+                and (t.numel() * t.element_size()) % 16 == 0 and t.data_ptr() % 16 == 0)
 
     def close(self) -> None:
-        """Free the workspace.  Called after a committed step, when every rank has synced its
-        streams, so no engine kernel is in flight anywhere.  Only this engine's stream is
-        drained: a device-wide sync would also wait for an in-flight snapshot copy (up to
-        ~0.5 s at a world change, profiles/r02_ttr_rejoin_*)."""
+        """Unmap registered buffers and free the workspace.  Called after a committed
+        step, when every rank has synced its streams, so no engine kernel is in flight
+        anywhere.  Only this engine's stream is drained: a device-wide sync would also
+        wait for an in-flight snapshot copy (up to ~0.5 s at a world change,
+        profiles/r02_ttr_rejoin_*)."""
         if self._ws is not None:
             torch.cuda.current_stream(self.device).synchronize()
             self.stream.synchronize()
+            for base, _ in self._opened.values():
+                self._rt("edl_xgmi_buf_close", self.device.index or 0, base)
+            self._registered, self._opened = [], {}
             self._rt("edl_xgmi_ws_destroy", self._ws)
             self._ws = None

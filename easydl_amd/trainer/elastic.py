@@ -328,35 +328,38 @@ class ElasticTrainer:
             return
         have = -1 if self.needs_state else self.step
         max_step = int(c.ctrl_all_reduce([have], dist.ReduceOp.MAX)[0])
+        holder = max_step >= 0 and not self.needs_state and self.step == max_step
         if max_step < 0:
             # nobody holds trained state: fresh start (or checkpoint restore on rank 0)
             if c.rank == 0 and self.checkpoint is not None:
                 self._maybe_restore()
-            src_rank = 0
+            holders = [0]
         else:
-            cand = c.rank if (not self.needs_state and self.step == max_step) else 1 << 30
-            src_rank = int(c.ctrl_all_reduce([cand], dist.ReduceOp.MIN)[0])
-        differ = 1 if (self.needs_state or self.step != max_step) else 0
-        need = int(c.ctrl_all_reduce([differ], dist.ReduceOp.MAX)[0])
-        if need or max_step < 0:
+            onehot = [0.0] * c.world_size
+            onehot[c.rank] = 1.0 if holder else 0.0
+            holders = [r for r, v in enumerate(c.ctrl_all_reduce(onehot, dist.ReduceOp.MAX).tolist()) if v > 0]
+        src_rank = holders[0]
+        if len(holders) < c.world_size or max_step < 0:
             t0 = time.time()
-            holder = not self.needs_state and self.step == max_step
             self._fence_snapshot_before_overwrite(c, src_rank, holder)
-            for t in self._state_tensors():
-                c.broadcast(t, src_rank)
+            # every up-to-date rank sends a slice (SURVEY.md §2.8 multi-source scatter):
+            # a joiner's inbound traffic is spread over one link per survivor
+            c.transfer_state(self._state_tensors(), holders if max_step >= 0 else [src_rank])
             scal = c.ctrl_broadcast([self.step, self.opt.step_count], src_rank)
             self.step = int(scal[0])
             self.opt.step_count = int(scal[1])
             if self.device.type == "cuda":
                 torch.cuda.current_stream(self.device).synchronize()
             nbytes = sum(t.numel() * t.element_size() for t in self._state_tensors())
-            self.events.emit("state_broadcast", src=src_rank, bytes=nbytes, s=round(time.time() - t0, 4))
+            self.events.emit("state_broadcast", src=src_rank, sources=len(holders), bytes=nbytes,
+                             s=round(time.time() - t0, 4))
         self.needs_state = False
 
     def _fence_snapshot_before_overwrite(self, c, src: int, holder: bool) -> None:
-        """A state broadcast rewrites this rank's buffers unless it is the source, or a
-        holder of the same step receiving identical bytes over RCCL.  The xGMI-only
-        broadcast zero-fills non-source ranks first.  If the buffers will change, the
+        """A state transfer rewrites this rank's buffers unless it is the source, or a
+        holder of the same step (multi-source transfer never writes holders; an RCCL
+        broadcast writes identical bytes).  The xGMI-only broadcast (TP groups)
+        zero-fills non-source ranks first.  If the buffers will change, the
         in-flight snapshot D2H (which reads them on the checkpoint engine's stream) must
         finish first, or its slot would mix old and new bytes under the old checksum.
         The fence is a stream wait, not a host block."""
@@ -419,8 +422,60 @@ class ElasticTrainer:
         c = self.dp_comm or self.comm  # TP ranks of one replica consume the same samples
         return plan.indices(self.step, c.rank, c.world_size)
 
+    def _sync_buffers(self) -> None:
+        """Module buffers (BatchNorm running statistics) are updated by each rank from its
+        own micro-batches, so they drift apart; rank 0's copy is broadcast after every
+        committed step (DDP's broadcast_buffers).  Snapshots shard the buffers like every
+        other state tensor and assume all ranks hold the same bytes."""
+        c = self.dp_comm
+        if c is None or c.world_size == 1 or not self.bufs.tensors:
+            return
+        try:
+            for t in self.bufs.tensors.values():
+                c.broadcast(t, 0)
+        except CommAborted:
+            pass   # the epoch broke after the commit: the next epoch's state sync covers it
+
+    def _seed_step(self) -> None:
+        """Random streams keyed by (seed, committed step, data-parallel rank): dropout
+        masks of step k do not depend on how the job got to step k (restarts, world
+        changes), so a resume from a snapshot of step k replays step k+1 bit-exactly
+        and a joiner taking over rank r draws what rank r would have drawn.  TP ranks
+        of one replica share the stream (replicated activations need equal masks)."""
+        c = self.dp_comm or self.comm
+        r = c.rank if c is not None else 0
+        torch.manual_seed((self._seed * 1_000_003 + self.step * 7_919 + r * 104_729) % (1 << 62))
+
+    def host_state(self) -> dict:
+        """Host-side training state a resume needs besides the tensors (recorded in every
+        snapshot and in the v1 manifest): the RNG policy + seed, the data-plan cursor and
+        the LR schedule.  Steps and optimizer step count travel separately."""
+        plan = getattr(self, "_plan", None)
+        sched = getattr(self.opt, "schedule", None)
+        return {"rng": {"policy": "per-step", "seed": self._seed},
+                "data": {"cursor_step": self.step, "global_batch": self.global_batch,
+                         "micro_batch": self.micro_batch, "plan_seed": getattr(plan, "seed", None),
+                         "dataset_len": getattr(plan, "n", None)},
+                "lr": sched.state_dict() if sched is not None else {"lr": getattr(self.opt, "lr", None)}}
+
+    def load_host_state(self, h: dict | None) -> None:
+        """Adopt a snapshot's host state (after its step has been restored)."""
+        if not h:
+            return
+        self._seed = int(h.get("rng", {}).get("seed", self._seed))
+        d = h.get("data", {})
+        if d.get("global_batch") and self.global_batch and int(d["global_batch"]) != self.global_batch:
+            log.warning("restored data plan had global batch %s, this run uses %s", d["global_batch"],
+                        self.global_batch)
+        lr = h.get("lr") or {}
+        sched = getattr(self.opt, "schedule", None)
+        if sched is not None and lr.get("total") is not None:
+            sched.lr, sched.warmup, sched.total, sched.min_ratio = (lr["lr"], lr["warmup"], lr["total"],
+                                                                    lr["min_ratio"])
+
     def _run_step(self, loss_fn, data, plan):
         mbs = self._micro_batches(data, plan)
+        self._seed_step()
         self.flat.zero_grad()
         total = 0.0
         loss_acc = None
@@ -467,6 +522,7 @@ class ElasticTrainer:
             gb = w * self.micro_batch
             self.global_batch = gb
         plan = ElasticBatchPlan(len(data), gb, self.micro_batch, seed=17)
+        self._plan = plan
         if os.environ.get("EDL_PREJOIN_WARMUP", "1") != "0":
             self._prejoin = lambda: self._prejoin_warmup(loss_fn, data, plan)
         self._connect()
@@ -504,6 +560,7 @@ class ElasticTrainer:
                         self.checkpoint.fence()  # never update params under an in-flight snapshot
                     with trace.range("optimizer"):
                         self.opt.step(pre_scale=1.0)
+                    self._sync_buffers()
                     self.step += 1
                     self.last_loss = loss
                     rec = {"step": self.step, "epoch": self.comm.epoch, "world": self.comm.world_size,

@@ -7,6 +7,7 @@ import json
 import os
 import sys
 import threading
+import time
 
 import torch
 import torch.distributed as dist
@@ -19,8 +20,24 @@ mode = os.environ.get("XG_MODE", "sum")
 torch.cuda.set_device(0)
 store = dist.TCPStore("127.0.0.1", int(os.environ["PORT"]), world, rank == 0,
                       timeout=datetime.timedelta(seconds=60))
-c = Communicator(store, rank, world, 3, device=torch.device("cuda", 0), job="t", timeout_s=5.0, data_backend="xgmi")
+# barriers give up 5 s after entry in the abort test; elsewhere host-side verification
+# between iterations must never look like a dead peer (and ranks meet at a store barrier)
+c = Communicator(store, rank, world, 3, device=torch.device("cuda", 0), job="t",
+                 timeout_s=float(os.environ.get("XG_TIMEOUT", 5.0 if mode == "abort" else 30.0)), data_backend="xgmi")
+NOSYNC = os.environ.get("XG_NOSYNC") == "1"   # diagnostics: round-2 behaviour (no store barrier)
 res = {"rank": rank, "ok": True, "errors": [], "backend": c.backend}
+_n = [0]
+
+
+def sync():
+    res.setdefault("t_launch", []).append(round(time.time(), 4))
+    if NOSYNC:
+        return
+    _n[0] += 1
+    store.set(f"it{_n[0]}/{rank}", "1")
+    store.wait([f"it{_n[0]}/{r}" for r in range(world)])
+
+
 if mode == "sum":
     grads = torch.empty(3 * (1 << 20) + 4096, device="cuda", dtype=torch.bfloat16)
     buckets = [grads[:4096], grads[4096:4096 + (1 << 20)], grads[4096 + (1 << 20):]]
@@ -30,6 +47,7 @@ if mode == "sum":
         exp = torch.zeros(grads.numel(), dtype=torch.float64)
         for r in range(world):
             exp += torch.randint(-8, 8, grads.shape, generator=torch.Generator().manual_seed(100 * it + r)).double()
+        sync()
         works = [c.all_reduce_async(b) for b in buckets]  # issued in bucket order, overlapping
         for w in works:
             w.wait()
@@ -76,9 +94,10 @@ elif mode == "mixed":
         def ints(n, seed):
             return torch.randint(-32, 32, (n,), generator=torch.Generator().manual_seed(seed)).float()
         big = [ints(6 << 20, 1000 * it + 10 * k + rank).cuda() for k in range(3)]
-        works = [x.all_reduce_async(b) for b in big]
         m = 5 << 20
         inp = ints(world * m, 2000 * it + rank).cuda()
+        sync()
+        works = [x.all_reduce_async(b) for b in big]
         part = torch.empty(m, device="cuda")
         x.reduce_scatter(part, inp)
         gat = torch.empty(world * m, device="cuda")
@@ -96,6 +115,7 @@ elif mode == "mixed":
             res["ok"] = False
             res["errors"].append(f"iter {it} rs/ag")
     res["healthy"] = c.healthy()
+    res["detail"] = x.status_detail()
 elif mode == "abort":
     if rank == 0:  # the peer never joins: the watchdog's abort() releases the kernel, healthy() says so
         t = torch.ones(1 << 16, device="cuda", dtype=torch.bfloat16)
@@ -107,6 +127,8 @@ elif mode == "abort":
         res["aborted"] = c.aborted
     store.set(f"done{rank}", "1")
     store.wait([f"done{r}" for r in range(world)])
+if c.xgmi is not None and "detail" not in res:
+    res["detail"] = c.xgmi.status_detail()
 print(json.dumps(res), flush=True)
 with open(os.environ["OUT"] + f".{rank}", "w") as f:
     json.dump(res, f)

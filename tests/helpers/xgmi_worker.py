@@ -1,5 +1,10 @@
-"""One rank of the xGMI all-reduce test (all ranks share one GPU: IPC mapping
-and the flag protocol are exercised exactly as across GPUs; only the link is local)."""
+"""One rank of the xGMI engine tests (all ranks share one GPU: IPC mapping and
+the flag protocol are exercised exactly as across GPUs; only the link is local).
+
+Ranks meet at a store barrier before every case: the engine's barriers wait
+for peers for at most ``timeout_s`` from barrier entry, and the expected values
+are computed on the CPU between cases (host skew must not look like a dead peer).
+"""
 import datetime
 import json
 import os
@@ -18,18 +23,29 @@ mode = os.environ.get("XG_MODE", "sum")
 torch.cuda.set_device(0)
 store = dist.TCPStore("127.0.0.1", int(os.environ["PORT"]), world, rank == 0,
                       timeout=datetime.timedelta(seconds=60))
-x = XgmiComm(store, "xg", rank, world, torch.device("cuda", 0), ws_bytes=8 << 20, timeout_s=5.0)
-res = {"rank": rank, "ok": True, "errors": []}
+x = XgmiComm(store, "xg", rank, world, torch.device("cuda", 0), ws_bytes=8 << 20,
+             timeout_s=5.0 if mode == "abort" else 30.0)
+res = {"rank": rank, "ok": True, "errors": [], "blocks": x.blocks, "ranks_per_device": x.ranks_per_device}
+_n = [0]
+
+
+def sync():
+    _n[0] += 1
+    store.set(f"b{_n[0]}/{rank}", "1")
+    store.wait([f"b{_n[0]}/{r}" for r in range(world)])
+
+
+def ints(n, seed, dt):
+    return torch.randint(-8, 8, (n,), generator=torch.Generator().manual_seed(seed)).to(dt)
+
+
 if mode == "sum":
     cases = [(torch.float32, 1024, "oneshot"), (torch.bfloat16, 4096, "oneshot"), (torch.float32, 1 << 20, "twoshot"),
              (torch.bfloat16, 3 * (1 << 20) + 64, "twoshot"), (torch.float32, 5 << 20, None)]  # last: > workspace
     for dt, n, algo in cases:
-        g = torch.Generator(device="cpu").manual_seed(1000 + rank)
-        t = torch.randint(-8, 8, (n,), generator=g).to(dt).cuda()
-        exp = torch.zeros(n, dtype=torch.float64)
-        for r in range(world):
-            gr = torch.Generator(device="cpu").manual_seed(1000 + r)
-            exp += torch.randint(-8, 8, (n,), generator=gr).double()
+        t = ints(n, 1000 + rank, dt).cuda()
+        exp = sum(ints(n, 1000 + r, dt).double() for r in range(world))
+        sync()
         for _ in range(3):  # repeated rounds reuse both parity buffers
             t2 = t.clone()
             x.all_reduce(t2, algo)
@@ -37,6 +53,48 @@ if mode == "sum":
         if not torch.equal(t2.double().cpu(), exp):
             res["ok"] = False
             res["errors"].append(f"{dt} n={n} algo={algo}: max err {(t2.double().cpu() - exp).abs().max().item()}")
+    res["status"] = x.status()
+    res["detail"] = x.status_detail()
+elif mode == "inplace":
+    # registered buffer (the flat-gradient case): bucket slices all-reduced in place,
+    # one launch each, several rounds and buckets in flight on the engine stream
+    for dt in (torch.bfloat16, torch.float32):
+        n = 3 * (1 << 20) + 4096 + 64 * 7   # odd chunking: the last rank's chunk is short
+        grads = torch.empty(n, dtype=dt, device="cuda")
+        reg = x.register(grads)
+        bounds = [0, 4096, 4096 + (1 << 20), n]   # 8 KB bucket: staged one-shot; others in place
+        for it in range(3):
+            grads.copy_(ints(n, 100 * it + rank, dt).cuda())
+            exp = sum(ints(n, 100 * it + r, dt).double() for r in range(world))
+            sync()
+            works = [x.all_reduce_async(grads[a:b]) for a, b in zip(bounds[:-1], bounds[1:])]
+            for w in works:
+                w.wait()
+            torch.cuda.current_stream().synchronize()
+            if not torch.equal(grads.double().cpu(), exp):
+                bad = (grads.double().cpu() - exp).abs()
+                res["ok"] = False
+                res["errors"].append(f"{dt} iter {it}: max err {bad.max().item()} at {int(bad.argmax())}")
+        sync()
+        x.unregister(reg)
+    res["status"] = x.status()
+    res["detail"] = x.status_detail()
+elif mode == "pull":
+    # state transfer: ranks 0..h-1 hold the state, the others receive it from all holders
+    holders = list(range(max(1, world // 2)))
+    shapes = ((1 << 20, torch.float32), (3 * 4096 + 8, torch.bfloat16), (4 * 1000, torch.int32))
+    ts = [torch.empty(n, dtype=dt, device="cuda") for n, dt in shapes]
+    for i, t in enumerate(ts):
+        t.copy_(ints(t.numel(), 77 + i, t.dtype).cuda() if rank in holders else torch.zeros_like(t))
+    sync()
+    t0 = time.time()
+    x.pull(ts, holders)
+    torch.cuda.synchronize()
+    res["elapsed"] = time.time() - t0
+    for i, t in enumerate(ts):
+        if not torch.equal(t.cpu(), ints(t.numel(), 77 + i, t.dtype)):
+            res["ok"] = False
+            res["errors"].append(f"tensor {i} differs on rank {rank}")
     res["status"] = x.status()
 elif mode == "abort":
     # rank 1 never joins the collective: rank 0's kernel must give up on abort, not hang
@@ -48,9 +106,11 @@ elif mode == "abort":
         torch.cuda.synchronize()
         res["elapsed"] = time.time() - t0
         res["status"] = x.status()
+        res["detail"] = x.status_detail()
     store.set(f"done{rank}", "1")
     store.wait([f"done{r}" for r in range(world)])
 print(json.dumps(res), flush=True)
 with open(os.environ["OUT"] + f".{rank}", "w") as f:
     json.dump(res, f)
+sync()
 x.close()

@@ -41,6 +41,24 @@ def _run(world, tmp_path, mode="sum", timeout=120, worker=WORKER):
 @pytest.mark.parametrize("world", [2, 4])
 def test_xgmi_allreduce_exact(cuda, tmp_path, world):
     for r in _run(world, tmp_path):
+        assert r["ok"], (r["errors"], r["detail"])
+        assert r["status"] == 0
+        # ranks sharing the GPU are detected and the grid capped for co-residency
+        assert r["ranks_per_device"] == world and r["blocks"] <= max(4, 128 // world)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_xgmi_inplace_registered_allreduce_exact(cuda, tmp_path, world):
+    """Registered (flat-gradient) buffer: bucket all-reduces in place, one launch each."""
+    for r in _run(world, tmp_path, mode="inplace"):
+        assert r["ok"], (r["errors"], r["detail"])
+        assert r["status"] == 0
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_xgmi_multi_source_pull(cuda, tmp_path, world):
+    """State transfer: receivers copy slice k of every tensor from holder k."""
+    for r in _run(world, tmp_path, mode="pull"):
         assert r["ok"], r["errors"]
         assert r["status"] == 0
 
@@ -49,6 +67,9 @@ def test_xgmi_abort_releases_spinning_kernel(cuda, tmp_path):
     r0 = _run(2, tmp_path, mode="abort")[0]
     assert r0["status"] == 1           # the barrier gave up ...
     assert r0["elapsed"] < 4.5         # ... on the abort word, before the 5 s deadline
+    d = r0["detail"]                   # ... and says where: entry barrier, waiting for rank 1
+    assert d["reason"] == "abort" and d["phase"] == 0 and d["peer"] == 1 and d["peer_flag"] == 0, d
+    assert 500 <= d["waited_ms"] < 4500, d
 
 
 def test_communicator_xgmi_bucket_allreduce(cuda, tmp_path):
@@ -76,8 +97,8 @@ def test_xgmi_sync_collectives_queue_behind_pending_async(cuda, tmp_path):
     """Sync reduce-scatter / all-gather issued while async all-reduces are pending on
     the same comm: one stream orders every round, all results exact."""
     for r in _run(2, tmp_path, mode="mixed", worker=COMM_WORKER):
-        assert r["ok"], r["errors"]
-        assert r["healthy"]
+        assert r["ok"], (r["errors"], r.get("detail"))
+        assert r["healthy"], r.get("detail")
 
 
 @pytest.mark.parametrize("sp", ["0", "1"])
