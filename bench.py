@@ -150,7 +150,13 @@ def main():
     tps = tokens / el
     fpt = cfg.flops_per_token(S)
     tflops_gpu = tps / (1 if (args.share_gpu and use_cuda) else comm.world_size) * fpt / 1e12
-    metric = "tokens/sec, Llama-3-8B elastic DDP (full train step: fwd+bwd+allreduce+commit+AdamW)"
+    dp_world = comm.world_size // tp
+    if dp_world > 1:
+        metric = "tokens/sec, Llama-3-8B elastic DDP (full train step: fwd+bwd+bucketed all-reduce+commit+AdamW)"
+    else:
+        # one data-parallel rank: the gradient all-reduce is the identity (LocalCommunicator)
+        # and no rendezvous commit runs; the step is fwd+bwd+clip+AdamW
+        metric = "tokens/sec, Llama-3-8B elastic DDP (full train step at N=1: fwd+bwd+clip+AdamW; all-reduce is identity)"
     if tp > 1:
         metric = f"tokens/sec, {args.model} elastic DP x TP={tp} (full train step)"
     res = {

@@ -293,6 +293,29 @@ int edl_shm_reassign(void* h, const char* new_name) {
   return 0;
 }
 
+// Re-use the segment for a new layout WITHOUT dropping the newest snapshot of the
+// old one: every slot except the current one is invalidated and the file gets a
+// second name (hard link) for the new layout.  Until the caller unlinks the old
+// name (once this rank's first new-layout snapshot has committed, just before the
+// kept slot is overwritten), a whole-job restart still finds the old world's
+// complete snapshot set.  Slots carry their layout in `meta`, so readers of either
+// name tell old-layout and new-layout slots apart.  Returns 0 or -errno.
+int edl_shm_relink(void* h, const char* new_name) {
+  auto* s = static_cast<Seg*>(h);
+  if (!s || !new_name || new_name[0] != '/') return -EINVAL;
+  const int32_t cur = __atomic_load_n(&s->hdr()->current, __ATOMIC_ACQUIRE);
+  for (uint32_t i = 0; i < s->hdr()->nslots; ++i)
+    if ((int32_t)i != cur) __atomic_store_n(&s->slot(i)->state, kEmpty, __ATOMIC_RELEASE);
+  msync(s->base, kHdr * (1 + s->hdr()->nslots), MS_SYNC);
+  const std::string from = "/dev/shm" + s->name, to = std::string("/dev/shm") + new_name;
+  if (from != to) {
+    unlink(to.c_str());  // a stale segment of that name (an older run's layout)
+    if (link(from.c_str(), to.c_str()) != 0) return -errno;
+  }
+  s->name = new_name;
+  return 0;
+}
+
 }  // extern "C"
 
 // ---------------------------------------------------------------------------

@@ -39,6 +39,7 @@ SIGS = {
     "edl_shm_close": (i32, [vp, i32]),
     "edl_shm_unlink": (i32, [cp]),
     "edl_shm_reassign": (i32, [vp, cp]),
+    "edl_shm_relink": (i32, [vp, cp]),
     "edl_ckpt_engine_create": (vp, [i32, u64, i32]),
     "edl_ckpt_snapshot": (i64, [vp, vp, i32, u64p, u64p, u64p, vp, i64, i64, i64, cp]),
     "edl_ckpt_fence": (i32, [vp, i64, vp]),

@@ -196,6 +196,7 @@ class CheckpointManager:
         self.pin = pin
         self._seg: ShmSegment | None = None
         self._seg_key = None
+        self._old_name = None       # previous layout's name of a relinked segment (see _segment)
         self._engine = None
         self._engine_dev = None
         self._ticket = None
@@ -263,17 +264,43 @@ class CheckpointManager:
             self.wait()
             self._join_persist()
             if self._seg.slot_bytes >= need_bytes:
-                rc = self._seg.rt("edl_shm_reassign", self._seg.h, name.encode())
+                old = self._seg.name
+                self._drop_old_name()
+                rc = self._seg.rt("edl_shm_relink", self._seg.h, name.encode())
                 if rc == 0:
+                    # the old layout's newest snapshot stays readable under the old name
+                    # until this rank's first new-layout snapshot has committed
+                    self._old_name = old if old != name else None
                     self._seg.name, self._seg_key = name, key
                     self.stats["reassigned"] = self.stats.get("reassigned", 0) + 1
                     return self._seg
                 log.warning("re-using snapshot segment as %s failed (%d): new segment", name, rc)
             self._seg.close()
             self._seg = None
+        self._drop_old_name()
         self._seg = ShmSegment(name, max(need_bytes, alloc_bytes), create=True, pin=self.pin and pin)
         self._seg_key = key
         return self._seg
+
+    @staticmethod
+    def _kept_slot_next(seg) -> bool:
+        """True once a new-layout snapshot is current: the next write targets the other
+        (kept, old-layout) slot."""
+        cur = seg.rt("edl_shm_current", seg.h)
+        info = seg.slot_info(cur) if cur >= 0 else None
+        return info is not None and info["meta"].get("world") is not None and \
+            seg.name.endswith(f"-w{info['meta']['world']}-s{info['meta'].get('shard')}")
+
+    def _drop_old_name(self) -> None:
+        """Unlink the previous layout's name of a relinked segment (its kept slot is about
+        to be overwritten, or the segment changes hands again)."""
+        old = getattr(self, "_old_name", None)
+        self._old_name = None
+        if old:
+            try:
+                os.unlink("/dev/shm" + old)
+            except OSError:
+                pass
 
     # -- snapshot ------------------------------------------------------------
     def on_step(self, trainer) -> None:
@@ -296,6 +323,8 @@ class CheckpointManager:
             # headroom: the largest shard of a world one rank smaller (+ alignment slack)
             alloc = max(shard_layout(state, s, world - 1)[1] for s in range(world - 1)) + 8
         seg = self._segment(world, shard, cs_off + 8, pin=state[0][1].is_cuda, tag=tag, alloc_bytes=alloc)
+        if getattr(self, "_old_name", None) and self._kept_slot_next(seg):
+            self._drop_old_name()   # this write overwrites the old layout's kept snapshot
         if self._persist_busy_slot(seg):
             # A/B slots: the slot this snapshot would overwrite is still being written to
             # disk (persisting takes longer than two intervals) -> skip rather than tear it
@@ -412,7 +441,10 @@ class CheckpointManager:
             per = []
             for s in range(w):
                 seg = ShmSegment(shards[s], create=False)
-                per.append({i["step"]: i for i in seg.committed()})
+                # a relinked segment is visible under two layouts' names: keep the slots
+                # whose recorded layout is the one this name stands for
+                per.append({i["step"]: i for i in seg.committed()
+                            if i["meta"].get("world", w) == w and i["meta"].get("shard", s) == s})
                 seg.close()
             common = set(per[0])
             for p in per[1:]:
@@ -538,6 +570,8 @@ class CheckpointManager:
     def close(self, unlink: bool = False) -> None:
         self.wait()
         self._join_persist(60)
+        if unlink:
+            self._drop_old_name()
         if self._seg is not None:
             self._seg.close(unlink)
             self._seg = None

@@ -182,8 +182,10 @@ def test_snapshot_skips_the_slot_a_persist_is_reading(tmp_path):
 
 def test_world_change_reuses_the_pinned_segment(tmp_path):
     """A shrink by one rank re-uses the (headroom-sized, page-locked) segment under the
-    new layout's name with its slots invalidated: no new mapping, no re-pinning, and
-    no stale old-layout slot visible under the new name."""
+    new layout's name: no new mapping, no re-pinning.  The old layout's newest snapshot
+    stays readable under the OLD name until this rank's first new-layout snapshot has
+    committed (a whole-job restart in between still finds a complete world), and the
+    new name never reports an old-layout slot as its own."""
     import os
     import types
     unlink_job_segments(JOB)
@@ -193,16 +195,52 @@ def test_world_change_reuses_the_pinned_segment(tmp_path):
         a.comm = types.SimpleNamespace(world_size=4, rank=1, epoch=1)
         a.step = 1
         ckpt.snapshot(a)
+        ckpt.wait()
         h0 = ckpt._seg.h
         assert os.path.exists(f"/dev/shm/edl-{JOB}-w4-s1")
         a.comm = types.SimpleNamespace(world_size=3, rank=2, epoch=2)     # renumbered survivor
         a.step = 2
         seg = ckpt._segment(3, 2, shard_layout(CheckpointManager.state_of(a), 2, 3)[1] + 8)
         assert seg.h == h0 and ckpt.stats["reassigned"] == 1
-        assert not os.path.exists(f"/dev/shm/edl-{JOB}-w4-s1") and os.path.exists(f"/dev/shm/edl-{JOB}-w3-s2")
-        assert seg.committed() == []                                       # old layout invalidated
+        assert os.path.exists(f"/dev/shm/edl-{JOB}-w4-s1") and os.path.exists(f"/dev/shm/edl-{JOB}-w3-s2")
+        old = ShmSegment(f"/edl-{JOB}-w4-s1", create=False)
+        assert [i["step"] for i in old.committed()] == [1]                 # old world's snapshot kept
+        old.close()
+        assert [i["meta"]["world"] for i in seg.committed()] == [4]       # ... and tagged with its layout
+        ckpt.snapshot(a)                                                   # first new-layout snapshot
+        ckpt.wait()
+        assert sorted(i["step"] for i in ckpt._seg.committed()) == [1, 2] and ckpt._seg.h == h0
+        assert os.path.exists(f"/dev/shm/edl-{JOB}-w4-s1")
+        a.step = 3
+        ckpt.snapshot(a)                                                   # overwrites the kept slot
+        ckpt.wait()
+        assert not os.path.exists(f"/dev/shm/edl-{JOB}-w4-s1")
+        assert sorted(i["step"] for i in ckpt._seg.committed()) == [2, 3]
+    finally:
+        ckpt.close()
+        unlink_job_segments(JOB)
+
+
+def test_find_latest_ignores_other_layout_slots(tmp_path):
+    """A relinked segment shows old-layout slots under the new name: find_latest only
+    counts slots whose recorded layout matches the name's (world, shard)."""
+    import types
+    unlink_job_segments(JOB)
+    ckpt = CheckpointManager(JOB, interval=1)
+    try:
+        a = _trainer(tmp_path, None)
+        a.comm = types.SimpleNamespace(world_size=1, rank=0, epoch=1)
+        a.step = 5
         ckpt.snapshot(a)
-        assert [i["step"] for i in ckpt._seg.committed()] == [2] and ckpt._seg.h == h0
+        ckpt.wait()
+        assert ckpt.find_latest()[:2] == (1, 5)
+        # pretend the world-1 segment was relinked to a world-2 layout without a snapshot
+        ckpt._seg.rt("edl_shm_relink", ckpt._seg.h, f"/edl-{JOB}-w2-s0".encode())
+        seg1 = ShmSegment(f"/edl-{JOB}-w2-s1", slot_bytes=4096, create=True)
+        seg1.commit(seg1.begin(), 5, 2, 8, 0, {"world": 2, "shard": 1, "t": []})
+        found = ckpt.find_latest()
+        assert found is not None and found[0] == 1     # not the half-matching world-2 set
+        seg1.close()
     finally:
         ckpt.close()
         unlink_job_segments(JOB)
@@ -257,3 +295,46 @@ def test_module_buffers_are_training_state(tmp_path):
         assert int(c.model.bn.num_batches_tracked) == nb
     finally:
         unlink_job_segments("ckbn")
+
+
+class _DropNet(torch.nn.Module):
+    """Tiny token model with dropout: resume is only bit-exact if the random stream is."""
+
+    def __init__(self, device=None):
+        super().__init__()
+        self.emb = torch.nn.Embedding(64, 32, device=device)
+        self.fc1 = torch.nn.Linear(32, 64, device=device)
+        self.drop = torch.nn.Dropout(0.3)
+        self.fc2 = torch.nn.Linear(64, 64, device=device)
+
+    def forward(self, ids, labels):
+        h = self.drop(torch.relu(self.fc1(self.emb(ids))))
+        return torch.nn.functional.cross_entropy(self.fc2(h).flatten(0, 1), labels.flatten())
+
+
+def test_resume_is_bit_exact_with_dropout(tmp_path):
+    """Snapshot at step 2 -> a NEW trainer (different constructor seed) restores it and
+    trains to step 4: parameters and optimizer state equal an uninterrupted 4-step run
+    bit for bit (per-step RNG streams + host state in the snapshot metadata)."""
+    unlink_job_segments(JOB)
+    data = SyntheticTokens(64, 16, num_samples=1024)
+
+    def mk(ckpt, seed, sub):
+        ctx = TrainerContext(job=JOB, run_dir=str(tmp_path / sub))
+        return ElasticTrainer(lambda d: _DropNet(d), global_batch=4, micro_batch=2, lr=1e-2, device="cpu", ctx=ctx,
+                              checkpoint=ckpt, seed=seed)
+
+    ref = mk(None, 7, "a").fit(lambda m, b: m(*b), data, num_steps=4)
+    ckpt = CheckpointManager(JOB, interval=2)
+    try:
+        mk(ckpt, 7, "b").fit(lambda m, b: m(*b), data, num_steps=2)
+        ckpt.wait()
+        resumed = mk(ckpt, 99, "c")     # wrong seed on purpose: the snapshot's host state wins
+        resumed.fit(lambda m, b: m(*b), data, num_steps=4)
+        assert resumed.step == 4 and resumed._seed == 7
+        assert torch.equal(_flat(ref), _flat(resumed))
+        info = ckpt.find_latest()
+        assert info is not None and info[2][0]["meta"]["host"]["data"]["cursor_step"] == info[1]
+    finally:
+        ckpt.close()
+        unlink_job_segments(JOB)
