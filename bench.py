@@ -156,7 +156,8 @@ def main():
     else:
         # one data-parallel rank: the gradient all-reduce is the identity (LocalCommunicator)
         # and no rendezvous commit runs; the step is fwd+bwd+clip+AdamW
-        metric = "tokens/sec, Llama-3-8B elastic DDP (full train step at N=1: fwd+bwd+clip+AdamW; all-reduce is identity)"
+        metric = ("tokens/sec, Llama-3-8B elastic DDP "
+                  "(full train step at N=1: fwd+bwd+clip+AdamW; all-reduce is identity)")
     if tp > 1:
         metric = f"tokens/sec, {args.model} elastic DP x TP={tp} (full train step)"
     res = {
