@@ -13,7 +13,14 @@
 //     (edl_sparse_adamw_rows) — untouched rows keep their moments, as in
 //     TF's lazy Adam, so the cost is O(touched rows), not O(table);
 //   * dense pull with cast (edl_ps_pull_cast): fp32 PS shard -> bf16 worker
-//     params, reading a peer pointer over xGMI.
+//     params, reading a peer pointer over xGMI;
+//   * multi-tensor dense push / pull (edl_ps_multi_copy): ONE launch moves every
+//     parameter of a shard between the worker's (scattered, bf16 or fp32)
+//     tensors and the PS's flat fp32 buffer — push writes gradients, cast to
+//     fp32, straight into the PS's inbox (peer writes over xGMI), pull reads
+//     the fp32 shard and writes the worker's parameters.  A tensor table in
+//     device memory drives it; workgroup -> (tensor, chunk) by a binary search
+//     over the per-tensor block prefix.
 // Index validity is checked on the host side of every entry (rows bound); a
 // bad id is clamped to a zero row on gather and dropped on scatter instead of
 // faulting the device.
@@ -138,9 +145,92 @@ __global__ __launch_bounds__(256) void pull_cast_kernel(const float* __restrict_
 
 inline int row_blocks(int64_t n) { return (int)((n + (kRowBlock / kWave) - 1) / (kRowBlock / kWave)); }
 
+// One tensor of a multi-tensor copy.  kind: 0 = local fp32, 1 = local bf16,
+// 2 = no local tensor (push: write zeros).
+struct PsEntry {
+  uint64_t local;   // worker tensor (device pointer)
+  int64_t off;      // element offset in the PS flat buffer (multiple of 4)
+  int64_t numel;
+  int32_t kind;
+  int32_t pad;
+};
+
+constexpr int kMcThreads = 256;
+constexpr int kMcChunk = kMcThreads * 4 * 8;   // elements per workgroup: 8 x 4-element steps per thread
+
+// PUSH: flat[off + i] = fp32(local[i]);  PULL: local[i] = cast(flat[off + i]).
+template <bool PUSH>
+__global__ __launch_bounds__(kMcThreads) void ps_multi_copy_kernel(const PsEntry* __restrict__ tab,
+                                                                   const int64_t* __restrict__ bstart, int n,
+                                                                   float* __restrict__ flat) {
+  // entry e owns workgroups [bstart[e], bstart[e+1])
+  int lo = 0, hi = n;
+  const int64_t b = blockIdx.x;
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (bstart[mid] <= b) lo = mid; else hi = mid;
+  }
+  const PsEntry e = tab[lo];
+  const int64_t c0 = (b - bstart[lo]) * kMcChunk;
+  const int64_t c1 = min(e.numel, c0 + kMcChunk);
+  float* f = flat + e.off;
+  const int64_t v1 = c1 & ~int64_t(3);   // 4-element vectors (16 B fp32 / 8 B bf16)
+  for (int64_t i = c0 + 4 * threadIdx.x; i < v1; i += 4 * kMcThreads) {
+    if (PUSH) {
+      f32x4 v;
+      if (e.kind == 0) {
+        v = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(e.local) + i);
+      } else if (e.kind == 1) {
+        const u32x2 w = *reinterpret_cast<const u32x2*>(reinterpret_cast<const bf16_t*>(e.local) + i);
+        v = f32x4{__uint_as_float(w[0] << 16), __uint_as_float(w[0] & 0xffff0000u), __uint_as_float(w[1] << 16),
+                  __uint_as_float(w[1] & 0xffff0000u)};
+      } else {
+        v = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+      *reinterpret_cast<f32x4*>(f + i) = v;
+    } else {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(f + i);
+      if (e.kind == 0) {
+        *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(e.local) + i) = v;
+      } else if (e.kind == 1) {
+        *reinterpret_cast<u32x2*>(reinterpret_cast<bf16_t*>(e.local) + i) = u32x2{pack2(v[0], v[1]), pack2(v[2], v[3])};
+      }
+    }
+  }
+  // tail of the tensor (numel % 4): scalar, in the last chunk only
+  for (int64_t i = v1 + threadIdx.x; i < c1; i += kMcThreads) {
+    if (PUSH) {
+      float x = 0.f;
+      if (e.kind == 0) x = reinterpret_cast<const float*>(e.local)[i];
+      else if (e.kind == 1) x = bf2f(reinterpret_cast<const bf16_t*>(e.local)[i]);
+      f[i] = x;
+    } else {
+      if (e.kind == 0) reinterpret_cast<float*>(e.local)[i] = f[i];
+      else if (e.kind == 1) reinterpret_cast<bf16_t*>(e.local)[i] = f2bf(f[i]);
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" {
+
+int edl_ps_multi_chunk() { return kMcChunk; }
+
+// table / bstart: device arrays built by the host (easydl_amd/ops/sparse.py
+// MultiCopyPlan); nblocks = bstart[n].  Local bf16 / fp32 tensors must be 8- /
+// 16-byte aligned and every PS offset a multiple of 4 elements.
+int edl_ps_multi_copy(const void* table, const int64_t* bstart, int n, int64_t nblocks, float* flat, int push,
+                      hipStream_t s) {
+  if (n <= 0 || nblocks <= 0) return 0;
+  if (nblocks > 0x7fffffff) return (int)hipErrorInvalidValue;
+  if (push)
+    ps_multi_copy_kernel<true><<<(unsigned)nblocks, kMcThreads, 0, s>>>((const PsEntry*)table, bstart, n, flat);
+  else
+    ps_multi_copy_kernel<false><<<(unsigned)nblocks, kMcThreads, 0, s>>>((const PsEntry*)table, bstart, n, flat);
+  EDL_LAUNCH_CHECK();
+  return 0;
+}
 
 int edl_embed_gather(const float* table, const int64_t* idx, int64_t n, int dim, int64_t rows, void* out,
                      int out_bf16, hipStream_t s) {

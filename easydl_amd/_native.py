@@ -94,6 +94,8 @@ _KERNEL_SIGS = {
     "edl_sparse_rows_update": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_i64, c_int, c_i64, c_int, c_float,
                                c_float, c_float, c_float, c_float, c_i64, c_float, c_void_p],
     "edl_ps_pull_cast": [c_void_p, c_void_p, c_i64, c_void_p],
+    "edl_ps_multi_chunk": [],
+    "edl_ps_multi_copy": [c_void_p, c_void_p, c_int, c_i64, c_void_p, c_int, c_void_p],
     "edl_xgmi_max_blocks": [],
     "edl_diag_lds_dma": [c_void_p, c_void_p, c_int, c_void_p],
     "edl_bn_groups": (c_int, [c_i64, c_int]),

@@ -101,13 +101,19 @@ class RendezvousManager:
         """Processes that announced themselves (RendezvousClient.arriving) and are still
         warming up: not joined, not dead, announced less than arrive_timeout_s ago."""
         raw = self.kv.get_str("rdzv/arriving", "") or ""
+        settled = self.__dict__.setdefault("_arrive_settled", set())
         out = []
         for n in dict.fromkeys(x for x in raw.split(",") if x):
+            if n in settled:
+                continue   # decided earlier: no store round trips for it on later ticks
             if n in joined or self.kv.exists(f"ev/dead/{n}") or self.kv.exists(f"ev/exit/{n}"):
-                continue   # joined already, or died while starting (supervisor exit event)
+                settled.add(n)   # joined already, or died while starting (supervisor exit event)
+                continue
             ts = self.kv.get(f"rdzv/arrive_ts/{n}")
             if ts is not None and now - float(ts) < self.cfg.arrive_timeout_s:
                 out.append(n)
+            elif ts is not None:
+                settled.add(n)   # announced too long ago: never counted again
         return out
 
     def mark_dead(self, node: str, reason: str) -> None:

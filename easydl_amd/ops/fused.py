@@ -176,6 +176,11 @@ class _XentFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dloss):
         k = _native.kernels()
+        if getattr(ctx, "consumed", False):
+            # the first backward turned the saved logits into their gradient in place
+            raise RuntimeError("fused cross_entropy: backward ran twice (retain_graph is not supported: "
+                               "the logits buffer is consumed by its gradient)")
+        ctx.consumed = True
         logits, labels, nvalid, loss = ctx.saved_tensors
         rows, V = logits.shape
         scale = (dloss.float() / nvalid).reshape(1).contiguous()

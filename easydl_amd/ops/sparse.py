@@ -118,3 +118,42 @@ def pull_cast(src: torch.Tensor, dst: torch.Tensor) -> torch.Tensor:
         return dst
     dst.copy_(src)
     return dst
+
+
+class MultiCopyPlan:
+    """One-launch dense push / pull between a worker's scattered parameter (or
+    gradient) tensors and a PS's flat fp32 buffer (``edl_ps_multi_copy``,
+    csrc/kernels/ps_sparse.hip).  ``items`` = [(tensor or None, flat offset, numel)];
+    None pushes zeros (a parameter without a gradient).  The tensor table lives in
+    device memory; :attr:`key` (the tensors' data pointers) tells the caller when
+    it must be rebuilt."""
+
+    def __init__(self, items, device):
+        k = _native.kernels()
+        chunk = k("edl_ps_multi_chunk")
+        rows, bstart = [], [0]
+        ptrs = []
+        for t, off, n in items:
+            if off % 4:
+                raise ValueError("MultiCopyPlan: PS offsets must be multiples of 4 elements")
+            if t is None:
+                kind, ptr = 2, 0
+            else:
+                if not t.is_contiguous() or t.numel() != n or t.dtype not in (torch.float32, torch.bfloat16):
+                    raise ValueError("MultiCopyPlan: contiguous fp32 / bf16 tensors of the layout's size")
+                kind, ptr = (1 if t.dtype == torch.bfloat16 else 0), t.data_ptr()
+                if ptr % (8 if kind == 1 else 16):
+                    raise ValueError("MultiCopyPlan: misaligned tensor")
+            ptrs.append(ptr)
+            rows.append([ptr, off, n, kind])
+            bstart.append(bstart[-1] + -(-n // chunk))
+        self.n = len(rows)
+        self.nblocks = bstart[-1]
+        self.table = torch.tensor(rows, dtype=torch.int64).to(device)
+        self.bstart = torch.tensor(bstart, dtype=torch.int64).to(device)
+        self.key = tuple(ptrs)
+
+    def run(self, flat_ptr: int, push: bool, stream=None) -> None:
+        s = stream if stream is not None else torch.cuda.current_stream(self.table.device).cuda_stream
+        _native.kernels().check("edl_ps_multi_copy", self.table.data_ptr(), self.bstart.data_ptr(), self.n,
+                                self.nblocks, flat_ptr, 1 if push else 0, s)

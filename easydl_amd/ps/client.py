@@ -125,6 +125,12 @@ class PSClient:
             time.sleep(0.2)  # PS being replaced: re-resolve and retry
 
     # -- GPU transport ---------------------------------------------------------------
+    # Bulk bytes never cross TCP: per PS, ONE kernel launch moves every parameter
+    # (pull: fp32 shard -> this worker's bf16/fp32 params) or every gradient (push:
+    # -> fp32, written into this worker's inbox in the PS's HBM).  Inboxes are double
+    # buffered: push k writes inbox k % 2, and the PS answers push k only once the
+    # update that read inbox (k - 1) % 2 has finished, so the next push may overwrite
+    # it — the PS never blocks on the update it has just launched.
     def _ipc_map(self, i: int) -> dict:
         m = self._ipc.get(i)
         if m is None or m["sock"] is not self._socks.get(i):
@@ -133,18 +139,36 @@ class PSClient:
             if not h.get("ok"):
                 raise RuntimeError(f"PS {i}: {h.get('error')}")
             d = h["ipc"]
-            m = {"w": import_tensor(d["w"]), "inbox": import_tensor(d["inbox"]), "layout": d["layout"],
-                 "sock": self._socks.get(i)}
+            m = {"w": import_tensor(d["w"]), "inbox": [import_tensor(x) for x in d["inbox"]], "layout": d["layout"],
+                 "sock": self._socks.get(i), "slot": 0, "pull_plan": None, "push_plan": None}
             self._ipc[i] = m
         return m
 
-    def _pull_ipc(self, i: int, params: dict, min_version=None) -> int:
-        from easydl_amd.ops.sparse import pull_cast
-        hdr = {"op": "pull_ipc"}
-        if min_version is not None:
-            hdr["min_version"] = min_version
+    @staticmethod
+    def _plan(m: dict, which: str, tensors: list, device):
+        """Cached MultiCopyPlan for this PS's layout (rebuilt if a tensor moved)."""
+        from easydl_amd.ops.sparse import MultiCopyPlan
+        key = tuple(0 if t is None else t.data_ptr() for t in tensors)
+        plan = m[which]
+        if plan is None or plan.key != key:
+            items = [(t, off, int(torch.Size(shape).numel())) for t, (off, shape) in zip(tensors, m["layout"].values())]
+            try:
+                plan = MultiCopyPlan(items, device)
+            except ValueError:
+                plan = False      # odd layout / dtype: per-tensor copies
+            m[which] = plan
+        return plan or None
+
+    def _pull_launch(self, i: int, params: dict) -> None:
+        """Copy PS i's shard into the parameters on the current stream (one launch)."""
         m = self._ipc_map(i)
-        h, _ = self._call(i, hdr)
+        ts = [params[n].data for n in m["layout"]]
+        dev = ts[0].device
+        plan = self._plan(m, "pull_plan", ts, dev)
+        if plan is not None:
+            plan.run(m["w"].data_ptr(), push=False)
+            return
+        from easydl_amd.ops.sparse import pull_cast
         w = m["w"]
         with torch.no_grad():
             for n, (off, shape) in m["layout"].items():
@@ -152,33 +176,49 @@ class PSClient:
                 k = p.numel()
                 src = w[off:off + k]
                 if p.dtype == torch.bfloat16 and k % 8 == 0 and p.is_contiguous():
-                    pull_cast(src, p.view(-1))   # HIP kernel on this GPU, fp32 read from the PS's HBM
+                    pull_cast(src, p.view(-1))
                 else:
                     p.copy_(src.view(p.shape))
-        torch.cuda.current_stream(next(iter(params.values())).device).synchronize()
-        return h["version"]
 
-    def _push_ipc(self, i: int, params: dict, extra: dict, step: int) -> int:
+    def _push_launch(self, i: int, params: dict) -> int:
+        """Write this worker's gradients of PS i's shard into inbox ``slot``; returns the slot."""
         m = self._ipc_map(i)
-        inbox = m["inbox"]
+        slot = m["slot"]
+        m["slot"] ^= 1
+        inbox = m["inbox"][slot]
+        gs = [params[n].grad for n in m["layout"]]
+        plan = self._plan(m, "push_plan", gs, inbox.device if not gs or gs[0] is None else gs[0].device)
+        if plan is not None:
+            plan.run(inbox.data_ptr(), push=True)
+            return slot
         with torch.no_grad():
-            for n, (off, shape) in m["layout"].items():
-                g = params[n].grad
+            for (n, (off, shape)), g in zip(m["layout"].items(), gs):
                 dst = inbox[off:off + params[n].numel()]
                 if g is None:
                     dst.zero_()
                 else:
-                    dst.copy_(g.reshape(-1))  # peer writes into the PS's HBM
-        torch.cuda.current_stream(next(iter(params.values())).device).synchronize()
-        h, _ = self._call(i, {"op": "push_ipc", "worker": self.worker_id, "step": step}, extra)
+                    dst.copy_(g.reshape(-1))
+        return slot
+
+    def _pull_ipc(self, i: int, params: dict, min_version=None) -> int:
+        hdr = {"op": "pull_ipc"}
+        if min_version is not None:
+            hdr["min_version"] = min_version
+        self._ipc_map(i)
+        h, _ = self._call(i, hdr)
         return h["version"]
 
     def pull(self, model: torch.nn.Module, min_versions=None) -> list[int]:
         params = dict(model.named_parameters())
         if self.transport == "ipc":
+            # control round trips in parallel (version / bounded-staleness wait; the PS
+            # answers once the update of that version has finished writing), then one
+            # copy kernel per shard on this thread's stream (ordered before forward)
             self.versions = list(self._pool.map(
                 lambda i: self._pull_ipc(i, params, None if min_versions is None else min_versions[i]),
                 range(self.num_ps)))
+            for i in range(self.num_ps):
+                self._pull_launch(i, params)
             return self.versions
 
         def one(i):
@@ -195,18 +235,37 @@ class PSClient:
         self.versions = list(self._pool.map(one, range(self.num_ps)))
         return self.versions
 
-    def push(self, model: torch.nn.Module, step: int = 0) -> list[int]:
-        params = dict(model.named_parameters())
+    def _take_sparse(self) -> dict:
         sparse_grads = {}
         for n, m in self.tables.items():
             got = m.take_grads()
             if got is not None:
                 parts, flat = self._split_rows(got[0].cpu())
                 sparse_grads[n] = (parts, flat, got[1].detach().cpu())
+        return sparse_grads
+
+    def push(self, model: torch.nn.Module, step: int = 0, then_pull: bool = False) -> list[int]:
+        """Push this step's gradients to every shard.  ``then_pull`` (GPU transport): the
+        same round trip returns once the shard has applied them, and the fresh
+        parameters are copied right away — push + pull in ONE control message per PS."""
+        params = dict(model.named_parameters())
+        sparse_grads = self._take_sparse()
 
         if self.transport == "ipc":
-            self.versions = list(self._pool.map(
-                lambda i: self._push_ipc(i, params, self._sparse_grads(i, sparse_grads), step), range(self.num_ps)))
+            slots = [self._push_launch(i, params) for i in range(self.num_ps)]
+            dev = next(iter(params.values())).device
+            torch.cuda.current_stream(dev).synchronize()   # inboxes complete before the PS reads them
+
+            def one(i):
+                hdr = {"op": "push_ipc", "worker": self.worker_id, "step": step, "slot": slots[i],
+                       "pull": bool(then_pull)}
+                h, _ = self._call(i, hdr, self._sparse_grads(i, sparse_grads))
+                return h["version"]
+
+            self.versions = list(self._pool.map(one, range(self.num_ps)))
+            if then_pull:
+                for i in range(self.num_ps):
+                    self._pull_launch(i, params)
             return self.versions
 
         def one(i):
@@ -219,6 +278,8 @@ class PSClient:
             return h["version"]
 
         self.versions = list(self._pool.map(one, range(self.num_ps)))
+        if then_pull:
+            self.pull(model)
         return self.versions
 
     def stats(self) -> list[dict]:

@@ -101,7 +101,11 @@ class ParameterServer:
         # row-sparse embedding stripes (easydl_amd/ps/embedding.py), lazily updated
         self.tables = {n: TableShard(n, t["rows"], t["dim"], t.get("init_std", 0.01), index, device, seed)
                        for n, t in (tables or {}).items()}
-        self.inboxes: dict[str, torch.Tensor] = {}   # GPU transport: worker -> gradient inbox in this HBM
+        # GPU transport: worker -> two gradient inboxes in this HBM (double buffered) and the
+        # completion event of the update that last read each one
+        self.inboxes: dict[str, list[torch.Tensor]] = {}
+        self._inbox_ev: dict[str, list] = {}
+        self._apply_ev = None      # completion of the newest update of the shard
         self.sparse_optimizer = sparse_optimizer or ("adam" if optimizer == "adam" else "sgd")
         self.sparse_lr = lr if sparse_lr is None else sparse_lr
         self.optimizer, self.lr, self.betas, self.eps = optimizer, lr, betas, eps
@@ -153,6 +157,10 @@ class ParameterServer:
                 self._apply_table(t, ids, grads, scale)
         self.version += 1
         self.stats["applied"] += 1
+        if st.w.is_cuda:
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(st.device))
+            self._apply_ev = ev
         if self.snapshot is not None and self.version % self.snapshot_every == 0:
             self.snapshot(self)
         self.lock.notify_all()
@@ -172,23 +180,27 @@ class ParameterServer:
             else:
                 t.pending.append((ids.to(t.w.device), g.to(t.w.device, torch.float32)))
 
-    def _push(self, worker: str, grads: dict[str, torch.Tensor], inbox: torch.Tensor | None = None) -> int:
+    def _push(self, worker: str, grads: dict[str, torch.Tensor], inbox: torch.Tensor | None = None,
+              slot: int = 0) -> int:
         with self.lock:
             st = self.state
             # sparse-table rows are updated below, before _apply: they are part of the
             # snapshot too, so the fence must come first
             self._fence_snapshot()
             if inbox is not None and self.mode == "async":
-                # GPU transport: the inbox IS the gradient of this update (no accumulate pass)
+                # GPU transport: the inbox IS the gradient of this update (no accumulate pass);
+                # its release is an event, waited for only when the worker wants this slot back
                 self._apply_sparse(grads, async_mode=True)
                 self.stats["pushes"] += 1
                 self.stats["workers"].add(worker)
                 self._apply(1.0, grad=inbox)
-                torch.cuda.current_stream(st.device).synchronize()  # inbox free for the next push
+                self._inbox_ev[worker][slot] = self._apply_ev
                 return self.version
             if inbox is not None:
                 st.g.add_(inbox)
-                torch.cuda.current_stream(st.device).synchronize()
+                ev = torch.cuda.Event()
+                ev.record(torch.cuda.current_stream(st.device))
+                self._inbox_ev[worker][slot] = ev
             for n, g in grads.items():
                 if n.startswith("sparse/"):
                     continue
@@ -249,8 +261,9 @@ class ParameterServer:
                     with self.lock:
                         wid = hdr.get("worker", "?")
                         if wid not in self.inboxes:
-                            self.inboxes[wid] = torch.zeros_like(st.w)
-                        desc = {"w": export_tensor(st.w), "inbox": export_tensor(self.inboxes[wid]),
+                            self.inboxes[wid] = [torch.zeros_like(st.w), torch.zeros_like(st.w)]
+                            self._inbox_ev[wid] = [None, None]
+                        desc = {"w": export_tensor(st.w), "inbox": [export_tensor(x) for x in self.inboxes[wid]],
                                 "layout": {n: [st.offsets[n], list(st.shapes[n])] for n in st.names}}
                     send_msg(conn, {"ok": True, "ipc": desc, "version": self.version})
                 elif op == "pull_ipc":
@@ -260,10 +273,21 @@ class ParameterServer:
                         while self.version < minv and time.monotonic() < t_end:
                             self.lock.wait(timeout=0.05)
                         self.stats["pulls"] += 1
-                        ver = self.version
+                        ver, ev = self.version, self._apply_ev
+                    if ev is not None:
+                        ev.synchronize()   # the worker reads the shard next: that version must be written
                     send_msg(conn, {"ok": True, "version": ver})
                 elif op == "push_ipc":
-                    ver = self._push(hdr.get("worker", "?"), tensors, inbox=self.inboxes[hdr["worker"]])
+                    wid, slot = hdr["worker"], int(hdr.get("slot", 0))
+                    ver = self._push(wid, tensors, inbox=self.inboxes[wid][slot], slot=slot)
+                    with self.lock:
+                        other = self._inbox_ev[wid][1 - slot]   # read by the previous push's update
+                        mine = self._apply_ev if hdr.get("pull") else None
+                    # outside the lock: other workers' pushes keep flowing meanwhile
+                    if other is not None:
+                        other.synchronize()
+                    if mine is not None:
+                        mine.synchronize()   # push + pull in one message: the update is written
                     send_msg(conn, {"ok": True, "version": ver})
                 elif op == "push":
                     ver = self._push(hdr.get("worker", "?"), tensors)

@@ -93,6 +93,10 @@ class PSWorker:
         self.rdzv.join()
         disp = ShardDispatcher(self.kv, len(data), shard_size, epochs)
         self.kv.set("data/config", json.dumps({"n": len(data), "shard_size": shard_size, "epochs": epochs}))
+        # GPU transport: the push of step k and the pull for step k+1 share one control
+        # message per PS (the PS answers once it has applied the push); the first step pulls
+        fused = self.client.transport == "ipc"
+        need_pull = True
         try:
             while True:
                 shard = disp.claim(self.ctx.node_id)
@@ -102,7 +106,8 @@ class PSWorker:
                 for b0 in range(lo, hi, batch_size):
                     self.fault.maybe_inject("step_start", self.steps, trainer=None)
                     t0 = time.perf_counter()
-                    self.client.pull(self.model)
+                    if need_pull:
+                        self.client.pull(self.model)
                     t1 = time.perf_counter()
                     self.model.zero_grad(set_to_none=False)
                     loss = loss_fn(self.model, data.batch(range(b0, min(hi, b0 + batch_size)), self.device))
@@ -110,7 +115,8 @@ class PSWorker:
                     if self.device.type == "cuda":
                         torch.cuda.current_stream(self.device).synchronize()
                     t2 = time.perf_counter()
-                    self.client.push(self.model, self.steps)
+                    self.client.push(self.model, self.steps, then_pull=fused)
+                    need_pull = not fused
                     t3 = time.perf_counter()
                     self.steps += 1
                     self._phase = [a + b for a, b in zip(self._phase, (t1 - t0, t2 - t1, t3 - t2))]

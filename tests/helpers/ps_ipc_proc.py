@@ -31,12 +31,13 @@ elif role == "worker":
     c = PSClient(1, lambda i: ("127.0.0.1", port), f"w{wid}", transport="ipc")
     c.bind(m)
     for step in range(steps):
-        c.pull(m)
+        if step == 0 or wid % 2:   # odd workers: separate pull; even: push + pull in one message
+            c.pull(m)
         m.zero_grad()
         b0 = (step * 2 + wid) * 32 % 5000
         x, y = data.batch(range(b0, b0 + 32), "cuda")
         m(x.bfloat16(), y).backward()
-        c.push(m, step)
+        c.push(m, step, then_pull=(wid % 2 == 0))
     print(json.dumps({"wid": wid, "versions": c.versions}))
 else:  # check: IPC pull (bf16 via the HIP kernel) == TCP pull (fp32 -> bf16) bit for bit
     port = int(sys.argv[2])

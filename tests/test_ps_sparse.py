@@ -241,3 +241,32 @@ def test_ps_sparse_push_during_inflight_snapshot(cuda):
         for f in os.listdir("/dev/shm"):
             if f.startswith("edl-snapsp-ps"):
                 os.unlink("/dev/shm/" + f)
+
+
+@pytest.mark.gpu
+def test_multi_tensor_push_pull_kernel(cuda):
+    """edl_ps_multi_copy: one launch pushes scattered bf16 / fp32 gradients (and zeros
+    for a missing one) into a flat fp32 buffer, and pulls it back with the cast."""
+    from easydl_amd.ops.sparse import MultiCopyPlan
+    torch.manual_seed(0)
+    sizes = [1, 3, 4, 7, 1000, 4096 * 8 + 5, 65536 * 3 + 2]
+    dts = [torch.bfloat16, torch.float32, torch.bfloat16, torch.float32, torch.bfloat16, torch.bfloat16,
+           torch.float32]
+    ts = [torch.randn(n, device=cuda).to(dt) for n, dt in zip(sizes, dts)]
+    offs, o = [], 0
+    for n in sizes + [16]:
+        offs.append(o)
+        o += (n + 3) // 4 * 4
+    flat = torch.full((o,), 7.0, device=cuda)
+    items = [(t, off, t.numel()) for t, off in zip(ts, offs)] + [(None, offs[-1], 16)]
+    MultiCopyPlan(items, cuda).run(flat.data_ptr(), push=True)
+    torch.cuda.synchronize()
+    for t, off in zip(ts, offs):
+        assert torch.equal(flat[off:off + t.numel()], t.float())
+    assert torch.equal(flat[offs[-1]:offs[-1] + 16], torch.zeros(16, device=cuda))
+    flat2 = torch.randn(o, device=cuda)
+    outs = [torch.empty_like(t) for t in ts]
+    MultiCopyPlan([(t, off, t.numel()) for t, off in zip(outs, offs)], cuda).run(flat2.data_ptr(), push=False)
+    torch.cuda.synchronize()
+    for t, off in zip(outs, offs):
+        assert torch.equal(t, flat2[off:off + t.numel()].to(t.dtype))   # RNE cast, like .to()
