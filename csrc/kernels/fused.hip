@@ -218,6 +218,90 @@ __global__ __launch_bounds__(256) void xent_fwd_bwd_kernel(bf16_t* __restrict__ 
   }
 }
 
+// Vocab-parallel cross-entropy (tensor parallelism, easydl_amd/parallel/tp.py): this
+// rank holds columns [vstart, vstart + V) of every row.
+//   stats mode: st[row] = (local max m, local sum exp(x - m), logit of the label if
+//     it falls in this shard else 0) -> the caller combines ranks with one MAX and
+//     one SUM all-reduce of [rows] / [rows, 2] fp32 (never the logits);
+//   grad mode: with the global (M, S) in gs[row] = (M, S), overwrite the logits in
+//     place with (exp(x - M) / S - onehot) * (*gscale); ignored rows -> 0.
+template <bool GRAD>
+__global__ __launch_bounds__(256) void xent_vp_kernel(bf16_t* __restrict__ logits, const int64_t* __restrict__ labels,
+                                                      float* __restrict__ st, int V, int64_t vstart,
+                                                      int64_t ignore_index, const float* __restrict__ gscale) {
+  const int64_t row = blockIdx.x;
+  bf16_t* lr = logits + row * (int64_t)V;
+  const int64_t lab = labels[row];
+  const int64_t loc = lab - vstart;
+  const bool ignored = lab == ignore_index;
+  const bool here = !ignored && loc >= 0 && loc < V;
+  const int nchunk = V >> 3;
+  if (GRAD) {
+    const float M = st[2 * row], S = st[2 * row + 1];
+    const float g = gscale ? *gscale : 1.f;
+    const float inv = g / S;
+    u32x4* lw = reinterpret_cast<u32x4*>(lr);
+    for (int c = threadIdx.x; c < nchunk; c += blockDim.x) {
+      float f[8];
+      unpack8(lw[c], f);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        float p = ignored ? 0.f : __expf(f[i] - M) * inv;
+        if (here && (int64_t)(c * 8 + i) == loc) p -= g;
+        f[i] = p;
+      }
+      lw[c] = pack8(f);
+    }
+    for (int c = (nchunk << 3) + threadIdx.x; c < V; c += blockDim.x) {
+      float p = ignored ? 0.f : __expf(bf2f(lr[c]) - M) * inv;
+      if (here && (int64_t)c == loc) p -= g;
+      lr[c] = f2bf(p);
+    }
+    return;
+  }
+  __shared__ float sm[4], ss[4];
+  float m = -INFINITY, s = 0.f;
+  const u32x4* lv = reinterpret_cast<const u32x4*>(lr);
+  for (int c = threadIdx.x; c < nchunk; c += blockDim.x) {
+    float f[8];
+    unpack8(lv[c], f);
+    float cm = f[0];
+#pragma unroll
+    for (int i = 1; i < 8; ++i) cm = fmaxf(cm, f[i]);
+    const float nm = fmaxf(m, cm);
+    float acc = s * __expf(m - nm);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc += __expf(f[i] - nm);
+    m = nm;
+    s = acc;
+  }
+  for (int c = (nchunk << 3) + threadIdx.x; c < V; c += blockDim.x) {
+    const float f = bf2f(lr[c]);
+    const float nm = fmaxf(m, f);
+    s = s * __expf(m - nm) + __expf(f - nm);
+    m = nm;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const float om = __shfl_xor(m, off, 64), os = __shfl_xor(s, off, 64);
+    const float nm = fmaxf(m, om);
+    s = (m == -INFINITY ? 0.f : s * __expf(m - nm)) + (om == -INFINITY ? 0.f : os * __expf(om - nm));
+    m = nm;
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  if (lane == 0) { sm[wid] = m; ss[wid] = s; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float M = sm[0];
+    for (int i = 1; i < nw; ++i) M = fmaxf(M, sm[i]);
+    float S = 0.f;
+    for (int i = 0; i < nw; ++i) S += ss[i] * __expf(sm[i] - M);
+    st[3 * row] = M;
+    st[3 * row + 1] = S;
+    st[3 * row + 2] = here ? bf2f(lr[loc]) : 0.f;
+  }
+}
+
 // y = x * s[0] in place over bf16 (s is a device scalar: no host sync).
 __global__ __launch_bounds__(256) void scale_bf16_kernel(bf16_t* __restrict__ x, int64_t n8,
                                                          const float* __restrict__ s, float hs) {
@@ -775,6 +859,21 @@ int edl_xent_fwd_bwd(void* logits, const int64_t* labels, float* loss, int64_t r
   if (rows <= 0) return 0;
   xent_fwd_bwd_kernel<<<(unsigned)rows, 256, 0, s>>>((bf16_t*)logits, labels, loss, V, ignore_index, write_grad,
                                                      gscale);
+  EDL_LAUNCH_CHECK();
+  return 0;
+}
+
+// vocab-parallel cross-entropy: grad = 0 -> st[rows, 3] = (local max, local sum, local target
+// logit); grad = 1 -> logits <- (softmax(global M, S from st[rows, 2]) - onehot) * (*gscale)
+int edl_xent_vp(void* logits, const int64_t* labels, float* st, int64_t rows, int V, int64_t vstart,
+                int64_t ignore_index, int grad, const float* gscale, hipStream_t s) {
+  if (rows <= 0) return 0;
+  if (V % 8) return (int)hipErrorInvalidValue;
+  if (grad)
+    xent_vp_kernel<true><<<(unsigned)rows, 256, 0, s>>>((bf16_t*)logits, labels, st, V, vstart, ignore_index, gscale);
+  else
+    xent_vp_kernel<false><<<(unsigned)rows, 256, 0, s>>>((bf16_t*)logits, labels, st, V, vstart, ignore_index,
+                                                         gscale);
   EDL_LAUNCH_CHECK();
   return 0;
 }

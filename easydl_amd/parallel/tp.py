@@ -170,7 +170,54 @@ class _VocabParallelXent(torch.autograd.Function):
         return (grad * (dl / n)).to(ctx.dtype), None, None, None, None
 
 
+class _VocabParallelXentHip(torch.autograd.Function):
+    """GPU form (csrc/kernels/fused.hip ``edl_xent_vp``): one pass over the bf16 local
+    logits gives per-row (max, sum-exp, target logit); the ranks combine them with one
+    MAX all-reduce of [T] fp32 and one SUM all-reduce of [T, 2] fp32; the backward
+    rewrites the logits in place with their gradient.  No fp32 [T, V/tp] tensor is
+    ever materialised (the eager form held x, e and p in fp32)."""
+
+    @staticmethod
+    def forward(ctx, logits, labels, vstart, g, ignore_index):
+        from easydl_amd import _native
+        k = _native.kernels()
+        logits = logits.contiguous()
+        rows, V = logits.shape
+        labels = labels.contiguous().to(torch.int64)
+        st = torch.empty(rows, 3, dtype=torch.float32, device=logits.device)
+        k.check("edl_xent_vp", logits.data_ptr(), labels.data_ptr(), st.data_ptr(), rows, V, vstart, ignore_index,
+                0, None, _native.stream_of(logits))
+        m_loc = st[:, 0]
+        M = g.all_reduce_max(m_loc.clone())
+        sums = torch.stack([st[:, 1] * torch.exp(m_loc - M), st[:, 2]], 1)
+        sums = g.all_reduce(sums)
+        S, tgt = sums[:, 0], sums[:, 1]
+        valid = labels != ignore_index
+        n = valid.sum().clamp_min(1).float()
+        loss = torch.where(valid, torch.log(S) + M - tgt, torch.zeros_like(M)).sum() / n
+        if ctx.needs_input_grad[0]:
+            ctx.save_for_backward(logits, labels, torch.stack([M, S], 1).contiguous(), n)
+            ctx.vstart, ctx.ignore_index = vstart, ignore_index
+        return loss
+
+    @staticmethod
+    def backward(ctx, dl):
+        from easydl_amd import _native
+        if getattr(ctx, "consumed", False):
+            raise RuntimeError("vocab-parallel cross_entropy: backward ran twice (logits consumed in place)")
+        ctx.consumed = True
+        logits, labels, ms, n = ctx.saved_tensors
+        rows, V = logits.shape
+        scale = (dl.float() / n).reshape(1).contiguous()
+        _native.kernels().check("edl_xent_vp", logits.data_ptr(), labels.data_ptr(), ms.data_ptr(), rows, V,
+                                ctx.vstart, ctx.ignore_index, 1, scale.data_ptr(), _native.stream_of(logits))
+        return logits, None, None, None, None
+
+
 def vocab_parallel_cross_entropy(logits_local, labels, vstart: int, g: TPGroup, ignore_index: int = -100):
+    if logits_local.is_cuda and logits_local.dtype == torch.bfloat16 and logits_local.shape[-1] % 8 == 0:
+        return _VocabParallelXentHip.apply(logits_local.reshape(-1, logits_local.shape[-1]), labels.reshape(-1),
+                                           vstart, g, ignore_index)
     return _VocabParallelXent.apply(logits_local, labels.reshape(-1), vstart, g, ignore_index)
 
 

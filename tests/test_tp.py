@@ -25,3 +25,68 @@ def test_tp2_matches_dense(tmp_path, sp):
         res = json.load(open(tmp_path / f"r.{r}"))
         assert abs(res["loss_d"] - res["loss_t"]) < 1e-5, res
         assert res["grad_rel_err"] < 1e-4, res
+
+
+class _ThreadGroup:
+    """TP group of `size` threads in ONE process (one GPU): all_reduce / all_reduce_max
+    meet at a barrier and combine every thread's tensor."""
+
+    def __init__(self, size, rank, shared):
+        self.size, self.rank, self.shared = size, rank, shared
+
+    def _combine(self, x, op):
+        import threading  # noqa: F401
+        sh = self.shared
+        sh["bufs"][self.rank] = x
+        sh["barrier"].wait()
+        out = sh["bufs"][0].clone()
+        for t in sh["bufs"][1:]:
+            out = torch.maximum(out, t) if op == "max" else out + t
+        sh["barrier"].wait()
+        return out
+
+    def all_reduce(self, x):
+        return self._combine(x.contiguous(), "sum")
+
+    def all_reduce_max(self, x):
+        return self._combine(x.contiguous(), "max")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tp", [2, 4])
+def test_vocab_parallel_xent_kernel_matches_dense(cuda, tp):
+    """edl_xent_vp + (MAX, SUM) exchange == the dense fp32 cross entropy: loss and the
+    in-place logits gradient of every vocab shard (incl. ignored rows)."""
+    import threading
+
+    import torch.nn.functional as F
+
+    from easydl_amd.parallel.tp import vocab_parallel_cross_entropy
+    torch.manual_seed(0)
+    T, V = 96, 1024
+    full = (torch.randn(T, V, device=cuda) * 3).to(torch.bfloat16)
+    labels = torch.randint(0, V, (T,), device=cuda)
+    labels[::7] = -100
+    ref_in = full.float().requires_grad_()
+    ref = F.cross_entropy(ref_in, labels, ignore_index=-100)
+    ref.backward()
+    shared = {"bufs": [None] * tp, "barrier": threading.Barrier(tp)}
+    out, grads = [None] * tp, [None] * tp
+    vs = V // tp
+
+    def rank(r):
+        torch.cuda.set_device(cuda)
+        x = full[:, r * vs:(r + 1) * vs].clone().requires_grad_()
+        loss = vocab_parallel_cross_entropy(x, labels, r * vs, _ThreadGroup(tp, r, shared))
+        loss.backward()
+        out[r], grads[r] = loss.detach(), x.grad
+
+    ts = [threading.Thread(target=rank, args=(r,)) for r in range(tp)]
+    [t.start() for t in ts]
+    [t.join(60) for t in ts]
+    torch.cuda.synchronize()
+    for r in range(tp):
+        assert abs(out[r].item() - ref.item()) < 1e-3 * max(1.0, abs(ref.item())), (out[r].item(), ref.item())
+        g = grads[r].float()
+        gr = ref_in.grad[:, r * vs:(r + 1) * vs]
+        assert (g - gr).abs().max().item() < 2e-3, (g - gr).abs().max().item()
