@@ -60,6 +60,10 @@ class ElasticTrainer:
                  rdzv_config: RendezvousConfig | None = None, checkpoint=None, log_every: int = 0,
                  store=None, tp: int | None = None):
         self.ctx = ctx or TrainerContext.from_env()
+        hang = float(os.environ.get("EDL_HANG_DUMP_S", 0) or 0)
+        if hang > 0:   # diagnostics: every thread's Python stack to stderr every `hang` seconds
+            import faulthandler
+            faulthandler.dump_traceback_later(hang, repeat=True)
         if device is None:
             if torch.cuda.is_available():
                 device = torch.device("cuda", self.ctx.gpu or 0)
@@ -265,7 +269,8 @@ class ElasticTrainer:
                 self.events.emit("epoch_skipped", epoch=self.comm.epoch, during="state_sync")
                 self.comm.abort()
                 continue
-            self.ddp.set_comm(self.dp_comm)
+            self.events.emit("state_transferred", epoch=self.comm.epoch, step=self.step)
+            self.ddp.set_comm(self.dp_comm)   # binds the epoch's comm (registers gradient buffers)
             self.events.emit("state_synced", epoch=self.comm.epoch, step=self.step)
             return
 
