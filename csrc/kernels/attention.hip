@@ -24,7 +24,6 @@
 //   * dQ kernel: the forward's structure with dP^T = V dO^T and dQ^T += K^T dS^T.
 // Capability source: Llama-3 training workloads (BASELINE.json configs 3/5).
 #include <cstdlib>
-#include <string>
 #include <type_traits>
 
 #include "common.h"
@@ -957,30 +956,17 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dkdv_kernel(
 // ~200 v_accvgpr moves per slice.  hipcc pads nothing inside asm: the first MFMA of a
 // chain takes C = 0 (no VALU-written C), chained MFMAs read C = their own D (0 wait
 // states), and mfma_d_fence pads the MFMA D -> VALU read once after both chains.
-// BI = true: the same MFMAs through the builtin, with this file compiled under
-// -mllvm --amdgpu-mfma-vgpr-form (easydl_amd/_build.py): results stay in VGPRs, and the
-// compiler sees the MFMAs, so it inserts the hazard waits itself and may schedule LDS
-// reads and VALU work between them (inline asm is a scheduling barrier for both).
-template <bool BI>
 __device__ __forceinline__ void mfma_v_first(f32x16& d, const bf16x8& a, const bf16x8& b) {
-  if constexpr (BI)
-    d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, f32x16{}, 0, 0, 0);
-  else
-    asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(d) : "v"(a), "v"(b));
+  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(d) : "v"(a), "v"(b));
 }
-template <bool BI>
 __device__ __forceinline__ void mfma_v(f32x16& d, const bf16x8& a, const bf16x8& b) {
-  if constexpr (BI)
-    d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, d, 0, 0, 0);
-  else
-    asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(d) : "v"(a), "v"(b));
+  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(d) : "v"(a), "v"(b));
 }
-template <bool BI>
 __device__ __forceinline__ void mfma_d_fence(f32x16 (&x)[2], f32x16 (&y)[2]) {
-  if constexpr (!BI) asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 4" : "+v"(x[0]), "+v"(x[1]), "+v"(y[0]), "+v"(y[1]));
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 4" : "+v"(x[0]), "+v"(x[1]), "+v"(y[0]), "+v"(y[1]));
 }
 
-template <bool MASK, bool CAUSAL, int D, bool BI>
+template <bool MASK, bool CAUSAL, int D>
 __device__ __forceinline__ void dkdv64_slice(const char* Qs, const char* Ds, const float* NL,
                                              const float* DL, int rb, const bf16x8 (&kf)[2][D / 16],
                                              const char* Vw, f32x16 (&dka)[2][D / 32], f32x16 (&dva)[2][D / 32],
@@ -997,11 +983,11 @@ __device__ __forceinline__ void dkdv64_slice(const char* Qs, const char* Ds, con
   for (int s = 0; s < D / 16; ++s) {
     const bf16x8 a = row_read<D>(Qs, rb + l31, s, h);
     if (s == 0) {
-      mfma_v_first<BI>(sa[0], a, kf[0][s]);
-      mfma_v_first<BI>(sa[1], a, kf[1][s]);
+      mfma_v_first(sa[0], a, kf[0][s]);
+      mfma_v_first(sa[1], a, kf[1][s]);
     } else {
-      mfma_v<BI>(sa[0], a, kf[0][s]);
-      mfma_v<BI>(sa[1], a, kf[1][s]);
+      mfma_v(sa[0], a, kf[0][s]);
+      mfma_v(sa[1], a, kf[1][s]);
     }
   }
 #pragma unroll
@@ -1010,14 +996,14 @@ __device__ __forceinline__ void dkdv64_slice(const char* Qs, const char* Ds, con
     const bf16x8 v0 = *(lds_bf16x8*)(Vl + swzd<D>(l31, 2 * s + h));
     const bf16x8 v1 = *(lds_bf16x8*)(Vl + swzd<D>(32 + l31, 2 * s + h));
     if (s == 0) {
-      mfma_v_first<BI>(dp[0], a, v0);
-      mfma_v_first<BI>(dp[1], a, v1);
+      mfma_v_first(dp[0], a, v0);
+      mfma_v_first(dp[1], a, v1);
     } else {
-      mfma_v<BI>(dp[0], a, v0);
-      mfma_v<BI>(dp[1], a, v1);
+      mfma_v(dp[0], a, v0);
+      mfma_v(dp[1], a, v1);
     }
   }
-  mfma_d_fence<BI>(sa, dp);
+  mfma_d_fence(sa, dp);
   // per-row softmax terms are read from LDS right where they are used (no 32-VGPR arrays)
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
@@ -1093,7 +1079,7 @@ __device__ __forceinline__ void store_accT_f32(float* rowp, const f32x16 (&acc)[
 // fewer than ~2 workgroups per CU the GQA group's query heads are split over
 // `gsplit` workgroups that write fp32 partials to `ws`, summed by
 // attn_dkdv_reduce_kernel.
-template <bool CAUSAL, int D, bool BI = false>
+template <bool CAUSAL, int D>
 __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv64_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
     const bf16_t* __restrict__ dout, const float* __restrict__ lse, const float* __restrict__ delta,
@@ -1175,7 +1161,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv64_kernel(
         for (int sub = 0; sub < QT / 32; ++sub) {
           const int qs0 = q0 + 32 * sub;
           if (CAUSAL && qs0 + 31 < key0) continue;  // wave-uniform: every key of the wave is after every query
-          dkdv64_slice<MASK, CAUSAL, D, BI>(Qs, Ds, NL, NL + QT, 32 * sub, kf, Vw, dka, dva, qs0, key0, S, scale_log2,
+          dkdv64_slice<MASK, CAUSAL, D>(Qs, Ds, NL, NL + QT, 32 * sub, kf, Vw, dka, dva, qs0, key0, S, scale_log2,
                                         lane);
         }
         wait_vm();
@@ -1359,7 +1345,6 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(
 
 }  // namespace
 
-#ifndef EDL_ATTN_VGPR_TU
 // XCD-aware work decode (grid_decode) for the forward and dQ kernels whenever every XCD
 // can take whole K/V groups: -21 % kernel time each at B 2, S 8192, H 32, KV 8
 // (profiles/r02_attn_xcd_ab.txt; the dK/dV kernel measured no gain from the same
@@ -1401,11 +1386,6 @@ static int dkdv_keys_per_wave() {
   return kpw;
 }
 
-extern "C" int edl_attn_dkdv64_vgpr(const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* dout,
-                                    const float* lse, const float* delta, void* dk, void* dv, float* ws, unsigned gx,
-                                    unsigned gy, unsigned gz, int S, int H, int KV, int gsplit, float sl2, float scale,
-                                    int64_t dkvs, int variant, hipStream_t s);
-
 // delta: fp32 [2,B,H,S] scratch filled here (delta, -lse*log2(e)).
 template <int D>
 static int attn_bwd_impl(const void* q, const void* k, const void* v, const void* o, const void* dout,
@@ -1431,20 +1411,8 @@ static int attn_bwd_impl(const void* q, const void* k, const void* v, const void
   dim3 gkv64;
   const int gsplit = dkdv64_plan(B, S, H, KV, causal, &gkv64);
   const bf16_t *bq = (const bf16_t*)q, *bk = (const bf16_t*)k, *bv = (const bf16_t*)v, *bdo = (const bf16_t*)dout;
-  // dK/dV variants built in attention_dkdv_vgpr.hip (MFMA results in VGPRs):
-  // EDL_ATTN_DKDV_MFMA=builtin (builtin MFMAs, compiler-scheduled) | asmvgpr (this kernel)
-  const int vgpr_variant = [] {   // read per call: A/B scripts switch it within one process
-    const char* e = getenv("EDL_ATTN_DKDV_MFMA");
-    if (!e) return -1;
-    const std::string v(e);
-    return v == "builtin" ? 1 : v == "asmvgpr" ? 0 : -1;
-  }();
   if (keys_per_wave == 64) {
-    if (causal && vgpr_variant >= 0 && D == 128) {
-      const int rc = edl_attn_dkdv64_vgpr(bq, bk, bv, bdo, lse, delta, dk, dv, ws, gkv64.x, gkv64.y, gkv64.z, S, H,
-                                          KV, gsplit, sl2, scale, dkvs, vgpr_variant, s);
-      if (rc) return rc;
-    } else if (causal)
+    if (causal)
       attn_bwd_dkdv64_kernel<true, D><<<gkv64, 256, 0, s>>>(bq, bk, bv, bdo, lse, delta, (bf16_t*)dk, (bf16_t*)dv,
                                                             ws, S, H, KV, gsplit, sl2, scale, dkvs);
     else
@@ -1537,4 +1505,3 @@ int edl_attn_bwd(const void* q, const void* k, const void* v, const void* o, con
 }
 
 }  // extern "C"
-#endif  // EDL_ATTN_VGPR_TU

@@ -61,13 +61,9 @@ def _check_resolves(lib: str) -> None:
         raise RuntimeError(f"{os.path.basename(lib)}: undefined kernel launch stubs: {missing}")
 
 
-# per-source extra hipcc flags (-fno-slp-vectorize on attention.hip measured the dK/dV
-# kernel 12 % slower in the bench, profiles/r02_bench_kernel_stats_*)
-_EXTRA_FLAGS: dict[str, list[str]] = {
-    # dK/dV kernel variants with MFMA results in VGPRs (EDL_ATTN_DKDV_MFMA=builtin|asmvgpr);
-    # a translation unit of their own: the flag crashes LLVM on other attention.hip kernels
-    "attention_dkdv_vgpr.hip": ["-mllvm", "--amdgpu-mfma-vgpr-form"],
-}
+# per-source extra hipcc flags (none at present: -fno-slp-vectorize on attention.hip
+# measured the dK/dV kernel 12 % slower in the bench, profiles/r02_bench_kernel_stats_*)
+_EXTRA_FLAGS: dict[str, list[str]] = {}
 
 
 def build_kernels(force: bool = False, verbose: bool = False) -> str:
@@ -80,8 +76,7 @@ def build_kernels(force: bool = False, verbose: bool = False) -> str:
         for s in srcs:
             o = os.path.join(LIBDIR, "obj", os.path.basename(s) + ".o")
             os.makedirs(os.path.dirname(o), exist_ok=True)
-            # a .hip may #include another one (attention_dkdv_vgpr.hip includes attention.hip)
-            if force or _stale(o, [s] + hdrs + srcs):
+            if force or _stale(o, [s] + hdrs):
                 cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-c", s, "-o", o,
                        "-Wno-unused-result"] + _EXTRA_FLAGS.get(os.path.basename(s), [])
                 if verbose:
