@@ -385,6 +385,56 @@ __global__ __launch_bounds__(XG_THREADS) void xg_pull(XgSync S, XgBufs G, int64_
   xg_barrier<NR>(S, 2);
 }
 
+// Staged multi-source pull for tensors too large to map (one window per launch): the
+// k-th holder stages slice k of the window into its workspace buffer, every receiver
+// copies slice k from holder k's workspace.  Round parity protects the buffers as in
+// the staged all-reduce.  src: this rank's tensor (holders), dst: the same tensor
+// (receivers); win_off / win_len in 16-byte vectors.
+template <int NR>
+__global__ __launch_bounds__(XG_THREADS) void xg_pull_staged(XgSync S, XgBufs W, const u32x4* __restrict__ src,
+                                                             u32x4* __restrict__ dst, int64_t win_off,
+                                                             int64_t win_len, uint32_t holder_mask) {
+  int hs[XG_MAX_RANKS];
+  int nh = 0, me = -1;
+#pragma unroll
+  for (int p = 0; p < NR; ++p)
+    if ((holder_mask >> p) & 1u) {
+      if (p == S.rank) me = nh;
+      hs[nh++] = p;
+    }
+  const int64_t slice = (win_len + nh - 1) / nh;
+  if (me >= 0) {   // holder: stage my slice of the window
+    const int64_t s0 = (int64_t)me * slice, n = min(slice, win_len - s0);
+    int64_t lo, hi;
+    block_range(n, lo, hi);
+    copy_range(src + win_off + s0, reinterpret_cast<u32x4*>(W.p[S.rank]), lo, hi);
+  }
+  if (!xg_barrier<NR>(S, 0)) return;
+  if (me < 0) {    // receiver: slice k from holder k, workgroups dealt over the holders
+    const int k = blockIdx.x % nh;
+    const int nb = (gridDim.x - k + nh - 1) / nh, bi = blockIdx.x / nh;
+    const int64_t s0 = (int64_t)k * slice, n = max<int64_t>(0, min(slice, win_len - s0));
+    const int64_t per = (n + nb - 1) / nb;
+    const int64_t lo = bi * per, hi = min(n, lo + per);
+    const u32x4* from = reinterpret_cast<const u32x4*>(W.p[hs[k]]);
+    u32x4* to = dst + win_off + s0;
+    constexpr int U = 8;
+    for (int64_t i0 = lo + threadIdx.x; i0 < hi; i0 += (int64_t)U * XG_THREADS) {
+      u32x4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t i = i0 + (int64_t)u * XG_THREADS;
+        if (i < hi) v[u] = from[i];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t i = i0 + (int64_t)u * XG_THREADS;
+        if (i < hi) to[i] = v[u];
+      }
+    }
+  }
+}
+
 // Flag-only barrier across ranks (e.g. before buffers are re-registered or freed).
 template <int NR>
 __global__ __launch_bounds__(64) void xg_barrier_kernel(XgSync S) {
@@ -511,6 +561,23 @@ int edl_xgmi_pull(void* const* bufs, void* const* flags, int nranks, int rank, i
   XgBufs G{};
   for (int r = 0; r < nranks; ++r) G.p[r] = (char*)bufs[r];
   XG_DISPATCH_NR(nranks, (xg_pull<NR><<<blocks, XG_THREADS, 0, s>>>(S, G, nbytes / 16, holder_mask)));
+  EDL_LAUNCH_CHECK();
+  return 0;
+}
+
+// Staged multi-source pull of one window (see xg_pull_staged); the holders' slices of
+// the window (win_bytes / #holders each) must fit one workspace buffer.
+int edl_xgmi_pull_staged(void* const* data, void* const* flags, int nranks, int rank, const void* src, void* dst,
+                         int64_t win_off_bytes, int64_t win_bytes, uint32_t holder_mask, uint32_t round, int blocks,
+                         const int* abort_word, double timeout_s, int* status, hipStream_t s) {
+  if (bad_common(nranks, rank, blocks) || (win_off_bytes & 15) || (win_bytes & 15) || holder_mask == 0 ||
+      (holder_mask >> nranks))
+    return (int)hipErrorInvalidValue;
+  const XgSync S = make_sync(flags, nranks, rank, round, abort_word, timeout_s, status);
+  const XgBufs W = parity_bufs(data, nranks, round & 1);
+  XG_DISPATCH_NR(nranks, (xg_pull_staged<NR><<<blocks, XG_THREADS, 0, s>>>(S, W, (const u32x4*)src, (u32x4*)dst,
+                                                                            win_off_bytes / 16, win_bytes / 16,
+                                                                            holder_mask)));
   EDL_LAUNCH_CHECK();
   return 0;
 }

@@ -85,6 +85,9 @@ _KERNEL_SIGS = {
     "edl_xgmi_barrier": [ctypes.POINTER(c_void_p), c_int, c_int, ctypes.c_uint32, c_void_p, ctypes.c_double, c_void_p,
                          c_void_p],
     "edl_xgmi_wallclock_hz": (c_i64, []),
+    "edl_xgmi_pull_staged": [ctypes.POINTER(c_void_p), ctypes.POINTER(c_void_p), c_int, c_int, c_void_p, c_void_p,
+                             c_i64, c_i64, ctypes.c_uint32, ctypes.c_uint32, c_int, c_void_p, ctypes.c_double, c_void_p,
+                             c_void_p],
     "edl_xgmi_pull": [ctypes.POINTER(c_void_p), ctypes.POINTER(c_void_p), c_int, c_int, c_i64, ctypes.c_uint32,
                       ctypes.c_uint32, c_int, c_void_p, ctypes.c_double, c_void_p, c_void_p],
     "edl_xgmi_collective": [ctypes.POINTER(c_void_p), ctypes.POINTER(c_void_p), c_int, c_int, c_void_p, c_void_p,

@@ -72,7 +72,8 @@ class Communicator:
         # default "auto": at world > 1 the hand-written xGMI engine is measured against
         # RCCL at the start of every epoch and kept for the message sizes where it wins
         data_backend = data_backend or os.environ.get("EDL_COMM", "auto")
-        self.xgmi_min_bytes = 0      # all-reduces at least this large go to the engine
+        self.xgmi_min_bytes = 0         # all-reduces (in place, registered) at least this large -> engine
+        self.xgmi_min_bytes_staged = 0  # ... and through the staging workspace
         if not data:
             self.data = None
             self.backend = "none"
@@ -151,15 +152,17 @@ class Communicator:
     PROBE_MB = (4, 32, 128)
 
     def _probe_xgmi(self, sizes_mb=None, iters: int = 3) -> None:
-        """Measure the xGMI engine against RCCL on THIS node at gradient-bucket sizes
-        (in place on a registered buffer, as ElasticDDP uses it) and keep it for the
-        sizes where every rank saw an exact result and it was faster everywhere
-        (integer-valued data: both sums are exact).  The per-size table is the
-        communication policy: all-reduces >= ``xgmi_min_bytes`` use the engine."""
+        """Measure the xGMI engine against RCCL on THIS node at gradient-bucket sizes, in
+        both of its forms (in place on a registered buffer, and staged through the
+        workspace for buffers too large to map), and keep each form for the sizes where
+        every rank saw an exact result and it was faster everywhere (integer-valued
+        data: both sums are exact).  The per-size table is the communication policy:
+        all-reduces >= ``xgmi_min_bytes`` (registered) / ``xgmi_min_bytes_staged`` use
+        the engine, smaller ones RCCL."""
         sizes_mb = tuple(sizes_mb or self.PROBE_MB)
-        n = (max(sizes_mb) << 20) // 2
+        nel = (max(sizes_mb) << 20) // 2
         g = torch.Generator(device="cpu").manual_seed(7 + self.rank)
-        src = torch.randint(-4, 5, (n,), generator=g, dtype=torch.int8).to(self.device, torch.bfloat16)
+        src = torch.randint(-4, 5, (nel,), generator=g, dtype=torch.int8).to(self.device, torch.bfloat16)
         a, b = src.clone(), src.clone()
         reg = None
         keep_timeout, self.xgmi.timeout_s = self.xgmi.timeout_s, 5.0  # a broken path gives up fast
@@ -197,37 +200,46 @@ class Communicator:
                 view = b[:(mb << 20) // 2]
                 try:
                     t_r = timed(lambda t: self.data.allreduce([t]).wait(), view)
-                    t_x = timed(self.xgmi.all_reduce, view)
+                    t_x = timed(self.xgmi.all_reduce, view)                      # in place (registered)
+                    t_s = timed(lambda t: self.xgmi.all_reduce(t, "twoshot"), view)   # staged
                 except Exception as e:  # noqa: BLE001
                     log.warning("xGMI probe: timing at %d MB failed: %s", mb, e)
-                    t_r, t_x = 1.0, float("inf")
-                table.append((mb, t_r, t_x))
+                    t_r, t_x, t_s = 1.0, float("inf"), float("inf")
+                table.append((mb, t_r, t_x, t_s))
             try:
                 bad = 0.0 if self.xgmi.status() == 0 else 1.0
             except Exception:  # noqa: BLE001
                 bad = 1.0
         self.xgmi.timeout_s = keep_timeout
-        diffs = [min(tx - tr, 1e9) for _, tr, tx in table] or [0.0] * len(sizes_mb)
+        n = len(sizes_mb)
+        diffs = ([min(tx - tr, 1e9) for _, tr, tx, _ in table] + [min(ts - tr, 1e9) for _, tr, _, ts in table]
+                 if table else [0.0] * (2 * n))
         worst = self.ctrl_all_reduce([bad] + diffs, dist.ReduceOp.MAX)
         exact = worst[0] == 0
-        # smallest probed size from which the engine wins at every larger probed size
-        min_mb = None
-        if exact:
-            for i in range(len(table) - 1, -1, -1):
-                if worst[1 + i] < 0:
-                    min_mb = table[i][0]
-                else:
-                    break
-        keep = min_mb is not None
+
+        def first_win(col):
+            """Smallest probed size from which the engine wins at every larger probed size."""
+            out = None
+            if exact and table:
+                for i in range(n - 1, -1, -1):
+                    if worst[1 + col * n + i] < 0:
+                        out = table[i][0]
+                    else:
+                        break
+            return out
+
+        min_inplace, min_staged = first_win(0), first_win(1)
+        keep = min_inplace is not None or min_staged is not None
+        bw = lambda m, t: round(2 * (self.world_size - 1) / self.world_size * (m << 20) / t / 1e9, 1)  # noqa: E731
         self.xgmi_probe = {
-            "sizes_mb": [m for m, _, _ in table],
-            "rccl_ms": [round(tr * 1e3, 3) for _, tr, _ in table],
-            "xgmi_ms": [round(tx * 1e3, 3) for _, _, tx in table],
-            "rccl_busbw_gbs": [round(2 * (self.world_size - 1) / self.world_size * (m << 20) / tr / 1e9, 1)
-                               for m, tr, _ in table],
-            "xgmi_busbw_gbs": [round(2 * (self.world_size - 1) / self.world_size * (m << 20) / tx / 1e9, 1)
-                               for m, _, tx in table],   # inf time -> 0.0
-            "exact_everywhere": bool(exact), "xgmi_min_mb": min_mb,
+            "sizes_mb": [r[0] for r in table],
+            "rccl_ms": [round(r[1] * 1e3, 3) for r in table],
+            "xgmi_inplace_ms": [round(r[2] * 1e3, 3) for r in table],
+            "xgmi_staged_ms": [round(r[3] * 1e3, 3) for r in table],
+            "rccl_busbw_gbs": [bw(r[0], r[1]) for r in table],
+            "xgmi_inplace_busbw_gbs": [bw(r[0], r[2]) for r in table],
+            "xgmi_staged_busbw_gbs": [bw(r[0], r[3]) for r in table],
+            "exact_everywhere": bool(exact), "xgmi_min_mb_inplace": min_inplace, "xgmi_min_mb_staged": min_staged,
             "selected": "xgmi" if keep else "rccl"}
         log.info("all-reduce probe (epoch %d, world %d): %s", self.epoch, self.world_size, self.xgmi_probe)
         if reg is not None:
@@ -236,9 +248,13 @@ class Communicator:
         if keep:
             self.xgmi_mode = "xgmi"
             self.backend = "rccl+xgmi"
-            # winning from the smallest probed size on: every size goes to the engine;
-            # otherwise only messages at least as large as the first winning size
-            self.xgmi_min_bytes = (min_mb << 20) if min_mb != sizes_mb[0] else 0
+            # winning from the smallest probed size on: every size of that path goes to the
+            # engine; otherwise only messages at least as large as the first winning size
+            never = 1 << 62
+            self.xgmi_min_bytes = (0 if min_inplace == sizes_mb[0] else
+                                   (min_inplace << 20) if min_inplace is not None else never)
+            self.xgmi_min_bytes_staged = (0 if min_staged == sizes_mb[0] else
+                                          (min_staged << 20) if min_staged is not None else never)
         else:
             self._sync_stream()
             self.xgmi.close()
@@ -250,8 +266,8 @@ class Communicator:
         gradient groups): the engine then all-reduces their slices in place."""
         if self.xgmi is None or self.xgmi_mode != "xgmi":
             return
-        for t in tensors:
-            if self.xgmi.supports(t):
+        for t in tensors:   # sizes are equal on every rank, so every rank skips the same ones
+            if self.xgmi.supports(t) and self.xgmi.registrable(t):
                 self.xgmi.register(t)
 
     def transfer_state(self, tensors, holders) -> None:
@@ -450,7 +466,13 @@ class Communicator:
         return self.xgmi is not None and self.xgmi_mode == "xgmi" and all(self.xgmi.supports(t) for t in ts)
 
     def _use_xgmi_allreduce(self, t) -> bool:
-        return self._use_xgmi(t) and (self.backend == "xgmi" or t.numel() * t.element_size() >= self.xgmi_min_bytes)
+        if not self._use_xgmi(t):
+            return False
+        if self.backend == "xgmi":
+            return True
+        nbytes = t.numel() * t.element_size()
+        reg, _ = self.xgmi._find_registered(t)
+        return nbytes >= (self.xgmi_min_bytes if reg is not None else self.xgmi_min_bytes_staged)
 
     def _xgmi_sync(self, fn, *args):
         """Run an xGMI collective on the caller's stream (TP/SP: the consumer is next)."""

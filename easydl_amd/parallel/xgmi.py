@@ -70,6 +70,10 @@ class _Registered:
 class XgmiComm:
     ONESHOT_MAX = 512 << 10      # bytes: below this latency dominates -> one-shot
     DEFAULT_WS = 128 << 20       # per parity: one 128 MiB bucket / TP message per launch
+    # hipIpcOpenMemHandle of a 3.9 GB caching-allocator segment never returned on the box
+    # (2 ranks, profiles/r03_ipc_size_probe.txt) while 128 MiB and 1 GiB open in ms: larger
+    # segments are not registered (their all-reduces take the staged path)
+    REGISTER_MAX = int(os.environ.get("EDL_XGMI_REGISTER_MAX_MB", 1024)) << 20
 
     def __init__(self, store, prefix: str, rank: int, world: int, device, ws_bytes: int | None = None,
                  timeout_s: float = 60.0):
@@ -148,12 +152,18 @@ class XgmiComm:
         return d
 
     # -- registered buffers ------------------------------------------------------
+    def registrable(self, t: torch.Tensor) -> bool:
+        """Small enough to map on every peer (decided from sizes alone: equal on all ranks)."""
+        return t.numel() * t.element_size() <= self.REGISTER_MAX
+
     def register(self, t: torch.Tensor, any_dtype: bool = False) -> "_Registered":
         """Map ``t`` (this rank's copy of a buffer every rank registers in the same
         order, e.g. a flat gradient group) on every peer.  Collective.  Later
         all-reduces of any 16-byte-aligned slice of it run in place."""
         if not (self.pullable(t) if any_dtype else self.supports(t)):
             raise XgmiError("register: contiguous fp32 / bf16 tensor of 16-byte multiple expected")
+        if not self.registrable(t):
+            raise XgmiError(f"register: {t.numel() * t.element_size() >> 20} MiB exceeds the IPC mapping limit")
         self._reg_seq += 1
         h = ctypes.create_string_buffer(64)
         off = ctypes.c_uint64()
@@ -208,14 +218,30 @@ class XgmiComm:
             raise XgmiError(f"pull: bad holder set {holders}")
         mask = sum(1 << h for h in holders)
         stream = torch.cuda.current_stream(self.device)
+        nb = int(max(len(holders), min(self.blocks, 256) // len(holders) * len(holders)))
+        for t in tensors:
+            if not self.pullable(t):
+                raise XgmiError("pull: contiguous tensors of 16-byte multiples expected")
+        small = [t for t in tensors if self.registrable(t)]
+        big = [t for t in tensors if not self.registrable(t)]
+        # too large to map: windows staged through the holders' workspaces
+        nh = len(holders)
+        win = (self.ws_bytes // 16) * 16 * nh
+        for t in big:
+            nbytes = t.numel() * t.element_size()
+            for off in range(0, nbytes, win):
+                w = min(win, nbytes - off)
+                self.round += 1
+                rc = self._k("edl_xgmi_pull_staged", self._data, self._flags, self.world_size, self.rank,
+                             t.data_ptr(), t.data_ptr(), off, w, mask, self.round, nb, self._abort_dev,
+                             float(self.timeout_s), self._status_dev, stream.cuda_stream)
+                if rc != 0:
+                    raise XgmiError(f"launch failed: hipError {rc}")
         regs = []
         try:
-            for t in tensors:
-                if not self.pullable(t):
-                    raise XgmiError("pull: contiguous tensors of 16-byte multiples expected")
+            for t in small:
                 regs.append(self.register(t, any_dtype=True))
-            nb = int(max(len(holders), min(self.blocks, 256) // len(holders) * len(holders)))
-            for t, r in zip(tensors, regs):
+            for t, r in zip(small, regs):
                 bufs = (ctypes.c_void_p * self.world_size)(*r.peers)
                 self.round += 1
                 rc = self._k("edl_xgmi_pull", bufs, self._flags, self.world_size, self.rank,

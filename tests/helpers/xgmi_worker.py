@@ -82,7 +82,8 @@ elif mode == "inplace":
 elif mode == "pull":
     # state transfer: ranks 0..h-1 hold the state, the others receive it from all holders
     holders = list(range(max(1, world // 2)))
-    shapes = ((1 << 20, torch.float32), (3 * 4096 + 8, torch.bfloat16), (4 * 1000, torch.int32))
+    shapes = ((1 << 20, torch.float32), (3 * 4096 + 8, torch.bfloat16), (4 * 1000, torch.int32),
+              (6 * (1 << 20) + 4, torch.float32))   # 24 MB: several staged windows of the 8 MB workspace
     ts = [torch.empty(n, dtype=dt, device="cuda") for n, dt in shapes]
     for i, t in enumerate(ts):
         t.copy_(ints(t.numel(), 77 + i, t.dtype).cuda() if rank in holders else torch.zeros_like(t))

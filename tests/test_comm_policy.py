@@ -62,7 +62,13 @@ class FakeEngine:
     def unregister(self, r):
         self.registered.remove(r)
 
-    def all_reduce(self, t):
+    def _find_registered(self, t):
+        return None, 0
+
+    def registrable(self, t):
+        return True
+
+    def all_reduce(self, t, algo=None):
         if not self.calls:   # the exactness check: a real sum (then only the timing matters)
             self.c.data.allreduce([t]).wait()
             if self.broken:
@@ -99,7 +105,7 @@ def test_probe_selects_per_size(case):
         assert nreg == 0                       # the probe buffer is unregistered again
         if case == "engine_wins_large":
             assert probe["selected"] == "xgmi" and mode == "xgmi", probe
-            assert probe["xgmi_min_mb"] == 4 and min_bytes == 4 << 20
+            assert probe["xgmi_min_mb_inplace"] == 4 and probe["xgmi_min_mb_staged"] == 4 and min_bytes == 4 << 20
         else:
             assert probe["selected"] == "rccl" and mode is None and closed, probe
         if case == "engine_inexact":

@@ -56,8 +56,13 @@ def test_xgmi_inplace_registered_allreduce_exact(cuda, tmp_path, world):
 
 
 @pytest.mark.parametrize("world", [2, 4])
-def test_xgmi_multi_source_pull(cuda, tmp_path, world):
-    """State transfer: receivers copy slice k of every tensor from holder k."""
+@pytest.mark.parametrize("staged", [False, True])
+def test_xgmi_multi_source_pull(cuda, tmp_path, world, staged, monkeypatch):
+    """State transfer: receivers copy slice k of every tensor from holder k — mapped in
+    place, or (tensors too large to map) staged window by window through the holders'
+    workspaces."""
+    if staged:
+        monkeypatch.setenv("EDL_XGMI_REGISTER_MAX_MB", "0")
     for r in _run(world, tmp_path, mode="pull"):
         assert r["ok"], r["errors"]
         assert r["status"] == 0
