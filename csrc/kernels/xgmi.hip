@@ -388,7 +388,8 @@ __global__ __launch_bounds__(XG_THREADS) void xg_pull(XgSync S, XgBufs G, int64_
 // Staged multi-source pull for tensors too large to map (one window per launch): the
 // k-th holder stages slice k of the window into its workspace buffer, every receiver
 // copies slice k from holder k's workspace.  Round parity protects the buffers as in
-// the staged all-reduce.  src: this rank's tensor (holders), dst: the same tensor
+// the staged all-reduce; workgroup b of a receiver reads only what workgroup b of each
+// holder staged.  src: this rank's tensor (holders), dst: the same tensor
 // (receivers); win_off / win_len in 16-byte vectors.
 template <int NR>
 __global__ __launch_bounds__(XG_THREADS) void xg_pull_staged(XgSync S, XgBufs W, const u32x4* __restrict__ src,
@@ -410,26 +411,28 @@ __global__ __launch_bounds__(XG_THREADS) void xg_pull_staged(XgSync S, XgBufs W,
     copy_range(src + win_off + s0, reinterpret_cast<u32x4*>(W.p[S.rank]), lo, hi);
   }
   if (!xg_barrier<NR>(S, 0)) return;
-  if (me < 0) {    // receiver: slice k from holder k, workgroups dealt over the holders
-    const int k = blockIdx.x % nh;
-    const int nb = (gridDim.x - k + nh - 1) / nh, bi = blockIdx.x / nh;
-    const int64_t s0 = (int64_t)k * slice, n = max<int64_t>(0, min(slice, win_len - s0));
-    const int64_t per = (n + nb - 1) / nb;
-    const int64_t lo = bi * per, hi = min(n, lo + per);
-    const u32x4* from = reinterpret_cast<const u32x4*>(W.p[hs[k]]);
-    u32x4* to = dst + win_off + s0;
-    constexpr int U = 8;
-    for (int64_t i0 = lo + threadIdx.x; i0 < hi; i0 += (int64_t)U * XG_THREADS) {
-      u32x4 v[U];
+  if (me < 0) {
+    // receiver: workgroup b copies, from EVERY holder k, exactly the sub-range holder k's
+    // workgroup b staged (the barrier above only orders workgroup b against workgroup b)
+    constexpr int U = 4;
+    for (int k = 0; k < nh; ++k) {
+      const int64_t s0 = (int64_t)k * slice, n = max<int64_t>(0, min(slice, win_len - s0));
+      int64_t lo, hi;
+      block_range(n, lo, hi);
+      const u32x4* from = reinterpret_cast<const u32x4*>(W.p[hs[k]]);
+      u32x4* to = dst + win_off + s0;
+      for (int64_t i0 = lo + threadIdx.x; i0 < hi; i0 += (int64_t)U * XG_THREADS) {
+        u32x4 v[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int64_t i = i0 + (int64_t)u * XG_THREADS;
-        if (i < hi) v[u] = from[i];
-      }
+        for (int u = 0; u < U; ++u) {
+          const int64_t i = i0 + (int64_t)u * XG_THREADS;
+          if (i < hi) v[u] = from[i];
+        }
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int64_t i = i0 + (int64_t)u * XG_THREADS;
-        if (i < hi) to[i] = v[u];
+        for (int u = 0; u < U; ++u) {
+          const int64_t i = i0 + (int64_t)u * XG_THREADS;
+          if (i < hi) to[i] = v[u];
+        }
       }
     }
   }

@@ -37,7 +37,8 @@ def worker():
 
 
 def main():
-    cases = [(4, 128, 0), (4, 1024, 0), (2, 3900, 0), (4, 3900, 0), (4, 3900, 20000)]
+    cases = [tuple(int(x) for x in c.split(":")) for c in
+             os.environ.get("PROBE_CASES", "4:128:0,4:1024:0,2:3900:0,4:3900:0").split(",")]
     for world, mb, pad in cases:
         s = socket.socket()
         s.bind(("127.0.0.1", 0))
