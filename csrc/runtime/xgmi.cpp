@@ -166,7 +166,7 @@ int edl_xgmi_ws_destroy(void* ws) {
 // ---- registered buffers (e.g. the flat gradient buffer, mapped by every peer) ----
 // IPC handles name whole allocations, so a tensor inside a caching-allocator
 // segment is exported as (handle of its segment, byte offset).
-int edl_xgmi_buf_handle(void* ptr, char* out_handle, uint64_t* out_offset) {
+int edl_xgmi_buf_handle(void* ptr, char* out_handle, uint64_t* out_offset, uint64_t* out_segment_bytes) {
   hipDeviceptr_t base = nullptr;
   size_t size = 0;
   hipError_t e = hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)ptr);
@@ -176,6 +176,7 @@ int edl_xgmi_buf_handle(void* ptr, char* out_handle, uint64_t* out_offset) {
   if (e != hipSuccess) return (int)e;
   memcpy(out_handle, &h, sizeof(h));
   *out_offset = (uint64_t)((char*)ptr - (char*)base);
+  *out_segment_bytes = (uint64_t)size;
   return 0;
 }
 

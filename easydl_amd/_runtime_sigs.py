@@ -65,7 +65,7 @@ SIGS = {
     "edl_xgmi_ws_status": (i32, [vp]),
     "edl_xgmi_ws_destroy": (i32, [vp]),
     "edl_xgmi_ws_status_detail": (i32, [vp, ctypes.POINTER(i32)]),
-    "edl_xgmi_buf_handle": (i32, [vp, ctypes.c_char_p, ctypes.POINTER(u64)]),
+    "edl_xgmi_buf_handle": (i32, [vp, ctypes.c_char_p, ctypes.POINTER(u64), ctypes.POINTER(u64)]),
     "edl_xgmi_buf_open": (i32, [i32, ctypes.c_char_p, ctypes.POINTER(vp)]),
     "edl_xgmi_buf_close": (i32, [i32, vp]),
     "edl_rccl_available": (i32, [ctypes.POINTER(i32), ctypes.POINTER(i32)]),

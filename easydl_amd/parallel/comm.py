@@ -266,9 +266,13 @@ class Communicator:
         gradient groups): the engine then all-reduces their slices in place."""
         if self.xgmi is None or self.xgmi_mode != "xgmi":
             return
+        from easydl_amd.parallel.xgmi import XgmiError
         for t in tensors:   # sizes are equal on every rank, so every rank skips the same ones
             if self.xgmi.supports(t) and self.xgmi.registrable(t):
-                self.xgmi.register(t)
+                try:
+                    self.xgmi.register(t)
+                except XgmiError as e:   # agreed on every rank (segment too large): staged path
+                    log.info("gradient buffer not registered: %s", e)
 
     def transfer_state(self, tensors, holders) -> None:
         """State transfer to joiners / replacements: every rank not in ``holders``

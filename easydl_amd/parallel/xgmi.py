@@ -70,10 +70,11 @@ class _Registered:
 class XgmiComm:
     ONESHOT_MAX = 512 << 10      # bytes: below this latency dominates -> one-shot
     DEFAULT_WS = 128 << 20       # per parity: one 128 MiB bucket / TP message per launch
-    # hipIpcOpenMemHandle of a 3.9 GB caching-allocator segment never returned on the box
-    # (2 ranks, profiles/r03_ipc_size_probe.txt) while 128 MiB and 1 GiB open in ms: larger
-    # segments are not registered (their all-reduces take the staged path)
-    REGISTER_MAX = int(os.environ.get("EDL_XGMI_REGISTER_MAX_MB", 1024)) << 20
+    # hipIpcOpenMemHandle of a caching-allocator segment of >= 2 GiB never returns on the
+    # box (2040 MiB opens in ms, 2056 MiB hangs: profiles/r03_ipc_size_probe*.txt), so a
+    # tensor whose SEGMENT is that large on any rank is not registered (its all-reduces
+    # take the staged path, its state transfer the staged pull)
+    REGISTER_MAX = int(os.environ.get("EDL_XGMI_REGISTER_MAX_MB", 2040)) << 20
 
     def __init__(self, store, prefix: str, rank: int, world: int, device, ws_bytes: int | None = None,
                  timeout_s: float = 60.0):
@@ -153,7 +154,7 @@ class XgmiComm:
 
     # -- registered buffers ------------------------------------------------------
     def registrable(self, t: torch.Tensor) -> bool:
-        """Small enough to map on every peer (decided from sizes alone: equal on all ranks)."""
+        """Small enough that mapping it can work (the segment check happens in register)."""
         return t.numel() * t.element_size() <= self.REGISTER_MAX
 
     def register(self, t: torch.Tensor, any_dtype: bool = False) -> "_Registered":
@@ -166,18 +167,24 @@ class XgmiComm:
             raise XgmiError(f"register: {t.numel() * t.element_size() >> 20} MiB exceeds the IPC mapping limit")
         self._reg_seq += 1
         h = ctypes.create_string_buffer(64)
-        off = ctypes.c_uint64()
-        rc = self._rt("edl_xgmi_buf_handle", t.data_ptr(), h, ctypes.byref(off))
-        if rc != 0:
-            raise XgmiError(f"register: hipIpcGetMemHandle failed: hipError {rc}")
+        off, seg = ctypes.c_uint64(), ctypes.c_uint64()
+        rc = self._rt("edl_xgmi_buf_handle", t.data_ptr(), h, ctypes.byref(off), ctypes.byref(seg))
+        if rc != 0:   # (still publish, so the peers do not wait forever for this record)
+            h, seg = ctypes.create_string_buffer(64), ctypes.c_uint64(1 << 62)
         key = f"{self._prefix}/reg/{self._reg_seq}"
-        self._store.set(f"{key}/{self.rank}", h.raw + int(off.value).to_bytes(8, "little"))
+        mine = h.raw + int(off.value).to_bytes(8, "little") + int(seg.value).to_bytes(8, "little")
+        self._store.set(f"{key}/{self.rank}", mine)
+        entries = [mine if p == self.rank else self._store.get(f"{key}/{p}") for p in range(self.world_size)]
+        biggest = max(int.from_bytes(e[72:80], "little") for e in entries)
+        if biggest > self.REGISTER_MAX:
+            # every rank sees the same records, so every rank gives up on this tensor
+            raise XgmiError(f"register: a {biggest >> 20} MiB segment exceeds the IPC mapping limit")
         peers, opened = [], []
         for p in range(self.world_size):
             if p == self.rank:
                 peers.append(t.data_ptr())
                 continue
-            e = self._store.get(f"{key}/{p}")
+            e = entries[p]
             hp, op = e[:64], int.from_bytes(e[64:72], "little")
             ent = self._opened.get((p, hp))
             if ent is None:   # segments shared by several registrations are mapped once
@@ -222,8 +229,14 @@ class XgmiComm:
         for t in tensors:
             if not self.pullable(t):
                 raise XgmiError("pull: contiguous tensors of 16-byte multiples expected")
-        small = [t for t in tensors if self.registrable(t)]
-        big = [t for t in tensors if not self.registrable(t)]
+        small, regs, big = [], [], []
+        for t in tensors:   # registration is collective and agreed: every rank splits alike
+            try:
+                regs.append(self.register(t, any_dtype=True) if self.registrable(t) else None)
+            except XgmiError:
+                regs.append(None)
+            (small if regs[-1] is not None else big).append(t)
+        regs = [r for r in regs if r is not None]
         # too large to map: windows staged through the holders' workspaces
         nh = len(holders)
         win = (self.ws_bytes // 16) * 16 * nh
@@ -237,10 +250,7 @@ class XgmiComm:
                              float(self.timeout_s), self._status_dev, stream.cuda_stream)
                 if rc != 0:
                     raise XgmiError(f"launch failed: hipError {rc}")
-        regs = []
         try:
-            for t in small:
-                regs.append(self.register(t, any_dtype=True))
             for t, r in zip(small, regs):
                 bufs = (ctypes.c_void_p * self.world_size)(*r.peers)
                 self.round += 1

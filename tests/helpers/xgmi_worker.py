@@ -97,6 +97,23 @@ elif mode == "pull":
             res["ok"] = False
             res["errors"].append(f"tensor {i} differs on rank {rank}")
     res["status"] = x.status()
+elif mode == "reglimit":
+    # a segment over the mapping limit (EDL_XGMI_REGISTER_MAX_MB) is refused on EVERY rank,
+    # before any IPC open, and the tensor still all-reduces (staged)
+    x.REGISTER_MAX = 1 << 20
+    t = ints(1 << 20, 5 + rank, torch.float32).cuda()    # 4 MB tensor in a >= 4 MB segment
+    try:
+        x.register(t)
+        res["refused"] = False
+    except Exception as e:  # noqa: BLE001
+        res["refused"] = "exceeds the IPC mapping limit" in str(e)
+    sync()
+    x.all_reduce(t)
+    torch.cuda.synchronize()
+    if not torch.equal(t.cpu(), sum(ints(1 << 20, 5 + r, torch.float32) for r in range(world))):
+        res["ok"] = False
+        res["errors"].append("staged all-reduce after refusal")
+    res["status"] = x.status()
 elif mode == "abort":
     # rank 1 never joins the collective: rank 0's kernel must give up on abort, not hang
     if rank == 0:

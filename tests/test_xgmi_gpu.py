@@ -68,6 +68,15 @@ def test_xgmi_multi_source_pull(cuda, tmp_path, world, staged, monkeypatch):
         assert r["status"] == 0
 
 
+def test_xgmi_register_refuses_oversized_segments_everywhere(cuda, tmp_path):
+    """hipIpcOpenMemHandle hangs on >= 2 GiB segments on this platform: the limit is agreed
+    through the store, so every rank refuses before any open and the tensor still
+    all-reduces through the workspace."""
+    for r in _run(2, tmp_path, mode="reglimit"):
+        assert r["refused"] and r["ok"], r
+        assert r["status"] == 0
+
+
 def test_xgmi_abort_releases_spinning_kernel(cuda, tmp_path):
     r0 = _run(2, tmp_path, mode="abort")[0]
     assert r0["status"] == 1           # the barrier gave up ...
