@@ -4,7 +4,9 @@ Written here (torchvision is not installed).  bf16 weights in channels-last
 memory format so MIOpen picks its NHWC implicit-GEMM (MFMA) convolutions.
 Every BatchNorm (fp32 weight and statistics) runs with its ReLU and, at the end
 of a bottleneck, the residual add fused in (:func:`easydl_amd.ops.batchnorm.bn_act`,
-HIP kernels on the GPU).  Synthetic ImageNet-shaped data (:class:`SyntheticImages`)
+HIP kernels on the GPU).  Convolutions deliver their weight gradients straight into
+the flat gradient buffer; the 1x1 ones run as hipBLASLt GEMMs over the channels-last
+pixel matrix (:func:`easydl_amd.ops.conv.conv2d`).  Synthetic ImageNet-shaped data (:class:`SyntheticImages`)
 since no dataset can be downloaded.
 """
 from __future__ import annotations
@@ -13,7 +15,9 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from easydl_amd.ops import fused
 from easydl_amd.ops.batchnorm import bn_act
+from easydl_amd.ops.conv import conv2d
 
 
 class Bottleneck(nn.Module):
@@ -35,10 +39,10 @@ class Bottleneck(nn.Module):
             idt = x
         else:
             conv, bn = self.downsample
-            idt = bn_act(conv(x), bn, relu=False)
-        y = bn_act(self.conv1(x), self.bn1)
-        y = bn_act(self.conv2(y), self.bn2)
-        return bn_act(self.conv3(y), self.bn3, residual=idt)
+            idt = bn_act(conv2d(x, conv), bn, relu=False)
+        y = bn_act(conv2d(x, self.conv1), self.bn1)
+        y = bn_act(conv2d(y, self.conv2), self.bn2)
+        return bn_act(conv2d(y, self.conv3), self.bn3, residual=idt)
 
 
 class ResNet(nn.Module):
@@ -63,11 +67,11 @@ class ResNet(nn.Module):
         self.fc = nn.Linear(cin, num_classes)
 
     def forward(self, x, y=None):
-        x = bn_act(self.conv1(x), self.bn1)
+        x = bn_act(conv2d(x, self.conv1), self.bn1)
         x = F.max_pool2d(x, 3, 2, 1)
         x = self.stages(x)
         x = torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)
-        logits = self.fc(x)
+        logits = fused.linear(x, self.fc.weight, self.fc.bias)
         if y is None:
             return logits
         return F.cross_entropy(logits.float(), y)

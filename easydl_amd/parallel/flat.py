@@ -108,15 +108,30 @@ class FlatParams:
                 off += _roundup(k)
             self.groups.append(grp)
         self.saw_autograd = False
-        # autograd-path parameters (ops that return the gradient) accumulate in place
+        self._autograd_slots: set = set()   # (group, slot) that autograd accumulated into
+        self._slot_of = {id(s.param): (g, s) for g in self.groups for s in g.slots}
+        # autograd-path parameters (ops that return the gradient) accumulate in place.  A
+        # fused op that delivers its gradient directly returns None, and the post-accumulate
+        # hook still fires for it; only the tensor hook sees whether a gradient really
+        # reached AccumulateGrad, so that is what marks a slot for zeroing.
         for g in self.groups:
             for s in g.slots:
+                s.param.register_hook(self._pre_accumulate(s.param))
                 s.param.register_post_accumulate_grad_hook(self._post_accumulate)
         self._ready_cb = None
 
     # -- gradient protocol -------------------------------------------------
+    def _pre_accumulate(self, p):
+        key = id(p)
+
+        def hook(g):
+            if g is not None:   # None: a fused op delivered this gradient itself
+                self.saw_autograd = True
+                self._autograd_slots.add(key)
+            return None
+        return hook
+
     def _post_accumulate(self, p):
-        self.saw_autograd = True
         p._edl_fresh = False
         if self._ready_cb is not None:
             self._ready_cb(p)
@@ -139,9 +154,17 @@ class FlatParams:
         from easydl_amd.ops.fused import new_weight_generation
         new_weight_generation()
         if self.saw_autograd:
-            for g in self.groups:
-                g.grad.zero_()
+            # only the slots autograd accumulated into (direct writers overwrite anyway):
+            # ResNet-50 / Llama no longer memset their whole gradient buffer every step
+            if len(self._autograd_slots) * 4 > sum(len(g.slots) for g in self.groups):
+                for g in self.groups:
+                    g.grad.zero_()
+            else:
+                for key in self._autograd_slots:
+                    g, s = self._slot_of[key]
+                    g.grad[s.offset:s.offset + s.numel].zero_()
             self.saw_autograd = False
+            self._autograd_slots = set()
         for g in self.groups:
             for s in g.slots:
                 s.param._edl_fresh = True
