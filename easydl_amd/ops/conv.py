@@ -7,16 +7,16 @@ because a parameter took the autograd path, ``FlatParams.zero_grad`` must
 memset the whole gradient buffer every step (profiles/r02_resnet50_kernel_stats.csv:
 702 ``CUDAFunctor_add`` launches, 4.3 % of the ResNet-50 step).
 
-* 1x1 stride-1 convolutions on channels-last bf16 tensors ARE GEMMs over the
-  [N*H*W, C] pixel matrix: forward, input gradient and weight gradient run as
-  hipBLASLt GEMMs, the weight gradient written into the flat buffer by
-  :func:`gradsink.write_mm` (no temporary, no add);
-* every other convolution keeps MIOpen (``aten.convolution`` /
-  ``aten.convolution_backward``); its weight gradient is delivered with
-  :func:`gradsink.write` (a copy on the first micro-batch instead of an add, and
-  the gradient buffer no longer needs its per-step memset).
-
-``EDL_CONV1X1_GEMM=0`` keeps MIOpen for the 1x1 convolutions too (A/B).
+* convolutions run on MIOpen (``aten.convolution`` / ``aten.convolution_backward``)
+  and the weight gradient is delivered with :func:`gradsink.write` (a copy on the
+  first micro-batch instead of an add, and the gradient buffer no longer needs its
+  per-step memset);
+* ``EDL_CONV1X1_GEMM=1``: 1x1 stride-1 convolutions on channels-last bf16 tensors
+  as GEMMs over the [N*H*W, C] pixel matrix (forward, input gradient, weight
+  gradient written by :func:`gradsink.write_mm`).  Off by default: hipBLASLt on
+  these skinny shapes (K or N = 64..2048 against 0.2-0.8 M pixel rows) took 21.7 ms
+  per step against MIOpen's 10.8 ms (profiles/r03_conv1x1_probe.txt), and the
+  ResNet-50 step went 34.9 -> 46.8 ms.
 """
 from __future__ import annotations
 
@@ -27,7 +27,7 @@ import torch.nn.functional as F
 
 from easydl_amd.ops import gradsink
 
-_GEMM_1X1 = os.environ.get("EDL_CONV1X1_GEMM", "1") != "0"
+_GEMM_1X1 = os.environ.get("EDL_CONV1X1_GEMM", "0") == "1"
 
 
 class _Conv1x1Fn(torch.autograd.Function):
