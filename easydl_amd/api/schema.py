@@ -67,6 +67,7 @@ SCHEMAS: dict[str, dict] = {
             "roles": {"type": "object", "additionalProperties": ROLE_RESOURCE},
             "per_rank": {"type": "object"}, "bucket_mb": {"type": ["number", "null"], "minimum": 0},
             "ckpt_interval": {"type": ["integer", "null"], "minimum": 0}, "reason": {"type": "string"},
+            "allreduce": {"type": ["object", "null"]},
         },
     },
     "PlanRequest": {
@@ -74,7 +75,7 @@ SCHEMAS: dict[str, dict] = {
         "properties": {
             "schema": {"const": SCHEMA_VERSION}, "job": _NAME, "kind": {"enum": ["startup", "next"]},
             "features": {"type": "object"}, "current": {"type": ["object", "null"]},
-            "metrics": {"type": "object"},
+            "metrics": {"type": "object"}, "comm": {"type": ["object", "null"]},
         },
     },
     "PlanResponse": {

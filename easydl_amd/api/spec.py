@@ -179,6 +179,7 @@ class JobResource:
     # plan-level MI355X knobs
     bucket_mb: float | None = None
     ckpt_interval: int | None = None
+    allreduce: dict | None = None      # all-reduce routing policy (parallel/comm_policy.py)
     version: int = 0
 
     @classmethod
@@ -205,7 +206,8 @@ class JobResource:
             upd.append(ResourceUpdation(name=_clean(u["name"]), resource=Resource.from_dict(u.get("resource"))))
         return cls(name=_clean((d.get("metadata") or {}).get("name") or f"{sel}-resource"), selector=sel,
                    roles=roles, resource_updation=upd, api_version=av, bucket_mb=_num(spec.get("bucket_mb")),
-                   ckpt_interval=_num(spec.get("ckpt_interval"), int), version=int(spec.get("version", 0)))
+                   ckpt_interval=_num(spec.get("ckpt_interval"), int), allreduce=spec.get("allreduce") or None,
+                   version=int(spec.get("version", 0)))
 
     def to_dict(self) -> dict:
         spec = {"selector": {"name": self.selector}}
@@ -218,6 +220,8 @@ class JobResource:
             spec["bucket_mb"] = self.bucket_mb
         if self.ckpt_interval is not None:
             spec["ckpt_interval"] = self.ckpt_interval
+        if self.allreduce:
+            spec["allreduce"] = self.allreduce
         spec["version"] = self.version
         return {"apiVersion": self.api_version, "kind": "JobResource", "metadata": {"name": self.name},
                 "spec": spec}
@@ -234,24 +238,26 @@ class ResourcePlan:
     per_rank: dict[str, dict] = field(default_factory=dict)   # process name -> {cu, hbm_gb, cpus}
     bucket_mb: float | None = None
     ckpt_interval: int | None = None
+    allreduce: dict | None = None      # {"world": W, "policy": {...}} from the probe history
     reason: str = ""
 
     def to_job_resource(self, job: str, version: int = 0) -> JobResource:
         return JobResource(name=f"{job}-resource", selector=job, roles=copy.deepcopy(self.roles),
-                           bucket_mb=self.bucket_mb, ckpt_interval=self.ckpt_interval, version=version)
+                           bucket_mb=self.bucket_mb, ckpt_interval=self.ckpt_interval,
+                           allreduce=copy.deepcopy(self.allreduce), version=version)
 
     def to_dict(self) -> dict:
         return {"roles": {r: {"replicas": rr.replicas, "resource": rr.resource.to_dict()}
                           for r, rr in self.roles.items()},
                 "per_rank": self.per_rank, "bucket_mb": self.bucket_mb, "ckpt_interval": self.ckpt_interval,
-                "reason": self.reason}
+                "allreduce": self.allreduce, "reason": self.reason}
 
     @classmethod
     def from_dict(cls, d: dict) -> "ResourcePlan":
         roles = {r: RoleResource(int(v.get("replicas", 0)), Resource.from_dict(v.get("resource")))
                  for r, v in (d.get("roles") or {}).items()}
         return cls(roles=roles, per_rank=dict(d.get("per_rank") or {}), bucket_mb=d.get("bucket_mb"),
-                   ckpt_interval=d.get("ckpt_interval"), reason=d.get("reason", ""))
+                   ckpt_interval=d.get("ckpt_interval"), allreduce=d.get("allreduce"), reason=d.get("reason", ""))
 
 
 def load_yaml_docs(path_or_text: str) -> list[dict]:

@@ -22,7 +22,14 @@ Periodic plan (from per-rank step metrics)
 * straggler eviction: a rank slower than ``straggler_ratio`` x median for a
   full window is replaced (resource_updation re-creates it);
 * bucket-size autotune: try neighbouring sizes window by window, keep the
-  fastest measured step time;
+  fastest measured step time — only over sizes at or above the all-reduce
+  bandwidth knee the probes measured;
+* all-reduce routing: every epoch's communicator times RCCL against the xGMI
+  engine's forms at 256 KB..128 MB and publishes the table (``comm/probe``);
+  the Brain takes the per-size median over the epochs of the same world size and
+  re-derives the policy (one-shot switch sizes, the size from which the engine
+  beats RCCL, with a margin in RCCL's favour) — a runtime knob the trainers switch
+  to at one committed step (parallel/comm_policy.py);
 * scale up to free GPUs when the job asked for more workers than it got.
 """
 from __future__ import annotations
@@ -69,6 +76,8 @@ class BrainConfig:
     bucket_choices: tuple = (32.0, 64.0, 128.0, 256.0, 512.0)
     ckpt_overhead: float = 0.05
     pcie_gbps: float = 50.0
+    comm_margin: float = 0.03       # the engine must beat RCCL by this share to take a size
+    comm_history: int = 8           # probe tables kept per world size
 
 
 def grad_bucket_mb(params: float, world: int, grad_bytes: int = 2) -> float:
@@ -95,6 +104,7 @@ class Planner:
     def __init__(self, cfg: BrainConfig | None = None):
         self.cfg = cfg or BrainConfig()
         self._tune: dict = {}
+        self._probes: dict[int, dict[int, dict]] = {}   # world -> epoch -> published probe table
 
     # ------------------------------------------------------------------ startup
     def startup_plan(self, feat: JobFeatures, inv: NodeInventory) -> ResourcePlan:
@@ -149,13 +159,49 @@ class Planner:
         frac = max(0.25, min(1.0, 0.25 + comp))
         return int(round(total_cus * frac / 8)) * 8   # whole CUs per XCD
 
+    # ------------------------------------------------------------------ communication
+    def observe_probe(self, comm: dict | None) -> None:
+        """Keep an epoch's published all-reduce probe table (``{"world", "epoch", "probe"}``)."""
+        if not comm or not comm.get("probe"):
+            return
+        world, epoch = int(comm.get("world", 0)), int(comm.get("epoch", 0))
+        hist = self._probes.setdefault(world, {})
+        hist[epoch] = comm["probe"]
+        for e in sorted(hist)[:-self.cfg.comm_history]:
+            del hist[e]
+
+    def allreduce_plan(self, world: int) -> dict | None:
+        """The all-reduce policy for ``world`` from the median of its probe tables."""
+        from easydl_amd.parallel import comm_policy
+        tab = comm_policy.median_table([self._probes[world][e] for e in sorted(self._probes.get(world, {}))])
+        if tab is None:
+            return None
+        pol = comm_policy.decide_from_probe(tab, world, margin=self.cfg.comm_margin)
+        return {"world": world, "epochs": tab["n"], "policy": pol}
+
     # ------------------------------------------------------------------ periodic
     def next_plan(self, feat: JobFeatures, inv: NodeInventory, current: ResourcePlan,
-                  metrics: dict[str, dict]) -> ResourcePlan | None:
-        """Return a changed plan, or None to keep the current one."""
+                  metrics: dict[str, dict], comm: dict | None = None) -> ResourcePlan | None:
+        """Return a changed plan, or None to keep the current one.  ``comm`` is the
+        latest published all-reduce probe (``comm/probe``), if any."""
         import copy
         plan = copy.deepcopy(current)
         changed = []
+        self.observe_probe(comm)
+        floor = None
+        if comm and comm.get("world"):
+            ar = self.allreduce_plan(int(comm["world"]))
+            if ar is not None:
+                floor = ar["policy"].get("bucket_floor_mb")
+                keys = ("oneshot_max_kb", "oneshot_max_staged_kb", "xgmi_min_kb_inplace", "xgmi_min_kb_staged")
+                old = (current.allreduce or {})
+                if (old.get("world") != ar["world"]
+                        or any((old.get("policy") or {}).get(k) != ar["policy"].get(k) for k in keys)):
+                    plan.allreduce = ar
+                    p = ar["policy"]
+                    changed.append(f"all-reduce policy (world {ar['world']}, {ar['epochs']} probes): engine from "
+                                   f"{p['xgmi_min_kb_inplace']} KB in place / {p['xgmi_min_kb_staged']} KB staged, "
+                                   f"one-shot <= {p['oneshot_max_kb']} KB")
         times = {n: m.get("step_time") for n, m in metrics.items() if m.get("step_time")}
         if len(times) >= 2:
             med = statistics.median(times.values())
@@ -172,10 +218,18 @@ class Planner:
             t.setdefault("results", {})
             t["results"][cur] = min(st, t["results"].get(cur, float("inf")))
             choices = list(self.cfg.bucket_choices)
+            if floor:
+                # buckets below the measured bandwidth knee leave link time on the table
+                choices = [c for c in choices if c >= floor] or choices[-1:]
             # hill-climb around the best size measured so far: try its untried neighbours,
             # settle on it once both have been measured
-            best = min(t["results"], key=t["results"].get)
-            if best in choices:
+            allowed = {c: v for c, v in t["results"].items() if c in choices}
+            best = min(allowed, key=allowed.get) if allowed else None
+            if best is None and floor:
+                plan.bucket_mb = choices[0]
+                changed.append(f"bucket {cur} MB is below the all-reduce bandwidth knee ({floor} MB): "
+                               f"{choices[0]} MB")
+            elif best is not None:
                 i = choices.index(best)
                 untried = [c for c in (choices[i - 1] if i > 0 else None, choices[i + 1] if i + 1 < len(choices)
                                        else None) if c is not None and c not in t["results"]]

@@ -3,7 +3,7 @@ environment — SURVEY.md §2.3 I2) plus an in-process client.
 
 Endpoints (POST, JSON in/out):
     /startup_plan   {features}                      -> ResourcePlan
-    /next_plan      {features, plan, metrics}       -> ResourcePlan | null
+    /next_plan      {features, plan, metrics, comm} -> ResourcePlan | null
     /inventory      {}                              -> NodeInventory
 Run: ``python -m easydl_amd.brain.service --port 8808``.
 """
@@ -44,11 +44,13 @@ class BrainClient:
             return ResourcePlan.from_dict(self._post("/startup_plan", {"features": features}))
         return self.planner.startup_plan(JobFeatures.from_dict(features), self.inventory())
 
-    def next_plan(self, features: dict, plan: ResourcePlan, metrics: dict) -> ResourcePlan | None:
+    def next_plan(self, features: dict, plan: ResourcePlan, metrics: dict,
+                  comm: dict | None = None) -> ResourcePlan | None:
         if self.url:
-            r = self._post("/next_plan", {"features": features, "plan": plan.to_dict(), "metrics": metrics})
+            r = self._post("/next_plan", {"features": features, "plan": plan.to_dict(), "metrics": metrics,
+                                          "comm": comm})
             return None if r is None else ResourcePlan.from_dict(r)
-        return self.planner.next_plan(JobFeatures.from_dict(features), self.inventory(True), plan, metrics)
+        return self.planner.next_plan(JobFeatures.from_dict(features), self.inventory(True), plan, metrics, comm)
 
 
 class _Handler(BaseHTTPRequestHandler):
@@ -78,7 +80,8 @@ class _Handler(BaseHTTPRequestHandler):
                 out = self.planner.startup_plan(JobFeatures.from_dict(body.get("features")), host_inventory()).to_dict()
             elif self.path == "/next_plan":
                 p = self.planner.next_plan(JobFeatures.from_dict(body.get("features")), host_inventory(True),
-                                           ResourcePlan.from_dict(body["plan"]), body.get("metrics") or {})
+                                           ResourcePlan.from_dict(body["plan"]), body.get("metrics") or {},
+                                           body.get("comm"))
                 out = None if p is None else p.to_dict()
             elif self.path == "/inventory":
                 out = host_inventory(True).to_dict()

@@ -5,8 +5,15 @@
    local ElasticOperator watches) — unless the user supplied one;
 2. periodically collect per-rank metrics (``metrics/<node>``), ask the Brain
    for a new plan and update the JobResource (scale, replace stragglers via
-   ``resource_updation``) and the runtime knobs (``plan/bucket_mb``) that the
-   trainers pick up at step boundaries.
+   ``resource_updation``) and the runtime knobs (bucket size, checkpoint
+   interval, all-reduce routing policy) that the trainers pick up at step
+   boundaries.  The epochs' all-reduce probe tables (``comm/probe``, written by
+   DP rank 0 of each epoch) go to the Brain with the metrics.
+
+Runtime knobs travel as ONE versioned document, ``plan/runtime/<v>``, written
+before the counter ``plan/version`` moves to ``v``: every rank switches to the
+version its step commit agreed on and reads exactly that document, so a plan
+applied between two ranks' reads can never give them different bucket layouts.
 """
 from __future__ import annotations
 
@@ -45,10 +52,10 @@ class PlanLoop:
         self.version += 1
         jr.version = self.version
         master.kv.set("jobresource", json.dumps(jr.to_dict()))
-        if jr.bucket_mb:
-            master.kv.set("plan/bucket_mb", str(jr.bucket_mb))
-        if jr.ckpt_interval:
-            master.kv.set("plan/ckpt_interval", str(jr.ckpt_interval))
+        # only the master moves plan/version: the next value is counter + 1
+        nxt = master.kv.counter("plan/version") + 1
+        master.kv.set(f"plan/runtime/{nxt}", json.dumps({"bucket_mb": jr.bucket_mb, "ckpt_interval": jr.ckpt_interval,
+                                                          "allreduce": jr.allreduce}))
         master.kv.add("plan/version", 1)
         wr = jr.roles.get("worker")
         if wr is not None and self.job.mode == "allreduce":
@@ -85,7 +92,7 @@ class PlanLoop:
                 self.version = jr.version
                 self.started = True
                 self.plan = ResourcePlan(roles=jr.roles, bucket_mb=jr.bucket_mb, ckpt_interval=jr.ckpt_interval,
-                                         reason="user JobResource")
+                                         allreduce=jr.allreduce, reason="user JobResource")
                 wr = jr.roles.get("worker")
                 if wr is not None and self.job.mode == "allreduce":
                     master.rdzv.target_nodes = wr.replicas
@@ -113,7 +120,8 @@ class PlanLoop:
             prof = profs.get(n.split(":")[0])
             if prof is not None:
                 metrics[n] = dict(metrics[n], rocprof=prof)
-        newp = self.brain.next_plan(self.features(), self.plan, metrics)
+        comm = master.kv.get("comm/probe")     # KV.get decodes JSON
+        newp = self.brain.next_plan(self.features(), self.plan, metrics, comm if isinstance(comm, dict) else None)
         if newp is None:
             return
         master.events.emit("replan", reason=newp.reason)

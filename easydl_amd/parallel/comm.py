@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import datetime
 import logging
+import math
 import os
 import threading
 import time
@@ -60,6 +61,7 @@ class Communicator:
         self.xgmi = None
         self.xgmi_mode = None
         self.xgmi_probe: dict | None = None
+        self.allreduce_policy: dict | None = None
         self._aborted = False
         self._lock = threading.Lock()
         # debug: verify every rank issues the same collective sequence (the classic
@@ -149,18 +151,20 @@ class Communicator:
             self._probe_xgmi()
         return time.perf_counter() - t0
 
-    PROBE_MB = (4, 32, 128)
+    PROBE_KB = (256, 1024, 4096, 32768, 131072)
+    ONESHOT_PROBE_KB = 4096     # one-shot is timed up to this size (it reads N x S per rank)
 
     def _probe_xgmi(self, sizes_mb=None, iters: int = 3) -> None:
-        """Measure the xGMI engine against RCCL on THIS node at gradient-bucket sizes, in
-        both of its forms (in place on a registered buffer, and staged through the
-        workspace for buffers too large to map), and keep each form for the sizes where
-        every rank saw an exact result and it was faster everywhere (integer-valued
-        data: both sums are exact).  The per-size table is the communication policy:
-        all-reduces >= ``xgmi_min_bytes`` (registered) / ``xgmi_min_bytes_staged`` use
-        the engine, smaller ones RCCL."""
-        sizes_mb = tuple(sizes_mb or self.PROBE_MB)
-        nel = (max(sizes_mb) << 20) // 2
+        """Measure the xGMI engine against RCCL on THIS node from latency-bound to
+        gradient-bucket sizes, in each of its forms (one-shot; two-shot in place on a
+        registered buffer; two-shot staged through the workspace for buffers too large
+        to map), on integer-valued data so every sum is exact.  The engine is kept only
+        if every rank saw an exact result; the policy (one-shot switch sizes, the size
+        from which each form beats RCCL) comes from :func:`comm_policy.decide` on the
+        per-size MAX over ranks, so every rank derives the same policy."""
+        from easydl_amd.parallel import comm_policy
+        sizes_kb = tuple(int(m * 1024) for m in sizes_mb) if sizes_mb else self.PROBE_KB
+        nel = (max(sizes_kb) << 10) // 2
         g = torch.Generator(device="cpu").manual_seed(7 + self.rank)
         src = torch.randint(-4, 5, (nel,), generator=g, dtype=torch.int8).to(self.device, torch.bfloat16)
         a, b = src.clone(), src.clone()
@@ -185,61 +189,61 @@ class Communicator:
                 log.warning("xGMI probe: exactness check failed: %s", e)
                 bad = 1.0
             bad = float(self.ctrl_all_reduce([bad], dist.ReduceOp.MAX)[0])
-        table = []
+        inf = float("inf")
+        n = len(sizes_kb)
+        cols = [[inf] * n for _ in range(4)]     # rccl, in place, staged, one-shot (seconds)
         if not bad:
-            def timed(fn, t):
+            def timed(fn, t, it):
                 fn(t)
                 self._sync_stream()
                 t0 = time.perf_counter()
-                for _ in range(iters):
+                for _ in range(it):
                     fn(t)
                 self._sync_stream()
-                return (time.perf_counter() - t0) / iters
+                return (time.perf_counter() - t0) / it
 
-            for mb in sizes_mb:
-                view = b[:(mb << 20) // 2]
-                try:
-                    t_r = timed(lambda t: self.data.allreduce([t]).wait(), view)
-                    t_x = timed(self.xgmi.all_reduce, view)                      # in place (registered)
-                    t_s = timed(lambda t: self.xgmi.all_reduce(t, "twoshot"), view)   # staged
-                except Exception as e:  # noqa: BLE001
-                    log.warning("xGMI probe: timing at %d MB failed: %s", mb, e)
-                    t_r, t_x, t_s = 1.0, float("inf"), float("inf")
-                table.append((mb, t_r, t_x, t_s))
+            forms = (lambda t: self.data.allreduce([t]).wait(),
+                     lambda t: self.xgmi.all_reduce(t, "inplace"),
+                     lambda t: self.xgmi.all_reduce(t, "twoshot"),
+                     lambda t: self.xgmi.all_reduce(t, "oneshot"))
+            for i, kb in enumerate(sizes_kb):
+                view = b[:(kb << 10) // 2]
+                it = iters if kb > 1024 else 4 * iters      # latency-bound sizes: more samples
+                for c, fn in enumerate(forms):
+                    if c == 3 and kb > self.ONESHOT_PROBE_KB:
+                        continue
+                    try:
+                        cols[c][i] = timed(fn, view, it)
+                    except Exception as e:  # noqa: BLE001
+                        log.warning("xGMI probe: form %d at %d KB failed: %s", c, kb, e)
+                        if c == 0:
+                            cols[0][i] = 0.0
             try:
                 bad = 0.0 if self.xgmi.status() == 0 else 1.0
             except Exception:  # noqa: BLE001
                 bad = 1.0
         self.xgmi.timeout_s = keep_timeout
-        n = len(sizes_mb)
-        diffs = ([min(tx - tr, 1e9) for _, tr, tx, _ in table] + [min(ts - tr, 1e9) for _, tr, _, ts in table]
-                 if table else [0.0] * (2 * n))
-        worst = self.ctrl_all_reduce([bad] + diffs, dist.ReduceOp.MAX)
+        big = 1e9    # inf does not travel through the control plane's tensors cleanly
+        flat = [bad] + [min(v, big) for col in cols for v in col]
+        worst = self.ctrl_all_reduce(flat, dist.ReduceOp.MAX)
         exact = worst[0] == 0
-
-        def first_win(col):
-            """Smallest probed size from which the engine wins at every larger probed size."""
-            out = None
-            if exact and table:
-                for i in range(n - 1, -1, -1):
-                    if worst[1 + col * n + i] < 0:
-                        out = table[i][0]
-                    else:
-                        break
-            return out
-
-        min_inplace, min_staged = first_win(0), first_win(1)
-        keep = min_inplace is not None or min_staged is not None
-        bw = lambda m, t: round(2 * (self.world_size - 1) / self.world_size * (m << 20) / t / 1e9, 1)  # noqa: E731
+        cols = [[inf if float(v) >= big else float(v) for v in worst[1 + c * n:1 + (c + 1) * n]] for c in range(4)]
+        pol = (comm_policy.decide(sizes_kb, *cols, world=self.world_size) if exact
+               else {"oneshot_max_kb": None, "oneshot_max_staged_kb": None, "xgmi_min_kb_inplace": None,
+                     "xgmi_min_kb_staged": None, "bucket_floor_mb": None, "busbw_gbs": []})
+        keep = exact and (pol["xgmi_min_kb_inplace"] is not None or pol["xgmi_min_kb_staged"] is not None)
+        ms = lambda col: [round(v * 1e3, 4) if math.isfinite(v) else None for v in col] if exact else []  # noqa: E731
+        bw = lambda col: [round(comm_policy.busbw_gbs(k, v, self.world_size), 1)  # noqa: E731
+                          for k, v in zip(sizes_kb, col)] if exact else []
+        mb = lambda kb: None if kb is None else kb / 1024.0  # noqa: E731
         self.xgmi_probe = {
-            "sizes_mb": [r[0] for r in table],
-            "rccl_ms": [round(r[1] * 1e3, 3) for r in table],
-            "xgmi_inplace_ms": [round(r[2] * 1e3, 3) for r in table],
-            "xgmi_staged_ms": [round(r[3] * 1e3, 3) for r in table],
-            "rccl_busbw_gbs": [bw(r[0], r[1]) for r in table],
-            "xgmi_inplace_busbw_gbs": [bw(r[0], r[2]) for r in table],
-            "xgmi_staged_busbw_gbs": [bw(r[0], r[3]) for r in table],
-            "exact_everywhere": bool(exact), "xgmi_min_mb_inplace": min_inplace, "xgmi_min_mb_staged": min_staged,
+            "epoch": self.epoch, "world": self.world_size,
+            "sizes_kb": list(sizes_kb) if exact else [], "sizes_mb": [k / 1024.0 for k in sizes_kb] if exact else [],
+            "rccl_ms": ms(cols[0]), "xgmi_inplace_ms": ms(cols[1]), "xgmi_staged_ms": ms(cols[2]),
+            "xgmi_oneshot_ms": ms(cols[3]),
+            "rccl_busbw_gbs": bw(cols[0]), "xgmi_inplace_busbw_gbs": bw(cols[1]), "xgmi_staged_busbw_gbs": bw(cols[2]),
+            "exact_everywhere": bool(exact), "policy": pol,
+            "xgmi_min_mb_inplace": mb(pol["xgmi_min_kb_inplace"]), "xgmi_min_mb_staged": mb(pol["xgmi_min_kb_staged"]),
             "selected": "xgmi" if keep else "rccl"}
         log.info("all-reduce probe (epoch %d, world %d): %s", self.epoch, self.world_size, self.xgmi_probe)
         if reg is not None:
@@ -248,18 +252,30 @@ class Communicator:
         if keep:
             self.xgmi_mode = "xgmi"
             self.backend = "rccl+xgmi"
-            # winning from the smallest probed size on: every size of that path goes to the
-            # engine; otherwise only messages at least as large as the first winning size
-            never = 1 << 62
-            self.xgmi_min_bytes = (0 if min_inplace == sizes_mb[0] else
-                                   (min_inplace << 20) if min_inplace is not None else never)
-            self.xgmi_min_bytes_staged = (0 if min_staged == sizes_mb[0] else
-                                          (min_staged << 20) if min_staged is not None else never)
+            self.apply_allreduce_policy(pol)
         else:
             self._sync_stream()
             self.xgmi.close()
             self.xgmi = None
             self.xgmi_mode = None
+
+    def apply_allreduce_policy(self, pol: dict) -> bool:
+        """Switch the per-size routing (RCCL / engine form) to ``pol`` (see
+        :func:`comm_policy.decide`).  Every rank must apply the same policy before the
+        same collective: callers switch at an agreed point (the probe's control-plane
+        agreement, or a committed step for the Brain's runtime plan)."""
+        if self.xgmi is None or self.xgmi_mode != "xgmi":
+            return False
+        never = 1 << 62
+        kb = lambda k: never if k is None else int(k) << 10  # noqa: E731
+        self.xgmi_min_bytes = kb(pol.get("xgmi_min_kb_inplace"))
+        self.xgmi_min_bytes_staged = kb(pol.get("xgmi_min_kb_staged"))
+        if pol.get("oneshot_max_kb") is not None:
+            self.xgmi.oneshot_max = int(pol["oneshot_max_kb"]) << 10
+        if pol.get("oneshot_max_staged_kb") is not None:
+            self.xgmi.oneshot_max_staged = int(pol["oneshot_max_staged_kb"]) << 10
+        self.allreduce_policy = dict(pol)
+        return True
 
     def register_buffers(self, tensors) -> None:
         """Long-lived buffers every rank registers in the same order (ElasticDDP's flat

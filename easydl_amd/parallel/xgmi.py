@@ -68,7 +68,11 @@ class _Registered:
 
 
 class XgmiComm:
-    ONESHOT_MAX = 512 << 10      # bytes: below this latency dominates -> one-shot
+    # bytes: below this latency dominates -> one-shot.  The epoch's probe (and the Brain's
+    # runtime plan) overwrite the per-instance switch sizes with measured crossovers
+    # (parallel/comm_policy.py): ``oneshot_max`` against the in-place two-shot on
+    # registered buffers, ``oneshot_max_staged`` against the staged two-shot
+    ONESHOT_MAX = 512 << 10
     DEFAULT_WS = 128 << 20       # per parity: one 128 MiB bucket / TP message per launch
     # hipIpcOpenMemHandle of a caching-allocator segment of >= 2 GiB never returns on the
     # box (2040 MiB opens in ms, 2056 MiB hangs: profiles/r03_ipc_size_probe*.txt), so a
@@ -122,6 +126,7 @@ class XgmiComm:
         self.blocks = max(1, min(hw, cap))
         # bucket all-reduces overlap backward: a bounded share of CUs (Brain-tunable)
         self.async_blocks = max(1, min(self.blocks, int(os.environ.get("EDL_XGMI_ASYNC_BLOCKS", 64))))
+        self.oneshot_max = self.oneshot_max_staged = self.ONESHOT_MAX
         self._aborted = False
         self._registered: list[_Registered] = []
         self._opened: dict[tuple[int, bytes], list] = {}   # (peer, handle) -> [mapped base, refcount]
@@ -304,7 +309,7 @@ class XgmiComm:
         stream = torch.cuda.current_stream(self.device).cuda_stream
         nbytes_all = flat.numel() * es
         reg, off = self._find_registered(t) if algo in (None, "inplace") else (None, 0)
-        if reg is not None and (nbytes_all > self.ONESHOT_MAX or algo == "inplace"):
+        if reg is not None and (nbytes_all > self.oneshot_max or algo == "inplace"):
             bufs = (ctypes.c_void_p * self.world_size)(*[p + off for p in reg.peers])
             nvec = nbytes_all // 16
             blocks = int(max(1, min(max_blocks, -(-nvec // (self.world_size * 1024)))))
@@ -316,10 +321,11 @@ class XgmiComm:
                 raise XgmiError(f"launch failed: hipError {rc}")
             return t
         piece = (self.ws_bytes // 16) * 16 // es
+        os_max = self.oneshot_max if reg is not None else self.oneshot_max_staged
         for lo in range(0, flat.numel(), piece):
             part = flat[lo:lo + piece]
             nbytes = part.numel() * es
-            a = (0 if nbytes <= self.ONESHOT_MAX else 1) if algo in (None, "inplace") else \
+            a = (0 if nbytes <= os_max else 1) if algo in (None, "inplace") else \
                 (0 if algo == "oneshot" else 1)
             nvec = nbytes // 16
             per_block = 2048 if a == 0 else 4096  # 16-byte vectors per workgroup before adding workgroups

@@ -24,6 +24,7 @@ Usage::
 """
 from __future__ import annotations
 
+import json
 import logging
 import os
 import threading
@@ -272,7 +273,36 @@ class ElasticTrainer:
             self.events.emit("state_transferred", epoch=self.comm.epoch, step=self.step)
             self.ddp.set_comm(self.dp_comm)   # binds the epoch's comm (registers gradient buffers)
             self.events.emit("state_synced", epoch=self.comm.epoch, step=self.step)
+            if self.rdzv is not None:
+                try:
+                    self._publish_probe()
+                    self._agree_runtime_plan()
+                except (CommAborted, RuntimeError) as e:
+                    if not (self.comm.aborted or self.rdzv.aborted(self.comm.epoch) or _is_comm_error(e)):
+                        raise
+                    self.events.emit("epoch_skipped", epoch=self.comm.epoch, during="runtime_plan")
+                    self.comm.abort()
+                    continue
             return
+
+    def _publish_probe(self) -> None:
+        """The epoch's RCCL-vs-engine table goes to the Brain (``comm/probe``): rank 0 only."""
+        probe = getattr(self.dp_comm, "xgmi_probe", None)
+        if probe and self.comm.rank == 0:
+            doc = {"epoch": self.comm.epoch, "world": self.dp_comm.world_size, "probe": probe}
+            self.kv.set("comm/probe", json.dumps(doc))
+            self.events.emit("allreduce_probe", epoch=self.comm.epoch, world=self.dp_comm.world_size,
+                             selected=probe.get("selected"), policy=probe.get("policy"))
+
+    def _agree_runtime_plan(self) -> None:
+        """Every rank of the new epoch switches to the same runtime plan: the highest plan
+        version any of them sees.  Joiners and survivors re-apply it alike, so the
+        Brain's all-reduce policy (which the epoch's own probe just replaced) holds
+        on every rank, not only on the survivors."""
+        seen = float(self.kv.counter("plan/version"))
+        v = int(self.comm.ctrl_all_reduce([seen], dist.ReduceOp.MAX)[0])
+        if v > 0:
+            self._apply_runtime_plan(v)
 
     def _build_comm(self, a):
         """Arrival barrier, then construct + warm up the epoch's communicator.
@@ -600,15 +630,24 @@ class ElasticTrainer:
         return self
 
     def _apply_runtime_plan(self, version: int) -> None:
-        """Brain runtime knobs, switched by every rank at the same committed step."""
+        """Brain runtime knobs of plan ``version`` (master/planner.py writes one document
+        per version), switched by every rank at the same committed step or epoch entry."""
         self.plan_version = version
-        mb = self.kv.get("plan/bucket_mb")
+        doc = self.kv.get(f"plan/runtime/{version}")
+        if not isinstance(doc, dict):
+            return
+        mb = doc.get("bucket_mb")
         if mb and float(mb) != self.ddp.bucket_mb:
             self.ddp.set_bucket_mb(float(mb))
             self.events.emit("plan_bucket_mb", mb=float(mb), step=self.step)
-        ci = self.kv.get("plan/ckpt_interval")
+        ci = doc.get("ckpt_interval")
         if ci and self.checkpoint is not None:
             self.checkpoint.interval = max(1, int(ci))
+        ar = doc.get("allreduce")
+        apply = getattr(self.dp_comm, "apply_allreduce_policy", None)
+        if ar and apply is not None and int(ar.get("world", -1)) == self.dp_comm.world_size:
+            if apply(ar["policy"]):
+                self.events.emit("plan_allreduce", step=self.step, world=ar["world"], policy=ar["policy"])
 
     def _reconfigure(self):
         old = self.comm

@@ -39,7 +39,8 @@ for g in (tr.flat.groups if tr.flat is not None else []):
 res = {"index": tr.ctx.index, "step": tr.step, "hash": h.hexdigest(), "tp_rank": tr.held_tp,
        "dp_rank": tr.dp_comm.rank if tr.dp_comm is not None else None,
        "worlds": [r["world"] for r in tr.history], "epochs": [r["epoch"] for r in tr.history],
-       "loss": float(tr.last_loss) if tr.last_loss is not None else None}
+       "loss": float(tr.last_loss) if tr.last_loss is not None else None,
+       "bucket_mb": tr.ddp.bucket_mb if tr.ddp is not None else None, "plan_version": tr.plan_version}
 out = os.environ.get("TEST_OUT") or os.path.join(os.environ["EDL_RUN_DIR"], f"res{tr.ctx.index}-{os.getpid()}.json")
 with open(out, "w") as f:
     json.dump(res, f)

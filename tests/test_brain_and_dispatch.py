@@ -144,3 +144,111 @@ def test_amdsmi_samples_give_link_rates_throttle_share_and_busy_by_hbm():
                         cpus=128, host_mem_gb=2048)
     nxt = Planner().next_plan(JobFeatures(params=8e9, max_workers=8), inv, _plan(workers=4), {})
     assert nxt is not None and nxt.roles["worker"].replicas == 6
+
+
+def _probe(epoch, world, rccl, inplace, exact=True):
+    kb = [1024, 4096, 32768, 131072]
+    return {"epoch": epoch, "world": world,
+            "probe": {"sizes_kb": kb, "exact_everywhere": exact, "rccl_ms": rccl, "xgmi_inplace_ms": inplace,
+                      "xgmi_staged_ms": [9.0] * 4, "xgmi_oneshot_ms": [0.02, None, None, None]}}
+
+
+def test_brain_allreduce_policy_from_probe_median_and_bucket_knee():
+    """The epochs' probe tables drive the all-reduce routing and the bucket floor:
+    the policy follows the per-size MEDIAN (one noisy epoch does not flip it), a
+    narrow engine win inside the margin stays with RCCL, and bucket sizes below the
+    bandwidth knee are not tried."""
+    p = Planner()
+    feat = JobFeatures(params=8e9, max_workers=8)
+    rccl = [0.040, 0.080, 0.400, 1.500]
+    good = [0.045, 0.060, 0.300, 1.100]          # engine wins from 4 MB, one-shot at 1 MB
+    plan = _plan(workers=8, bucket=32.0)
+    m = {f"w{i}": {"step_time": 1.0, "window": 20} for i in range(8)}
+    nxt = p.next_plan(feat, _inv(8, busy=90), plan, m, _probe(1, 8, rccl, good))
+    assert nxt is not None and nxt.allreduce["world"] == 8
+    pol = nxt.allreduce["policy"]
+    assert pol["oneshot_max_kb"] == 1024 and pol["xgmi_min_kb_inplace"] == 0
+    assert pol["xgmi_min_kb_staged"] is None and pol["oneshot_max_staged_kb"] == 1024
+    assert pol["bucket_floor_mb"] == 32.0 and nxt.bucket_mb >= 32.0     # autotune goes on above the floor
+    plan = nxt
+    # one epoch where the engine looked slow everywhere: the median keeps the policy
+    nxt = p.next_plan(feat, _inv(8, busy=90), plan, m, _probe(2, 8, rccl, [9.0] * 4))
+    assert nxt is None or nxt.allreduce == plan.allreduce
+    # narrow wins (< 3 %) at 4..128 MB: the per-epoch probe (no margin) would route them to
+    # the engine, the Brain's policy keeps them on RCCL
+    from easydl_amd.parallel.comm_policy import decide_from_probe
+    narrow = [0.045, 0.079, 0.395, 1.49]
+    assert decide_from_probe(_probe(0, 8, rccl, narrow)["probe"], 8)["xgmi_min_kb_inplace"] == 0
+    p2 = Planner()
+    nxt = p2.next_plan(feat, _inv(8, busy=90), _plan(workers=8), m, _probe(0, 8, rccl, narrow))
+    assert nxt.allreduce["policy"]["xgmi_min_kb_inplace"] is None, nxt.allreduce
+    # inexact probes are never used
+    p3 = Planner()
+    assert p3.next_plan(feat, _inv(8, busy=90), _plan(workers=8), {}, _probe(0, 8, rccl, good, exact=False)) is None
+
+
+def test_brain_bucket_floor_skips_sizes_below_the_knee():
+    p = Planner()
+    feat = JobFeatures(params=8e9, max_workers=8)
+    # RCCL only: bus bandwidth keeps rising to 128 MB -> 32/64 MB buckets are below 85 %
+    rccl = [0.040, 0.080, 0.700, 1.500]
+    plan = _plan(workers=8, bucket=32.0)
+    m = {f"w{i}": {"step_time": 1.0, "window": 20} for i in range(8)}
+    nxt = p.next_plan(feat, _inv(8, busy=90), plan, m, _probe(1, 8, rccl, [9.0] * 4))
+    assert nxt is not None and nxt.allreduce["policy"]["xgmi_min_kb_inplace"] in (0, None)
+    floor = nxt.allreduce["policy"]["bucket_floor_mb"]
+    assert floor == 128.0 and nxt.bucket_mb == 128.0, (floor, nxt.reason)
+
+
+def test_plan_loop_writes_one_versioned_runtime_document(tmp_path):
+    """master/planner.py: the plan's knobs (bucket, interval, all-reduce policy) go to
+    plan/runtime/<v> before plan/version moves to v; the probe reaches the Brain."""
+    import json
+    from easydl_amd.api.spec import ElasticJob
+    from easydl_amd.master.planner import PlanLoop
+
+    kv = _kv()
+
+    class Rdzv:
+        target_nodes = 0
+
+        def members(self):
+            return [f"w{i}" for i in range(8)]
+
+    class Events:
+        def emit(self, *a, **k):
+            pass
+
+    class Master:
+        pass
+
+    master = Master()
+    master.kv, master.rdzv, master.events, master.run_dir = kv, Rdzv(), Events(), str(tmp_path)
+
+    class Brain:
+        def __init__(self):
+            self.p = Planner()
+
+        def startup_plan(self, features):
+            return _plan(workers=8, bucket=32.0)
+
+        def next_plan(self, features, plan, metrics, comm=None):
+            return self.p.next_plan(JobFeatures(params=8e9, max_workers=8), _inv(8, busy=90), plan, metrics, comm)
+
+    job = ElasticJob.from_dict({"apiVersion": "elastic.easydl.org/v1alpha1", "kind": "ElasticJob",
+                                "metadata": {"name": "t"}, "spec": {"worker": {"image": "x"}}})
+    loop = PlanLoop(job, Brain(), period_s=0.001, user_wait_s=0.0)
+    loop._features = {}
+    loop.maybe_replan(master)                 # startup plan -> version 1
+    assert kv.counter("plan/version") == 1
+    assert kv.get("plan/runtime/1")["bucket_mb"] == 32.0
+    for i in range(8):
+        kv.set(f"metrics/w{i}", json.dumps({"step_time": 1.0, "window": 20}))
+    kv.set("comm/probe", json.dumps(_probe(1, 8, [0.040, 0.080, 0.400, 1.500], [0.045, 0.060, 0.300, 1.100])))
+    import time
+    time.sleep(0.01)
+    loop.maybe_replan(master)
+    assert kv.counter("plan/version") == 2
+    doc = kv.get("plan/runtime/2")
+    assert doc["allreduce"]["world"] == 8 and doc["allreduce"]["policy"]["oneshot_max_kb"] == 1024
+    assert json.loads(kv.get_str("jobresource"))["spec"]["allreduce"] == doc["allreduce"]

@@ -126,3 +126,73 @@ def test_transfer_state_multi_source(world, holders):
         return all(torch.equal(t, mk(seed, n, dt)) for t, (seed, n, dt) in zip(ts, specs))
 
     assert all(_spawn(world, fn).values())
+
+
+# --- the policy function shared by the per-epoch probe and the Brain ------------------
+
+def test_decide_oneshot_crossover_first_win_and_bucket_knee():
+    from easydl_amd.parallel.comm_policy import decide
+    inf = float("inf")
+    kb = [256, 1024, 4096, 32768, 131072]
+    us = 1e-6
+    rccl = [30 * us, 40 * us, 80 * us, 400 * us, 1500 * us]
+    inplace = [35 * us, 38 * us, 60 * us, 300 * us, 1100 * us]
+    staged = [40 * us, 50 * us, 90 * us, 420 * us, 1700 * us]
+    oneshot = [12 * us, 30 * us, 95 * us, inf, inf]
+    p = decide(kb, rccl, inplace, staged, oneshot, world=8)
+    # one-shot beats the in-place two-shot up to 1 MB, the staged one up to 1 MB as well
+    assert p["oneshot_max_kb"] == 1024 and p["oneshot_max_staged_kb"] == 1024
+    # registered path: 12 < 30, 30 < 40, 60 < 80, ... -> engine everywhere
+    assert p["xgmi_min_kb_inplace"] == 0
+    # staged: wins at 256 KB and 1 MB (one-shot) but loses from 4 MB on -> never
+    assert p["xgmi_min_kb_staged"] is None
+    # bandwidth knee: 128 MB is best (213 GB/s); 32 MB reaches 196 GB/s (> 85 %), 4 MB 122 GB/s
+    bw = p["busbw_gbs"]
+    assert bw[-1] == max(bw) and p["bucket_floor_mb"] == 32.0
+    # a margin in RCCL's favour removes narrow wins (60 vs 80 us survives 10 %, 38 vs 40 does not)
+    p = decide(kb, rccl, inplace, staged, [inf] * 5, world=8, margin=0.1)
+    assert p["oneshot_max_kb"] == 0 and p["xgmi_min_kb_inplace"] == 4096
+
+
+def test_median_table_ignores_inexact_and_mismatched_probes():
+    from easydl_amd.parallel.comm_policy import median_table
+    base = {"sizes_kb": [1024, 4096], "exact_everywhere": True, "xgmi_staged_ms": [1, 1], "xgmi_oneshot_ms": [1, None]}
+    probes = [dict(base, sizes_kb=[1], rccl_ms=[5.0], xgmi_inplace_ms=[5.0]),     # older size grid: dropped
+              dict(base, rccl_ms=[1.0, 2.0], xgmi_inplace_ms=[0.5, 9.0]),
+              dict(base, rccl_ms=[3.0, 2.0], xgmi_inplace_ms=[0.7, 1.0]),
+              dict(base, rccl_ms=[2.0, 2.0], xgmi_inplace_ms=[0.6, 1.0]),
+              dict(base, rccl_ms=[99.0, 99.0], xgmi_inplace_ms=[0.1, 0.1], exact_everywhere=False)]
+    t = median_table(probes)
+    assert t is not None and t["n"] == 3 and t["sizes_kb"] == [1024, 4096]
+    assert t["rccl_ms"] == [2.0, 2.0] and t["xgmi_inplace_ms"] == [0.6, 1.0]
+    assert t["xgmi_oneshot_ms"][1] == float("inf")
+
+
+def test_apply_allreduce_policy_routes_by_size():
+    def fn(c, st):
+        eng = FakeEngine(c, lambda nb: 0.0)
+        eng.oneshot_max = eng.oneshot_max_staged = 0
+        c.xgmi, c.xgmi_mode = eng, "xgmi"
+        ok = c.apply_allreduce_policy({"xgmi_min_kb_inplace": 4096, "xgmi_min_kb_staged": None,
+                                       "oneshot_max_kb": 512, "oneshot_max_staged_kb": 256})
+        small = torch.zeros((1 << 20) // 4)         # 1 MB: RCCL
+        big = torch.zeros((8 << 20) // 4)           # 8 MB: the engine (unregistered -> staged rule)
+        return ok, c.xgmi_min_bytes, c.xgmi_min_bytes_staged, eng.oneshot_max, eng.oneshot_max_staged, \
+            c._use_xgmi_allreduce(small), c._use_xgmi_allreduce(big)
+
+    for ok, mi, ms, om, oms, u_small, u_big in _spawn(2, fn).values():
+        assert ok and mi == 4 << 20 and ms == 1 << 62 and om == 512 << 10 and oms == 256 << 10
+        assert not u_small and not u_big    # unregistered: staged rule says never
+
+
+def test_probe_publishes_policy_with_oneshot_column():
+    def fn(c, st):
+        eng = FakeEngine(c, lambda nb: 0.0 if nb > (3 << 20) else 0.05)
+        c.xgmi, c.xgmi_mode = eng, "auto"
+        c._probe_xgmi(sizes_mb=(2, 4, 8), iters=1)
+        return c.xgmi_probe, c.allreduce_policy
+
+    for probe, pol in _spawn(2, fn).values():
+        assert probe["sizes_kb"] == [2048, 4096, 8192]
+        assert probe["xgmi_oneshot_ms"][2] is None and probe["xgmi_oneshot_ms"][0] is not None
+        assert pol == probe["policy"] and pol["xgmi_min_kb_inplace"] == 4096

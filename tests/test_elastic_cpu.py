@@ -274,3 +274,42 @@ def test_snapshot_fenced_before_a_broadcast_rewrites_state():
        False)
     fn(SimpleNamespace(checkpoint=ck, device=torch.device("cpu")), SimpleNamespace(rank=1, backend="xgmi"), 0, False)
     assert not calls   # no checkpoint manager / CPU state: nothing to fence
+
+
+@pytest.mark.slow
+def test_runtime_plan_switches_every_rank_at_one_step(tmp_path):
+    """Brain runtime knobs (master/planner.py): one document per plan version; ranks
+    adopt the agreed version at epoch entry and switch at one committed step."""
+    from easydl_amd.master.store import KV, make_tcp_store
+    from easydl_amd.utils.events import read_events
+    port = free_port()
+    m = _start_master(tmp_path, port, 1, 2, initial=2)
+    try:
+        kv = KV(make_tcp_store("127.0.0.1", port, False), "edl/t")
+        kv.set("plan/runtime/1", json.dumps({"bucket_mb": 0.1, "ckpt_interval": None, "allreduce": None}))
+        kv.add("plan/version", 1)
+        procs = {}
+        for i in range(2):
+            env = _env(tmp_path, i, {"EDL_MASTER_ADDR": "127.0.0.1", "EDL_MASTER_PORT": str(port),
+                                     "TEST_STEPS": "40", "TEST_GB": "4", "TEST_STEP_SLEEP": "0.1"})
+            procs[i] = subprocess.Popen([sys.executable, WORKER], env=env, cwd=ROOT)
+
+        def applied(mb):
+            return {e.get("proc"): e.get("step") for e in read_events(str(tmp_path))
+                    if e["kind"] == "plan_bucket_mb" and e.get("mb") == mb}
+
+        t_end = time.time() + 120
+        while len(applied(0.1)) < 2 and time.time() < t_end:
+            time.sleep(0.1)
+        assert len(applied(0.1)) == 2, "version 1 not adopted at epoch entry"
+        kv.set("plan/runtime/2", json.dumps({"bucket_mb": 0.05, "ckpt_interval": None, "allreduce": None}))
+        kv.add("plan/version", 1)
+        codes = _wait(procs)
+        assert codes == {0: 0, 1: 0}, codes
+        r = _results(tmp_path, [0, 1])
+        assert r[0]["hash"] == r[1]["hash"]
+        assert r[0]["bucket_mb"] == r[1]["bucket_mb"] == 0.05 and r[0]["plan_version"] == r[1]["plan_version"] == 2
+        steps = applied(0.05)
+        assert len(steps) == 2 and len(set(steps.values())) == 1, steps   # the same committed step
+    finally:
+        m.terminate()
