@@ -33,7 +33,7 @@ def worker():
     from easydl_amd.parallel.xgmi import XgmiComm
 
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
-    sizes = [int(x) for x in os.environ["XB_MB"].split(",")]
+    sizes = [float(x) for x in os.environ["XB_MB"].split(",")]
     iters = int(os.environ["XB_ITERS"])
     torch.cuda.set_device(0)
     st = dist.TCPStore("127.0.0.1", int(os.environ["PORT"]), world, rank == 0, timeout=datetime.timedelta(seconds=60))
@@ -46,14 +46,17 @@ def worker():
         st.set(f"{tag}{n}/{rank}", "1")
         st.wait([f"{tag}{n}/{r}" for r in range(world)])
 
-    buf = torch.ones((max(sizes) << 20) // 2, dtype=torch.bfloat16, device="cuda")
+    buf = torch.ones(int(max(sizes) * (1 << 20)) // 2, dtype=torch.bfloat16, device="cuda")
     reg = x.register(buf)
     res = []
     for mb in sizes:
-        view = buf[:(mb << 20) // 2]
-        for algo, fn in (("inplace", lambda: x.all_reduce(view, "inplace")),
-                         ("staged", lambda: x.all_reduce(view, "twoshot")),
-                         ("pull", lambda: x.pull([view], [0]))):
+        view = buf[:int(mb * (1 << 20)) // 2]
+        forms = [("inplace", lambda: x.all_reduce(view, "inplace")),
+                 ("staged", lambda: x.all_reduce(view, "twoshot")),
+                 ("pull", lambda: x.pull([view], [0]))]
+        if mb <= 4:
+            forms.append(("oneshot", lambda: x.all_reduce(view, "oneshot")))
+        for algo, fn in forms:
             fn()
             torch.cuda.synchronize()
             sync("w")
@@ -76,7 +79,7 @@ def worker():
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ranks", type=int, nargs="+", default=[2, 4])
-    ap.add_argument("--mb", type=int, nargs="+", default=[16, 128])
+    ap.add_argument("--mb", type=float, nargs="+", default=[16, 128])
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
@@ -95,10 +98,12 @@ def main():
             raise SystemExit(f"world {world}: worker failed {[p.returncode for p in procs]}")
         d = json.loads([ln for ln in outs[0].splitlines() if ln.startswith("{")][0])
         for r in d["res"]:
-            S = r["mb"] << 20
+            S = r["mb"] * (1 << 20)
             t = r["ms"] / 1e3
             if r["algo"] == "pull":
                 traffic = 2 * (world - 1) * S          # every receiver reads S and writes S
+            elif r["algo"] == "oneshot":                # stage copy + every rank reads N x S
+                traffic = world * (2 * S + world * S + S)
             elif r["algo"] == "inplace":
                 traffic = world * (S + S / world + 2 * (world - 1) / world * S)
             else:                                       # staged: + stage copy (read S, write S)
