@@ -140,16 +140,20 @@ class LlamaBlock(nn.Module):
         # column-parallel projections, tp_reduce after the row-parallel ones
         self.tp_reduce = None
         self.tp_copy = None
+        # overlapped TP (parallel/tp.py): start(tensor) -> finish() all-reduce hooks used
+        # inside the GEMM ops instead of tp_copy / tp_reduce
+        self.tp_dx_reduce = None
+        self.tp_out_reduce = None
 
     def _attn(self, n1, B, S, cos, sin):
         hd = self.cfg.head_dim
         if self.tp_copy is not None:
             n1 = self.tp_copy(n1)
-        qkv = fused.linear(n1, self.wqkv)
+        qkv = fused.linear(n1, self.wqkv, dx_reduce=self.tp_dx_reduce)
         q, k, v = fused.rope_qkv(qkv, cos, sin, B, S, self.n_heads, self.n_kv, hd)
         o = attention(q, k, v, causal=True)
         o = o.transpose(1, 2).reshape(B * S, self.n_heads * hd)
-        a = fused.linear(o, self.wo)
+        a = fused.linear(o, self.wo, out_reduce=self.tp_out_reduce)
         if self.tp_reduce is not None:
             a = self.tp_reduce(a)
         return a
@@ -157,7 +161,8 @@ class LlamaBlock(nn.Module):
     def _mlp(self, n2):
         if self.tp_copy is not None:
             n2 = self.tp_copy(n2)
-        m = fused.swiglu_mlp(n2, self.w_gu, self.w_down)
+        m = fused.swiglu_mlp(n2, self.w_gu, self.w_down, dx_reduce=self.tp_dx_reduce,
+                             out_reduce=self.tp_out_reduce)
         if self.tp_reduce is not None:
             m = self.tp_reduce(m)
         return m

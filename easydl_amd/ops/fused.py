@@ -286,15 +286,48 @@ def _nt_wgrad_ok(dy2: torch.Tensor, x2: torch.Tensor) -> bool:
             and x2.shape[1] % 8 == 0)
 
 
+# Tensor-parallel overlap hooks (parallel/tp.py).  ``out_reduce``: the output of a
+# row-parallel GEMM is a partial sum; it is computed in row chunks and each chunk's
+# all-reduce starts (on the communicator's stream) while the next chunk's GEMM runs.
+# ``dx_reduce``: the input gradient of a column-parallel GEMM is a partial sum; its
+# all-reduce starts as soon as dX exists and runs under the weight-gradient GEMM(s).
+# Both are ``start(tensor) -> finish()`` callables: ``finish`` orders the compute
+# stream after the collective and returns the reduced tensor.
+_TP_CHUNK_ROWS = int(os.environ.get("EDL_TP_CHUNK_ROWS", 2048))
+
+
+def _chunked_reduced_mm(x2, w, start, out=None):
+    """``x2 @ w^T`` with each row chunk's all-reduce started behind its GEMM."""
+    M = x2.shape[0]
+    y = out if out is not None else torch.empty(M, w.shape[0], dtype=x2.dtype, device=x2.device)
+    n = max(1, min(8, M // max(8, _TP_CHUNK_ROWS)))
+    step = -(-M // n)
+    step = -(-step // 8) * 8
+    fins = []
+    for lo in range(0, M, step):
+        hi = min(M, lo + step)
+        torch.mm(x2[lo:hi], w.t(), out=y[lo:hi])
+        fins.append(start(y[lo:hi]))
+    for f in fins:
+        f()
+    return y
+
+
 class _LinearFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b):
+    def forward(ctx, x, w, b, dx_reduce=None, out_reduce=None):
         x2 = x.reshape(-1, x.shape[-1])
-        y = F.linear(x2, w, b)
+        if out_reduce is not None:
+            if b is not None:
+                raise ValueError("row-parallel linear with an output all-reduce takes no bias")
+            y = _chunked_reduced_mm(x2, w, out_reduce)
+        else:
+            y = F.linear(x2, w, b)
         wt = _wt_of(w) if ctx.needs_input_grad[0] else None
         ctx.save_for_backward(x2, w, wt)
         ctx.has_b = b is not None
         ctx.b = b
+        ctx.dx_reduce = dx_reduce
         return y.view(*x.shape[:-1], w.shape[0])
 
     @staticmethod
@@ -302,8 +335,11 @@ class _LinearFn(torch.autograd.Function):
         x2, w, wt = ctx.saved_tensors
         dy2 = dy.reshape(-1, dy.shape[-1])
         dx = None
+        fin = None
         if ctx.needs_input_grad[0]:
             dx = (torch.mm(dy2, wt.t()) if wt is not None else torch.mm(dy2, w)).view(*dy.shape[:-1], w.shape[1])
+            if ctx.dx_reduce is not None:
+                fin = ctx.dx_reduce(dx)      # runs under the weight-gradient GEMM below
         dw = db = None
         bias_partial = None   # (partial slab, G): bias gradient computed by the dY transpose
         want_db = ctx.has_b and ctx.needs_input_grad[2]
@@ -332,12 +368,15 @@ class _LinearFn(torch.autograd.Function):
                     gradsink.write(b, g)
                 else:
                     db = g.to(b.dtype)
-        return dx, dw, db
+        if fin is not None:
+            dx = fin()
+        return dx, dw, db, None, None
 
 
-def linear(x, w, b=None):
-    if _native.use_hip(x) or gradsink.is_flat(w):
-        return _LinearFn.apply(x, w, b)
+def linear(x, w, b=None, *, dx_reduce=None, out_reduce=None):
+    """``x @ w^T + b``; ``dx_reduce`` / ``out_reduce``: tensor-parallel overlap hooks (above)."""
+    if _native.use_hip(x) or gradsink.is_flat(w) or dx_reduce is not None or out_reduce is not None:
+        return _LinearFn.apply(x, w, b, dx_reduce, out_reduce)
     return F.linear(x, w, b)
 
 
@@ -420,7 +459,7 @@ class _SwiGLUMLPFn(torch.autograd.Function):
     in the 15 % slower TN form there)."""
 
     @staticmethod
-    def forward(ctx, x, w_gu, w_down):
+    def forward(ctx, x, w_gu, w_down, dx_reduce=None, out_reduce=None):
         k = _native.kernels()
         x2 = x.reshape(-1, x.shape[-1])
         gu = F.linear(x2, w_gu)
@@ -430,10 +469,11 @@ class _SwiGLUMLPFn(torch.autograd.Function):
         hT = torch.empty(Fh, M, dtype=gu.dtype, device=gu.device)
         st = _native.stream_of(gu)
         k.check("edl_swiglu_fwd_t", gu.data_ptr(), h.data_ptr(), hT.data_ptr(), M, Fh, st)
-        y = F.linear(h, w_down)
+        y = _chunked_reduced_mm(h, w_down, out_reduce) if out_reduce is not None else F.linear(h, w_down)
         del h
         wt_gu = _wt_of(w_gu) if ctx.needs_input_grad[0] else None
         ctx.save_for_backward(x2, gu, hT, w_gu, w_down, wt_gu, _wt_of(w_down))
+        ctx.dx_reduce = dx_reduce
         return y.view(*x.shape[:-1], w_down.shape[0])
 
     @staticmethod
@@ -445,28 +485,39 @@ class _SwiGLUMLPFn(torch.autograd.Function):
         Fh = F2 // 2
         st = _native.stream_of(gu)
         dh = torch.mm(dy2, wt_down.t()) if wt_down is not None else torch.mm(dy2, w_down)
-        dw_down = _deliver_wgrad(w_down, _transposed(dy2), hT.t())
-        del hT
+        overlap = ctx.dx_reduce is not None and ctx.needs_input_grad[0]
+        dw_down = None
+        if not overlap:
+            dw_down = _deliver_wgrad(w_down, _transposed(dy2), hT.t())
+            del hT
         dgu = torch.empty_like(gu)
         dguT = torch.empty(F2, M, dtype=gu.dtype, device=gu.device)
         k.check("edl_swiglu_bwd_t", dh.data_ptr(), gu.data_ptr(), dgu.data_ptr(), dguT.data_ptr(), M, Fh, st)
         del dh
-        dx = None
+        dx = fin = None
         if ctx.needs_input_grad[0]:
             dx = torch.mm(dgu, wt_gu.t()) if wt_gu is not None else torch.mm(dgu, w_gu)
             dx = dx.view(*dy.shape[:-1], w_gu.shape[1])
         del dgu
+        if overlap:
+            # tensor parallel: dX's all-reduce runs under BOTH weight-gradient GEMMs
+            fin = ctx.dx_reduce(dx)
+            dw_down = _deliver_wgrad(w_down, _transposed(dy2), hT.t())
+            del hT
         dw_gu = _deliver_wgrad(w_gu, dguT, _transposed(x2).t())
-        return dx, dw_gu, dw_down
+        if fin is not None:
+            dx = fin()
+        return dx, dw_gu, dw_down, None, None
 
 
-def swiglu_mlp(x, w_gu, w_down):
-    """Llama MLP ``down(silu(gate) * up)`` with ``w_gu`` = [gate; up] stacked on dim 0."""
+def swiglu_mlp(x, w_gu, w_down, *, dx_reduce=None, out_reduce=None):
+    """Llama MLP ``down(silu(gate) * up)`` with ``w_gu`` = [gate; up] stacked on dim 0.
+    ``dx_reduce`` / ``out_reduce``: tensor-parallel overlap hooks (see ``linear``)."""
     x2 = x.reshape(-1, x.shape[-1])
     if (_MLP_FUSED and _native.use_hip(x) and x.dtype == torch.bfloat16 and _nt_wgrad_ok(x2, x2)
             and x2.shape[0] % 8 == 0 and w_gu.shape[0] % 16 == 0):
-        return _SwiGLUMLPFn.apply(x, w_gu, w_down)
-    return linear(swiglu(linear(x, w_gu)), w_down)
+        return _SwiGLUMLPFn.apply(x, w_gu, w_down, dx_reduce, out_reduce)
+    return linear(swiglu(linear(x, w_gu, dx_reduce=dx_reduce)), w_down, out_reduce=out_reduce)
 
 
 def _bias_grad(k, b, partial, G, cols, stream):

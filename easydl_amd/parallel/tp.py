@@ -19,9 +19,16 @@ per block in each direction: [T, d] bf16 = 64 MiB at 4k tokens x d=8192 for
 70B — large messages that keep all 7 xGMI links of a node busy.
 Sequence parallelism (P4) swaps each all-reduce for reduce-scatter +
 all-gather over the token dimension (``sequence_parallel=True``).
+
+Without SP the collectives overlap compute (``EDL_TP_OVERLAP``, default on): a
+row-parallel GEMM runs in row chunks and each chunk's all-reduce starts on the
+communicator's stream while the next chunk multiplies; a column-parallel GEMM's
+input-gradient all-reduce starts as soon as dX exists and runs under the
+weight-gradient GEMMs (``fused.linear`` / ``fused.swiglu_mlp`` hooks).
 """
 from __future__ import annotations
 
+import os
 
 import torch
 import torch.nn as nn
@@ -56,6 +63,17 @@ class TPGroup:
         x = x.contiguous()
         self.comm.all_reduce(x)
         return x
+
+    def all_reduce_start(self, x: torch.Tensor):
+        """Start an in-place SUM of ``x`` (contiguous) on the communicator's stream;
+        returns ``finish()``, which orders the compute stream after it and returns x.
+        The overlap hooks of ``fused.linear`` / ``fused.swiglu_mlp`` use it."""
+        work = self.comm.all_reduce_async(x)
+
+        def finish():
+            self.comm.wait_work(work)
+            return x
+        return finish
 
     def all_reduce_max(self, x: torch.Tensor) -> torch.Tensor:
         if self.size == 1:
@@ -231,6 +249,7 @@ class LlamaTP(nn.Module):
             raise ValueError(f"config not divisible by tp={tp}")
         self.cfg, self.g = cfg, g
         self.vshard = cfg.vocab_size // tp
+        self.overlap = tp > 1 and not g.sequence_parallel and os.environ.get("EDL_TP_OVERLAP", "1") != "0"
         d = cfg.dim
         self.embed = _param((self.vshard, d), cfg.init_std, device, dtype)
         self.layers = nn.ModuleList()
@@ -243,6 +262,11 @@ class LlamaTP(nn.Module):
                 # row-parallel ones (same bytes as the all-reduce, 1/tp the activations)
                 blk.tp_reduce = lambda x, _g=g: scatter_to_sp(x, _g)
                 blk.tp_copy = lambda x, _g=g: gather_from_sp(x, _g)
+            elif self.overlap:
+                # the two all-reduces per block run beside GEMMs: the row-parallel outputs
+                # chunk by chunk behind their own GEMM, the column-parallel input gradients
+                # under the weight-gradient GEMMs (fused.linear / swiglu_mlp hooks)
+                blk.tp_out_reduce = blk.tp_dx_reduce = g.all_reduce_start
             else:
                 blk.tp_reduce = lambda x, _g=g: reduce_from_tp(x, _g)
                 blk.tp_copy = lambda x, _g=g: copy_to_tp(x, _g)
@@ -293,8 +317,11 @@ class LlamaTP(nn.Module):
         for layer in self.layers:
             resid, delta = layer(resid, delta, B, S, cos, sin)
         n, _ = norms.add_rmsnorm(delta, resid, self.norm, self.cfg.norm_eps)
-        n = gather_from_sp(n, self.g) if sp else copy_to_tp(n, self.g)
-        logits = fused.linear(n, self.lm_head)
+        if self.overlap:
+            logits = fused.linear(n, self.lm_head, dx_reduce=self.g.all_reduce_start)
+        else:
+            n = gather_from_sp(n, self.g) if sp else copy_to_tp(n, self.g)
+            logits = fused.linear(n, self.lm_head)
         if labels is None:
             return logits
         return vocab_parallel_cross_entropy(logits, labels, self.vstart, self.g)

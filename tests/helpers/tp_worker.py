@@ -24,6 +24,16 @@ labels = torch.randint(0, 128, (2, 16))
 loss_d = dense(ids, labels)
 loss_d.backward()
 g = TPGroup(comm, sequence_parallel=os.environ.get("SP") == "1")
+starts = [0]
+_start = g.all_reduce_start
+
+
+def counted_start(x):
+    starts[0] += 1
+    return _start(x)
+
+
+g.all_reduce_start = counted_start
 tp = LlamaTP(cfg, g, dtype=torch.float32)
 sd = shard_state_dict({k: v.detach() for k, v in dense.named_parameters()}, cfg, rank, world)
 with torch.no_grad():
@@ -35,6 +45,7 @@ tp.sync_sp_grads()
 dgrads = shard_state_dict({k: v.grad for k, v in dense.named_parameters()}, cfg, rank, world)
 err = max((p.grad - dgrads[n]).abs().max().item() / (dgrads[n].abs().max().item() + 1e-9)
           for n, p in tp.named_parameters())
-json.dump({"loss_d": loss_d.item(), "loss_t": loss_t.item(), "grad_rel_err": err},
+json.dump({"loss_d": loss_d.item(), "loss_t": loss_t.item(), "grad_rel_err": err, "overlap": tp.overlap,
+           "async_starts": starts[0]},
           open(os.environ["OUT"] + f".{rank}", "w"))
 comm.barrier()

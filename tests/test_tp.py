@@ -11,21 +11,26 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-@pytest.mark.parametrize("sp", ["0", "1"])
-def test_tp2_matches_dense(tmp_path, sp):
-    """sp=1: Megatron sequence parallelism (token-sharded residual stream and norms)."""
+@pytest.mark.parametrize("sp,overlap", [("0", "0"), ("0", "1"), ("1", "0")])
+def test_tp2_matches_dense(tmp_path, sp, overlap):
+    """sp=1: Megatron sequence parallelism (token-sharded residual stream and norms);
+    overlap=1: row-parallel outputs all-reduced chunk by chunk (8-row chunks here) and
+    column-parallel input gradients all-reduced under the weight-gradient GEMMs."""
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
     procs = [subprocess.Popen([sys.executable, os.path.join(ROOT, "tests/helpers/tp_worker.py")],
                               env=dict(os.environ, RANK=str(r), WORLD_SIZE="2", PORT=str(port),
-                                       OUT=str(tmp_path / "r"), PYTHONPATH=ROOT, SP=sp)) for r in range(2)]
+                                       OUT=str(tmp_path / "r"), PYTHONPATH=ROOT, SP=sp, EDL_TP_OVERLAP=overlap,
+                                       EDL_TP_CHUNK_ROWS="8")) for r in range(2)]
     assert [p.wait(timeout=120) for p in procs] == [0, 0]
     for r in range(2):
         res = json.load(open(tmp_path / f"r.{r}"))
         assert abs(res["loss_d"] - res["loss_t"]) < 1e-5, res
         assert res["grad_rel_err"] < 1e-4, res
+        # 2 layers x (2 row-parallel outputs in 4 chunks + 2 column-parallel dX) + LM-head dX
+        assert res["async_starts"] == (2 * (2 * 4 + 2) + 1 if overlap == "1" else 0), res
 
 
 class _ThreadGroup:
