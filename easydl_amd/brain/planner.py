@@ -76,6 +76,7 @@ class BrainConfig:
     bucket_choices: tuple = (32.0, 64.0, 128.0, 256.0, 512.0)
     ckpt_overhead: float = 0.05
     pcie_gbps: float = 50.0
+    snapshot_host_fraction: float = 0.8   # host DRAM the in-memory snapshot slots may take
     comm_margin: float = 0.03       # the engine must beat RCCL by this share to take a size
     comm_history: int = 8           # probe tables kept per world size
 
@@ -98,6 +99,24 @@ def ckpt_interval(params: float, world: int, step_time_s: float | None, cfg: Bra
     copy_s = per_rank_gb / cfg.pcie_gbps
     st = step_time_s or 1.0
     return max(1, int(math.ceil(copy_s / (cfg.ckpt_overhead * st))))
+
+
+def snapshot_mode(feat: JobFeatures, inv: NodeInventory, cfg: BrainConfig) -> str | None:
+    """Host-DRAM check for the node's A/B snapshot slots: DP ranks shard
+    the replicated state, TP ranks each hold a unique shard, so the node always holds
+    two copies of the whole state: 12 B/param (fp32 master + Adam moments), or 4 B/param
+    for lean (master-only) snapshots.  The trainers' CheckpointManager makes the same
+    decision from the live MemAvailable; this puts it in the plan up front."""
+    host = inv.host_mem_gb or feat.host_mem_gb
+    if not host or not feat.params or feat.mode == "ps":
+        return None
+    budget = cfg.snapshot_host_fraction * host
+    full, lean = 2 * 12 * feat.params / 2**30, 2 * 4 * feat.params / 2**30
+    if full <= budget:
+        return f"full ({full:.0f} of {host:.0f} GB host DRAM)"
+    if lean <= budget:
+        return f"lean: moments dropped ({lean:.0f} GB; full needs {full:.0f} of {host:.0f} GB)"
+    return f"off ({lean:.0f} GB even lean > {budget:.0f} GB)"
 
 
 class Planner:
@@ -146,6 +165,9 @@ class Planner:
         world = plan.roles["worker"].replicas
         plan.bucket_mb = grad_bucket_mb(feat.params, world)
         plan.ckpt_interval = ckpt_interval(feat.params, world, feat.step_time_s, self.cfg)
+        mode = snapshot_mode(feat, inv, self.cfg)
+        if mode is not None:
+            plan.reason += f"; in-memory snapshots {mode}"
         return plan
 
     @staticmethod

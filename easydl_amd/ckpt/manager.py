@@ -38,6 +38,7 @@ import time
 
 import numpy as np
 import torch
+import torch.distributed as dist
 
 from easydl_amd import _native
 
@@ -184,11 +185,33 @@ class CheckpointManager:
         persist_dir: if set, every ``persist_every`` snapshots are also written
             to ``<persist_dir>/step-<N>/`` in format v1 (background thread).
         sharded: each rank stores 1/W of the replicated state (DDP).
+        host_budget_gb: host DRAM one rank's two snapshot slots may take (default:
+            ``EDL_CKPT_HOST_GB``, else ``host_fraction`` of min(MemAvailable, free
+            /dev/shm) split over the node's ranks).
+        lean: "auto" | "never" | "always" — a lean snapshot keeps the weights
+            (fp32 master) and drops the optimizer moments (8 of AdamW's 12 B/param).
+
+    Host-DRAM sizing: a DDP rank snapshots 1/W of the replicated
+    state, but a tensor-parallel rank's shard is unique (Llama-3 70B at TP=8:
+    ~105 GB per rank of master + moments, ~1.7 TB for the node's A/B slots).  At
+    the first snapshot of each layout the DP group agrees (MAX over ranks) on the
+    mode: ``full`` if every rank's two slots fit its budget, ``lean`` if the
+    master-only slots fit, else ``off`` (no in-memory snapshots; disk persistence
+    and survivor state transfer still work).  Restoring a lean snapshot zeroes the
+    moments and restarts Adam's bias correction from that step
+    (``FlatAdamW.moment_origin``) — a warm restart of the moments, not bit-exact.
     """
 
     def __init__(self, job: str, interval: int = 10, persist_dir: str | None = None, persist_every: int = 0,
-                 sharded: bool = True, pin: bool = True):
+                 sharded: bool = True, pin: bool = True, host_budget_gb: float | None = None,
+                 host_fraction: float = 0.8, lean: str = "auto"):
         self.job = job
+        env = os.environ.get("EDL_CKPT_HOST_GB")
+        self.host_budget_gb = host_budget_gb if host_budget_gb is not None else (float(env) if env else None)
+        self.host_fraction = host_fraction
+        self.lean = os.environ.get("EDL_CKPT_LEAN", lean)
+        self.mode = None            # "full" | "lean" | "off", agreed per layout (see _decide_mode)
+        self._mode_key = None
         self.interval = max(1, interval)
         self.persist_dir = persist_dir
         self.persist_every = persist_every
@@ -235,6 +258,27 @@ class CheckpointManager:
         if bufs is not None:
             out += [(f"model.buffers.{k}", t) for k, t in bufs.tensors.items()]
         return out
+
+    @staticmethod
+    def _moment_names(trainer) -> set:
+        fn = getattr(trainer.opt, "moment_names", None)
+        return set(fn()) if fn is not None else set()
+
+    @staticmethod
+    def _restore_scalars(trainer, meta: dict) -> None:
+        """Step counters of a restored snapshot; a lean one restarts the moments."""
+        trainer.step = int(meta["step"])
+        trainer.opt.step_count = int(meta["opt_step"])
+        if meta.get("lean"):
+            st = trainer.opt.state_tensors()
+            with torch.no_grad():
+                for n in CheckpointManager._moment_names(trainer):
+                    st[n].zero_()
+            origin = trainer.opt.step_count
+        else:
+            origin = int(meta.get("moment_origin", 0))
+        if hasattr(trainer.opt, "moment_origin"):
+            trainer.opt.moment_origin = origin
 
     @staticmethod
     def finish_restore(trainer) -> None:
@@ -302,6 +346,45 @@ class CheckpointManager:
             except OSError:
                 pass
 
+    # -- host-DRAM sizing ----------------------------------------------------------
+    def host_budget_bytes(self, trainer) -> int:
+        """Host bytes this rank's snapshot slots may occupy."""
+        if self.host_budget_gb is not None:
+            return int(self.host_budget_gb * 2**30)
+        avail = _meminfo_bytes("MemAvailable")
+        try:
+            st = os.statvfs("/dev/shm")
+            avail = min(avail, st.f_bavail * st.f_frsize)
+        except OSError:
+            pass
+        own = 2 * self._seg.slot_bytes if self._seg is not None else 0   # already counted as used
+        ranks = int(os.environ.get("LOCAL_WORLD_SIZE") or 0) or int(getattr(trainer.comm, "world_size", 1) or 1)
+        return int((avail + own) * self.host_fraction / max(1, ranks))
+
+    def _decide_mode(self, trainer, comm, key, full_bytes: int, lean_bytes: int) -> str:
+        """Agree (MAX over the group) on full / lean / off for this layout."""
+        if self._mode_key == key and self.mode is not None:
+            return self.mode
+        budget = self.host_budget_bytes(trainer)
+        if self.lean == "always":
+            want = 1 if 2 * lean_bytes <= budget else 2
+        elif 2 * full_bytes <= budget:
+            want = 0
+        elif self.lean != "never" and 2 * lean_bytes <= budget:
+            want = 1
+        else:
+            want = 2
+        agree = getattr(comm, "ctrl_all_reduce", None)
+        agreed = int(agree([float(want)], _MAX)[0]) if comm.world_size > 1 and agree is not None else want
+        self.mode = ("full", "lean", "off")[agreed]
+        self._mode_key = key
+        self.stats["mode"] = self.mode
+        self.stats["host_budget_gb"] = round(budget / 2**30, 2)
+        if self.mode != "full":
+            log.warning("in-memory snapshots %s: two slots need %.1f GB (lean %.1f GB), budget %.1f GB per rank",
+                        self.mode, 2 * full_bytes / 2**30, 2 * lean_bytes / 2**30, budget / 2**30)
+        return self.mode
+
     # -- snapshot ------------------------------------------------------------
     def on_step(self, trainer) -> None:
         if trainer.step % self.interval:
@@ -317,11 +400,24 @@ class CheckpointManager:
             return
         state = self.state_of(trainer)
         layout, cs_off = shard_layout(state, shard, world)
+        moments = self._moment_names(trainer)
+        lean_state = [(n, t) for n, t in state if n not in moments]
+        headroom = lambda st: (max(shard_layout(st, s, world - 1)[1] for s in range(world - 1)) + 8  # noqa: E731
+                               if world > 1 else 0)
+        mode = self._decide_mode(trainer, comm, (world, shard, tag),
+                                 max(cs_off + 8, headroom(state)),
+                                 max(shard_layout(lean_state, shard, world)[1] + 8, headroom(lean_state)))
+        if mode == "off":
+            self.stats["skipped_host"] = self.stats.get("skipped_host", 0) + 1
+            return
+        if mode == "lean":
+            state = lean_state
+            layout, cs_off = shard_layout(state, shard, world)
         self.wait()  # at most one snapshot in flight (and never one across a segment change)
         alloc = 0
         if world > 1 and self._seg is None:
             # headroom: the largest shard of a world one rank smaller (+ alignment slack)
-            alloc = max(shard_layout(state, s, world - 1)[1] for s in range(world - 1)) + 8
+            alloc = headroom(state)
         seg = self._segment(world, shard, cs_off + 8, pin=state[0][1].is_cuda, tag=tag, alloc_bytes=alloc)
         if getattr(self, "_old_name", None) and self._kept_slot_next(seg):
             self._drop_old_name()   # this write overwrites the old layout's kept snapshot
@@ -332,6 +428,7 @@ class CheckpointManager:
             return
         meta = {"format": FORMAT, "step": trainer.step, "opt_step": trainer.opt.step_count, "world": world,
                 "shard": shard, "epoch": comm.epoch, "tag": tag, "host": _host_state(trainer),
+                "lean": mode == "lean", "moment_origin": int(getattr(trainer.opt, "moment_origin", 0)),
                 "t": [[d["name"], d["dtype"], d["numel"], d["lo"], d["hi"], d["offset"]] for d in layout]}
         dev = state[0][1].device
         if dev.type == "cuda":
@@ -486,8 +583,7 @@ class CheckpointManager:
                 seg.close()
         self.finish_restore(trainer)
         meta = infos[0]["meta"]
-        trainer.step = int(meta["step"])
-        trainer.opt.step_count = int(meta["opt_step"])
+        self._restore_scalars(trainer, meta)
         _load_host_state(trainer, meta.get("host"))
         return f"shm{tag}:w{world}:step{step}"
 
@@ -543,7 +639,8 @@ class CheckpointManager:
         if m["shard"] == 0:
             with open(os.path.join(d, f"manifest{tag}.json"), "w") as f:
                 json.dump({"format": FORMAT, "step": step, "opt_step": m["opt_step"], "world": m["world"],
-                           "epoch": m["epoch"], "host": m.get("host"), "time": time.time()}, f)
+                           "epoch": m["epoch"], "host": m.get("host"), "lean": bool(m.get("lean")),
+                           "moment_origin": int(m.get("moment_origin", 0)), "time": time.time()}, f)
 
     def load_dir_latest(self, trainer) -> str | None:
         dirs = sorted(glob.glob(os.path.join(self.persist_dir or "", "step-*")),
@@ -591,9 +688,22 @@ def load_dir(d: str, trainer, tag: str = "") -> None:
         _load_shard(lambda off, nb: np.array(raw[off:off + nb]), sm["tensors"], state, dev, sm["checksum"],
                     sm["file"])
     CheckpointManager.finish_restore(trainer)
-    trainer.step = int(m["step"])
-    trainer.opt.step_count = int(m["opt_step"])
+    CheckpointManager._restore_scalars(trainer, m)
     _load_host_state(trainer, m.get("host"))
+
+
+_MAX = dist.ReduceOp.MAX
+
+
+def _meminfo_bytes(key: str) -> int:
+    try:
+        with open("/proc/meminfo") as f:
+            for line in f:
+                if line.startswith(key + ":"):
+                    return int(line.split()[1]) * 1024
+    except OSError:
+        pass
+    return 0
 
 
 def _host_state(trainer) -> dict | None:

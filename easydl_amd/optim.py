@@ -44,6 +44,9 @@ class FlatAdamW:
         self.max_grad_norm = max_grad_norm
         self.schedule = schedule
         self.step_count = 0
+        # step at which the moments (m, v) last started from zero: bias correction counts
+        # from here (a lean snapshot restores the master weights only, ckpt/manager.py)
+        self.moment_origin = 0
         self.last_stats = None  # device tensor [coef, norm, nonfinite]
         # model parallelism: per-group sum-of-squares weights + group all-reduce
         self.norm_weights = None
@@ -73,7 +76,8 @@ class FlatAdamW:
         for g, st in zip(self.flat.groups, self.state):
             p16 = g.data if g.data.dtype != torch.float32 else None
             adamw_flat_(p16, st["master"], st["m"], st["v"], g.grad, lr=lr, beta1=self.beta1, beta2=self.beta2,
-                        eps=self.eps, weight_decay=g.weight_decay, step=self.step_count, dscale=stats)
+                        eps=self.eps, weight_decay=g.weight_decay, step=self.step_count - self.moment_origin,
+                        dscale=stats)
         self.last_stats = stats
         return stats
 
@@ -88,11 +92,15 @@ class FlatAdamW:
             out[f"opt.{g.name}.v"] = st["v"]
         return out
 
+    def moment_names(self) -> set[str]:
+        return {n for n in self.state_tensors() if n.endswith((".m", ".v"))}
+
     def scalars(self) -> dict:
-        return {"step_count": self.step_count, "lr": self.lr}
+        return {"step_count": self.step_count, "lr": self.lr, "moment_origin": self.moment_origin}
 
     def load_scalars(self, d: dict) -> None:
         self.step_count = int(d["step_count"])
+        self.moment_origin = int(d.get("moment_origin", 0))
 
 
 class FlatSGD:
@@ -133,6 +141,9 @@ class FlatSGD:
             if st["mom"] is not None:
                 out[f"opt.{g.name}.mom"] = st["mom"]
         return out
+
+    def moment_names(self) -> set[str]:
+        return {n for n in self.state_tensors() if n.endswith(".mom")}
 
     def scalars(self):
         return {"step_count": self.step_count, "lr": self.lr}

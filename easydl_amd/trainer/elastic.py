@@ -380,9 +380,12 @@ class ElasticTrainer:
             # every up-to-date rank sends a slice (SURVEY.md §2.8 multi-source scatter):
             # a joiner's inbound traffic is spread over one link per survivor
             c.transfer_state(self._state_tensors(), holders if max_step >= 0 else [src_rank])
-            scal = c.ctrl_broadcast([self.step, self.opt.step_count], src_rank)
+            scal = c.ctrl_broadcast([self.step, self.opt.step_count, getattr(self.opt, "moment_origin", 0)],
+                                    src_rank)
             self.step = int(scal[0])
             self.opt.step_count = int(scal[1])
+            if hasattr(self.opt, "moment_origin"):
+                self.opt.moment_origin = int(scal[2])
             if self.device.type == "cuda":
                 torch.cuda.current_stream(self.device).synchronize()
             nbytes = sum(t.numel() * t.element_size() for t in self._state_tensors())
@@ -425,8 +428,11 @@ class ElasticTrainer:
                 self._fence_snapshot_before_overwrite(c.dp, src, bool(mine_ok))
                 for ten in self._state_tensors():
                     c.dp.broadcast(ten, src)
-                scal = c.dp.ctrl_broadcast([self.step, self.opt.step_count], src)
+                scal = c.dp.ctrl_broadcast([self.step, self.opt.step_count,
+                                            getattr(self.opt, "moment_origin", 0)], src)
                 self.step, self.opt.step_count = int(scal[0]), int(scal[1])
+                if hasattr(self.opt, "moment_origin"):
+                    self.opt.moment_origin = int(scal[2])
                 if self.device.type == "cuda":
                     torch.cuda.current_stream(self.device).synchronize()
                 self.events.emit("state_broadcast", src=src, group="dp", tp_rank=t, s=round(time.time() - t0, 4))

@@ -252,3 +252,16 @@ def test_plan_loop_writes_one_versioned_runtime_document(tmp_path):
     doc = kv.get("plan/runtime/2")
     assert doc["allreduce"]["world"] == 8 and doc["allreduce"]["policy"]["oneshot_max_kb"] == 1024
     assert json.loads(kv.get_str("jobresource"))["spec"]["allreduce"] == doc["allreduce"]
+
+
+def test_startup_plan_sizes_snapshots_for_host_dram():
+    """70B (TP) state: two full A/B copies (1.7 TB) exceed 1.5 TB of host DRAM, two lean
+    copies (0.56 TB) fit; 8B fits in full."""
+    inv = NodeInventory(gpus=[GpuInfo(i, "gfx950", 256, 288.0) for i in range(8)], cpus=128, host_mem_gb=1536)
+    p70 = Planner().startup_plan(JobFeatures(params=70.6e9, activation_gb_per_rank=10, bytes_per_param_state=2),
+                                 inv)
+    assert "in-memory snapshots lean" in p70.reason, p70.reason
+    p8 = Planner().startup_plan(JobFeatures(params=8.03e9), inv)
+    assert "in-memory snapshots full" in p8.reason, p8.reason
+    small = NodeInventory(gpus=inv.gpus, cpus=128, host_mem_gb=64)
+    assert "in-memory snapshots off" in Planner().startup_plan(JobFeatures(params=8.03e9), small).reason

@@ -338,3 +338,80 @@ def test_resume_is_bit_exact_with_dropout(tmp_path):
     finally:
         ckpt.close()
         unlink_job_segments(JOB)
+
+
+def test_host_budget_selects_lean_and_lean_restore_restarts_the_moments(tmp_path):
+    """SURVEY.md §5.4 host-DRAM sizing: when two full slots do not fit the per-rank host
+    budget but master-only slots do, snapshots go lean (no Adam moments); restoring one
+    gives the weights back exactly, zeroes the moments and restarts the bias correction
+    (moment_origin); with no room at all in-memory snapshots are off."""
+    unlink_job_segments(JOB)
+    data = SyntheticTokens(CFG.vocab_size, 16, num_samples=1024)
+    sizing = _trainer(tmp_path, None)
+    st = CheckpointManager.state_of(sizing)
+    full = sum(t.numel() * t.element_size() for _, t in st)
+    lean = sum(t.numel() * t.element_size() for n, t in st if not n.endswith((".m", ".v")))
+    assert lean * 2 < full
+    budget_gb = (2 * lean + 2 * full) / 2 / 2**30          # between two lean and two full slots
+    ckpt = CheckpointManager(JOB, interval=2, host_budget_gb=budget_gb)
+    try:
+        a = _trainer(tmp_path, ckpt)
+        a.fit(lambda m, b: m(*b), data, num_steps=4)
+        ckpt.wait()
+        assert ckpt.mode == "lean" and ckpt.stats["snapshots"] == 2
+        info = max(ckpt._seg.committed(), key=lambda i: i["step"])
+        assert info["meta"]["lean"] and not any(n.endswith((".m", ".v")) for n, *_ in info["meta"]["t"])
+        weights = [g.data.clone() for g in a.flat.groups]
+        with torch.no_grad():
+            for g in a.flat.groups:
+                g.data.add_(1.0)
+            for t in a.opt.state_tensors().values():
+                t.add_(1.0)
+        a.step = 99
+        assert ckpt.restore_latest(a) is not None
+        assert a.step == 4 and all(torch.equal(g.data, w) for g, w in zip(a.flat.groups, weights))
+        assert all(float(a.opt.state_tensors()[n].abs().max()) == 0 for n in a.opt.moment_names())
+        assert a.opt.moment_origin == a.opt.step_count == 4
+        a.fit(lambda m, b: m(*b), data, num_steps=6)           # trains on from the warm restart
+        assert a.step == 6 and torch.isfinite(torch.as_tensor(a.last_loss))
+    finally:
+        ckpt.close(unlink=True)
+    off = CheckpointManager(JOB + "x", interval=1, host_budget_gb=1e-9)
+    try:
+        b = _trainer(tmp_path, off)
+        b.fit(lambda m, b_: m(*b_), data, num_steps=2)
+        assert off.mode == "off" and off.stats["skipped_host"] == 2 and off._seg is None
+    finally:
+        off.close(unlink=True)
+
+
+def test_snapshot_mode_is_agreed_over_the_group():
+    """One rank short of host memory makes the whole DP group lean (mixed layouts could
+    not be restored together)."""
+    import datetime
+    import socket
+    import threading
+    import types
+
+    import torch.distributed as dist
+    from easydl_amd.parallel.comm import Communicator
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    out = {}
+
+    def run(r):
+        st = dist.TCPStore("127.0.0.1", port, 2, r == 0, timeout=datetime.timedelta(seconds=30))
+        c = Communicator(st, r, 2, 1, device=torch.device("cpu"), job="ckm")
+        m = CheckpointManager(f"{JOB}-agree{r}", host_budget_gb=(10.0 if r == 0 else 2.5e-6))
+        tr = types.SimpleNamespace(comm=c)
+        out[r] = (m._decide_mode(tr, c, (2, r, ""), full_bytes=1 << 20, lean_bytes=1 << 10),
+                  m._decide_mode(tr, c, (2, r, ""), full_bytes=1 << 20, lean_bytes=1 << 10))  # cached
+        c.shutdown()
+
+    ts = [threading.Thread(target=run, args=(r,)) for r in range(2)]
+    [t.start() for t in ts]
+    [t.join(60) for t in ts]
+    assert out == {0: ("lean", "lean"), 1: ("lean", "lean")}, out
