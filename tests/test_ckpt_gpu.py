@@ -71,3 +71,28 @@ def test_restore_right_after_enqueue_drains_the_inflight_snapshot(cuda, tmp_path
     finally:
         ckpt.close()
         unlink_job_segments("ckg")
+
+
+def test_lean_snapshot_through_the_d2h_engine(cuda, tmp_path):
+    """Lean mode on the GPU path (native D2H engine + pipelined restore): the bf16 model
+    is rebuilt from the restored fp32 master, the moments restart from zero."""
+    unlink_job_segments("ckg")
+    data = SyntheticTokens(CFG.vocab_size, 64, num_samples=4096)
+    ckpt = CheckpointManager("ckg", interval=2, lean="always")
+    try:
+        a = _trainer(tmp_path, ckpt, 1, cuda)
+        a.fit(lambda m, b: m(*b), data, num_steps=4)
+        ckpt.wait()
+        assert ckpt.mode == "lean" and ckpt.last_snapshot_step == 4
+        master = {n: t.clone() for n, t in a.opt.state_tensors().items() if n.endswith(".master")}
+        model = [g.data.clone() for g in a.flat.groups]
+        b = _trainer(tmp_path, CheckpointManager("ckg", interval=1000), 2, cuda)
+        b.fit(lambda m, b_: m(*b_), data, num_steps=4)   # restores step 4
+        assert b.step == 4 and b.opt.moment_origin == 4
+        st = b.opt.state_tensors()
+        assert all(torch.equal(st[n], t) for n, t in master.items())
+        assert all(torch.equal(g.data, w) for g, w in zip(b.flat.groups, model))
+        assert all(float(st[n].abs().max()) == 0 for n in b.opt.moment_names())
+    finally:
+        ckpt.close()
+        unlink_job_segments("ckg")
