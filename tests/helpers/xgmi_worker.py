@@ -127,6 +127,42 @@ elif mode == "abort":
         res["detail"] = x.status_detail()
     store.set(f"done{rank}", "1")
     store.wait([f"done{r}" for r in range(world)])
+elif mode == "lifetime":
+    # IPC lifetime (docs/design_notes.md): rank 1 registers a buffer and EXITS; rank 0 then
+    # copies from its mapping of that buffer.  With dmabuf IPC the import holds a reference
+    # on the buffer object, so the memory must still be there with rank 1's data.
+    t = torch.full((1 << 20,), float(rank + 7), device="cuda")
+    reg = x.register(t)
+    torch.cuda.synchronize()
+    store.set(f"pid{rank}", str(os.getpid()))
+    sync()
+    if rank == 1:
+        with open(os.environ["OUT"] + f".{rank}", "w") as f:
+            json.dump(res, f)
+        os._exit(0)
+    import ctypes
+    pid = int(store.get("pid1"))
+    t_end = time.time() + 30
+    while time.time() < t_end:
+        try:
+            state = open(f"/proc/{pid}/stat").read().rsplit(")", 1)[1].split()[0]
+        except OSError:
+            state = "gone"
+        if state in ("Z", "X", "gone"):
+            break
+        time.sleep(0.05)
+    res["exporter_state"] = state
+    time.sleep(2.0)    # let the driver finish tearing the dead process down
+    out = torch.zeros_like(t)
+    hip = ctypes.CDLL("libamdhip64.so")
+    rc = hip.hipMemcpy(ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(reg.peers[1]),
+                       ctypes.c_size_t(t.numel() * 4), 3)    # hipMemcpyDeviceToDevice
+    torch.cuda.synchronize()
+    res["rc"] = rc
+    res["ok"] = rc == 0 and bool(torch.all(out == 8.0))
+    with open(os.environ["OUT"] + f".{rank}", "w") as f:
+        json.dump(res, f)
+    os._exit(0)
 print(json.dumps(res), flush=True)
 with open(os.environ["OUT"] + f".{rank}", "w") as f:
     json.dump(res, f)

@@ -77,6 +77,15 @@ def test_xgmi_register_refuses_oversized_segments_everywhere(cuda, tmp_path):
         assert r["status"] == 0
 
 
+def test_ipc_mapping_outlives_the_exporting_process(cuda, tmp_path):
+    """A peer's registered buffer stays readable through this rank's mapping after the
+    peer process has exited (dmabuf IPC: the import holds a buffer-object reference),
+    so a survivor's kernel never touches freed memory of a dead rank."""
+    r0 = _run(2, tmp_path, mode="lifetime")[0]
+    assert r0["exporter_state"] in ("Z", "X", "gone"), r0
+    assert r0["rc"] == 0 and r0["ok"], r0
+
+
 def test_xgmi_abort_releases_spinning_kernel(cuda, tmp_path):
     r0 = _run(2, tmp_path, mode="abort")[0]
     assert r0["status"] == 1           # the barrier gave up ...
