@@ -13,6 +13,12 @@ framework is built on:
   large contiguous D2H copies (``easydl_amd/ckpt``);
 * state transfer to a joining rank is a few large broadcasts.
 
+A group is split at parameter boundaries into parts of at most
+``EDL_FLAT_GROUP_MAX_MB`` (default 1900 MiB) of gradient bytes ("decay",
+"decay.1", ...): each part is a separate allocation, so the xGMI engine can
+IPC-map every gradient buffer of a multi-GB model and all-reduce its buckets in
+place (segments of >= 2 GiB do not map on this platform).
+
 Parameters are laid out in *reverse registration order* so gradients, which
 backward produces roughly last-layer-first, fill buckets front to back.  Each
 parameter starts on a 64-element boundary (128 B for bf16) so every view is
@@ -20,6 +26,7 @@ parameter starts on a 64-element boundary (128 B for bf16) so every view is
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass, field
 
 import torch
@@ -53,6 +60,27 @@ class FlatGroup:
         return self.data.numel()
 
 
+def _split_by_bytes(plist, elem_bytes: int, max_bytes: int) -> list[list]:
+    """Split a group's (name, param) list at parameter boundaries so that each part's
+    gradient buffer stays under ``max_bytes``.  Each part is its own allocation (its own
+    caching-allocator segment), so the xGMI engine can map every gradient group of a
+    multi-GB model in place: IPC mappings of >= 2 GiB segments never open on this
+    platform (parallel/xgmi.py REGISTER_MAX)."""
+    if max_bytes <= 0:
+        return [plist]
+    parts, cur, used = [], [], 0
+    for n, p in plist:
+        b = _roundup(p.numel()) * elem_bytes
+        if cur and used + b > max_bytes:
+            parts.append(cur)
+            cur, used = [], 0
+        cur.append((n, p))
+        used += b
+    if cur:
+        parts.append(cur)
+    return parts
+
+
 class FlatParams:
     """Re-home a module's parameters into flat buffers.
 
@@ -64,7 +92,9 @@ class FlatParams:
     """
 
     def __init__(self, module: torch.nn.Module, weight_decay: float = 0.0, grad_dtype: torch.dtype | None = None,
-                 no_decay=None):
+                 no_decay=None, max_group_bytes: int | None = None):
+        if max_group_bytes is None:
+            max_group_bytes = int(float(os.environ.get("EDL_FLAT_GROUP_MAX_MB", 1900)) * 2**20)
         if no_decay is None:
             no_decay = lambda n, p: p.ndim < 2  # noqa: E731
         named = [(n, p) for n, p in module.named_parameters() if p.requires_grad]
@@ -86,9 +116,14 @@ class FlatParams:
             key = ("no_decay" if no_decay(n, p) else "decay", p.dtype)
             buckets.setdefault(key, []).append((n, p))
         self.groups: list[FlatGroup] = []
+        chunks = []
         for (cls, dt), plist in sorted(buckets.items(), key=lambda kv: (kv[0][0], str(kv[0][1]))):
-            gname = cls if dt == self.dtype else f"{cls}_{str(dt).split('.')[-1]}"
+            base = cls if dt == self.dtype else f"{cls}_{str(dt).split('.')[-1]}"
             gdt = grad_dtype if (grad_dtype is not None and dt == self.dtype) else dt
+            for i, part in enumerate(_split_by_bytes(plist, torch.empty((), dtype=gdt).element_size(),
+                                                     max_group_bytes)):
+                chunks.append((cls, dt, gdt, base if i == 0 else f"{base}.{i}", part))
+        for cls, dt, gdt, gname, plist in chunks:
             total = sum(_roundup(p.numel()) for _, p in plist)
             data = torch.zeros(total, dtype=dt, device=self.device)
             grad = torch.zeros(total, dtype=gdt, device=self.device)

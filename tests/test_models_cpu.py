@@ -64,3 +64,36 @@ def test_flat_params_mixed_dtypes():
     names = sorted(g.name for g in flat.groups)
     assert names == ["decay", "no_decay", "no_decay_float32"], names
     assert {g.data.dtype for g in flat.groups} == {torch.bfloat16, torch.float32}
+
+
+def test_flat_groups_split_under_the_byte_cap_and_train_identically():
+    """Groups split at parameter boundaries into separately allocated parts of at most
+    max_group_bytes of gradient (each mappable by the xGMI engine); the split changes
+    nothing numerically: same losses, same final weights as one group per class."""
+    cfg = get_config("llama-tiny")
+    ids = torch.randint(0, cfg.vocab_size, (2, 32), generator=torch.Generator().manual_seed(3))
+    out = {}
+    for cap in (0, 64 << 10):
+        torch.manual_seed(0)
+        m = Llama(cfg, dtype=torch.float32)
+        flat = FlatParams(m, max_group_bytes=cap)
+        opt = FlatAdamW(flat, lr=3e-3, weight_decay=0.1)
+        losses = []
+        for _ in range(4):
+            flat.zero_grad()
+            loss = m(ids, ids)
+            loss.backward()
+            flat.finalize_untouched()
+            opt.step()
+            losses.append(loss.item())
+        out[cap] = (flat, losses, torch.cat([p.detach().reshape(-1) for p in m.parameters()]))
+    one, split = out[0][0], out[64 << 10][0]
+    assert [g.name for g in one.groups] == ["decay", "no_decay"]
+    decay_parts = [g for g in split.groups if g.name.split(".")[0] == "decay"]
+    assert len(decay_parts) > 2 and decay_parts[1].name == "decay.1"
+    assert all(g.grad.numel() * 4 <= (64 << 10) or len(g.slots) == 1 for g in split.groups)
+    assert len({g.grad.data_ptr() for g in split.groups}) == len(split.groups)
+    assert sum(g.numel for g in split.groups) == sum(g.numel for g in one.groups)
+    assert all(g.weight_decay == 0.1 for g in decay_parts)
+    assert out[0][1] == out[64 << 10][1]
+    assert torch.equal(out[0][2], out[64 << 10][2])
