@@ -282,6 +282,9 @@ class Communicator:
         gradient groups): the engine then all-reduces their slices in place."""
         if self.xgmi is None or self.xgmi_mode != "xgmi":
             return
+        if self.xgmi_min_bytes >= 1 << 62:
+            # the (agreed) policy never routes a registered buffer to the engine: no mappings
+            return
         from easydl_amd.parallel.xgmi import XgmiError
         for t in tensors:   # sizes are equal on every rank, so every rank skips the same ones
             if self.xgmi.supports(t) and self.xgmi.registrable(t):

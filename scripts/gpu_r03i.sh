@@ -16,3 +16,5 @@ EDL_GEMM_TUNING=use EDL_GEMM_TUNING_FILE=$PWD/gpurun_out/r03i/tunableop_bert.csv
 EDL_GEMM_TUNING=off timeout -k 10 300 \
   python3 benchmarks/train_bench.py --model bert-large --batch 32 --steps 10 --warmup 3 > gpurun_out/r03i/bert_off.log 2>&1
 grep -h '"metric"' gpurun_out/r03i/bert_*.log | cut -c1-200
+timeout -k 10 600 python bench.py --steps 6 --warmup 2 --out gpurun_out/r03i/bench_groups_split.json > gpurun_out/r03i/bench.log 2>&1
+tail -1 gpurun_out/r03i/bench.log | cut -c1-300
