@@ -142,8 +142,9 @@ def test_ddp_step_xgmi_only_ranks_sharing_one_gpu(cuda, tmp_path):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--share-gpu", "--gpus", "2",
            "--model", "llama-tiny", "--seq", "256", "--mbs", "1", "--accum", "1", "--steps", "3", "--warmup", "1"]
+    # gradient groups capped at 128 KB: several separately registered flat gradient buffers
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=240,
-                       env=dict(os.environ, EDL_RUN_DIR=str(tmp_path)))
+                       env=dict(os.environ, EDL_RUN_DIR=str(tmp_path), EDL_FLAT_GROUP_MAX_MB="0.125"))
     assert r.returncode == 0, r.stderr[-3000:]
     d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
     assert d["ranks"] == 2 and d["n_gpus"] == 1 and d["shared_gpu"]
