@@ -313,3 +313,47 @@ def test_runtime_plan_switches_every_rank_at_one_step(tmp_path):
         assert len(steps) == 2 and len(set(steps.values())) == 1, steps   # the same committed step
     finally:
         m.terminate()
+
+
+@pytest.mark.slow
+def test_brain_plan_loop_retunes_buckets_on_running_workers(tmp_path):
+    """The whole Brain loop on a live job: the master asks the Brain for a startup plan
+    (bucket size in plan/runtime/1), collects the workers' step metrics, the Brain's
+    bucket autotune re-plans, and both workers switch to the new bucket size at one
+    committed step with identical weights."""
+    from easydl_amd.utils.events import read_events
+    spec = {"apiVersion": "edl.mi355x/v1", "kind": "ElasticJob", "metadata": {"name": "t"},
+            "spec": {"command": "python -m x", "min_workers": 2, "max_workers": 2,
+                     "features": {"model": "tiny", "params": 2e5, "mode": "allreduce", "min_workers": 2,
+                                  "max_workers": 2}}}
+    jf = tmp_path / "job.json"
+    jf.write_text(json.dumps(spec))
+    port = free_port()
+    m = subprocess.Popen([sys.executable, "-m", "easydl_amd.master.main", "--job", "t", "--port", str(port),
+                          "--min", "1", "--max", "2", "--join-window", "0.3", "--initial", "2",
+                          "--run-dir", str(tmp_path), "--job-spec", str(jf), "--plan-period", "0.5"],
+                         cwd=ROOT, env=dict(os.environ, PYTHONPATH=ROOT), stdout=subprocess.PIPE,
+                         stderr=subprocess.STDOUT)
+    try:
+        procs = {}
+        for i in range(2):
+            env = _env(tmp_path, i, {"EDL_MASTER_ADDR": "127.0.0.1", "EDL_MASTER_PORT": str(port),
+                                     "TEST_STEPS": "60", "TEST_GB": "4", "TEST_STEP_SLEEP": "0.05"})
+            procs[i] = subprocess.Popen([sys.executable, WORKER], env=env, cwd=ROOT)
+        codes = _wait(procs)
+        assert codes == {0: 0, 1: 0}, codes
+        r = _results(tmp_path, [0, 1])
+        assert r[0]["hash"] == r[1]["hash"]
+        ev = read_events(str(tmp_path))
+        kinds = {e["kind"] for e in ev}
+        assert "startup_plan" in kinds and "replan" in kinds, kinds
+        switched = {}
+        for e in ev:
+            if e["kind"] == "plan_bucket_mb":
+                switched.setdefault(e.get("proc"), []).append((e["step"], e["mb"]))
+        assert set(switched) == {"worker0", "worker1"}, switched
+        assert switched["worker0"] == switched["worker1"], switched      # same sizes at the same steps
+        assert len(switched["worker0"]) >= 2, switched                   # startup plan + >= 1 autotune move
+        assert r[0]["plan_version"] == r[1]["plan_version"] >= 2
+    finally:
+        m.terminate()
