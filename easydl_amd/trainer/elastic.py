@@ -272,7 +272,9 @@ class ElasticTrainer:
                 continue
             self.events.emit("state_transferred", epoch=self.comm.epoch, step=self.step)
             self.ddp.set_comm(self.dp_comm)   # binds the epoch's comm (registers gradient buffers)
-            self.events.emit("state_synced", epoch=self.comm.epoch, step=self.step)
+            xg = getattr(self.dp_comm, "xgmi", None)
+            self.events.emit("state_synced", epoch=self.comm.epoch, step=self.step,
+                             grad_buffers_mapped=len(getattr(xg, "_registered", ())) if xg is not None else 0)
             if self.rdzv is not None:
                 try:
                     self._publish_probe()
