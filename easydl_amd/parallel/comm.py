@@ -209,6 +209,7 @@ class Communicator:
             for i, kb in enumerate(sizes_kb):
                 view = b[:(kb << 10) // 2]
                 it = iters if kb > 1024 else 4 * iters      # latency-bound sizes: more samples
+                failed = 0.0
                 for c, fn in enumerate(forms):
                     if c == 3 and kb > self.ONESHOT_PROBE_KB:
                         continue
@@ -216,10 +217,18 @@ class Communicator:
                         cols[c][i] = timed(fn, view, it)
                     except Exception as e:  # noqa: BLE001
                         log.warning("xGMI probe: form %d at %d KB failed: %s", c, kb, e)
-                        if c == 0:
-                            cols[0][i] = 0.0
+                        failed = 1.0
+                        break   # the rest of this size would meet peers out of step
+                try:
+                    failed = max(failed, 0.0 if self.xgmi.status() == 0 else 1.0)
+                except Exception:  # noqa: BLE001
+                    failed = 1.0
+                # agreed after every size: one rank's failure ends the probe on all ranks
+                if float(self.ctrl_all_reduce([failed], dist.ReduceOp.MAX)[0]):
+                    bad = 1.0
+                    break
             try:
-                bad = 0.0 if self.xgmi.status() == 0 else 1.0
+                bad = max(bad, 0.0 if self.xgmi.status() == 0 else 1.0)
             except Exception:  # noqa: BLE001
                 bad = 1.0
         self.xgmi.timeout_s = keep_timeout

@@ -196,3 +196,23 @@ def test_probe_publishes_policy_with_oneshot_column():
         assert probe["sizes_kb"] == [2048, 4096, 8192]
         assert probe["xgmi_oneshot_ms"][2] is None and probe["xgmi_oneshot_ms"][0] is not None
         assert pol == probe["policy"] and pol["xgmi_min_kb_inplace"] == 4096
+
+
+def test_probe_failure_on_one_rank_drops_the_engine_everywhere():
+    """A form that raises on ONE rank mid-probe: every rank stops after that size (agreed
+    over the control plane) and keeps RCCL only."""
+    def fn(c, st):
+        eng = FakeEngine(c, lambda nb: 0.0)
+        real = eng.all_reduce
+
+        def flaky(t, algo=None):
+            if c.rank == 1 and eng.calls > 3 and algo == "twoshot":
+                raise RuntimeError("launch failed")
+            return real(t, algo)
+        eng.all_reduce = flaky
+        c.xgmi, c.xgmi_mode = eng, "auto"
+        c._probe_xgmi(sizes_mb=(2, 4, 8), iters=1)
+        return c.xgmi_probe, c.xgmi_mode, eng.closed
+
+    for probe, mode, closed in _spawn(2, fn).values():
+        assert probe["selected"] == "rccl" and mode is None and closed, probe
