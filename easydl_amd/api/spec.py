@@ -238,7 +238,7 @@ class ResourcePlan:
     per_rank: dict[str, dict] = field(default_factory=dict)   # process name -> {cu, hbm_gb, cpus}
     bucket_mb: float | None = None
     ckpt_interval: int | None = None
-    allreduce: dict | None = None      # {"world": W, "policy": {...}} from the probe history
+    allreduce: dict | None = None      # {"dp"|"tp": {"world", "epochs", "policy"}} from the probe history
     reason: str = ""
 
     def to_job_resource(self, job: str, version: int = 0) -> JobResource:

@@ -25,7 +25,8 @@ Periodic plan (from per-rank step metrics)
   fastest measured step time — only over sizes at or above the all-reduce
   bandwidth knee the probes measured;
 * all-reduce routing: every epoch's communicator times RCCL against the xGMI
-  engine's forms at 256 KB..128 MB and publishes the table (``comm/probe``);
+  engine's forms at 256 KB..128 MB and publishes the table (``comm/probe/dp``,
+  ``comm/probe/tp``: DP gradient buckets and TP activations get separate policies);
   the Brain takes the per-size median over the epochs of the same world size and
   re-derives the policy (one-shot switch sizes, the size from which the engine
   beats RCCL, with a margin in RCCL's favour) — a runtime knob the trainers switch
@@ -123,7 +124,7 @@ class Planner:
     def __init__(self, cfg: BrainConfig | None = None):
         self.cfg = cfg or BrainConfig()
         self._tune: dict = {}
-        self._probes: dict[int, dict[int, dict]] = {}   # world -> epoch -> published probe table
+        self._probes: dict[tuple, dict[int, dict]] = {}   # (group, world) -> epoch -> probe table
 
     # ------------------------------------------------------------------ startup
     def startup_plan(self, feat: JobFeatures, inv: NodeInventory) -> ResourcePlan:
@@ -182,20 +183,31 @@ class Planner:
         return int(round(total_cus * frac / 8)) * 8   # whole CUs per XCD
 
     # ------------------------------------------------------------------ communication
-    def observe_probe(self, comm: dict | None) -> None:
-        """Keep an epoch's published all-reduce probe table (``{"world", "epoch", "probe"}``)."""
-        if not comm or not comm.get("probe"):
-            return
-        world, epoch = int(comm.get("world", 0)), int(comm.get("epoch", 0))
-        hist = self._probes.setdefault(world, {})
-        hist[epoch] = comm["probe"]
-        for e in sorted(hist)[:-self.cfg.comm_history]:
-            del hist[e]
+    GROUPS = ("dp", "tp")
 
-    def allreduce_plan(self, world: int) -> dict | None:
-        """The all-reduce policy for ``world`` from the median of its probe tables."""
+    @staticmethod
+    def _by_group(comm: dict | None) -> dict:
+        """``{"dp": doc, "tp": doc}`` (a single ``{"world", "epoch", "probe"}`` doc is DP's)."""
+        if not comm:
+            return {}
+        if "probe" in comm:
+            return {"dp": comm}
+        return {g: d for g, d in comm.items() if isinstance(d, dict) and d.get("probe")}
+
+    def observe_probe(self, comm: dict | None) -> None:
+        """Keep the epochs' published all-reduce probe tables, per (group, world size)."""
+        for group, doc in self._by_group(comm).items():
+            world, epoch = int(doc.get("world", 0)), int(doc.get("epoch", 0))
+            hist = self._probes.setdefault((group, world), {})
+            hist[epoch] = doc["probe"]
+            for e in sorted(hist)[:-self.cfg.comm_history]:
+                del hist[e]
+
+    def allreduce_plan(self, world: int, group: str = "dp") -> dict | None:
+        """The all-reduce policy of a ``group`` of ``world`` ranks from the median of its probe tables."""
         from easydl_amd.parallel import comm_policy
-        tab = comm_policy.median_table([self._probes[world][e] for e in sorted(self._probes.get(world, {}))])
+        hist = self._probes.get((group, world), {})
+        tab = comm_policy.median_table([hist[e] for e in sorted(hist)])
         if tab is None:
             return None
         pol = comm_policy.decide_from_probe(tab, world, margin=self.cfg.comm_margin)
@@ -204,26 +216,30 @@ class Planner:
     # ------------------------------------------------------------------ periodic
     def next_plan(self, feat: JobFeatures, inv: NodeInventory, current: ResourcePlan,
                   metrics: dict[str, dict], comm: dict | None = None) -> ResourcePlan | None:
-        """Return a changed plan, or None to keep the current one.  ``comm`` is the
-        latest published all-reduce probe (``comm/probe``), if any."""
+        """Return a changed plan, or None to keep the current one.  ``comm``: the latest
+        published all-reduce probes per communicator group (``comm/probe/dp``,
+        ``comm/probe/tp``), if any.  The plan's ``allreduce`` holds one policy per group:
+        the DP gradient buckets and the TP activation all-reduces each get their own."""
         import copy
         plan = copy.deepcopy(current)
         changed = []
         self.observe_probe(comm)
         floor = None
-        if comm and comm.get("world"):
-            ar = self.allreduce_plan(int(comm["world"]))
-            if ar is not None:
+        keys = ("oneshot_max_kb", "oneshot_max_staged_kb", "xgmi_min_kb_inplace", "xgmi_min_kb_staged")
+        for group, doc in self._by_group(comm).items():
+            ar = self.allreduce_plan(int(doc["world"]), group)
+            if ar is None:
+                continue
+            if group == "dp":
                 floor = ar["policy"].get("bucket_floor_mb")
-                keys = ("oneshot_max_kb", "oneshot_max_staged_kb", "xgmi_min_kb_inplace", "xgmi_min_kb_staged")
-                old = (current.allreduce or {})
-                if (old.get("world") != ar["world"]
-                        or any((old.get("policy") or {}).get(k) != ar["policy"].get(k) for k in keys)):
-                    plan.allreduce = ar
-                    p = ar["policy"]
-                    changed.append(f"all-reduce policy (world {ar['world']}, {ar['epochs']} probes): engine from "
-                                   f"{p['xgmi_min_kb_inplace']} KB in place / {p['xgmi_min_kb_staged']} KB staged, "
-                                   f"one-shot <= {p['oneshot_max_kb']} KB")
+            old = (current.allreduce or {}).get(group) or {}
+            if (old.get("world") != ar["world"]
+                    or any((old.get("policy") or {}).get(k) != ar["policy"].get(k) for k in keys)):
+                plan.allreduce = dict(plan.allreduce or {}, **{group: ar})
+                p = ar["policy"]
+                changed.append(f"{group} all-reduce policy (world {ar['world']}, {ar['epochs']} probes): engine "
+                               f"from {p['xgmi_min_kb_inplace']} KB in place / {p['xgmi_min_kb_staged']} KB staged, "
+                               f"one-shot <= {p['oneshot_max_kb']} KB")
         times = {n: m.get("step_time") for n, m in metrics.items() if m.get("step_time")}
         if len(times) >= 2:
             med = statistics.median(times.values())

@@ -7,8 +7,8 @@
    for a new plan and update the JobResource (scale, replace stragglers via
    ``resource_updation``) and the runtime knobs (bucket size, checkpoint
    interval, all-reduce routing policy) that the trainers pick up at step
-   boundaries.  The epochs' all-reduce probe tables (``comm/probe``, written by
-   DP rank 0 of each epoch) go to the Brain with the metrics.
+   boundaries.  The epochs' all-reduce probe tables (``comm/probe/dp`` and
+   ``comm/probe/tp``, written by rank 0 of each group) go to the Brain with the metrics.
 
 Runtime knobs travel as ONE versioned document, ``plan/runtime/<v>``, written
 before the counter ``plan/version`` moves to ``v``: every rank switches to the
@@ -120,8 +120,8 @@ class PlanLoop:
             prof = profs.get(n.split(":")[0])
             if prof is not None:
                 metrics[n] = dict(metrics[n], rocprof=prof)
-        comm = master.kv.get("comm/probe")     # KV.get decodes JSON
-        newp = self.brain.next_plan(self.features(), self.plan, metrics, comm if isinstance(comm, dict) else None)
+        comm = {g: d for g in ("dp", "tp") if isinstance(d := master.kv.get(f"comm/probe/{g}"), dict)}
+        newp = self.brain.next_plan(self.features(), self.plan, metrics, comm or None)
         if newp is None:
             return
         master.events.emit("replan", reason=newp.reason)

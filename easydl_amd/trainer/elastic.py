@@ -287,14 +287,23 @@ class ElasticTrainer:
                     continue
             return
 
+    def _comm_groups(self):
+        """(name, communicator) of this rank's data-plane groups: DP, and TP when sharded."""
+        out = [("dp", self.dp_comm)]
+        if self.tp > 1 and getattr(self.comm, "tp", None) is not None:
+            out.append(("tp", self.comm.tp))
+        return out
+
     def _publish_probe(self) -> None:
-        """The epoch's RCCL-vs-engine table goes to the Brain (``comm/probe``): rank 0 only."""
-        probe = getattr(self.dp_comm, "xgmi_probe", None)
-        if probe and self.comm.rank == 0:
-            doc = {"epoch": self.comm.epoch, "world": self.dp_comm.world_size, "probe": probe}
-            self.kv.set("comm/probe", json.dumps(doc))
-            self.events.emit("allreduce_probe", epoch=self.comm.epoch, world=self.dp_comm.world_size,
-                             selected=probe.get("selected"), policy=probe.get("policy"))
+        """The epoch's RCCL-vs-engine tables go to the Brain (``comm/probe/<group>``), one
+        per group, written by the group's rank 0."""
+        for group, c in self._comm_groups():
+            probe = getattr(c, "xgmi_probe", None)
+            if probe and c.rank == 0:
+                doc = {"epoch": self.comm.epoch, "world": c.world_size, "group": group, "probe": probe}
+                self.kv.set(f"comm/probe/{group}", json.dumps(doc))
+                self.events.emit("allreduce_probe", epoch=self.comm.epoch, group=group, world=c.world_size,
+                                 selected=probe.get("selected"), policy=probe.get("policy"))
 
     def _agree_runtime_plan(self) -> None:
         """Every rank of the new epoch switches to the same runtime plan: the highest plan
@@ -651,11 +660,12 @@ class ElasticTrainer:
         ci = doc.get("ckpt_interval")
         if ci and self.checkpoint is not None:
             self.checkpoint.interval = max(1, int(ci))
-        ar = doc.get("allreduce")
-        apply = getattr(self.dp_comm, "apply_allreduce_policy", None)
-        if ar and apply is not None and int(ar.get("world", -1)) == self.dp_comm.world_size:
-            if apply(ar["policy"]):
-                self.events.emit("plan_allreduce", step=self.step, world=ar["world"], policy=ar["policy"])
+        for group, c in self._comm_groups():
+            ar = (doc.get("allreduce") or {}).get(group)
+            apply = getattr(c, "apply_allreduce_policy", None)
+            if ar and apply is not None and int(ar.get("world", -1)) == c.world_size and apply(ar["policy"]):
+                self.events.emit("plan_allreduce", step=self.step, group=group, world=ar["world"],
+                                 policy=ar["policy"])
 
     def _reconfigure(self):
         old = self.comm

@@ -165,8 +165,8 @@ def test_brain_allreduce_policy_from_probe_median_and_bucket_knee():
     plan = _plan(workers=8, bucket=32.0)
     m = {f"w{i}": {"step_time": 1.0, "window": 20} for i in range(8)}
     nxt = p.next_plan(feat, _inv(8, busy=90), plan, m, _probe(1, 8, rccl, good))
-    assert nxt is not None and nxt.allreduce["world"] == 8
-    pol = nxt.allreduce["policy"]
+    assert nxt is not None and nxt.allreduce["dp"]["world"] == 8
+    pol = nxt.allreduce["dp"]["policy"]
     assert pol["oneshot_max_kb"] == 1024 and pol["xgmi_min_kb_inplace"] == 0
     assert pol["xgmi_min_kb_staged"] is None and pol["oneshot_max_staged_kb"] == 1024
     assert pol["bucket_floor_mb"] == 32.0 and nxt.bucket_mb >= 32.0     # autotune goes on above the floor
@@ -181,7 +181,7 @@ def test_brain_allreduce_policy_from_probe_median_and_bucket_knee():
     assert decide_from_probe(_probe(0, 8, rccl, narrow)["probe"], 8)["xgmi_min_kb_inplace"] == 0
     p2 = Planner()
     nxt = p2.next_plan(feat, _inv(8, busy=90), _plan(workers=8), m, _probe(0, 8, rccl, narrow))
-    assert nxt.allreduce["policy"]["xgmi_min_kb_inplace"] is None, nxt.allreduce
+    assert nxt.allreduce["dp"]["policy"]["xgmi_min_kb_inplace"] is None, nxt.allreduce
     # inexact probes are never used
     p3 = Planner()
     assert p3.next_plan(feat, _inv(8, busy=90), _plan(workers=8), {}, _probe(0, 8, rccl, good, exact=False)) is None
@@ -195,8 +195,8 @@ def test_brain_bucket_floor_skips_sizes_below_the_knee():
     plan = _plan(workers=8, bucket=32.0)
     m = {f"w{i}": {"step_time": 1.0, "window": 20} for i in range(8)}
     nxt = p.next_plan(feat, _inv(8, busy=90), plan, m, _probe(1, 8, rccl, [9.0] * 4))
-    assert nxt is not None and nxt.allreduce["policy"]["xgmi_min_kb_inplace"] in (0, None)
-    floor = nxt.allreduce["policy"]["bucket_floor_mb"]
+    assert nxt is not None and nxt.allreduce["dp"]["policy"]["xgmi_min_kb_inplace"] in (0, None)
+    floor = nxt.allreduce["dp"]["policy"]["bucket_floor_mb"]
     assert floor == 128.0 and nxt.bucket_mb == 128.0, (floor, nxt.reason)
 
 
@@ -244,13 +244,17 @@ def test_plan_loop_writes_one_versioned_runtime_document(tmp_path):
     assert kv.get("plan/runtime/1")["bucket_mb"] == 32.0
     for i in range(8):
         kv.set(f"metrics/w{i}", json.dumps({"step_time": 1.0, "window": 20}))
-    kv.set("comm/probe", json.dumps(_probe(1, 8, [0.040, 0.080, 0.400, 1.500], [0.045, 0.060, 0.300, 1.100])))
+    kv.set("comm/probe/dp", json.dumps(_probe(1, 8, [0.040, 0.080, 0.400, 1.500], [0.045, 0.060, 0.300, 1.100])))
+    kv.set("comm/probe/tp", json.dumps(_probe(1, 4, [0.040, 0.080, 0.400, 1.500], [0.09, 0.2, 0.9, 3.0])))
     import time
     time.sleep(0.01)
     loop.maybe_replan(master)
     assert kv.counter("plan/version") == 2
     doc = kv.get("plan/runtime/2")
-    assert doc["allreduce"]["world"] == 8 and doc["allreduce"]["policy"]["oneshot_max_kb"] == 1024
+    assert doc["allreduce"]["dp"]["world"] == 8 and doc["allreduce"]["dp"]["policy"]["oneshot_max_kb"] == 1024
+    # the TP group (4 ranks) gets its own policy: its engine loses at every two-shot size
+    assert doc["allreduce"]["tp"]["world"] == 4
+    assert doc["allreduce"]["tp"]["policy"]["xgmi_min_kb_inplace"] is None
     assert json.loads(kv.get_str("jobresource"))["spec"]["allreduce"] == doc["allreduce"]
 
 
