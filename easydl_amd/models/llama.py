@@ -144,12 +144,15 @@ class LlamaBlock(nn.Module):
         # inside the GEMM ops instead of tp_copy / tp_reduce
         self.tp_dx_reduce = None
         self.tp_out_reduce = None
+        # sequence parallel: column-parallel weight gradients on the side stream, beside the
+        # reduce-scatter of their input gradient
+        self.tp_wgrad_side = False
 
     def _attn(self, n1, B, S, cos, sin):
         hd = self.cfg.head_dim
         if self.tp_copy is not None:
             n1 = self.tp_copy(n1)
-        qkv = fused.linear(n1, self.wqkv, dx_reduce=self.tp_dx_reduce)
+        qkv = fused.linear(n1, self.wqkv, dx_reduce=self.tp_dx_reduce, wgrad_side=self.tp_wgrad_side)
         q, k, v = fused.rope_qkv(qkv, cos, sin, B, S, self.n_heads, self.n_kv, hd)
         o = attention(q, k, v, causal=True)
         o = o.transpose(1, 2).reshape(B * S, self.n_heads * hd)
@@ -162,7 +165,7 @@ class LlamaBlock(nn.Module):
         if self.tp_copy is not None:
             n2 = self.tp_copy(n2)
         m = fused.swiglu_mlp(n2, self.w_gu, self.w_down, dx_reduce=self.tp_dx_reduce,
-                             out_reduce=self.tp_out_reduce)
+                             out_reduce=self.tp_out_reduce, wgrad_side=self.tp_wgrad_side)
         if self.tp_reduce is not None:
             m = self.tp_reduce(m)
         return m

@@ -315,7 +315,7 @@ def _chunked_reduced_mm(x2, w, start, out=None):
 
 class _LinearFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, dx_reduce=None, out_reduce=None):
+    def forward(ctx, x, w, b, dx_reduce=None, out_reduce=None, wgrad_side=False):
         x2 = x.reshape(-1, x.shape[-1])
         if out_reduce is not None:
             if b is not None:
@@ -328,6 +328,7 @@ class _LinearFn(torch.autograd.Function):
         ctx.has_b = b is not None
         ctx.b = b
         ctx.dx_reduce = dx_reduce
+        ctx.wgrad_side = wgrad_side
         return y.view(*x.shape[:-1], w.shape[0])
 
     @staticmethod
@@ -353,7 +354,7 @@ class _LinearFn(torch.autograd.Function):
                 a, b_ = dyT, _transposed(x2).t()   # dY^T (contiguous) @ (X^T)^T: NT GEMM
             else:
                 a, b_ = dy2.t(), x2
-            dw = _deliver_wgrad(w, a, b_)
+            dw = _deliver_wgrad(w, a, b_, side=ctx.wgrad_side)
         if want_db:
             b = ctx.b
             if bias_partial is not None:
@@ -370,13 +371,15 @@ class _LinearFn(torch.autograd.Function):
                     db = g.to(b.dtype)
         if fin is not None:
             dx = fin()
-        return dx, dw, db, None, None
+        return dx, dw, db, None, None, None
 
 
-def linear(x, w, b=None, *, dx_reduce=None, out_reduce=None):
-    """``x @ w^T + b``; ``dx_reduce`` / ``out_reduce``: tensor-parallel overlap hooks (above)."""
+def linear(x, w, b=None, *, dx_reduce=None, out_reduce=None, wgrad_side=False):
+    """``x @ w^T + b``; ``dx_reduce`` / ``out_reduce``: tensor-parallel overlap hooks (above);
+    ``wgrad_side``: the weight-gradient GEMM runs on the side stream, so the collective that
+    consumes dX next (sequence parallelism's reduce-scatter) overlaps it."""
     if _native.use_hip(x) or gradsink.is_flat(w) or dx_reduce is not None or out_reduce is not None:
-        return _LinearFn.apply(x, w, b, dx_reduce, out_reduce)
+        return _LinearFn.apply(x, w, b, dx_reduce, out_reduce, wgrad_side)
     return F.linear(x, w, b)
 
 
@@ -420,10 +423,12 @@ def join_side_streams(device) -> None:
         torch.cuda.current_stream(device).wait_stream(side)
 
 
-def _deliver_wgrad(w, a, b_):
-    """dW = a @ b_ into the flat gradient buffer (or returned)."""
+def _deliver_wgrad(w, a, b_, side: bool = False):
+    """dW = a @ b_ into the flat gradient buffer (or returned).  ``side``: on the side stream
+    (also when EDL_WGRAD_STREAM is off) — used where a collective, not another GEMM, runs
+    beside it."""
     if gradsink.is_flat(w):
-        if _WGRAD_STREAM and a.is_cuda:
+        if (_WGRAD_STREAM or side) and a.is_cuda:
             i = _dev_index(a.device)
             main = torch.cuda.current_stream(a.device)
             side = _SIDE.get(i)
@@ -459,7 +464,7 @@ class _SwiGLUMLPFn(torch.autograd.Function):
     in the 15 % slower TN form there)."""
 
     @staticmethod
-    def forward(ctx, x, w_gu, w_down, dx_reduce=None, out_reduce=None):
+    def forward(ctx, x, w_gu, w_down, dx_reduce=None, out_reduce=None, wgrad_side=False):
         k = _native.kernels()
         x2 = x.reshape(-1, x.shape[-1])
         gu = F.linear(x2, w_gu)
@@ -474,6 +479,7 @@ class _SwiGLUMLPFn(torch.autograd.Function):
         wt_gu = _wt_of(w_gu) if ctx.needs_input_grad[0] else None
         ctx.save_for_backward(x2, gu, hT, w_gu, w_down, wt_gu, _wt_of(w_down))
         ctx.dx_reduce = dx_reduce
+        ctx.wgrad_side = wgrad_side
         return y.view(*x.shape[:-1], w_down.shape[0])
 
     @staticmethod
@@ -504,20 +510,22 @@ class _SwiGLUMLPFn(torch.autograd.Function):
             fin = ctx.dx_reduce(dx)
             dw_down = _deliver_wgrad(w_down, _transposed(dy2), hT.t())
             del hT
-        dw_gu = _deliver_wgrad(w_gu, dguT, _transposed(x2).t())
+        dw_gu = _deliver_wgrad(w_gu, dguT, _transposed(x2).t(), side=ctx.wgrad_side)
         if fin is not None:
             dx = fin()
-        return dx, dw_gu, dw_down, None, None
+        return dx, dw_gu, dw_down, None, None, None
 
 
-def swiglu_mlp(x, w_gu, w_down, *, dx_reduce=None, out_reduce=None):
+def swiglu_mlp(x, w_gu, w_down, *, dx_reduce=None, out_reduce=None, wgrad_side=False):
     """Llama MLP ``down(silu(gate) * up)`` with ``w_gu`` = [gate; up] stacked on dim 0.
-    ``dx_reduce`` / ``out_reduce``: tensor-parallel overlap hooks (see ``linear``)."""
+    ``dx_reduce`` / ``out_reduce`` / ``wgrad_side``: tensor-parallel overlap hooks (see
+    ``linear``; ``wgrad_side`` applies to the gate/up weight gradient)."""
     x2 = x.reshape(-1, x.shape[-1])
     if (_MLP_FUSED and _native.use_hip(x) and x.dtype == torch.bfloat16 and _nt_wgrad_ok(x2, x2)
             and x2.shape[0] % 8 == 0 and w_gu.shape[0] % 16 == 0):
-        return _SwiGLUMLPFn.apply(x, w_gu, w_down, dx_reduce, out_reduce)
-    return linear(swiglu(linear(x, w_gu, dx_reduce=dx_reduce)), w_down, out_reduce=out_reduce)
+        return _SwiGLUMLPFn.apply(x, w_gu, w_down, dx_reduce, out_reduce, wgrad_side)
+    return linear(swiglu(linear(x, w_gu, dx_reduce=dx_reduce, wgrad_side=wgrad_side)), w_down,
+                  out_reduce=out_reduce)
 
 
 def _bias_grad(k, b, partial, G, cols, stream):

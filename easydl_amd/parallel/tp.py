@@ -24,7 +24,9 @@ Without SP the collectives overlap compute (``EDL_TP_OVERLAP``, default on): a
 row-parallel GEMM runs in row chunks and each chunk's all-reduce starts on the
 communicator's stream while the next chunk multiplies; a column-parallel GEMM's
 input-gradient all-reduce starts as soon as dX exists and runs under the
-weight-gradient GEMMs (``fused.linear`` / ``fused.swiglu_mlp`` hooks).
+weight-gradient GEMMs (``fused.linear`` / ``fused.swiglu_mlp`` hooks).  With SP,
+the column-parallel weight gradients run on the side stream so each input
+gradient's reduce-scatter overlaps them.
 """
 from __future__ import annotations
 
@@ -249,7 +251,9 @@ class LlamaTP(nn.Module):
             raise ValueError(f"config not divisible by tp={tp}")
         self.cfg, self.g = cfg, g
         self.vshard = cfg.vocab_size // tp
-        self.overlap = tp > 1 and not g.sequence_parallel and os.environ.get("EDL_TP_OVERLAP", "1") != "0"
+        on = os.environ.get("EDL_TP_OVERLAP", "1") != "0"
+        self.overlap = tp > 1 and not g.sequence_parallel and on
+        self.sp_overlap = tp > 1 and g.sequence_parallel and on
         d = cfg.dim
         self.embed = _param((self.vshard, d), cfg.init_std, device, dtype)
         self.layers = nn.ModuleList()
@@ -262,6 +266,9 @@ class LlamaTP(nn.Module):
                 # row-parallel ones (same bytes as the all-reduce, 1/tp the activations)
                 blk.tp_reduce = lambda x, _g=g: scatter_to_sp(x, _g)
                 blk.tp_copy = lambda x, _g=g: gather_from_sp(x, _g)
+                # the reduce-scatter of each column-parallel input gradient runs beside that
+                # GEMM's weight gradient (side stream) instead of after it
+                blk.tp_wgrad_side = self.sp_overlap
             elif self.overlap:
                 # the two all-reduces per block run beside GEMMs: the row-parallel outputs
                 # chunk by chunk behind their own GEMM, the column-parallel input gradients
@@ -321,7 +328,7 @@ class LlamaTP(nn.Module):
             logits = fused.linear(n, self.lm_head, dx_reduce=self.g.all_reduce_start)
         else:
             n = gather_from_sp(n, self.g) if sp else copy_to_tp(n, self.g)
-            logits = fused.linear(n, self.lm_head)
+            logits = fused.linear(n, self.lm_head, wgrad_side=self.sp_overlap)
         if labels is None:
             return logits
         return vocab_parallel_cross_entropy(logits, labels, self.vstart, self.g)
