@@ -691,6 +691,7 @@ __global__ __launch_bounds__(256) void gelu_fwd_t_reg_kernel(const bf16_t* __res
     o8[i] = pack8(x);
     *reinterpret_cast<u32x4*>(h + (int64_t)(r + i) * F + c) = o8[i];
   }
+  if (!hT) return;   // no transposed copy (weight gradient by the TN GEMM, gemm_tn.hip)
   transpose8x8(o8, t8);
 #pragma unroll
   for (int j = 0; j < 8; ++j) *reinterpret_cast<u32x4*>(hT + (int64_t)(c + j) * M + r) = t8[j];
@@ -727,9 +728,11 @@ __global__ __launch_bounds__(256) void gelu_bwd_t_reg_kernel(const bf16_t* __res
       a8[i] = pack8(x);
       *reinterpret_cast<u32x4*>(du + (int64_t)(r + i) * F + c) = a8[i];
     }
-    transpose8x8(a8, d8);
+    if (duT) {   // null: no transposed copy (weight gradient by the TN GEMM)
+      transpose8x8(a8, d8);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) *reinterpret_cast<u32x4*>(duT + (int64_t)(c + j) * M + r) = d8[j];
+      for (int j = 0; j < 8; ++j) *reinterpret_cast<u32x4*>(duT + (int64_t)(c + j) * M + r) = d8[j];
+    }
   }
 #pragma unroll
   for (int k = 0; k < 8; ++k) red[rg][c0 + k] = cs[k];
@@ -813,7 +816,7 @@ int edl_qkv_split(const void* qkv, void* q, void* k, void* v, int64_t T, int HD,
   return 0;
 }
 
-// h = gelu_tanh(u) and hT = h^T (M, F multiples of 8)
+// h = gelu_tanh(u) and hT = h^T (M, F multiples of 8; hT may be null: h only)
 int edl_gelu_fwd_t(const void* u, void* h, void* hT, int M, int F, hipStream_t s) {
   if (F % 8 || M % 8 || M <= 0 || F <= 0) return (int)hipErrorInvalidValue;
   dim3 grid((F + RT - 1) / RT, (M + RT - 1) / RT);
@@ -822,7 +825,7 @@ int edl_gelu_fwd_t(const void* u, void* h, void* hT, int M, int F, hipStream_t s
   return 0;
 }
 
-// du = gelu_tanh'(u) * dh, duT = du^T, partial[edl_transpose_tiles(M), F] = column sums of du
+// du = gelu_tanh'(u) * dh, duT = du^T (may be null), partial[edl_transpose_tiles(M), F] = column sums of du
 int edl_gelu_bwd_t(const void* dh, const void* u, void* du, void* duT, float* partial, int M, int F,
                    hipStream_t s) {
   if (F % 8 || M % 8 || M <= 0 || F <= 0) return (int)hipErrorInvalidValue;

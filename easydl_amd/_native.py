@@ -102,6 +102,11 @@ _KERNEL_SIGS = {
     "edl_ps_multi_copy": [c_void_p, c_void_p, c_int, c_i64, c_void_p, c_int, c_void_p],
     "edl_xgmi_max_blocks": [],
     "edl_diag_lds_dma": [c_void_p, c_void_p, c_int, c_void_p],
+    "edl_gemm_tn_splits": [c_int, c_int, c_int],
+    "edl_gemm_tn_ws_bytes": (c_i64, [c_int, c_int, c_int]),
+    "edl_gemm_tn": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
+    "edl_colsum_bf16_groups": [c_int],
+    "edl_colsum_bf16_partial": [c_void_p, c_int, c_int, c_void_p, c_int, c_void_p],
     "edl_bn_groups": (c_int, [c_i64, c_int]),
     "edl_bn_fwd_train": [c_void_p] * 11 + [c_i64, c_int, c_float, c_float, c_int, c_void_p, c_void_p],
     "edl_bn_apply": [c_void_p] * 4 + [c_i64, c_int, c_int, c_void_p],

@@ -8,13 +8,14 @@ decoder).  Attention (head_dim 64, bidirectional) runs through SDPA.
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from easydl_amd.ops import fused, norms
+from easydl_amd.ops import fused, gradsink, norms
 from easydl_amd.ops.attention import packed_qkv_attention
 
 
@@ -35,6 +36,8 @@ class BertConfig:
 
 
 BERT_LARGE = BertConfig()
+# EDL_RESGRAD=0: autograd sums each layer input's two gradients (A/B switch)
+_RESGRAD = os.environ.get("EDL_RESGRAD", "1") != "0"
 BERT_TINY = BertConfig(vocab_size=512, dim=64, n_layers=2, n_heads=4, ffn_dim=128, max_pos=64)
 
 
@@ -70,7 +73,10 @@ class BertLayer(nn.Module):
     def forward(self, x, B, S, mask=None):
         c = self.c
         H, hd = c.n_heads, c.dim // c.n_heads
-        qkv = fused.linear(x, self.wqkv, self.bqkv)
+        # x's two gradients (qkv input gradient + LN1's residual gradient) meet in the qkv
+        # GEMM's epilogue instead of an add kernel (gradsink.ResidualGrad); same for the MLP
+        r1, r2 = (gradsink.ResidualGrad(), gradsink.ResidualGrad()) if _RESGRAD else (None, None)
+        qkv = fused.linear(x, self.wqkv, self.bqkv, res_grad=r1)
         if qkv.is_cuda and mask is None:
             # HIP kernels, head dim 64; dq / dk / dv land in one packed qkv gradient
             o = packed_qkv_attention(qkv, B, S, H, causal=False)
@@ -82,9 +88,9 @@ class BertLayer(nn.Module):
                 o = F.scaled_dot_product_attention(q.float(), k.float(), v.float(), attn_mask=mask).to(q.dtype)
             o = o.transpose(1, 2).reshape(B * S, c.dim)
         a = fused.linear(o, self.wo, self.bo)
-        x, _ = norms.add_layernorm(a, x, self.ln1_w, self.ln1_b, c.eps)
-        m = fused.gelu_mlp(x, self.w1, self.b1, self.w2, self.b2)
-        x, _ = norms.add_layernorm(m, x, self.ln2_w, self.ln2_b, c.eps)
+        x, _ = norms.add_layernorm(a, x, self.ln1_w, self.ln1_b, c.eps, res_grad=r1)
+        m = fused.gelu_mlp(x, self.w1, self.b1, self.w2, self.b2, res_grad=r2)
+        x, _ = norms.add_layernorm(m, x, self.ln2_w, self.ln2_b, c.eps, res_grad=r2)
         return x
 
 

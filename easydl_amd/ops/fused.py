@@ -286,6 +286,62 @@ def _nt_wgrad_ok(dy2: torch.Tensor, x2: torch.Tensor) -> bool:
             and x2.shape[1] % 8 == 0)
 
 
+# Weight gradients from the row-major operands (csrc/kernels/gemm_tn.hip): dW = dY^T X
+# read straight from dY [M, N] and X [M, J] through transposing LDS reads, so the
+# backward writes no transposed copies at all (no dY / X transposes, the MLP kernels
+# drop their h^T / d(gate_up)^T / du^T outputs).  Applies when N % 128 == 0 and
+# J % 256 == 0.  Measured per shape at M = 16384 (profiles/r03_gemm_tn_ab.md): it beats
+# hipBLASLt NT + the two transposes on every BERT-large weight (N*J <= 4.2 M: 0.05-0.14 ms
+# vs 0.08-0.20 ms) and loses on the Llama-3-8B ones (N*J >= 16.8 M: its 128 x 256 tile
+# runs 0.8-1.2 PF/s against hipBLASLt's 256 x 256 at 1.5+), so by default ("auto") it
+# takes weights of at most EDL_WGRAD_TN_MAX_ELEMS (8 M) elements.  EDL_WGRAD_TN=1: every
+# eligible weight; 0: never (NT form on transposed copies).
+_WGRAD_TN = os.environ.get("EDL_WGRAD_TN", "auto")
+_WGRAD_TN_MAX = int(os.environ.get("EDL_WGRAD_TN_MAX_ELEMS", 8 << 20))
+
+
+def _tn_dims(t: torch.Tensor, N: int, J: int) -> bool:
+    """The TN kernel takes dW [N, J] for activations like ``t`` (bf16 on the GPU)."""
+    if _WGRAD_TN == "0" or (_WGRAD_TN == "auto" and N * J > _WGRAD_TN_MAX):
+        return False
+    return t.is_cuda and t.dtype == torch.bfloat16 and N % 128 == 0 and J % 256 == 0
+
+
+def _tn_ok(dy2: torch.Tensor, x2: torch.Tensor) -> bool:
+    return (_tn_dims(dy2, dy2.shape[1], x2.shape[1]) and x2.dtype == torch.bfloat16
+            and dy2.dim() == 2 and x2.dim() == 2 and dy2.shape[0] == x2.shape[0]
+            and dy2.is_contiguous() and x2.is_contiguous()
+            and dy2.data_ptr() % 16 == 0 and x2.data_ptr() % 16 == 0)
+
+
+def gemm_tn(dy2: torch.Tensor, x2: torch.Tensor, out: torch.Tensor | None = None, accumulate: bool = False):
+    """``dy2^T @ x2`` ([M, N]^T [M, J] -> [N, J]) by the HIP TN kernel, written into (or
+    accumulated onto) ``out`` (bf16 or fp32, contiguous) or a new bf16 tensor."""
+    k = _native.kernels()
+    M, N = dy2.shape
+    J = x2.shape[1]
+    if out is None:
+        out = torch.empty(N, J, dtype=dy2.dtype, device=dy2.device)
+        accumulate = False
+    if out.dtype not in (torch.bfloat16, torch.float32) or not out.is_contiguous() or out.numel() != N * J:
+        raise ValueError("gemm_tn: out must be a contiguous bf16/fp32 [N, J] tensor")
+    nws = k.raw("edl_gemm_tn_ws_bytes")(M, N, J)
+    ws = torch.empty(nws // 4, dtype=torch.float32, device=dy2.device) if nws else None
+    k.check("edl_gemm_tn", dy2.data_ptr(), x2.data_ptr(), out.data_ptr(), M, N, J,
+            int(out.dtype == torch.float32), int(accumulate), _native.ptr(ws), _native.stream_of(dy2))
+    return out
+
+
+def _colsum_partial(t: torch.Tensor) -> tuple[torch.Tensor, int]:
+    """[G, cols] fp32 column-sum partials of a bf16 [M, cols] matrix (reduced by edl_colsum)."""
+    k = _native.kernels()
+    M, C = t.shape
+    G = k("edl_colsum_bf16_groups", M)
+    part = torch.empty(G, C, dtype=torch.float32, device=t.device)
+    k.check("edl_colsum_bf16_partial", t.data_ptr(), M, C, part.data_ptr(), G, _native.stream_of(t))
+    return part, G
+
+
 # Tensor-parallel overlap hooks (parallel/tp.py).  ``out_reduce``: the output of a
 # row-parallel GEMM is a partial sum; it is computed in row chunks and each chunk's
 # all-reduce starts (on the communicator's stream) while the next chunk's GEMM runs.
@@ -315,8 +371,12 @@ def _chunked_reduced_mm(x2, w, start, out=None):
 
 class _LinearFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, dx_reduce=None, out_reduce=None, wgrad_side=False):
+    def forward(ctx, x, w, b, dx_reduce=None, out_reduce=None, wgrad_side=False, res_grad=None):
         x2 = x.reshape(-1, x.shape[-1])
+        ctx.res_grad = None
+        if res_grad is not None and dx_reduce is None and ctx.needs_input_grad[0]:
+            res_grad.arm()
+            ctx.res_grad = res_grad
         if out_reduce is not None:
             if b is not None:
                 raise ValueError("row-parallel linear with an output all-reduce takes no bias")
@@ -338,23 +398,28 @@ class _LinearFn(torch.autograd.Function):
         dx = None
         fin = None
         if ctx.needs_input_grad[0]:
-            dx = (torch.mm(dy2, wt.t()) if wt is not None else torch.mm(dy2, w)).view(*dy.shape[:-1], w.shape[1])
+            dx = gradsink.input_grad_mm(dy2, wt.t() if wt is not None else w, ctx.res_grad,
+                                        (*dy.shape[:-1], w.shape[1]))
             if ctx.dx_reduce is not None:
                 fin = ctx.dx_reduce(dx)      # runs under the weight-gradient GEMM below
         dw = db = None
         bias_partial = None   # (partial slab, G): bias gradient computed by the dY transpose
         want_db = ctx.has_b and ctx.needs_input_grad[2]
         if ctx.needs_input_grad[1]:
-            if _nt_wgrad_ok(dy2, x2):
+            if _tn_ok(dy2, x2):
+                if want_db:
+                    bias_partial = _colsum_partial(dy2)
+                dw = _deliver_wgrad(w, dy2, x2, side=ctx.wgrad_side, tn=True)
+            elif _nt_wgrad_ok(dy2, x2):
                 if want_db:
                     dyT, part, G = _transposed_colsum(dy2)
                     bias_partial = (part, G)
                 else:
                     dyT = _transposed(dy2)
                 a, b_ = dyT, _transposed(x2).t()   # dY^T (contiguous) @ (X^T)^T: NT GEMM
+                dw = _deliver_wgrad(w, a, b_, side=ctx.wgrad_side)
             else:
-                a, b_ = dy2.t(), x2
-            dw = _deliver_wgrad(w, a, b_, side=ctx.wgrad_side)
+                dw = _deliver_wgrad(w, dy2.t(), x2, side=ctx.wgrad_side)
         if want_db:
             b = ctx.b
             if bias_partial is not None:
@@ -371,15 +436,17 @@ class _LinearFn(torch.autograd.Function):
                     db = g.to(b.dtype)
         if fin is not None:
             dx = fin()
-        return dx, dw, db, None, None, None
+        return dx, dw, db, None, None, None, None
 
 
-def linear(x, w, b=None, *, dx_reduce=None, out_reduce=None, wgrad_side=False):
+def linear(x, w, b=None, *, dx_reduce=None, out_reduce=None, wgrad_side=False, res_grad=None):
     """``x @ w^T + b``; ``dx_reduce`` / ``out_reduce``: tensor-parallel overlap hooks (above);
     ``wgrad_side``: the weight-gradient GEMM runs on the side stream, so the collective that
-    consumes dX next (sequence parallelism's reduce-scatter) overlaps it."""
-    if _native.use_hip(x) or gradsink.is_flat(w) or dx_reduce is not None or out_reduce is not None:
-        return _LinearFn.apply(x, w, b, dx_reduce, out_reduce, wgrad_side)
+    consumes dX next (sequence parallelism's reduce-scatter) overlaps it; ``res_grad``: a
+    :class:`gradsink.ResidualGrad` slot whose parked residual gradient dX accumulates onto."""
+    if (_native.use_hip(x) or gradsink.is_flat(w) or dx_reduce is not None or out_reduce is not None
+            or res_grad is not None):
+        return _LinearFn.apply(x, w, b, dx_reduce, out_reduce, wgrad_side, res_grad)
     return F.linear(x, w, b)
 
 
@@ -423,10 +490,21 @@ def join_side_streams(device) -> None:
         torch.cuda.current_stream(device).wait_stream(side)
 
 
-def _deliver_wgrad(w, a, b_, side: bool = False):
-    """dW = a @ b_ into the flat gradient buffer (or returned).  ``side``: on the side stream
+def _write_tn(w, dy2, x2):
+    g = w.grad
+    gemm_tn(dy2, x2, out=g.view(dy2.shape[1], x2.shape[1]), accumulate=not gradsink.is_fresh(w))
+    gradsink.commit(w)
+
+
+def _deliver_wgrad(w, a, b_, side: bool = False, tn: bool = False):
+    """dW = a @ b_ into the flat gradient buffer (or returned); ``tn``: a = dY, b_ = X (both
+    row-major [M, *]) and dW = a^T b_ by the TN kernel.  ``side``: on the side stream
     (also when EDL_WGRAD_STREAM is off) — used where a collective, not another GEMM, runs
     beside it."""
+    if tn and not (gradsink.is_flat(w) and w.grad.dtype in (torch.bfloat16, torch.float32)
+                   and w.grad.is_contiguous()):
+        return gemm_tn(a, b_)
+    write = _write_tn if tn else gradsink.write_mm
     if gradsink.is_flat(w):
         if (_WGRAD_STREAM or side) and a.is_cuda:
             i = _dev_index(a.device)
@@ -437,7 +515,7 @@ def _deliver_wgrad(w, a, b_, side: bool = False):
             _MAIN[i] = main
             side.wait_stream(main)
             with torch.cuda.stream(side):
-                gradsink.write_mm(w, a, b_)
+                write(w, a, b_)
             a.record_stream(side)
             b_.record_stream(side)
             if not _JOIN_QUEUED.get(i):
@@ -450,7 +528,7 @@ def _deliver_wgrad(w, a, b_, side: bool = False):
                     main.wait_stream(side)
                 torch.autograd.Variable._execution_engine.queue_callback(_join)
             return None
-        gradsink.write_mm(w, a, b_)
+        write(w, a, b_)
         return None
     return torch.mm(a, b_)
 
@@ -470,14 +548,22 @@ class _SwiGLUMLPFn(torch.autograd.Function):
         gu = F.linear(x2, w_gu)
         M, F2 = gu.shape
         Fh = F2 // 2
+        # TN weight gradients need h itself; the NT form needs only h^T (saved instead of h)
+        ctx.tn = _tn_dims(x2, w_down.shape[0], Fh) and _tn_dims(x2, F2, x2.shape[1])
         h = torch.empty(M, Fh, dtype=gu.dtype, device=gu.device)
-        hT = torch.empty(Fh, M, dtype=gu.dtype, device=gu.device)
         st = _native.stream_of(gu)
-        k.check("edl_swiglu_fwd_t", gu.data_ptr(), h.data_ptr(), hT.data_ptr(), M, Fh, st)
+        if ctx.tn:
+            hT = None
+            k.check("edl_swiglu_fwd", gu.data_ptr(), h.data_ptr(), M, Fh, st)
+        else:
+            hT = torch.empty(Fh, M, dtype=gu.dtype, device=gu.device)
+            k.check("edl_swiglu_fwd_t", gu.data_ptr(), h.data_ptr(), hT.data_ptr(), M, Fh, st)
         y = _chunked_reduced_mm(h, w_down, out_reduce) if out_reduce is not None else F.linear(h, w_down)
-        del h
+        if not ctx.tn:
+            del h
+            h = hT
         wt_gu = _wt_of(w_gu) if ctx.needs_input_grad[0] else None
-        ctx.save_for_backward(x2, gu, hT, w_gu, w_down, wt_gu, _wt_of(w_down))
+        ctx.save_for_backward(x2, gu, h, w_gu, w_down, wt_gu, _wt_of(w_down))
         ctx.dx_reduce = dx_reduce
         ctx.wgrad_side = wgrad_side
         return y.view(*x.shape[:-1], w_down.shape[0])
@@ -485,32 +571,47 @@ class _SwiGLUMLPFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         k = _native.kernels()
-        x2, gu, hT, w_gu, w_down, wt_gu, wt_down = ctx.saved_tensors
+        x2, gu, hs, w_gu, w_down, wt_gu, wt_down = ctx.saved_tensors   # hs: h (TN) or h^T (NT)
         dy2 = dy.reshape(-1, dy.shape[-1]).contiguous()
         M, F2 = gu.shape
         Fh = F2 // 2
         st = _native.stream_of(gu)
+        tn = ctx.tn
+
+        def down_wgrad():
+            if tn:
+                return _deliver_wgrad(w_down, dy2, hs, tn=True)
+            return _deliver_wgrad(w_down, _transposed(dy2), hs.t())
+
         dh = torch.mm(dy2, wt_down.t()) if wt_down is not None else torch.mm(dy2, w_down)
         overlap = ctx.dx_reduce is not None and ctx.needs_input_grad[0]
         dw_down = None
         if not overlap:
-            dw_down = _deliver_wgrad(w_down, _transposed(dy2), hT.t())
-            del hT
+            dw_down = down_wgrad()
+            del hs
         dgu = torch.empty_like(gu)
-        dguT = torch.empty(F2, M, dtype=gu.dtype, device=gu.device)
-        k.check("edl_swiglu_bwd_t", dh.data_ptr(), gu.data_ptr(), dgu.data_ptr(), dguT.data_ptr(), M, Fh, st)
+        if tn:
+            dguT = None
+            k.check("edl_swiglu_bwd", dh.data_ptr(), gu.data_ptr(), dgu.data_ptr(), M, Fh, st)
+        else:
+            dguT = torch.empty(F2, M, dtype=gu.dtype, device=gu.device)
+            k.check("edl_swiglu_bwd_t", dh.data_ptr(), gu.data_ptr(), dgu.data_ptr(), dguT.data_ptr(), M, Fh, st)
         del dh
         dx = fin = None
         if ctx.needs_input_grad[0]:
             dx = torch.mm(dgu, wt_gu.t()) if wt_gu is not None else torch.mm(dgu, w_gu)
             dx = dx.view(*dy.shape[:-1], w_gu.shape[1])
-        del dgu
+        if not tn:
+            del dgu
         if overlap:
             # tensor parallel: dX's all-reduce runs under BOTH weight-gradient GEMMs
             fin = ctx.dx_reduce(dx)
-            dw_down = _deliver_wgrad(w_down, _transposed(dy2), hT.t())
-            del hT
-        dw_gu = _deliver_wgrad(w_gu, dguT, _transposed(x2).t(), side=ctx.wgrad_side)
+            dw_down = down_wgrad()
+            del hs
+        if tn:
+            dw_gu = _deliver_wgrad(w_gu, dgu, x2, side=ctx.wgrad_side, tn=True)
+        else:
+            dw_gu = _deliver_wgrad(w_gu, dguT, _transposed(x2).t(), side=ctx.wgrad_side)
         if fin is not None:
             dx = fin()
         return dx, dw_gu, dw_down, None, None, None
@@ -544,57 +645,73 @@ class _GeluMLPFn(torch.autograd.Function):
     kernels, the transpose of h and the transpose + column sum of du."""
 
     @staticmethod
-    def forward(ctx, x, w1, b1, w2, b2):
+    def forward(ctx, x, w1, b1, w2, b2, res_grad=None):
         k = _native.kernels()
         x2 = x.reshape(-1, x.shape[-1])
+        ctx.res_grad = None
+        if res_grad is not None and ctx.needs_input_grad[0]:
+            res_grad.arm()
+            ctx.res_grad = res_grad
         u = F.linear(x2, w1, b1)
         M, Fd = u.shape
+        ctx.tn = _tn_dims(x2, w2.shape[0], Fd) and _tn_dims(x2, Fd, x2.shape[1])
         h = torch.empty_like(u)
-        hT = torch.empty(Fd, M, dtype=u.dtype, device=u.device)
+        hT = None if ctx.tn else torch.empty(Fd, M, dtype=u.dtype, device=u.device)
         st = _native.stream_of(u)
-        k.check("edl_gelu_fwd_t", u.data_ptr(), h.data_ptr(), hT.data_ptr(), M, Fd, st)
+        k.check("edl_gelu_fwd_t", u.data_ptr(), h.data_ptr(), _native.ptr(hT), M, Fd, st)
         y = F.linear(h, w2, b2)
+        hs = h if ctx.tn else hT   # TN weight gradients read h itself, the NT form h^T
         del h
         wt1 = _wt_of(w1) if ctx.needs_input_grad[0] else None
-        ctx.save_for_backward(x2, u, hT, w1, w2, wt1, _wt_of(w2))
+        ctx.save_for_backward(x2, u, hs, w1, w2, wt1, _wt_of(w2))
         ctx.b1, ctx.b2 = b1, b2
         return y.view(*x.shape[:-1], w2.shape[0])
 
     @staticmethod
     def backward(ctx, dy):
         k = _native.kernels()
-        x2, u, hT, w1, w2, wt1, wt2 = ctx.saved_tensors
+        x2, u, hs, w1, w2, wt1, wt2 = ctx.saved_tensors   # hs: h (TN) or h^T (NT)
         dy2 = dy.reshape(-1, dy.shape[-1]).contiguous()
         M, Fd = u.shape
         st = _native.stream_of(u)
+        tn = ctx.tn
         dh = torch.mm(dy2, wt2.t()) if wt2 is not None else torch.mm(dy2, w2)
-        dyT, part2, G = _transposed_colsum(dy2)
-        dw2 = _deliver_wgrad(w2, dyT, hT.t())
-        del hT, dyT
-        db2 = _bias_grad(k, ctx.b2, part2, G, dy2.shape[1], st) if ctx.needs_input_grad[4] else None
+        if tn:
+            part2, G2 = _colsum_partial(dy2)
+            dw2 = _deliver_wgrad(w2, dy2, hs, tn=True)
+        else:
+            dyT, part2, G2 = _transposed_colsum(dy2)
+            dw2 = _deliver_wgrad(w2, dyT, hs.t())
+            del dyT
+        del hs
+        db2 = _bias_grad(k, ctx.b2, part2, G2, dy2.shape[1], st) if ctx.needs_input_grad[4] else None
         du = torch.empty_like(u)
-        duT = torch.empty(Fd, M, dtype=u.dtype, device=u.device)
+        duT = None if tn else torch.empty(Fd, M, dtype=u.dtype, device=u.device)
+        G = k("edl_transpose_tiles", M)
         part1 = torch.empty(G, Fd, dtype=torch.float32, device=u.device)
-        k.check("edl_gelu_bwd_t", dh.data_ptr(), u.data_ptr(), du.data_ptr(), duT.data_ptr(), part1.data_ptr(),
+        k.check("edl_gelu_bwd_t", dh.data_ptr(), u.data_ptr(), du.data_ptr(), _native.ptr(duT), part1.data_ptr(),
                 M, Fd, st)
         del dh
         dx = None
         if ctx.needs_input_grad[0]:
-            dx = torch.mm(du, wt1.t()) if wt1 is not None else torch.mm(du, w1)
-            dx = dx.view(*dy.shape[:-1], w1.shape[1])
+            dx = gradsink.input_grad_mm(du, wt1.t() if wt1 is not None else w1, ctx.res_grad,
+                                        (*dy.shape[:-1], w1.shape[1]))
+        if tn:
+            dw1 = _deliver_wgrad(w1, du, x2, tn=True)
+        else:
+            dw1 = _deliver_wgrad(w1, duT, _transposed(x2).t())
         del du
-        dw1 = _deliver_wgrad(w1, duT, _transposed(x2).t())
         db1 = _bias_grad(k, ctx.b1, part1, G, Fd, st) if ctx.needs_input_grad[2] else None
-        return dx, dw1, db1, dw2, db2
+        return dx, dw1, db1, dw2, db2, None
 
 
-def gelu_mlp(x, w1, b1, w2, b2):
-    """BERT MLP ``fc2(gelu_tanh(fc1(x)))`` (biases ``b1``, ``b2``)."""
+def gelu_mlp(x, w1, b1, w2, b2, res_grad=None):
+    """BERT MLP ``fc2(gelu_tanh(fc1(x)))`` (biases ``b1``, ``b2``); ``res_grad``: see ``linear``."""
     x2 = x.reshape(-1, x.shape[-1])
     if (_MLP_FUSED and _native.use_hip(x) and x.dtype == torch.bfloat16 and _nt_wgrad_ok(x2, x2)
             and x2.shape[0] % 8 == 0 and w1.shape[0] % 8 == 0 and b1 is not None and b2 is not None):
-        return _GeluMLPFn.apply(x, w1, b1, w2, b2)
-    return linear(F.gelu(linear(x, w1, b1), approximate="tanh"), w2, b2)
+        return _GeluMLPFn.apply(x, w1, b1, w2, b2, res_grad)
+    return linear(F.gelu(linear(x, w1, b1, res_grad=res_grad), approximate="tanh"), w2, b2)
 
 
 class _EmbeddingFn(torch.autograd.Function):

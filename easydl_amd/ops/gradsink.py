@@ -45,6 +45,52 @@ def write(p: torch.Tensor, g: torch.Tensor) -> None:
     commit(p)
 
 
+class ResidualGrad:
+    """Hand-off of a residual-path gradient to the GEMM that makes the other gradient of
+    the same tensor.
+
+    In a post-norm block ``y = norm(f(x) + x)`` the input ``x`` gets two gradients: the
+    norm's residual gradient and ``f``'s first GEMM's input gradient ``dY W``; autograd
+    sums them with a separate add kernel.  With a slot shared by the two ops, the norm's
+    backward (which always runs first: ``f(x)`` feeds it) parks its residual gradient
+    here instead of returning it, and the GEMM accumulates into it in place
+    (``r.addmm_(dY, W)``: hipBLASLt with beta = 1), so the add costs only the GEMM
+    epilogue's read of ``r``.  A slot serves one forward/backward pass.  The GEMM op arms
+    the slot in its forward (it will take the gradient in its backward); the norm uses
+    the slot only when it is armed, so a consumer that cannot take it (a fallback path)
+    never loses the residual gradient."""
+
+    __slots__ = ("g", "armed")
+
+    def __init__(self):
+        self.g = None
+        self.armed = False
+
+    def arm(self) -> None:
+        self.armed = True
+
+    def put(self, g: torch.Tensor) -> None:
+        if self.g is not None:
+            raise RuntimeError("ResidualGrad: a residual gradient is already parked (slot reused?)")
+        self.g = g
+
+    def take(self):
+        g, self.g = self.g, None
+        return g
+
+
+def input_grad_mm(dy2: torch.Tensor, w: torch.Tensor, slot: "ResidualGrad | None", shape) -> torch.Tensor:
+    """``dy2 @ w`` (+ the residual gradient parked in ``slot``, accumulated in place)."""
+    r = slot.take() if slot is not None else None
+    if r is None:
+        return torch.mm(dy2, w).view(*shape)
+    r2 = r.view(dy2.shape[0], w.shape[1])
+    if r2.dtype != dy2.dtype or not r2.is_contiguous():
+        return (torch.mm(dy2, w) + r2).view(*shape)
+    r2.addmm_(dy2, w)
+    return r2.view(*shape)
+
+
 def write_mm(p: torch.Tensor, a: torch.Tensor, b: torch.Tensor) -> None:
     """Deliver ``a @ b`` into ``p.grad`` without a temporary when dtypes allow."""
     tgt = p.grad

@@ -50,7 +50,7 @@ def _deliver_colsum(k, p, partial, G, cols, stream):
 
 class _NormFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, res, w, b, eps, ln):
+    def forward(ctx, x, res, w, b, eps, ln, slot=None):
         k = _native.kernels()
         cols = x.shape[-1]
         if cols % 8 or cols > k("edl_norm_max_cols"):
@@ -79,6 +79,7 @@ class _NormFn(torch.autograd.Function):
         ctx.save_for_backward(src, w, b if ln else None, mean, rstd)
         ctx.ln = ln
         ctx.has_res = res is not None
+        ctx.slot = slot if res is not None and slot is not None and slot.armed else None
         if s is not None:
             return y, s
         return y
@@ -107,7 +108,12 @@ class _NormFn(torch.autograd.Function):
         db = None
         if ctx.ln and ctx.needs_input_grad[3]:
             db = _deliver_colsum(k, b, pb, G, cols, st)
-        return dx, (dx if ctx.has_res else None), dw, db, None, None
+        dres = dx if ctx.has_res else None
+        if ctx.slot is not None and ctx.needs_input_grad[1]:
+            # the residual input's other gradient comes from a GEMM that accumulates onto this one
+            ctx.slot.put(dx)
+            dres = None
+        return dx, dres, dw, db, None, None, None
 
 
 def rmsnorm(x, w, eps: float = 1e-5):
@@ -132,10 +138,13 @@ def layernorm(x, w, b, eps: float = 1e-5):
     return layernorm_ref(x, w, b, eps)
 
 
-def add_layernorm(x, residual, w, b, eps: float = 1e-5):
+def add_layernorm(x, residual, w, b, eps: float = 1e-5, res_grad: gradsink.ResidualGrad | None = None):
+    """``(layernorm(x + residual), x + residual)``.  ``res_grad``: a slot shared with the GEMM
+    that consumed ``residual`` (see :class:`gradsink.ResidualGrad`) -- the residual's gradient
+    is handed to that GEMM's input gradient instead of being summed by autograd."""
     if residual is None:
         return layernorm(x, w, b, eps), x
     if _native.use_hip(x):
-        return _NormFn.apply(x, residual, w, b, eps, True)
+        return _NormFn.apply(x, residual, w, b, eps, True, res_grad)
     s = x + residual
     return layernorm_ref(s, w, b, eps), s

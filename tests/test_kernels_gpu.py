@@ -405,3 +405,100 @@ def test_side_stream_weight_gradients_match_compute_stream(cuda, monkeypatch):
         grads.append(torch.cat([g.grad.float().clone() for g in flat.groups]))
     err = ((grads[0] - grads[1]).abs().max() / grads[0].abs().max()).item()
     assert err < 1e-2, err   # same GEMMs on another stream; an ordering race shows as O(1) errors
+
+
+@pytest.mark.parametrize("flat", [False, True])
+def test_bert_layer_residual_grad_slots_match_fp32(cuda, flat, monkeypatch):
+    """A post-LN BERT layer on the HIP kernels, where the input's two gradients (the qkv /
+    fc1 GEMM input gradient and LayerNorm's residual gradient) are summed in the GEMM
+    epilogue (gradsink.ResidualGrad, addmm_ with beta = 1) instead of an add kernel, vs the
+    same layer in fp32 on the CPU: input gradient and every parameter gradient, over two
+    accumulated micro-batches; both slots are used."""
+    from easydl_amd.models.bert import BertConfig, BertLayer
+    from easydl_amd.ops import gradsink
+    from easydl_amd.parallel.flat import FlatParams
+    used = []
+    orig = gradsink.input_grad_mm
+
+    def counting(dy2, w, slot, shape):
+        used.append(slot is not None and slot.g is not None)
+        return orig(dy2, w, slot, shape)
+    monkeypatch.setattr(gradsink, "input_grad_mm", counting)
+    torch.manual_seed(5)
+    c = BertConfig(vocab_size=512, dim=256, n_layers=1, n_heads=4, ffn_dim=1024, max_pos=128)
+    layer = BertLayer(c, cuda, torch.bfloat16)
+    with torch.no_grad():
+        for p in layer.parameters():
+            p.add_(0.05 * torch.randn_like(p))
+    ref = BertLayer(c, "cpu", torch.float32)
+    ref.load_state_dict({k: v.float().cpu() for k, v in layer.state_dict().items()})
+    if flat:
+        FlatParams(layer)
+    fused.new_weight_generation()
+    B, S = 2, 128
+    for mb in range(2):
+        x = torch.randn(B * S, c.dim, device=cuda).bfloat16().requires_grad_(True)
+        y = layer(x, B, S)
+        dy = torch.randn_like(y)
+        y.backward(dy)
+        xr = x.detach().float().cpu().requires_grad_(True)
+        yr = ref(xr, B, S)
+        yr.backward(dy.float().cpu())
+        _close(y.cpu(), yr, 3e-2)
+        _close(x.grad.cpu(), xr.grad, 3e-2)
+    assert sum(used) == 4, used   # qkv + fc1 input gradients took their slot, per micro-batch
+    for (n, p), r in zip(layer.named_parameters(), ref.parameters()):
+        err = ((p.grad.float().cpu() - r.grad).abs().max() / (r.grad.abs().max() + 1e-6)).item()
+        assert err < 3e-2, (n, err)
+
+
+@pytest.mark.parametrize("M,N,J", [(1000, 128, 256), (2048, 1024, 1024), (4096, 256, 512), (96, 384, 768),
+                                   (16384, 128, 256)])
+@pytest.mark.parametrize("out_dt", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("acc", [False, True])
+def test_gemm_tn_matches_fp32(cuda, M, N, J, out_dt, acc):
+    """edl_gemm_tn (dW = dY^T X from the row-major operands via transposing LDS reads) vs
+    fp32 torch: row tails (M % 32 != 0), the split-M partial-slab path, bf16 / fp32
+    outputs, overwrite and accumulate."""
+    torch.manual_seed(6)
+    dy = torch.randn(M, N, device=cuda).bfloat16()
+    x = torch.randn(M, J, device=cuda).bfloat16()
+    out = torch.randn(N, J, device=cuda).to(out_dt)
+    ref = dy.float().t() @ x.float() + (out.float() if acc else 0)
+    fused.gemm_tn(dy, x, out=out, accumulate=acc)
+    err = ((out.float() - ref).abs().max() / ref.abs().max()).item()
+    assert err < (1e-2 if out_dt == torch.bfloat16 else 1e-4), err
+
+
+@pytest.mark.parametrize("M,C", [(16384, 1024), (1000, 64), (40, 4096)])
+def test_colsum_bf16_partials(cuda, M, C):
+    """Bias-gradient column sums of a bf16 [M, C] matrix (edl_colsum_bf16_partial + edl_colsum)."""
+    from easydl_amd import _native
+    t = torch.randn(M, C, device=cuda).bfloat16()
+    part, G = fused._colsum_partial(t)
+    out = torch.empty(C, device=cuda)
+    _native.kernels().check("edl_colsum", part.data_ptr(), G, C, out.data_ptr(), 1, 0, _native.stream_of(t))
+    torch.testing.assert_close(out, t.float().sum(0), rtol=1e-4, atol=1e-3 * M ** 0.5)
+
+
+@pytest.mark.parametrize("tn", ["0", "1"])
+def test_linear_bias_wgrad_tn_and_nt_match_fp32(cuda, tn, monkeypatch):
+    """A biased linear layer's weight / bias gradients through the TN kernel (no transposes)
+    and through the NT form on transposed copies, flat buffers, two micro-batches."""
+    from easydl_amd.parallel.flat import FlatParams
+    monkeypatch.setattr(fused, "_WGRAD_TN", tn)
+    torch.manual_seed(7)
+    mod = torch.nn.ParameterList([torch.nn.Parameter((torch.randn(384, 512, device=cuda) * 0.05).bfloat16()),
+                                  torch.nn.Parameter((torch.randn(384, device=cuda) * 0.1).bfloat16())])
+    pr = [p.detach().float().requires_grad_(True) for p in mod]
+    FlatParams(mod)
+    fused.new_weight_generation()
+    for mb in range(2):
+        x = torch.randn(1024, 512, device=cuda).bfloat16().requires_grad_(True)
+        y = fused.linear(x, mod[0], mod[1])
+        dy = torch.randn_like(y)
+        y.backward(dy)
+        F.linear(x.detach().float(), pr[0], pr[1]).backward(dy.float())
+    for p, r in zip(mod, pr):
+        err = ((p.grad.float() - r.grad).abs().max() / (r.grad.abs().max() + 1e-6)).item()
+        assert err < 2e-2, (tuple(p.shape), err)

@@ -1,4 +1,5 @@
 """Model families on CPU: forward/backward shapes, flat-param training step, loss decreases."""
+import pytest
 import torch
 
 from easydl_amd.models.bert import BERT_TINY, BertMLM, SyntheticMLM
@@ -97,3 +98,24 @@ def test_flat_groups_split_under_the_byte_cap_and_train_identically():
     assert all(g.weight_decay == 0.1 for g in decay_parts)
     assert out[0][1] == out[64 << 10][1]
     assert torch.equal(out[0][2], out[64 << 10][2])
+
+
+def test_residual_grad_slot_accumulates_in_place():
+    """gradsink.input_grad_mm: with nothing parked it is dY @ W; with a parked residual
+    gradient r it returns r + dY @ W computed in place in r's storage (one GEMM, beta = 1);
+    an unarmed slot is never filled by the norm, and a slot refuses a second gradient."""
+    from easydl_amd.ops import gradsink
+    dy, w = torch.randn(6, 4), torch.randn(4, 5)
+    assert torch.allclose(gradsink.input_grad_mm(dy, w, None, (6, 5)), dy @ w)
+    s = gradsink.ResidualGrad()
+    assert not s.armed and s.take() is None
+    r = torch.randn(6, 5)
+    want = r + dy @ w
+    s.arm()
+    s.put(r)
+    with pytest.raises(RuntimeError):
+        s.put(r)
+    out = gradsink.input_grad_mm(dy, w, s, (2, 3, 5))
+    assert out.shape == (2, 3, 5) and out.data_ptr() == r.data_ptr()
+    assert torch.allclose(out.reshape(6, 5), want, atol=1e-5)
+    assert s.take() is None
