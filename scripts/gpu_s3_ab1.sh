@@ -4,7 +4,8 @@
 set -u
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 mkdir -p gpurun_out/ab1
-timeout -k 10 200 python -u -m pytest tests/test_kernels_gpu.py -k "bert_layer_residual or gelu_mlp" -x -q --timeout 120 --timeout-method thread > gpurun_out/ab1/pytest.log 2>&1 || { tail -30 gpurun_out/ab1/pytest.log; exit 1; }
+timeout -k 10 200 python -u -m pytest tests/test_kernels_gpu.py -k "bert_layer_residual or gelu_mlp" -x -q \
+  --timeout 120 --timeout-method thread > gpurun_out/ab1/pytest.log 2>&1 || { tail -30 gpurun_out/ab1/pytest.log; exit 1; }
 tail -1 gpurun_out/ab1/pytest.log
 for i in 1 2; do
   for rg in 0 1; do

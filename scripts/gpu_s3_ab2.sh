@@ -4,7 +4,8 @@
 set -u
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 mkdir -p gpurun_out/ab2
-timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py -k "tn or colsum or gelu or bert or swiglu" -x -q --timeout 120 --timeout-method thread > gpurun_out/ab2/pytest.log 2>&1 || { tail -40 gpurun_out/ab2/pytest.log; exit 1; }
+timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py -k "tn or colsum or gelu or bert or swiglu" -x -q \
+  --timeout 120 --timeout-method thread > gpurun_out/ab2/pytest.log 2>&1 || { tail -40 gpurun_out/ab2/pytest.log; exit 1; }
 tail -1 gpurun_out/ab2/pytest.log
 PYTHONPATH=$PWD timeout -k 10 300 python -u scripts/gemm_tn_bench.py > gpurun_out/ab2/gemm_tn_bench.jsonl 2>&1 || { tail -20 gpurun_out/ab2/gemm_tn_bench.jsonl; exit 1; }
 cat gpurun_out/ab2/gemm_tn_bench.jsonl
