@@ -453,13 +453,13 @@ def test_bert_layer_residual_grad_slots_match_fp32(cuda, flat, monkeypatch):
 
 
 @pytest.mark.parametrize("M,N,J", [(1000, 128, 256), (2048, 1024, 1024), (4096, 256, 512), (96, 384, 768),
-                                   (16384, 128, 256)])
+                                   (16384, 128, 256), (1000, 4096, 4096), (160, 8192, 2048)])
 @pytest.mark.parametrize("out_dt", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("acc", [False, True])
 def test_gemm_tn_matches_fp32(cuda, M, N, J, out_dt, acc):
     """edl_gemm_tn (dW = dY^T X from the row-major operands via transposing LDS reads) vs
-    fp32 torch: row tails (M % 32 != 0), the split-M partial-slab path, bf16 / fp32
-    outputs, overwrite and accumulate."""
+    fp32 torch: row tails (M % 32 != 0), the split-M partial-slab path, the 256 x 256 kernel
+    (>= 256 output tiles), bf16 / fp32 outputs, overwrite and accumulate."""
     torch.manual_seed(6)
     dy = torch.randn(M, N, device=cuda).bfloat16()
     x = torch.randn(M, J, device=cuda).bfloat16()
