@@ -219,11 +219,23 @@ __global__ __launch_bounds__(kThreads) void bn_apply_kernel(const bf16_t* __rest
 }
 
 // ---------------------------------------------------------------------------- backward
+// d += dz2, rounded to bf16 exactly as the separate bf16 add it replaces would store it
+__device__ __forceinline__ void add_rounded(float (&d)[8], const u32x4& v2) {
+  float e[8];
+  unpack8(v2, e);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) d[j] += e[j];
+  unpack8(pack8(d), d);
+}
+
 // dp = relu ? (z > 0 ? dz : 0) : dz;   partials of sum dp and sum dp * (x - mean)
 // MX: no residual was added, so the ReLU mask is recomputed from x with the forward's
 // own coefficients (z > 0  <=>  fma(x, sc, sh) > 0) instead of reading z back from HBM
-template <bool RELU, bool MX>
+// D2: the output's gradient arrives in two parts, dz + dz2 (a ResNet block output's
+// identity-path gradient, parked by the next block instead of summed by an add kernel)
+template <bool RELU, bool MX, bool D2 = false>
 __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(const bf16_t* __restrict__ dz,
+                                                                 const bf16_t* __restrict__ dz2,
                                                                  const bf16_t* __restrict__ z,
                                                                  const bf16_t* __restrict__ x,
                                                                  const float* __restrict__ mean,
@@ -247,6 +259,7 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(const bf16_t* _
       unpack8(*reinterpret_cast<const u32x4*>(dz + o), d);
       unpack8(*reinterpret_cast<const u32x4*>(x + o), f);
       if (RELU && !MX) unpack8(*reinterpret_cast<const u32x4*>(z + o), y);
+      if (D2) add_rounded(d, *reinterpret_cast<const u32x4*>(dz2 + o));
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         if (MX) y[j] = __builtin_fmaf(f[j], sc[j], sh[j]);
@@ -284,8 +297,9 @@ __global__ __launch_bounds__(kFinThreads) void bn_bwd_finalize_kernel(const floa
   coef[2 * C + c] = (float)(K1 * (double)mean[c] - A * gb / (double)M);
 }
 
-template <bool RELU, bool DRES, bool MX>
+template <bool RELU, bool DRES, bool MX, bool D2 = false>
 __global__ __launch_bounds__(kThreads) void bn_bwd_dx_kernel(const bf16_t* __restrict__ dz,
+                                                             const bf16_t* __restrict__ dz2,
                                                              const bf16_t* __restrict__ z,
                                                              const bf16_t* __restrict__ x,
                                                              const float* __restrict__ coef,
@@ -310,6 +324,7 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_dx_kernel(const bf16_t* __res
     unpack8(*reinterpret_cast<const u32x4*>(dz + o), d);
     unpack8(*reinterpret_cast<const u32x4*>(x + o), f);
     if (RELU && !MX) unpack8(*reinterpret_cast<const u32x4*>(z + o), y);
+    if (D2) add_rounded(d, *reinterpret_cast<const u32x4*>(dz2 + o));
     float gx[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -406,35 +421,41 @@ int edl_bn_apply(const void* x, const void* res, void* z, const float* coef, int
 // coef: fp32 [3C] scratch; part as in the forward.
 // fcoef: the forward's (scale, shift) coefficients [2C]; with relu and z == nullptr the
 // ReLU mask is recomputed from x (forward without a residual), saving a read of z per pass
-int edl_bn_bwd(const void* dz, const void* z, const void* x, const float* w, const float* mean, const float* rstd,
-               const float* fcoef, void* dx, void* dres, float* dw, float* db, float* coef, float* part, int64_t M,
-               int C, int relu, int acc, hipStream_t s) {
+// dz2 (may be null): a second part of the output gradient, added in both passes (only with
+// relu and z given: the block-output BatchNorm of a ResNet bottleneck)
+int edl_bn_bwd(const void* dz, const void* dz2, const void* z, const void* x, const float* w, const float* mean,
+               const float* rstd, const float* fcoef, void* dx, void* dres, float* dw, float* db, float* coef,
+               float* part, int64_t M, int C, int relu, int acc, hipStream_t s) {
   if (!shape_ok(M, C) || (relu && z == nullptr && fcoef == nullptr)) return (int)hipErrorInvalidValue;
+  if (dz2 && !(relu && z)) return (int)hipErrorInvalidValue;
   const bool mx = relu && z == nullptr;
   const int G = row_blocks(M, C), Cb = chunk_of(C);
   const dim3 grid(G, C / Cb);
+  const bf16_t *bdz = (const bf16_t*)dz, *bdz2 = (const bf16_t*)dz2, *bz = (const bf16_t*)z, *bx = (const bf16_t*)x;
   if (mx)
-    bn_bwd_reduce_kernel<true, true><<<grid, kThreads, 0, s>>>((const bf16_t*)dz, nullptr, (const bf16_t*)x, mean,
-                                                               fcoef, M, C, Cb, part);
+    bn_bwd_reduce_kernel<true, true><<<grid, kThreads, 0, s>>>(bdz, nullptr, nullptr, bx, mean, fcoef, M, C, Cb, part);
+  else if (relu && dz2)
+    bn_bwd_reduce_kernel<true, false, true><<<grid, kThreads, 0, s>>>(bdz, bdz2, bz, bx, mean, nullptr, M, C, Cb, part);
   else if (relu)
-    bn_bwd_reduce_kernel<true, false><<<grid, kThreads, 0, s>>>((const bf16_t*)dz, (const bf16_t*)z,
-                                                                (const bf16_t*)x, mean, nullptr, M, C, Cb, part);
+    bn_bwd_reduce_kernel<true, false><<<grid, kThreads, 0, s>>>(bdz, nullptr, bz, bx, mean, nullptr, M, C, Cb, part);
   else
-    bn_bwd_reduce_kernel<false, false><<<grid, kThreads, 0, s>>>((const bf16_t*)dz, nullptr, (const bf16_t*)x, mean,
-                                                                 nullptr, M, C, Cb, part);
+    bn_bwd_reduce_kernel<false, false><<<grid, kThreads, 0, s>>>(bdz, nullptr, nullptr, bx, mean, nullptr, M, C, Cb,
+                                                                 part);
   EDL_LAUNCH_CHECK();
   bn_bwd_finalize_kernel<<<(C + 63) / 64, kFinThreads, 0, s>>>(part, G, C, M, w, mean, rstd, dw, db, coef, acc);
   EDL_LAUNCH_CHECK();
   const int GA = blocks_for(M, C, 4, 2048);
-#define EDL_BN_DX(L, D, X)                                                                                    \
-  bn_bwd_dx_kernel<L, D, X><<<GA, kThreads, 0, s>>>((const bf16_t*)dz, (const bf16_t*)z, (const bf16_t*)x, coef, \
-                                                    fcoef, M, C, (bf16_t*)dx, (bf16_t*)dres)
-  if (dres) {
-    if (mx) EDL_BN_DX(true, true, true); else if (relu) EDL_BN_DX(true, true, false);
-    else EDL_BN_DX(false, true, false);
+#define EDL_BN_DX(L, D, X, D2)                                                                    \
+  bn_bwd_dx_kernel<L, D, X, D2><<<GA, kThreads, 0, s>>>(bdz, bdz2, bz, bx, coef, fcoef, M, C, (bf16_t*)dx, \
+                                                        (bf16_t*)dres)
+  if (dz2) {
+    if (dres) EDL_BN_DX(true, true, false, true); else EDL_BN_DX(true, false, false, true);
+  } else if (dres) {
+    if (mx) EDL_BN_DX(true, true, true, false); else if (relu) EDL_BN_DX(true, true, false, false);
+    else EDL_BN_DX(false, true, false, false);
   } else {
-    if (mx) EDL_BN_DX(true, false, true); else if (relu) EDL_BN_DX(true, false, false);
-    else EDL_BN_DX(false, false, false);
+    if (mx) EDL_BN_DX(true, false, true, false); else if (relu) EDL_BN_DX(true, false, false, false);
+    else EDL_BN_DX(false, false, false, false);
   }
 #undef EDL_BN_DX
   EDL_LAUNCH_CHECK();

@@ -110,7 +110,7 @@ _KERNEL_SIGS = {
     "edl_bn_groups": (c_int, [c_i64, c_int]),
     "edl_bn_fwd_train": [c_void_p] * 11 + [c_i64, c_int, c_float, c_float, c_int, c_void_p, c_void_p],
     "edl_bn_apply": [c_void_p] * 4 + [c_i64, c_int, c_int, c_void_p],
-    "edl_bn_bwd": [c_void_p] * 13 + [c_i64, c_int, c_int, c_int, c_void_p],
+    "edl_bn_bwd": [c_void_p] * 14 + [c_i64, c_int, c_int, c_int, c_void_p],
 }
 
 

@@ -49,6 +49,9 @@ def _nhwc(t):
 # buffer; EDL_BN_MASK_FROM_X=0 keeps z and reads it back for the ReLU mask.
 _DIRECT_GRADS = os.environ.get("EDL_BN_DIRECT_GRADS", "1") != "0"
 _MASK_FROM_X = os.environ.get("EDL_BN_MASK_FROM_X", "1") != "0"
+# EDL_BN_RES_HANDOFF=0: autograd sums a block output's two gradients (conv1's input gradient and
+# the next block's identity path) with an add kernel instead of the BatchNorm backward reading both
+_RES_HANDOFF = os.environ.get("EDL_BN_RES_HANDOFF", "1") != "0"
 
 
 class _BNActFn(torch.autograd.Function):
@@ -63,6 +66,10 @@ class _BNActFn(torch.autograd.Function):
         if x.dtype != torch.bfloat16 or w.dtype != torch.float32:
             raise TypeError("batchnorm kernel expects bf16 activations and fp32 weight / statistics")
         r2 = None
+        # identity-path hand-off: a residual produced by a block-output BatchNorm (one with
+        # relu and a residual of its own) takes this op's residual gradient in its backward
+        # kernels (dz + dz2) -- no autograd add of the two gradients of the block output
+        ctx.res_slot = getattr(res, "_edl_grad_slot", None) if (res is not None and _RES_HANDOFF) else None
         if res is not None:
             res, r2 = _nhwc(res)
         z = torch.empty_like(x)
@@ -81,6 +88,9 @@ class _BNActFn(torch.autograd.Function):
                               coef if mx else None)
         ctx.relu, ctx.has_res = relu, res is not None
         ctx.bn_b = b
+        ctx.out_slot = None
+        if relu and res is not None and not mx and _RES_HANDOFF:
+            ctx.out_slot = z._edl_grad_slot = gradsink.ResidualGrad()
         return z
 
     @staticmethod
@@ -108,9 +118,14 @@ class _BNActFn(torch.autograd.Function):
             acc = 0
         coef = torch.empty(3 * C, dtype=torch.float32, device=dev)
         part = torch.empty(2 * C * G, dtype=torch.float32, device=dev)
-        k.check("edl_bn_bwd", dz2.data_ptr(), _native.ptr(z), x.data_ptr(), w.data_ptr(), mean.data_ptr(),
-                rstd.data_ptr(), _native.ptr(fcoef), dx.data_ptr(), _native.ptr(dres), dw.data_ptr(), db.data_ptr(),
-                coef.data_ptr(), part.data_ptr(), M, C, int(ctx.relu), acc, _native.stream_of(x))
+        extra = ctx.out_slot.take() if ctx.out_slot is not None else None   # the next block's identity grad
+        e2 = _nhwc(extra)[1] if extra is not None else None
+        k.check("edl_bn_bwd", dz2.data_ptr(), _native.ptr(e2), _native.ptr(z), x.data_ptr(), w.data_ptr(),
+                mean.data_ptr(), rstd.data_ptr(), _native.ptr(fcoef), dx.data_ptr(), _native.ptr(dres), dw.data_ptr(),
+                db.data_ptr(), coef.data_ptr(), part.data_ptr(), M, C, int(ctx.relu), acc, _native.stream_of(x))
+        if dres is not None and ctx.res_slot is not None:
+            ctx.res_slot.put(dres)   # summed by the residual's producer (above), not by autograd
+            dres = None
         if direct:
             gradsink.commit(w)
             gradsink.commit(b)

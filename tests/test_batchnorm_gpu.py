@@ -113,3 +113,49 @@ def test_bn_param_grads_go_straight_into_flat_buffer(cuda):
     assert len(fired) == 4
     for pa, pb in ((bn_a.weight, bn_b.weight), (bn_a.bias, bn_b.bias)):
         assert _rel(pb.grad, pa.grad) < 1e-5
+
+
+def _two_blocks(a, r, bns, scale):
+    """Block output z1 = relu(bn1(a) + r); next block: y = relu(bn2(scale * z1));
+    z2 = relu(bn3(y) + z1) (identity residual).  z1's gradient has two parts: through
+    bn2's input and through bn3's residual."""
+    z1 = bn_act(a, bns[0], residual=r)
+    y = bn_act(z1 * scale, bns[1])
+    return bn_act(y, bns[2], residual=z1)
+
+
+def test_block_output_gradient_handoff_matches_add_and_fp32(cuda, monkeypatch):
+    """The identity-path gradient of a block output parked by the next block's BatchNorm
+    and added inside the producing BatchNorm's backward kernels (dz + dz2, rounded like the
+    bf16 add it replaces) gives bitwise the gradients of autograd's add, the hand-off
+    really ran (one parked gradient), and both match the fp32 reference."""
+    from easydl_amd.ops import batchnorm as bnmod
+    torch.manual_seed(8)
+    N, C, H, W = 4, 64, 14, 14
+    mk = lambda: torch.randn(N, C, H, W, device=cuda).bfloat16().to(memory_format=torch.channels_last)
+    a0, r0, g = mk(), mk(), mk()
+    puts = []
+    orig_put = bnmod.gradsink.ResidualGrad.put
+
+    def put(self, t):
+        puts.append(t.shape)
+        return orig_put(self, t)
+    monkeypatch.setattr(bnmod.gradsink.ResidualGrad, "put", put)
+    grads = {}
+    for handoff in (True, False):
+        monkeypatch.setattr(bnmod, "_RES_HANDOFF", handoff)
+        a, r = a0.clone().requires_grad_(True), r0.clone().requires_grad_(True)
+        bns = [_bn(C, s) for s in (1, 2, 3)]
+        _two_blocks(a, r, bns, 0.5).backward(g)
+        grads[handoff] = [a.grad, r.grad] + [p.grad for b in bns for p in (b.weight, b.bias)]
+    assert len(puts) == 1
+    for x, y in zip(grads[True], grads[False]):
+        assert torch.equal(x, y)
+    ref_bns = [copy.deepcopy(_bn(C, s)).cpu() for s in (1, 2, 3)]
+    ar, rr = (t.float().cpu().requires_grad_(True) for t in (a0, r0))
+    z1r = bn_act_ref(ar, ref_bns[0], residual=rr)
+    z2r = bn_act_ref(bn_act_ref(z1r * 0.5, ref_bns[1]), ref_bns[2], residual=z1r)
+    z2r.backward(g.float().cpu())
+    want = [ar.grad, rr.grad] + [p.grad for b in ref_bns for p in (b.weight, b.bias)]
+    for x, y in zip(grads[True], want):
+        assert _rel_l2(x.cpu(), y) < 5e-2
