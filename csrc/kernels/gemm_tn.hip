@@ -421,9 +421,13 @@ extern "C" {
 // work ids for ~one workgroup per CU, each split at least 1024 rows deep.
 int edl_gemm_tn_splits(int M, int N, int J) {
   if (N <= 0 || J <= 0 || N % BN || J % BJ) return 0;
+  static const int target = [] {   // work ids to aim for (EDL_GEMM_TN_WGS, default two per CU)
+    const char* e = getenv("EDL_GEMM_TN_WGS");
+    return e && atoi(e) > 0 ? atoi(e) : 2 * kCUs;
+  }();
   const int T = (N / BN) * (J / BJ);
   int s = 1;
-  while (T * s * 2 <= kCUs && M / (2 * s) >= 1024 && s < 16) s *= 2;
+  while (T * s * 2 <= target && M / (2 * s) >= 1024 && s < 16) s *= 2;
   return s;
 }
 
