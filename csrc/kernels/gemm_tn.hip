@@ -204,35 +204,37 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const bf16_t* __restric
 
 // ---------------------------------------------------------------------------
 // 256 x 256 tiles for weights big enough to fill the chip without splitting M (the
-// Llama-3-8B projections: 384-1792 tiles).  One workgroup per CU, wave (wn, wj) owns
-// 128 x 128 = 4 x 4 blocks (256 accumulators, in AGPRs), so a k-step of 16 reads 4 A +
-// 4 B fragments for 16 MFMAs -- half the LDS and L2 traffic per FLOP of the 128 x 256
-// kernel above.  Four 32 KiB LDS stages: the DMA of stage it+2 is issued at the top of
-// stage it into the buffer stage it-2 used (every wave finished it before the previous
-// barrier), and the transposed reads run one k-step ahead of the MFMAs across the
-// barrier: k-step 1's reads are issued before k-step 0's MFMAs, and the next stage's
-// k-step 0 reads right after the barrier that publishes it, before k-step 1's MFMAs.
+// Llama-3-8B projections: 384-1792 tiles).  One workgroup of 8 waves per CU, two per
+// SIMD: wave (wn, wj) owns 128 (n) x 64 (j) = 4 x 2 blocks (128 accumulators), a k-step
+// of 16 reads 4 A + 2 B fragments for 8 MFMAs.  A 4-wave form (128 x 128 per wave, one
+// wave per SIMD) ran at 42 % MFMA busy, issue-bound on its LDS-DMA pieces and waits with
+// nothing to hide them (PMC, profiles/r03_gemm_tn_ab.md); with two waves per SIMD one
+// wave's DMA issue and waits run under the other's MFMAs (gate/up 3.85 -> 3.35 ms).
+// Four 32 KiB LDS stages: the DMA of stage it+2 is issued at the top of stage it into
+// the buffer stage it-2 used (every wave finished it before the previous barrier), and
+// the transposed reads run one k-step ahead of the MFMAs across the barrier: k-step 1's
+// reads are issued before k-step 0's MFMAs, and the next stage's k-step 0 reads right
+// after the barrier that publishes it, before k-step 1's MFMAs.
 // Tiles are visited in groups of 8 n-rows (j within the group, then the next group),
 // each XCD taking a contiguous range: the ~32 workgroups an XCD runs at once share
 // 8 A column blocks and 4 B column blocks in its L2.
 // ---------------------------------------------------------------------------
 constexpr int B2 = 256, STAGE2 = 4 * TILE, NB2 = 4;
 
-template <int N8>
-__device__ __forceinline__ void lgkm_wait8(bf16x8 (&f)[8]) {
-  asm volatile("s_waitcnt lgkmcnt(%8)"
-               : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]), "+v"(f[4]), "+v"(f[5]), "+v"(f[6]), "+v"(f[7])
-               : "i"(N8));
+template <int N6>
+__device__ __forceinline__ void lgkm_wait6(bf16x8 (&f)[6]) {
+  asm volatile("s_waitcnt lgkmcnt(%6)" : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]), "+v"(f[4]), "+v"(f[5])
+               : "i"(N6));
 }
 
 template <int OUT>   // 0 = bf16 C, 1 = fp32 C
-__global__ __launch_bounds__(256, 1) void gemm_tn256_kernel(const bf16_t* __restrict__ A,
+__global__ __launch_bounds__(512, 1) void gemm_tn256_kernel(const bf16_t* __restrict__ A,
                                                             const bf16_t* __restrict__ B, void* __restrict__ C,
                                                             int M, int N, int J, int accumulate) {
   __shared__ __attribute__((aligned(16))) char smem[NB2 * STAGE2];
   const int lane = threadIdx.x & 63, h = lane >> 5, l31 = lane & 31;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wn = w >> 1, wj = w & 1;
+  const int wn = w >> 2, wj = w & 3;
   const int tnn = N / B2, tjn = J / B2, T = tnn * tjn;
   int t = blockIdx.x;
   {   // contiguous range per XCD (bijective for any T: the first T % 8 XCDs get one more)
@@ -243,8 +245,8 @@ __global__ __launch_bounds__(256, 1) void gemm_tn256_kernel(const bf16_t* __rest
   const int g = t / (GROUP * tjn), rows_g = min(GROUP, tnn - g * GROUP), within = t - g * GROUP * tjn;
   const int n0 = (g * GROUP + within % rows_g) * B2, j0 = (within / rows_g) * B2;
   const int nk = (M + KS - 1) / KS;
-  const DmaPlan<KS, 4> pa(N, w, lane), pb(J, w, lane);
-  uint32_t alo[4], ahi[4], blo[4], bhi[4];   // this lane's fragment addresses, stage 0, k-step 0
+  const DmaPlan<KS, 8> pa(N, w, lane), pb(J, w, lane);
+  uint32_t alo[4], ahi[4], blo[2], bhi[2];   // this lane's fragment addresses, stage 0, k-step 0
   {
     const uint32_t base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
     const int i = lane & 15, qq = i >> 2, p = i & 3;
@@ -256,8 +258,11 @@ __global__ __launch_bounds__(256, 1) void gemm_tn256_kernel(const bf16_t* __rest
     for (int q = 0; q < 4; ++q) {
       alo[q] = addr(4 * h + qq, q) + wn * TILE;
       ahi[q] = addr(4 * h + 8 + qq, q) + wn * TILE;
-      blo[q] = addr(4 * h + qq, q) + (2 + wj) * TILE;
-      bhi[q] = addr(4 * h + 8 + qq, q) + (2 + wj) * TILE;
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      blo[q] = addr(4 * h + qq, (wj & 1) * 2 + q) + (2 + (wj >> 1)) * TILE;
+      bhi[q] = addr(4 * h + 8 + qq, (wj & 1) * 2 + q) + (2 + (wj >> 1)) * TILE;
     }
   }
   auto dma = [&](int it, int buf) {
@@ -271,35 +276,35 @@ __global__ __launch_bounds__(256, 1) void gemm_tn256_kernel(const bf16_t* __rest
     pb.issue(st + 2 * TILE, make_rsrc(bp, rows * (uint32_t)J * 2), w);
     pb.issue(st + 3 * TILE, make_rsrc(bp + 128, rows * (uint32_t)J * 2 - 256), w);
   };
-  // the 8 fragments of k-step KSTEP of the stage in buffer `buf`: A blocks 0..3, B blocks 0..3
-  auto reads = [&](bf16x8 (&f)[8], int buf, auto kstep) {
+  // the 6 fragments of k-step KSTEP of the stage in buffer `buf`: A blocks 0..3, B blocks 0..1
+  auto reads = [&](bf16x8 (&f)[6], int buf, auto kstep) {
     constexpr int KO = decltype(kstep)::value * 16 * 256;
     const uint32_t bo = (uint32_t)buf * STAGE2;
 #pragma unroll
     for (int q = 0; q < 4; ++q) f[q] = frag_tr<KO>(alo[q] + bo, ahi[q] + bo);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) f[4 + q] = frag_tr<KO>(blo[q] + bo, bhi[q] + bo);
+    for (int q = 0; q < 2; ++q) f[4 + q] = frag_tr<KO>(blo[q] + bo, bhi[q] + bo);
   };
-  f32x16 acc[4][4];
+  f32x16 acc[4][2];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
 #pragma unroll
-    for (int jj = 0; jj < 4; ++jj) acc[i][jj] = f32x16{};
+    for (int jj = 0; jj < 2; ++jj) acc[i][jj] = f32x16{};
   }
-  auto mmas = [&](const bf16x8 (&f)[8]) {
+  auto mmas = [&](const bf16x8 (&f)[6]) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
 #pragma unroll
-      for (int jj = 0; jj < 4; ++jj) acc[i][jj] = mfma(f[i], f[4 + jj], acc[i][jj]);
+      for (int jj = 0; jj < 2; ++jj) acc[i][jj] = mfma(f[i], f[4 + jj], acc[i][jj]);
     }
   };
   using K0 = std::integral_constant<int, 0>;
   using K1 = std::integral_constant<int, 1>;
-  bf16x8 cur[8], nxt[8];
+  bf16x8 cur[6], nxt[6];
   if (nk > 0) dma(0, 0);
   if (nk > 1) dma(1, 1);
   if (nk > 1)
-    __builtin_amdgcn_s_waitcnt(0x0078);   // vmcnt(8): stage 0 landed (stage 1 may fly)
+    __builtin_amdgcn_s_waitcnt(0x0074);   // vmcnt(4): stage 0 landed (stage 1 may fly)
   else
     __builtin_amdgcn_s_waitcnt(0x0070);
   __builtin_amdgcn_s_barrier();
@@ -308,21 +313,21 @@ __global__ __launch_bounds__(256, 1) void gemm_tn256_kernel(const bf16_t* __rest
   for (int it = 0; it < nk; ++it) {
     const int buf = it & 3;
     if (it + 2 < nk) dma(it + 2, (it + 2) & 3);
-    lgkm_wait8<0>(cur);                    // k-step 0 of stage it
+    lgkm_wait6<0>(cur);                    // k-step 0 of stage it
     reads(nxt, buf, K1{});                 // k-step 1 reads fly under k-step 0's MFMAs
     __builtin_amdgcn_sched_barrier(0);
     mmas(cur);
     __builtin_amdgcn_sched_barrier(0);
     if (it + 1 < nk) {
       if (it + 2 < nk)
-        __builtin_amdgcn_s_waitcnt(0x0078);   // vmcnt(8): stage it+1 landed (it+2 may fly)
+        __builtin_amdgcn_s_waitcnt(0x0074);   // vmcnt(4): stage it+1 landed (it+2 may fly)
       else
         __builtin_amdgcn_s_waitcnt(0x0070);
       __builtin_amdgcn_s_barrier();           // ... in every wave: stage it+1 is readable
       reads(cur, (it + 1) & 3, K0{});         // next stage's k-step 0 under k-step 1's MFMAs
-      lgkm_wait8<15>(nxt);   // lgkmcnt holds 15 at most: + one of the next stage's reads
+      lgkm_wait6<12>(nxt);
     } else {
-      lgkm_wait8<0>(nxt);
+      lgkm_wait6<0>(nxt);
     }
     __builtin_amdgcn_sched_barrier(0);
     mmas(nxt);
@@ -331,8 +336,8 @@ __global__ __launch_bounds__(256, 1) void gemm_tn256_kernel(const bf16_t* __rest
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
 #pragma unroll
-    for (int jj = 0; jj < 4; ++jj) {
-      const int j = j0 + wj * 128 + jj * 32 + l31;
+    for (int jj = 0; jj < 2; ++jj) {
+      const int j = j0 + wj * 64 + jj * 32 + l31;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int n = n0 + wn * 128 + i * 32 + acc_row(r, h);
@@ -457,9 +462,9 @@ int edl_gemm_tn(const void* A, const void* B, void* C, int M, int N, int J, int 
     if ((int64_t)32 * N * 2 >= (1ll << 32) || (int64_t)32 * J * 2 >= (1ll << 32)) return (int)hipErrorInvalidValue;
     const dim3 grid((N / B2) * (J / B2));
     if (out_fp32)
-      gemm_tn256_kernel<1><<<grid, 256, 0, s>>>((const bf16_t*)A, (const bf16_t*)B, C, M, N, J, accumulate);
+      gemm_tn256_kernel<1><<<grid, 512, 0, s>>>((const bf16_t*)A, (const bf16_t*)B, C, M, N, J, accumulate);
     else
-      gemm_tn256_kernel<0><<<grid, 256, 0, s>>>((const bf16_t*)A, (const bf16_t*)B, C, M, N, J, accumulate);
+      gemm_tn256_kernel<0><<<grid, 512, 0, s>>>((const bf16_t*)A, (const bf16_t*)B, C, M, N, J, accumulate);
     EDL_LAUNCH_CHECK();
     return 0;
   }

@@ -298,11 +298,17 @@ def _nt_wgrad_ok(dy2: torch.Tensor, x2: torch.Tensor) -> bool:
 # eligible weight; 0: never (NT form on transposed copies).
 _WGRAD_TN = os.environ.get("EDL_WGRAD_TN", "auto")
 _WGRAD_TN_MAX = int(os.environ.get("EDL_WGRAD_TN_MAX_ELEMS", 8 << 20))
+# EDL_WGRAD_TN_WIDE_J > 0: also weights whose input is at least that wide (the NT form would
+# transpose a wide X).  Off by default: for Llama-3-8B's down projection (J = 14336) the TN
+# kernel wins in isolation (1.73 ms vs NT 1.67 + 0.23 ms of transposes) but the step ran
+# 2,874 vs 2,791 ms with it (profiles/r03_gemm_tn_ab.md).
+_WGRAD_TN_WIDE = int(os.environ.get("EDL_WGRAD_TN_WIDE_J", 0))
 
 
 def _tn_dims(t: torch.Tensor, N: int, J: int) -> bool:
     """The TN kernel takes dW [N, J] for activations like ``t`` (bf16 on the GPU)."""
-    if _WGRAD_TN == "0" or (_WGRAD_TN == "auto" and N * J > _WGRAD_TN_MAX):
+    wide = 0 < _WGRAD_TN_WIDE <= J
+    if _WGRAD_TN == "0" or (_WGRAD_TN == "auto" and N * J > _WGRAD_TN_MAX and not wide):
         return False
     return t.is_cuda and t.dtype == torch.bfloat16 and N % 128 == 0 and J % 256 == 0
 
@@ -548,18 +554,20 @@ class _SwiGLUMLPFn(torch.autograd.Function):
         gu = F.linear(x2, w_gu)
         M, F2 = gu.shape
         Fh = F2 // 2
-        # TN weight gradients need h itself; the NT form needs only h^T (saved instead of h)
-        ctx.tn = _tn_dims(x2, w_down.shape[0], Fh) and _tn_dims(x2, F2, x2.shape[1])
+        # TN weight gradients need h itself; the NT form needs only h^T (saved instead of h).
+        # The two GEMMs choose their forms separately (tn_down, tn_gu).
+        ctx.tn_down = _tn_dims(x2, w_down.shape[0], Fh)
+        ctx.tn_gu = _tn_dims(x2, F2, x2.shape[1])
         h = torch.empty(M, Fh, dtype=gu.dtype, device=gu.device)
         st = _native.stream_of(gu)
-        if ctx.tn:
+        if ctx.tn_down:
             hT = None
             k.check("edl_swiglu_fwd", gu.data_ptr(), h.data_ptr(), M, Fh, st)
         else:
             hT = torch.empty(Fh, M, dtype=gu.dtype, device=gu.device)
             k.check("edl_swiglu_fwd_t", gu.data_ptr(), h.data_ptr(), hT.data_ptr(), M, Fh, st)
         y = _chunked_reduced_mm(h, w_down, out_reduce) if out_reduce is not None else F.linear(h, w_down)
-        if not ctx.tn:
+        if not ctx.tn_down:
             del h
             h = hT
         wt_gu = _wt_of(w_gu) if ctx.needs_input_grad[0] else None
@@ -576,10 +584,10 @@ class _SwiGLUMLPFn(torch.autograd.Function):
         M, F2 = gu.shape
         Fh = F2 // 2
         st = _native.stream_of(gu)
-        tn = ctx.tn
+        tn = ctx.tn_gu
 
         def down_wgrad():
-            if tn:
+            if ctx.tn_down:
                 return _deliver_wgrad(w_down, dy2, hs, tn=True)
             return _deliver_wgrad(w_down, _transposed(dy2), hs.t())
 

@@ -502,3 +502,31 @@ def test_linear_bias_wgrad_tn_and_nt_match_fp32(cuda, tn, monkeypatch):
     for p, r in zip(mod, pr):
         err = ((p.grad.float() - r.grad).abs().max() / (r.grad.abs().max() + 1e-6)).item()
         assert err < 2e-2, (tuple(p.shape), err)
+
+
+def test_swiglu_mlp_mixed_weight_gradient_forms_match_fp32(cuda, monkeypatch):
+    """SwiGLU MLP whose two weight gradients take different forms under the auto policy with
+    EDL_WGRAD_TN_WIDE_J = 8192: the down projection (input width 8448) on the TN kernel from h,
+    the big gate/up one as hipBLASLt NT on d(gate_up)^T; output, input and weight gradients vs fp32."""
+    from easydl_amd.parallel.flat import FlatParams
+    monkeypatch.setattr(fused, "_WGRAD_TN_WIDE", 8192)
+    torch.manual_seed(10)
+    M, D, Fh = 256, 512, 8448
+    assert fused._tn_dims(torch.empty(1, device=cuda, dtype=torch.bfloat16), D, Fh)          # down: TN
+    assert not fused._tn_dims(torch.empty(1, device=cuda, dtype=torch.bfloat16), 2 * Fh, D)  # gate/up: NT
+    mod = torch.nn.ParameterList([torch.nn.Parameter((torch.randn(2 * Fh, D, device=cuda) * 0.03).bfloat16()),
+                                  torch.nn.Parameter((torch.randn(D, Fh, device=cuda) * 0.02).bfloat16())])
+    pr = [p.detach().float().requires_grad_(True) for p in mod]
+    FlatParams(mod)
+    fused.new_weight_generation()
+    x = torch.randn(M, D, device=cuda).bfloat16().requires_grad_(True)
+    y = fused.swiglu_mlp(x, mod[0], mod[1])
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    xr = x.detach().float().requires_grad_(True)
+    g, u = (xr @ pr[0].t()).chunk(2, dim=-1)
+    yr = (F.silu(g) * u) @ pr[1].t()
+    yr.backward(dy.float())
+    for a, b in ((y, yr), (x.grad, xr.grad), (mod[0].grad, pr[0].grad), (mod[1].grad, pr[1].grad)):
+        err = ((a.float() - b).abs().max() / (b.abs().max() + 1e-6)).item()
+        assert err < 3e-2, err
