@@ -10,6 +10,6 @@ for i in 1 2; do
   for wj in 1000000 8192; do
     EDL_WGRAD_TN_WIDE_J=$wj timeout -k 10 300 python3 bench.py --steps 6 --warmup 2 > gpurun_out/tnwide/l$wj.log 2>&1 \
       || { tail -20 gpurun_out/tnwide/l$wj.log; exit 1; }
-    echo "llama EDL_WGRAD_TN_WIDE_J=$wj $(grep -h '"metric"' gpurun_out/tnwide/l$wj.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"], d["peak_mem_gb"])')"
+    echo "llama EDL_WGRAD_TN_WIDE_J=$wj $(grep -h '"metric"' gpurun_out/tnwide/l$wj.log | cut -c150-230)"
   done
 done
