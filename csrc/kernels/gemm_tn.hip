@@ -13,7 +13,7 @@
 // MFMAs need anyway.  No transposed copies are ever written.
 //
 // Tiling: a workgroup (4 waves) owns a 128 (n) x 256 (j) block of C; wave (wn, wj)
-// owns 64 x 128 = 2 x 4 blocks of 32 x 32 (8 accumulators, 128 AGPRs), so each k-step
+// owns 64 x 128 = 2 x 4 blocks of 32 x 32 (8 accumulators, 128 registers), so each k-step
 // of 16 reads 2 A + 4 B fragments for 8 MFMAs.  32-row k-stages, three LDS stages
 // (72 KiB) filled two stages ahead, one barrier per stage; two workgroups per CU.
 // Weight gradients of small layers have few C tiles against a deep M (BERT-large:
@@ -82,9 +82,12 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const bf16_t* __restric
   const int m_begin = s * mchunk, m_end = min(M, m_begin + mchunk);
   const int nk = (m_end - m_begin + KS - 1) / KS;
   const DmaPlan<KS, 4> pa(N, w, lane), pb(J, w, lane);
-  // loop-invariant LDS byte addresses of this lane's transposed fragment reads (tr_read of
-  // mfma_tile.h, k-step 0 of stage 0; stage and k-step offsets go in the immediate): rows
-  // 4h + qq and 4h + 8 + qq, 16-B chunk of column block dt.  wj's B half is folded in here.
+  // loop-invariant LDS byte addresses of this lane's transposed fragment reads (k-step 0 of
+  // stage 0; stage and k-step offsets go in the immediate).  The MFMA operand with rows =
+  // tile columns 32*dt .. 32*dt+31 (lane & 31) and k = tile rows kb.. comes from two
+  // ds_read_b64_tr_b16 at rows kb + qq and kb + 8 + qq (qq = (lane & 15) >> 2, kb = 4h),
+  // element j <-> k row kb + 8*(j>>2) + (j&3): two operands read with the same kb pair the
+  // same k in every element, so their MFMA sums over 16 tile rows.  wj's B half is folded in.
   uint32_t alo[2], ahi[2], blo[4], bhi[4];
   {
     const uint32_t base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;

@@ -12,7 +12,6 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef short i16x4 __attribute__((ext_vector_type(4)));
 typedef short i16x8 __attribute__((ext_vector_type(8)));
-typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
 typedef __attribute__((address_space(3))) void lds_void;
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
 
@@ -22,21 +21,6 @@ __device__ __forceinline__ int swz_x(int r) { return ((r & 3) << 2) | ((r >> 2) 
 
 __device__ __forceinline__ f32x16 mfma(const bf16x8& a, const bf16x8& b, const f32x16& c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
-}
-
-// MFMA operand of a row-major [k][128] tile read TRANSPOSED: rows = columns 32*dt ..
-// 32*dt+31 of the tile (lane & 31), k = tile rows kb.. in the permuted order
-// element j <-> row kb + 8*(j>>2) + (j&3); pass kb = k0 + 4*(lane>>5).  Two operands
-// read this way with the same kb pair the same k in every element, so their MFMA
-// sums over rows k0 .. k0+15 of both tiles.
-__device__ __forceinline__ bf16x8 tr_read(const char* tile, int kb, int dt, int lane) {
-  const int i = lane & 15, qq = i >> 2, p = i & 3;
-  const int col = dt * 32 + ((lane >> 4) & 1) * 16 + 4 * p;
-  const int c = col >> 3, half = (col >> 2) & 1;
-  const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(tile + swz(kb + qq, c) + half * 8));
-  const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(tile + swz(kb + 8 + qq, c) + half * 8));
-  const i16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-  return __builtin_bit_cast(bf16x8, v);
 }
 
 // row (within a 32-row block) of accumulator register i for lane half h
