@@ -147,7 +147,8 @@ __global__ __launch_bounds__(256) void rope_qkv_kernel(const bf16_t* __restrict_
 __global__ __launch_bounds__(256) void xent_fwd_bwd_kernel(bf16_t* __restrict__ logits,
                                                            const int64_t* __restrict__ labels,
                                                            float* __restrict__ loss, int V, int64_t ignore_index,
-                                                           int write_grad, const float* __restrict__ gscale) {
+                                                           int write_grad, const float* __restrict__ gscale,
+                                                           float* __restrict__ lse_out) {
   __shared__ float sm[4], ss[4];
   __shared__ float s_tgt;
   const int64_t row = blockIdx.x;
@@ -193,7 +194,10 @@ __global__ __launch_bounds__(256) void xent_fwd_bwd_kernel(bf16_t* __restrict__ 
   float Ssum = 0.f;
   for (int i = 0; i < nw; ++i) Ssum += ss[i] * __expf(sm[i] - M);
   const float lse = M + __logf(Ssum);
-  if (threadIdx.x == 0) loss[row] = ignored ? 0.f : (lse - s_tgt);
+  if (threadIdx.x == 0) {
+    loss[row] = ignored ? 0.f : (lse - s_tgt);
+    if (lse_out) lse_out[row] = lse;
+  }
   if (!write_grad) return;
   // gradient multiplier (device scalar, e.g. dloss / n_valid): the backward writes the
   // final gradient in one pass instead of a separate scaling pass over V x rows
@@ -213,6 +217,39 @@ __global__ __launch_bounds__(256) void xent_fwd_bwd_kernel(bf16_t* __restrict__ 
   }
   for (int c = (nchunk << 3) + threadIdx.x; c < V; c += blockDim.x) {
     float p = ignored ? 0.f : __expf(bf2f(lr[c]) - M) * inv;
+    if (!ignored && (int64_t)c == lab) p -= g;
+    lr[c] = f2bf(p);
+  }
+}
+
+// Backward from the forward's per-row log-sum-exp: grad = (exp(x - lse) - onehot) * (*gscale)
+// written in place -- one read + one write of the logits (the recomputing form above reads
+// them twice).  ignore_index rows -> 0.
+__global__ __launch_bounds__(256) void xent_grad_lse_kernel(bf16_t* __restrict__ logits,
+                                                            const int64_t* __restrict__ labels,
+                                                            const float* __restrict__ lse_in, int V,
+                                                            int64_t ignore_index, const float* __restrict__ gscale) {
+  const int64_t row = blockIdx.x;
+  bf16_t* lr = logits + row * (int64_t)V;
+  const int64_t lab = labels[row];
+  const bool ignored = (lab == ignore_index) || lab < 0 || lab >= V;
+  const float g = gscale ? *gscale : 1.f;
+  const float lse = lse_in[row];
+  const int nchunk = V >> 3;
+  u32x4* lw = reinterpret_cast<u32x4*>(lr);
+  for (int c = threadIdx.x; c < nchunk; c += blockDim.x) {
+    float f[8];
+    unpack8(lw[c], f);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float p = ignored ? 0.f : __expf(f[i] - lse) * g;
+      if (!ignored && (int64_t)(c * 8 + i) == lab) p -= g;
+      f[i] = p;
+    }
+    lw[c] = pack8(f);
+  }
+  for (int c = (nchunk << 3) + threadIdx.x; c < V; c += blockDim.x) {
+    float p = ignored ? 0.f : __expf(bf2f(lr[c]) - lse) * g;
     if (!ignored && (int64_t)c == lab) p -= g;
     lr[c] = f2bf(p);
   }
@@ -857,11 +894,21 @@ int edl_rope_qkv_bwd(const void* dq, const void* dk, const void* dv, void* dqkv,
 }
 
 // write_grad: overwrite logits with (softmax - onehot) * (*gscale) (gscale may be null = 1)
+// lse_out (may be null): the per-row log-sum-exp, for edl_xent_grad_lse
 int edl_xent_fwd_bwd(void* logits, const int64_t* labels, float* loss, int64_t rows, int V, int64_t ignore_index,
-                     int write_grad, const float* gscale, hipStream_t s) {
+                     int write_grad, const float* gscale, float* lse_out, hipStream_t s) {
   if (rows <= 0) return 0;
   xent_fwd_bwd_kernel<<<(unsigned)rows, 256, 0, s>>>((bf16_t*)logits, labels, loss, V, ignore_index, write_grad,
-                                                     gscale);
+                                                     gscale, lse_out);
+  EDL_LAUNCH_CHECK();
+  return 0;
+}
+
+// logits <- (softmax - onehot) * (*gscale) from the forward's lse (one read + one write)
+int edl_xent_grad_lse(void* logits, const int64_t* labels, const float* lse, int64_t rows, int V,
+                      int64_t ignore_index, const float* gscale, hipStream_t s) {
+  if (rows <= 0) return 0;
+  xent_grad_lse_kernel<<<(unsigned)rows, 256, 0, s>>>((bf16_t*)logits, labels, lse, V, ignore_index, gscale);
   EDL_LAUNCH_CHECK();
   return 0;
 }

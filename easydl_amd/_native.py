@@ -58,7 +58,8 @@ _KERNEL_SIGS = {
                          c_int, c_void_p],
     "edl_rope_qkv_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_i64, c_int, c_int, c_int,
                          c_int, c_void_p],
-    "edl_xent_fwd_bwd": [c_void_p, c_void_p, c_void_p, c_i64, c_int, c_i64, c_int, c_void_p, c_void_p],
+    "edl_xent_fwd_bwd": [c_void_p, c_void_p, c_void_p, c_i64, c_int, c_i64, c_int, c_void_p, c_void_p, c_void_p],
+    "edl_xent_grad_lse": [c_void_p, c_void_p, c_void_p, c_i64, c_int, c_i64, c_void_p, c_void_p],
     "edl_xent_vp": [c_void_p, c_void_p, c_void_p, c_i64, c_int, c_i64, c_i64, c_int, c_void_p, c_void_p],
     "edl_scale_bf16": [c_void_p, c_i64, c_void_p, c_float, c_void_p],
     "edl_transpose_bf16": [c_void_p, c_void_p, c_int, c_int, c_void_p],

@@ -149,12 +149,16 @@ def cross_entropy_ref(logits, labels, ignore_index=-100):
     return F.cross_entropy(logits.float(), labels, ignore_index=ignore_index)
 
 
+_XENT_LSE = os.environ.get("EDL_XENT_LSE", "1") != "0"
+
+
 class _XentFn(torch.autograd.Function):
     """Mean token cross-entropy over bf16 logits.  The forward only reads the logits
-    (loss per row); the backward recomputes the row max / sum and writes the final
-    gradient (softmax - onehot) * dloss / n_valid in place into the logits buffer: one
-    read-write pass instead of a write in the forward plus a separate scaling pass
-    (-1.8 ms per 16k x 128k micro-batch)."""
+    (loss and log-sum-exp per row); the backward writes the final gradient
+    (exp(x - lse) - onehot) * dloss / n_valid in place into the logits buffer: one read +
+    one write, instead of a write in the forward plus a separate scaling pass (-1.8 ms per
+    16k x 128k micro-batch) and without re-reading the row for its statistics
+    (EDL_XENT_LSE=0: the backward recomputes them)."""
 
     @staticmethod
     def forward(ctx, logits, labels, ignore_index):
@@ -163,13 +167,14 @@ class _XentFn(torch.autograd.Function):
             logits = logits.contiguous()
         rows, V = logits.shape
         loss = torch.empty(rows, dtype=torch.float32, device=logits.device)
+        lse = torch.empty(rows, dtype=torch.float32, device=logits.device) if _XENT_LSE else None
         labels = labels.contiguous().to(torch.int64)
         k.check("edl_xent_fwd_bwd", logits.data_ptr(), labels.data_ptr(), loss.data_ptr(), rows, V, ignore_index,
-                0, None, _native.stream_of(logits))
+                0, None, _native.ptr(lse), _native.stream_of(logits))
         nvalid = (labels != ignore_index).sum().clamp_min(1).float()
         out = loss.sum() / nvalid
         if ctx.needs_input_grad[0]:
-            ctx.save_for_backward(logits, labels, nvalid, loss)
+            ctx.save_for_backward(logits, labels, nvalid, loss, lse)
             ctx.ignore_index = ignore_index
         return out
 
@@ -181,12 +186,16 @@ class _XentFn(torch.autograd.Function):
             raise RuntimeError("fused cross_entropy: backward ran twice (retain_graph is not supported: "
                                "the logits buffer is consumed by its gradient)")
         ctx.consumed = True
-        logits, labels, nvalid, loss = ctx.saved_tensors
+        logits, labels, nvalid, loss, lse = ctx.saved_tensors
         rows, V = logits.shape
         scale = (dloss.float() / nvalid).reshape(1).contiguous()
         # NOTE: the saved logits buffer becomes its own gradient (no second V x rows buffer)
-        k.check("edl_xent_fwd_bwd", logits.data_ptr(), labels.data_ptr(), loss.data_ptr(), rows, V,
-                ctx.ignore_index, 1, scale.data_ptr(), _native.stream_of(logits))
+        if lse is not None:
+            k.check("edl_xent_grad_lse", logits.data_ptr(), labels.data_ptr(), lse.data_ptr(), rows, V,
+                    ctx.ignore_index, scale.data_ptr(), _native.stream_of(logits))
+        else:
+            k.check("edl_xent_fwd_bwd", logits.data_ptr(), labels.data_ptr(), loss.data_ptr(), rows, V,
+                    ctx.ignore_index, 1, scale.data_ptr(), None, _native.stream_of(logits))
         return logits, None, None
 
 

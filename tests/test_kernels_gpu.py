@@ -105,7 +105,11 @@ def test_rope_qkv(cuda, B, S, H, KV, D):
 
 
 @pytest.mark.parametrize("T,V", [(4, 512), (64, 128256), (3, 1000)])
-def test_cross_entropy(cuda, T, V):
+@pytest.mark.parametrize("lse", [True, False])
+def test_cross_entropy(cuda, T, V, lse, monkeypatch):
+    """Fused cross-entropy vs fp32 torch; the backward from the forward's saved log-sum-exp
+    (default) and recomputing the row statistics (EDL_XENT_LSE=0)."""
+    monkeypatch.setattr(fused, "_XENT_LSE", lse)
     torch.manual_seed(4)
     logits = (3 * torch.randn(T, V, device=cuda)).to(torch.bfloat16)
     labels = torch.randint(0, V, (T,), device=cuda)
