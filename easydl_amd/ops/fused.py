@@ -301,9 +301,10 @@ def _nt_wgrad_ok(dy2: torch.Tensor, x2: torch.Tensor) -> bool:
 # drop their h^T / d(gate_up)^T / du^T outputs).  Applies when N % 128 == 0 and
 # J % 256 == 0.  Measured per shape at M = 16384 (profiles/r03_gemm_tn_ab.md): it beats
 # hipBLASLt NT + the two transposes on every BERT-large weight (N*J <= 4.2 M: 0.05-0.14 ms
-# vs 0.08-0.20 ms) and loses on the Llama-3-8B ones (N*J >= 16.8 M: its 128 x 256 tile
-# runs 0.8-1.2 PF/s against hipBLASLt's 256 x 256 at 1.5+), so by default ("auto") it
-# takes weights of at most EDL_WGRAD_TN_MAX_ELEMS (8 M) elements.  EDL_WGRAD_TN=1: every
+# vs 0.08-0.20 ms) and loses on the Llama-3-8B ones (N*J >= 16.8 M: its 256 x 256 kernel
+# runs 1.1-1.2 PF/s against hipBLASLt NT's 1.4-1.6, and the step is slower with any of them
+# on it), so by default ("auto") it takes weights of at most EDL_WGRAD_TN_MAX_ELEMS (8 M)
+# elements.  EDL_WGRAD_TN=1: every
 # eligible weight; 0: never (NT form on transposed copies).
 _WGRAD_TN = os.environ.get("EDL_WGRAD_TN", "auto")
 _WGRAD_TN_MAX = int(os.environ.get("EDL_WGRAD_TN_MAX_ELEMS", 8 << 20))
