@@ -203,35 +203,40 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(const bf16_t* __restrict_
   }
 }
 
-// out[c] (+)= sum_g partial[g][c]; out dtype bf16 (odt=0) or fp32 (odt=1).
-// Workgroup = 16 column groups (4 columns each, f32x4 loads) x 16 row slices;
-// slices are combined through LDS.  cols % 4 == 0.
-// Column sums of a [G, cols] fp32 partial slab.  A 1024-thread block owns 64 columns
-// (16 groups of 4) and splits the G rows over 64 slices: at G = 1024 each thread adds 16
-// independent 16-B loads (4 chains) instead of 64 serial ones, then an LDS tree.  The
-// 256-thread version was latency-bound: 13.5 us per call, 197 calls per BERT-large step.
+// out[c] (+)= sum_g partial[g][c]; out dtype bf16 (odt=0) or fp32 (odt=1); cols % 4 == 0.
+// Column sums of a [G, cols] fp32 partial slab.  A 1024-thread block owns CG column groups
+// of 4 (f32x4 loads) and splits the G rows over 1024/CG slices; the slices are summed across
+// the lanes of each wave (xor shuffles), then the 16 waves' sums through LDS.  CG is picked
+// per call so the launch has >= ~128 blocks: the 16-group block gave BERT-large's 1024-wide
+// slabs 16 blocks on 256 CUs (5.5 us per call, 197 calls per step).
+template <int CG>
 __global__ __launch_bounds__(1024) void colsum_kernel(const float* __restrict__ partial, int G, int cols,
                                                       void* __restrict__ out, int odt, int accumulate) {
-  __shared__ f32x4 red[64][16];
-  const int cg = threadIdx.x & 15, sl = threadIdx.x >> 4;
-  const int c = (blockIdx.x * 16 + cg) * 4;
+  constexpr int SL = 1024 / CG;
+  __shared__ f32x4 red[16][CG];
+  const int cg = threadIdx.x % CG, sl = threadIdx.x / CG;
+  const int c = (blockIdx.x * CG + cg) * 4;
   f32x4 s4[4] = {};
   if (c < cols) {
     int g = sl;
-    for (; g + 192 < G; g += 256) {
+    for (; g + 3 * SL < G; g += 4 * SL) {
 #pragma unroll
-      for (int u = 0; u < 4; ++u) s4[u] += *reinterpret_cast<const f32x4*>(partial + (int64_t)(g + 64 * u) * cols + c);
+      for (int u = 0; u < 4; ++u) s4[u] += *reinterpret_cast<const f32x4*>(partial + (int64_t)(g + SL * u) * cols + c);
     }
-    for (; g < G; g += 64) s4[0] += *reinterpret_cast<const f32x4*>(partial + (int64_t)g * cols + c);
+    for (; g < G; g += SL) s4[0] += *reinterpret_cast<const f32x4*>(partial + (int64_t)g * cols + c);
   }
-  red[sl][cg] = (s4[0] + s4[1]) + (s4[2] + s4[3]);
+  f32x4 s = (s4[0] + s4[1]) + (s4[2] + s4[3]);
+#pragma unroll
+  for (int off = CG; off < 64; off <<= 1) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) s[k] += __shfl_xor(s[k], off, 64);
+  }
+  if ((threadIdx.x & 63) < CG) red[threadIdx.x >> 6][cg] = s;
   __syncthreads();
-  for (int w = 32; w >= 1; w >>= 1) {
-    if (sl < w) red[sl][cg] += red[sl + w][cg];
-    __syncthreads();
-  }
-  if (sl != 0 || c >= cols) return;
-  const f32x4 s = red[0][cg];
+  if ((int)threadIdx.x >= CG || c >= cols) return;
+  s = red[0][cg];
+#pragma unroll
+  for (int w = 1; w < 16; ++w) s += red[w][cg];
   if (odt == 0) {
     bf16_t* o = reinterpret_cast<bf16_t*>(out) + c;
 #pragma unroll
@@ -329,7 +334,16 @@ int edl_layernorm_bwd(const void* dy, const void* x, const void* w, const float*
 
 int edl_colsum(const float* partial, int G, int cols, void* out, int odt, int accumulate, hipStream_t s) {
   if (cols % 4) return (int)hipErrorInvalidValue;
-  colsum_kernel<<<(cols + 63) / 64, 1024, 0, s>>>(partial, G, cols, out, odt, accumulate);
+  int cg = 16;   // column groups per block: the widest that still gives >= 128 blocks
+  while (cg > 1 && (cols / 4 + cg - 1) / cg < 128) cg >>= 1;
+  const unsigned nb = (unsigned)((cols / 4 + cg - 1) / cg);
+  switch (cg) {
+    case 16: colsum_kernel<16><<<nb, 1024, 0, s>>>(partial, G, cols, out, odt, accumulate); break;
+    case 8: colsum_kernel<8><<<nb, 1024, 0, s>>>(partial, G, cols, out, odt, accumulate); break;
+    case 4: colsum_kernel<4><<<nb, 1024, 0, s>>>(partial, G, cols, out, odt, accumulate); break;
+    case 2: colsum_kernel<2><<<nb, 1024, 0, s>>>(partial, G, cols, out, odt, accumulate); break;
+    default: colsum_kernel<1><<<nb, 1024, 0, s>>>(partial, G, cols, out, odt, accumulate); break;
+  }
   EDL_LAUNCH_CHECK();
   return 0;
 }

@@ -474,7 +474,7 @@ def test_gemm_tn_matches_fp32(cuda, M, N, J, out_dt, acc):
     assert err < (1e-2 if out_dt == torch.bfloat16 else 1e-4), err
 
 
-@pytest.mark.parametrize("M,C", [(16384, 1024), (1000, 64), (40, 4096)])
+@pytest.mark.parametrize("M,C", [(16384, 1024), (1000, 64), (40, 4096), (16384, 3072), (777, 512), (5000, 2056)])
 def test_colsum_bf16_partials(cuda, M, C):
     """Bias-gradient column sums of a bf16 [M, C] matrix (edl_colsum_bf16_partial + edl_colsum)."""
     from easydl_amd import _native
@@ -483,6 +483,22 @@ def test_colsum_bf16_partials(cuda, M, C):
     out = torch.empty(C, device=cuda)
     _native.kernels().check("edl_colsum", part.data_ptr(), G, C, out.data_ptr(), 1, 0, _native.stream_of(t))
     torch.testing.assert_close(out, t.float().sum(0), rtol=1e-4, atol=1e-3 * M ** 0.5)
+
+
+@pytest.mark.parametrize("G,C", [(1024, 1024), (1000, 4096), (512, 3072), (37, 8192), (1024, 16384), (7, 260),
+                                 (33, 4100)])
+@pytest.mark.parametrize("odt,acc", [(1, 0), (1, 1), (0, 1)])
+def test_colsum_block_widths(cuda, G, C, odt, acc):
+    """edl_colsum on slabs whose width picks each column-group block shape (16/8/4/2/1
+    groups of 4 per block), a ragged last block and G not a multiple of the slice count."""
+    from easydl_amd import _native
+    part = torch.randn(G, C, device=cuda)
+    dt = torch.float32 if odt else torch.bfloat16
+    out = torch.randn(C, device=cuda).to(dt)
+    want = part.sum(0) + (out.float() if acc else 0)
+    _native.kernels().check("edl_colsum", part.data_ptr(), G, C, out.data_ptr(), odt, acc, _native.stream_of(part))
+    tol = 1e-4 * G ** 0.5 if odt else 2e-2 * G ** 0.5
+    torch.testing.assert_close(out.float(), want, rtol=1e-4 if odt else 1e-2, atol=tol)
 
 
 @pytest.mark.parametrize("tn", ["0", "1"])
