@@ -1,5 +1,5 @@
 #!/bin/bash
-# dK/dV kernel with exp(S) interleaved into the dP MFMA chain:
+# dK/dV kernel variants (exp under the dP chain; straight-line sub-slices below the diagonal):
 # numerics tests, then kernel and whole-step A/B against the previous library (abtmp/lib_base).
 set -u
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
