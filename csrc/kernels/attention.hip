@@ -316,7 +316,7 @@ template <bool CAUSAL, int D>
 __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
                                                           const bf16_t* __restrict__ v, bf16_t* __restrict__ o,
                                                           float* __restrict__ lse, int S, int H, int KV,
-                                                          float scale_log2, int xcd) {
+                                                          float scale_log2, int xcd, int64_t qis, int64_t kvs) {
   constexpr int BQ = 128;
   constexpr int TILE = 64 * 2 * D, STAGE = 2 * TILE;   // one 64-row K (or V) tile; K + V
   __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
@@ -327,15 +327,17 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_t* __restri
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // provably wave-uniform
   const int q0 = qb * BQ;
   const int wq0 = q0 + 32 * w;  // first query of this wave
-  const int64_t qs = (int64_t)H * D, ks = (int64_t)KV * D;
-  const bf16_t* qp = q + (int64_t)b * S * qs + hq * D;
+  // q / k / v token rows are qis / kvs elements apart (H*D / KV*D, or 3*H*D for the slices of
+  // one packed qkv projection); o is written contiguous
+  const int64_t qs = (int64_t)H * D, ks = kvs;
+  const bf16_t* qp = q + (int64_t)b * S * qis + hq * D;
   const bf16_t* kp = k + (int64_t)b * S * ks + hk * D;
   const bf16_t* vp = v + (int64_t)b * S * ks + hk * D;
 
   const int qr = wq0 + l31;
   bf16x8 qf[D / 16];
 #pragma unroll
-  for (int s = 0; s < D / 16; ++s) qf[s] = load_frag(qp + (int64_t)min(qr, S - 1) * qs, s, h);
+  for (int s = 0; s < D / 16; ++s) qf[s] = load_frag(qp + (int64_t)min(qr, S - 1) * qis, s, h);
   const int kv_end = CAUSAL ? min(S, q0 + BQ) : S;
   const int ntiles = (kv_end + 63) / 64;
   f32x16 oacc[D / 32];
@@ -629,7 +631,7 @@ template <bool CAUSAL>
 __global__ __launch_bounds__(256, 1) void attn_fwd64_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
                                                             const bf16_t* __restrict__ v, bf16_t* __restrict__ o,
                                                             float* __restrict__ lse, int S, int H, int KV,
-                                                            float sl2) {
+                                                            float sl2, int64_t qis, int64_t kvs) {
   using namespace fwd64;
   constexpr int BQ = 256;
   __shared__ __attribute__((aligned(16))) char smem[2 * NS * TB];   // K ring, then V ring (one array)
@@ -638,15 +640,15 @@ __global__ __launch_bounds__(256, 1) void attn_fwd64_kernel(const bf16_t* __rest
   const int lane = threadIdx.x & 63, h = lane >> 5, l31 = lane & 31;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int q0 = qblk * BQ, wq0 = q0 + 64 * w;
-  const int64_t qs = (int64_t)H * HD, ks = (int64_t)KV * HD;
-  const bf16_t* qp = q + (int64_t)b * S * qs + hq * HD;
+  const int64_t qs = (int64_t)H * HD, ks = kvs;   // input row strides as in attn_fwd_kernel
+  const bf16_t* qp = q + (int64_t)b * S * qis + hq * HD;
   const bf16_t* kp = k + (int64_t)b * S * ks + hk * HD;
   const bf16_t* vp = v + (int64_t)b * S * ks + hk * HD;
 
   State st;
 #pragma unroll
   for (int qb = 0; qb < 2; ++qb) {
-    const bf16_t* rowp = qp + (int64_t)min(wq0 + 32 * qb + l31, S - 1) * qs;
+    const bf16_t* rowp = qp + (int64_t)min(wq0 + 32 * qb + l31, S - 1) * qis;
 #pragma unroll
     for (int s = 0; s < 8; ++s) st.qf[qb][s] = load_frag(rowp, s, h);
     st.m[qb] = -1e30f;
@@ -861,7 +863,7 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dkdv_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
     const bf16_t* __restrict__ dout, const float* __restrict__ lse, const float* __restrict__ delta,
     bf16_t* __restrict__ dk, bf16_t* __restrict__ dv, int S, int H, int KV, float scale_log2, float scale,
-    int64_t dkvs) {
+    int64_t dkvs, int64_t kvs) {
   constexpr int QT = 64;  // queries per staged tile
   constexpr int TILE = QT * 2 * D, STAGE = 2 * TILE;
   // 2 stages x (Q tile + dO tile) + 2 x (-lse2, delta) x 64 floats
@@ -870,7 +872,7 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dkdv_kernel(
   const int lane = threadIdx.x & 63, h = lane >> 5, l31 = lane & 31;
   const int w = threadIdx.x >> 6;
   const int group = H / KV;
-  const int64_t qs = (int64_t)H * D, ks = (int64_t)KV * D;
+  const int64_t qs = (int64_t)H * D, ks = kvs;   // q / dO rows contiguous; k / v rows kvs apart
   const int mykey = kb * 128 + 32 * w + l31;
   const int64_t krow_off = (int64_t)b * S * ks + (int64_t)min(mykey, S - 1) * ks + hk * D;
   bf16x8 kf[D / 16], vf[D / 16];
@@ -1084,7 +1086,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv64_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
     const bf16_t* __restrict__ dout, const float* __restrict__ lse, const float* __restrict__ delta,
     bf16_t* __restrict__ dk, bf16_t* __restrict__ dv, float* __restrict__ ws, int S, int H, int KV, int gsplit,
-    float scale_log2, float scale, int64_t dkvs) {
+    float scale_log2, float scale, int64_t dkvs, int64_t kvs) {
   constexpr int QT = 64;   // queries per staged tile
   constexpr int KW = 64;   // keys per wave
   constexpr int KB = 4 * KW;
@@ -1095,7 +1097,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv64_kernel(
   const int lane = threadIdx.x & 63, h = lane >> 5, l31 = lane & 31;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // provably wave-uniform
   const int heads = (H / KV) / gsplit, hq0 = hk * (H / KV) + gs * heads;
-  const int64_t qs = (int64_t)H * D, ks = (int64_t)KV * D;
+  const int64_t qs = (int64_t)H * D, ks = kvs;   // q / dO rows contiguous; k / v rows kvs apart
   const int nkb = (S + KB - 1) / KB, nqt = (S + QT - 1) / QT;
   const int64_t nBHS = (int64_t)gridDim.z * H * S;  // delta = [delta | -lse*log2e]
   const DmaPlan<QT, 4, D> plan(qs, w, lane);
@@ -1272,7 +1274,8 @@ template <bool CAUSAL, int D>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
     const bf16_t* __restrict__ dout, const float* __restrict__ lse, const float* __restrict__ delta,
-    bf16_t* __restrict__ dq, int S, int H, int KV, float scale_log2, float scale, int xcd, int64_t dqs) {
+    bf16_t* __restrict__ dq, int S, int H, int KV, float scale_log2, float scale, int xcd, int64_t dqs,
+    int64_t kvs) {
   constexpr int BQ = 128;
   constexpr int TILE = 64 * 2 * D, STAGE = 2 * TILE;
   __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
@@ -1283,7 +1286,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(
   const int w = threadIdx.x >> 6;
   const int q0 = qb * BQ;
   const int wq0 = q0 + 32 * w;
-  const int64_t qs = (int64_t)H * D, ks = (int64_t)KV * D;
+  const int64_t qs = (int64_t)H * D, ks = kvs;
   const bf16_t* kp = k + (int64_t)b * S * ks + hk * D;
   const bf16_t* vp = v + (int64_t)b * S * ks + hk * D;
   const int qr = wq0 + l31, qc = min(qr, S - 1);
@@ -1357,15 +1360,15 @@ static int attn_xcd_map(int B, int KV) {
 
 template <int D>
 static void attn_fwd_launch(const void* q, const void* k, const void* v, void* o, float* lse, int B, int S, int H,
-                            int KV, int causal, float sl2, hipStream_t s) {
+                            int KV, int causal, float sl2, int64_t qis, int64_t kvs, hipStream_t s) {
   dim3 grid((S + 127) / 128, H, B);
   const int xcd = attn_xcd_map(B, KV);
   if (causal)
     attn_fwd_kernel<true, D><<<grid, 256, 0, s>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
-                                                      (bf16_t*)o, lse, S, H, KV, sl2, xcd);
+                                                      (bf16_t*)o, lse, S, H, KV, sl2, xcd, qis, kvs);
   else
     attn_fwd_kernel<false, D><<<grid, 256, 0, s>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
-                                                       (bf16_t*)o, lse, S, H, KV, sl2, xcd);
+                                                       (bf16_t*)o, lse, S, H, KV, sl2, xcd, qis, kvs);
 }
 
 // dK/dV-64 work decomposition (see attn_bwd_dkdv64_kernel): returns gsplit, fills the grid
@@ -1390,7 +1393,7 @@ static int dkdv_keys_per_wave() {
 template <int D>
 static int attn_bwd_impl(const void* q, const void* k, const void* v, const void* o, const void* dout,
                          const float* lse, float* delta, void* dq, void* dk, void* dv, float* ws, int B, int S, int H,
-                         int KV, int causal, float scale, int64_t dqs, int64_t dkvs, hipStream_t s) {
+                         int KV, int causal, float scale, int64_t dqs, int64_t dkvs, int64_t kvs, hipStream_t s) {
   const int64_t nrows = (int64_t)B * S * H;
   attn_bwd_delta_kernel<D><<<(unsigned)((nrows * (D / 8) + 255) / 256), 256, 0, s>>>(
       (const bf16_t*)o, (const bf16_t*)dout, lse, delta, S, H, nrows);
@@ -1414,10 +1417,10 @@ static int attn_bwd_impl(const void* q, const void* k, const void* v, const void
   if (keys_per_wave == 64) {
     if (causal)
       attn_bwd_dkdv64_kernel<true, D><<<gkv64, 256, 0, s>>>(bq, bk, bv, bdo, lse, delta, (bf16_t*)dk, (bf16_t*)dv,
-                                                            ws, S, H, KV, gsplit, sl2, scale, dkvs);
+                                                            ws, S, H, KV, gsplit, sl2, scale, dkvs, kvs);
     else
       attn_bwd_dkdv64_kernel<false, D><<<gkv64, 256, 0, s>>>(bq, bk, bv, bdo, lse, delta, (bf16_t*)dk, (bf16_t*)dv,
-                                                             ws, S, H, KV, gsplit, sl2, scale, dkvs);
+                                                             ws, S, H, KV, gsplit, sl2, scale, dkvs, kvs);
     if (gsplit > 1) {
       EDL_LAUNCH_CHECK();
       const int64_t rows = (int64_t)B * S * KV;
@@ -1427,7 +1430,7 @@ static int attn_bwd_impl(const void* q, const void* k, const void* v, const void
   } else {
 #define EDL_DKDV(C, O)                                                                                       \
   attn_bwd_dkdv_kernel<C, O, D><<<gkv, 256, 0, s>>>(bq, bk, bv, bdo, lse, delta, (bf16_t*)dk, (bf16_t*)dv, S, H, \
-                                                    KV, sl2, scale, dkvs)
+                                                    KV, sl2, scale, dkvs, kvs)
     if (causal) {
       if (occ == 2 || D == 64) EDL_DKDV(true, 2); else EDL_DKDV(true, 1);
     } else {
@@ -1438,20 +1441,29 @@ static int attn_bwd_impl(const void* q, const void* k, const void* v, const void
   EDL_LAUNCH_CHECK();
   if (causal)
     attn_bwd_dq_kernel<true, D><<<gq, 256, 0, s>>>(bq, bk, bv, bdo, lse, delta, (bf16_t*)dq, S, H, KV, sl2, scale,
-                                                   attn_xcd_map(B, KV), dqs);
+                                                   attn_xcd_map(B, KV), dqs, kvs);
   else
     attn_bwd_dq_kernel<false, D><<<gq, 256, 0, s>>>(bq, bk, bv, bdo, lse, delta, (bf16_t*)dq, S, H, KV, sl2, scale,
-                                                    attn_xcd_map(B, KV), dqs);
+                                                    attn_xcd_map(B, KV), dqs, kvs);
   EDL_LAUNCH_CHECK();
   return 0;
 }
 
 extern "C" {
 
-// head dim D = 64 or 128 (bf16, any S, GQA with H % KV == 0)
-int edl_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int S, int H, int KV,
-                 int D, int causal, float scale, hipStream_t s) {
+// input row strides: q rows qis (>= H*D) and k / v rows kvs (>= KV*D) elements apart, e.g. the
+// q / k / v slices of one packed [B, S, 3, H, D] projection (BERT's fused qkv Linear: no split
+// pass).  The LDS-DMA descriptors address a batch's S rows in 32 bits.
+static bool strides_ok(int S, int H, int KV, int D, int64_t qis, int64_t kvs) {
+  return qis >= (int64_t)H * D && kvs >= (int64_t)KV * D && qis % 8 == 0 && kvs % 8 == 0 &&
+         (int64_t)S * kvs * 2 < (int64_t(1) << 32) && (int64_t)S * qis * 2 < (int64_t(1) << 32);
+}
+
+// head dim D = 64 or 128 (bf16, any S, GQA with H % KV == 0); o is written contiguous [B, S, H, D]
+int edl_attn_fwd_strided(const void* q, const void* k, const void* v, void* o, float* lse, int B, int S, int H,
+                         int KV, int D, int causal, float scale, int64_t qis, int64_t kvs, hipStream_t s) {
   if ((D != 64 && D != 128) || H % KV != 0 || S <= 0) return (int)hipErrorInvalidValue;
+  if (!strides_ok(S, H, KV, D, qis, kvs)) return (int)hipErrorInvalidValue;
   const float sl2 = scale * LOG2E;
   // EDL_ATTN_FWD=64: the software-pipelined 64-queries-per-wave kernel (head dim 128)
   const char* sel = getenv("EDL_ATTN_FWD");
@@ -1459,19 +1471,24 @@ int edl_attn_fwd(const void* q, const void* k, const void* v, void* o, float* ls
     dim3 g64((S + 255) / 256, H, B);
     if (causal)
       attn_fwd64_kernel<true><<<g64, 256, 0, s>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
-                                                     (bf16_t*)o, lse, S, H, KV, sl2);
+                                                     (bf16_t*)o, lse, S, H, KV, sl2, qis, kvs);
     else
       attn_fwd64_kernel<false><<<g64, 256, 0, s>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
-                                                      (bf16_t*)o, lse, S, H, KV, sl2);
+                                                      (bf16_t*)o, lse, S, H, KV, sl2, qis, kvs);
     EDL_LAUNCH_CHECK();
     return 0;
   }
   if (D == 128)
-    attn_fwd_launch<128>(q, k, v, o, lse, B, S, H, KV, causal, sl2, s);
+    attn_fwd_launch<128>(q, k, v, o, lse, B, S, H, KV, causal, sl2, qis, kvs, s);
   else
-    attn_fwd_launch<64>(q, k, v, o, lse, B, S, H, KV, causal, sl2, s);
+    attn_fwd_launch<64>(q, k, v, o, lse, B, S, H, KV, causal, sl2, qis, kvs, s);
   EDL_LAUNCH_CHECK();
   return 0;
+}
+
+int edl_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int S, int H, int KV,
+                 int D, int causal, float scale, hipStream_t s) {
+  return edl_attn_fwd_strided(q, k, v, o, lse, B, S, H, KV, D, causal, scale, (int64_t)H * D, (int64_t)KV * D, s);
 }
 
 // fp32 workspace the backward needs for the head-split dK/dV partials (0 = none); sized
@@ -1484,24 +1501,29 @@ int64_t edl_attn_bwd_ws_bytes(int B, int S, int H, int KV, int causal) {
 
 // dq / dk / dv may be row-strided views: token rows dqs (>= H*D) and dkvs (>= KV*D) elements
 // apart, e.g. the q / k / v slices of one packed [B, S, 3, H, D] gradient (BERT's fused
-// qkv projection takes it without a concatenation pass)
+// qkv projection takes it without a concatenation pass).  Inputs: k / v rows kvs apart (the
+// packed projection's slices); q, o and dout contiguous [B, S, H, D] (the dK/dV kernel stages
+// q and dout tiles with one DMA plan).
 int edl_attn_bwd_strided(const void* q, const void* k, const void* v, const void* o, const void* dout,
                          const float* lse, float* delta, void* dq, void* dk, void* dv, float* ws, int B, int S, int H,
-                         int KV, int D, int causal, float scale, int64_t dqs, int64_t dkvs, hipStream_t s) {
+                         int KV, int D, int causal, float scale, int64_t dqs, int64_t dkvs, int64_t kvs,
+                         hipStream_t s) {
   if ((D != 64 && D != 128) || H % KV != 0 || S <= 0) return (int)hipErrorInvalidValue;
   if (dqs < (int64_t)H * D || dkvs < (int64_t)KV * D || dqs % 8 || dkvs % 8) return (int)hipErrorInvalidValue;
+  if (!strides_ok(S, H, KV, D, (int64_t)H * D, kvs)) return (int)hipErrorInvalidValue;
   if (edl_attn_bwd_ws_bytes(B, S, H, KV, causal) > 0 && ws == nullptr) return (int)hipErrorInvalidValue;
   if (D == 128)
     return attn_bwd_impl<128>(q, k, v, o, dout, lse, delta, dq, dk, dv, ws, B, S, H, KV, causal, scale, dqs, dkvs,
-                              s);
-  return attn_bwd_impl<64>(q, k, v, o, dout, lse, delta, dq, dk, dv, ws, B, S, H, KV, causal, scale, dqs, dkvs, s);
+                              kvs, s);
+  return attn_bwd_impl<64>(q, k, v, o, dout, lse, delta, dq, dk, dv, ws, B, S, H, KV, causal, scale, dqs, dkvs, kvs,
+                           s);
 }
 
 int edl_attn_bwd(const void* q, const void* k, const void* v, const void* o, const void* dout, const float* lse,
                  float* delta, void* dq, void* dk, void* dv, float* ws, int B, int S, int H, int KV, int D,
                  int causal, float scale, hipStream_t s) {
   return edl_attn_bwd_strided(q, k, v, o, dout, lse, delta, dq, dk, dv, ws, B, S, H, KV, D, causal, scale,
-                              (int64_t)H * D, (int64_t)KV * D, s);
+                              (int64_t)H * D, (int64_t)KV * D, (int64_t)KV * D, s);
 }
 
 }  // extern "C"

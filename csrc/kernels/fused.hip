@@ -681,10 +681,9 @@ __global__ __launch_bounds__(256) void qkv_split_kernel(const bf16_t* __restrict
     const int64_t t = i / hd8;
     const int c = (int)(i - t * hd8);
     const u32x4* src = reinterpret_cast<const u32x4*>(qkv) + t * 3 * hd8 + c;
-    const u32x4 a = src[0], b = src[hd8], d = src[2 * hd8];
-    reinterpret_cast<u32x4*>(q)[i] = a;
-    reinterpret_cast<u32x4*>(k)[i] = b;
-    reinterpret_cast<u32x4*>(v)[i] = d;
+    reinterpret_cast<u32x4*>(q)[i] = src[0];
+    if (k) reinterpret_cast<u32x4*>(k)[i] = src[hd8];   // k / v null: q only
+    if (v) reinterpret_cast<u32x4*>(v)[i] = src[2 * hd8];
   }
 }
 
@@ -844,7 +843,7 @@ int edl_swiglu_bwd_t_lds(const void* dh, const void* gu, void* dgu, void* dguT, 
   return 0;
 }
 
-// q / k / v [T, HD] = slices of packed qkv [T, 3 * HD] (HD multiple of 8)
+// q / k / v [T, HD] = slices of packed qkv [T, 3 * HD] (HD multiple of 8); k and v may be null (q only)
 int edl_qkv_split(const void* qkv, void* q, void* k, void* v, int64_t T, int HD, hipStream_t s) {
   if (HD % 8 || T <= 0) return (int)hipErrorInvalidValue;
   qkv_split_kernel<<<grid_for(T * (HD / 8)), 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)q, (bf16_t*)k, (bf16_t*)v, T,

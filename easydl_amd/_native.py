@@ -73,9 +73,11 @@ _KERNEL_SIGS = {
                      c_float, c_void_p],
     "edl_attn_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                      c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_void_p],
+    "edl_attn_fwd_strided": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int,
+                             c_int, c_float, c_i64, c_i64, c_void_p],
     "edl_attn_bwd_strided": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                              c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_i64,
-                             c_i64, c_void_p],
+                             c_i64, c_i64, c_void_p],
     "edl_attn_bwd_ws_bytes": (c_i64, [c_int, c_int, c_int, c_int, c_int]),
     "edl_xgmi_allreduce": [ctypes.POINTER(c_void_p), ctypes.POINTER(c_void_p), c_int, c_int, c_void_p, c_void_p,
                            c_i64, c_int, c_int, ctypes.c_uint32, c_int, c_void_p, ctypes.c_double, c_void_p,

@@ -19,6 +19,9 @@ import torch.nn.functional as F
 
 from easydl_amd import _native
 
+# EDL_ATTN_QKV_SPLIT=1: split packed qkv into three tensors before the forward (A/B)
+_QKV_SPLIT = os.environ.get("EDL_ATTN_QKV_SPLIT", "0") == "1"
+
 
 def _bshd(t: torch.Tensor) -> torch.Tensor:
     """[B,H,S,D]-shaped tensor -> contiguous [B,S,H,D] memory (no copy if already laid out so)."""
@@ -62,41 +65,62 @@ class _FlashAttnFn(torch.autograd.Function):
 
 class _PackedQKVAttnFn(torch.autograd.Function):
     """Attention over one packed ``[B*S, 3*H*D]`` q|k|v projection (BERT's fused qkv
-    Linear).  The backward kernels write dq / dk / dv straight into the slices of one
-    packed gradient (row stride 3*H*D), so the qkv projection's backward gets its input
-    gradient without the concatenation pass autograd's unbind would run."""
+    Linear).  The forward kernels read q, k and v as row-strided slices of the packed
+    tensor (row stride 3*H*D, no split pass); the backward copies q out once (the dK/dV
+    kernel stages q and dO tiles with one DMA plan) and reads k / v strided.  The backward
+    kernels write dq / dk / dv straight into the slices of one packed gradient, so the qkv
+    projection's backward gets its input gradient without the concatenation pass
+    autograd's unbind would run.  ``EDL_ATTN_QKV_SPLIT=1`` restores the split of all three."""
 
     @staticmethod
     def forward(ctx, qkv, B, S, H, causal, scale):
         kn = _native.kernels()
         D = qkv.shape[-1] // (3 * H)
-        qm, km, vm = (torch.empty(B, S, H, D, dtype=qkv.dtype, device=qkv.device) for _ in range(3))
-        kn.check("edl_qkv_split", qkv.data_ptr(), qm.data_ptr(), km.data_ptr(), vm.data_ptr(), B * S, H * D,
-                 _native.stream_of(qkv))
-        o = torch.empty_like(qm)
+        row = H * D
+        st = _native.stream_of(qkv)
+        o = torch.empty(B, S, H, D, dtype=qkv.dtype, device=qkv.device)
         lse = torch.empty(B, H, S, dtype=torch.float32, device=qkv.device)
-        kn.check("edl_attn_fwd", qm.data_ptr(), km.data_ptr(), vm.data_ptr(), o.data_ptr(), lse.data_ptr(), B, S, H,
-                 H, D, 1 if causal else 0, scale, _native.stream_of(qkv))
-        ctx.save_for_backward(qm, km, vm, o, lse)
-        ctx.causal, ctx.scale = causal, scale
+        if _QKV_SPLIT:
+            qm, km, vm = (torch.empty(B, S, H, D, dtype=qkv.dtype, device=qkv.device) for _ in range(3))
+            kn.check("edl_qkv_split", qkv.data_ptr(), qm.data_ptr(), km.data_ptr(), vm.data_ptr(), B * S, row, st)
+            kn.check("edl_attn_fwd", qm.data_ptr(), km.data_ptr(), vm.data_ptr(), o.data_ptr(), lse.data_ptr(), B, S,
+                     H, H, D, 1 if causal else 0, scale, st)
+            ctx.save_for_backward(qm, km, vm, o, lse)
+        else:
+            base, es = qkv.data_ptr(), qkv.element_size()
+            kn.check("edl_attn_fwd_strided", base, base + row * es, base + 2 * row * es, o.data_ptr(), lse.data_ptr(),
+                     B, S, H, H, D, 1 if causal else 0, scale, 3 * row, 3 * row, st)
+            ctx.save_for_backward(qkv, o, lse)
+        ctx.causal, ctx.scale, ctx.shape = causal, scale, (B, S, H, D)
         return o.view(B * S, H * D)
 
     @staticmethod
     def backward(ctx, do):
         kn = _native.kernels()
-        qm, km, vm, o, lse = ctx.saved_tensors
-        B, S, H, D = qm.shape
+        B, S, H, D = ctx.shape
+        row = H * D
+        saved = ctx.saved_tensors
+        st = _native.stream_of(do)
+        if len(saved) == 5:
+            qm, km, vm, o, lse = saved
+            kptr, vptr, kvs = km.data_ptr(), vm.data_ptr(), row
+        else:
+            qkv, o, lse = saved
+            qm = torch.empty(B, S, H, D, dtype=qkv.dtype, device=qkv.device)
+            kn.check("edl_qkv_split", qkv.data_ptr(), qm.data_ptr(), None, None, B * S, row, st)
+            es = qkv.element_size()
+            kptr, vptr, kvs = qkv.data_ptr() + row * es, qkv.data_ptr() + 2 * row * es, 3 * row
         dom = do.reshape(B, S, H, D).contiguous()
-        dqkv = torch.empty(B * S, 3 * H * D, dtype=qm.dtype, device=qm.device)
+        dqkv = torch.empty(B * S, 3 * row, dtype=qm.dtype, device=qm.device)
         delta = torch.empty(2, B, H, S, dtype=torch.float32, device=qm.device)
         causal = 1 if ctx.causal else 0
         nws = kn.raw("edl_attn_bwd_ws_bytes")(B, S, H, H, causal)
         ws = torch.empty(nws // 4, dtype=torch.float32, device=qm.device) if nws else None
-        base, row = dqkv.data_ptr(), H * D
-        kn.check("edl_attn_bwd_strided", qm.data_ptr(), km.data_ptr(), vm.data_ptr(), o.data_ptr(), dom.data_ptr(),
-                 lse.data_ptr(), delta.data_ptr(), base, base + 2 * row, base + 4 * row,
-                 ws.data_ptr() if ws is not None else None, B, S, H, H, D, causal, ctx.scale, 3 * row, 3 * row,
-                 _native.stream_of(qm))
+        base, es = dqkv.data_ptr(), dqkv.element_size()
+        kn.check("edl_attn_bwd_strided", qm.data_ptr(), kptr, vptr, o.data_ptr(), dom.data_ptr(),
+                 lse.data_ptr(), delta.data_ptr(), base, base + row * es, base + 2 * row * es,
+                 ws.data_ptr() if ws is not None else None, B, S, H, H, D, causal, ctx.scale, 3 * row, 3 * row, kvs,
+                 st)
         return dqkv, None, None, None, None, None
 
 

@@ -148,11 +148,15 @@ def test_llama_on_hip_kernels_matches_fp32_cpu_model(cuda, hd):
 
 @pytest.mark.parametrize("B,S,H,D,causal", [(2, 512, 16, 64, False), (1, 200, 4, 64, True), (2, 384, 8, 128, False),
                                            (1, 1000, 4, 128, True)])
-def test_packed_qkv_attention_writes_strided_gradients(cuda, B, S, H, D, causal):
-    """packed_qkv_attention (BERT: one [B*S, 3*H*D] projection in, dq/dk/dv written by the
-    kernels straight into one packed gradient at row stride 3*H*D) is bitwise identical to
+@pytest.mark.parametrize("split", [False, True])
+def test_packed_qkv_attention_writes_strided_gradients(cuda, B, S, H, D, causal, split, monkeypatch):
+    """packed_qkv_attention (BERT: one [B*S, 3*H*D] projection in, q/k/v read by the kernels
+    as row-strided slices -- or split first, EDL_ATTN_QKV_SPLIT=1 --, dq/dk/dv written
+    straight into one packed gradient at row stride 3*H*D) is bitwise identical to
     flash_attention on the unpacked views, and within tolerance of the fp32 reference."""
+    from easydl_amd.ops import attention
     from easydl_amd.ops.attention import packed_qkv_attention
+    monkeypatch.setattr(attention, "_QKV_SPLIT", split)
     g = torch.Generator(device=cuda).manual_seed(S + H)
     qkv = torch.randn(B * S, 3 * H * D, device=cuda, generator=g).to(torch.bfloat16)
     do = torch.randn(B * S, H * D, device=cuda, generator=g).to(torch.bfloat16)
