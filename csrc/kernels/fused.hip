@@ -556,6 +556,34 @@ __global__ __launch_bounds__(256) void transpose_bf16_reg_kernel(const bf16_t* _
   for (int j = 0; j < 8; ++j) *reinterpret_cast<u32x4*>(dst + (int64_t)(c + j) * R + r) = out[j];
 }
 
+// Many transposes in one launch (the per-step refresh of every cached W^T): one 128x128 tile
+// per workgroup over the concatenated tile lists.  A BERT-large weight alone is 64-256
+// tiles, too few for 256 CUs (9.4 us per 1024 x 1024 transpose as separate launches).
+// Descriptor i = 4 int64: src, dst, (R << 32) | C, (first tile << 32) | column tiles.
+__global__ __launch_bounds__(256) void transpose_bf16_multi_kernel(const int64_t* __restrict__ desc, int n) {
+  const int b = blockIdx.x;
+  int lo = 0, hi = n - 1;   // last descriptor whose first tile <= b (wave-uniform search)
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if ((int)(desc[4 * mid + 3] >> 32) <= b) lo = mid; else hi = mid - 1;
+  }
+  const int64_t* d = desc + 4 * lo;
+  const bf16_t* src = reinterpret_cast<const bf16_t*>(d[0]);
+  bf16_t* dst = reinterpret_cast<bf16_t*>(d[1]);
+  const int R = (int)(d[2] >> 32), C = (int)(d[2] & 0xffffffff);
+  const int local = b - (int)(d[3] >> 32), tx_n = (int)(d[3] & 0xffffffff);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r = (local / tx_n) * RT + (w >> 1) * 64 + (lane >> 3) * 8;
+  const int c = (local % tx_n) * RT + (w & 1) * 64 + (lane & 7) * 8;
+  if (r >= R || c >= C) return;  // R, C multiples of 8: a block is all in or all out
+  u32x4 in[8], out[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) in[i] = *reinterpret_cast<const u32x4*>(src + (int64_t)(r + i) * C + c);
+  transpose8x8(in, out);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) *reinterpret_cast<u32x4*>(dst + (int64_t)(c + j) * R + r) = out[j];
+}
+
 // Transpose + column sums of src (the bias gradient of a linear layer is the column
 // sum of dY, whose transpose the NT weight-gradient GEMM needs anyway): each thread
 // sums its 8x8 block's columns, the 16 row groups of a 128x128 tile meet in LDS, and
@@ -928,6 +956,15 @@ int edl_xent_vp(void* logits, const int64_t* labels, float* st, int64_t rows, in
 }
 
 // dst[C, R] = src[R, C]^T (bf16, R and C multiples of 8)
+// n transposes in one launch; desc: device int64 [n, 4] (see transpose_bf16_multi_kernel),
+// first tiles ascending, tiles = the total 128x128 tile count
+int edl_transpose_bf16_multi(const void* desc, int n, int tiles, hipStream_t s) {
+  if (n <= 0 || tiles <= 0) return (int)hipErrorInvalidValue;
+  transpose_bf16_multi_kernel<<<tiles, 256, 0, s>>>((const int64_t*)desc, n);
+  EDL_LAUNCH_CHECK();
+  return 0;
+}
+
 int edl_transpose_bf16(const void* src, void* dst, int R, int C, hipStream_t s) {
   if (R % 8 || C % 8 || R <= 0 || C <= 0) return (int)hipErrorInvalidValue;
   dim3 grid((C + RT - 1) / RT, (R + RT - 1) / RT);

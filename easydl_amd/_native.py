@@ -73,6 +73,7 @@ _KERNEL_SIGS = {
                      c_float, c_void_p],
     "edl_attn_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                      c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_void_p],
+    "edl_transpose_bf16_multi": [c_void_p, c_int, c_int, c_void_p],
     "edl_attn_fwd_strided": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int,
                              c_int, c_float, c_i64, c_i64, c_void_p],
     "edl_attn_bwd_strided": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,

@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import math
 import os
+import weakref
 
 import torch
 import torch.nn.functional as F
@@ -221,6 +222,45 @@ def cross_entropy(logits, labels, ignore_index: int = -100):
 _WT_GEN = [0]
 _WT_ON = os.environ.get("EDL_WT_CACHE", "1") != "0"
 _WT_BUDGET: list = [None]   # bytes the transposed copies may still take (set at first use)
+# Batched refresh: at the first use of a new generation every stale cached copy on that device is
+# re-transposed in ONE launch (edl_transpose_bf16_multi) instead of one small launch per weight at
+# its first use (a BERT-large weight is 64-256 tiles: 9.4 us per 1024 x 1024 transpose alone).
+# EDL_WT_BATCH=0: per-weight refresh.
+_WT_BATCH = os.environ.get("EDL_WT_BATCH", "1") != "0"
+_WT_ALL: list = []            # weakrefs of every weight holding a cached copy
+_WT_DESC: dict = {}           # device -> (key, device descriptor tensor, tiles)
+
+
+def _refresh_stale_wt(w: torch.Tensor) -> bool:
+    """Re-transpose every stale cached copy on w's device in one launch; False when only w is
+    stale (the caller's single transpose is as good)."""
+    gen, live, stale = _WT_GEN[0], [], []
+    for ref in _WT_ALL:
+        t = ref()
+        if t is None:
+            continue
+        live.append(ref)
+        if t.device == w.device and t._edl_wt_gen != gen:
+            stale.append(t)
+    _WT_ALL[:] = live
+    if len(stale) <= 1:
+        return False
+    key = tuple((t.data_ptr(), t._edl_wt.data_ptr(), t.shape[0], t.shape[1]) for t in stale)
+    ent = _WT_DESC.get(w.device)
+    if ent is None or ent[0] != key:
+        rows, tiles = [], 0
+        for t in stale:
+            R, C = t.shape
+            tx = (C + 127) // 128
+            rows.append([t.data_ptr(), t._edl_wt.data_ptr(), (R << 32) | C, (tiles << 32) | tx])
+            tiles += tx * ((R + 127) // 128)
+        ent = (key, torch.tensor(rows, dtype=torch.int64).to(w.device), tiles)
+        _WT_DESC[w.device] = ent
+    _native.kernels().check("edl_transpose_bf16_multi", ent[1].data_ptr(), len(stale), ent[2],
+                            _native.stream_of(w))
+    for t in stale:
+        t._edl_wt_gen = gen
+    return True
 
 
 def new_weight_generation() -> None:
@@ -248,7 +288,8 @@ def _wt_of(w: torch.Tensor):
         wt = torch.empty(w.shape[1], w.shape[0], dtype=w.dtype, device=w.device)
         w._edl_wt = wt
         w._edl_wt_gen = -1
-    if w._edl_wt_gen != _WT_GEN[0]:
+        _WT_ALL.append(weakref.ref(w))
+    if w._edl_wt_gen != _WT_GEN[0] and not (_WT_BATCH and _refresh_stale_wt(w)):
         _native.kernels().check("edl_transpose_bf16", w.data_ptr(), wt.data_ptr(), w.shape[0], w.shape[1],
                                 _native.stream_of(w))
         w._edl_wt_gen = _WT_GEN[0]

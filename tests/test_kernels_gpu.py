@@ -501,6 +501,27 @@ def test_colsum_block_widths(cuda, G, C, odt, acc):
     torch.testing.assert_close(out.float(), want, rtol=1e-4 if odt else 1e-2, atol=tol)
 
 
+def test_wt_cache_batched_refresh(cuda, monkeypatch):
+    """The cached transposed weights of a new generation are refreshed together in one
+    edl_transpose_bf16_multi launch (ragged tile counts, rows/cols not multiples of 128)
+    and equal the transposes of the mutated weights; the per-weight path agrees."""
+    monkeypatch.setattr(fused, "_WT_ALL", [])
+    monkeypatch.setattr(fused, "_WT_DESC", {})
+    ws = [torch.randn(r, c, device=cuda).bfloat16() for r, c in ((384, 512), (1000, 24), (256, 1032), (8, 8))]
+    fused.new_weight_generation()
+    for w in ws:
+        torch.testing.assert_close(fused._wt_of(w), w.t(), rtol=0, atol=0)
+    for batch in (True, False):
+        monkeypatch.setattr(fused, "_WT_BATCH", batch)
+        for w in ws:
+            w.mul_(-2).add_(1)   # parameter mutation between steps
+        fused.new_weight_generation()
+        fused._wt_of(ws[1])      # first use: every stale copy refreshed (one launch when batched)
+        assert all(w._edl_wt_gen == fused._WT_GEN[0] for w in ws) == batch
+        for w in ws:
+            torch.testing.assert_close(fused._wt_of(w), w.t(), rtol=0, atol=0)
+
+
 @pytest.mark.parametrize("tn", ["0", "1"])
 def test_linear_bias_wgrad_tn_and_nt_match_fp32(cuda, tn, monkeypatch):
     """A biased linear layer's weight / bias gradients through the TN kernel (no transposes)
