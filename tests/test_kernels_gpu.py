@@ -457,7 +457,8 @@ def test_bert_layer_residual_grad_slots_match_fp32(cuda, flat, monkeypatch):
 
 
 @pytest.mark.parametrize("M,N,J", [(1000, 128, 256), (2048, 1024, 1024), (4096, 256, 512), (96, 384, 768),
-                                   (16384, 128, 256), (1000, 4096, 4096), (160, 8192, 2048)])
+                                   (16384, 128, 256), (1000, 4096, 4096), (160, 8192, 2048),
+                                   (8192, 1024, 1024)])
 @pytest.mark.parametrize("out_dt", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("acc", [False, True])
 def test_gemm_tn_matches_fp32(cuda, M, N, J, out_dt, acc):
