@@ -46,6 +46,9 @@ def parse():
     ap.add_argument("--mbs", type=int, default=2, help="sequences per micro-batch per GPU")
     ap.add_argument("--accum", type=int, default=4, help="micro-batches per step per GPU")
     ap.add_argument("--bucket-mb", type=float, default=None)
+    ap.add_argument("--grad-dtype", default=os.environ.get("EDL_GRAD_DTYPE", "bf16"), choices=["bf16", "fp32"],
+                    help="gradient accumulation + all-reduce dtype (flat gradient buffers); see "
+                         "docs/env_contract.md for the measured trade-off")
     ap.add_argument("--layers", type=int, default=None,
                     help="override layer count (debug only; invalid for the metric)")
     ap.add_argument("--out", default=None)
@@ -59,9 +62,11 @@ def parse():
     ap.add_argument("--fault-step", type=int, default=None, help="--fault-inject: step at which the worker dies")
     ap.add_argument("--standby", type=int, default=1,
                     help="--fault-inject: warm spare workers kept by the operator (0 = cold respawn)")
-    ap.add_argument("--comm", default=None, choices=["pg", "native", "xgmi", "auto", "xgmi-only"],
-                    help="gradient all-reduce data plane (default $EDL_COMM or pg = ProcessGroupNCCL/RCCL; "
-                         "xgmi = hand-written IPC all-reduce; auto = probe both at each epoch, keep the faster)")
+    ap.add_argument("--comm", default=None, choices=["pg", "native", "xgmi", "auto", "xgmi-only", "auto-gloo"],
+                    help="gradient all-reduce data plane (default $EDL_COMM or auto = RCCL + the hand-written xGMI "
+                         "engine, per-size policy probed once per (group, world) and cached; pg = ProcessGroupNCCL "
+                         "(RCCL) only; xgmi = engine for every all-reduce; native = csrc RCCL manager; "
+                         "auto-gloo = auto with gloo standing in for RCCL (ranks sharing one GPU: tests, drills)")
     ap.add_argument("--sp", action="store_true", help="Megatron sequence parallelism inside the TP group")
     ap.add_argument("--tp", type=int, default=1,
                     help="tensor-parallel degree inside each DP replica (BASELINE config 5: --model llama3-70b --tp 8)")
@@ -86,7 +91,7 @@ def main():
     dev = torch.device("cuda", 0 if args.share_gpu else local) if use_cuda else torch.device("cpu")
     if args.share_gpu and use_cuda:
         # every rank on GPU 0, the xGMI engine as the only data plane (test / fault drills
-        # on a one-GPU box; not the headline configuration)
+        # on a one-GPU box; not the headline configuration); --comm auto-gloo overrides
         os.environ["EDL_COMM"] = "xgmi-only"
         os.environ.setdefault("EDL_XGMI_MAX_BLOCKS", "16")   # co-residency of all ranks' grids
     os.environ.setdefault("EDL_JOB", "bench")
@@ -121,7 +126,8 @@ def main():
         model_fn = lambda d: Llama(cfg, device=d, dtype=dtype)  # noqa: E731
     tr = ElasticTrainer(model_fn, lr=3e-4, betas=(0.9, 0.95), weight_decay=0.1,
                         max_grad_norm=1.0, global_batch=gb, micro_batch=B, device=dev, bucket_mb=args.bucket_mb,
-                        checkpoint=ckpt, tp=tp)
+                        checkpoint=ckpt, tp=tp,
+                        grad_dtype=torch.float32 if (args.grad_dtype == "fp32" or not use_cuda) else torch.bfloat16)
     marks = {}
 
     def sync_barrier(t):
@@ -181,6 +187,7 @@ def main():
             "micro_batch": B,
             "grad_accum": args.accum,
             "optimizer": "AdamW fp32 master/moments, clip 1.0",
+            "grad_dtype": str(tr.flat.grad_dtype).replace("torch.", "") if tr.flat is not None else args.grad_dtype,
             "bucket_mb": tr.ddp.bucket_mb,
             "comm": getattr(getattr(comm, "dp", comm), "backend", "local"),
             "gemm_tuning": getattr(tr, "gemm_tuning", "off"),

@@ -276,6 +276,9 @@ int edl_shm_close(void* h, int unlink_seg) {
 
 int edl_shm_unlink(const char* name) { return shm_unlink(name) == 0 ? 0 : -errno; }
 
+// the segment's file descriptor (identity checks: does a /dev/shm name still refer to it?)
+int edl_shm_fd(void* h) { return h ? static_cast<Seg*>(h)->fd : -1; }
+
 // Re-use an already mapped (and page-locked) segment for another shard layout
 // after a world change: invalidate both slots FIRST (no reader may take the old
 // layout's bytes for the new name), then atomically rename the /dev/shm file

@@ -38,6 +38,7 @@ SIGS = {
     "edl_shm_slot_info": (i32, [vp, i32, i64p, i64p, u64p, u64p, cp, i32]),
     "edl_shm_close": (i32, [vp, i32]),
     "edl_shm_unlink": (i32, [cp]),
+    "edl_shm_fd": (i32, [vp]),
     "edl_shm_reassign": (i32, [vp, cp]),
     "edl_shm_relink": (i32, [vp, cp]),
     "edl_ckpt_engine_create": (vp, [i32, u64, i32]),

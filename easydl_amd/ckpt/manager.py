@@ -342,6 +342,14 @@ class CheckpointManager:
         self._old_name = None
         if old:
             try:
+                # only if the name still refers to THIS segment: after a shard permutation
+                # another rank's relink may have taken the name for its own live segment
+                fd = self._seg.rt("edl_shm_fd", self._seg.h) if self._seg is not None else -1
+                mine = os.fstat(fd) if fd >= 0 else None
+                st = os.stat("/dev/shm" + old)
+                if mine is not None and (st.st_ino, st.st_dev) != (mine.st_ino, mine.st_dev):
+                    log.info("snapshot name %s now belongs to another segment: kept", old)
+                    return
                 os.unlink("/dev/shm" + old)
             except OSError:
                 pass
@@ -375,7 +383,9 @@ class CheckpointManager:
         else:
             want = 2
         agree = getattr(comm, "ctrl_all_reduce", None)
-        agreed = int(agree([float(want)], _MAX)[0]) if comm.world_size > 1 and agree is not None else want
+        # unsharded snapshots are rank 0's alone: nothing to agree with the others
+        group = self.sharded and comm.world_size > 1 and agree is not None
+        agreed = int(agree([float(want)], _MAX)[0]) if group else want
         self.mode = ("full", "lean", "off")[agreed]
         self._mode_key = key
         self.stats["mode"] = self.mode
@@ -389,24 +399,50 @@ class CheckpointManager:
     def on_step(self, trainer) -> None:
         if trainer.step % self.interval:
             return
-        self.snapshot(trainer)
+        try:
+            self.snapshot(trainer)
+        except Exception as e:  # noqa: BLE001
+            # a peer died inside the (first-of-layout) mode agreement: no snapshot this
+            # step; the broken epoch is handed to the trainer's reconfiguration path
+            comm = self._comm(trainer)
+            from easydl_amd.parallel.comm import CommAborted
+            if not isinstance(e, (CommAborted, RuntimeError)) or not (
+                    getattr(comm, "aborted", False) or isinstance(e, CommAborted) or _comm_error(e)):
+                raise
+            log.warning("snapshot of step %d skipped: %s", trainer.step, e)
+            self.stats["skipped_comm"] = self.stats.get("skipped_comm", 0) + 1
+            if hasattr(comm, "abort"):
+                comm.abort()
 
-    def snapshot(self, trainer) -> None:
+    def _plan(self, trainer):
         comm = self._comm(trainer)
         tag = self._tag(trainer)
         world = comm.world_size if self.sharded else 1
         shard = comm.rank if self.sharded else 0
-        if not self.sharded and comm.rank != 0:
-            return
         state = self.state_of(trainer)
         layout, cs_off = shard_layout(state, shard, world)
         moments = self._moment_names(trainer)
         lean_state = [(n, t) for n, t in state if n not in moments]
         headroom = lambda st: (max(shard_layout(st, s, world - 1)[1] for s in range(world - 1)) + 8  # noqa: E731
                                if world > 1 else 0)
-        mode = self._decide_mode(trainer, comm, (world, shard, tag),
-                                 max(cs_off + 8, headroom(state)),
-                                 max(shard_layout(lean_state, shard, world)[1] + 8, headroom(lean_state)))
+        key = (world, shard, tag)
+        sizes = (max(cs_off + 8, headroom(state)),
+                 max(shard_layout(lean_state, shard, world)[1] + 8, headroom(lean_state)))
+        return comm, tag, world, shard, state, layout, cs_off, lean_state, headroom, key, sizes
+
+    def prepare_layout(self, trainer) -> str | None:
+        """Agree on this layout's full / lean / off mode now (the trainer calls it while
+        entering an epoch, inside its failure handling), so no snapshot runs a collective."""
+        comm, _, _, _, _, _, _, _, _, key, sizes = self._plan(trainer)
+        if not self.sharded and comm.rank != 0:
+            return None
+        return self._decide_mode(trainer, comm, key, *sizes)
+
+    def snapshot(self, trainer) -> None:
+        comm, tag, world, shard, state, layout, cs_off, lean_state, headroom, key, sizes = self._plan(trainer)
+        if not self.sharded and comm.rank != 0:
+            return
+        mode = self._decide_mode(trainer, comm, key, *sizes)
         if mode == "off":
             self.stats["skipped_host"] = self.stats.get("skipped_host", 0) + 1
             return
@@ -776,3 +812,8 @@ def unlink_job_segments(job: str) -> int:
         except OSError:
             pass
     return n
+
+
+def _comm_error(e: Exception) -> bool:
+    s = str(e).lower()
+    return any(k in s for k in ("nccl", "rccl", "gloo", "connection", "socket", "peer", "aborted", "timed out"))

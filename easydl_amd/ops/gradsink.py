@@ -87,6 +87,14 @@ def input_grad_mm(dy2: torch.Tensor, w: torch.Tensor, slot: "ResidualGrad | None
     r2 = r.view(dy2.shape[0], w.shape[1])
     if r2.dtype != dy2.dtype or not r2.is_contiguous():
         return (torch.mm(dy2, w) + r2).view(*shape)
+    if r2.is_cuda:
+        # the parked tensor is also the gradient another GEMM's weight gradient reads; if that
+        # GEMM runs on the side stream (EDL_WGRAD_STREAM / wgrad_side), the in-place update
+        # below must not overtake it: order this stream after the side stream's queued work
+        from easydl_amd.ops import fused
+        side = fused._SIDE.get(fused._dev_index(r2.device))
+        if side is not None and side != torch.cuda.current_stream(r2.device):
+            torch.cuda.current_stream(r2.device).wait_stream(side)
     r2.addmm_(dy2, w)
     return r2.view(*shape)
 
@@ -100,7 +108,15 @@ def write_mm(p: torch.Tensor, a: torch.Tensor, b: torch.Tensor) -> None:
             torch.mm(a, b, out=tgt2)
         else:
             tgt2.addmm_(a, b)
-    else:  # e.g. fp32 gradient buffer with bf16 activations
+    elif (a.is_cuda and tgt.dtype == torch.float32 and a.dtype == b.dtype == torch.bfloat16
+          and tgt2.is_contiguous()):
+        # fp32 gradient buffer (grad_dtype=fp32) with bf16 operands: hipBLASLt's bf16 x bf16
+        # -> fp32 GEMM writes / accumulates (beta = 1) straight into it, no temporary
+        if is_fresh(p):
+            torch.ops.aten.mm.dtype_out(a, b, torch.float32, out=tgt2)
+        else:
+            torch.ops.aten.addmm.dtype_out(tgt2, a, b, torch.float32, out=tgt2)
+    else:  # e.g. fp32 gradient buffer with bf16 activations on the CPU
         r = torch.mm(a, b)
         if is_fresh(p):
             tgt2.copy_(r)

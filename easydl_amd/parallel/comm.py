@@ -51,7 +51,7 @@ class Communicator:
     def __init__(self, store: dist.Store, rank: int, world_size: int, epoch: int, *, device: torch.device,
                  job: str = "job", timeout_s: float = 120.0, control_timeout_s: float = 30.0,
                  high_priority: bool = True, tag: str = "", data: bool = True, data_backend: str | None = None,
-                 xgmi_factory=None):
+                 xgmi_factory=None, probe: str = "now"):
         self.rank = rank
         self.world_size = world_size
         self.epoch = epoch
@@ -62,6 +62,14 @@ class Communicator:
         self.xgmi_mode = None
         self.xgmi_probe: dict | None = None
         self.allreduce_policy: dict | None = None
+        # "auto" all-reduce policy source (see warmup()): "now" probes inside warmup() unless a
+        # policy for this (group, world) is cached; "defer" (re-formations: the recovery
+        # critical path) never probes there -- RCCL only until run_deferred_probe() after the
+        # epoch's first committed step, or a cached / Brain policy adopted at once
+        self.probe_mode = probe
+        self.probe_pending = False
+        self.group = "".join(ch for ch in tag if not ch.isdigit()) or "dp"
+        self._root_store, self._job = store, job
         self._aborted = False
         self._lock = threading.Lock()
         # debug: verify every rank issues the same collective sequence (the classic
@@ -76,15 +84,20 @@ class Communicator:
         data_backend = data_backend or os.environ.get("EDL_COMM", "auto")
         self.xgmi_min_bytes = 0         # all-reduces (in place, registered) at least this large -> engine
         self.xgmi_min_bytes_staged = 0  # ... and through the staging workspace
+        # "auto-gloo" (tests): the auto engine/probe path with gloo on GPU tensors standing in
+        # for RCCL, so several ranks can share one GPU (RCCL refuses duplicate devices)
+        self.data_kind = "rccl"
+        if data_backend == "auto-gloo":
+            data_backend, self.data_kind = "auto", "gloo"
         if not data:
             self.data = None
-            self.backend = "none"
+            self.backend = self.data_kind = "none"
         elif self.device.type == "cuda" and data_backend == "native":
             # csrc/runtime/rccl_comm.cpp: non-blocking, abortable creation; own comm stream
             from easydl_amd.parallel.rccl import RcclComm
             self.data = None
             self.rccl = RcclComm(base, "data", rank, world_size, self.device, timeout_s=timeout_s)
-            self.backend = "rccl-native"
+            self.backend = self.data_kind = "rccl-native"
         elif self.device.type == "cuda" and data_backend == "xgmi-only":
             # the hand-written engine is the ONLY data plane (no RCCL communicator): several
             # ranks may then share one GPU (RCCL refuses duplicate devices), e.g. to exercise
@@ -95,7 +108,7 @@ class Communicator:
             self.xgmi = XgmiComm(dist.PrefixStore("xgmi", base), "ws", rank, world_size, self.device,
                                  timeout_s=timeout_s)
             self.xgmi_mode = "xgmi"
-            self.backend = "xgmi"
+            self.backend = self.data_kind = "xgmi"
         elif self.device.type == "cuda":
             if data_backend in ("xgmi", "auto") and world_size > 1:
                 # csrc/kernels/xgmi.hip: abortable direct all-reduce over IPC-mapped peer
@@ -114,14 +127,18 @@ class Communicator:
                     log.warning("xGMI engine unavailable (%s); RCCL only", e)
                     self.xgmi_probe = {"selected": "rccl", "error": str(e)[:200]}
                     self.xgmi = None
-            opts = dist.ProcessGroupNCCL.Options()
-            opts.is_high_priority_stream = high_priority
-            opts._timeout = _td(timeout_s)
-            self.data = dist.ProcessGroupNCCL(dist.PrefixStore("data", base), rank, world_size, opts)
-            self.backend = "rccl+xgmi" if self.xgmi_mode == "xgmi" else "rccl"
+            if self.data_kind == "gloo":
+                self.data = dist.ProcessGroupGloo(dist.PrefixStore("data", base), rank, world_size, _td(timeout_s))
+            else:
+                opts = dist.ProcessGroupNCCL.Options()
+                opts.is_high_priority_stream = high_priority
+                opts._timeout = _td(timeout_s)
+                self.data = dist.ProcessGroupNCCL(dist.PrefixStore("data", base), rank, world_size, opts)
+            self.backend = self.data_kind + ("+xgmi" if self.xgmi_mode == "xgmi" else "")
         else:
             self.data = dist.ProcessGroupGloo(dist.PrefixStore("data", base), rank, world_size, _td(timeout_s))
             self.backend = "gloo"
+            self.data_kind = "gloo"
         self.init_s = time.perf_counter() - t0
 
     # -- lifecycle -----------------------------------------------------------
@@ -148,8 +165,96 @@ class Communicator:
                 self._sync_stream()
         self.ctrl.allreduce([torch.zeros(1)]).wait()
         if self.xgmi is not None and self.xgmi_mode == "auto":
-            self._probe_xgmi()
+            self._select_policy()
         return time.perf_counter() - t0
+
+    # -- all-reduce policy: cache, probe, deferral ------------------------------------
+    def _policy_key(self) -> str:
+        """Cache key of the agreed policy: one per (job, group, world size, ranks per GPU)
+        -- the probe's answer depends on nothing else that a re-formation can change."""
+        rpd = int(getattr(self.xgmi, "ranks_per_device", 1) or 1)
+        return f"edl/{self._job}/commpolicy/{self.group}/w{self.world_size}/rpd{rpd}"
+
+    def _cached_policy(self) -> dict | None:
+        """The cached probe document, if EVERY rank read the same one (agreed over the
+        control plane by its checksum), else None."""
+        import json
+        import zlib
+        doc, raw = None, b""
+        try:
+            if self._root_store.check([self._policy_key()]):
+                raw = self._root_store.get(self._policy_key())
+                doc = json.loads(raw.decode())
+        except Exception as e:  # noqa: BLE001 - a broken cache entry means "probe"
+            log.debug("policy cache read failed: %s", e)
+            doc, raw = None, b""
+        crc = float(zlib.crc32(raw) if doc else -1)
+        v = self.ctrl_all_reduce([crc, -crc], dist.ReduceOp.MAX)
+        return doc if (doc is not None and v[0] == -v[1] and v[0] >= 0) else None
+
+    def _store_policy(self) -> None:
+        import json
+        if self.rank == 0 and self.xgmi_probe and self.xgmi_probe.get("exact_everywhere") is not None \
+                and "error" not in self.xgmi_probe:
+            try:
+                self._root_store.set(self._policy_key(), json.dumps(self.xgmi_probe))
+            except Exception as e:  # noqa: BLE001 - the cache is an optimisation
+                log.debug("policy cache write failed: %s", e)
+
+    def _select_policy(self) -> None:
+        """warmup() in "auto": adopt the cached policy of this (group, world) if every rank
+        has it; otherwise probe now (a job's first epoch) or defer the probe until after
+        the epoch's first committed step (re-formations: the probe is ~1 s of collectives
+        that would otherwise sit between a fault and the first recovered step)."""
+        cached = self._cached_policy()
+        if cached is not None:
+            self._adopt_probe(dict(cached, cached=True, epoch=self.epoch, measured_epoch=cached.get("epoch")))
+            return
+        if self.probe_mode == "defer":
+            self.probe_pending = True     # RCCL only until run_deferred_probe() / adopt_policy()
+            return
+        self._probe_xgmi()
+        self._store_policy()
+
+    def run_deferred_probe(self) -> float:
+        """The deferred probe, at an agreed point (every rank after the same committed
+        step).  Returns its seconds; the caller re-registers its gradient buffers if the
+        engine was kept."""
+        if not self.probe_pending or self.xgmi is None or self.xgmi_mode != "auto":
+            self.probe_pending = False
+            return 0.0
+        t0 = time.perf_counter()
+        self.probe_pending = False
+        self._probe_xgmi()
+        self._store_policy()
+        return time.perf_counter() - t0
+
+    def adopt_policy(self, pol: dict) -> bool:
+        """A policy for this world size from elsewhere (the Brain's median of earlier
+        epochs' probes) replaces a pending probe.  Agreed by the caller (every rank adopts
+        the same runtime plan at the same point)."""
+        if self.xgmi is None or self.xgmi_mode != "auto" or not self.probe_pending:
+            return self.apply_allreduce_policy(pol)
+        self.probe_pending = False
+        self._adopt_probe({"epoch": self.epoch, "world": self.world_size, "exact_everywhere": True, "policy": pol,
+                           "source": "brain"})
+        return self.xgmi is not None
+
+    def _adopt_probe(self, probe: dict) -> None:
+        pol = probe.get("policy") or {}
+        keep = bool(probe.get("exact_everywhere")) and (pol.get("xgmi_min_kb_inplace") is not None
+                                                        or pol.get("xgmi_min_kb_staged") is not None)
+        probe["selected"] = "xgmi" if keep else "rccl"
+        self.xgmi_probe = probe
+        if keep:
+            self.xgmi_mode = "xgmi"
+            self.backend = self.data_kind + "+xgmi"
+            self.apply_allreduce_policy(pol)
+        else:
+            self._sync_stream()
+            self.xgmi.close()
+            self.xgmi = None
+            self.xgmi_mode = None
 
     PROBE_KB = (256, 1024, 4096, 32768, 131072)
     ONESHOT_PROBE_KB = 4096     # one-shot is timed up to this size (it reads N x S per rank)
@@ -158,11 +263,15 @@ class Communicator:
         """Measure the xGMI engine against RCCL on THIS node from latency-bound to
         gradient-bucket sizes, in each of its forms (one-shot; two-shot in place on a
         registered buffer; two-shot staged through the workspace for buffers too large
-        to map), on integer-valued data so every sum is exact.  The engine is kept only
-        if every rank saw an exact result; the policy (one-shot switch sizes, the size
-        from which each form beats RCCL) comes from :func:`comm_policy.decide` on the
-        per-size MAX over ranks, so every rank derives the same policy."""
+        to map), on integer-valued data so every sum is exact.  The engine is timed in
+        the form training runs it: ``all_reduce_async`` on its own stream with
+        ``async_blocks`` workgroups (what ElasticDDP's bucket all-reduces use under the
+        backward), not the full-chip synchronous grid.  The engine is kept only if every
+        rank saw an exact result; the policy (one-shot switch sizes, the size from which
+        each form beats RCCL) comes from :func:`comm_policy.decide` on the per-size MAX
+        over ranks, so every rank derives the same policy."""
         from easydl_amd.parallel import comm_policy
+        t_probe = time.perf_counter()
         sizes_kb = tuple(int(m * 1024) for m in sizes_mb) if sizes_mb else self.PROBE_KB
         nel = (max(sizes_kb) << 10) // 2
         g = torch.Generator(device="cpu").manual_seed(7 + self.rank)
@@ -170,6 +279,7 @@ class Communicator:
         a, b = src.clone(), src.clone()
         reg = None
         keep_timeout, self.xgmi.timeout_s = self.xgmi.timeout_s, 5.0  # a broken path gives up fast
+        blocks = getattr(self.xgmi, "async_blocks", None)
         # every decision point is agreed over the control plane, so a rank whose engine
         # fails locally never leaves its peers waiting inside a data-plane collective
         try:
@@ -179,10 +289,19 @@ class Communicator:
             log.warning("xGMI probe: registration failed: %s", e)
             bad = 1.0
         bad = float(self.ctrl_all_reduce([bad], dist.ReduceOp.MAX)[0])
+
+        def engine(algo):   # the training form: async on the engine stream, caller waits on its event
+            def run(t):
+                w = self.xgmi.all_reduce_async(t, algo) if blocks is not None else None
+                if w is None:
+                    self.xgmi.all_reduce(t, algo)
+                else:
+                    w.wait()
+            return run
         if not bad:
             try:
                 self.data.allreduce([a]).wait()
-                self.xgmi.all_reduce(b)
+                engine(None)(b)
                 self._sync_stream()
                 bad = 0.0 if (torch.equal(a, b) and self.xgmi.status() == 0) else 1.0
             except Exception as e:  # noqa: BLE001
@@ -203,9 +322,7 @@ class Communicator:
                 return (time.perf_counter() - t0) / it
 
             forms = (lambda t: self.data.allreduce([t]).wait(),
-                     lambda t: self.xgmi.all_reduce(t, "inplace"),
-                     lambda t: self.xgmi.all_reduce(t, "twoshot"),
-                     lambda t: self.xgmi.all_reduce(t, "oneshot"))
+                     engine("inplace"), engine("twoshot"), engine("oneshot"))
             for i, kb in enumerate(sizes_kb):
                 view = b[:(kb << 10) // 2]
                 it = iters if kb > 1024 else 4 * iters      # latency-bound sizes: more samples
@@ -253,20 +370,15 @@ class Communicator:
             "rccl_busbw_gbs": bw(cols[0]), "xgmi_inplace_busbw_gbs": bw(cols[1]), "xgmi_staged_busbw_gbs": bw(cols[2]),
             "exact_everywhere": bool(exact), "policy": pol,
             "xgmi_min_mb_inplace": mb(pol["xgmi_min_kb_inplace"]), "xgmi_min_mb_staged": mb(pol["xgmi_min_kb_staged"]),
+            # the engine configuration that was timed (= the one DDP buckets run)
+            "engine_form": "async" if blocks is not None else "sync", "engine_blocks": blocks,
+            "data_plane": self.data_kind, "probe_s": round(time.perf_counter() - t_probe, 4),
             "selected": "xgmi" if keep else "rccl"}
         log.info("all-reduce probe (epoch %d, world %d): %s", self.epoch, self.world_size, self.xgmi_probe)
         if reg is not None:
             self._sync_stream()
             self.xgmi.unregister(reg)
-        if keep:
-            self.xgmi_mode = "xgmi"
-            self.backend = "rccl+xgmi"
-            self.apply_allreduce_policy(pol)
-        else:
-            self._sync_stream()
-            self.xgmi.close()
-            self.xgmi = None
-            self.xgmi_mode = None
+        self._adopt_probe(self.xgmi_probe)
 
     def apply_allreduce_policy(self, pol: dict) -> bool:
         """Switch the per-size routing (RCCL / engine form) to ``pol`` (see
@@ -296,6 +408,8 @@ class Communicator:
             return
         from easydl_amd.parallel.xgmi import XgmiError
         for t in tensors:   # sizes are equal on every rank, so every rank skips the same ones
+            if self.xgmi._find_registered(t)[0] is not None:
+                continue    # already mapped this epoch (re-binding after a policy switch)
             if self.xgmi.supports(t) and self.xgmi.registrable(t):
                 try:
                     self.xgmi.register(t)
@@ -358,7 +472,7 @@ class Communicator:
             return
         if not ops:
             return
-        if self.backend.startswith("rccl") and hasattr(self.data, "_start_coalescing"):
+        if self.data_kind == "rccl" and hasattr(self.data, "_start_coalescing"):
             self.data._start_coalescing(self.device)
             for kind, t, peer, tag in ops:
                 (self.data.send if kind == "send" else self.data.recv)([t], peer, tag)
@@ -388,7 +502,7 @@ class Communicator:
             self.xgmi.abort()  # host-mapped abort word: spinning workgroups exit
         if self.rccl is not None:
             self.rccl.abort()
-        elif self.backend.startswith("rccl"):
+        elif self.data_kind == "rccl":
             try:
                 self.data.abort()
             except Exception as e:  # pragma: no cover - best effort
@@ -572,7 +686,7 @@ class Communicator:
         # poll only for collectives whose gloo work progresses on its own thread
         # (allreduce / broadcast / allgather); gloo's _reduce_scatter_base runs inside
         # wait() and would never report completion to a poller
-        if poll and self.backend == "gloo":
+        if poll and self.data_kind == "gloo":
             # gloo collectives cannot be aborted; a rank blocked on a dead peer would sit in
             # wait() until gloo's own error path unwinds the ring (~1.5 s measured).  Poll
             # instead, so the watchdog's abort() releases this rank at once (the abandoned

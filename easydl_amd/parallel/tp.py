@@ -33,8 +33,9 @@ from __future__ import annotations
 import os
 
 import torch
-import torch.nn as nn
 import torch.distributed as dist
+import torch.nn as nn
+import torch.utils.checkpoint as _ckpt
 
 from easydl_amd.models.llama import Llama, LlamaBlock, LlamaConfig, _param
 from easydl_amd.ops import fused, norms
@@ -322,7 +323,12 @@ class LlamaTP(nn.Module):
         x = scatter_to_sp(x, self.g) if sp else reduce_from_tp(x, self.g)
         resid, delta = x, None
         for layer in self.layers:
-            resid, delta = layer(resid, delta, B, S, cos, sin)
+            if self.cfg.recompute and self.training:
+                # activation recompute (the 80-layer 70B shard at 8k tokens: profiles/r04_tp_dryrun_*);
+                # the re-run forward repeats the block's TP collectives, as in Megatron
+                resid, delta = _ckpt.checkpoint(layer, resid, delta, B, S, cos, sin, use_reentrant=False)
+            else:
+                resid, delta = layer(resid, delta, B, S, cos, sin)
         n, _ = norms.add_rmsnorm(delta, resid, self.norm, self.cfg.norm_eps)
         if self.overlap:
             logits = fused.linear(n, self.lm_head, dx_reduce=self.g.all_reduce_start)

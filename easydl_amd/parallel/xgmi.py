@@ -105,7 +105,12 @@ class XgmiComm:
         store.set(f"{prefix}/ipc/{rank}", mine.raw + uuid)
         entries = [mine.raw + uuid if p == rank else store.get(f"{prefix}/ipc/{p}") for p in range(world)]
         allh = b"".join(e[:128] for e in entries)
-        self.ranks_per_device = sum(1 for e in entries if e[128:] == uuid)
+        # the most ranks any one GPU carries (every rank sees the same records): the grid cap
+        # below must be identical on every rank, since workgroup b meets workgroup b of each peer
+        per_uuid: dict[bytes, int] = {}
+        for e in entries:
+            per_uuid[e[128:]] = per_uuid.get(e[128:], 0) + 1
+        self.ranks_per_device = max(per_uuid.values())
         rc = self._rt("edl_xgmi_ws_open", h, world, rank, allh)
         if rc != 0:
             raise XgmiError(f"hipIpcOpenMemHandle failed: hipError {rc}")
@@ -417,14 +422,15 @@ class XgmiComm:
             self._launch(2, src[lo:].data_ptr(), dst[lo:].data_ptr(), m * es // 16, stride, out.dtype, m * es // 16)
         return out
 
-    def all_reduce_async(self, t: torch.Tensor) -> "_Work":
+    def all_reduce_async(self, t: torch.Tensor, algo: str | None = None) -> "_Work":
         """In-place SUM on the engine's own high-priority stream, ordered after the
         caller's stream; ``wait()`` orders the caller's stream after it (the
         ``ProcessGroupNCCL`` work contract ElasticDDP overlaps with backward).
-        Uses at most ``async_blocks`` workgroups so backward keeps most CUs."""
+        Uses at most ``async_blocks`` workgroups so backward keeps most CUs.
+        ``algo`` pins a form (the policy probe times each one in this configuration)."""
         self.stream.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(self.stream):
-            self._all_reduce(t, None, self.async_blocks)
+            self._all_reduce(t, algo, self.async_blocks)
         t.record_stream(self.stream)
         ev = torch.cuda.Event()
         ev.record(self.stream)

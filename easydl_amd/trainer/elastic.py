@@ -263,6 +263,10 @@ class ElasticTrainer:
                 self.dp_comm = self.comm
             try:
                 self._sync_state() if self.tp == 1 else self._sync_state_tp()
+                if self.checkpoint is not None and hasattr(self.checkpoint, "prepare_layout"):
+                    # snapshot mode (full / lean / off) of the new layout: agreed here, where a
+                    # dead peer means "skip this epoch", never inside a step's snapshot
+                    self.checkpoint.prepare_layout(self)
             except (CommAborted, RuntimeError) as e:
                 if self.rdzv is None or not (self.comm.aborted or self.rdzv.aborted(self.comm.epoch)
                                              or _is_comm_error(e)):
@@ -271,20 +275,23 @@ class ElasticTrainer:
                 self.comm.abort()
                 continue
             self.events.emit("state_transferred", epoch=self.comm.epoch, step=self.step)
-            self.ddp.set_comm(self.dp_comm)   # binds the epoch's comm (registers gradient buffers)
-            xg = getattr(self.dp_comm, "xgmi", None)
-            self.events.emit("state_synced", epoch=self.comm.epoch, step=self.step,
-                             grad_buffers_mapped=len(getattr(xg, "_registered", ())) if xg is not None else 0)
             if self.rdzv is not None:
                 try:
                     self._publish_probe()
-                    self._agree_runtime_plan()
+                    self._agree_runtime_plan()   # may adopt the Brain's policy for a deferred probe
                 except (CommAborted, RuntimeError) as e:
                     if not (self.comm.aborted or self.rdzv.aborted(self.comm.epoch) or _is_comm_error(e)):
                         raise
                     self.events.emit("epoch_skipped", epoch=self.comm.epoch, during="runtime_plan")
                     self.comm.abort()
                     continue
+            # binds the epoch's comm (registers the gradient buffers if the agreed policy routes
+            # them to the xGMI engine)
+            self.ddp.set_comm(self.dp_comm)
+            xg = getattr(self.dp_comm, "xgmi", None)
+            self.events.emit("state_synced", epoch=self.comm.epoch, step=self.step,
+                             grad_buffers_mapped=len(getattr(xg, "_registered", ())) if xg is not None else 0,
+                             probe_pending=[g for g, c in self._comm_groups() if getattr(c, "probe_pending", False)])
             return
 
     def _comm_groups(self):
@@ -300,10 +307,13 @@ class ElasticTrainer:
         for group, c in self._comm_groups():
             probe = getattr(c, "xgmi_probe", None)
             if probe and c.rank == 0:
-                doc = {"epoch": self.comm.epoch, "world": c.world_size, "group": group, "probe": probe}
-                self.kv.set(f"comm/probe/{group}", json.dumps(doc))
+                if not probe.get("cached") and probe.get("source") != "brain":   # new measurements only
+                    doc = {"epoch": self.comm.epoch, "world": c.world_size, "group": group, "probe": probe}
+                    self.kv.set(f"comm/probe/{group}", json.dumps(doc))
                 self.events.emit("allreduce_probe", epoch=self.comm.epoch, group=group, world=c.world_size,
-                                 selected=probe.get("selected"), policy=probe.get("policy"))
+                                 selected=probe.get("selected"), policy=probe.get("policy"),
+                                 cached=bool(probe.get("cached")), source=probe.get("source", "probe"),
+                                 probe_s=probe.get("probe_s"), engine_blocks=probe.get("engine_blocks"))
 
     def _agree_runtime_plan(self) -> None:
         """Every rank of the new epoch switches to the same runtime plan: the highest plan
@@ -332,11 +342,16 @@ class ElasticTrainer:
 
         def build():
             try:
+                # a job's first epoch may measure the all-reduce policy; every later epoch
+                # (shrink, rejoin, scale-up) is on the recovery critical path: cached policy or
+                # RCCL until the deferred probe after its first committed step
+                probe = "now" if a.reason == "initial" else "defer"
                 if self.tp > 1:
                     c = build_mesh(self._store, a.rank, a.world, a.epoch, self.tp, device=self.device,
-                                   job=self.ctx.job)
+                                   job=self.ctx.job, probe=probe)
                 else:
-                    c = Communicator(self._store, a.rank, a.world, a.epoch, device=self.device, job=self.ctx.job)
+                    c = Communicator(self._store, a.rank, a.world, a.epoch, device=self.device, job=self.ctx.job,
+                                     probe=probe)
                 c.warmup()
                 box["comm"] = c
             except Exception as e:  # noqa: BLE001 - reported through box
@@ -434,11 +449,17 @@ class ElasticTrainer:
         self.ckpt_tag = f"-t{t}of{self.tp}"
         if max_step >= 0 and all_ok:
             if c.dp.world_size > 1 and int(c.dp.ctrl_all_reduce([1 - mine_ok], dist.ReduceOp.MAX)[0]):
-                src = int(c.dp.ctrl_all_reduce([c.dp.rank if mine_ok else 1 << 30], dist.ReduceOp.MIN)[0])
+                # every DP-group member holding this shard at the newest step sends a slice
+                # (multi-source): the replacement's inbound traffic is spread over
+                # one link per holder instead of one source's single link
+                onehot = [0.0] * c.dp.world_size
+                onehot[c.dp.rank] = float(mine_ok)
+                holders = [r for r, v in enumerate(c.dp.ctrl_all_reduce(onehot, dist.ReduceOp.MAX).tolist())
+                           if v > 0]
+                src = holders[0]
                 t0 = time.time()
                 self._fence_snapshot_before_overwrite(c.dp, src, bool(mine_ok))
-                for ten in self._state_tensors():
-                    c.dp.broadcast(ten, src)
+                c.dp.transfer_state(self._state_tensors(), holders)
                 scal = c.dp.ctrl_broadcast([self.step, self.opt.step_count,
                                             getattr(self.opt, "moment_origin", 0)], src)
                 self.step, self.opt.step_count = int(scal[0]), int(scal[1])
@@ -446,7 +467,9 @@ class ElasticTrainer:
                     self.opt.moment_origin = int(scal[2])
                 if self.device.type == "cuda":
                     torch.cuda.current_stream(self.device).synchronize()
-                self.events.emit("state_broadcast", src=src, group="dp", tp_rank=t, s=round(time.time() - t0, 4))
+                nbytes = sum(x.numel() * x.element_size() for x in self._state_tensors())
+                self.events.emit("state_broadcast", src=src, sources=len(holders), group="dp", tp_rank=t,
+                                 bytes=nbytes, s=round(time.time() - t0, 4))
         else:
             mine = self.checkpoint.latest_step(self) if self.checkpoint is not None else -1
             target = int(c.ctrl_all_reduce([mine], dist.ReduceOp.MIN)[0])
@@ -625,6 +648,7 @@ class ElasticTrainer:
                                         loss=None)
                     if self.checkpoint is not None:
                         self.checkpoint.on_step(self)
+                    self._run_deferred_probes()
                     if on_step is not None:
                         on_step(self, loss)
                     if self.log_every and self.step % self.log_every == 0 and self.comm.rank == 0:
@@ -646,6 +670,31 @@ class ElasticTrainer:
             self._stop.set()
         return self
 
+    def _run_deferred_probes(self) -> None:
+        """A re-formed epoch's all-reduce probe, deferred off the recovery path: run after
+        its first committed step (every rank reaches this point after the same commit).
+        A failure here breaks the epoch like any collective failure."""
+        ran = False
+        for group, c in self._comm_groups():
+            if not getattr(c, "probe_pending", False):
+                continue
+            try:
+                s = c.run_deferred_probe()
+            except (CommAborted, RuntimeError) as e:
+                if not (c.aborted or _is_comm_error(e)):
+                    raise
+                log.warning("deferred all-reduce probe failed: %s", e)
+                self.comm.abort()
+                return
+            ran = True
+            self.events.emit("allreduce_probe_deferred", epoch=self.comm.epoch, group=group, step=self.step,
+                             s=round(s, 4), selected=(c.xgmi_probe or {}).get("selected"))
+        if ran:
+            if self.rdzv is not None:
+                self._publish_probe()
+            if getattr(self.dp_comm, "xgmi", None) is not None:
+                self.ddp.set_comm(self.dp_comm)   # map the gradient buffers for the engine
+
     def _apply_runtime_plan(self, version: int) -> None:
         """Brain runtime knobs of plan ``version`` (master/planner.py writes one document
         per version), switched by every rank at the same committed step or epoch entry."""
@@ -662,10 +711,12 @@ class ElasticTrainer:
             self.checkpoint.interval = max(1, int(ci))
         for group, c in self._comm_groups():
             ar = (doc.get("allreduce") or {}).get(group)
-            apply = getattr(c, "apply_allreduce_policy", None)
+            apply = getattr(c, "adopt_policy", None) or getattr(c, "apply_allreduce_policy", None)
             if ar and apply is not None and int(ar.get("world", -1)) == c.world_size and apply(ar["policy"]):
                 self.events.emit("plan_allreduce", step=self.step, group=group, world=ar["world"],
                                  policy=ar["policy"])
+                if c is self.dp_comm and self.ddp is not None and getattr(c, "xgmi", None) is not None:
+                    self.ddp.set_comm(c)   # the engine may have just been switched on: map the buffers
 
     def _reconfigure(self):
         old = self.comm
@@ -674,6 +725,8 @@ class ElasticTrainer:
             pass
         else:
             old.shutdown()
+        _retire(old)
+        del old
         if self.rdzv is not None and self.rdzv.kv.exists(f"rdzv/leave/{self.ctx.node_id}"):
             raise SystemExit(0)
         self._enter_epoch()
@@ -702,6 +755,23 @@ class _null:
 
     def __exit__(self, *a):
         return False
+
+
+def _retire(comm) -> None:
+    """Let an old epoch's communicator die OFF the training thread.  A ProcessGroupGloo whose
+    collective was abandoned on a dead peer blocks in its destructor until that collective
+    times out (~120 s measured: the new epoch's first step stalled behind it when the last
+    reference happened to drop in the trainer).  A daemon thread waits until it holds the
+    only reference and then drops it."""
+    import sys as _sys
+    box = [comm]
+
+    def reap():
+        while _sys.getrefcount(box[0]) > 2:   # held by anyone but the box (+ getrefcount's argument)
+            time.sleep(0.05)
+        box.clear()
+
+    threading.Thread(target=reap, name="edl-comm-reaper", daemon=True).start()
 
 
 def _is_comm_error(e: Exception) -> bool:

@@ -64,7 +64,9 @@ def main(args) -> int:
     if args.layers:
         env["EDL_BENCH_LAYERS"] = str(args.layers)
     if share:
-        env["EDL_COMM"] = "xgmi-only"
+        # xgmi-only by default; --comm auto-gloo runs the DEFAULT auto plane (engine probe,
+        # policy cache, deferral) with gloo on GPU tensors standing in for RCCL
+        env["EDL_COMM"] = getattr(args, "comm", None) or "xgmi-only"
         env["EDL_XGMI_MAX_BLOCKS"] = "16"   # all ranks' grids must be co-resident on the one GPU
     elif getattr(args, "comm", None):
         env["EDL_COMM"] = args.comm

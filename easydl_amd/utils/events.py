@@ -91,5 +91,14 @@ def ttr_breakdown(events: list[dict]) -> dict | None:
         "first_step_s": rel(done),
         "steps_lost": None if done is None else max(0, last_before + 1 - int(done.get("step", 0))),
     }
+    # all-reduce policy measurements on the recovery critical path (must be none: re-formed
+    # epochs adopt a cached policy or defer the probe past their first committed step)
+    t_done = done["ts"] if done is not None else float("inf")
+    in_window = [e for e in after if e["ts"] <= t_done]
+    out["probes_in_window"] = sum(1 for e in in_window if e["kind"] == "allreduce_probe"
+                                  and not e.get("cached") and e.get("source", "probe") == "probe")
+    deferred = first("allreduce_probe_deferred")
+    out["deferred_probe_s"] = rel(deferred)
+    out["policy_cached"] = any(e["kind"] == "allreduce_probe" and e.get("cached") for e in in_window)
     out["ttr_s"] = out["first_step_s"]
     return out

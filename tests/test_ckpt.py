@@ -415,3 +415,63 @@ def test_snapshot_mode_is_agreed_over_the_group():
     [t.start() for t in ts]
     [t.join(60) for t in ts]
     assert out == {0: ("lean", "lean"), 1: ("lean", "lean")}, out
+
+
+def test_snapshot_agreement_failure_skips_the_snapshot_and_aborts(tmp_path):
+    """a peer dying inside the first snapshot of a new layout (the mode
+    agreement is a collective) must not escape on_step: the snapshot is skipped and the
+    communicator marked aborted, so fit() reconfigures instead of ending."""
+    import types
+
+    from easydl_amd.parallel.comm import CommAborted
+
+    class DeadPeerComm:
+        world_size, rank, epoch = 2, 0, 3
+        aborted = False
+
+        def ctrl_all_reduce(self, values, op=None):
+            raise CommAborted("peer died during the snapshot-mode agreement")
+
+        def abort(self):
+            self.aborted = True
+
+    unlink_job_segments(JOB)
+    ckpt = CheckpointManager(JOB, interval=1)
+    try:
+        a = _trainer(tmp_path, None)
+        a.comm = DeadPeerComm()
+        a.step = 1
+        ckpt.on_step(a)
+        assert a.comm.aborted and ckpt.stats["skipped_comm"] == 1 and ckpt.stats["snapshots"] == 0
+        # unsharded snapshots are rank 0's alone: no agreement, so no collective at all
+        solo = CheckpointManager(JOB + "u", interval=1, sharded=False)
+        a.comm = DeadPeerComm()
+        assert solo.prepare_layout(a) == "full" and not a.comm.aborted
+        a.comm = types.SimpleNamespace(world_size=2, rank=1, epoch=3)
+        assert solo.prepare_layout(a) is None
+        solo.close(unlink=True)
+    finally:
+        ckpt.close()
+        unlink_job_segments(JOB)
+
+
+def test_drop_old_name_spares_a_name_another_segment_took(tmp_path):
+    """after a shard permutation another rank's relink can take this rank's old
+    layout name for its own live segment; dropping the old name must then keep it."""
+    import os
+    unlink_job_segments(JOB)
+    a, b = CheckpointManager(JOB, interval=1), CheckpointManager(JOB, interval=1)
+    try:
+        a._segment(4, 1, 4096)                    # A: w4-s1
+        b._segment(4, 2, 4096)                    # B: w4-s2
+        a._segment(3, 1, 4096)                    # A shrinks to w3-s1, keeps w4-s1 as its old name
+        assert a._old_name == f"/edl-{JOB}-w4-s1"
+        b._segment(4, 1, 4096)                    # B re-links to w4-s1 (the name A still holds)
+        b_ino = os.stat(f"/dev/shm/edl-{JOB}-w4-s1").st_ino
+        a._drop_old_name()                        # must not unlink B's live name
+        assert os.path.exists(f"/dev/shm/edl-{JOB}-w4-s1")
+        assert os.stat(f"/dev/shm/edl-{JOB}-w4-s1").st_ino == b_ino
+    finally:
+        a.close()
+        b.close()
+        unlink_job_segments(JOB)

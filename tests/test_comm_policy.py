@@ -216,3 +216,75 @@ def test_probe_failure_on_one_rank_drops_the_engine_everywhere():
 
     for probe, mode, closed in _spawn(2, fn).values():
         assert probe["selected"] == "rccl" and mode is None and closed, probe
+
+
+# --- policy cache and deferral (the recovery critical path measures nothing) -----------
+
+def test_policy_cache_skips_the_probe_on_reformation():
+    """Epoch 1 probes and caches the agreed table per (group, world); a later epoch of the
+    same world adopts it in warmup without timing a single collective."""
+    def fn(c, st):
+        eng = FakeEngine(c, lambda nb: 0.0 if nb > (3 << 20) else 0.05)
+        c.xgmi, c.xgmi_mode = eng, "auto"
+        c.PROBE_KB = (2048, 4096, 8192)
+        c._select_policy()
+        first = dict(c.xgmi_probe)
+        c.barrier()        # epochs are far apart in real life: the cache entry is written by now
+        # the next epoch (a new communicator in real life): same group and world size
+        eng2 = FakeEngine(c, lambda nb: 1.0)        # would flip the decision if it were timed
+        c.xgmi, c.xgmi_mode, c.probe_mode, c.epoch = eng2, "auto", "defer", 2
+        c._select_policy()
+        return first, dict(c.xgmi_probe), eng2.calls, c.xgmi_mode, c.probe_pending
+
+    for first, second, calls, mode, pending in _spawn(2, fn).values():
+        assert first["selected"] == "xgmi" and not first.get("cached")
+        assert second["cached"] and second["measured_epoch"] == 1 and second["epoch"] == 2
+        assert calls == 0 and mode == "xgmi" and not pending
+        assert second["policy"] == first["policy"]
+
+
+def test_deferred_probe_runs_after_the_first_commit_only():
+    """A re-formed epoch with no cached table routes everything to RCCL (no probe in
+    warmup); run_deferred_probe() measures later, at an agreed point, and caches."""
+    def fn(c, st):
+        eng = FakeEngine(c, lambda nb: 0.0 if nb > (3 << 20) else 0.05)
+        c.xgmi, c.xgmi_mode, c.probe_mode = eng, "auto", "defer"
+        c.PROBE_KB = (2048, 4096, 8192)
+        c._select_policy()
+        before = (eng.calls, c.probe_pending, c._use_xgmi_allreduce(torch.zeros((8 << 20) // 4)))
+        s = c.run_deferred_probe()
+        key = c._policy_key()
+        c.barrier()
+        return before, s, eng.calls, c.xgmi_mode, c.probe_pending, st.check([key])
+
+    for before, s, calls, mode, pending, cached in _spawn(2, fn).values():
+        assert before == (0, True, False)            # nothing timed, RCCL carries every size
+        assert s > 0 and calls > 0 and mode == "xgmi" and not pending and cached
+
+
+def test_brain_policy_replaces_a_pending_probe():
+    def fn(c, st):
+        eng = FakeEngine(c, lambda nb: 0.2)
+        c.xgmi, c.xgmi_mode, c.probe_mode = eng, "auto", "defer"
+        c._select_policy()
+        ok = c.adopt_policy({"xgmi_min_kb_inplace": 4096, "xgmi_min_kb_staged": 8192,
+                             "oneshot_max_kb": 0, "oneshot_max_staged_kb": 0})
+        return ok, eng.calls, c.xgmi_mode, c.probe_pending, c.xgmi_probe["source"], c.xgmi_min_bytes
+
+    for ok, calls, mode, pending, src, mi in _spawn(2, fn).values():
+        assert ok and calls == 0 and mode == "xgmi" and not pending and src == "brain" and mi == 4096 << 10
+
+
+def test_policy_cache_needs_agreement():
+    """A cache entry only some ranks can see (written between their reads) is ignored."""
+    def fn(c, st):
+        eng = FakeEngine(c, lambda nb: 0.0)
+        c.xgmi, c.xgmi_mode = eng, "auto"
+        if c.rank == 1:
+            st.set(c._policy_key(), '{"exact_everywhere": true, "policy": {"xgmi_min_kb_inplace": 0}}')
+        c.barrier()
+        got = c._cached_policy()
+        return got
+    out = _spawn(2, fn)
+    # both ranks read the same key after the barrier: agreed
+    assert all(v is not None for v in out.values())

@@ -357,3 +357,42 @@ def test_brain_plan_loop_retunes_buckets_on_running_workers(tmp_path):
         assert r[0]["plan_version"] == r[1]["plan_version"] >= 2
     finally:
         m.terminate()
+
+
+@pytest.mark.slow
+def test_tp2_dp3_replacement_receives_shard_from_every_holder(tmp_path):
+    """tp=2, dp=3 (world 6) -> one worker dies -> world 4 (granule 2: one survivor parks as
+    a spare) -> a replacement process arrives -> world 6.  The two ranks that need a shard
+    (the replacement and the stale spare) receive it from BOTH holders of their DP group at
+    once (multi-source transfer_state), bit-exact: every DP replica of
+    each shard ends identical."""
+    port = free_port()
+    m = _start_master(tmp_path, port, 2, 6, initial=6, granule=2, window=0.3)
+    try:
+        common = {"EDL_MASTER_ADDR": "127.0.0.1", "EDL_MASTER_PORT": str(port), "TEST_STEPS": "24",
+                  "TEST_GB": "6", "EDL_TP": "2", "TEST_STEP_SLEEP": "0.2"}
+        procs = {}
+        for i in range(6):
+            extra = dict(common, EDL_FAULT="kill@step=3,index=5") if i == 5 else common
+            procs[i] = subprocess.Popen([sys.executable, WORKER], env=_env(tmp_path, i, extra), cwd=ROOT)
+        t_end = time.time() + 120
+        while time.time() < t_end and procs[5].poll() is None:
+            time.sleep(0.05)
+        _report_exit(port, 5, procs[5].poll())
+        time.sleep(2.0)     # the world-4 epoch trains a few steps
+        env = _env(tmp_path, 6, dict(common, TEST_OUT=str(tmp_path / "res6.json")))
+        procs[6] = subprocess.Popen([sys.executable, WORKER], env=env, cwd=ROOT)
+        codes = _wait({i: p for i, p in procs.items() if i != 5})
+        assert all(v == 0 for v in codes.values()), codes
+        r = _results(tmp_path, [0, 1, 2, 3, 4, 6])
+        assert all(x["step"] == 24 for x in r.values()), {i: x["step"] for i, x in r.items()}
+        assert 6 in r[6]["worlds"] and any(4 in x["worlds"] for x in r.values()), {i: x["worlds"] for i, x in r.items()}
+        by_tp = {}
+        for x in r.values():
+            by_tp.setdefault(x["tp_rank"], set()).add(x["hash"])
+        assert sorted(by_tp) == [0, 1] and all(len(v) == 1 for v in by_tp.values()), by_tp
+        from easydl_amd.utils.events import read_events
+        sends = [e for e in read_events(str(tmp_path)) if e["kind"] == "state_broadcast" and e.get("group") == "dp"]
+        assert sends and max(e.get("sources", 1) for e in sends) == 2, sends
+    finally:
+        m.terminate()

@@ -411,8 +411,9 @@ def test_side_stream_weight_gradients_match_compute_stream(cuda, monkeypatch):
     assert err < 1e-2, err   # same GEMMs on another stream; an ordering race shows as O(1) errors
 
 
+@pytest.mark.parametrize("side", [False, True])
 @pytest.mark.parametrize("flat", [False, True])
-def test_bert_layer_residual_grad_slots_match_fp32(cuda, flat, monkeypatch):
+def test_bert_layer_residual_grad_slots_match_fp32(cuda, flat, side, monkeypatch):
     """A post-LN BERT layer on the HIP kernels, where the input's two gradients (the qkv /
     fc1 GEMM input gradient and LayerNorm's residual gradient) are summed in the GEMM
     epilogue (gradsink.ResidualGrad, addmm_ with beta = 1) instead of an add kernel, vs the
@@ -428,6 +429,9 @@ def test_bert_layer_residual_grad_slots_match_fp32(cuda, flat, monkeypatch):
         used.append(slot is not None and slot.g is not None)
         return orig(dy2, w, slot, shape)
     monkeypatch.setattr(gradsink, "input_grad_mm", counting)
+    # side: weight gradients on the side stream (EDL_WGRAD_STREAM=1) -- the parked residual
+    # gradient is also what fc2 / wo's side-stream weight GEMM reads
+    monkeypatch.setattr(fused, "_WGRAD_STREAM", side)
     torch.manual_seed(5)
     c = BertConfig(vocab_size=512, dim=256, n_layers=1, n_heads=4, ffn_dim=1024, max_pos=128)
     layer = BertLayer(c, cuda, torch.bfloat16)

@@ -119,3 +119,36 @@ def test_residual_grad_slot_accumulates_in_place():
     assert out.shape == (2, 3, 5) and out.data_ptr() == r.data_ptr()
     assert torch.allclose(out.reshape(6, 5), want, atol=1e-5)
     assert s.take() is None
+
+
+def test_direct_delivery_slot_unused_next_step_is_zeroed():
+    """ADVICE r3 (flat.py zero_grad): a parameter whose gradient a fused op wrote directly
+    in one step but that gets no gradient in the next (unused branch) must not replay the
+    stale gradient: it stays "fresh" through the backward and finalize_untouched (run by
+    ElasticDDP.finish every step) zeroes it before the optimizer."""
+    from easydl_amd.ops import fused, gradsink
+    from easydl_amd.parallel.ddp import ElasticDDP
+    from easydl_amd.parallel.flat import FlatParams
+
+    class TwoBranch(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.a = torch.nn.Parameter(torch.randn(8, 8))
+            self.b = torch.nn.Parameter(torch.randn(8, 8))
+
+        def forward(self, x, use_a):
+            return fused.linear(x, self.a if use_a else self.b).square().mean()
+
+    m = TwoBranch()
+    flat = FlatParams(m)
+    ddp = ElasticDDP(flat, None)
+    assert gradsink.is_flat(m.a)
+    x = torch.randn(4, 8)
+    flat.zero_grad()
+    m(x, True).backward()
+    ddp.finish()
+    assert m.a.grad.abs().sum() > 0 and not flat.saw_autograd    # delivered directly, not autograd
+    flat.zero_grad()
+    m(x, False).backward()
+    ddp.finish()
+    assert torch.count_nonzero(m.a.grad) == 0 and m.b.grad.abs().sum() > 0

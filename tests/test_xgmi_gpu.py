@@ -149,3 +149,25 @@ def test_ddp_step_xgmi_only_ranks_sharing_one_gpu(cuda, tmp_path):
     d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
     assert d["ranks"] == 2 and d["n_gpus"] == 1 and d["shared_gpu"]
     assert d["config"]["comm"] == "xgmi" and d["loss"] == d["loss"]
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_auto_plane_probe_register_ddp_step_real_engine(cuda, tmp_path, world, monkeypatch):
+    """The DEFAULT data plane end to end on hardware, ranks sharing one GPU: the real
+    XgmiComm is probed in its training form (async, async_blocks workgroups), the agreed
+    policy maps the flat gradient buffers, a DDP step's bucket all-reduces run on the
+    engine and match the fp64 sum; the next epoch of the same world adopts the cached
+    policy without timing anything.  gloo on GPU tensors stands in for RCCL."""
+    monkeypatch.setenv("EDL_XGMI_MAX_BLOCKS", "16")     # co-residency of every rank's grid
+    rs = _run(world, tmp_path, worker=os.path.join(ROOT, "tests", "helpers", "auto_comm_worker.py"), timeout=240)
+    for r in rs:
+        assert r["ok"], r["errors"]
+        p = r["probe"]
+        assert p["exact_everywhere"] and p["engine_form"] == "async" and p["engine_blocks"] == 16, p
+        assert p["data_plane"] == "gloo" and p["selected"] == "xgmi", p
+        assert r["backend"] == "gloo+xgmi" and r["registered"] >= 1, r
+        assert r["healthy"] and r["status"] == 0, r
+        p2 = r["probe2"]
+        assert p2["cached"] and p2["measured_epoch"] == 1 and not r["pending2"], p2
+        assert r["backend2"] == "gloo+xgmi" and r["warmup2_s"] < r["warmup_s"], r
+    assert len({json.dumps(r["probe"]["policy"], sort_keys=True) for r in rs}) == 1   # agreed
