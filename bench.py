@@ -62,10 +62,10 @@ def parse():
     ap.add_argument("--fault-step", type=int, default=None, help="--fault-inject: step at which the worker dies")
     ap.add_argument("--standby", type=int, default=1,
                     help="--fault-inject: warm spare workers kept by the operator (0 = cold respawn)")
-    ap.add_argument("--comm", default=None, choices=["pg", "native", "xgmi", "auto", "xgmi-only", "auto-gloo"],
+    ap.add_argument("--comm", default=None, choices=["pg", "xgmi", "auto", "xgmi-only", "auto-gloo"],
                     help="gradient all-reduce data plane (default $EDL_COMM or auto = RCCL + the hand-written xGMI "
                          "engine, per-size policy probed once per (group, world) and cached; pg = ProcessGroupNCCL "
-                         "(RCCL) only; xgmi = engine for every all-reduce; native = csrc RCCL manager; "
+                         "(RCCL) only; xgmi = engine for every all-reduce; "
                          "auto-gloo = auto with gloo standing in for RCCL (ranks sharing one GPU: tests, drills)")
     ap.add_argument("--sp", action="store_true", help="Megatron sequence parallelism inside the TP group")
     ap.add_argument("--tp", type=int, default=1,

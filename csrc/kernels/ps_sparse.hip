@@ -86,6 +86,11 @@ struct SparseOpt {
   float lr, beta1, beta2, eps, wd, step_size, inv_bc2_sqrt, scale;
 };
 
+// one wave updates table row `id` with gradient row G (lazy AdamW / Adagrad / SGD)
+__device__ __forceinline__ void update_row(float* __restrict__ w, float* __restrict__ m, float* __restrict__ v,
+                                           int64_t id, const float* __restrict__ grow, int dim, const SparseOpt& o,
+                                           int lane);
+
 // Update table rows rows[u] with compact gradient grad[u, :].
 __global__ __launch_bounds__(kRowBlock) void sparse_rows_update_kernel(float* __restrict__ w, float* __restrict__ m,
                                                                        float* __restrict__ v,
@@ -96,12 +101,35 @@ __global__ __launch_bounds__(kRowBlock) void sparse_rows_update_kernel(float* __
   if (u >= nu) return;
   const int64_t id = rows_idx[u];
   if (id < 0 || id >= rows) return;
-  const int lane = threadIdx.x & 63;
+  update_row(w, m, v, id, grad + u * (int64_t)dim, dim, o, threadIdx.x & 63);
+}
+
+// PS side of the GPU sparse push: the rows a worker wrote into its inbox (local row ids,
+// fp32 gradients, the row count written last by the worker's count kernel).  The count is
+// read on the device (no host round trip); a grid-stride loop covers it.
+__global__ __launch_bounds__(kRowBlock) void sparse_inbox_update_kernel(float* __restrict__ w, float* __restrict__ m,
+                                                                        float* __restrict__ v,
+                                                                        const int64_t* __restrict__ ids,
+                                                                        const float* __restrict__ grad,
+                                                                        const int* __restrict__ count, int64_t cap,
+                                                                        int dim, int64_t rows, SparseOpt o) {
+  const int64_t n = min((int64_t)*count, cap);
+  const int64_t nw = (int64_t)gridDim.x * (kRowBlock / kWave);
+  for (int64_t u = (int64_t)blockIdx.x * (kRowBlock / kWave) + (threadIdx.x >> 6); u < n; u += nw) {
+    const int64_t id = ids[u];
+    if (id < 0 || id >= rows) continue;
+    update_row(w, m, v, id, grad + u * (int64_t)dim, dim, o, threadIdx.x & 63);
+  }
+}
+
+__device__ __forceinline__ void update_row(float* __restrict__ w, float* __restrict__ m, float* __restrict__ v,
+                                           int64_t id, const float* __restrict__ grow, int dim, const SparseOpt& o,
+                                           int lane) {
   const int d4 = dim >> 2;
   f32x4* W = reinterpret_cast<f32x4*>(w + id * (int64_t)dim);
   f32x4* M = m ? reinterpret_cast<f32x4*>(m + id * (int64_t)dim) : nullptr;
   f32x4* V = v ? reinterpret_cast<f32x4*>(v + id * (int64_t)dim) : nullptr;
-  const f32x4* G = reinterpret_cast<const f32x4*>(grad + u * (int64_t)dim);
+  const f32x4* G = reinterpret_cast<const f32x4*>(grow);
   const float decay = 1.f - o.lr * o.wd;
   for (int c = lane; c < d4; c += kWave) {
     f32x4 g = G[c] * o.scale, p = W[c];
@@ -128,6 +156,94 @@ __global__ __launch_bounds__(kRowBlock) void sparse_rows_update_kernel(float* __
       for (int j = 0; j < 4; ++j) p[j] = p[j] * decay - o.lr * g[j];
     }
     W[c] = p;
+  }
+}
+
+// Worker-side pull of a row-sparse table striped over P parameter servers (global row r
+// lives at local row r / P of PS r % P): every PS's stripe is an IPC-mapped peer pointer,
+// so ONE launch gathers the rows of all owners over xGMI (no host-side owner split).
+// tabs[p] / nrows[p]: device arrays of the P stripe pointers and their row counts.
+template <bool OUT_BF16>
+__global__ __launch_bounds__(kRowBlock) void embed_gather_striped_kernel(const uint64_t* __restrict__ tabs,
+                                                                         const int64_t* __restrict__ nrows, int P,
+                                                                         const int64_t* __restrict__ idx, int64_t n,
+                                                                         int dim, void* __restrict__ out) {
+  const int64_t r = (int64_t)blockIdx.x * (kRowBlock / kWave) + (threadIdx.x >> 6);
+  if (r >= n) return;
+  const int lane = threadIdx.x & 63;
+  const int64_t id = idx[r];
+  const int owner = id >= 0 ? (int)(id % P) : 0;
+  const int64_t local = id >= 0 ? id / P : -1;
+  const bool ok = id >= 0 && local < nrows[owner];
+  const float* table = reinterpret_cast<const float*>(tabs[owner]);
+  const f32x4* src = reinterpret_cast<const f32x4*>(table + (ok ? local : 0) * (int64_t)dim);
+  const int d4 = dim >> 2;
+  for (int c = lane; c < d4; c += kWave) {
+    f32x4 v = ok ? src[c] : f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (OUT_BF16) {
+      u32x2 o{pack2(v[0], v[1]), pack2(v[2], v[3])};
+      reinterpret_cast<u32x2*>(static_cast<bf16_t*>(out) + r * (int64_t)dim)[c] = o;
+    } else {
+      reinterpret_cast<f32x4*>(static_cast<float*>(out) + r * (int64_t)dim)[c] = v;
+    }
+  }
+}
+
+// Worker-side sparse push: unique global ids [n] + fp32 row gradients [n, dim] are split by
+// owner on the device and written straight into each PS's inbox (peer writes over xGMI):
+// inbox_ids[p][pos] = id / P, inbox_grad[p][pos, :] = grad row.  pos comes from a per-owner
+// counter in LOCAL memory (cnt, zeroed by the caller); sparse_push_counts_kernel then
+// publishes the counts into the inboxes.  Row order inside an inbox is arbitrary (ids are
+// unique, the update is per row).  Rows past `cap` are dropped (the host checks n <= cap).
+__global__ __launch_bounds__(kRowBlock) void sparse_split_push_kernel(const int64_t* __restrict__ ids,
+                                                                      const float* __restrict__ grad, int64_t n,
+                                                                      int dim, int P,
+                                                                      const uint64_t* __restrict__ inbox_ids,
+                                                                      const uint64_t* __restrict__ inbox_grad,
+                                                                      int* __restrict__ cnt, int64_t cap) {
+  const int64_t r = (int64_t)blockIdx.x * (kRowBlock / kWave) + (threadIdx.x >> 6);
+  if (r >= n) return;
+  const int lane = threadIdx.x & 63;
+  const int64_t id = ids[r];
+  if (id < 0) return;
+  const int owner = (int)(id % P);
+  int pos = 0;
+  if (lane == 0) pos = atomicAdd(cnt + owner, 1);
+  pos = __shfl(pos, 0);
+  if (pos >= cap) return;
+  if (lane == 0) reinterpret_cast<int64_t*>(inbox_ids[owner])[pos] = id / P;
+  const f32x4* src = reinterpret_cast<const f32x4*>(grad + r * (int64_t)dim);
+  f32x4* dst = reinterpret_cast<f32x4*>(reinterpret_cast<float*>(inbox_grad[owner]) + (int64_t)pos * dim);
+  for (int c = lane; c < (dim >> 2); c += kWave) dst[c] = src[c];
+}
+
+__global__ void sparse_push_counts_kernel(const int* __restrict__ cnt, int P, const uint64_t* __restrict__ inbox_cnt,
+                                          int64_t cap) {
+  const int p = threadIdx.x;
+  if (p < P) *reinterpret_cast<int*>(inbox_cnt[p]) = (int)min((int64_t)cnt[p], cap);
+}
+
+// Push ordering without a host sync on the worker.  The worker's stream, after its inbox
+// writes, runs ps_signal: a system-scope release store of the push sequence number into a
+// flag word in the PS's HBM (IPC-mapped).  The PS's stream runs ps_wait before the update
+// that reads the inboxes: one thread spins on a system-scope acquire load of that word,
+// bounded by a wall-clock deadline (a worker killed between enqueue and execution must not
+// wedge the PS's stream); a give-up is recorded in status[0] and the update is then skipped
+// by the host (it reads the status after the update's event).
+__global__ void ps_signal_kernel(uint32_t* __restrict__ flag, uint32_t value) {
+  __threadfence_system();   // the inbox writes of the kernels before this one, past the L2
+  __hip_atomic_store(flag, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ void ps_wait_kernel(const uint32_t* __restrict__ flag, uint32_t value, uint64_t timeout_ticks,
+                               int* __restrict__ status) {
+  const uint64_t t0 = wall_clock64();
+  while ((int32_t)(__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - value) < 0) {
+    if (wall_clock64() - t0 > timeout_ticks) {
+      __hip_atomic_store(status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return;
+    }
+    __builtin_amdgcn_s_sleep(2);
   }
 }
 
@@ -270,6 +386,67 @@ int edl_sparse_rows_update(float* w, float* m, float* v, const int64_t* rows_idx
     o.inv_bc2_sqrt = 1.f / sqrtf(1.f - powf(beta2, (float)step));
   }
   sparse_rows_update_kernel<<<row_blocks(nu), kRowBlock, 0, s>>>(w, m, v, rows_idx, grad, nu, dim, rows, o);
+  EDL_LAUNCH_CHECK();
+  return 0;
+}
+
+int edl_embed_gather_striped(const uint64_t* tabs, const int64_t* nrows, int P, const int64_t* idx, int64_t n,
+                             int dim, void* out, int out_bf16, hipStream_t s) {
+  if (dim % 4 || n < 0 || P < 1) return (int)hipErrorInvalidValue;
+  if (n == 0) return 0;
+  if (out_bf16)
+    embed_gather_striped_kernel<true><<<row_blocks(n), kRowBlock, 0, s>>>(tabs, nrows, P, idx, n, dim, out);
+  else
+    embed_gather_striped_kernel<false><<<row_blocks(n), kRowBlock, 0, s>>>(tabs, nrows, P, idx, n, dim, out);
+  EDL_LAUNCH_CHECK();
+  return 0;
+}
+
+// cnt: P int32 of local scratch (zeroed here); inbox_* : device arrays of P peer pointers
+int edl_sparse_split_push(const int64_t* ids, const float* grad, int64_t n, int dim, int P, const uint64_t* inbox_ids,
+                          const uint64_t* inbox_grad, const uint64_t* inbox_cnt, int* cnt, int64_t cap,
+                          hipStream_t s) {
+  if (dim % 4 || n < 0 || P < 1 || P > 256 || n > cap) return (int)hipErrorInvalidValue;
+  hipError_t e = hipMemsetAsync(cnt, 0, sizeof(int) * P, s);
+  if (e != hipSuccess) return (int)e;
+  if (n > 0)
+    sparse_split_push_kernel<<<row_blocks(n), kRowBlock, 0, s>>>(ids, grad, n, dim, P, inbox_ids, inbox_grad, cnt,
+                                                                  cap);
+  EDL_LAUNCH_CHECK();
+  sparse_push_counts_kernel<<<1, 256, 0, s>>>(cnt, P, inbox_cnt, cap);
+  EDL_LAUNCH_CHECK();
+  return 0;
+}
+
+int edl_sparse_inbox_update(float* w, float* m, float* v, const int64_t* ids, const float* grad, const int* count,
+                            int64_t cap, int dim, int64_t rows, int kind, float lr, float beta1, float beta2, float eps,
+                            float wd, int64_t step, float scale, hipStream_t s) {
+  if (dim % 4 || cap < 0 || kind < 0 || kind > 2) return (int)hipErrorInvalidValue;
+  if ((kind == 0 && (!m || !v)) || (kind == 1 && !v)) return (int)hipErrorInvalidValue;
+  if (cap == 0) return 0;
+  SparseOpt o{kind, lr, beta1, beta2, eps, wd, lr, 1.f, scale};
+  if (kind == 0) {
+    o.step_size = lr / (1.f - powf(beta1, (float)step));
+    o.inv_bc2_sqrt = 1.f / sqrtf(1.f - powf(beta2, (float)step));
+  }
+  const int blocks = row_blocks(cap) < 1024 ? row_blocks(cap) : 1024;
+  sparse_inbox_update_kernel<<<blocks, kRowBlock, 0, s>>>(w, m, v, ids, grad, count, cap, dim, rows, o);
+  EDL_LAUNCH_CHECK();
+  return 0;
+}
+
+int edl_ps_signal(uint32_t* flag, uint32_t value, hipStream_t s) {
+  ps_signal_kernel<<<1, 1, 0, s>>>(flag, value);
+  EDL_LAUNCH_CHECK();
+  return 0;
+}
+
+int edl_ps_wait(const uint32_t* flag, uint32_t value, double timeout_s, int* status, hipStream_t s) {
+  int dev = 0, khz = 0;
+  hipGetDevice(&dev);
+  if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0) khz = 100000;
+  const uint64_t ticks = (uint64_t)(timeout_s * 1000.0 * (double)khz);
+  ps_wait_kernel<<<1, 1, 0, s>>>(flag, value, ticks, status);
   EDL_LAUNCH_CHECK();
   return 0;
 }

@@ -102,6 +102,13 @@ _KERNEL_SIGS = {
     "edl_sparse_rows_update": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_i64, c_int, c_i64, c_int, c_float,
                                c_float, c_float, c_float, c_float, c_i64, c_float, c_void_p],
     "edl_ps_pull_cast": [c_void_p, c_void_p, c_i64, c_void_p],
+    "edl_ps_signal": [c_void_p, ctypes.c_uint32, c_void_p],
+    "edl_ps_wait": [c_void_p, ctypes.c_uint32, ctypes.c_double, c_void_p, c_void_p],
+    "edl_embed_gather_striped": [c_void_p, c_void_p, c_int, c_void_p, c_i64, c_int, c_void_p, c_int, c_void_p],
+    "edl_sparse_split_push": [c_void_p, c_void_p, c_i64, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_i64,
+                              c_void_p],
+    "edl_sparse_inbox_update": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_i64, c_int, c_i64, c_int,
+                                c_float, c_float, c_float, c_float, c_float, c_i64, c_float, c_void_p],
     "edl_ps_multi_chunk": [],
     "edl_ps_multi_copy": [c_void_p, c_void_p, c_int, c_i64, c_void_p, c_int, c_void_p],
     "edl_xgmi_max_blocks": [],

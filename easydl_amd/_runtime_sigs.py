@@ -69,19 +69,4 @@ SIGS = {
     "edl_xgmi_buf_handle": (i32, [vp, ctypes.c_char_p, ctypes.POINTER(u64), ctypes.POINTER(u64)]),
     "edl_xgmi_buf_open": (i32, [i32, ctypes.c_char_p, ctypes.POINTER(vp)]),
     "edl_xgmi_buf_close": (i32, [i32, vp]),
-    "edl_rccl_available": (i32, [ctypes.POINTER(i32), ctypes.POINTER(i32)]),
-    "edl_rccl_error_string": (cp, [i32]),
-    "edl_rccl_unique_id": (i32, [ctypes.c_char_p]),
-    "edl_rccl_init": (i32, [cp, i32, i32, i32, ctypes.POINTER(i32), ctypes.c_double, ctypes.POINTER(vp)]),
-    "edl_rccl_shrink": (i32, [vp, ctypes.POINTER(i32), i32, i32, ctypes.POINTER(i32), ctypes.c_double,
-                              ctypes.POINTER(vp)]),
-    "edl_rccl_abort": (i32, [vp]),
-    "edl_rccl_destroy": (i32, [vp]),
-    "edl_rccl_async_error": (i32, [vp]),
-    "edl_rccl_all_reduce": (i32, [vp, vp, vp, ctypes.c_size_t, i32, i32, vp]),
-    "edl_rccl_broadcast": (i32, [vp, vp, vp, ctypes.c_size_t, i32, i32, vp]),
-    "edl_rccl_reduce_scatter": (i32, [vp, vp, vp, ctypes.c_size_t, i32, i32, vp]),
-    "edl_rccl_all_gather": (i32, [vp, vp, vp, ctypes.c_size_t, i32, vp]),
-    "edl_rccl_sendrecv": (i32, [vp, i32, ctypes.POINTER(i32), ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_size_t),
-                                ctypes.POINTER(i32), i32, vp]),
 }

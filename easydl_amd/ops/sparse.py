@@ -157,3 +157,58 @@ class MultiCopyPlan:
         s = stream if stream is not None else torch.cuda.current_stream(self.table.device).cuda_stream
         _native.kernels().check("edl_ps_multi_copy", self.table.data_ptr(), self.bstart.data_ptr(), self.n,
                                 self.nblocks, flat_ptr, 1 if push else 0, s)
+
+
+def ptr_array(tensors_or_ptrs, device) -> torch.Tensor:
+    """Device int64 array of pointers (the kernels' per-PS tables)."""
+    vals = [t if isinstance(t, int) else t.data_ptr() for t in tensors_or_ptrs]
+    return torch.tensor(vals, dtype=torch.int64).to(device)
+
+
+def embed_gather_striped(tabs: torch.Tensor, nrows: torch.Tensor, ids: torch.Tensor, dim: int,
+                         out_dtype=torch.float32) -> torch.Tensor:
+    """Rows ``ids`` (global) of a table striped over ``P = len(tabs)`` PS stripes (row r at
+    local row r // P of stripe r % P); ``tabs``/``nrows``: device int64 arrays of the
+    (IPC-mapped) stripe pointers and their row counts.  One launch, no host sync."""
+    ids = ids.reshape(-1).to(torch.int64).contiguous()
+    out = torch.empty(ids.numel(), dim, dtype=out_dtype, device=ids.device)
+    _native.kernels().check("edl_embed_gather_striped", tabs.data_ptr(), nrows.data_ptr(), tabs.numel(),
+                            ids.data_ptr(), ids.numel(), dim, out.data_ptr(), 1 if out_dtype == torch.bfloat16 else 0,
+                            _native.stream_of(ids))
+    return out
+
+
+def sparse_split_push(ids: torch.Tensor, grad: torch.Tensor, inbox_ids: torch.Tensor, inbox_grad: torch.Tensor,
+                      inbox_cnt: torch.Tensor, cap: int, scratch: torch.Tensor) -> None:
+    """Write unique global ``ids`` and their fp32 row ``grad`` into the owners' inboxes
+    (device arrays of P peer pointers: local-id buffers, gradient buffers, int32 counts).
+    ``scratch``: int32 [>= P] on ids' device."""
+    ids = ids.reshape(-1).to(torch.int64).contiguous()
+    grad = grad.float().contiguous()
+    if ids.numel() > cap:
+        raise ValueError(f"sparse push of {ids.numel()} rows exceeds the inbox capacity {cap}")
+    _native.kernels().check("edl_sparse_split_push", ids.data_ptr(), grad.data_ptr(), ids.numel(), grad.shape[1],
+                            inbox_ids.numel(), inbox_ids.data_ptr(), inbox_grad.data_ptr(), inbox_cnt.data_ptr(),
+                            scratch.data_ptr(), int(cap), _native.stream_of(ids))
+
+
+def sparse_inbox_update(w: torch.Tensor, m, v, ids: torch.Tensor, grad: torch.Tensor, count: torch.Tensor, *,
+                        kind: str = "adam", lr: float, beta1: float = 0.9, beta2: float = 0.999, eps: float = 1e-8,
+                        weight_decay: float = 0.0, step: int = 1, scale: float = 1.0) -> None:
+    """Lazy optimizer update from a worker's sparse inbox; the row count is read on the
+    device (``count``: int32, written by the worker's push)."""
+    _check_rows(w)
+    _native.kernels().check("edl_sparse_inbox_update", w.data_ptr(), _native.ptr(m), _native.ptr(v), ids.data_ptr(),
+                            grad.data_ptr(), count.data_ptr(), ids.numel(), w.shape[1], w.shape[0], OPT_KIND[kind],
+                            lr, beta1, beta2, eps, weight_decay, int(step), float(scale), _native.stream_of(w))
+
+
+def ps_signal(flag: torch.Tensor, value: int, stream) -> None:
+    """Stream-ordered system-scope store of ``value`` into ``flag`` (an IPC-mapped peer word)."""
+    _native.kernels().check("edl_ps_signal", flag.data_ptr(), int(value) & 0xFFFFFFFF, stream.cuda_stream)
+
+
+def ps_wait(flag: torch.Tensor, value: int, timeout_s: float, status: torch.Tensor, stream) -> None:
+    """``stream`` waits (on the device, bounded) until ``flag`` >= ``value``; a give-up sets status[0]."""
+    _native.kernels().check("edl_ps_wait", flag.data_ptr(), int(value) & 0xFFFFFFFF, float(timeout_s),
+                            status.data_ptr(), stream.cuda_stream)

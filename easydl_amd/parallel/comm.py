@@ -57,7 +57,6 @@ class Communicator:
         self.epoch = epoch
         self.device = torch.device(device)
         self.tag = tag
-        self.rccl = None
         self.xgmi = None
         self.xgmi_mode = None
         self.xgmi_probe: dict | None = None
@@ -92,12 +91,6 @@ class Communicator:
         if not data:
             self.data = None
             self.backend = self.data_kind = "none"
-        elif self.device.type == "cuda" and data_backend == "native":
-            # csrc/runtime/rccl_comm.cpp: non-blocking, abortable creation; own comm stream
-            from easydl_amd.parallel.rccl import RcclComm
-            self.data = None
-            self.rccl = RcclComm(base, "data", rank, world_size, self.device, timeout_s=timeout_s)
-            self.backend = self.data_kind = "rccl-native"
         elif self.device.type == "cuda" and data_backend == "xgmi-only":
             # the hand-written engine is the ONLY data plane (no RCCL communicator): several
             # ranks may then share one GPU (RCCL refuses duplicate devices), e.g. to exercise
@@ -152,10 +145,7 @@ class Communicator:
     def warmup(self) -> float:
         """Force lazy communicator creation now (so it is not hidden in step 1)."""
         t0 = time.perf_counter()
-        if self.rccl is not None:
-            self.all_reduce(torch.zeros(1, device=self.device))
-            self._sync_stream()
-        elif self.backend == "xgmi":
+        if self.backend == "xgmi":
             self.xgmi.all_reduce(torch.zeros(64, device=self.device))
             self._sync_stream()
         elif self.data is not None:
@@ -466,10 +456,6 @@ class Communicator:
 
     def _p2p_batch(self, ops) -> None:
         """Concurrent point-to-point transfers (one grouped launch on RCCL)."""
-        if self.rccl is not None:
-            if ops:
-                self._wait(self._native(self.rccl.sendrecv_async, [o[:3] for o in ops]))
-            return
         if not ops:
             return
         if self.data_kind == "rccl" and hasattr(self.data, "_start_coalescing"):
@@ -500,9 +486,7 @@ class Communicator:
         # process at teardown, so gloo groups are only marked, never aborted.
         if self.xgmi is not None:
             self.xgmi.abort()  # host-mapped abort word: spinning workgroups exit
-        if self.rccl is not None:
-            self.rccl.abort()
-        elif self.data_kind == "rccl":
+        if self.data_kind == "rccl":
             try:
                 self.data.abort()
             except Exception as e:  # pragma: no cover - best effort
@@ -515,8 +499,6 @@ class Communicator:
     def shutdown(self) -> None:
         if self._aborted:
             return
-        if self.rccl is not None:
-            self.rccl.destroy()
         if self.xgmi is not None:
             self.xgmi.close()
             self.xgmi = None
@@ -546,8 +528,6 @@ class Communicator:
         if self._aborted:
             raise CommAborted("communicator aborted")
         self._verify("all_reduce", t, int(op))
-        if self.rccl is not None:
-            return self._native(self.rccl.all_reduce_async, t, op)
         if self._use_xgmi_allreduce(t):
             if op == dist.ReduceOp.SUM:
                 return self._native(self.xgmi.all_reduce_async, t)
@@ -567,9 +547,6 @@ class Communicator:
         if self._aborted:
             raise CommAborted("communicator aborted")
         self._verify("broadcast", t, src)
-        if self.rccl is not None:
-            self._wait(self._native(self.rccl.broadcast_async, t, src))
-            return t
         if self.backend == "xgmi":
             if self._use_xgmi(t):
                 if self.rank != src:
@@ -629,9 +606,6 @@ class Communicator:
         if self._use_xgmi(out, inp):
             self._native(self.xgmi.all_gather, out, inp)
             return out
-        if self.rccl is not None:
-            self._wait(self._native(self.rccl.all_gather_async, out, inp))
-            return out
         self._wait(self.data._allgather_base(out, inp))
         return out
 
@@ -639,36 +613,19 @@ class Communicator:
         if op == dist.ReduceOp.SUM and self._use_xgmi(out, inp):
             self._native(self.xgmi.reduce_scatter, out, inp)
             return out
-        if self.rccl is not None:
-            self._wait(self._native(self.rccl.reduce_scatter_async, out, inp, op))
-            return out
         o = dist.ReduceScatterOptions()
         o.reduceOp = op
         self._wait(self.data._reduce_scatter_base(out, inp, o))
         return out
 
     def all_to_all_single(self, out: torch.Tensor, inp: torch.Tensor):
-        if self.rccl is not None:  # equal splits as one grouped send/recv batch
-            n = self.world_size
-            src, dst = inp.reshape(n, -1), out.reshape(n, -1)
-            dst[self.rank].copy_(src[self.rank])
-            ops = [op for p in range(n) if p != self.rank for op in (("send", src[p], p), ("recv", dst[p], p))]
-            if ops:
-                self._wait(self._native(self.rccl.sendrecv_async, ops))
-            return out
         self._wait(self.data.alltoall_base(out, inp, [], [], dist.AllToAllOptions()))
         return out
 
     def send(self, t: torch.Tensor, dst: int, tag: int = 0):
-        if self.rccl is not None:
-            self._wait(self._native(self.rccl.sendrecv_async, [("send", t, dst)]))
-            return
         self._wait(self.data.send([t], dst, tag))
 
     def recv(self, t: torch.Tensor, src: int, tag: int = 0):
-        if self.rccl is not None:
-            self._wait(self._native(self.rccl.sendrecv_async, [("recv", t, src)]))
-            return t
         self._wait(self.data.recv([t], src, tag))
         return t
 
@@ -676,7 +633,7 @@ class Communicator:
         try:
             return fn(*args)
         except RuntimeError as e:
-            raise CommAborted(f"native RCCL call failed in epoch {self.epoch}: {e}") from e
+            raise CommAborted(f"xGMI engine call failed in epoch {self.epoch}: {e}") from e
 
     def wait_work(self, work) -> None:
         """Wait for an all-reduce work object (DDP buckets): abortable on gloo."""

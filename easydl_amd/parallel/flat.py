@@ -135,6 +135,11 @@ class FlatParams:
                 with torch.no_grad():
                     view.copy_(p.data)
                 p.data = view
+                if gdt != dt and hasattr(p, "grad_dtype"):
+                    # fp32 gradient buffers under bf16 parameters (grad_dtype=fp32): torch >= 2.10
+                    # checks .grad against the tensor's grad_dtype; autograd-path gradients are
+                    # then accumulated into the fp32 buffer
+                    p.grad_dtype = gdt
                 p.grad = grad[off:off + k].view(p.shape)
                 p._edl_flat = True
                 p._edl_fresh = True

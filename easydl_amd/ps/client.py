@@ -10,6 +10,7 @@ coordination.  PS addresses are discovered through the job master's store
 from __future__ import annotations
 
 import json
+import os
 import socket
 import threading
 import time
@@ -63,6 +64,11 @@ class PSClient:
         self.rows_bf16 = False  # pull embedding rows as bf16 (halves the wire bytes)
         self.transport = transport
         self._ipc: dict[int, dict] = {}   # PS index -> {"w", "inbox", "layout", "sock"}
+        # GPU transport, row-sparse tables: rows per push a sparse inbox holds (a larger push
+        # falls back to the TCP path for that step), per-table device pointer tables
+        self.sparse_cap = int(os.environ.get("EDL_PS_SPARSE_CAP", 65536))
+        self._sp_plan: dict = {}
+        self.sparse_path = {"ipc_pulls": 0, "ipc_pushes": 0, "tcp_pulls": 0, "tcp_pushes": 0}
 
     def bind(self, model: torch.nn.Module) -> None:
         from easydl_amd.ps.embedding import tables_of
@@ -77,9 +83,44 @@ class PSClient:
         owner = ids % self.num_ps
         return [(i, (owner == i).nonzero().view(-1)) for i in range(self.num_ps)], ids
 
+    def _sparse_ipc(self, device) -> bool:
+        """Row-sparse traffic goes through the mapped tables / inboxes (no host copies)."""
+        if self.transport != "ipc" or not self.tables or torch.device(device).type != "cuda":
+            return False
+        return all("tables" in self._ipc_map(i, device) for i in range(self.num_ps))
+
+    def _table_ptrs(self, table: str, device):
+        maps = [self._ipc_map(i, device) for i in range(self.num_ps)]
+        key = ("tab", table, tuple(m["tables"][table][0].data_ptr() for m in maps))
+        got = self._sp_plan.get(key[:2])
+        if got is None or got[0] != key:
+            from easydl_amd.ops.sparse import ptr_array
+            tabs = ptr_array([m["tables"][table][0] for m in maps], device)
+            nrows = torch.tensor([m["tables"][table][1] for m in maps], dtype=torch.int64).to(device)
+            got = self._sp_plan[key[:2]] = (key, tabs, nrows)
+        return got[1], got[2]
+
+    def _inbox_ptrs(self, table: str, slots, device):
+        maps = [self._ipc_map(i, device) for i in range(self.num_ps)]
+        bufs = [m["sp_inbox"][table][s] for m, s in zip(maps, slots)]
+        key = ("inbox", table, tuple(b[0].data_ptr() for b in bufs))
+        got = self._sp_plan.get(key)
+        if got is None:
+            from easydl_amd.ops.sparse import ptr_array
+            got = self._sp_plan[key] = tuple(ptr_array([b[k] for b in bufs], device) for k in range(3)) + (
+                torch.zeros(max(4, self.num_ps), dtype=torch.int32, device=device),)
+        return got
+
     def pull_rows(self, table: str, ids: torch.Tensor) -> torch.Tensor:
         """Rows ``ids`` (global) of ``table`` from their owning shards, fp32 [n, dim] on ids' device."""
         m = self.tables[table]
+        if ids.is_cuda and self._sparse_ipc(ids.device):
+            # one gather kernel reads every owner's mapped stripe (device-side owner split)
+            from easydl_amd.ops.sparse import embed_gather_striped
+            tabs, nrows = self._table_ptrs(table, ids.device)
+            self.sparse_path["ipc_pulls"] += 1
+            return embed_gather_striped(tabs, nrows, ids, m.dim)
+        self.sparse_path["tcp_pulls"] += 1
         parts, flat = self._split_rows(ids.cpu())
         out = torch.empty(flat.numel(), m.dim, dtype=torch.float32)
 
@@ -131,17 +172,24 @@ class PSClient:
     # buffered: push k writes inbox k % 2, and the PS answers push k only once the
     # update that read inbox (k - 1) % 2 has finished, so the next push may overwrite
     # it — the PS never blocks on the update it has just launched.
-    def _ipc_map(self, i: int) -> dict:
+    def _ipc_map(self, i: int, device=None) -> dict:
         m = self._ipc.get(i)
         if m is None or m["sock"] is not self._socks.get(i):
             from easydl_amd.ps.ipc import import_tensor
-            h, _ = self._call(i, {"op": "ipc_open", "worker": self.worker_id})
+            hdr = {"op": "ipc_open", "worker": self.worker_id, "sparse_cap": self.sparse_cap if self.tables else 0}
+            h, _ = self._call(i, hdr)
             if not h.get("ok"):
                 raise RuntimeError(f"PS {i}: {h.get('error')}")
             d = h["ipc"]
             m = {"w": import_tensor(d["w"]), "inbox": [import_tensor(x) for x in d["inbox"]], "layout": d["layout"],
-                 "sock": self._socks.get(i), "slot": 0, "pull_plan": None, "push_plan": None}
+                 "sock": self._socks.get(i), "slot": 0, "pull_plan": None, "push_plan": None,
+                 "flag": import_tensor(d["flag"]) if "flag" in d else None, "seq": 0}
+            if "tables" in d:
+                m["tables"] = {n: (import_tensor(x["w"]), int(x["rows"])) for n, x in d["tables"].items()}
+                m["sp_inbox"] = {n: [[import_tensor(x) for x in b] for b in bufs]
+                                 for n, bufs in d["sparse_inbox"].items()}
             self._ipc[i] = m
+            self._sp_plan = {}
         return m
 
     @staticmethod
@@ -161,7 +209,7 @@ class PSClient:
 
     def _pull_launch(self, i: int, params: dict) -> None:
         """Copy PS i's shard into the parameters on the current stream (one launch)."""
-        m = self._ipc_map(i)
+        m = self._ipc_map(i, next(iter(params.values())).device)
         ts = [params[n].data for n in m["layout"]]
         dev = ts[0].device
         plan = self._plan(m, "pull_plan", ts, dev)
@@ -182,7 +230,8 @@ class PSClient:
 
     def _push_launch(self, i: int, params: dict) -> int:
         """Write this worker's gradients of PS i's shard into inbox ``slot``; returns the slot."""
-        m = self._ipc_map(i)
+        dev = next(iter(params.values())).device
+        m = self._ipc_map(i, dev)
         slot = m["slot"]
         m["slot"] ^= 1
         inbox = m["inbox"][slot]
@@ -204,7 +253,7 @@ class PSClient:
         hdr = {"op": "pull_ipc"}
         if min_version is not None:
             hdr["min_version"] = min_version
-        self._ipc_map(i)
+        self._ipc_map(i, next(iter(params.values())).device)
         h, _ = self._call(i, hdr)
         return h["version"]
 
@@ -249,16 +298,56 @@ class PSClient:
         same round trip returns once the shard has applied them, and the fresh
         parameters are copied right away — push + pull in ONE control message per PS."""
         params = dict(model.named_parameters())
-        sparse_grads = self._take_sparse()
+        sparse_dev = {}
+        if self.transport == "ipc" and self.tables:
+            dev = next(iter(params.values())).device
+            if self._sparse_ipc(dev):
+                for n, mod in self.tables.items():
+                    got = mod.take_grads()
+                    if got is not None:
+                        sparse_dev[n] = (got[0], got[1].detach())
+                if any(ids.numel() > self.sparse_cap for ids, _ in sparse_dev.values()):
+                    # larger than an inbox: this step's rows go over TCP
+                    for n, (ids, g) in sparse_dev.items():
+                        self.tables[n]._pending.append((ids, _Grad(g)))
+                    sparse_dev = {}
+        sparse_grads = {} if sparse_dev else self._take_sparse()
+        if sparse_grads:
+            self.sparse_path["tcp_pushes"] += 1
 
         if self.transport == "ipc":
-            slots = [self._push_launch(i, params) for i in range(self.num_ps)]
             dev = next(iter(params.values())).device
-            torch.cuda.current_stream(dev).synchronize()   # inboxes complete before the PS reads them
+            slots = [self._push_launch(i, params) for i in range(self.num_ps)]
+            sp_ipc = bool(sparse_dev) or (bool(self.tables) and self._sparse_ipc(dev))
+            if sp_ipc:
+                # row-sparse gradients: split by owner on the device, written into each PS's
+                # sparse inbox of this slot (every table, 0 rows included: the PS reads counts)
+                from easydl_amd.ops.sparse import sparse_split_push
+                for n, mod in self.tables.items():
+                    ids, g = sparse_dev.get(n, (None, None))
+                    iids, igrad, icnt, scratch = self._inbox_ptrs(n, slots, dev)
+                    if ids is None:
+                        ids = torch.empty(0, dtype=torch.int64, device=dev)
+                        g = torch.empty(0, mod.dim, dtype=torch.float32, device=dev)
+                    sparse_split_push(ids, g, iids, igrad, icnt, self.sparse_cap, scratch)
+                self.sparse_path["ipc_pushes"] += 1
+            seqs = [None] * self.num_ps
+            if all(self._ipc[i].get("flag") is not None for i in range(self.num_ps)):
+                # stream-ordered flag stores into each PS's HBM; the PS's stream waits for them
+                # (bounded) before reading any inbox: no host sync on this worker
+                from easydl_amd.ops.sparse import ps_signal
+                stream = torch.cuda.current_stream(dev)
+                for i in range(self.num_ps):
+                    m = self._ipc[i]
+                    m["seq"] += 1
+                    seqs[i] = m["seq"]
+                    ps_signal(m["flag"], m["seq"], stream)
+            else:
+                torch.cuda.current_stream(dev).synchronize()   # inboxes complete before the PS reads them
 
             def one(i):
                 hdr = {"op": "push_ipc", "worker": self.worker_id, "step": step, "slot": slots[i],
-                       "pull": bool(then_pull)}
+                       "pull": bool(then_pull), "sparse_ipc": sp_ipc, "seq": seqs[i]}
                 h, _ = self._call(i, hdr, self._sparse_grads(i, sparse_grads))
                 return h["version"]
 
@@ -307,3 +396,10 @@ def store_resolver(kv, timeout_s: float = 300.0):
         raise TimeoutError(f"PS {i} address not published")
 
     return resolve
+
+
+class _Grad:
+    """Stands in for a leaf whose ``.grad`` holds already de-duplicated row gradients."""
+
+    def __init__(self, g):
+        self.grad = g

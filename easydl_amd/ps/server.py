@@ -105,6 +105,15 @@ class ParameterServer:
         # completion event of the update that last read each one
         self.inboxes: dict[str, list[torch.Tensor]] = {}
         self._inbox_ev: dict[str, list] = {}
+        # ... and, per row-sparse table, two sparse inboxes (local ids, fp32 rows, row count)
+        # the worker fills on its GPU; the worker's interprocess event orders the PS's reads
+        # after those writes (no host synchronisation on the worker)
+        self.sp_inboxes: dict[str, dict[str, list[tuple]]] = {}
+        # push ordering: the worker's stream stores its push sequence number into this flag
+        # word after its inbox writes (edl_ps_signal); our stream waits for it (edl_ps_wait,
+        # bounded) before the update -- the worker never host-synchronises before a push
+        self._push_flag: dict[str, torch.Tensor] = {}
+        self._push_status: dict[str, torch.Tensor] = {}
         self._apply_ev = None      # completion of the newest update of the shard
         self.sparse_optimizer = sparse_optimizer or ("adam" if optimizer == "adam" else "sgd")
         self.sparse_lr = lr if sparse_lr is None else sparse_lr
@@ -119,6 +128,7 @@ class ParameterServer:
         self.stats = {"pushes": 0, "pulls": 0, "applied": 0, "workers": set()}
         self.snapshot = snapshot
         self.snapshot_every = snapshot_every
+        self.push_wait_s = 30.0
         self._srv = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
         self._srv.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
         self._srv.bind((host, port))
@@ -180,13 +190,29 @@ class ParameterServer:
             else:
                 t.pending.append((ids.to(t.w.device), g.to(t.w.device, torch.float32)))
 
+    def _apply_sparse_inbox(self, worker: str, slot: int, async_mode: bool) -> None:
+        """Row-sparse gradients a worker wrote into its sparse inboxes (GPU transport)."""
+        for n, t in self.tables.items():
+            ids, g, cnt = self.sp_inboxes[worker][n][slot]
+            if async_mode:
+                t.step += 1
+                sparse.sparse_inbox_update(t.w, t.m, t.v, ids, g, cnt, kind=self.sparse_optimizer, lr=self.sparse_lr,
+                                           beta1=self.betas[0], beta2=self.betas[1], eps=self.eps, weight_decay=0.0,
+                                           step=t.step, scale=1.0)
+            else:
+                k = int(cnt[0])   # sync rounds wait for every worker anyway: a host read is fine here
+                if k:
+                    t.pending.append((ids[:k].clone(), g[:k].clone()))
+
     def _push(self, worker: str, grads: dict[str, torch.Tensor], inbox: torch.Tensor | None = None,
-              slot: int = 0) -> int:
+              slot: int = 0, sparse_inbox: bool = False) -> int:
         with self.lock:
             st = self.state
             # sparse-table rows are updated below, before _apply: they are part of the
             # snapshot too, so the fence must come first
             self._fence_snapshot()
+            if sparse_inbox:
+                self._apply_sparse_inbox(worker, slot, async_mode=self.mode == "async")
             if inbox is not None and self.mode == "async":
                 # GPU transport: the inbox IS the gradient of this update (no accumulate pass);
                 # its release is an event, waited for only when the worker wants this slot back
@@ -265,6 +291,25 @@ class ParameterServer:
                             self._inbox_ev[wid] = [None, None]
                         desc = {"w": export_tensor(st.w), "inbox": [export_tensor(x) for x in self.inboxes[wid]],
                                 "layout": {n: [st.offsets[n], list(st.shapes[n])] for n in st.names}}
+                        if wid not in self._push_flag:
+                            self._push_flag[wid] = torch.zeros(4, dtype=torch.int32, device=st.device)
+                            self._push_status[wid] = torch.zeros(4, dtype=torch.int32, device=st.device)
+                        desc["flag"] = export_tensor(self._push_flag[wid])
+                        cap = int(hdr.get("sparse_cap", 0))
+                        if self.tables and cap > 0:
+                            if wid not in self.sp_inboxes or any(
+                                    b[0][0].numel() != cap for b in self.sp_inboxes[wid].values()):
+                                dev = st.device
+                                self.sp_inboxes[wid] = {
+                                    n: [(torch.zeros(cap, dtype=torch.int64, device=dev),
+                                         torch.zeros(cap, t.dim, dtype=torch.float32, device=dev),
+                                         torch.zeros(4, dtype=torch.int32, device=dev)) for _ in range(2)]
+                                    for n, t in self.tables.items()}
+                            desc["tables"] = {n: {"w": export_tensor(t.w), "rows": t.rows}
+                                              for n, t in self.tables.items()}
+                            desc["sparse_inbox"] = {n: [[export_tensor(x) for x in b] for b in bufs]
+                                                    for n, bufs in self.sp_inboxes[wid].items()}
+                            desc["sparse_cap"] = cap
                     send_msg(conn, {"ok": True, "ipc": desc, "version": self.version})
                 elif op == "pull_ipc":
                     minv = int(hdr.get("min_version", 0))
@@ -279,7 +324,12 @@ class ParameterServer:
                     send_msg(conn, {"ok": True, "version": ver})
                 elif op == "push_ipc":
                     wid, slot = hdr["worker"], int(hdr.get("slot", 0))
-                    ver = self._push(wid, tensors, inbox=self.inboxes[wid][slot], slot=slot)
+                    if hdr.get("seq") is not None:   # the worker's inbox writes before our reads
+                        dev = self.state.device
+                        sparse.ps_wait(self._push_flag[wid], int(hdr["seq"]), self.push_wait_s,
+                                       self._push_status[wid], torch.cuda.current_stream(dev))
+                    ver = self._push(wid, tensors, inbox=self.inboxes[wid][slot], slot=slot,
+                                     sparse_inbox=bool(hdr.get("sparse_ipc")))
                     with self.lock:
                         other = self._inbox_ev[wid][1 - slot]   # read by the previous push's update
                         mine = self._apply_ev if hdr.get("pull") else None
@@ -288,6 +338,14 @@ class ParameterServer:
                         other.synchronize()
                     if mine is not None:
                         mine.synchronize()   # push + pull in one message: the update is written
+                    if hdr.get("seq") is not None and (other is not None or mine is not None):
+                        # a bounded wait that gave up (a worker killed mid-push): counted
+                        stw = self._push_status[wid]
+                        if int(stw[0]):
+                            self.stats["push_wait_timeouts"] = self.stats.get("push_wait_timeouts", 0) + 1
+                            log.warning("PS %d: push of %s applied after its ordering wait gave up", self.index,
+                                        wid)
+                            stw.zero_()
                     send_msg(conn, {"ok": True, "version": ver})
                 elif op == "push":
                     ver = self._push(hdr.get("worker", "?"), tensors)

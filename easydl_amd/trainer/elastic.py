@@ -758,20 +758,20 @@ class _null:
 
 
 def _retire(comm) -> None:
-    """Let an old epoch's communicator die OFF the training thread.  A ProcessGroupGloo whose
+    """Shorten the teardown of an aborted epoch's gloo groups.  A ProcessGroupGloo whose
     collective was abandoned on a dead peer blocks in its destructor until that collective
-    times out (~120 s measured: the new epoch's first step stalled behind it when the last
-    reference happened to drop in the trainer).  A daemon thread waits until it holds the
-    only reference and then drops it."""
-    import sys as _sys
-    box = [comm]
-
-    def reap():
-        while _sys.getrefcount(box[0]) > 2:   # held by anyone but the box (+ getrefcount's argument)
-            time.sleep(0.05)
-        box.clear()
-
-    threading.Thread(target=reap, name="edl-comm-reaper", daemon=True).start()
+    times out; two survivors dropping their old groups at once can each wait for the other's
+    sockets for the full timeout (~120 s measured: the new epoch's first step stalled).  The
+    groups get a short timeout first, so the abandoned collective fails within seconds."""
+    if not getattr(comm, "aborted", False):
+        return
+    import datetime
+    for pg in (getattr(comm, "data", None), getattr(comm, "ctrl", None)):
+        if isinstance(pg, dist.ProcessGroupGloo):
+            try:
+                pg.set_timeout(datetime.timedelta(seconds=2))
+            except Exception:  # noqa: BLE001 - best effort
+                pass
 
 
 def _is_comm_error(e: Exception) -> bool:

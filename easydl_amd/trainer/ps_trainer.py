@@ -84,6 +84,7 @@ class PSWorker:
                                proc=f"worker{self.ctx.index}")
         self.rdzv = RendezvousClient(self.kv, self.ctx.node_id, {"index": self.ctx.index, "role": "worker"})
         self.client = PSClient(num_ps, store_resolver(self.kv), self.ctx.node_id, transport=_transport(self.device))
+        self._phase_sync = os.environ.get("EDL_PS_PHASE_SYNC", "0") == "1"
         self.client.bind(self.model)
         self.fault = fault.FaultInjector.from_env(self.ctx, self.events)
         self.steps = 0
@@ -112,7 +113,9 @@ class PSWorker:
                     self.model.zero_grad(set_to_none=False)
                     loss = loss_fn(self.model, data.batch(range(b0, min(hi, b0 + batch_size)), self.device))
                     loss.backward()
-                    if self.device.type == "cuda":
+                    if self._phase_sync and self.device.type == "cuda":
+                        # diagnostics only (EDL_PS_PHASE_SYNC=1): exact compute-vs-push split; the GPU
+                        # transport otherwise never host-synchronises inside a step
                         torch.cuda.current_stream(self.device).synchronize()
                     t2 = time.perf_counter()
                     self.client.push(self.model, self.steps, then_pull=fused)

@@ -176,7 +176,14 @@ def main(argv=None) -> int:
     ap.add_argument("--sp", type=int, default=0)
     ap.add_argument("--out", default=None)
     a = ap.parse_args(argv)
-    res = run(a.model, a.tp, a.rank, a.seq, a.mbs, a.accum, a.steps, a.warmup, bool(a.recompute), bool(a.sp))
+    try:
+        res = run(a.model, a.tp, a.rank, a.seq, a.mbs, a.accum, a.steps, a.warmup, bool(a.recompute), bool(a.sp))
+    except torch.OutOfMemoryError as e:   # the answer for this configuration: it does not fit
+        res = {"model": a.model, "tp": a.tp, "seq_len": a.seq, "micro_batch": a.mbs, "grad_accum": a.accum,
+               "recompute": bool(a.recompute), "oom": True,
+               "peak_alloc_gb": round(torch.cuda.max_memory_allocated() / 2**30, 2),
+               "hbm_gb": round(torch.cuda.get_device_properties(0).total_memory / 2**30, 1),
+               "error": str(e).splitlines()[0][:300]}
     line = json.dumps(res)
     print(line, flush=True)
     if a.out:
