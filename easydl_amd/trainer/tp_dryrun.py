@@ -68,22 +68,25 @@ class LoopbackComm:
 
 
 def run(model: str, tp: int, rank: int, seq: int, mbs: int, accum: int, steps: int, warmup: int, recompute: bool,
-        sp: bool = False) -> dict:
+        sp: bool = False, device: str = "cuda") -> dict:
     from easydl_amd.ckpt.manager import CheckpointManager, shard_layout
     from easydl_amd.models.llama import get_config
     from easydl_amd.optim import FlatAdamW
     from easydl_amd.parallel.flat import FlatBuffers, FlatParams
     from easydl_amd.parallel.tp import LlamaTP, TPGroup
 
-    dev = torch.device("cuda", 0)
-    torch.cuda.set_device(dev)
-    torch.cuda.reset_peak_memory_stats(dev)
+    cuda = device == "cuda"
+    dev = torch.device("cuda", 0) if cuda else torch.device("cpu")
+    if cuda:
+        torch.cuda.set_device(dev)
+        torch.cuda.reset_peak_memory_stats(dev)
+    sync = (lambda: torch.cuda.synchronize(dev)) if cuda else (lambda: None)  # noqa: E731
     cfg = get_config(model, recompute=recompute)
     comm = LoopbackComm(tp, rank, dev)
     g = TPGroup(comm, sequence_parallel=sp)
     torch.manual_seed(1009 * rank)
     t0 = time.perf_counter()
-    m = LlamaTP(cfg, g, device=dev, dtype=torch.bfloat16)
+    m = LlamaTP(cfg, g, device=dev, dtype=torch.bfloat16 if cuda else torch.float32)
     flat = FlatParams(m, weight_decay=0.1)
     bufs = FlatBuffers(m)
     opt = FlatAdamW(flat, lr=3e-4, betas=(0.9, 0.95), weight_decay=0.1, max_grad_norm=1.0)
@@ -93,9 +96,11 @@ def run(model: str, tp: int, rank: int, seq: int, mbs: int, accum: int, steps: i
         w.append(1.0 / tp if rep.pop() else 1.0)
     opt.norm_weights = w
     opt.norm_reduce = lambda t: comm.all_reduce(t)
-    torch.cuda.synchronize(dev)
+    sync()
     build_s = time.perf_counter() - t0
-    state_gb = torch.cuda.memory_allocated(dev) / 2**30
+    state_gb = (torch.cuda.memory_allocated(dev) if cuda else
+                sum(t.numel() * t.element_size() for t in list(m.parameters()) + [grp.grad for grp in flat.groups]
+                    + list(opt.state_tensors().values()))) / 2**30
     ids = [torch.randint(0, cfg.vocab_size, (mbs, seq), device=dev) for _ in range(accum)]
 
     def step():
@@ -111,12 +116,12 @@ def run(model: str, tp: int, rank: int, seq: int, mbs: int, accum: int, steps: i
 
     for _ in range(warmup):
         step()
-    torch.cuda.synchronize(dev)
+    sync()
     comm.bytes = 0
     t1 = time.perf_counter()
     for _ in range(steps):
         loss = step()
-    torch.cuda.synchronize(dev)
+    sync()
     dt = (time.perf_counter() - t1) / steps
     tokens = mbs * seq * accum                       # per model replica (= per TP group) per step
     fpt = cfg.flops_per_token(seq)
@@ -139,9 +144,9 @@ def run(model: str, tp: int, rank: int, seq: int, mbs: int, accum: int, steps: i
         "model": model, "tp": tp, "rank": rank, "seq_len": seq, "micro_batch": mbs, "grad_accum": accum,
         "recompute": recompute, "sequence_parallel": sp, "layers": cfg.n_layers,
         "params_per_rank": flat.num_params(), "state_gb": round(state_gb, 2),
-        "peak_alloc_gb": round(torch.cuda.max_memory_allocated(dev) / 2**30, 2),
-        "peak_reserved_gb": round(torch.cuda.max_memory_reserved(dev) / 2**30, 2),
-        "hbm_gb": round(torch.cuda.get_device_properties(dev).total_memory / 2**30, 1),
+        "peak_alloc_gb": round(torch.cuda.max_memory_allocated(dev) / 2**30, 2) if cuda else None,
+        "peak_reserved_gb": round(torch.cuda.max_memory_reserved(dev) / 2**30, 2) if cuda else None,
+        "hbm_gb": round(torch.cuda.get_device_properties(dev).total_memory / 2**30, 1) if cuda else None,
         "build_s": round(build_s, 2), "ms_per_step": round(dt * 1e3, 1), "steps": steps, "warmup": warmup,
         "tokens_per_step_per_replica": tokens,
         "projected_tokens_per_s_per_gpu": round(tokens / dt / tp, 1),
@@ -149,6 +154,7 @@ def run(model: str, tp: int, rank: int, seq: int, mbs: int, accum: int, steps: i
         "tp_collective_bytes_per_step_per_rank": comm.bytes // max(1, steps),
         "loss": round(float(loss.detach()) * accum, 4),
         "snapshot": {"full_gb": round(full / 2**30, 2), "lean_gb": round(lean / 2**30, 2),
+                     "full_bytes": int(full), "lean_bytes": int(lean),
                      "host_budget_gb_per_rank": budget, "ranks_per_node": tp, "mode": mode,
                      "mem_available_gb": round(_mem_available() / 2**30, 1)},
     }
@@ -175,9 +181,11 @@ def main(argv=None) -> int:
     ap.add_argument("--recompute", type=int, default=1)
     ap.add_argument("--sp", type=int, default=0)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"])
     a = ap.parse_args(argv)
     try:
-        res = run(a.model, a.tp, a.rank, a.seq, a.mbs, a.accum, a.steps, a.warmup, bool(a.recompute), bool(a.sp))
+        res = run(a.model, a.tp, a.rank, a.seq, a.mbs, a.accum, a.steps, a.warmup, bool(a.recompute), bool(a.sp),
+                  a.device)
     except torch.OutOfMemoryError as e:   # the answer for this configuration: it does not fit
         res = {"model": a.model, "tp": a.tp, "seq_len": a.seq, "micro_batch": a.mbs, "grad_accum": a.accum,
                "recompute": bool(a.recompute), "oom": True,

@@ -9,3 +9,5 @@ EDL_TTR_KEEP=1 EDL_TTR_DIR=gpurun_out/ttr_n1 timeout -k 10 400 python -u bench.p
     --mbs 1 --accum 1 --steps 4 --warmup 3 --fault-step 4 > gpurun_out/r04_ttr_n1.log 2>&1
 EDL_STANDBY_PREMAP=1 EDL_TTR_KEEP=1 EDL_TTR_DIR=gpurun_out/ttr_n1 timeout -k 10 400 python -u bench.py --fault-inject \
     --gpus 1 --mbs 1 --accum 1 --steps 4 --warmup 3 --fault-step 4 > gpurun_out/r04_ttr_n1_premap.log 2>&1
+# config 4 re-measured (BERT-large async PS, 2 PS + 6 workers on one GPU, IPC transport, flag-ordered pushes)
+timeout -k 10 580 bash scripts/bert_ps_1gpu.sh > gpurun_out/r04_bert_ps.log 2>&1

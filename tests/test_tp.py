@@ -96,3 +96,16 @@ def test_vocab_parallel_xent_kernel_matches_dense(cuda, tp):
         g = grads[r].float()
         gr = ref_in.grad[:, r * vs:(r + 1) * vs]
         assert (g - gr).abs().max().item() < 2e-3, (g - gr).abs().max().item()
+
+
+def test_tp_shard_dry_run_on_cpu(tmp_path):
+    """trainer/tp_dryrun.py (config-5 sizing): one TP shard at full depth against a loopback
+    TP group -- here a tiny Llama on the CPU, with and without recompute: real steps, the
+    TP collective bytes a real group would move, and the snapshot-mode decision."""
+    from easydl_amd.trainer import tp_dryrun
+    for rc in (True, False):
+        r = tp_dryrun.run("llama-tiny", 2, 1, 32, 2, 2, 2, 1, rc, device="cpu")
+        assert r["recompute"] == rc and r["layers"] == 2 and r["ms_per_step"] > 0
+        assert r["tp_collective_bytes_per_step_per_rank"] > 0
+        assert r["snapshot"]["mode"] in ("full", "lean", "off") and r["snapshot"]["full_bytes"] > r["snapshot"]["lean_bytes"]
+        assert r["loss"] == r["loss"]
