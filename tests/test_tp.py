@@ -107,5 +107,6 @@ def test_tp_shard_dry_run_on_cpu(tmp_path):
         r = tp_dryrun.run("llama-tiny", 2, 1, 32, 2, 2, 2, 1, rc, device="cpu")
         assert r["recompute"] == rc and r["layers"] == 2 and r["ms_per_step"] > 0
         assert r["tp_collective_bytes_per_step_per_rank"] > 0
-        assert r["snapshot"]["mode"] in ("full", "lean", "off") and r["snapshot"]["full_bytes"] > r["snapshot"]["lean_bytes"]
+        snap = r["snapshot"]
+        assert snap["mode"] in ("full", "lean", "off") and snap["full_bytes"] > snap["lean_bytes"]
         assert r["loss"] == r["loss"]
