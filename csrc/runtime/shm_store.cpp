@@ -573,6 +573,133 @@ int edl_ckpt_restore_pipelined(void* seg, int slot, int nbuf, const uint64_t* de
   return (int)err;
 }
 
+// Restore, v2: a persistent pool of `threads` copy threads (one stripe of every chunk each)
+// and `stages` pinned staging buffers; chunk c is copied into stage c % stages while the DMA
+// of the previous chunks drains.  stats (may be null) receives {copy_s, dma_wait_s, total_s,
+// bytes}: where the time goes (host memcpy out of the shm pages vs waiting for the H2D
+// engine), so the restore can be tuned from a measurement.  Blocks until done.
+static double now_s() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return ts.tv_sec + ts.tv_nsec * 1e-9;
+}
+
+int edl_ckpt_restore_pipelined2(void* seg, int slot, int nbuf, const uint64_t* dev_ptrs, const uint64_t* sizes,
+                                const uint64_t* offsets, hipStream_t stream, uint64_t chunk, int threads, int stages,
+                                double* stats) {
+  auto* s = static_cast<Seg*>(seg);
+  if (slot < 0) slot = edl_shm_current(s);
+  if (slot < 0) return -1;
+  if (chunk == 0) chunk = 128ull << 20;
+  if (threads <= 0) threads = 16;
+  if (stages < 2) stages = 2;
+  if (stages > 8) stages = 8;
+  const double t_start = now_s();
+  std::vector<void*> stage(stages, nullptr);
+  std::vector<hipEvent_t> ev(stages, nullptr);
+  std::vector<bool> used(stages, false);
+  hipError_t err = hipSuccess;
+  for (int i = 0; i < stages && err == hipSuccess; ++i) {
+    err = hipHostMalloc(&stage[i], chunk, hipHostMallocDefault);
+    if (err == hipSuccess) err = hipEventCreateWithFlags(&ev[i], hipEventDisableTiming);
+  }
+  // the work list: (src, dst device pointer, bytes) per chunk
+  struct Piece {
+    const uint8_t* src;
+    uint8_t* dst;
+    uint64_t n;
+  };
+  std::vector<Piece> pieces;
+  const uint8_t* base = s->data(slot);
+  for (int b = 0; b < nbuf; ++b)
+    for (uint64_t off = 0; off < sizes[b]; off += chunk)
+      pieces.push_back({base + offsets[b] + off, (uint8_t*)dev_ptrs[b] + off,
+                        sizes[b] - off < chunk ? sizes[b] - off : chunk});
+  // persistent copy pool: generation-numbered jobs, one stripe per thread
+  std::mutex mu;
+  std::condition_variable cv_job, cv_done;
+  uint64_t gen = 0;
+  int pending = 0;
+  bool stop = false;
+  const uint8_t* job_src = nullptr;
+  uint8_t* job_dst = nullptr;
+  uint64_t job_n = 0;
+  std::vector<std::thread> pool;
+  for (int t = 0; t < threads && err == hipSuccess; ++t) {
+    pool.emplace_back([&, t] {
+      uint64_t seen = 0;
+      for (;;) {
+        const uint8_t* src;
+        uint8_t* dst;
+        uint64_t n;
+        {
+          std::unique_lock<std::mutex> lk(mu);
+          cv_job.wait(lk, [&] { return stop || gen != seen; });
+          if (stop) return;
+          seen = gen;
+          src = job_src;
+          dst = job_dst;
+          n = job_n;
+        }
+        const uint64_t per = ((n + threads - 1) / threads + 63) & ~uint64_t(63);
+        const uint64_t lo = per * t;
+        if (lo < n) memcpy(dst + lo, src + lo, (lo + per > n) ? n - lo : per);
+        {
+          std::lock_guard<std::mutex> lk(mu);
+          if (--pending == 0) cv_done.notify_one();
+        }
+      }
+    });
+  }
+  double copy_s = 0.0, wait_s = 0.0;
+  uint64_t bytes = 0;
+  for (size_t c = 0; c < pieces.size() && err == hipSuccess; ++c) {
+    const int k = (int)(c % stages);
+    if (used[k]) {
+      const double t0 = now_s();
+      err = hipEventSynchronize(ev[k]);  // staging buffer k free again
+      wait_s += now_s() - t0;
+      if (err != hipSuccess) break;
+    }
+    const double t0 = now_s();
+    {
+      std::unique_lock<std::mutex> lk(mu);
+      job_src = pieces[c].src;
+      job_dst = (uint8_t*)stage[k];
+      job_n = pieces[c].n;
+      pending = threads;
+      ++gen;
+      cv_job.notify_all();
+      cv_done.wait(lk, [&] { return pending == 0; });
+    }
+    copy_s += now_s() - t0;
+    err = hipMemcpyAsync(pieces[c].dst, stage[k], pieces[c].n, hipMemcpyHostToDevice, stream);
+    if (err == hipSuccess) err = hipEventRecord(ev[k], stream);
+    used[k] = true;
+    bytes += pieces[c].n;
+  }
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    stop = true;
+  }
+  cv_job.notify_all();
+  for (auto& th : pool) th.join();
+  const double t0 = now_s();
+  if (err == hipSuccess) err = hipStreamSynchronize(stream);
+  wait_s += now_s() - t0;
+  for (int i = 0; i < stages; ++i) {
+    if (ev[i]) hipEventDestroy(ev[i]);
+    if (stage[i]) hipHostFree(stage[i]);
+  }
+  if (stats) {
+    stats[0] = copy_s;
+    stats[1] = wait_s;
+    stats[2] = now_s() - t_start;
+    stats[3] = (double)bytes;
+  }
+  return (int)err;
+}
+
 void edl_ckpt_engine_destroy(void* eng) {
   auto* e = static_cast<Engine*>(eng);
   if (!e) return;

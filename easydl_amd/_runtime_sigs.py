@@ -49,6 +49,8 @@ SIGS = {
     "edl_ckpt_restore": (i32, [vp, i32, i32, u64p, u64p, u64p, vp]),
     "edl_ckpt_engine_destroy": (None, [vp]),
     "edl_ckpt_restore_pipelined": (i32, [vp, i32, i32, u64p, u64p, u64p, vp, u64, i32]),
+    "edl_ckpt_restore_pipelined2": (i32, [vp, i32, i32, u64p, u64p, u64p, vp, u64, i32, i32,
+                                          ctypes.POINTER(ctypes.c_double)]),
     "edl_stream_create_cumask": (vp, [i32, ctypes.POINTER(ctypes.c_uint32), i32, i32]),
     "edl_stream_destroy": (i32, [vp]),
     "edl_roctx_available": (i32, []),

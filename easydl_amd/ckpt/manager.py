@@ -753,6 +753,9 @@ def _load_host_state(trainer, h) -> None:
         fn(h)
 
 
+LAST_RESTORE_STATS: dict = {}   # where the newest shm -> HBM restore spent its time (copy vs DMA wait)
+
+
 def _load_shard(read, table, state, dev, expect: int, what: str, seg=None, slot=None) -> None:
     """Copy one shard's tensor slices to their device buffers and verify the checksum
     (on the GPU for device tensors: no host pass over tens of GB).  From a shm
@@ -772,8 +775,19 @@ def _load_shard(read, table, state, dev, expect: int, what: str, seg=None, slot=
                 items.append((dst, off))
         n = len(ptrs)
         arr = lambda v: (ctypes.c_uint64 * n)(*v)  # noqa: E731
-        rc = _native.runtime()("edl_ckpt_restore_pipelined", seg.h, slot, n, arr(ptrs), arr(sizes), arr(offs),
-                               ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream), 256 << 20, 16)
+        stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        if os.environ.get("EDL_RESTORE_V1") == "1":   # A/B: per-chunk threads, 2 stages of 256 MiB
+            rc = _native.runtime()("edl_ckpt_restore_pipelined", seg.h, slot, n, arr(ptrs), arr(sizes), arr(offs),
+                                   stream, 256 << 20, 16)
+        else:
+            st = (ctypes.c_double * 4)()
+            rc = _native.runtime()("edl_ckpt_restore_pipelined2", seg.h, slot, n, arr(ptrs), arr(sizes), arr(offs),
+                                   stream, int(os.environ.get("EDL_RESTORE_CHUNK_MB", 128)) << 20,
+                                   int(os.environ.get("EDL_RESTORE_THREADS", 16)),
+                                   int(os.environ.get("EDL_RESTORE_STAGES", 4)), st)
+            LAST_RESTORE_STATS.update(copy_s=round(st[0], 3), dma_wait_s=round(st[1], 3), total_s=round(st[2], 3),
+                                      gb=round(st[3] / 2**30, 2),
+                                      gbps=round(st[3] / 2**30 / max(st[2], 1e-9), 1))
         if rc != 0:
             raise RuntimeError(f"pipelined restore failed: hipError {rc}")
         for dst, off in items:

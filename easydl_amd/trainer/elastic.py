@@ -490,7 +490,9 @@ class ElasticTrainer:
         t0 = time.perf_counter()
         st = self.checkpoint.restore_latest(self)
         if st is not None:
-            self.events.emit("restored", step=self.step, source=st, s=round(time.perf_counter() - t0, 3))
+            from easydl_amd.ckpt import manager as _ckm
+            self.events.emit("restored", step=self.step, source=st, s=round(time.perf_counter() - t0, 3),
+                             h2d=dict(_ckm.LAST_RESTORE_STATS))
 
     # ------------------------------------------------------------------ steps
     def _micro_batches(self, data, plan: ElasticBatchPlan):
