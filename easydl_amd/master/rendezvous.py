@@ -30,6 +30,7 @@ transfer at all.
 """
 from __future__ import annotations
 
+import datetime
 import json
 import logging
 import os
@@ -354,16 +355,32 @@ class RendezvousClient:
         agreed runtime-plan version is left in ``self.plan_version``.
         """
         dkey = f"decision/{epoch}/{step}"
+        known = None   # the decision, when this rank's own compare_set already returned it
         if ok:
             c = self.kv.add(f"commit/{epoch}/{step}", 1)
             if c >= world:
-                self.kv.compare_set(dkey, "", self._decision("commit"))
+                known = self.kv.compare_set(dkey, "", self._decision("commit"))
         else:
-            self.kv.compare_set(dkey, "", self._decision("abort"))
+            known = self.kv.compare_set(dkey, "", self._decision("abort"))
+        if known:   # compare_set returns the stored value: ours, or the one that won the race
+            kind, e, pv = known.split(":")
+            self.plan_version = int(pv)
+            if gc and step >= 2:
+                self.kv.delete(f"commit/{epoch}/{step - 2}")
+                self.kv.delete(f"decision/{epoch}/{step - 2}")
+            return kind == "commit", int(e)
         t_end = time.monotonic() + timeout_s
-        poll = 0.0002
+        # server-side wait: the store answers the moment the decision key is written (a
+        # polling loop answered 0.5-0.7 ms late, profiles/r04_commit_latency.txt); between
+        # short waits the epoch's abort flag is checked, so a dead peer still breaks the wait
+        slice_td = datetime.timedelta(milliseconds=20)
         while True:
-            if self.kv.exists(dkey):
+            try:
+                self.kv.store.wait([dkey], slice_td)
+                ready = True
+            except Exception:  # noqa: BLE001 - the store signals the timeout by raising
+                ready = False
+            if ready:
                 d = self.kv.get_str(dkey)
                 kind, e, pv = d.split(":")
                 self.plan_version = int(pv)
@@ -377,5 +394,3 @@ class RendezvousClient:
                 continue
             if time.monotonic() > t_end:
                 raise TimeoutError(f"commit of step {step} in epoch {epoch} timed out")
-            time.sleep(poll)
-            poll = min(poll * 2, 0.005)
