@@ -600,6 +600,8 @@ class CheckpointManager:
         # Drain this rank's in-flight snapshot first: its D2H reads the very buffers the
         # restore is about to overwrite, and its commit must not publish a slot that
         # mixes pre- and post-rollback bytes under a pre-restore checksum.
+        t_start = time.perf_counter()
+        LAST_RESTORE_STATS.clear()
         self.wait()
         tag = self._tag(trainer)
         found = self.find_latest(tag, max_step)
@@ -608,16 +610,27 @@ class CheckpointManager:
                 return self.load_dir_latest(trainer)
             return None
         world, step, infos = found
+        t0 = time.perf_counter()
         state = dict(self.state_of(trainer))
         dev = next(iter(state.values())).device
+        phases = {"find_s": round(t0 - t_start, 3)}
         for s, info in enumerate(infos):
+            t1 = time.perf_counter()
             seg = _open_segment(self.seg_name(world, s, tag))
+            phases["open_s"] = round(phases.get("open_s", 0) + time.perf_counter() - t1, 3)
             try:
                 _load_shard(lambda off, nb: seg.view(info["slot"], off, nb), info["meta"]["t"], state, dev,
                             info["checksum"], f"shm shard {s} of step {step}", seg=seg, slot=info["slot"])
             finally:
-                seg.close()
+                # unmapping tens of GB of populated shm pages takes seconds of page-table teardown:
+                # nothing reads the mapping any more, so it is closed off the recovery path
+                threading.Thread(target=seg.close, name="edl-shm-unmap", daemon=True).start()
+        t2 = time.perf_counter()
         self.finish_restore(trainer)
+        if dev.type == "cuda":
+            torch.cuda.current_stream(dev).synchronize()
+        phases["finish_s"] = round(time.perf_counter() - t2, 3)
+        LAST_RESTORE_STATS.update(phases)
         meta = infos[0]["meta"]
         self._restore_scalars(trainer, meta)
         _load_host_state(trainer, meta.get("host"))
@@ -790,9 +803,11 @@ def _load_shard(read, table, state, dev, expect: int, what: str, seg=None, slot=
                                       gbps=round(st[3] / 2**30 / max(st[2], 1e-9), 1))
         if rc != 0:
             raise RuntimeError(f"pipelined restore failed: hipError {rc}")
+        t_cs = time.perf_counter()
         for dst, off in items:
             checksum_tensor(dst, acc, base_index=off // 4)
         got = int(acc.item()) & ((1 << 64) - 1)
+        LAST_RESTORE_STATS["checksum_s"] = round(time.perf_counter() - t_cs, 3)
         if got != expect:
             raise RuntimeError(f"checksum mismatch in {what}: {got:#x} != {expect:#x}")
         return

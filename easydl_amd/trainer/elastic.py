@@ -114,6 +114,7 @@ class ElasticTrainer:
         self.assignment = None
         self.checkpoint = checkpoint
         self.log_every = log_every
+        self._phases = os.environ.get("EDL_STEP_PHASES", "0") == "1"
         self.rdzv_config = rdzv_config
         self._store = store
         self._manager = None
@@ -617,7 +618,9 @@ class ElasticTrainer:
                 try:
                     self.fault.maybe_inject("step_start", self.step, trainer=self)
                     loss = self._run_step(loss_fn, data, plan)
+                    t_run = time.perf_counter()
                     ok = self._sync_point()
+                    t_sync = time.perf_counter()
                 except CommAborted as e:
                     log.warning("step %d aborted: %s", self.step, e)
                     ok = False
@@ -632,12 +635,21 @@ class ElasticTrainer:
                                                      gc=self.comm.rank == 0)
                 else:
                     apply, latest = ok, 0
+                t_commit = time.perf_counter()
                 if apply:
                     if self.checkpoint is not None:
                         self.checkpoint.fence()  # never update params under an in-flight snapshot
+                    t_fence = time.perf_counter()
                     with trace.range("optimizer"):
                         self.opt.step(pre_scale=1.0)
                     self._sync_buffers()
+                    if self._phases and ok:
+                        # host-side split of one step (EDL_STEP_PHASES=1): enqueue of the micro-batches,
+                        # wait for the GPU (compute + all-reduce), commit round, snapshot fence, optimizer
+                        self.events.emit("step_phases", step=self.step + 1, run=round(t_run - t0, 4),
+                                         sync=round(t_sync - t_run, 4), commit=round(t_commit - t_sync, 4),
+                                         fence=round(t_fence - t_commit, 4),
+                                         opt=round(time.perf_counter() - t_fence, 4))
                     self.step += 1
                     self.last_loss = loss
                     rec = {"step": self.step, "epoch": self.comm.epoch, "world": self.comm.world_size,
