@@ -203,7 +203,8 @@ def main():
         "time_to_recover_s": None,
         "ckpt": None if ckpt is None else {
             "interval": args.ckpt_interval, "snapshots": ckpt.stats["snapshots"],
-            "bytes_per_snapshot": ckpt.stats["d2h_bytes"] // max(1, ckpt.stats["snapshots"])},
+            "bytes_per_snapshot": ckpt.stats["d2h_bytes"] // max(1, ckpt.stats["snapshots"]),
+            "pinned": ckpt.pin, "staged_last": ckpt.stats.get("staged_last")},
     }
     if comm.rank == 0:
         line = json.dumps(res)

@@ -223,7 +223,7 @@ __global__ void sparse_push_counts_kernel(const int* __restrict__ cnt, int P, co
   if (p < P) *reinterpret_cast<int*>(inbox_cnt[p]) = (int)min((int64_t)cnt[p], cap);
 }
 
-// Push ordering without a host sync on the worker.  The worker's stream, after its inbox
+// Push ordering on the device.  The worker's stream, after its inbox
 // writes, runs ps_signal: a system-scope release store of the push sequence number into a
 // flag word in the PS's HBM (IPC-mapped).  The PS's stream runs ps_wait before the update
 // that reads the inboxes: one thread spins on a system-scope acquire load of that word,

@@ -84,6 +84,74 @@ int64_t now_ns() {
 
 uint64_t round_up(uint64_t v, uint64_t a) { return (v + a - 1) / a * a; }
 
+double now_s() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return ts.tv_sec + ts.tv_nsec * 1e-9;
+}
+
+// Persistent memcpy threads: run() splits one copy into one 64-byte-aligned stripe per
+// thread and returns when every stripe is done.  Host DRAM <-> pinned staging copies of
+// tens of GB need many cores: one thread moves ~6-10 GB/s out of shm pages.
+class CopyPool {
+ public:
+  explicit CopyPool(int threads) : n_(threads < 1 ? 1 : threads) {
+    for (int t = 0; t < n_; ++t) th_.emplace_back([this, t] { loop(t); });
+  }
+  ~CopyPool() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_job_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  void run(uint8_t* dst, const uint8_t* src, uint64_t n) {
+    std::unique_lock<std::mutex> lk(mu_);
+    dst_ = dst;
+    src_ = src;
+    len_ = n;
+    pending_ = n_;
+    ++gen_;
+    cv_job_.notify_all();
+    cv_done_.wait(lk, [&] { return pending_ == 0; });
+  }
+
+ private:
+  void loop(int t) {
+    uint64_t seen = 0;
+    for (;;) {
+      uint8_t* dst;
+      const uint8_t* src;
+      uint64_t n;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_job_.wait(lk, [&] { return stop_ || gen_ != seen; });
+        if (stop_) return;
+        seen = gen_;
+        dst = dst_;
+        src = src_;
+        n = len_;
+      }
+      const uint64_t per = ((n + n_ - 1) / n_ + 63) & ~uint64_t(63);
+      const uint64_t lo = per * t;
+      if (lo < n) memcpy(dst + lo, src + lo, (lo + per > n) ? n - lo : per);
+      std::lock_guard<std::mutex> lk(mu_);
+      if (--pending_ == 0) cv_done_.notify_one();
+    }
+  }
+  const int n_;
+  std::vector<std::thread> th_;
+  std::mutex mu_;
+  std::condition_variable cv_job_, cv_done_;
+  uint64_t gen_ = 0;
+  int pending_ = 0;
+  bool stop_ = false;
+  uint8_t* dst_ = nullptr;
+  const uint8_t* src_ = nullptr;
+  uint64_t len_ = 0;
+};
+
 }  // namespace
 
 extern "C" {
@@ -335,6 +403,10 @@ struct Job {
   int64_t checksum_off;
   std::string meta;
   hipEvent_t done;
+  // staged form (slot not page-locked): the worker thread copies through pinned stages
+  bool staged = false;
+  hipEvent_t ready = nullptr;
+  std::vector<uint64_t> ptrs, sizes, offs;
 };
 
 struct Engine {
@@ -343,13 +415,89 @@ struct Engine {
   std::thread committer;
   std::mutex mu;
   std::condition_variable cv;
+  std::condition_variable cv_reads;      // staged jobs: device reads finished
   std::deque<Job> queue;
   std::map<int64_t, int> status;         // 0 pending, 1 committed, <0 error
   std::map<int64_t, hipEvent_t> events;  // completion events (for fences)
+  std::map<int64_t, bool> reads;         // staged tickets: true once every D2H has landed
   int64_t next = 1;
   bool stop = false;
   uint64_t chunk = 256ull << 20;
+  // staged snapshots: pinned staging ring + memcpy pool, created at the first staged job
+  uint64_t stage_bytes = 128ull << 20;
+  int nstage = 4;
+  int threads = 16;
+  std::vector<void*> stage;
+  std::vector<hipEvent_t> sev;
+  CopyPool* pool = nullptr;
+  double last_staged[4] = {0, 0, 0, 0};  // d2h_wait_s, copy_s, total_s, bytes of the last staged job
 };
+
+// Device buffers -> (pageable) slot through the pinned staging ring: D2H of chunk c into
+// stage c % S on the (CU-masked) side stream while the pool copies an earlier stage out to
+// the shm pages.  Marks the ticket's device reads done as soon as the last D2H has landed
+// (fences wait for that, not for the host copies), then returns after the last host copy.
+hipError_t run_staged(Engine* e, Job& j) {
+  hipError_t err = hipSuccess;
+  if (!e->pool) {
+    e->stage.assign(e->nstage, nullptr);
+    e->sev.assign(e->nstage, nullptr);
+    for (int i = 0; i < e->nstage && err == hipSuccess; ++i) {
+      err = hipHostMalloc(&e->stage[i], e->stage_bytes, hipHostMallocDefault);
+      if (err == hipSuccess) err = hipEventCreateWithFlags(&e->sev[i], hipEventDisableTiming);
+    }
+    if (err != hipSuccess) return err;
+    e->pool = new CopyPool(e->threads);
+  }
+  struct Piece {
+    const uint8_t* src;
+    uint8_t* dst;
+    uint64_t n;
+  };
+  std::vector<Piece> pieces;
+  uint8_t* base = j.seg->data(j.slot);
+  for (size_t b = 0; b < j.ptrs.size(); ++b)
+    for (uint64_t off = 0; off < j.sizes[b]; off += e->stage_bytes)
+      pieces.push_back({(const uint8_t*)j.ptrs[b] + off, base + j.offs[b] + off,
+                        j.sizes[b] - off < e->stage_bytes ? j.sizes[b] - off : e->stage_bytes});
+  const double t_start = now_s();
+  double wait_s = 0, copy_s = 0;
+  uint64_t bytes = 0;
+  const size_t S = (size_t)e->nstage, P = pieces.size();
+  err = hipStreamWaitEvent(e->side, j.ready, 0);
+  auto drain = [&](size_t c) {  // stage c % S holds piece c: wait for its D2H, copy it out
+    const int k = (int)(c % S);
+    double t0 = now_s();
+    hipError_t r = hipEventSynchronize(e->sev[k]);
+    wait_s += now_s() - t0;
+    if (r != hipSuccess) return r;
+    if (c + 1 == P) {  // every device read has landed: release the fence before the host copy
+      std::lock_guard<std::mutex> g(e->mu);
+      e->reads[j.ticket] = true;
+      e->cv_reads.notify_all();
+    }
+    t0 = now_s();
+    e->pool->run(pieces[c].dst, (const uint8_t*)e->stage[k], pieces[c].n);
+    copy_s += now_s() - t0;
+    bytes += pieces[c].n;
+    return hipSuccess;
+  };
+  for (size_t c = 0; c < P && err == hipSuccess; ++c) {
+    const int k = (int)(c % S);
+    if (c >= S) err = drain(c - S);
+    if (err == hipSuccess) err = hipMemcpyAsync(e->stage[k], pieces[c].src, pieces[c].n, hipMemcpyDeviceToHost,
+                                                e->side);
+    if (err == hipSuccess) err = hipEventRecord(e->sev[k], e->side);
+  }
+  for (size_t c = P > S ? P - S : 0; c < P && err == hipSuccess; ++c) err = drain(c);
+  if (P == 0 && err == hipSuccess) err = hipStreamSynchronize(e->side);
+  std::lock_guard<std::mutex> g(e->mu);
+  e->last_staged[0] = wait_s;
+  e->last_staged[1] = copy_s;
+  e->last_staged[2] = now_s() - t_start;
+  e->last_staged[3] = (double)bytes;
+  return err;
+}
 
 void commit_loop(Engine* e) {
   hipSetDevice(e->device);
@@ -362,7 +510,8 @@ void commit_loop(Engine* e) {
       j = e->queue.front();
       e->queue.pop_front();
     }
-    hipError_t err = hipEventSynchronize(j.done);
+    hipError_t err = j.staged ? run_staged(e, j) : hipEventSynchronize(j.done);
+    if (j.ready) hipEventDestroy(j.ready);
     int st = 1;
     if (err != hipSuccess) {
       st = -(int)err;
@@ -373,6 +522,10 @@ void commit_loop(Engine* e) {
     }
     std::lock_guard<std::mutex> g(e->mu);
     e->status[j.ticket] = st;
+    if (j.staged) {
+      e->reads[j.ticket] = true;  // also on failure: a fence never waits forever
+      e->cv_reads.notify_all();
+    }
   }
 }
 
@@ -442,6 +595,27 @@ int64_t edl_ckpt_snapshot(void* eng, void* seg, int nbuf, const uint64_t* dev_pt
     if (offsets[i] + sizes[i] > total) total = offsets[i] + sizes[i];
   }
   int slot = edl_shm_begin(s);
+  if (!s->pinned) {
+    // pageable slot: the worker thread streams it through the pinned staging ring
+    Job j{0, s, slot, step, epoch, total, checksum_off, meta ? meta : "", nullptr};
+    j.staged = true;
+    hipError_t err = hipEventCreateWithFlags(&j.ready, hipEventDisableTiming);
+    if (err == hipSuccess) err = hipEventRecord(j.ready, after_stream);
+    if (err != hipSuccess) {
+      if (j.ready) hipEventDestroy(j.ready);
+      return -(int64_t)err;
+    }
+    j.ptrs.assign(dev_ptrs, dev_ptrs + nbuf);
+    j.sizes.assign(sizes, sizes + nbuf);
+    j.offs.assign(offsets, offsets + nbuf);
+    std::lock_guard<std::mutex> g(e->mu);
+    j.ticket = e->next++;
+    e->status[j.ticket] = 0;
+    e->reads[j.ticket] = false;
+    e->queue.push_back(std::move(j));
+    e->cv.notify_one();
+    return e->next - 1;
+  }
   hipEvent_t ready, done;
   hipEventCreateWithFlags(&ready, hipEventDisableTiming);
   hipEventCreateWithFlags(&done, hipEventDisableTiming);
@@ -475,7 +649,14 @@ int edl_ckpt_fence(void* eng, int64_t ticket, hipStream_t stream) {
   auto* e = static_cast<Engine*>(eng);
   hipEvent_t ev = nullptr;
   {
-    std::lock_guard<std::mutex> g(e->mu);
+    std::unique_lock<std::mutex> g(e->mu);
+    auto rd = e->reads.find(ticket);
+    if (rd != e->reads.end()) {
+      // staged snapshot: its D2H copies are issued by the worker thread as stages free up,
+      // so there is no event to chain the stream on; wait on the host for the last one
+      e->cv_reads.wait(g, [&] { return rd->second; });
+      return 0;
+    }
     auto it = e->events.find(ticket);
     if (it == e->events.end()) return 0;
     ev = it->second;
@@ -496,6 +677,7 @@ int edl_ckpt_status(void* eng, int64_t ticket) {
       hipEventDestroy(ev->second);
       e->events.erase(ev);
     }
+    e->reads.erase(ticket);
     e->status.erase(it);
   }
   return st;
@@ -578,12 +760,6 @@ int edl_ckpt_restore_pipelined(void* seg, int slot, int nbuf, const uint64_t* de
 // of the previous chunks drains.  stats (may be null) receives {copy_s, dma_wait_s, total_s,
 // bytes}: where the time goes (host memcpy out of the shm pages vs waiting for the H2D
 // engine), so the restore can be tuned from a measurement.  Blocks until done.
-static double now_s() {
-  timespec ts;
-  clock_gettime(CLOCK_MONOTONIC, &ts);
-  return ts.tv_sec + ts.tv_nsec * 1e-9;
-}
-
 int edl_ckpt_restore_pipelined2(void* seg, int slot, int nbuf, const uint64_t* dev_ptrs, const uint64_t* sizes,
                                 const uint64_t* offsets, hipStream_t stream, uint64_t chunk, int threads, int stages,
                                 double* stats) {
@@ -615,42 +791,7 @@ int edl_ckpt_restore_pipelined2(void* seg, int slot, int nbuf, const uint64_t* d
     for (uint64_t off = 0; off < sizes[b]; off += chunk)
       pieces.push_back({base + offsets[b] + off, (uint8_t*)dev_ptrs[b] + off,
                         sizes[b] - off < chunk ? sizes[b] - off : chunk});
-  // persistent copy pool: generation-numbered jobs, one stripe per thread
-  std::mutex mu;
-  std::condition_variable cv_job, cv_done;
-  uint64_t gen = 0;
-  int pending = 0;
-  bool stop = false;
-  const uint8_t* job_src = nullptr;
-  uint8_t* job_dst = nullptr;
-  uint64_t job_n = 0;
-  std::vector<std::thread> pool;
-  for (int t = 0; t < threads && err == hipSuccess; ++t) {
-    pool.emplace_back([&, t] {
-      uint64_t seen = 0;
-      for (;;) {
-        const uint8_t* src;
-        uint8_t* dst;
-        uint64_t n;
-        {
-          std::unique_lock<std::mutex> lk(mu);
-          cv_job.wait(lk, [&] { return stop || gen != seen; });
-          if (stop) return;
-          seen = gen;
-          src = job_src;
-          dst = job_dst;
-          n = job_n;
-        }
-        const uint64_t per = ((n + threads - 1) / threads + 63) & ~uint64_t(63);
-        const uint64_t lo = per * t;
-        if (lo < n) memcpy(dst + lo, src + lo, (lo + per > n) ? n - lo : per);
-        {
-          std::lock_guard<std::mutex> lk(mu);
-          if (--pending == 0) cv_done.notify_one();
-        }
-      }
-    });
-  }
+  CopyPool pool(threads);
   double copy_s = 0.0, wait_s = 0.0;
   uint64_t bytes = 0;
   for (size_t c = 0; c < pieces.size() && err == hipSuccess; ++c) {
@@ -662,28 +803,13 @@ int edl_ckpt_restore_pipelined2(void* seg, int slot, int nbuf, const uint64_t* d
       if (err != hipSuccess) break;
     }
     const double t0 = now_s();
-    {
-      std::unique_lock<std::mutex> lk(mu);
-      job_src = pieces[c].src;
-      job_dst = (uint8_t*)stage[k];
-      job_n = pieces[c].n;
-      pending = threads;
-      ++gen;
-      cv_job.notify_all();
-      cv_done.wait(lk, [&] { return pending == 0; });
-    }
+    pool.run((uint8_t*)stage[k], pieces[c].src, pieces[c].n);
     copy_s += now_s() - t0;
     err = hipMemcpyAsync(pieces[c].dst, stage[k], pieces[c].n, hipMemcpyHostToDevice, stream);
     if (err == hipSuccess) err = hipEventRecord(ev[k], stream);
     used[k] = true;
     bytes += pieces[c].n;
   }
-  {
-    std::lock_guard<std::mutex> lk(mu);
-    stop = true;
-  }
-  cv_job.notify_all();
-  for (auto& th : pool) th.join();
   const double t0 = now_s();
   if (err == hipSuccess) err = hipStreamSynchronize(stream);
   wait_s += now_s() - t0;
@@ -700,6 +826,26 @@ int edl_ckpt_restore_pipelined2(void* seg, int slot, int nbuf, const uint64_t* d
   return (int)err;
 }
 
+// Staged-snapshot parameters (before the first staged job): stage size, ring depth, copy threads.
+int edl_ckpt_engine_staging(void* eng, uint64_t stage_bytes, int nstage, int threads) {
+  auto* e = static_cast<Engine*>(eng);
+  std::lock_guard<std::mutex> g(e->mu);
+  if (e->pool) return -1;
+  if (stage_bytes) e->stage_bytes = round_up(stage_bytes, 2 << 20);
+  if (nstage >= 2) e->nstage = nstage > 16 ? 16 : nstage;
+  if (threads >= 1) e->threads = threads > 64 ? 64 : threads;
+  return 0;
+}
+
+// {d2h_wait_s, copy_s, total_s, bytes} of the last finished staged snapshot.
+void edl_ckpt_engine_staged_stats(void* eng, double* out) {
+  auto* e = static_cast<Engine*>(eng);
+  std::lock_guard<std::mutex> g(e->mu);
+  for (int i = 0; i < 4; ++i) out[i] = e->last_staged[i];
+}
+
+int edl_shm_pinned(void* h) { return h && static_cast<Seg*>(h)->pinned ? 1 : 0; }
+
 void edl_ckpt_engine_destroy(void* eng) {
   auto* e = static_cast<Engine*>(eng);
   if (!e) return;
@@ -710,6 +856,11 @@ void edl_ckpt_engine_destroy(void* eng) {
   e->cv.notify_all();
   if (e->committer.joinable()) e->committer.join();
   for (auto& kv : e->events) hipEventDestroy(kv.second);
+  delete e->pool;
+  for (auto ev : e->sev)
+    if (ev) hipEventDestroy(ev);
+  for (auto p : e->stage)
+    if (p) hipHostFree(p);
   if (e->side) hipStreamDestroy(e->side);
   delete e;
 }

@@ -48,6 +48,9 @@ SIGS = {
     "edl_ckpt_wait": (i32, [vp, i64, i32]),
     "edl_ckpt_restore": (i32, [vp, i32, i32, u64p, u64p, u64p, vp]),
     "edl_ckpt_engine_destroy": (None, [vp]),
+    "edl_ckpt_engine_staging": (i32, [vp, u64, i32, i32]),
+    "edl_ckpt_engine_staged_stats": (None, [vp, ctypes.POINTER(ctypes.c_double)]),
+    "edl_shm_pinned": (i32, [vp]),
     "edl_ckpt_restore_pipelined": (i32, [vp, i32, i32, u64p, u64p, u64p, vp, u64, i32]),
     "edl_ckpt_restore_pipelined2": (i32, [vp, i32, i32, u64p, u64p, u64p, vp, u64, i32, i32,
                                           ctypes.POINTER(ctypes.c_double)]),

@@ -203,7 +203,7 @@ class CheckpointManager:
     """
 
     def __init__(self, job: str, interval: int = 10, persist_dir: str | None = None, persist_every: int = 0,
-                 sharded: bool = True, pin: bool = True, host_budget_gb: float | None = None,
+                 sharded: bool = True, pin: bool | None = None, host_budget_gb: float | None = None,
                  host_fraction: float = 0.8, lean: str = "auto"):
         self.job = job
         env = os.environ.get("EDL_CKPT_HOST_GB")
@@ -216,7 +216,13 @@ class CheckpointManager:
         self.persist_dir = persist_dir
         self.persist_every = persist_every
         self.sharded = sharded
-        self.pin = pin
+        # Page-locked slots (EDL_SNAPSHOT_PIN=1): snapshots DMA straight into the shm pages,
+        # at the price of hipHostRegister on the first snapshot of a process (seconds for a
+        # ~100 GB slot pair, serialised with the training thread's HIP calls) and of the
+        # unpinning when the process dies.  0: slots stay pageable; snapshots stream through
+        # a small pinned staging ring (csrc/runtime/shm_store.cpp run_staged).  A segment a
+        # restore adopted is never pinned (see restore_latest).
+        self.pin = pin if pin is not None else os.environ.get("EDL_SNAPSHOT_PIN", "1") != "0"
         self._seg: ShmSegment | None = None
         self._seg_key = None
         self._old_name = None       # previous layout's name of a relinked segment (see _segment)
@@ -430,6 +436,13 @@ class CheckpointManager:
                  max(shard_layout(lean_state, shard, world)[1] + 8, headroom(lean_state)))
         return comm, tag, world, shard, state, layout, cs_off, lean_state, headroom, key, sizes
 
+    def _own_key(self, trainer):
+        """(world, shard, tag) of the segment this rank's snapshots go to (None: it writes none)."""
+        comm = self._comm(trainer)
+        if not self.sharded and comm.rank != 0:
+            return None
+        return ((comm.world_size, comm.rank) if self.sharded else (1, 0)) + (self._tag(trainer),)
+
     def prepare_layout(self, trainer) -> str | None:
         """Agree on this layout's full / lean / off mode now (the trainer calls it while
         entering an epoch, inside its failure handling), so no snapshot runs a collective."""
@@ -521,9 +534,12 @@ class CheckpointManager:
         # snapshot copies run as blit kernels: confine them to EDL_CKPT_CUS CUs (default 8,
         # one per XCD) so they barely touch the training kernels (csrc/runtime/shm_store.cpp)
         cus = int(os.environ.get("EDL_CKPT_CUS", 8))
-        e = _native.runtime()("edl_ckpt_engine_create", device, 256 << 20, cus)
+        rt = _native.runtime()
+        e = rt("edl_ckpt_engine_create", device, 256 << 20, cus)
         if not e:
             raise RuntimeError("cannot create checkpoint engine")
+        rt("edl_ckpt_engine_staging", e, int(os.environ.get("EDL_CKPT_STAGE_MB", 128)) << 20,
+           int(os.environ.get("EDL_CKPT_STAGES", 4)), int(os.environ.get("EDL_CKPT_COPY_THREADS", 16)))
         return e
 
     def fence(self) -> None:
@@ -539,6 +555,12 @@ class CheckpointManager:
             if st < 0:
                 raise RuntimeError(f"snapshot failed: {st}")
             self._ticket = None
+            if self._seg is not None and not self._seg.pinned:
+                out = (ctypes.c_double * 4)()
+                _native.runtime()("edl_ckpt_engine_staged_stats", self._engine, out)
+                if out[2] > 0:
+                    self.stats["staged_last"] = {"d2h_wait_s": round(out[0], 3), "copy_s": round(out[1], 3),
+                                                 "total_s": round(out[2], 3), "gb": round(out[3] / 2**30, 2)}
 
     @staticmethod
     def _next_slot(seg: ShmSegment) -> int:
@@ -614,17 +636,27 @@ class CheckpointManager:
         state = dict(self.state_of(trainer))
         dev = next(iter(state.values())).device
         phases = {"find_s": round(t0 - t_start, 3)}
+        own = self._own_key(trainer)
         for s, info in enumerate(infos):
             t1 = time.perf_counter()
             seg = _open_segment(self.seg_name(world, s, tag))
             phases["open_s"] = round(phases.get("open_s", 0) + time.perf_counter() - t1, 3)
+            keep = False
             try:
                 _load_shard(lambda off, nb: seg.view(info["slot"], off, nb), info["meta"]["t"], state, dev,
                             info["checksum"], f"shm shard {s} of step {step}", seg=seg, slot=info["slot"])
+                # The segment this rank will write next (same layout, e.g. the only worker restarted):
+                # keep the mapping as this rank's snapshot segment.  Unmapping ~100 GB of populated
+                # pages costs seconds and takes the address-space lock the first step's allocations
+                # need (3.1 s measured); re-mapping and page-locking it for the next snapshot would
+                # cost seconds more.  It stays pageable: snapshots stream through the staging ring.
+                keep = self._seg is None and own == (world, s, tag)
             finally:
-                # unmapping tens of GB of populated shm pages takes seconds of page-table teardown:
-                # nothing reads the mapping any more, so it is closed off the recovery path
-                threading.Thread(target=seg.close, name="edl-shm-unmap", daemon=True).start()
+                if keep:
+                    self._seg, self._seg_key = seg, own
+                    self.stats["adopted"] = self.stats.get("adopted", 0) + 1
+                else:
+                    threading.Thread(target=seg.close, name="edl-shm-unmap", daemon=True).start()
         t2 = time.perf_counter()
         self.finish_restore(trainer)
         if dev.type == "cuda":

@@ -332,20 +332,27 @@ class PSClient:
                     sparse_split_push(ids, g, iids, igrad, icnt, self.sparse_cap, scratch)
                 self.sparse_path["ipc_pushes"] += 1
             seqs = [None] * self.num_ps
+            stream = torch.cuda.current_stream(dev)
             if all(self._ipc[i].get("flag") is not None for i in range(self.num_ps)):
                 # stream-ordered flag stores into each PS's HBM; the PS's stream waits for them
-                # (bounded) before reading any inbox: no host sync on this worker
+                # (bounded) before reading any inbox
                 from easydl_amd.ops.sparse import ps_signal
-                stream = torch.cuda.current_stream(dev)
                 for i in range(self.num_ps):
                     m = self._ipc[i]
                     m["seq"] += 1
                     seqs[i] = m["seq"]
                     ps_signal(m["flag"], m["seq"], stream)
-            else:
-                torch.cuda.current_stream(dev).synchronize()   # inboxes complete before the PS reads them
+            # The control message leaves once this worker's stream has reached the flag stores
+            # (each sender thread waits on the event; the main thread waits for the replies
+            # anyway).  Sent earlier, it parks the PS's stream in its flag wait behind this
+            # worker's backward, and every other worker's update queues behind that wait:
+            # config 4 ran 243 samples/s that way vs 316 with the message sent on completion
+            # (profiles/r04_bert_ps_flag_wait.md).  The device wait stays as the ordering guard.
+            ready = torch.cuda.Event()
+            ready.record(stream)
 
             def one(i):
+                ready.synchronize()
                 hdr = {"op": "push_ipc", "worker": self.worker_id, "step": step, "slot": slots[i],
                        "pull": bool(then_pull), "sparse_ipc": sp_ipc, "seq": seqs[i]}
                 h, _ = self._call(i, hdr, self._sparse_grads(i, sparse_grads))

@@ -106,12 +106,12 @@ class ParameterServer:
         self.inboxes: dict[str, list[torch.Tensor]] = {}
         self._inbox_ev: dict[str, list] = {}
         # ... and, per row-sparse table, two sparse inboxes (local ids, fp32 rows, row count)
-        # the worker fills on its GPU; the worker's interprocess event orders the PS's reads
-        # after those writes (no host synchronisation on the worker)
+        # the worker fills on its GPU; the push flag below orders the PS's reads after those writes
         self.sp_inboxes: dict[str, dict[str, list[tuple]]] = {}
         # push ordering: the worker's stream stores its push sequence number into this flag
         # word after its inbox writes (edl_ps_signal); our stream waits for it (edl_ps_wait,
-        # bounded) before the update -- the worker never host-synchronises before a push
+        # bounded) before the update.  The worker sends push_ipc once its stream has passed the
+        # flag store (ps/client.py), so the wait normally returns at once; it guards the order
         self._push_flag: dict[str, torch.Tensor] = {}
         self._push_status: dict[str, torch.Tensor] = {}
         self._apply_ev = None      # completion of the newest update of the shard

@@ -86,7 +86,12 @@ class ElasticTrainer:
             torch.cuda.set_stream(self.compute_stream)
         self.events = EventLog(os.path.join(self.ctx.run_dir, f"events-{self.ctx.role}{self.ctx.index}.jsonl"),
                                proc=f"{self.ctx.role}{self.ctx.index}")
-        self.events.emit("device_ready", s=round(time.perf_counter() - t_init, 4))
+        try:
+            ncpu = len(os.sched_getaffinity(0))
+        except (AttributeError, OSError):
+            ncpu = os.cpu_count()
+        self.events.emit("device_ready", s=round(time.perf_counter() - t_init, 4), cpus=ncpu,
+                         threads=torch.get_num_threads())
         if optimizer not in ("adamw", "sgd"):
             raise ValueError(f"unknown optimizer {optimizer}")
         self._model_fn, self._seed = model_fn, seed
@@ -571,6 +576,12 @@ class ElasticTrainer:
             ld = loss.detach() * w
             loss_acc = ld if loss_acc is None else loss_acc + ld
             total += w
+        t_mb = time.perf_counter()
+        if self._phases and self.device.type == "cuda":
+            # diagnostic mode: drain the compute stream so 'finish' is the gradient all-reduce alone
+            torch.cuda.current_stream(self.device).synchronize()
+            self._t_host = t_mb - getattr(self, "_t_step", t_mb)
+            t_mb = time.perf_counter()
         # a rank without samples (world > batch) still joins every all-reduce with zeros:
         # finish() zero-fills untouched gradients before flushing the buckets.
         with trace.range("grad_sync"):
@@ -578,6 +589,7 @@ class ElasticTrainer:
             if hasattr(self.model, "sync_sp_grads"):
                 self.model.sync_sp_grads(self.flat)   # sequence-parallel norm grads: sum over TP
         self.fault.maybe_inject("after_backward", self.step, trainer=self)
+        self._t_mb = t_mb
         return None if loss_acc is None else loss_acc / total
 
     def _sync_point(self) -> bool:
@@ -612,7 +624,7 @@ class ElasticTrainer:
                 self.events.emit("finished_waiting", node=self.ctx.node_id)
                 return self
             while self.step < num_steps:
-                t0 = time.perf_counter()
+                t0 = self._t_step = time.perf_counter()
                 ok = True
                 loss = None
                 try:
@@ -647,6 +659,8 @@ class ElasticTrainer:
                         # host-side split of one step (EDL_STEP_PHASES=1): enqueue of the micro-batches,
                         # wait for the GPU (compute + all-reduce), commit round, snapshot fence, optimizer
                         self.events.emit("step_phases", step=self.step + 1, run=round(t_run - t0, 4),
+                                         mb=round(self._t_mb - t0, 4), finish=round(t_run - self._t_mb, 4),
+                                         mb_host=round(getattr(self, "_t_host", 0.0), 4),
                                          sync=round(t_sync - t_run, 4), commit=round(t_commit - t_sync, 4),
                                          fence=round(t_fence - t_commit, 4),
                                          opt=round(time.perf_counter() - t_fence, 4))

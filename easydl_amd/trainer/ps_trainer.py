@@ -115,7 +115,7 @@ class PSWorker:
                     loss.backward()
                     if self._phase_sync and self.device.type == "cuda":
                         # diagnostics only (EDL_PS_PHASE_SYNC=1): exact compute-vs-push split; the GPU
-                        # transport otherwise never host-synchronises inside a step
+                        # transport otherwise never synchronises the stream on the main thread
                         torch.cuda.current_stream(self.device).synchronize()
                     t2 = time.perf_counter()
                     self.client.push(self.model, self.steps, then_pull=fused)

@@ -94,6 +94,30 @@ def test_snapshot_restore_resumes_bit_identically(tmp_path):
         unlink_job_segments(JOB)
 
 
+def test_restarted_trainer_adopts_the_segment_it_restored_from(tmp_path):
+    """The restarted (only) worker keeps the mapping it restored from as its own snapshot
+    segment: the next snapshot goes to the other A/B slot of that same mapping, and the
+    restored step stays committed until the new one is."""
+    unlink_job_segments(JOB)
+    data = SyntheticTokens(CFG.vocab_size, 16, num_samples=1024)
+    ckpt = CheckpointManager(JOB, interval=3)
+    try:
+        a = _trainer(tmp_path, ckpt)
+        a.fit(lambda m, b: m(*b), data, num_steps=7)
+        ckpt.wait()
+        ckpt2 = CheckpointManager(JOB, interval=2)
+        b = _trainer(tmp_path, ckpt2, seed=999)
+        b.fit(lambda m, b_: m(*b_), data, num_steps=6)     # restore of step 6 only
+        assert ckpt2.stats.get("adopted") == 1 and ckpt2._seg is not None
+        seg = ckpt2._seg
+        assert [i["step"] for i in seg.committed()] == [3, 6]
+        b.fit(lambda m, b_: m(*b_), data, num_steps=8)     # snapshot of step 8 into the adopted mapping
+        ckpt2.wait()
+        assert ckpt2._seg is seg and sorted(i["step"] for i in seg.committed()) == [6, 8]
+    finally:
+        unlink_job_segments(JOB)
+
+
 def test_snapshot_evaluator_reads_latest(tmp_path):
     from easydl_amd.trainer.evaluator import SnapshotEvaluator
     unlink_job_segments("ckev")

@@ -96,3 +96,37 @@ def test_lean_snapshot_through_the_d2h_engine(cuda, tmp_path):
     finally:
         ckpt.close()
         unlink_job_segments("ckg")
+
+
+def test_staged_snapshots_into_an_adopted_segment_resume_bit_exactly(cuda, tmp_path, monkeypatch):
+    """Pageable slots (EDL_SNAPSHOT_PIN=0 path): snapshots stream through a 2-deep ring of
+    1 MiB pinned stages, so one snapshot wraps the ring many times.  A restarted trainer
+    adopts the segment it restored from (no unmap, no page-locking) and keeps snapshotting
+    into it; a third one restores the adopted segment's newest step and matches an
+    uninterrupted run bit for bit."""
+    monkeypatch.setenv("EDL_CKPT_STAGE_MB", "1")
+    monkeypatch.setenv("EDL_CKPT_STAGES", "2")
+    monkeypatch.setenv("EDL_CKPT_COPY_THREADS", "3")
+    unlink_job_segments("ckg")
+    data = SyntheticTokens(CFG.vocab_size, 64, num_samples=4096)
+    ck_a, ck_b = CheckpointManager("ckg", interval=2, pin=False), CheckpointManager("ckg", interval=2, pin=False)
+    try:
+        a = _trainer(tmp_path, ck_a, 1, cuda)
+        a.fit(lambda m, b: m(*b), data, num_steps=5)
+        ck_a.wait()
+        assert not ck_a._seg.pinned and ck_a.stats["staged_last"]["gb"] > 0
+        b = _trainer(tmp_path, ck_b, 2, cuda)
+        b.fit(lambda m, b_: m(*b_), data, num_steps=8)   # restores step 4, snapshots 6 and 8
+        ck_b.wait()
+        assert ck_b.stats.get("adopted") == 1 and not ck_b._seg.pinned
+        assert ck_b.last_snapshot_step == 8 and ck_b.stats["snapshots"] == 2
+        c = _trainer(tmp_path, CheckpointManager("ckg", interval=1000), 3, cuda)
+        c.fit(lambda m, b_: m(*b_), data, num_steps=8)   # restores step 8
+        assert c.step == 8
+        ref = _trainer(tmp_path, None, 1, cuda)
+        ref.fit(lambda m, b_: m(*b_), data, num_steps=8)
+        assert torch.equal(_flat(c), _flat(ref))
+    finally:
+        ck_a.close()
+        ck_b.close()
+        unlink_job_segments("ckg")
