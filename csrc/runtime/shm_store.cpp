@@ -69,6 +69,11 @@ struct Seg {
   uint8_t* base = nullptr;
   uint64_t total = 0;
   bool pinned = false;
+  // background population (edl_shm_populate_async): pieces handed out by an atomic cursor
+  std::vector<std::thread> pop;
+  std::atomic<uint64_t> pop_next{0}, pop_done{0};
+  std::atomic<bool> pop_stop{false};
+  uint64_t pop_bytes = 0;
   SegHdr* hdr() { return reinterpret_cast<SegHdr*>(base); }
   SlotHdr* slot(int i) { return reinterpret_cast<SlotHdr*>(base + kHdr * (1 + i)); }
   uint8_t* data(int i) {
@@ -331,9 +336,57 @@ int edl_shm_slot_info(void* h, int slot, int64_t* step, int64_t* epoch, uint64_t
   return st;
 }
 
+// Populate every slot's pages in `threads` background threads (MADV_POPULATE_WRITE over 64 MiB
+// pieces).  First-touch of tmpfs pages runs at only ~4-5 GB/s however many threads fault them
+// (measured on the MI355X box: a snapshot's copy into a never-written 96 GB slot stalled the step
+// for 25 s), so a segment is populated off the training path as soon as it exists, and a
+// snapshot waits for (or skips) an unfinished population instead of faulting inside its copy.
+// Returns 0, or -1 if a population is already running.
+int edl_shm_populate_async(void* h, int threads) {
+#ifndef MADV_POPULATE_WRITE
+#define MADV_POPULATE_WRITE 23
+#endif
+  auto* s = static_cast<Seg*>(h);
+  if (!s->pop.empty()) return -1;
+  if (threads < 1) threads = 1;
+  const uint64_t piece = 64ull << 20;
+  s->pop_bytes = s->hdr()->slot_bytes * s->hdr()->nslots;
+  s->pop_next = 0;
+  s->pop_done = 0;
+  uint8_t* d0 = s->data(0);
+  for (int t = 0; t < threads; ++t) {
+    s->pop.emplace_back([s, d0, piece] {
+      for (;;) {
+        if (s->pop_stop.load(std::memory_order_relaxed)) return;
+        const uint64_t lo = s->pop_next.fetch_add(piece);
+        if (lo >= s->pop_bytes) return;
+        const uint64_t len = lo + piece > s->pop_bytes ? s->pop_bytes - lo : piece;
+        if (madvise(d0 + lo, len, MADV_POPULATE_WRITE) != 0)
+          madvise(d0 + lo, len, MADV_POPULATE_READ);  // kernels without POPULATE_WRITE
+        s->pop_done.fetch_add(len);
+      }
+    });
+  }
+  return 0;
+}
+
+// Bytes populated so far and the total (0 / 0: no population started).
+uint64_t edl_shm_populate_progress(void* h, uint64_t* total) {
+  auto* s = static_cast<Seg*>(h);
+  if (total) *total = s->pop.empty() ? 0 : s->pop_bytes;
+  return s->pop.empty() ? 0 : s->pop_done.load();
+}
+
+static void populate_join(Seg* s) {
+  s->pop_stop = true;
+  for (auto& t : s->pop) t.join();
+  s->pop.clear();
+}
+
 int edl_shm_close(void* h, int unlink_seg) {
   auto* s = static_cast<Seg*>(h);
   if (!s) return 0;
+  populate_join(s);
   if (s->pinned) hipHostUnregister(s->data(0));
   munmap(s->base, s->total);
   close(s->fd);

@@ -140,6 +140,16 @@ class ShmSegment:
         if rc != 0:
             raise OSError(-rc, "shm commit failed (meta too large?)")
 
+    def populate_async(self, threads: int = 16) -> bool:
+        """Fault every slot's pages in on background threads (csrc: edl_shm_populate_async)."""
+        return self.rt("edl_shm_populate_async", self.h, threads) == 0
+
+    def populated(self) -> bool:
+        """False while a background population is still running."""
+        total = ctypes.c_uint64()
+        done = self.rt("edl_shm_populate_progress", self.h, ctypes.byref(total))
+        return done >= total.value
+
     def close(self, unlink: bool = False):
         if self.h:
             self.rt("edl_shm_close", self.h, 1 if unlink else 0)
@@ -222,7 +232,13 @@ class CheckpointManager:
         # unpinning when the process dies.  0: slots stay pageable; snapshots stream through
         # a small pinned staging ring (csrc/runtime/shm_store.cpp run_staged).  A segment a
         # restore adopted is never pinned (see restore_latest).
-        self.pin = pin if pin is not None else os.environ.get("EDL_SNAPSHOT_PIN", "1") != "0"
+        self.pin = pin if pin is not None else os.environ.get("EDL_SNAPSHOT_PIN", "0") == "1"
+        # Pageable slots are populated on background threads as soon as the segment exists
+        # (EDL_SHM_POPULATE_THREADS, 0 = never); the first snapshot waits for what is left.  A
+        # segment adopted by a restore skips snapshots until its population is done instead:
+        # the restored slot already holds a valid snapshot, and recovery should not stall.
+        self.populate_threads = int(os.environ.get("EDL_SHM_POPULATE_THREADS", 16))
+        self._skip_populating = False
         self._seg: ShmSegment | None = None
         self._seg_key = None
         self._old_name = None       # previous layout's name of a relinked segment (see _segment)
@@ -330,6 +346,9 @@ class CheckpointManager:
         self._drop_old_name()
         self._seg = ShmSegment(name, max(need_bytes, alloc_bytes), create=True, pin=self.pin and pin)
         self._seg_key = key
+        self._skip_populating = False
+        if not self._seg.pinned and self.populate_threads > 0:
+            self._seg.populate_async(self.populate_threads)
         return self._seg
 
     @staticmethod
@@ -445,11 +464,21 @@ class CheckpointManager:
 
     def prepare_layout(self, trainer) -> str | None:
         """Agree on this layout's full / lean / off mode now (the trainer calls it while
-        entering an epoch, inside its failure handling), so no snapshot runs a collective."""
-        comm, _, _, _, _, _, _, _, _, key, sizes = self._plan(trainer)
+        entering an epoch, inside its failure handling), so no snapshot runs a collective;
+        and create the layout's segment, so its pages are populated before the first
+        snapshot needs them."""
+        comm, tag, world, shard, state, _, _, lean_state, headroom, key, sizes = self._plan(trainer)
         if not self.sharded and comm.rank != 0:
             return None
-        return self._decide_mode(trainer, comm, key, *sizes)
+        mode = self._decide_mode(trainer, comm, key, *sizes)
+        if mode != "off" and state and state[0][1].is_cuda:
+            self._layout_segment(world, shard, tag, state if mode == "full" else lean_state, headroom)
+        return mode
+
+    def _layout_segment(self, world, shard, tag, state, headroom) -> ShmSegment:
+        _, cs_off = shard_layout(state, shard, world)
+        alloc = headroom(state) if world > 1 and self._seg is None else 0
+        return self._segment(world, shard, cs_off + 8, pin=state[0][1].is_cuda, tag=tag, alloc_bytes=alloc)
 
     def snapshot(self, trainer) -> None:
         comm, tag, world, shard, state, layout, cs_off, lean_state, headroom, key, sizes = self._plan(trainer)
@@ -463,11 +492,16 @@ class CheckpointManager:
             state = lean_state
             layout, cs_off = shard_layout(state, shard, world)
         self.wait()  # at most one snapshot in flight (and never one across a segment change)
-        alloc = 0
-        if world > 1 and self._seg is None:
-            # headroom: the largest shard of a world one rank smaller (+ alignment slack)
-            alloc = headroom(state)
-        seg = self._segment(world, shard, cs_off + 8, pin=state[0][1].is_cuda, tag=tag, alloc_bytes=alloc)
+        # (the first segment gets headroom: the largest shard of a world one rank smaller)
+        seg = self._layout_segment(world, shard, tag, state, headroom)
+        if not seg.populated():
+            if self._skip_populating:
+                self.stats["skipped_populating"] = self.stats.get("skipped_populating", 0) + 1
+                return
+            t0 = time.perf_counter()
+            while not seg.populated():
+                time.sleep(0.01)
+            self.stats["populate_wait_s"] = round(self.stats.get("populate_wait_s", 0) + time.perf_counter() - t0, 3)
         if getattr(self, "_old_name", None) and self._kept_slot_next(seg):
             self._drop_old_name()   # this write overwrites the old layout's kept snapshot
         if self._persist_busy_slot(seg):
@@ -560,7 +594,7 @@ class CheckpointManager:
                 _native.runtime()("edl_ckpt_engine_staged_stats", self._engine, out)
                 if out[2] > 0:
                     self.stats["staged_last"] = {"d2h_wait_s": round(out[0], 3), "copy_s": round(out[1], 3),
-                                                 "total_s": round(out[2], 3), "gb": round(out[3] / 2**30, 2)}
+                                                 "total_s": round(out[2], 3), "mb": round(out[3] / 2**20, 1)}
 
     @staticmethod
     def _next_slot(seg: ShmSegment) -> int:
@@ -655,6 +689,11 @@ class CheckpointManager:
                 if keep:
                     self._seg, self._seg_key = seg, own
                     self.stats["adopted"] = self.stats.get("adopted", 0) + 1
+                    if self.populate_threads > 0 and dev.type == "cuda":
+                        # pages the dead writer never touched (a slot it was still filling) fault in
+                        # off the recovery path; snapshots wait for that by skipping
+                        seg.populate_async(self.populate_threads)
+                        self._skip_populating = True
                 else:
                     threading.Thread(target=seg.close, name="edl-shm-unmap", daemon=True).start()
         t2 = time.perf_counter()

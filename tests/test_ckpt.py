@@ -137,6 +137,23 @@ def test_snapshot_evaluator_reads_latest(tmp_path):
         unlink_job_segments("ckev")
 
 
+def test_background_population_covers_every_slot():
+    import time
+    seg = ShmSegment("/edl-poptest-w1-s0", 48 << 20, create=True)
+    try:
+        assert seg.populated()                      # nothing started: nothing to wait for
+        assert seg.populate_async(3) and not seg.populate_async(3)   # one population at a time
+        t_end = time.time() + 30
+        while not seg.populated() and time.time() < t_end:
+            time.sleep(0.005)
+        assert seg.populated()
+        s0 = seg.begin()
+        seg.view(s0, 0, 8)[:] = 5                   # the mapping stays usable
+        assert int(seg.view(s0, 0, 8)[3]) == 5
+    finally:
+        seg.close(unlink=True)                      # joins the (finished) threads
+
+
 def test_premapped_segments_are_reused_by_restore(tmp_path):
     """A hot standby maps + pre-faults the job's segments; the restore then uses that mapping."""
     from easydl_amd.ckpt import manager as m

@@ -114,12 +114,14 @@ def test_staged_snapshots_into_an_adopted_segment_resume_bit_exactly(cuda, tmp_p
         a = _trainer(tmp_path, ck_a, 1, cuda)
         a.fit(lambda m, b: m(*b), data, num_steps=5)
         ck_a.wait()
-        assert not ck_a._seg.pinned and ck_a.stats["staged_last"]["gb"] > 0
+        assert not ck_a._seg.pinned and ck_a.stats["staged_last"]["mb"] > 4
         b = _trainer(tmp_path, ck_b, 2, cuda)
         b.fit(lambda m, b_: m(*b_), data, num_steps=8)   # restores step 4, snapshots 6 and 8
         ck_b.wait()
         assert ck_b.stats.get("adopted") == 1 and not ck_b._seg.pinned
-        assert ck_b.last_snapshot_step == 8 and ck_b.stats["snapshots"] == 2
+        # (a snapshot may be skipped while the adopted segment's pages are still being populated)
+        assert ck_b.last_snapshot_step == 8
+        assert ck_b.stats["snapshots"] + ck_b.stats.get("skipped_populating", 0) == 2
         c = _trainer(tmp_path, CheckpointManager("ckg", interval=1000), 3, cuda)
         c.fit(lambda m, b_: m(*b_), data, num_steps=8)   # restores step 8
         assert c.step == 8
