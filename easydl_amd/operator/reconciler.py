@@ -165,6 +165,9 @@ class ElasticOperator:
         env.update({"EDL_JOB": self.job.name, "EDL_MASTER_ADDR": "127.0.0.1",
                     "EDL_MASTER_PORT": str(self.master_port), "EDL_RUN_DIR": self.run_dir})
         env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        if max(self.cfg.standby, getattr(self.job, "standby", 0)) > 0:
+            # workers export their state buffers, a standby adopts a dead one's (utils/vram.py)
+            env.setdefault("EDL_VRAM_HANDOFF", "1")
         for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_USE_AGENT_STORE"):
             env.pop(k, None)
         return env

@@ -60,6 +60,36 @@ def prewarm() -> dict:
     return out
 
 
+def _import_vram(kv, held: dict) -> None:
+    """Map (IPC) the state buffers every worker published; keep them referenced while parked."""
+    from easydl_amd.utils import vram
+    try:
+        slots = vram.slots(kv)
+    except Exception:  # noqa: BLE001
+        return
+    for slot in slots:
+        try:
+            held[slot] = vram.import_published(kv, slot, held.get(slot))
+        except Exception as e:  # noqa: BLE001 - a worker mid-restart: try again next scan
+            print(f"standby: vram import of {slot} failed: {e}", file=sys.stderr)
+
+
+def _adopt_vram(held: dict, slot: str, kv, name: str) -> None:
+    """Takeover of ``slot``: its dead predecessor's buffers back this process's state; every
+    other worker's imports are released (they belong to live processes)."""
+    from easydl_amd.utils import vram
+    got = held.pop(slot, None)
+    held.clear()
+    if not got or not got.get("tensors"):
+        return
+    if not vram.dead(got.get("pid")):
+        print(f"standby: {slot}'s exporter {got.get('pid')} is alive; not adopting", file=sys.stderr)
+        return
+    vram.adopt(got["tensors"])
+    kv.set(f"standby/vram/{name}", json.dumps({"slot": slot, "from": got.get("owner"),
+                                               "tensors": len(got["tensors"])}))
+
+
 def main() -> int:
     from easydl_amd.master.store import KV, make_tcp_store
     name = os.environ["EDL_STANDBY_NAME"]
@@ -71,13 +101,19 @@ def main() -> int:
     kv.set(f"standby/ready/{name}", json.dumps(info))
     key = f"standby/assign/{name}"
     premap = os.environ.get("EDL_STANDBY_PREMAP", "0") == "1"
-    next_scan = 0.0
+    from easydl_amd.utils import vram
+    handoff = vram.enabled() and info.get("gpus", 0) > 0
+    held: dict[str, dict] = {}     # worker slot -> imported state buffers (utils/vram.py)
+    next_scan = next_vram = 0.0
     while True:
         a = kv.get(key)
         if a is not None:
             break
         if kv.exists("job/done"):
             return 0
+        if handoff and time.monotonic() > next_vram:
+            _import_vram(kv, held)
+            next_vram = time.monotonic() + 1.0
         if premap and time.monotonic() > next_scan:
             from easydl_amd.ckpt.manager import premap_job_segments
             mapped = premap_job_segments(job)
@@ -87,6 +123,8 @@ def main() -> int:
         time.sleep(0.005)
     a = a if isinstance(a, dict) else json.loads(a)
     os.environ.update({k: str(v) for k, v in a["env"].items()})
+    if handoff:
+        _adopt_vram(held, f"worker{a['env'].get('EDL_INDEX', '')}", kv, name)
     argv = a["argv"]
     mod = module_of(argv)
     if mod is None:

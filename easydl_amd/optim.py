@@ -14,6 +14,7 @@ import torch
 
 from easydl_amd.ops.optim import adamw_flat_, grad_clip_scale, sgd_flat_
 from easydl_amd.parallel.flat import FlatParams
+from easydl_amd.utils import vram
 
 
 class LRSchedule:
@@ -32,6 +33,13 @@ class LRSchedule:
 
     def state_dict(self):
         return dict(lr=self.lr, warmup=self.warmup, total=self.total, min_ratio=self.min_ratio)
+
+
+def _zeros(name: str, g) -> torch.Tensor:
+    """fp32 optimizer state of flat group ``g``: a buffer handed over by the previous worker on
+    this GPU (utils/vram.py), zeroed, or a new one."""
+    t = vram.take(name, g.numel, torch.float32, g.data.device)
+    return torch.zeros(g.numel, dtype=torch.float32, device=g.data.device) if t is None else t
 
 
 class FlatAdamW:
@@ -56,12 +64,12 @@ class FlatAdamW:
             if weight_decay is not None and g.name.startswith("decay"):
                 g.weight_decay = weight_decay
             has16 = g.data.dtype != torch.float32
-            master = g.data.float() if has16 else g.data
-            self.state.append({
-                "master": master,
-                "m": torch.zeros(g.numel, dtype=torch.float32, device=g.data.device),
-                "v": torch.zeros(g.numel, dtype=torch.float32, device=g.data.device),
-            })
+            if has16:
+                master = vram.take(f"opt/{g.name}/master", g.numel, torch.float32, g.data.device)
+                master = g.data.float() if master is None else master.copy_(g.data)
+            else:
+                master = g.data
+            self.state.append({"master": master, "m": _zeros(f"opt/{g.name}/m", g), "v": _zeros(f"opt/{g.name}/v", g)})
 
     def current_lr(self) -> float:
         return self.schedule(self.step_count + 1) if self.schedule else self.lr
@@ -118,7 +126,7 @@ class FlatSGD:
             has16 = g.data.dtype != torch.float32
             self.state.append({
                 "master": g.data.float() if has16 else g.data,
-                "mom": torch.zeros(g.numel, dtype=torch.float32, device=g.data.device) if momentum else None,
+                "mom": _zeros(f"opt/{g.name}/mom", g) if momentum else None,
             })
 
     @torch.no_grad()

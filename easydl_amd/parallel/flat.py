@@ -31,6 +31,8 @@ from dataclasses import dataclass, field
 
 import torch
 
+from easydl_amd.utils import vram
+
 ALIGN = 64
 
 
@@ -94,7 +96,10 @@ class FlatParams:
     def __init__(self, module: torch.nn.Module, weight_decay: float = 0.0, grad_dtype: torch.dtype | None = None,
                  no_decay=None, max_group_bytes: int | None = None):
         if max_group_bytes is None:
-            max_group_bytes = int(float(os.environ.get("EDL_FLAT_GROUP_MAX_MB", 1900)) * 2**20)
+            # VRAM hand-over to a hot standby (utils/vram.py) maps every state tensor over IPC, which
+            # takes allocations below 2 GiB: the fp32 master / moments of a group are 2x its bf16 size
+            default_mb = vram.GROUP_MAX_MB if vram.enabled() else 1900
+            max_group_bytes = int(float(os.environ.get("EDL_FLAT_GROUP_MAX_MB", default_mb)) * 2**20)
         if no_decay is None:
             no_decay = lambda n, p: p.ndim < 2  # noqa: E731
         named = [(n, p) for n, p in module.named_parameters() if p.requires_grad]
@@ -125,8 +130,10 @@ class FlatParams:
                 chunks.append((cls, dt, gdt, base if i == 0 else f"{base}.{i}", part))
         for cls, dt, gdt, gname, plist in chunks:
             total = sum(_roundup(p.numel()) for _, p in plist)
-            data = torch.zeros(total, dtype=dt, device=self.device)
-            grad = torch.zeros(total, dtype=gdt, device=self.device)
+            data = vram.take(f"flat/{gname}/data", total, dt, self.device)
+            grad = vram.take(f"flat/{gname}/grad", total, gdt, self.device)
+            data = torch.zeros(total, dtype=dt, device=self.device) if data is None else data
+            grad = torch.zeros(total, dtype=gdt, device=self.device) if grad is None else grad
             grp = FlatGroup(gname, weight_decay if cls == "decay" else 0.0, data, grad)
             off = 0
             for n, p in plist:

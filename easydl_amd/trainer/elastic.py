@@ -490,6 +490,28 @@ class ElasticTrainer:
         self.held_tp = t
         self.needs_state = False
 
+    def _publish_vram(self) -> None:
+        """Export the persistent state buffers for the hot standby on this GPU (utils/vram.py):
+        if this process dies, the standby builds on them instead of waiting for the driver to
+        reclaim and re-allocate 128 GB (Llama-3-8B)."""
+        from easydl_amd.utils import vram
+        if not (vram.enabled() and self.device.type == "cuda" and getattr(self, "kv", None) is not None):
+            return
+        ts = {}
+        for g in self.flat.groups:
+            ts[f"flat/{g.name}/data"], ts[f"flat/{g.name}/grad"] = g.data, g.grad
+        for g, st in zip(self.flat.groups, getattr(self.opt, "state", [])):
+            for k, t in st.items():
+                if isinstance(t, torch.Tensor) and t is not g.data:
+                    ts[f"opt/{g.name}/{k}"] = t
+        try:
+            n = vram.publish(self.kv, f"{self.ctx.role}{self.ctx.index}", self.ctx.node_id, ts)
+        except Exception as e:  # noqa: BLE001 - hand-over is an optimisation; training goes on
+            log.warning("vram hand-over export failed: %s", e)
+            return
+        self.events.emit("vram_published", tensors=n, of=len(ts),
+                         adopted=dict(vram.STATS, adopted_gb=round(vram.STATS["adopted_bytes"] / 2**30, 1)))
+
     def _maybe_restore(self):
         if self.checkpoint is None:
             return
@@ -623,6 +645,7 @@ class ElasticTrainer:
             except JobFinished:
                 self.events.emit("finished_waiting", node=self.ctx.node_id)
                 return self
+            self._publish_vram()
             while self.step < num_steps:
                 t0 = self._t_step = time.perf_counter()
                 ok = True

@@ -1,0 +1,133 @@
+"""Hand the training state's HBM from a dying worker to the hot standby on its GPU.
+
+Why (round 4 no-survivor restore, ``profiles/r04_ttr_n1_restore.md``): a replacement on the
+GPU of a killed Llama-3-8B worker spent 5.4 s of its 10 s time-to-recover inside
+``hipMalloc`` of its 128 GB of flat parameters, gradients and AdamW state.  The dead
+process's 210 GB are released by the driver only after its teardown, and new allocations
+wait until it has reclaimed them (``docs/design_notes.md``, "TTR is dominated by the
+driver").
+
+How: every worker exports its persistent state tensors as IPC handles into the job store
+(``vram/gpu<k>``).  The parked standby imports them while the worker is still alive.  The
+imports keep the physical memory referenced, so when the worker dies those 128 GB are never
+released or reclaimed.  At takeover the standby's ``FlatParams`` / ``FlatAdamW`` build on
+the imported tensors (``take``) instead of allocating.  The restore then overwrites them
+from the shm snapshot as before: the dead worker may have died in the middle of an update.
+
+Constraint: ``hipIpcOpenMemHandle`` hangs on allocations of 2 GiB or more on this stack
+(``profiles/r03_ipc_size_probe2.txt``), so with hand-over on, flat groups are capped at
+960 MiB of bf16 and their fp32 master / moments stay under 2 GiB (``FlatParams``).  A larger
+tensor is simply not exported and is allocated as usual at takeover.
+
+``EDL_VRAM_HANDOFF=1`` turns it on.  The local operator sets it for workers and standbys
+when the job runs hot standbys.
+"""
+from __future__ import annotations
+
+import json
+import logging
+import os
+
+import torch
+
+log = logging.getLogger(__name__)
+
+IPC_MAX_BYTES = 2040 << 20       # largest allocation hipIpcOpenMemHandle maps here
+GROUP_MAX_MB = 960               # flat-group cap (bf16) under hand-over: fp32 state < 2 GiB
+
+_ADOPTED: dict[str, torch.Tensor] = {}
+STATS = {"exported": 0, "adopted": 0, "adopted_bytes": 0}
+
+
+def enabled() -> bool:
+    return os.environ.get("EDL_VRAM_HANDOFF", "0") == "1"
+
+
+def key(slot: str) -> str:
+    """Store key of one worker slot's export (``worker<index>``: the slot a replacement takes over)."""
+    return f"vram/{slot}"
+
+
+def _block_bytes(t: torch.Tensor) -> int:
+    return t.untyped_storage().nbytes()
+
+
+def publish(kv, slot: str, owner: str, tensors: dict[str, torch.Tensor]) -> int:
+    """Export ``tensors`` (name -> CUDA tensor owning its whole allocation) for the standby."""
+    from easydl_amd.ps.ipc import export_tensor
+    descs = {}
+    for name, t in tensors.items():
+        if t is None or not t.is_cuda or _block_bytes(t) > IPC_MAX_BYTES:
+            continue
+        try:
+            descs[name] = export_tensor(t)
+        except RuntimeError as e:   # e.g. a tensor this process itself imported (an adopted buffer)
+            log.debug("vram: %s not exportable: %s", name, e)
+    gpu = next((t.device.index for t in tensors.values() if t is not None and t.is_cuda), 0)
+    kv.set(key(slot), json.dumps({"owner": owner, "pid": os.getpid(), "gpu": gpu, "tensors": descs}))
+    if slot not in slots(kv):
+        kv.append("vram/slots", slot + ",")
+    STATS["exported"] = len(descs)
+    return len(descs)
+
+
+def slots(kv) -> list[str]:
+    return sorted({s for s in (kv.get_str("vram/slots") or "").split(",") if s})
+
+
+def import_published(kv, slot: str, held: dict | None = None) -> dict | None:
+    """Standby: (re-)import the tensors published for worker ``slot``.  Returns {"owner", "pid",
+    "gpu", "tensors"}, or ``held`` unchanged when nothing new was published."""
+    raw = kv.get_str(key(slot))
+    if raw is None:
+        return held
+    d = json.loads(raw)
+    if held is not None and held.get("owner") == d.get("owner") and held.get("pid") == d.get("pid"):
+        return held
+    from easydl_amd.ps.ipc import import_tensor
+    with torch.cuda.device(int(d.get("gpu", 0))):
+        ts = {}
+        for name, desc in d.get("tensors", {}).items():
+            try:
+                ts[name] = import_tensor(desc)
+            except RuntimeError as e:
+                log.warning("vram: cannot import %s from %s: %s", name, d.get("owner"), e)
+    return {"owner": d.get("owner"), "pid": d.get("pid"), "gpu": int(d.get("gpu", 0)), "tensors": ts}
+
+
+def dead(pid) -> bool:
+    """True once the exporting process is gone: only then may its buffers be written by another."""
+    try:
+        os.kill(int(pid), 0)
+    except ProcessLookupError:
+        return True
+    except (PermissionError, TypeError, ValueError):
+        return False
+    return False
+
+
+def adopt(tensors: dict[str, torch.Tensor]) -> None:
+    """Takeover: these imported tensors back the next FlatParams / optimizer built here."""
+    _ADOPTED.clear()
+    _ADOPTED.update(tensors)
+
+
+def take(name: str, numel: int, dtype: torch.dtype, device) -> torch.Tensor | None:
+    """The adopted tensor for ``name`` if it matches (numel, dtype, device), zero-filled; else None."""
+    t = _ADOPTED.pop(name, None)
+    if t is None:
+        return None
+    dev = torch.device(device)
+    if t.numel() != numel or t.dtype != dtype or t.device != dev:
+        log.warning("vram: adopted %s does not match (%s %s %s vs %s %s %s): allocating", name, t.numel(), t.dtype,
+                    t.device, numel, dtype, dev)
+        return None
+    t.zero_()
+    STATS["adopted"] += 1
+    STATS["adopted_bytes"] += t.numel() * t.element_size()
+    return t
+
+
+def release_unused() -> None:
+    """Drop adopted tensors nothing took (their memory goes back to the driver)."""
+    _ADOPTED.clear()

@@ -1,0 +1,123 @@
+"""VRAM hand-over from a dead worker to the hot standby (easydl_amd/utils/vram.py).
+
+CPU tier: the allocation side (FlatParams / FlatAdamW build on adopted buffers, the group cap,
+mismatches fall back to allocation).  GPU tier: a real IPC export by a child process, imported
+here, still readable after the child has exited, and adopted by the next FlatParams/FlatAdamW.
+"""
+import os
+import subprocess
+import sys
+import time
+
+import pytest
+import torch
+
+from easydl_amd.optim import FlatAdamW
+from easydl_amd.parallel.flat import FlatParams
+from easydl_amd.utils import vram
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _model(seed, device="cpu"):
+    torch.manual_seed(seed)
+    return torch.nn.Sequential(torch.nn.Linear(64, 128), torch.nn.ReLU(), torch.nn.Linear(128, 32)).to(device)
+
+
+def _state(flat, opt):
+    ts = {}
+    for g in flat.groups:
+        ts[f"flat/{g.name}/data"], ts[f"flat/{g.name}/grad"] = g.data, g.grad
+    for g, st in zip(flat.groups, opt.state):
+        for k, t in st.items():
+            if isinstance(t, torch.Tensor) and t is not g.data:
+                ts[f"opt/{g.name}/{k}"] = t
+    return ts
+
+
+def test_group_cap_under_handoff(monkeypatch):
+    monkeypatch.setenv("EDL_VRAM_HANDOFF", "1")
+    monkeypatch.delenv("EDL_FLAT_GROUP_MAX_MB", raising=False)
+    assert vram.enabled() and vram.GROUP_MAX_MB * 2 * 2**20 < vram.IPC_MAX_BYTES
+    # a 1,100 MiB-equivalent budget split: the cap bounds every group (fp32 state < 2 GiB)
+    m = torch.nn.Sequential(*[torch.nn.Linear(64, 64, bias=False) for _ in range(4)]).to(torch.bfloat16)
+    f = FlatParams(m, max_group_bytes=2 * 64 * 64 * 2)   # explicit cap still honoured
+    assert len(f.groups) == 2
+
+
+def test_flat_and_adamw_build_on_adopted_buffers():
+    src = _model(1)
+    f0 = FlatParams(src)
+    o0 = FlatAdamW(f0)
+    old = {k: t.clone().fill_(7.0) for k, t in _state(f0, o0).items()}
+    vram.adopt(old)
+    try:
+        m = _model(2)
+        f1 = FlatParams(m)
+        o1 = FlatAdamW(f1)
+        got = _state(f1, o1)
+        assert set(got) == set(old)
+        for k, t in got.items():
+            assert t.data_ptr() == old[k].data_ptr(), k            # the adopted storage, not a copy
+        for g, st in zip(f1.groups, o1.state):
+            assert torch.count_nonzero(g.grad) == 0                   # zeroed, not the dead worker's 7s
+            assert torch.count_nonzero(st["m"]) == 0 and torch.count_nonzero(st["v"]) == 0
+        for p_new, p_ref in zip(m.parameters(), _model(2).parameters()):
+            assert torch.equal(p_new.data, p_ref.data)                # this process's params were copied in
+        assert vram.STATS["adopted"] >= len(old)
+    finally:
+        vram.release_unused()
+
+
+def test_mismatched_buffer_is_not_adopted():
+    vram.adopt({"flat/decay/data": torch.zeros(3)})
+    try:
+        f = FlatParams(_model(3))
+        assert f.groups[0].data.numel() != 3
+    finally:
+        vram.release_unused()
+
+
+def test_dead_pid():
+    p = subprocess.Popen([sys.executable, "-c", "pass"])
+    p.wait()
+    assert vram.dead(p.pid) and not vram.dead(os.getpid())
+
+
+@pytest.mark.gpu
+def test_ipc_export_survives_the_exporter_and_is_adopted(cuda):
+    import torch.distributed as dist
+
+    from easydl_amd.master.store import KV
+    store = dist.TCPStore("127.0.0.1", 0, is_master=True, wait_for_workers=False)
+    kv = KV(store, "edl/vramtest")
+    env = dict(os.environ, EDL_VRAM_HANDOFF="1", VT_PORT=str(store.port))
+    child = subprocess.Popen([sys.executable, os.path.join(HERE, "helpers", "vram_export_proc.py")], env=env)
+    try:
+        assert kv.wait_for("vt/published", 120)
+        held = vram.import_published(kv, "worker0")
+        assert held and held["pid"] == child.pid and held["tensors"]
+        kv.set("vt/imported", "1")
+        assert child.wait(60) == 0
+        t_end = time.time() + 10
+        while not vram.dead(child.pid) and time.time() < t_end:
+            time.sleep(0.05)
+        # the exporter is gone; the imported memory still holds what it wrote
+        for name, t in held["tensors"].items():
+            assert float(t.float().mean()) == pytest.approx(3.0), name
+        vram.adopt(held["tensors"])
+        torch.manual_seed(5)
+        m = torch.nn.Sequential(torch.nn.Linear(256, 512), torch.nn.Linear(512, 256)).to(cuda, torch.bfloat16)
+        f = FlatParams(m)
+        o = FlatAdamW(f)
+        got = _state(f, o)
+        assert all(got[k].data_ptr() == t.data_ptr() for k, t in held["tensors"].items())
+        g = f.groups[0]
+        g.grad.fill_(1)
+        o.step()                                       # the adopted buffers are live device memory
+        torch.cuda.synchronize()
+        assert torch.isfinite(g.data.float()).all()
+    finally:
+        vram.release_unused()
+        if child.poll() is None:
+            child.kill()
