@@ -345,9 +345,10 @@ class PSClient:
             # The control message leaves once this worker's stream has reached the flag stores
             # (each sender thread waits on the event; the main thread waits for the replies
             # anyway).  Sent earlier, it parks the PS's stream in its flag wait behind this
-            # worker's backward, and every other worker's update queues behind that wait:
-            # config 4 ran 243 samples/s that way vs 316 with the message sent on completion
-            # (profiles/r04_bert_ps_flag_wait.md).  The device wait stays as the ordering guard.
+            # worker's backward, and every other worker's update queues behind that wait: in
+            # config 4 ps_wait_kernel took 7.9 of a PS's 10.2 s of kernel time and the workers'
+            # steady rate fell ~9 % (profiles/r04_bert_ps_flag_wait.md).  The device wait stays
+            # as the ordering guard.
             ready = torch.cuda.Event()
             ready.record(stream)
 
