@@ -73,6 +73,7 @@ struct Seg {
   std::vector<std::thread> pop;
   std::atomic<uint64_t> pop_next{0}, pop_done{0};
   std::atomic<bool> pop_stop{false};
+  std::atomic<bool> drop_running{false};
   uint64_t pop_bytes = 0;
   SegHdr* hdr() { return reinterpret_cast<SegHdr*>(base); }
   SlotHdr* slot(int i) { return reinterpret_cast<SlotHdr*>(base + kHdr * (1 + i)); }
@@ -336,8 +337,7 @@ int edl_shm_slot_info(void* h, int slot, int64_t* step, int64_t* epoch, uint64_t
   return st;
 }
 
-// Populate every slot's pages in `threads` background threads (MADV_POPULATE_WRITE over 64 MiB
-// pieces).  First-touch of tmpfs pages runs at only ~4-5 GB/s however many threads fault them
+// Populate every slot's pages in `threads` background threads (fallocate over 64 MiB pieces).  First-touch of tmpfs pages runs at only ~4-5 GB/s however many threads fault them
 // (measured on the MI355X box: a snapshot's copy into a never-written 96 GB slot stalled the step
 // for 25 s), so a segment is populated off the training path as soon as it exists, and a
 // snapshot waits for (or skips) an unfinished population instead of faulting inside its copy.
@@ -361,12 +361,35 @@ int edl_shm_populate_async(void* h, int threads) {
         const uint64_t lo = s->pop_next.fetch_add(piece);
         if (lo >= s->pop_bytes) return;
         const uint64_t len = lo + piece > s->pop_bytes ? s->pop_bytes - lo : piece;
-        if (madvise(d0 + lo, len, MADV_POPULATE_WRITE) != 0)
-          madvise(d0 + lo, len, MADV_POPULATE_READ);  // kernels without POPULATE_WRITE
+        // fallocate allocates the file's pages without mapping them here (no page-table
+        // entries to tear down at exit); kernels / filesystems without it: fault them in
+        if (fallocate(s->fd, 0, (off_t)(d0 - s->base + lo), (off_t)len) != 0 &&
+            madvise(d0 + lo, len, MADV_POPULATE_WRITE) != 0)
+          madvise(d0 + lo, len, MADV_POPULATE_READ);
         s->pop_done.fetch_add(len);
       }
     });
   }
+  return 0;
+}
+
+// Drop this process's page-table entries of every slot (MADV_DONTNEED: a shared tmpfs mapping
+// keeps its data) on a background thread, 256 MiB at a time so an allocation that needs the
+// address-space lock never waits long behind it.  A restore reads a slot through the mapping
+// and leaves ~100 GB mapped; this keeps a later death of this process cheap to tear down.
+int edl_shm_drop_mapped_async(void* h) {
+  auto* s = static_cast<Seg*>(h);
+  uint8_t* d0 = s->data(0);
+  const uint64_t bytes = s->hdr()->slot_bytes * s->hdr()->nslots;
+  if (s->drop_running.exchange(true)) return -1;  // one at a time
+  std::thread([s, d0, bytes] {
+    const uint64_t chunk = 256ull << 20;
+    for (uint64_t lo = 0; lo < bytes && !s->pop_stop.load(); lo += chunk) {
+      madvise(d0 + lo, lo + chunk > bytes ? bytes - lo : chunk, MADV_DONTNEED);
+      usleep(200);
+    }
+    s->drop_running = false;
+  }).detach();
   return 0;
 }
 
@@ -381,6 +404,7 @@ static void populate_join(Seg* s) {
   s->pop_stop = true;
   for (auto& t : s->pop) t.join();
   s->pop.clear();
+  while (s->drop_running.load()) usleep(1000);  // the detached dropper reads s
 }
 
 int edl_shm_close(void* h, int unlink_seg) {
@@ -483,6 +507,7 @@ struct Engine {
   std::vector<void*> stage;
   std::vector<hipEvent_t> sev;
   CopyPool* pool = nullptr;
+  bool windowed = true;                  // EDL_SNAPSHOT_WINDOW=0: copy through the segment mapping
   double last_staged[4] = {0, 0, 0, 0};  // d2h_wait_s, copy_s, total_s, bytes of the last staged job
 };
 
@@ -504,15 +529,16 @@ hipError_t run_staged(Engine* e, Job& j) {
   }
   struct Piece {
     const uint8_t* src;
-    uint8_t* dst;
+    uint64_t fo;  // byte offset in the segment file
     uint64_t n;
   };
   std::vector<Piece> pieces;
-  uint8_t* base = j.seg->data(j.slot);
+  const uint64_t slot_fo = (uint64_t)(j.seg->data(j.slot) - j.seg->base);
   for (size_t b = 0; b < j.ptrs.size(); ++b)
     for (uint64_t off = 0; off < j.sizes[b]; off += e->stage_bytes)
-      pieces.push_back({(const uint8_t*)j.ptrs[b] + off, base + j.offs[b] + off,
+      pieces.push_back({(const uint8_t*)j.ptrs[b] + off, slot_fo + j.offs[b] + off,
                         j.sizes[b] - off < e->stage_bytes ? j.sizes[b] - off : e->stage_bytes});
+  static const uint64_t page = (uint64_t)sysconf(_SC_PAGESIZE);
   const double t_start = now_s();
   double wait_s = 0, copy_s = 0;
   uint64_t bytes = 0;
@@ -530,7 +556,21 @@ hipError_t run_staged(Engine* e, Job& j) {
       e->cv_reads.notify_all();
     }
     t0 = now_s();
-    e->pool->run(pieces[c].dst, (const uint8_t*)e->stage[k], pieces[c].n);
+    // Written through a window mapped for this piece only, not through the segment's
+    // process-wide mapping: every page of a snapshot slot mapped in this process is a page
+    // table entry the kernel must tear down when the process dies, and the operator hands
+    // the GPU to a replacement only after that (19 ms per GB on the MI355X box,
+    // scripts/exit_cost_probe.cpp: ~3.6 s for a 192 GB slot pair).  The window costs a
+    // minor fault per page and a 128 MB unmap per piece, off the training thread.
+    const uint64_t a = pieces[c].fo & ~(page - 1), d = pieces[c].fo - a, len = d + pieces[c].n;
+    uint8_t* w = e->windowed ? (uint8_t*)mmap(nullptr, len, PROT_READ | PROT_WRITE, MAP_SHARED, j.seg->fd, (off_t)a)
+                             : (uint8_t*)MAP_FAILED;
+    if (w != (uint8_t*)MAP_FAILED) {
+      e->pool->run(w + d, (const uint8_t*)e->stage[k], pieces[c].n);
+      munmap(w, len);
+    } else {
+      e->pool->run(j.seg->base + pieces[c].fo, (const uint8_t*)e->stage[k], pieces[c].n);
+    }
     copy_s += now_s() - t0;
     bytes += pieces[c].n;
     return hipSuccess;
@@ -597,6 +637,8 @@ extern "C" {
 void* edl_ckpt_engine_create(int device, uint64_t chunk_bytes, int copy_cus) {
   auto* e = new Engine();
   e->device = device;
+  const char* win = getenv("EDL_SNAPSHOT_WINDOW");
+  e->windowed = !(win && win[0] == '0');
   if (chunk_bytes) e->chunk = chunk_bytes;
   if (hipSetDevice(device) != hipSuccess) {
     delete e;

@@ -144,10 +144,18 @@ class ShmSegment:
         """Fault every slot's pages in on background threads (csrc: edl_shm_populate_async)."""
         return self.rt("edl_shm_populate_async", self.h, threads) == 0
 
-    def populated(self) -> bool:
-        """False while a background population is still running."""
+    def drop_mapped_async(self) -> None:
+        """Drop this process's page tables of the slots in the background (data stays)."""
+        self.rt("edl_shm_drop_mapped_async", self.h)
+
+    def populated(self, slot: int | None = None) -> bool:
+        """False while a background population is still running (``slot``: only as far as the
+        end of that slot; population runs slot 0 first, and a straggling piece of it is just
+        faulted in by the copy)."""
         total = ctypes.c_uint64()
         done = self.rt("edl_shm_populate_progress", self.h, ctypes.byref(total))
+        if slot is not None and total.value:
+            return done >= min(total.value, (slot + 1) * self.slot_bytes)
         return done >= total.value
 
     def close(self, unlink: bool = False):
@@ -237,7 +245,7 @@ class CheckpointManager:
         # (EDL_SHM_POPULATE_THREADS, 0 = never); the first snapshot waits for what is left.  A
         # segment adopted by a restore skips snapshots until its population is done instead:
         # the restored slot already holds a valid snapshot, and recovery should not stall.
-        self.populate_threads = int(os.environ.get("EDL_SHM_POPULATE_THREADS", 16))
+        self.populate_threads = int(os.environ.get("EDL_SHM_POPULATE_THREADS", 4))
         self._skip_populating = False
         self._seg: ShmSegment | None = None
         self._seg_key = None
@@ -494,12 +502,12 @@ class CheckpointManager:
         self.wait()  # at most one snapshot in flight (and never one across a segment change)
         # (the first segment gets headroom: the largest shard of a world one rank smaller)
         seg = self._layout_segment(world, shard, tag, state, headroom)
-        if not seg.populated():
+        if not seg.populated(self._next_slot(seg)):
             if self._skip_populating:
                 self.stats["skipped_populating"] = self.stats.get("skipped_populating", 0) + 1
                 return
             t0 = time.perf_counter()
-            while not seg.populated():
+            while not seg.populated(self._next_slot(seg)):
                 time.sleep(0.01)
             self.stats["populate_wait_s"] = round(self.stats.get("populate_wait_s", 0) + time.perf_counter() - t0, 3)
         if getattr(self, "_old_name", None) and self._kept_slot_next(seg):
@@ -689,9 +697,13 @@ class CheckpointManager:
                 if keep:
                     self._seg, self._seg_key = seg, own
                     self.stats["adopted"] = self.stats.get("adopted", 0) + 1
+                    if dev.type == "cuda":
+                        # the restore read the slot through the mapping: drop those page-table
+                        # entries again (a later death of this process tears down none of them)
+                        seg.drop_mapped_async()
                     if self.populate_threads > 0 and dev.type == "cuda":
-                        # pages the dead writer never touched (a slot it was still filling) fault in
-                        # off the recovery path; snapshots wait for that by skipping
+                        # pages the dead writer never touched (a slot it was still filling) are
+                        # allocated off the recovery path; snapshots wait for that by skipping
                         seg.populate_async(self.populate_threads)
                         self._skip_populating = True
                 else:
