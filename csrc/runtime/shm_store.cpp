@@ -337,7 +337,8 @@ int edl_shm_slot_info(void* h, int slot, int64_t* step, int64_t* epoch, uint64_t
   return st;
 }
 
-// Populate every slot's pages in `threads` background threads (fallocate over 64 MiB pieces).  First-touch of tmpfs pages runs at only ~4-5 GB/s however many threads fault them
+// Populate every slot's pages in `threads` background threads (fallocate over 64 MiB pieces).
+// First-touch of tmpfs pages runs at only ~4-5 GB/s however many threads fault them
 // (measured on the MI355X box: a snapshot's copy into a never-written 96 GB slot stalled the step
 // for 25 s), so a segment is populated off the training path as soon as it exists, and a
 // snapshot waits for (or skips) an unfinished population instead of faulting inside its copy.
