@@ -68,6 +68,11 @@ int main(int argc, char** argv) {
     if (mode == "touch_read") par(p, bytes, 16, MADV_POPULATE_READ);
     if (mode == "populate_write" || mode == "populate_write_unmap") par(p, bytes, 16, MADV_POPULATE_WRITE);
     if (mode == "memcpy") par(p, bytes, 16, 0);
+    if (mode == "gpu_memcpy") {  // a GPU context (and VRAM) plus a populated mapping
+      void* d = nullptr;
+      hipMalloc(&d, 1ull << 30);
+      par(p, bytes, 16, 0);
+    }
     if (mode == "pin") {
       hipError_t e = hipHostRegister(p, bytes, hipHostRegisterPortable);
       if (e != hipSuccess) fprintf(stderr, "hipHostRegister %d\n", (int)e);
@@ -82,12 +87,23 @@ int main(int argc, char** argv) {
   }
   char buf[128] = {0};
   if (read(pfd[0], buf, sizeof buf - 1) <= 0) return 6;
-  double t0 = now();
+  // the KFD process entry of the child: it disappears when the driver has torn down the
+  // child's GPU queues, which may be long before the kernel has reaped the process
+  char kfd[96];
+  snprintf(kfd, sizeof kfd, "/sys/class/kfd/kfd/proc/%d", (int)pid);
+  const bool had_kfd = access(kfd, F_OK) == 0;
+  double t0 = now(), t_kfd = -1;
   kill(pid, SIGKILL);
   int st;
-  waitpid(pid, &st, 0);
+  for (;;) {
+    if (t_kfd < 0 && had_kfd && access(kfd, F_OK) != 0) t_kfd = now() - t0;
+    if (waitpid(pid, &st, WNOHANG) == pid) break;
+    usleep(500);
+  }
   double t1 = now();
-  printf("mode=%s gib=%lu setup/unmap_s=%s exit_s=%.3f\n", mode.c_str(), bytes >> 30, buf, t1 - t0);
+  if (had_kfd && t_kfd < 0) t_kfd = t1 - t0;
+  printf("mode=%s gib=%lu setup/unmap_s=%s exit_s=%.3f kfd_entry=%d kfd_gone_s=%.3f\n", mode.c_str(), bytes >> 30, buf,
+         t1 - t0, (int)had_kfd, t_kfd);
   shm_unlink(name);
   return 0;
 }
