@@ -524,7 +524,7 @@ struct Engine {
   std::vector<void*> stage;
   std::vector<hipEvent_t> sev;
   CopyPool* pool = nullptr;
-  bool windowed = true;                  // EDL_SNAPSHOT_WINDOW=0: copy through the segment mapping
+  bool windowed = false;                 // EDL_SNAPSHOT_WINDOW=1: copy through per-piece windows
   double last_staged[4] = {0, 0, 0, 0};  // d2h_wait_s, copy_s, total_s, bytes of the last staged job
 };
 
@@ -655,7 +655,7 @@ void* edl_ckpt_engine_create(int device, uint64_t chunk_bytes, int copy_cus) {
   auto* e = new Engine();
   e->device = device;
   const char* win = getenv("EDL_SNAPSHOT_WINDOW");
-  e->windowed = !(win && win[0] == '0');
+  e->windowed = win && win[0] == '1';
   if (chunk_bytes) e->chunk = chunk_bytes;
   if (hipSetDevice(device) != hipSuccess) {
     delete e;

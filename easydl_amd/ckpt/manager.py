@@ -247,6 +247,7 @@ class CheckpointManager:
         # the restored slot already holds a valid snapshot, and recovery should not stall.
         self.populate_threads = int(os.environ.get("EDL_SHM_POPULATE_THREADS", 4))
         self._skip_populating = False
+        self._verify = None         # pending post-teardown check of an early hand-over (fence)
         self._seg: ShmSegment | None = None
         self._seg_key = None
         self._old_name = None       # previous layout's name of a relinked segment (see _segment)
@@ -584,8 +585,37 @@ class CheckpointManager:
            int(os.environ.get("EDL_CKPT_STAGES", 4)), int(os.environ.get("EDL_CKPT_COPY_THREADS", 16)))
         return e
 
+    def _verify_handover(self) -> None:
+        """After an early hand-over (operator/reconciler.py _early_replace) the restore wrote
+        HBM adopted from a process the kernel had not finished tearing down.  Its GPU queues
+        were gone (its address space was released first), but wait for the reap and check
+        that the restored state is still exactly what the snapshot held, before the first
+        optimizer step changes it: the master weights / moments by their checksum, the bf16
+        weights against the master."""
+        v, self._verify = self._verify, None
+        from easydl_amd.utils import vram
+        t0 = time.perf_counter()
+        while not vram.reaped(v["pid"]) and time.perf_counter() - t0 < 120:
+            time.sleep(0.005)
+        for items, expect in v["shards"]:
+            acc = torch.zeros(1, dtype=torch.int64, device=items[0][0].device)
+            for dst, off in items:
+                checksum_tensor(dst, acc, base_index=off // 4)
+            got = int(acc.item()) & ((1 << 64) - 1)
+            if got != expect:
+                raise RuntimeError(f"restored state changed during the previous worker's teardown: {got:#x} != "
+                                   f"{expect:#x}")
+        tr = v["trainer"]
+        for g, st in zip(tr.flat.groups, getattr(tr.opt, "state", [])):
+            m = st.get("master")
+            if m is not None and m is not g.data and not torch.equal(g.data, m.to(g.data.dtype)):
+                raise RuntimeError(f"restored weights of {g.name} changed during the previous worker's teardown")
+        self.stats["handover_verified_s"] = round(time.perf_counter() - t0, 3)
+
     def fence(self) -> None:
         """Make the current stream wait for the in-flight snapshot (call before the optimizer)."""
+        if self._verify is not None:
+            self._verify_handover()
         if self._ticket is not None and self._engine is not None:
             _native.runtime()("edl_ckpt_fence", self._engine, self._ticket,
                               ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
@@ -679,14 +709,17 @@ class CheckpointManager:
         dev = next(iter(state.values())).device
         phases = {"find_s": round(t0 - t_start, 3)}
         own = self._own_key(trainer)
+        verify = []
         for s, info in enumerate(infos):
             t1 = time.perf_counter()
             seg = _open_segment(self.seg_name(world, s, tag))
             phases["open_s"] = round(phases.get("open_s", 0) + time.perf_counter() - t1, 3)
             keep = False
             try:
-                _load_shard(lambda off, nb: seg.view(info["slot"], off, nb), info["meta"]["t"], state, dev,
-                            info["checksum"], f"shm shard {s} of step {step}", seg=seg, slot=info["slot"])
+                loaded = _load_shard(lambda off, nb: seg.view(info["slot"], off, nb), info["meta"]["t"], state, dev,
+                                     info["checksum"], f"shm shard {s} of step {step}", seg=seg, slot=info["slot"])
+                if loaded is not None:
+                    verify.append(loaded)
                 # The segment this rank will write next (same layout, e.g. the only worker restarted):
                 # keep the mapping as this rank's snapshot segment.  Unmapping ~100 GB of populated
                 # pages costs seconds and takes the address-space lock the first step's allocations
@@ -714,6 +747,12 @@ class CheckpointManager:
             torch.cuda.current_stream(dev).synchronize()
         phases["finish_s"] = round(time.perf_counter() - t2, 3)
         LAST_RESTORE_STATS.update(phases)
+        from easydl_amd.utils import vram
+        pid = vram.ADOPTED_FROM.get("pid")
+        if verify and pid is not None and not vram.reaped(pid):
+            # this state lives in HBM adopted from a worker that is still being torn down
+            # (early hand-over): re-verify it once that process is gone, before the first update
+            self._verify = {"pid": pid, "shards": verify, "trainer": trainer}
         meta = infos[0]["meta"]
         self._restore_scalars(trainer, meta)
         _load_host_state(trainer, meta.get("host"))
@@ -893,7 +932,7 @@ def _load_shard(read, table, state, dev, expect: int, what: str, seg=None, slot=
         LAST_RESTORE_STATS["checksum_s"] = round(time.perf_counter() - t_cs, 3)
         if got != expect:
             raise RuntimeError(f"checksum mismatch in {what}: {got:#x} != {expect:#x}")
-        return
+        return items, expect
     total = 0
     for name, dt, numel, lo, hi, off in table:
         t = state[name]

@@ -32,6 +32,7 @@ from dataclasses import dataclass, field
 
 from easydl_amd.api.spec import ROLE_SHORT, ElasticJob, JobResource, Resource
 from easydl_amd.utils.events import EventLog
+from easydl_amd.utils.procfs import mm_released
 
 log = logging.getLogger("edl.operator")
 
@@ -391,6 +392,10 @@ class ElasticOperator:
         p = next((q for q in list(self.procs.values()) + self.history if q.pid == ex.pid), None)
         if p is None:
             return
+        if getattr(p, "_early_replaced", False):   # already replaced when its address space went away
+            self.events.emit("exit", name=p.name, pid=p.pid, code=ex.exit_code, signal=ex.signal, role=p.role,
+                             early=True)
+            return
         p.exit_code = ex.exit_code if not ex.signal else -ex.signal
         self.events.emit("exit", name=p.name, pid=p.pid, code=ex.exit_code, signal=ex.signal, role=p.role)
         if p.role == "trainer":
@@ -473,8 +478,42 @@ class ElasticOperator:
                 except Exception:
                     pass
 
+    def _early_replace(self) -> None:
+        """Replace a dying worker once its address space is gone, before the kernel has torn
+        it down and reaped it.  The GPU's queues of a process are destroyed at the start of
+        its address-space teardown (the amdkfd MMU-notifier release), but tearing down the
+        page tables of a large mapped snapshot segment takes ~19 ms per GB after that
+        (scripts/exit_cost_probe.cpp); the replacement does not wait for it.  A replacement
+        that adopted the dead worker's HBM re-verifies its restored state once the dead
+        process is reaped, before its first optimizer step (ckpt/manager.py fence).
+        EDL_EARLY_HANDOVER=0: wait for the reap as before."""
+        if os.environ.get("EDL_EARLY_HANDOVER", "1") == "0":
+            return
+        now = time.time()
+        for p in list(self.procs.values()):
+            if p.role != "worker" or p.state != "running" or not getattr(p, "_early_reported", False):
+                continue
+            if not mm_released(p.pid):
+                continue
+            t = getattr(p, "_mm_gone_ts", None)
+            if t is None:
+                p._mm_gone_ts = now
+                continue
+            if now - t < 0.1:   # grace for the driver's queue teardown
+                continue
+            p._early_replaced = True
+            p.exit_code = -signal.SIGKILL
+            self.events.emit("exit_early", name=p.name, pid=p.pid, role=p.role, mm_gone_s=round(now - t, 3))
+            self._release_gpu(p)
+            p.state = "exited"
+            self.restarts += 1
+            if self.procs.get(p.name) is p:
+                del self.procs[p.name]
+                self.history.append(p)
+
     def tick(self, timeout_s: float = 0.05) -> None:
         self._early_exits()
+        self._early_replace()
         for ex in self.launcher.poll(timeout_s):
             self.handle_exit(ex)
         self._poll_jobresource()

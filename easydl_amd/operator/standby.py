@@ -85,7 +85,7 @@ def _adopt_vram(held: dict, slot: str, kv, name: str) -> None:
     if not vram.dead(got.get("pid")):
         print(f"standby: {slot}'s exporter {got.get('pid')} is alive; not adopting", file=sys.stderr)
         return
-    vram.adopt(got["tensors"])
+    vram.adopt(got["tensors"], pid=got.get("pid"))
     kv.set(f"standby/vram/{name}", json.dumps({"slot": slot, "from": got.get("owner"),
                                                "tensors": len(got["tensors"])}))
 

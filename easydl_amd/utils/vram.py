@@ -96,20 +96,43 @@ def import_published(kv, slot: str, held: dict | None = None) -> dict | None:
 
 
 def dead(pid) -> bool:
-    """True once the exporting process is gone: only then may its buffers be written by another."""
+    """True once the exporting process runs no more GPU work: reaped, or its address space
+    is released (utils/procfs.py) -- only then may another process write its buffers."""
+    from easydl_amd.utils.procfs import mm_released
     try:
         os.kill(int(pid), 0)
     except ProcessLookupError:
         return True
     except (PermissionError, TypeError, ValueError):
         return False
-    return False
+    return mm_released(int(pid))
 
 
-def adopt(tensors: dict[str, torch.Tensor]) -> None:
+def reaped(pid) -> bool:
+    try:
+        os.kill(int(pid), 0)
+    except ProcessLookupError:
+        return True
+    except (PermissionError, TypeError, ValueError):
+        return False
+    # a zombie counts: its teardown is complete
+    try:
+        with open(f"/proc/{int(pid)}/stat") as f:
+            return f.read().rsplit(")", 1)[1].split()[0] in ("Z", "X")
+    except OSError:
+        return True
+
+
+ADOPTED_FROM: dict = {}          # {"pid": ...} of the process whose buffers were adopted
+
+
+def adopt(tensors: dict[str, torch.Tensor], pid=None) -> None:
     """Takeover: these imported tensors back the next FlatParams / optimizer built here."""
     _ADOPTED.clear()
     _ADOPTED.update(tensors)
+    ADOPTED_FROM.clear()
+    if pid is not None:
+        ADOPTED_FROM["pid"] = int(pid)
 
 
 def take(name: str, numel: int, dtype: torch.dtype, device) -> torch.Tensor | None:

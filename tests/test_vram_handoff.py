@@ -121,3 +121,23 @@ def test_ipc_export_survives_the_exporter_and_is_adopted(cuda):
         vram.release_unused()
         if child.poll() is None:
             child.kill()
+
+
+def test_mm_released_tracks_a_killed_process():
+    import signal as _signal
+
+    from easydl_amd.utils.procfs import mm_released
+    assert not mm_released(os.getpid())
+    p = subprocess.Popen([sys.executable, "-c", "import time; time.sleep(60)"])
+    try:
+        time.sleep(0.2)
+        assert not mm_released(p.pid)
+        os.kill(p.pid, _signal.SIGKILL)
+        t_end = time.time() + 10
+        while not mm_released(p.pid) and time.time() < t_end:   # a zombie holds no address space
+            time.sleep(0.01)
+        assert mm_released(p.pid) and vram.dead(p.pid)
+        assert vram.reaped(p.pid)                                # zombie: teardown complete
+    finally:
+        p.wait()
+    assert mm_released(p.pid) and vram.reaped(p.pid)
