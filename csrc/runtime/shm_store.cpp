@@ -73,8 +73,8 @@ struct Seg {
   std::vector<std::thread> pop;
   std::atomic<uint64_t> pop_next{0}, pop_done{0};
   std::atomic<bool> pop_stop{false};
-  std::atomic<bool> drop_running{false};
   uint64_t pop_bytes = 0;
+  bool pop_map = true;  // also map the populated pages into this process (see populate_async)
   SegHdr* hdr() { return reinterpret_cast<SegHdr*>(base); }
   SlotHdr* slot(int i) { return reinterpret_cast<SlotHdr*>(base + kHdr * (1 + i)); }
   uint8_t* data(int i) {
@@ -378,35 +378,22 @@ int edl_shm_populate_async(void* h, int threads) {
         const uint64_t lo = s->pop_next.fetch_add(piece);
         if (lo >= s->pop_bytes) return;
         const uint64_t len = lo + piece > s->pop_bytes ? s->pop_bytes - lo : piece;
-        // fallocate allocates the file's pages without mapping them here (no page-table
-        // entries to tear down at exit); kernels / filesystems without it: fault them in
+        // fallocate allocates the file's pages (the slow first touch, ~4 GB/s here); one read
+        // per 64 KiB then maps them into this process 16 pages per fault (fault-around), so a
+        // snapshot's copy takes no page fault.  Kernels / filesystems without fallocate: fault
+        // the pages in directly.
         if (fallocate(s->fd, 0, (off_t)(d0 - s->base + lo), (off_t)len) != 0 &&
             madvise(d0 + lo, len, MADV_POPULATE_WRITE) != 0)
           madvise(d0 + lo, len, MADV_POPULATE_READ);
+        if (s->pop_map) {
+          volatile uint8_t sink = 0;
+          for (uint64_t o = 0; o < len; o += 65536) sink = sink + d0[lo + o];
+          (void)sink;
+        }
         s->pop_done.fetch_add(len);
       }
     });
   }
-  return 0;
-}
-
-// Drop this process's page-table entries of every slot (MADV_DONTNEED: a shared tmpfs mapping
-// keeps its data) on a background thread, 256 MiB at a time so an allocation that needs the
-// address-space lock never waits long behind it.  A restore reads a slot through the mapping
-// and leaves ~100 GB mapped; this keeps a later death of this process cheap to tear down.
-int edl_shm_drop_mapped_async(void* h) {
-  auto* s = static_cast<Seg*>(h);
-  uint8_t* d0 = s->data(0);
-  const uint64_t bytes = s->hdr()->slot_bytes * s->hdr()->nslots;
-  if (s->drop_running.exchange(true)) return -1;  // one at a time
-  std::thread([s, d0, bytes] {
-    const uint64_t chunk = 256ull << 20;
-    for (uint64_t lo = 0; lo < bytes && !s->pop_stop.load(); lo += chunk) {
-      madvise(d0 + lo, lo + chunk > bytes ? bytes - lo : chunk, MADV_DONTNEED);
-      usleep(200);
-    }
-    s->drop_running = false;
-  }).detach();
   return 0;
 }
 
@@ -421,7 +408,6 @@ static void populate_join(Seg* s) {
   s->pop_stop = true;
   for (auto& t : s->pop) t.join();
   s->pop.clear();
-  while (s->drop_running.load()) usleep(1000);  // the detached dropper reads s
 }
 
 int edl_shm_close(void* h, int unlink_seg) {
@@ -586,7 +572,7 @@ hipError_t run_staged(Engine* e, Job& j) {
       e->pool->run(w + d, (const uint8_t*)e->stage[k], pieces[c].n, true);
       munmap(w, len);
     } else {
-      e->pool->run(j.seg->base + pieces[c].fo, (const uint8_t*)e->stage[k], pieces[c].n);
+      e->pool->run(j.seg->base + pieces[c].fo, (const uint8_t*)e->stage[k], pieces[c].n, true);
     }
     copy_s += now_s() - t0;
     bytes += pieces[c].n;

@@ -52,7 +52,6 @@ SIGS = {
     "edl_ckpt_engine_staged_stats": (None, [vp, ctypes.POINTER(ctypes.c_double)]),
     "edl_shm_pinned": (i32, [vp]),
     "edl_shm_populate_async": (i32, [vp, i32]),
-    "edl_shm_drop_mapped_async": (i32, [vp]),
     "edl_shm_populate_progress": (u64, [vp, u64p]),
     "edl_ckpt_restore_pipelined": (i32, [vp, i32, i32, u64p, u64p, u64p, vp, u64, i32]),
     "edl_ckpt_restore_pipelined2": (i32, [vp, i32, i32, u64p, u64p, u64p, vp, u64, i32, i32,

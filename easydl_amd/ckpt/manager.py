@@ -144,10 +144,6 @@ class ShmSegment:
         """Fault every slot's pages in on background threads (csrc: edl_shm_populate_async)."""
         return self.rt("edl_shm_populate_async", self.h, threads) == 0
 
-    def drop_mapped_async(self) -> None:
-        """Drop this process's page tables of the slots in the background (data stays)."""
-        self.rt("edl_shm_drop_mapped_async", self.h)
-
     def populated(self, slot: int | None = None) -> bool:
         """False while a background population is still running (``slot``: only as far as the
         end of that slot; population runs slot 0 first, and a straggling piece of it is just
@@ -730,10 +726,6 @@ class CheckpointManager:
                 if keep:
                     self._seg, self._seg_key = seg, own
                     self.stats["adopted"] = self.stats.get("adopted", 0) + 1
-                    if dev.type == "cuda":
-                        # the restore read the slot through the mapping: drop those page-table
-                        # entries again (a later death of this process tears down none of them)
-                        seg.drop_mapped_async()
                     if self.populate_threads > 0 and dev.type == "cuda":
                         # pages the dead writer never touched (a slot it was still filling) are
                         # allocated off the recovery path; snapshots wait for that by skipping

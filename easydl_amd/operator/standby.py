@@ -72,6 +72,15 @@ def _import_vram(kv, held: dict) -> None:
             held[slot] = vram.import_published(kv, slot, held.get(slot))
         except Exception as e:  # noqa: BLE001 - a worker mid-restart: try again next scan
             print(f"standby: vram import of {slot} failed: {e}", file=sys.stderr)
+    # An exporter that died without this standby taking its place (a scale-down, another
+    # spare took it, the job ended): let its HBM go back to the driver.
+    now = time.monotonic()
+    for slot, h in list(held.items()):
+        if h is None or not vram.reaped(h.get("pid")):
+            continue
+        h.setdefault("dead_since", now)
+        if now - h["dead_since"] > 10.0:
+            del held[slot]
 
 
 def _adopt_vram(held: dict, slot: str, kv, name: str) -> None:

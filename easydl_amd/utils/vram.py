@@ -84,6 +84,8 @@ def import_published(kv, slot: str, held: dict | None = None) -> dict | None:
     d = json.loads(raw)
     if held is not None and held.get("owner") == d.get("owner") and held.get("pid") == d.get("pid"):
         return held
+    if d.get("pid") is None or reaped(d["pid"]):
+        return held     # never map the handles of a process that is gone (its memory may be freed)
     from easydl_amd.ps.ipc import import_tensor
     with torch.cuda.device(int(d.get("gpu", 0))):
         ts = {}
