@@ -120,6 +120,8 @@ class ElasticTrainer:
         self.checkpoint = checkpoint
         self.log_every = log_every
         self._phases = os.environ.get("EDL_STEP_PHASES", "0") == "1"
+        self._step_sync = self._phases or os.environ.get("EDL_STEP_SYNC", "0") == "1"
+        self._sync_next = True
         self.rdzv_config = rdzv_config
         self._store = store
         self._manager = None
@@ -239,6 +241,7 @@ class ElasticTrainer:
 
     def _enter_epoch(self):
         """Join the next live epoch; retries when the epoch breaks while it is being built."""
+        self._sync_next = True
         while True:
             t0 = time.time()
             if self.rdzv is None:
@@ -615,9 +618,16 @@ class ElasticTrainer:
         return None if loss_acc is None else loss_acc / total
 
     def _sync_point(self) -> bool:
-        """Host-side completion of every gradient all-reduce; False if the epoch broke."""
-        if self.device.type == "cuda":
+        """Host-side completion of every gradient all-reduce; False if the epoch broke.
+
+        At world 1 there is no collective whose outcome the commit must wait for, so the
+        host does not drain the stream: it goes on enqueueing the optimizer and the next
+        step while the GPU works (no per-step bubble; EDL_STEP_SYNC=1 restores the drain)."""
+        if self.device.type == "cuda" and (self.comm.world_size > 1 or self._step_sync or self._sync_next):
+            # (the first step of an epoch always completes on the GPU before it counts:
+            # time-to-recover is measured to a finished step)
             torch.cuda.current_stream(self.device).synchronize()
+        self._sync_next = False
         if self.comm.aborted:
             return False
         if not self.comm.healthy():  # a hand-written collective hit its deadline: the grads are not a sum
