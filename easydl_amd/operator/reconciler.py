@@ -32,7 +32,7 @@ from dataclasses import dataclass, field
 
 from easydl_amd.api.spec import ROLE_SHORT, ElasticJob, JobResource, Resource
 from easydl_amd.utils.events import EventLog
-from easydl_amd.utils.procfs import mm_released
+from easydl_amd.utils.procfs import exit_status, mm_released
 
 log = logging.getLogger("edl.operator")
 
@@ -495,6 +495,8 @@ class ElasticOperator:
                 continue
             if not mm_released(p.pid):
                 continue
+            if not exit_status(p.pid):   # a normal exit(0) (or unknown): its reap decides, as before
+                continue
             t = getattr(p, "_mm_gone_ts", None)
             if t is None:
                 p._mm_gone_ts = now
@@ -502,7 +504,8 @@ class ElasticOperator:
             if now - t < 0.1:   # grace for the driver's queue teardown
                 continue
             p._early_replaced = True
-            p.exit_code = -signal.SIGKILL
+            st = exit_status(p.pid) or 0
+            p.exit_code = -(st & 0x7F) if st & 0x7F else (st >> 8) & 0xFF
             self.events.emit("exit_early", name=p.name, pid=p.pid, role=p.role, mm_gone_s=round(now - t, 3))
             self._release_gpu(p)
             p.state = "exited"

@@ -23,3 +23,15 @@ def mm_released(pid: int) -> bool:
         except OSError:
             continue
     return True
+
+
+def exit_status(pid: int) -> int | None:
+    """The wait status a dying (or zombie) process will report (/proc/<pid>/stat field 52,
+    set at the start of its exit), or None if it is gone or the field is unavailable.
+    0: a normal exit(0); a SIGKILL reads 9."""
+    try:
+        with open(f"/proc/{pid}/stat") as f:
+            fields = f.read().rsplit(")", 1)[1].split()
+        return int(fields[49])       # field 52; fields[0] is field 3 (state)
+    except (OSError, IndexError, ValueError):
+        return None

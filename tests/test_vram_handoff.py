@@ -126,7 +126,7 @@ def test_ipc_export_survives_the_exporter_and_is_adopted(cuda):
 def test_mm_released_tracks_a_killed_process():
     import signal as _signal
 
-    from easydl_amd.utils.procfs import mm_released
+    from easydl_amd.utils.procfs import exit_status, mm_released
     assert not mm_released(os.getpid())
     p = subprocess.Popen([sys.executable, "-c", "import time; time.sleep(60)"])
     try:
@@ -138,6 +138,22 @@ def test_mm_released_tracks_a_killed_process():
             time.sleep(0.01)
         assert mm_released(p.pid) and vram.dead(p.pid)
         assert vram.reaped(p.pid)                                # zombie: teardown complete
+        assert exit_status(p.pid) == _signal.SIGKILL
     finally:
         p.wait()
     assert mm_released(p.pid) and vram.reaped(p.pid)
+
+
+def test_exit_status_of_a_normal_exit_is_zero():
+    from easydl_amd.utils.procfs import exit_status
+    p = subprocess.Popen([sys.executable, "-c", "pass"])
+    t_end = time.time() + 20
+    while exit_status(p.pid) is not None and time.time() < t_end:
+        st = exit_status(p.pid)
+        with open(f"/proc/{p.pid}/stat") as f:
+            zombie = f.read().rsplit(")", 1)[1].split()[0] == "Z"
+        if zombie:
+            assert st == 0          # exit(0): the operator waits for the reap (no early hand-over)
+            break
+        time.sleep(0.01)
+    p.wait()
