@@ -27,6 +27,7 @@ from __future__ import annotations
 import json
 import logging
 import os
+import time
 
 import torch
 
@@ -64,7 +65,8 @@ def publish(kv, slot: str, owner: str, tensors: dict[str, torch.Tensor]) -> int:
         except RuntimeError as e:   # e.g. a tensor this process itself imported (an adopted buffer)
             log.debug("vram: %s not exportable: %s", name, e)
     gpu = next((t.device.index for t in tensors.values() if t is not None and t.is_cuda), 0)
-    kv.set(key(slot), json.dumps({"owner": owner, "pid": os.getpid(), "gpu": gpu, "tensors": descs}))
+    kv.set(key(slot), json.dumps({"owner": owner, "pid": os.getpid(), "gpu": gpu, "gen": time.time_ns(),
+                                  "tensors": descs}))
     if slot not in slots(kv):
         kv.append("vram/slots", slot + ",")
     STATS["exported"] = len(descs)
@@ -82,8 +84,13 @@ def import_published(kv, slot: str, held: dict | None = None) -> dict | None:
     if raw is None:
         return held
     d = json.loads(raw)
-    if held is not None and held.get("owner") == d.get("owner") and held.get("pid") == d.get("pid"):
+    if held is not None and (held.get("owner"), held.get("pid"), held.get("gen")) == (
+            d.get("owner"), d.get("pid"), d.get("gen")):
         return held
+    # a new export (new process, or the same one after rebuilding its buffers): the old
+    # imports go first, so memory the exporter has freed is not kept alive here
+    if held is not None:
+        held.get("tensors", {}).clear()
     if d.get("pid") is None or reaped(d["pid"]):
         return held     # never map the handles of a process that is gone (its memory may be freed)
     from easydl_amd.ps.ipc import import_tensor
@@ -94,7 +101,8 @@ def import_published(kv, slot: str, held: dict | None = None) -> dict | None:
                 ts[name] = import_tensor(desc)
             except RuntimeError as e:
                 log.warning("vram: cannot import %s from %s: %s", name, d.get("owner"), e)
-    return {"owner": d.get("owner"), "pid": d.get("pid"), "gpu": int(d.get("gpu", 0)), "tensors": ts}
+    return {"owner": d.get("owner"), "pid": d.get("pid"), "gpu": int(d.get("gpu", 0)), "gen": d.get("gen"),
+            "tensors": ts}
 
 
 def dead(pid) -> bool:
