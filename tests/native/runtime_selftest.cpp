@@ -33,6 +33,8 @@ int edl_shm_begin(void*);
 int edl_shm_commit(void*, int, int64_t, int64_t, uint64_t, uint64_t, const char*);
 int edl_shm_latest(void*, int64_t*, int64_t*, uint64_t*, uint64_t*, char*, int);
 int edl_shm_close(void*, int);
+int edl_shm_populate_async(void*, int);
+uint64_t edl_shm_populate_progress(void*, uint64_t*);
 }
 
 #define CHECK(c)                                                     \
@@ -146,6 +148,19 @@ static void test_shm_store() {
   }
   stop = true;
   reader.join();
+  // background population racing the writer and the reader's mapping, then a close that
+  // must join the populating threads (one started, one cut short by close)
+  CHECK(edl_shm_populate_async(w, 3) == 0 && edl_shm_populate_async(w, 3) == -1);
+  for (int64_t s = 401; s <= 420; ++s) {
+    int slot = edl_shm_begin(w);
+    auto* p = static_cast<uint64_t*>(edl_shm_data(w, slot));
+    for (uint64_t i = 0; i < bytes / 8; i += 512) p[i] = (uint64_t)s;
+    CHECK(edl_shm_commit(w, slot, s, 1, bytes, (uint64_t)s * 7 + 1, ("step=" + std::to_string(s)).c_str()) == 0);
+  }
+  uint64_t total = 0, done = 0;
+  for (int i = 0; i < 5000 && (done = edl_shm_populate_progress(w, &total)) < total; ++i) usleep(1000);
+  CHECK(total >= 2 * bytes && done >= total);   // slots are rounded up to 2 MiB
+  CHECK(edl_shm_populate_async(r, 2) == 0);   // closed below while (maybe) still running
   CHECK(edl_shm_latest(r, &step, &epoch, &nb, &cs, meta, sizeof(meta)) >= 0 && step == 400);
   CHECK(edl_shm_commit(w, 5, 1, 1, 8, 0, "") != 0);       // bad slot
   CHECK(edl_shm_commit(w, 0, 1, 1, bytes << 20, 0, "") != 0);  // larger than a slot
