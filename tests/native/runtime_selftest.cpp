@@ -161,7 +161,7 @@ static void test_shm_store() {
   for (int i = 0; i < 5000 && (done = edl_shm_populate_progress(w, &total)) < total; ++i) usleep(1000);
   CHECK(total >= 2 * bytes && done >= total);   // slots are rounded up to 2 MiB
   CHECK(edl_shm_populate_async(r, 2) == 0);   // closed below while (maybe) still running
-  CHECK(edl_shm_latest(r, &step, &epoch, &nb, &cs, meta, sizeof(meta)) >= 0 && step == 400);
+  CHECK(edl_shm_latest(r, &step, &epoch, &nb, &cs, meta, sizeof(meta)) >= 0 && step == 420);
   CHECK(edl_shm_commit(w, 5, 1, 1, 8, 0, "") != 0);       // bad slot
   CHECK(edl_shm_commit(w, 0, 1, 1, bytes << 20, 0, "") != 0);  // larger than a slot
   edl_shm_close(r, 0);
