@@ -90,6 +90,15 @@ int64_t now_ns() {
 
 uint64_t round_up(uint64_t v, uint64_t a) { return (v + a - 1) / a * a; }
 
+// One read per 64 KiB: a read fault on a shared tmpfs mapping maps 16 pages at once
+// (fault-around), writable.  The values are discarded, so a snapshot writing the same
+// pages concurrently is harmless; ThreadSanitizer is told not to flag that.
+__attribute__((no_sanitize("thread"))) void touch_pages(const uint8_t* p, uint64_t len) {
+  volatile uint8_t sink = 0;
+  for (uint64_t o = 0; o < len; o += 65536) sink = sink + p[o];
+  (void)sink;
+}
+
 double now_s() {
   timespec ts;
   clock_gettime(CLOCK_MONOTONIC, &ts);
@@ -385,11 +394,7 @@ int edl_shm_populate_async(void* h, int threads) {
         if (fallocate(s->fd, 0, (off_t)(d0 - s->base + lo), (off_t)len) != 0 &&
             madvise(d0 + lo, len, MADV_POPULATE_WRITE) != 0)
           madvise(d0 + lo, len, MADV_POPULATE_READ);
-        if (s->pop_map) {
-          volatile uint8_t sink = 0;
-          for (uint64_t o = 0; o < len; o += 65536) sink = sink + d0[lo + o];
-          (void)sink;
-        }
+        if (s->pop_map) touch_pages(d0 + lo, len);
         s->pop_done.fetch_add(len);
       }
     });
