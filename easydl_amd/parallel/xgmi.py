@@ -447,6 +447,22 @@ class XgmiComm:
         return (t.is_cuda and t.dtype in (torch.float32, torch.bfloat16) and t.is_contiguous()
                 and (t.numel() * t.element_size()) % 16 == 0 and t.data_ptr() % 16 == 0)
 
+    def close_after_abort(self) -> None:
+        """Release an aborted engine: its spinning workgroups leave on the abort word (bounded
+        by the deadline in any case), so only this engine's stream is drained; then every IPC
+        mapping is closed -- including those of a dead peer's buffers, which would otherwise
+        keep that peer's HBM allocated on its GPU -- and the workspace freed.  May run on a
+        background thread (hipStreamSynchronize and the unmaps are thread-safe)."""
+        if self._ws is None:
+            return
+        self.abort()
+        self.stream.synchronize()
+        for base, _ in self._opened.values():
+            self._rt("edl_xgmi_buf_close", self.device.index or 0, base)
+        self._registered, self._opened = [], {}
+        self._rt("edl_xgmi_ws_destroy", self._ws)
+        self._ws = None
+
     def close(self) -> None:
         """Unmap registered buffers and free the workspace.  Called after a committed
         step, when every rank has synced its streams, so no engine kernel is in flight

@@ -826,6 +826,19 @@ def _retire(comm) -> None:
     groups get a short timeout first, so the abandoned collective fails within seconds."""
     if not getattr(comm, "aborted", False):
         return
+    x = getattr(comm, "xgmi", None)
+    if x is not None and hasattr(x, "close_after_abort"):
+        # The aborted epoch's engine still maps its peers' registered buffers (a dead peer's
+        # included: the mapping keeps that HBM allocated) and owns a workspace; release them
+        # off the recovery path once its stream has drained (the abort word ends every spin).
+        comm.xgmi = None
+
+        def _release(eng=x):
+            try:
+                eng.close_after_abort()
+            except Exception as e:  # noqa: BLE001
+                log.warning("releasing an aborted xGMI engine failed: %s", e)
+        threading.Thread(target=_release, name="edl-xgmi-release", daemon=True).start()
     import datetime
     for pg in (getattr(comm, "data", None), getattr(comm, "ctrl", None)):
         if isinstance(pg, dist.ProcessGroupGloo):

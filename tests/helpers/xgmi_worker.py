@@ -125,6 +125,10 @@ elif mode == "abort":
         res["elapsed"] = time.time() - t0
         res["status"] = x.status()
         res["detail"] = x.status_detail()
+        t1 = time.time()
+        x.close_after_abort()                # what the trainer does with an aborted epoch's engine
+        res["release_s"] = time.time() - t1
+        res["released"] = x._ws is None
     store.set(f"done{rank}", "1")
     store.wait([f"done{r}" for r in range(world)])
 elif mode == "lifetime":

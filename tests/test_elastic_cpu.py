@@ -396,3 +396,29 @@ def test_tp2_dp3_replacement_receives_shard_from_every_holder(tmp_path):
         assert sends and max(e.get("sources", 1) for e in sends) == 2, sends
     finally:
         m.terminate()
+
+
+def test_retire_releases_an_aborted_engine_off_thread():
+    """An aborted epoch's xGMI engine is released (close_after_abort) on a background thread;
+    a healthy epoch's engine is left to the normal shutdown."""
+    import threading as _th
+
+    from easydl_amd.trainer.elastic import _retire
+
+    class Eng:
+        def __init__(self):
+            self.closed = _th.Event()
+
+        def close_after_abort(self):
+            self.closed.set()
+
+    class C:
+        def __init__(self, aborted):
+            self.aborted, self.xgmi, self.data, self.ctrl = aborted, Eng(), None, None
+
+    live, dead = C(False), C(True)
+    e_live, e_dead = live.xgmi, dead.xgmi
+    _retire(live)
+    _retire(dead)
+    assert e_dead.closed.wait(5) and dead.xgmi is None
+    assert live.xgmi is e_live and not e_live.closed.is_set()

@@ -93,6 +93,7 @@ def test_xgmi_abort_releases_spinning_kernel(cuda, tmp_path):
     d = r0["detail"]                   # ... and says where: entry barrier, waiting for rank 1
     assert d["reason"] == "abort" and d["phase"] == 0 and d["peer"] == 1 and d["peer_flag"] == 0, d
     assert 500 <= d["waited_ms"] < 4500, d
+    assert r0["released"] and r0["release_s"] < 2.0   # the aborted engine is freed right away
 
 
 def test_communicator_xgmi_bucket_allreduce(cuda, tmp_path):
