@@ -14,3 +14,6 @@ EDL_TTR_KEEP=1 EDL_TTR_DIR=gpurun_out/final_drill timeout -k 10 300 python -u be
     > gpurun_out/r04_final_drill.log 2>&1
 EDL_TTR_KEEP=1 EDL_TTR_DIR=gpurun_out/final_ttr timeout -k 10 500 python -u bench.py --fault-inject --gpus 1 \
     --mbs 1 --accum 1 --steps 10 --warmup 7 --fault-step 10 > gpurun_out/r04_final_ttr.log 2>&1
+# a fresh process's first Llama-3-8B step, cold vs after a 1-layer warm-up of the same width
+timeout -k 10 300 python -u scripts/first_step_probe.py cold > gpurun_out/r04_first_step_cold.log 2>&1
+timeout -k 10 300 python -u scripts/first_step_probe.py warm > gpurun_out/r04_first_step_warm.log 2>&1
