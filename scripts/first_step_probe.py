@@ -7,14 +7,17 @@ can be warmed up beforehand?  Runs one process per mode (call once per mode):
 
 Prints one JSON line per mode.  (A no-survivor replacement pays the cold first step: 1.2 s vs 0.4 s.)"""
 import json
+import os
 import sys
 import time
 
 import torch
 
-from easydl_amd.models.llama import Llama, get_config
-from easydl_amd.trainer.data import SyntheticTokens
-from easydl_amd.trainer.elastic import ElasticTrainer
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from easydl_amd.models.llama import Llama, get_config  # noqa: E402
+from easydl_amd.trainer.data import SyntheticTokens  # noqa: E402
+from easydl_amd.trainer.elastic import ElasticTrainer  # noqa: E402
 
 
 def trainer(cfg):
