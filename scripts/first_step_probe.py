@@ -21,7 +21,8 @@ from easydl_amd.trainer.elastic import ElasticTrainer  # noqa: E402
 
 
 def trainer(cfg):
-    return ElasticTrainer(lambda d: Llama(cfg, device=d), global_batch=1, micro_batch=1, device="cuda")
+    return ElasticTrainer(lambda d: Llama(cfg, device=d), global_batch=1, micro_batch=1,
+                          device=torch.device("cuda", 0))
 
 
 def step_times(tr, data, n):
