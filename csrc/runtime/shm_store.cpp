@@ -929,6 +929,57 @@ int edl_ckpt_restore_pipelined2(void* seg, int slot, int nbuf, const uint64_t* d
   return (int)err;
 }
 
+// ---------------------------------------------------------------------------
+// Step marks: one 4 KiB shm page per worker slot that survives the worker.  The worker's GPU
+// writes, in stream order, the step whose optimizer update is about to start (begin) and the
+// step whose update has finished (done) -- kernel-side system-scope stores (edl_ps_signal)
+// into the page, page-locked and mapped for the device.  A replacement that adopted the dead
+// worker's HBM (utils/vram.py) reads them: begin == done == K means the HBM holds exactly the
+// state after step K (no update was in flight), so no snapshot needs restoring.
+// ---------------------------------------------------------------------------
+struct MarkPage {
+  std::string name;
+  int fd = -1;
+  uint8_t* base = nullptr;
+  bool pinned = false;
+};
+
+// Returns a handle; *host = the page, *dev = its device address (null unless pinned).
+void* edl_mark_open(const char* name, int create, int pin, void** host, void** dev) {
+  auto* m = new MarkPage();
+  m->name = name;
+  m->fd = shm_open(name, O_RDWR | (create ? O_CREAT : 0), 0600);
+  if (m->fd < 0 || (create && ftruncate(m->fd, 4096) != 0)) {
+    if (m->fd >= 0) close(m->fd);
+    delete m;
+    return nullptr;
+  }
+  m->base = (uint8_t*)mmap(nullptr, 4096, PROT_READ | PROT_WRITE, MAP_SHARED, m->fd, 0);
+  if (m->base == MAP_FAILED) {
+    close(m->fd);
+    delete m;
+    return nullptr;
+  }
+  if (host) *host = m->base;
+  if (dev) *dev = nullptr;
+  if (pin && hipHostRegister(m->base, 4096, hipHostRegisterMapped) == hipSuccess) {
+    m->pinned = true;
+    void* d = nullptr;
+    if (dev && hipHostGetDevicePointer(&d, m->base, 0) == hipSuccess) *dev = d;
+  }
+  return m;
+}
+
+void edl_mark_close(void* h, int unlink_page) {
+  auto* m = static_cast<MarkPage*>(h);
+  if (!m) return;
+  if (m->pinned) hipHostUnregister(m->base);
+  munmap(m->base, 4096);
+  close(m->fd);
+  if (unlink_page) shm_unlink(m->name.c_str());
+  delete m;
+}
+
 // Staged-snapshot parameters (before the first staged job): stage size, ring depth, copy threads.
 int edl_ckpt_engine_staging(void* eng, uint64_t stage_bytes, int nstage, int threads) {
   auto* e = static_cast<Engine*>(eng);

@@ -51,6 +51,8 @@ SIGS = {
     "edl_ckpt_engine_staging": (i32, [vp, u64, i32, i32]),
     "edl_ckpt_engine_staged_stats": (None, [vp, ctypes.POINTER(ctypes.c_double)]),
     "edl_shm_pinned": (i32, [vp]),
+    "edl_mark_open": (vp, [cp, i32, i32, ctypes.POINTER(vp), ctypes.POINTER(vp)]),
+    "edl_mark_close": (None, [vp, i32]),
     "edl_shm_populate_async": (i32, [vp, i32]),
     "edl_shm_populate_progress": (u64, [vp, u64p]),
     "edl_ckpt_restore_pipelined": (i32, [vp, i32, i32, u64p, u64p, u64p, vp, u64, i32]),

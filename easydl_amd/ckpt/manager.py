@@ -307,6 +307,26 @@ class CheckpointManager:
         if hasattr(trainer.opt, "moment_origin"):
             trainer.opt.moment_origin = origin
 
+    def resume_from_hbm(self, trainer, step: int, verify: dict | None = None) -> str:
+        """The weights / master / moments in HBM are exactly the state after ``step`` (adopted
+        from a dead worker whose step marks say no update was in flight, utils/stepmarks.py).
+        Only the host-side counters and host state are set: from the newest snapshot at or
+        before ``step`` (seed, LR schedule, moment origin), advanced to ``step``."""
+        found = self.find_latest(self._tag(trainer), max_step=step)
+        trainer.step = int(step)
+        self._skip_populating = True    # recovering: a snapshot skips rather than waits for pages
+        if verify is not None:
+            self._verify = verify       # re-read the marks after the dead worker's reap (fence)
+        if found is None:
+            trainer.opt.step_count = int(step)
+            return f"hbm:step{step}"
+        meta = found[2][0]["meta"]
+        trainer.opt.step_count = int(meta["opt_step"]) + (int(step) - int(meta["step"]))
+        if hasattr(trainer.opt, "moment_origin"):
+            trainer.opt.moment_origin = int(meta.get("moment_origin", 0))
+        _load_host_state(trainer, meta.get("host"))
+        return f"hbm:step{step}"
+
     @staticmethod
     def finish_restore(trainer) -> None:
         opt = trainer.opt.state_tensors()
@@ -351,7 +371,6 @@ class CheckpointManager:
         self._drop_old_name()
         self._seg = ShmSegment(name, max(need_bytes, alloc_bytes), create=True, pin=self.pin and pin)
         self._seg_key = key
-        self._skip_populating = False
         if not self._seg.pinned and self.populate_threads > 0:
             self._seg.populate_async(self.populate_threads)
         return self._seg
@@ -593,6 +612,14 @@ class CheckpointManager:
         t0 = time.perf_counter()
         while not vram.reaped(v["pid"]) and time.perf_counter() - t0 < 120:
             time.sleep(0.005)
+        if "marks" in v:   # an HBM resume: the dead worker's step marks must not have moved since
+            from easydl_amd.utils.stepmarks import read_slot
+            now = read_slot(v["job"], v["slot"])
+            if now is None or now[:2] != v["marks"]:
+                raise RuntimeError(f"step marks of {v['slot']} moved during the previous worker's teardown: "
+                                   f"{v['marks']} -> {now}")
+            self.stats["handover_verified_s"] = round(time.perf_counter() - t0, 3)
+            return
         for items, expect in v["shards"]:
             acc = torch.zeros(1, dtype=torch.int64, device=items[0][0].device)
             for dst, off in items:
@@ -945,7 +972,7 @@ def _load_shard(read, table, state, dev, expect: int, what: str, seg=None, slot=
 
 def unlink_job_segments(job: str) -> int:
     n = 0
-    pat = re.compile(rf"^edl-{re.escape(job)}(-t\d+of\d+)?-w\d+-s\d+$")
+    pat = re.compile(rf"^edl-{re.escape(job)}((-t\d+of\d+)?-w\d+-s\d+|-marks-[a-z]+\d+)$")
     for path in glob.glob(f"/dev/shm/edl-{job}-*"):
         if not pat.match(os.path.basename(path)):
             continue

@@ -37,8 +37,8 @@ class LRSchedule:
 
 def _zeros(name: str, g) -> torch.Tensor:
     """fp32 optimizer state of flat group ``g``: a buffer handed over by the previous worker on
-    this GPU (utils/vram.py), zeroed, or a new one."""
-    t = vram.take(name, g.numel, torch.float32, g.data.device)
+    this GPU (utils/vram.py, its values kept for an HBM resume), or a new zeroed one."""
+    t = vram.take(name, g.numel, torch.float32, g.data.device, keep=True)
     return torch.zeros(g.numel, dtype=torch.float32, device=g.data.device) if t is None else t
 
 
@@ -65,8 +65,8 @@ class FlatAdamW:
                 g.weight_decay = weight_decay
             has16 = g.data.dtype != torch.float32
             if has16:
-                master = vram.take(f"opt/{g.name}/master", g.numel, torch.float32, g.data.device)
-                master = g.data.float() if master is None else master.copy_(g.data)
+                master = vram.take(f"opt/{g.name}/master", g.numel, torch.float32, g.data.device, keep=True)
+                master = g.data.float() if master is None else master
             else:
                 master = g.data
             self.state.append({"master": master, "m": _zeros(f"opt/{g.name}/m", g), "v": _zeros(f"opt/{g.name}/v", g)})

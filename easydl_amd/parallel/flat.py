@@ -130,8 +130,9 @@ class FlatParams:
                 chunks.append((cls, dt, gdt, base if i == 0 else f"{base}.{i}", part))
         for cls, dt, gdt, gname, plist in chunks:
             total = sum(_roundup(p.numel()) for _, p in plist)
-            data = vram.take(f"flat/{gname}/data", total, dt, self.device)
+            data = vram.take(f"flat/{gname}/data", total, dt, self.device, keep=True)
             grad = vram.take(f"flat/{gname}/grad", total, gdt, self.device)
+            adopted = data is not None   # the previous worker's weights: not overwritten by this init
             data = torch.zeros(total, dtype=dt, device=self.device) if data is None else data
             grad = torch.zeros(total, dtype=gdt, device=self.device) if grad is None else grad
             grp = FlatGroup(gname, weight_decay if cls == "decay" else 0.0, data, grad)
@@ -139,8 +140,9 @@ class FlatParams:
             for n, p in plist:
                 k = p.numel()
                 view = data[off:off + k].view(p.shape)
-                with torch.no_grad():
-                    view.copy_(p.data)
+                if not adopted:
+                    with torch.no_grad():
+                        view.copy_(p.data)
                 p.data = view
                 if gdt != dt and hasattr(p, "grad_dtype"):
                     # fp32 gradient buffers under bf16 parameters (grad_dtype=fp32): torch >= 2.10

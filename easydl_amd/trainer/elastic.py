@@ -121,6 +121,7 @@ class ElasticTrainer:
         self.log_every = log_every
         self._phases = os.environ.get("EDL_STEP_PHASES", "0") == "1"
         self._step_sync = self._phases or os.environ.get("EDL_STEP_SYNC", "0") == "1"
+        self._marks = None          # step-mark page (utils/stepmarks.py), opened in fit()
         self._sync_next = True
         self.rdzv_config = rdzv_config
         self._store = store
@@ -493,6 +494,27 @@ class ElasticTrainer:
         self.held_tp = t
         self.needs_state = False
 
+    def _open_marks(self) -> None:
+        """Step-mark page of this worker slot (utils/stepmarks.py), with VRAM hand-over on."""
+        from easydl_amd.utils import vram
+        if self._marks is not None or not vram.enabled() or getattr(self, "kv", None) is None:
+            return
+        from easydl_amd.utils.stepmarks import StepMarks
+        try:
+            self._marks = StepMarks(self.ctx.job, f"{self.ctx.role}{self.ctx.index}", device=self.device)
+        except OSError as e:
+            log.warning("step marks unavailable: %s", e)
+            return
+        self._settle_marks()
+
+    def _settle_marks(self) -> None:
+        """The state is settled at self.step (epoch entry: restore / transfer done)."""
+        if self._marks is None:
+            return
+        if self.device.type == "cuda":
+            torch.cuda.current_stream(self.device).synchronize()
+        self._marks.set_now(self.step)
+
     def _publish_vram(self) -> None:
         """Export the persistent state buffers for the hot standby on this GPU (utils/vram.py):
         if this process dies, the standby builds on them instead of waiting for the driver to
@@ -515,10 +537,36 @@ class ElasticTrainer:
         self.events.emit("vram_published", tensors=n, of=len(ts),
                          adopted=dict(vram.STATS, adopted_gb=round(vram.STATS["adopted_bytes"] / 2**30, 1)))
 
+    def _hbm_resume_step(self) -> int | None:
+        """Step K if this process adopted a dead worker's HBM (utils/vram.py) whose step marks
+        (utils/stepmarks.py) say the update of step K had finished and none was in flight."""
+        from easydl_amd.utils import stepmarks, vram
+        pid = vram.ADOPTED_FROM.get("pid")
+        if (pid is None or self.tp > 1 or self.comm is None or self.comm.world_size != 1
+                or os.environ.get("EDL_HBM_RESUME", "1") == "0"):
+            return None
+        marks = stepmarks.read_slot(self.ctx.job, f"{self.ctx.role}{self.ctx.index}")
+        if marks is None:
+            return None
+        begin, done, writer = marks
+        if writer != pid or begin != done:
+            self.events.emit("hbm_resume_refused", begin=begin, done=done, writer=writer, adopted_from=pid)
+            return None
+        return done
+
     def _maybe_restore(self):
         if self.checkpoint is None:
             return
         t0 = time.perf_counter()
+        k = self._hbm_resume_step()
+        if k is not None:
+            from easydl_amd.utils import vram
+            pid = vram.ADOPTED_FROM.get("pid")
+            verify = None if vram.reaped(pid) else {"pid": pid, "marks": (k, k), "job": self.ctx.job,
+                                                    "slot": f"{self.ctx.role}{self.ctx.index}"}
+            src = self.checkpoint.resume_from_hbm(self, k, verify)
+            self.events.emit("restored", step=self.step, source=src, s=round(time.perf_counter() - t0, 3))
+            return
         st = self.checkpoint.restore_latest(self)
         if st is not None:
             from easydl_amd.ckpt import manager as _ckm
@@ -656,6 +704,7 @@ class ElasticTrainer:
                 self.events.emit("finished_waiting", node=self.ctx.node_id)
                 return self
             self._publish_vram()
+            self._open_marks()
             while self.step < num_steps:
                 t0 = self._t_step = time.perf_counter()
                 ok = True
@@ -685,9 +734,15 @@ class ElasticTrainer:
                     if self.checkpoint is not None:
                         self.checkpoint.fence()  # never update params under an in-flight snapshot
                     t_fence = time.perf_counter()
+                    if self._marks is not None:
+                        self._marks.begin(self.step + 1, torch.cuda.current_stream(self.device)
+                                          if self.device.type == "cuda" else None)
                     with trace.range("optimizer"):
                         self.opt.step(pre_scale=1.0)
                     self._sync_buffers()
+                    if self._marks is not None:
+                        self._marks.done(self.step + 1, torch.cuda.current_stream(self.device)
+                                         if self.device.type == "cuda" else None)
                     if self._phases and ok:
                         # host-side split of one step (EDL_STEP_PHASES=1): enqueue of the micro-batches,
                         # wait for the GPU (compute + all-reduce), commit round, snapshot fence, optimizer
@@ -791,6 +846,7 @@ class ElasticTrainer:
         if self.rdzv is not None and self.rdzv.kv.exists(f"rdzv/leave/{self.ctx.node_id}"):
             raise SystemExit(0)
         self._enter_epoch()
+        self._settle_marks()
 
     def close(self):
         self._stop.set()

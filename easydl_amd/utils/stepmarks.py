@@ -1,0 +1,91 @@
+"""Step marks: which optimizer update the HBM state of a worker slot has finished.
+
+One 4 KiB shm page per worker slot (``/edl-<job>-marks-<role><index>``), written by the
+worker's GPU in stream order (``edl_ps_signal`` kernel, system-scope store into the page,
+page-locked and device-mapped), read by the process that replaces it:
+
+* ``begin`` = the step whose update is about to start (written before the optimizer kernels),
+* ``done``  = the step whose update has finished (written after them),
+* ``pid``   = the writer.
+
+When a worker is SIGKILLed, its GPU queues stop (utils/procfs.py).  If ``begin == done == K``
+no update was in flight, so the weights, fp32 master and moments in its HBM are exactly the
+state after step K.  A replacement that adopted that HBM (utils/vram.py) then resumes from
+step K without restoring a snapshot: no host -> HBM copy, no lost steps, and the same
+per-step seeds as an uninterrupted run.  With ``begin != done`` it restores from /dev/shm.
+
+Reference: the reference's recovery contract ("resume the training" after a failure,
+/root/reference/README.md:25-29); the mechanism is ours.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch
+
+from easydl_amd import _native
+
+BEGIN, DONE, PID = 0, 4, 8     # byte offsets in the page
+
+
+def page_name(job: str, slot: str) -> str:
+    return f"/edl-{job}-marks-{slot}"
+
+
+class StepMarks:
+    def __init__(self, job: str, slot: str, create: bool = True, device: torch.device | None = None):
+        self.name = page_name(job, slot)
+        self.rt = _native.runtime()
+        host, dev = ctypes.c_void_p(), ctypes.c_void_p()
+        pin = device is not None and device.type == "cuda"
+        self.h = self.rt("edl_mark_open", self.name.encode(), 1 if create else 0, 1 if pin else 0,
+                         ctypes.byref(host), ctypes.byref(dev))
+        if not self.h:
+            raise OSError(f"cannot open step-mark page {self.name}")
+        self.host = host.value
+        self.dev = dev.value            # None: written from the host (CPU training / not pinned)
+        self.device = device
+
+    def _u32(self, off: int):
+        return ctypes.c_uint32.from_address(self.host + off)
+
+    def set_now(self, step: int) -> None:
+        """Host write of begin = done = ``step`` (no update in flight; the stream is idle)."""
+        self._u32(BEGIN).value = step & 0xFFFFFFFF
+        self._u32(DONE).value = step & 0xFFFFFFFF
+        ctypes.c_int64.from_address(self.host + PID).value = os.getpid()
+
+    def _mark(self, off: int, step: int, stream) -> None:
+        if self.dev is not None:
+            _native.kernels().check("edl_ps_signal", self.dev + off, step & 0xFFFFFFFF,
+                                    stream.cuda_stream if stream is not None else None)
+        else:
+            self._u32(off).value = step & 0xFFFFFFFF
+
+    def begin(self, step: int, stream=None) -> None:
+        self._mark(BEGIN, step, stream)
+
+    def done(self, step: int, stream=None) -> None:
+        self._mark(DONE, step, stream)
+
+    def read(self) -> tuple[int, int, int]:
+        return (self._u32(BEGIN).value, self._u32(DONE).value,
+                ctypes.c_int64.from_address(self.host + PID).value)
+
+    def close(self, unlink: bool = False) -> None:
+        if self.h:
+            self.rt("edl_mark_close", self.h, 1 if unlink else 0)
+            self.h = None
+
+
+def read_slot(job: str, slot: str) -> tuple[int, int, int] | None:
+    """(begin, done, pid) of a slot's page, or None if there is none."""
+    try:
+        m = StepMarks(job, slot, create=False)
+    except OSError:
+        return None
+    try:
+        return m.read()
+    finally:
+        m.close()

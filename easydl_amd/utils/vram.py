@@ -145,8 +145,11 @@ def adopt(tensors: dict[str, torch.Tensor], pid=None) -> None:
         ADOPTED_FROM["pid"] = int(pid)
 
 
-def take(name: str, numel: int, dtype: torch.dtype, device) -> torch.Tensor | None:
-    """The adopted tensor for ``name`` if it matches (numel, dtype, device), zero-filled; else None."""
+def take(name: str, numel: int, dtype: torch.dtype, device, keep: bool = False) -> torch.Tensor | None:
+    """The adopted tensor for ``name`` if it matches (numel, dtype, device), else None.  Zero-filled,
+    unless ``keep``: training state (weights, master, moments) keeps the dead worker's values, so a
+    replacement can resume from them when its step marks say they are consistent
+    (utils/stepmarks.py); otherwise a restore or state transfer overwrites them anyway."""
     t = _ADOPTED.pop(name, None)
     if t is None:
         return None
@@ -155,7 +158,8 @@ def take(name: str, numel: int, dtype: torch.dtype, device) -> torch.Tensor | No
         log.warning("vram: adopted %s does not match (%s %s %s vs %s %s %s): allocating", name, t.numel(), t.dtype,
                     t.device, numel, dtype, dev)
         return None
-    t.zero_()
+    if not keep:
+        t.zero_()
     STATS["adopted"] += 1
     STATS["adopted_bytes"] += t.numel() * t.element_size()
     return t

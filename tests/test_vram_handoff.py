@@ -60,10 +60,13 @@ def test_flat_and_adamw_build_on_adopted_buffers():
         for k, t in got.items():
             assert t.data_ptr() == old[k].data_ptr(), k            # the adopted storage, not a copy
         for g, st in zip(f1.groups, o1.state):
-            assert torch.count_nonzero(g.grad) == 0                   # zeroed, not the dead worker's 7s
-            assert torch.count_nonzero(st["m"]) == 0 and torch.count_nonzero(st["v"]) == 0
-        for p_new, p_ref in zip(m.parameters(), _model(2).parameters()):
-            assert torch.equal(p_new.data, p_ref.data)                # this process's params were copied in
+            assert torch.count_nonzero(g.grad) == 0                   # gradients start from zero
+            # the training state keeps the previous worker's values (an HBM resume needs them;
+            # a restore / state transfer overwrites them otherwise)
+            for t in (g.data, st["master"], st["m"], st["v"]):
+                assert bool((t == 7.0).all())
+        for p_new in m.parameters():                                   # the model now views that state
+            assert bool((p_new.data == 7.0).all())
         assert vram.STATS["adopted"] >= len(old)
     finally:
         vram.release_unused()
@@ -157,3 +160,63 @@ def test_exit_status_of_a_normal_exit_is_zero():
             break
         time.sleep(0.01)
     p.wait()
+
+
+def test_step_marks_host_path(tmp_path):
+    from easydl_amd.utils import stepmarks
+    job = f"sm{os.getpid()}"
+    m = stepmarks.StepMarks(job, "worker0")
+    try:
+        m.set_now(5)
+        assert m.read() == (5, 5, os.getpid())
+        m.begin(6)
+        assert stepmarks.read_slot(job, "worker0")[:2] == (6, 5)      # an update in flight
+        m.done(6)
+        assert stepmarks.read_slot(job, "worker0")[:2] == (6, 6)
+        assert stepmarks.read_slot(job, "worker9") is None
+    finally:
+        m.close(unlink=True)
+
+
+def test_hbm_resume_continues_bit_exactly_without_a_restore(tmp_path):
+    """A replacement that adopted a dead worker's state whose step marks say begin == done == 7
+    resumes at step 7 from that state (no snapshot restored: the newest snapshot is step 6) and
+    matches an uninterrupted run."""
+    from easydl_amd.ckpt.manager import CheckpointManager, unlink_job_segments
+    from easydl_amd.models.llama import Llama, get_config
+    from easydl_amd.trainer.context import TrainerContext
+    from easydl_amd.trainer.data import SyntheticTokens
+    from easydl_amd.trainer.elastic import ElasticTrainer
+    from easydl_amd.utils import stepmarks
+    job = f"hbm{os.getpid()}"
+    cfg = get_config("llama-tiny", n_layers=1, dim=64, n_heads=4, n_kv_heads=2, ffn_dim=128, vocab_size=128)
+    data = SyntheticTokens(cfg.vocab_size, 16, num_samples=1024)
+
+    def mk(ckpt, seed):
+        ctx = TrainerContext(job=job, run_dir=str(tmp_path))
+        return ElasticTrainer(lambda d: Llama(cfg, device=d, dtype=torch.float32), global_batch=4, micro_batch=2,
+                              lr=1e-3, device="cpu", ctx=ctx, checkpoint=ckpt, seed=seed)
+
+    unlink_job_segments(job)
+    try:
+        ref = mk(None, 1234)
+        ref.fit(lambda m, b: m(*b), data, num_steps=10)
+        a = mk(CheckpointManager(job, interval=3), 1234)
+        a.fit(lambda m, b: m(*b), data, num_steps=7)       # snapshots of 3 and 6; HBM at 7
+        a.checkpoint.wait()
+        marks = stepmarks.StepMarks(job, f"{a.ctx.role}{a.ctx.index}")
+        marks.set_now(7)
+        vram.adopt({k: t.clone() for k, t in _state(a.flat, a.opt).items()}, pid=os.getpid())
+        b = mk(CheckpointManager(job, interval=100), 999)
+        b.fit(lambda m, b_: m(*b_), data, num_steps=10)
+        assert b.history[0]["step"] == 8                    # resumed after 7, nothing lost
+        assert b.opt.step_count == 10
+        ev = [line for line in open(tmp_path / f"events-{b.ctx.role}{b.ctx.index}.jsonl") if '"restored"' in line]
+        assert ev and "hbm:step7" in ev[-1]
+        assert torch.equal(torch.cat([g.data for g in b.flat.groups]), torch.cat([g.data for g in ref.flat.groups]))
+        assert all(torch.equal(x, y) for x, y in zip(b.opt.state_tensors().values(), ref.opt.state_tensors().values()))
+        marks.close()
+    finally:
+        vram.release_unused()
+        vram.ADOPTED_FROM.clear()
+        unlink_job_segments(job)
