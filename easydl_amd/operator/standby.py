@@ -60,6 +60,38 @@ def prewarm() -> dict:
     return out
 
 
+def warm_device(gpu: int) -> float:
+    """One forward + backward + optimizer step of a small Llama of head dim 128 on ``gpu``.
+
+    A fresh process's first training step pays ~0.8 s of first-use costs on the host:
+    code-object loads of this framework's kernels and of the PyTorch kernels the model uses,
+    hipBLASLt initialisation, allocator growth (scripts/first_step_probe.py: first step
+    1.21 s cold, 0.41 s after a warm-up).  A parked standby that already holds a context on
+    the GPU (it mapped the workers' HBM there, utils/vram.py) pays most of that up front, so
+    the replacement's first step -- the last phase of its time-to-recover -- does not.  The
+    model is tiny (a few MB): the running worker does not notice it.  Returns seconds."""
+    import torch
+
+    from easydl_amd.models.llama import Llama, LlamaConfig
+    from easydl_amd.optim import FlatAdamW
+    from easydl_amd.parallel.flat import FlatParams
+    t0 = time.perf_counter()
+    dev = torch.device("cuda", gpu)
+    cfg = LlamaConfig(vocab_size=1024, dim=512, n_layers=1, n_heads=4, n_kv_heads=2, ffn_dim=1024, max_seq_len=256)
+    with torch.cuda.device(dev):
+        model = Llama(cfg, device=dev)
+        flat = FlatParams(model)
+        opt = FlatAdamW(flat)
+        ids = torch.randint(0, cfg.vocab_size, (2, 256), device=dev)
+        loss = model(ids, ids)
+        loss.backward()
+        opt.step()
+        torch.cuda.synchronize(dev)
+        del model, flat, opt, loss, ids
+        torch.cuda.empty_cache()
+    return time.perf_counter() - t0
+
+
 def _import_vram(kv, held: dict) -> None:
     """Map (IPC) the state buffers every worker published; keep them referenced while parked."""
     from easydl_amd.utils import vram
@@ -113,6 +145,7 @@ def main() -> int:
     from easydl_amd.utils import vram
     handoff = vram.enabled() and info.get("gpus", 0) > 0
     held: dict[str, dict] = {}     # worker slot -> imported state buffers (utils/vram.py)
+    warmed: set[int] = set()       # GPUs this standby has run its warm-up step on
     next_scan = next_vram = 0.0
     while True:
         a = kv.get(key)
@@ -123,6 +156,13 @@ def main() -> int:
         if handoff and time.monotonic() > next_vram:
             _import_vram(kv, held)
             next_vram = time.monotonic() + 1.0
+            for g in sorted({h["gpu"] for h in held.values() if h and h.get("tensors")} - warmed):
+                warmed.add(g)
+                if os.environ.get("EDL_STANDBY_WARMUP", "1") != "0":
+                    try:
+                        kv.set(f"standby/warm/{name}/gpu{g}", json.dumps({"s": round(warm_device(g), 3)}))
+                    except Exception as e:  # noqa: BLE001 - an optimisation only
+                        print(f"standby: warm-up on GPU {g} failed: {e}", file=sys.stderr)
         if premap and time.monotonic() > next_scan:
             from easydl_amd.ckpt.manager import premap_job_segments
             mapped = premap_job_segments(job)

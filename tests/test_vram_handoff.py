@@ -220,3 +220,11 @@ def test_hbm_resume_continues_bit_exactly_without_a_restore(tmp_path):
         vram.release_unused()
         vram.ADOPTED_FROM.clear()
         unlink_job_segments(job)
+
+
+@pytest.mark.gpu
+def test_standby_warm_up_step_runs_and_frees(cuda):
+    from easydl_amd.operator.standby import warm_device
+    before = torch.cuda.memory_allocated(cuda)
+    s = warm_device(cuda.index or 0)
+    assert s > 0 and torch.cuda.memory_allocated(cuda) == before
