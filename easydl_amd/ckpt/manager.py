@@ -244,6 +244,7 @@ class CheckpointManager:
         self.populate_threads = int(os.environ.get("EDL_SHM_POPULATE_THREADS", 4))
         self._skip_populating = False
         self._verify = None         # pending post-teardown check of an early hand-over (fence)
+        self._marks_check = None    # background post-reap check of an HBM resume
         self._seg: ShmSegment | None = None
         self._seg_key = None
         self._old_name = None       # previous layout's name of a relinked segment (see _segment)
@@ -316,7 +317,12 @@ class CheckpointManager:
         trainer.step = int(step)
         self._skip_populating = True    # recovering: a snapshot skips rather than waits for pages
         if verify is not None:
-            self._verify = verify       # re-read the marks after the dead worker's reap (fence)
+            # re-read the marks once the dead worker is gone, without holding up training; no
+            # snapshot is taken meanwhile, and a failed check stops this process at the next
+            # optimizer step (its replacement then restores from /dev/shm)
+            self._marks_check = {"result": None}
+            threading.Thread(target=self._check_marks_after_reap, args=(verify, self._marks_check),
+                             name="edl-marks-check", daemon=True).start()
         if found is None:
             trainer.opt.step_count = int(step)
             return f"hbm:step{step}"
@@ -447,6 +453,11 @@ class CheckpointManager:
     # -- snapshot ------------------------------------------------------------
     def on_step(self, trainer) -> None:
         if trainer.step % self.interval:
+            return
+        if self.hbm_unverified():
+            # resumed from a dead worker's HBM that is not verified yet: never let a snapshot
+            # publish that state before the check
+            self.stats["skipped_unverified"] = self.stats.get("skipped_unverified", 0) + 1
             return
         try:
             self.snapshot(trainer)
@@ -612,14 +623,6 @@ class CheckpointManager:
         t0 = time.perf_counter()
         while not vram.reaped(v["pid"]) and time.perf_counter() - t0 < 120:
             time.sleep(0.005)
-        if "marks" in v:   # an HBM resume: the dead worker's step marks must not have moved since
-            from easydl_amd.utils.stepmarks import read_slot
-            now = read_slot(v["job"], v["slot"])
-            if now is None or now[:2] != v["marks"]:
-                raise RuntimeError(f"step marks of {v['slot']} moved during the previous worker's teardown: "
-                                   f"{v['marks']} -> {now}")
-            self.stats["handover_verified_s"] = round(time.perf_counter() - t0, 3)
-            return
         for items, expect in v["shards"]:
             acc = torch.zeros(1, dtype=torch.int64, device=items[0][0].device)
             for dst, off in items:
@@ -635,8 +638,32 @@ class CheckpointManager:
                 raise RuntimeError(f"restored weights of {g.name} changed during the previous worker's teardown")
         self.stats["handover_verified_s"] = round(time.perf_counter() - t0, 3)
 
+    def _check_marks_after_reap(self, v: dict, out: dict) -> None:
+        """HBM resume: once the dead worker is gone, its step marks must still read (K, K) --
+        had its GPU run another update on the adopted buffers after this process resumed from
+        them, 'begin' would have moved."""
+        from easydl_amd.utils import vram
+        from easydl_amd.utils.stepmarks import read_slot
+        t0 = time.perf_counter()
+        while not vram.reaped(v["pid"]) and time.perf_counter() - t0 < 120:
+            time.sleep(0.01)
+        now = read_slot(v["job"], v["slot"])
+        out["s"] = round(time.perf_counter() - t0, 3)
+        out["result"] = "ok" if now is not None and now[:2] == v["marks"] else f"marks moved: {v['marks']} -> {now}"
+
+    def hbm_unverified(self) -> bool:
+        c = self._marks_check
+        return c is not None and c["result"] is None
+
     def fence(self) -> None:
         """Make the current stream wait for the in-flight snapshot (call before the optimizer)."""
+        c = self._marks_check
+        if c is not None and c["result"] is not None:
+            self._marks_check = None
+            if c["result"] != "ok":
+                raise RuntimeError(f"HBM resume invalidated after the previous worker's teardown ({c['result']});"
+                                   f" exiting so the replacement restores from the snapshot")
+            self.stats["handover_verified_s"] = c["s"]
         if self._verify is not None:
             self._verify_handover()
         if self._ticket is not None and self._engine is not None:

@@ -119,18 +119,17 @@ def dead(pid) -> bool:
 
 
 def reaped(pid) -> bool:
+    """True once ``pid`` is gone altogether (its parent has collected it): its teardown -- GPU
+    queues included -- is complete.  A zombie does not count: when a last address-space
+    reference is dropped late, the address space (and the GPU queues it holds) is torn down
+    after the task already reads as a zombie."""
     try:
         os.kill(int(pid), 0)
     except ProcessLookupError:
         return True
     except (PermissionError, TypeError, ValueError):
         return False
-    # a zombie counts: its teardown is complete
-    try:
-        with open(f"/proc/{int(pid)}/stat") as f:
-            return f.read().rsplit(")", 1)[1].split()[0] in ("Z", "X")
-    except OSError:
-        return True
+    return False
 
 
 ADOPTED_FROM: dict = {}          # {"pid": ...} of the process whose buffers were adopted

@@ -140,7 +140,7 @@ def test_mm_released_tracks_a_killed_process():
         while not mm_released(p.pid) and time.time() < t_end:   # a zombie holds no address space
             time.sleep(0.01)
         assert mm_released(p.pid) and vram.dead(p.pid)
-        assert vram.reaped(p.pid)                                # zombie: teardown complete
+        assert not vram.reaped(p.pid)                            # a zombie is not reaped yet
         assert exit_status(p.pid) == _signal.SIGKILL
     finally:
         p.wait()
@@ -229,3 +229,32 @@ def test_standby_warm_up_step_runs_and_frees(cuda):
     s = warm_device(cuda.index or 0)
     # (module-level caches of the ops -- RoPE tables, descriptor tensors -- may keep a few MB)
     assert s > 0 and torch.cuda.memory_allocated(cuda) - before < 64 << 20
+
+
+def test_hbm_resume_check_failure_stops_at_the_next_update(tmp_path):
+    """The post-reap re-read of the step marks runs off the training path; if the marks moved
+    (the dead worker's GPU updated the adopted state after the resume), the next optimizer
+    step raises instead of training on -- and snapshots wait for the check meanwhile."""
+    from types import SimpleNamespace
+
+    from easydl_amd.ckpt.manager import CheckpointManager
+    from easydl_amd.utils import stepmarks
+    job = f"hbmchk{os.getpid()}"
+    gone = subprocess.Popen([sys.executable, "-c", "pass"])
+    gone.wait()
+    m = stepmarks.StepMarks(job, "worker0")
+    try:
+        m.set_now(5)
+        m.begin(6)                                  # the page now reads (6, 5): moved since (5, 5)
+        tr = SimpleNamespace(step=0, ckpt_tag="", opt=SimpleNamespace(step_count=0, moment_origin=0),
+                             load_host_state=lambda h: None)
+        ck = CheckpointManager(job, interval=1)
+        ck.resume_from_hbm(tr, 5, {"pid": gone.pid, "marks": (5, 5), "job": job, "slot": "worker0"})
+        assert tr.step == 5 and tr.opt.step_count == 5
+        t_end = time.time() + 10
+        while ck.hbm_unverified() and time.time() < t_end:
+            time.sleep(0.01)
+        with pytest.raises(RuntimeError, match="HBM resume invalidated"):
+            ck.fence()
+    finally:
+        m.close(unlink=True)
