@@ -60,8 +60,40 @@ def prewarm() -> dict:
     return out
 
 
-def warm_device(gpu: int) -> float:
-    """One forward + backward + optimizer step of a small Llama of head dim 128 on ``gpu``.
+def _llama_warm_bytes(cfg, tokens: int) -> int:
+    """Rough peak of a one-layer forward/backward: bf16 weights + gradients, activations, logits."""
+    kv = cfg.dim // cfg.n_heads * cfg.n_kv_heads
+    layer = cfg.dim * (2 * cfg.dim + 2 * kv) + 3 * cfg.dim * cfg.ffn_dim
+    params = cfg.vocab_size * cfg.dim * (1 if cfg.tie_embeddings else 2) + cfg.n_layers * layer
+    return 4 * params + tokens * (10 * cfg.vocab_size + 64 * cfg.dim + 16 * cfg.ffn_dim)
+
+
+def _warm_llama(dev, spec: dict) -> bool:
+    """Forward + backward of one layer of the worker's model at its micro-batch shape: the
+    GEMM shapes (hipBLASLt solutions), attention and norm kernels of the real step.  Skipped
+    when the GPU has not got twice the memory it needs free."""
+    import torch
+
+    from easydl_amd.models.llama import Llama, LlamaConfig
+    fields = LlamaConfig.__dataclass_fields__
+    cfg = LlamaConfig(**{k: v for k, v in spec.get("cfg", {}).items() if k in fields})
+    cfg.n_layers = 1
+    b, s = (int(x) for x in spec["batch"])
+    free, _ = torch.cuda.mem_get_info(dev)
+    if free < 2 * _llama_warm_bytes(cfg, b * s) + (4 << 30):
+        return False
+    model = Llama(cfg, device=dev)
+    ids = torch.randint(0, cfg.vocab_size, (b, s), device=dev)
+    model(ids, ids).backward()
+    torch.cuda.synchronize(dev)
+    del model, ids
+    return True
+
+
+def warm_device(gpu: int, spec: dict | None = None) -> float:
+    """One forward + backward + optimizer step of a small Llama of head dim 128 on ``gpu``,
+    preceded, when the worker published its shape (``spec``, ElasticTrainer._publish_warm_spec),
+    by a forward + backward of one layer of its model at full width.
 
     A fresh process's first training step pays ~0.8 s of first-use costs on the host:
     code-object loads of this framework's kernels and of the PyTorch kernels the model uses,
@@ -69,7 +101,9 @@ def warm_device(gpu: int) -> float:
     1.21 s cold, 0.41 s after a warm-up).  A parked standby that already holds a context on
     the GPU (it mapped the workers' HBM there, utils/vram.py) pays most of that up front, so
     the replacement's first step -- the last phase of its time-to-recover -- does not.  The
-    model is tiny (a few MB): the running worker does not notice it.  Returns seconds."""
+    small model covers the optimizer and the framework's kernels; the full-width layer covers
+    the shape-dependent part (GEMM solutions, 1.21 s -> 0.41 s in the probe).  Its memory is
+    freed before this returns.  Returns seconds."""
     import torch
 
     from easydl_amd.models.llama import Llama, LlamaConfig
@@ -79,6 +113,8 @@ def warm_device(gpu: int) -> float:
     dev = torch.device("cuda", gpu)
     cfg = LlamaConfig(vocab_size=1024, dim=512, n_layers=1, n_heads=4, n_kv_heads=2, ffn_dim=1024, max_seq_len=256)
     with torch.cuda.device(dev):
+        if spec and spec.get("model") == "llama":
+            _warm_llama(dev, spec)
         model = Llama(cfg, device=dev)
         flat = FlatParams(model)
         opt = FlatAdamW(flat)
@@ -146,6 +182,7 @@ def main() -> int:
     handoff = vram.enabled() and info.get("gpus", 0) > 0
     held: dict[str, dict] = {}     # worker slot -> imported state buffers (utils/vram.py)
     warmed: set[int] = set()       # GPUs this standby has run its warm-up step on
+    warm_on = os.environ.get("EDL_STANDBY_WARMUP", "1") != "0"
     next_scan = next_vram = 0.0
     while True:
         a = kv.get(key)
@@ -156,13 +193,18 @@ def main() -> int:
         if handoff and time.monotonic() > next_vram:
             _import_vram(kv, held)
             next_vram = time.monotonic() + 1.0
-            for g in sorted({h["gpu"] for h in held.values() if h and h.get("tensors")} - warmed):
-                warmed.add(g)
-                if os.environ.get("EDL_STANDBY_WARMUP", "1") != "0":
-                    try:
-                        kv.set(f"standby/warm/{name}/gpu{g}", json.dumps({"s": round(warm_device(g), 3)}))
-                    except Exception as e:  # noqa: BLE001 - an optimisation only
-                        print(f"standby: warm-up on GPU {g} failed: {e}", file=sys.stderr)
+            for slot, h in sorted(held.items()):
+                if not warm_on or not h or not h.get("tensors") or h["gpu"] in warmed:
+                    continue
+                published, spec = vram.read_warm(kv, slot)
+                if not published:
+                    continue            # the worker has not finished its first step yet
+                warmed.add(h["gpu"])
+                try:
+                    s = round(warm_device(h["gpu"], spec), 3)
+                    kv.set(f"standby/warm/{name}/gpu{h['gpu']}", json.dumps({"s": s, "spec": spec is not None}))
+                except Exception as e:  # noqa: BLE001 - an optimisation only
+                    print(f"standby: warm-up on GPU {h['gpu']} failed: {e}", file=sys.stderr)
         if premap and time.monotonic() > next_scan:
             from easydl_amd.ckpt.manager import premap_job_segments
             mapped = premap_job_segments(job)

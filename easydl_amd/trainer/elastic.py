@@ -114,7 +114,8 @@ class ElasticTrainer:
         self.global_batch = global_batch
         self.micro_batch = micro_batch
         self.step = 0                # committed optimizer steps
-        self.needs_state = True      # fresh process: must receive state unless everyone is fresh
+        self._warm_published = False
+        self.needs_state = True     # fresh process: must receive state unless everyone is fresh
         self.comm = None
         self.assignment = None
         self.checkpoint = checkpoint
@@ -537,6 +538,28 @@ class ElasticTrainer:
         self.events.emit("vram_published", tensors=n, of=len(ts),
                          adopted=dict(vram.STATS, adopted_gb=round(vram.STATS["adopted_bytes"] / 2**30, 1)))
 
+    def _publish_warm_spec(self, data) -> None:
+        """Tell the parked standby on this GPU what to warm up with (operator/standby.py
+        warm_device): one layer of this model's width at this job's micro-batch shape, so the
+        GEMM solutions, kernels and library handles of the replacement's first step are loaded
+        before it is needed.  Published after this worker's first step, once its allocator holds
+        its peak, so the standby's warm-up never competes with it for memory."""
+        from easydl_amd.utils import vram
+        if (self._warm_published or not vram.enabled() or self.device.type != "cuda"
+                or getattr(self, "kv", None) is None):
+            return
+        self._warm_published = True
+        from dataclasses import asdict
+
+        from easydl_amd.models.llama import Llama
+        seq = getattr(data, "seq", None)
+        spec = None
+        if isinstance(self.model, Llama) and self.tp == 1 and seq:
+            cfg = {k: v for k, v in asdict(self.model.cfg).items() if isinstance(v, (bool, int, float))}
+            cfg["n_layers"] = 1
+            spec = {"model": "llama", "cfg": cfg, "batch": [self.micro_batch, int(seq)]}
+        vram.publish_warm(self.kv, f"{self.ctx.role}{self.ctx.index}", spec)
+
     def _hbm_resume_step(self) -> int | None:
         """Step K if this process adopted a dead worker's HBM (utils/vram.py) whose step marks
         (utils/stepmarks.py) say the update of step K had finished and none was in flight."""
@@ -733,6 +756,9 @@ class ElasticTrainer:
                 if apply:
                     if self.checkpoint is not None:
                         self.checkpoint.fence()  # never update params under an in-flight snapshot
+                        hv = self.checkpoint.stats.pop("handover_verified_s", None)
+                        if hv is not None:
+                            self.events.emit("handover_verified", step=self.step, s=hv)
                     t_fence = time.perf_counter()
                     if self._marks is not None:
                         self._marks.begin(self.step + 1, torch.cuda.current_stream(self.device)
@@ -765,6 +791,7 @@ class ElasticTrainer:
                     if self.checkpoint is not None:
                         self.checkpoint.on_step(self)
                     self._run_deferred_probes()
+                    self._publish_warm_spec(data)
                     if on_step is not None:
                         on_step(self, loss)
                     if self.log_every and self.step % self.log_every == 0 and self.comm.rank == 0:

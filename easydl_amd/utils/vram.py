@@ -73,6 +73,20 @@ def publish(kv, slot: str, owner: str, tensors: dict[str, torch.Tensor]) -> int:
     return len(descs)
 
 
+def publish_warm(kv, slot: str, spec: dict | None) -> None:
+    """The warm-up a standby should run for ``slot`` (operator/standby.py warm_device); None:
+    only the generic small one."""
+    kv.set(f"vram/warm/{slot}", json.dumps({"spec": spec}))
+
+
+def read_warm(kv, slot: str) -> tuple[bool, dict | None]:
+    """(published, spec) of ``slot``'s warm-up."""
+    raw = kv.get_str(f"vram/warm/{slot}")
+    if raw is None:
+        return False, None
+    return True, json.loads(raw).get("spec")
+
+
 def slots(kv) -> list[str]:
     return sorted({s for s in (kv.get_str("vram/slots") or "").split(",") if s})
 

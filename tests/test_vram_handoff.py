@@ -231,6 +231,41 @@ def test_standby_warm_up_step_runs_and_frees(cuda):
     assert s > 0 and torch.cuda.memory_allocated(cuda) - before < 64 << 20
 
 
+@pytest.mark.gpu
+def test_standby_full_width_warm_up_from_the_published_spec(cuda):
+    from easydl_amd.operator.standby import _warm_llama, warm_device
+    spec = {"model": "llama", "batch": [1, 512],
+            "cfg": {"vocab_size": 4096, "dim": 1024, "n_layers": 4, "n_heads": 8, "n_kv_heads": 2, "ffn_dim": 2048,
+                    "max_seq_len": 512}}
+    before = torch.cuda.memory_allocated(cuda)
+    assert _warm_llama(cuda, spec)
+    assert warm_device(cuda.index or 0, spec) > 0
+    assert torch.cuda.memory_allocated(cuda) - before < 64 << 20
+
+
+def test_warm_spec_round_trip_and_sizing():
+    from easydl_amd.models.llama import get_config
+    from easydl_amd.operator.standby import _llama_warm_bytes
+
+    class KV(dict):
+        def set(self, k, v):
+            self[k] = v
+
+        def get_str(self, k):
+            return self.get(k)
+
+    kv = KV()
+    assert vram.read_warm(kv, "worker0") == (False, None)
+    vram.publish_warm(kv, "worker0", None)
+    assert vram.read_warm(kv, "worker0") == (True, None)
+    spec = {"model": "llama", "cfg": {"dim": 4096}, "batch": [1, 8192]}
+    vram.publish_warm(kv, "worker0", spec)
+    assert vram.read_warm(kv, "worker0") == (True, spec)
+    # one Llama-3-8B layer at one 8k sequence: ~20 GB, far below what a worker leaves free
+    gb = _llama_warm_bytes(get_config("llama3-8b", n_layers=1), 8192) / 2**30
+    assert 10 < gb < 30
+
+
 def test_hbm_resume_check_failure_stops_at_the_next_update(tmp_path):
     """The post-reap re-read of the step marks runs off the training path; if the marks moved
     (the dead worker's GPU updated the adopted state after the resume), the next optimizer
