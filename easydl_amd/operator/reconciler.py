@@ -279,6 +279,17 @@ class ElasticOperator:
             self.standbys[name] = Proc(name, "standby", self._standby_seq - 1, pid, None, Resource(), time.time())
             self.events.emit("standby_spawn", name=name, pid=pid)
 
+    def _standby_ready(self) -> bool:
+        if self.kv is None:
+            return False
+        for sname in list(self.standbys):
+            try:
+                if self.kv.get(f"standby/ready/{sname}"):
+                    return True
+            except Exception:  # noqa: BLE001 - store unreachable: no standby to count on
+                return False
+        return False
+
     def _take_standby(self, role, name, argv, delta, gpu, cpus, res, index, generation) -> Proc | None:
         from easydl_amd.operator.standby import module_of
         if role != "worker" or not self.standbys or self.kv is None or module_of(argv) is None:
@@ -485,8 +496,10 @@ class ElasticOperator:
         page tables of a large mapped snapshot segment takes ~19 ms per GB after that
         (scripts/exit_cost_probe.cpp); the replacement does not wait for it.  A replacement
         that adopted the dead worker's HBM re-verifies its restored state once the dead
-        process is reaped, before its first optimizer step (ckpt/manager.py fence).
-        EDL_EARLY_HANDOVER=0: wait for the reap as before."""
+        process is reaped, before its first optimizer step (ckpt/manager.py fence).  Only when
+        a parked standby is ready to take over: it builds on the dead worker's HBM (utils/vram.py),
+        while a freshly started process would allocate it and run out of memory until the dead
+        one's HBM is released.  EDL_EARLY_HANDOVER=0: wait for the reap as before."""
         if os.environ.get("EDL_EARLY_HANDOVER", "1") == "0":
             return
         now = time.time()
@@ -496,6 +509,8 @@ class ElasticOperator:
             if not mm_released(p.pid):
                 continue
             if not exit_status(p.pid):   # a normal exit(0) (or unknown): its reap decides, as before
+                continue
+            if not self._standby_ready():
                 continue
             t = getattr(p, "_mm_gone_ts", None)
             if t is None:

@@ -496,9 +496,16 @@ class ElasticTrainer:
         self.needs_state = False
 
     def _open_marks(self) -> None:
-        """Step-mark page of this worker slot (utils/stepmarks.py), with VRAM hand-over on."""
+        """Step-mark page of this worker slot (utils/stepmarks.py), with VRAM hand-over on.
+        After an HBM resume the page still holds the dead worker's marks, which the post-reap
+        check re-reads (ckpt/manager.py _check_marks_after_reap): this process writes its own
+        only once that check has passed (the step loop calls this again after each fence).  If
+        it dies before, its replacement finds marks of a writer it did not adopt from and
+        restores from the snapshot."""
         from easydl_amd.utils import vram
         if self._marks is not None or not vram.enabled() or getattr(self, "kv", None) is None:
+            return
+        if self.checkpoint is not None and self.checkpoint.hbm_unverified():
             return
         from easydl_amd.utils.stepmarks import StepMarks
         try:
@@ -759,6 +766,7 @@ class ElasticTrainer:
                         hv = self.checkpoint.stats.pop("handover_verified_s", None)
                         if hv is not None:
                             self.events.emit("handover_verified", step=self.step, s=hv)
+                            self._open_marks()
                     t_fence = time.perf_counter()
                     if self._marks is not None:
                         self._marks.begin(self.step + 1, torch.cuda.current_stream(self.device)

@@ -293,3 +293,40 @@ def test_hbm_resume_check_failure_stops_at_the_next_update(tmp_path):
             ck.fence()
     finally:
         m.close(unlink=True)
+
+
+def test_early_hand_over_only_when_a_standby_is_ready():
+    """A SIGKILLed worker is replaced before its reap only if a parked standby will take its
+    place (it builds on the dead worker's HBM); a freshly started process would have to
+    allocate that HBM while the dead one still holds it."""
+    import signal
+    from types import SimpleNamespace
+
+    from easydl_amd.operator.reconciler import ElasticOperator, Proc
+    from easydl_amd.api.spec import Resource
+    child = subprocess.Popen([sys.executable, "-c", "import time; time.sleep(60)"])
+    try:
+        os.kill(child.pid, signal.SIGKILL)
+        t_end = time.time() + 10
+        from easydl_amd.utils.procfs import exit_status
+        while not exit_status(child.pid) and time.time() < t_end:   # a zombie, not yet reaped
+            time.sleep(0.01)
+        events = []
+        ready = {"v": False}
+        p = Proc("job-worker-0", "worker", 0, child.pid, 0, Resource(), time.time())
+        p._early_reported = True
+        op = SimpleNamespace(procs={p.name: p}, history=[], restarts=0,
+                             events=SimpleNamespace(emit=lambda kind, **kw: events.append(kind)),
+                             _standby_ready=lambda: ready["v"], _release_gpu=lambda q: None)
+        for _ in range(3):
+            ElasticOperator._early_replace(op)
+            time.sleep(0.12)
+        assert p.state == "running" and not events          # no standby: wait for the reap
+        ready["v"] = True
+        for _ in range(3):
+            ElasticOperator._early_replace(op)
+            time.sleep(0.12)
+        assert events == ["exit_early"] and p.state == "exited" and p.exit_code == -9
+        assert p.name not in op.procs and op.history == [p]
+    finally:
+        child.wait()
