@@ -68,9 +68,14 @@ def _llama_warm_bytes(cfg, tokens: int) -> int:
     return 4 * params + tokens * (10 * cfg.vocab_size + 64 * cfg.dim + 16 * cfg.ffn_dim)
 
 
+WARM_INFO: dict = {}     # what the last warm_device did (logged by the standby)
+
+
 def _warm_llama(dev, spec: dict) -> bool:
-    """Forward + backward of one layer of the worker's model at its micro-batch shape: the
-    GEMM shapes (hipBLASLt solutions), attention and norm kernels of the real step.  Skipped
+    """Forward + backward of one layer of the worker's model at its micro-batch shape, with its
+    parameters in flat buffers as the trainer has them (parallel/flat.py: weight gradients are
+    GEMMs accumulating into the flat gradient buffer, a different hipBLASLt solution than a
+    plain ``.grad``): the GEMM shapes, attention and norm kernels of the real step.  Skipped
     when the GPU has not got twice the memory it needs free."""
     import torch
 
@@ -80,17 +85,21 @@ def _warm_llama(dev, spec: dict) -> bool:
     cfg.n_layers = 1
     b, s = (int(x) for x in spec["batch"])
     free, _ = torch.cuda.mem_get_info(dev)
-    if free < 2 * _llama_warm_bytes(cfg, b * s) + (4 << 30):
+    need = _llama_warm_bytes(cfg, b * s)
+    WARM_INFO.update(free_gb=round(free / 2**30, 1), need_gb=round(need / 2**30, 1))
+    if free < 2 * need + (4 << 30):
         return False
+    from easydl_amd.parallel.flat import FlatParams
     model = Llama(cfg, device=dev)
+    flat = FlatParams(model)
     ids = torch.randint(0, cfg.vocab_size, (b, s), device=dev)
     model(ids, ids).backward()
     torch.cuda.synchronize(dev)
-    del model, ids
+    del model, flat, ids
     return True
 
 
-def warm_device(gpu: int, spec: dict | None = None) -> float:
+def warm_device(gpu: int, spec: dict | None = None, set_stream: bool = False) -> float:
     """One forward + backward + optimizer step of a small Llama of head dim 128 on ``gpu``,
     preceded, when the worker published its shape (``spec``, ElasticTrainer._publish_warm_spec),
     by a forward + backward of one layer of its model at full width.
@@ -109,12 +118,23 @@ def warm_device(gpu: int, spec: dict | None = None) -> float:
     from easydl_amd.models.llama import Llama, LlamaConfig
     from easydl_amd.optim import FlatAdamW
     from easydl_amd.parallel.flat import FlatParams
+    from easydl_amd.ops import gemm_tuning
     t0 = time.perf_counter()
     dev = torch.device("cuda", gpu)
+    # the replacement's GEMMs run through TunableOp with the shipped selections
+    # (ElasticTrainer.__init__) on a non-default stream: warm up in the same configuration,
+    # on the stream the trainer will then keep using (``set_stream``: a per-stream hipBLASLt
+    # workspace; the process's current stream stays set)
+    gemm_tuning.apply()
+    if set_stream and torch.cuda.current_stream(dev).cuda_stream == 0:
+        torch.cuda.set_stream(torch.cuda.Stream(dev))
     cfg = LlamaConfig(vocab_size=1024, dim=512, n_layers=1, n_heads=4, n_kv_heads=2, ffn_dim=1024, max_seq_len=256)
     with torch.cuda.device(dev):
+        WARM_INFO.clear()
         if spec and spec.get("model") == "llama":
-            _warm_llama(dev, spec)
+            t1 = time.perf_counter()
+            WARM_INFO["full_width"] = _warm_llama(dev, spec)
+            WARM_INFO["full_width_s"] = round(time.perf_counter() - t1, 3)
         model = Llama(cfg, device=dev)
         flat = FlatParams(model)
         opt = FlatAdamW(flat)
@@ -201,8 +221,9 @@ def main() -> int:
                     continue            # the worker has not finished its first step yet
                 warmed.add(h["gpu"])
                 try:
-                    s = round(warm_device(h["gpu"], spec), 3)
-                    kv.set(f"standby/warm/{name}/gpu{h['gpu']}", json.dumps({"s": s, "spec": spec is not None}))
+                    info = dict(s=round(warm_device(h["gpu"], spec, set_stream=True), 3), spec=spec is not None, **WARM_INFO)
+                    kv.set(f"standby/warm/{name}/gpu{h['gpu']}", json.dumps(info))
+                    print(f"standby {name}: warm-up on GPU {h['gpu']}: {json.dumps(info)}", file=sys.stderr, flush=True)
                 except Exception as e:  # noqa: BLE001 - an optimisation only
                     print(f"standby: warm-up on GPU {h['gpu']} failed: {e}", file=sys.stderr)
         if premap and time.monotonic() > next_scan:

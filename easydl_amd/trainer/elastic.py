@@ -735,7 +735,16 @@ class ElasticTrainer:
                 return self
             self._publish_vram()
             self._open_marks()
+            prof = None
+            if os.environ.get("EDL_PROFILE_FIRST_STEP", "0") == "1":
+                import cProfile         # diagnostics: host profile of this process's first step
+                prof = cProfile.Profile()
+                prof.enable()
             while self.step < num_steps:
+                if prof is not None and self.history:
+                    prof.disable()
+                    self._dump_profile(prof)
+                    prof = None
                 t0 = self._t_step = time.perf_counter()
                 ok = True
                 loss = None
@@ -820,6 +829,16 @@ class ElasticTrainer:
         finally:
             self._stop.set()
         return self
+
+    def _dump_profile(self, prof) -> None:
+        import io
+        import pstats
+        out = io.StringIO()
+        st = pstats.Stats(prof, stream=out)
+        st.sort_stats("cumulative").print_stats(40)
+        st.sort_stats("tottime").print_stats(25)
+        log.warning("first-step host profile (step %d):\n%s", self.step, out.getvalue())
+        print(out.getvalue(), file=__import__("sys").stderr, flush=True)
 
     def _run_deferred_probes(self) -> None:
         """A re-formed epoch's all-reduce probe, deferred off the recovery path: run after
