@@ -223,7 +223,8 @@ def main() -> int:
                 try:
                     info = dict(s=round(warm_device(h["gpu"], spec, set_stream=True), 3), spec=spec is not None, **WARM_INFO)
                     kv.set(f"standby/warm/{name}/gpu{h['gpu']}", json.dumps(info))
-                    print(f"standby {name}: warm-up on GPU {h['gpu']}: {json.dumps(info)}", file=sys.stderr, flush=True)
+                    print(f"standby {name}: warm-up on GPU {h['gpu']}: {json.dumps(info)}", file=sys.stderr,
+                          flush=True)
                 except Exception as e:  # noqa: BLE001 - an optimisation only
                     print(f"standby: warm-up on GPU {h['gpu']} failed: {e}", file=sys.stderr)
         if premap and time.monotonic() > next_scan:

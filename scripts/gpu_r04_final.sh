@@ -1,6 +1,7 @@
 #!/bin/bash
 # round 4, final validation on the final tree: the whole GPU test tier, the smoke test, the headline bench, the
-# 3-rank kill -> shrink -> rejoin drill (auto plane, hot standby with VRAM hand-over) and the no-survivor restore
+# 3-rank kill -> shrink -> rejoin drill (auto plane, hot standby with VRAM hand-over) and the no-survivor drills:
+# a kill inside an update (restore from /dev/shm) and a kill between updates (HBM resume)
 set -euo pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
@@ -14,6 +15,5 @@ EDL_TTR_KEEP=1 EDL_TTR_DIR=gpurun_out/final_drill timeout -k 10 300 python -u be
     > gpurun_out/r04_final_drill.log 2>&1
 EDL_TTR_KEEP=1 EDL_TTR_DIR=gpurun_out/final_ttr timeout -k 10 500 python -u bench.py --fault-inject --gpus 1 \
     --mbs 1 --accum 1 --steps 10 --warmup 7 --fault-step 10 > gpurun_out/r04_final_ttr.log 2>&1
-# a fresh process's first Llama-3-8B step, cold vs after a 1-layer warm-up of the same width
-timeout -k 10 300 python -u scripts/first_step_probe.py cold > gpurun_out/r04_first_step_cold.log 2>&1
-timeout -k 10 300 python -u scripts/first_step_probe.py warm > gpurun_out/r04_first_step_warm.log 2>&1
+EDL_TTR_KEEP=1 EDL_TTR_DIR=gpurun_out/final_ttr timeout -k 10 400 python -u bench.py --fault-inject --gpus 1 \
+    --mbs 1 --accum 1 --steps 12 --warmup 3 --fault-step 4 > gpurun_out/r04_final_ttr_hbm.log 2>&1
