@@ -221,7 +221,8 @@ def main() -> int:
                     continue            # the worker has not finished its first step yet
                 warmed.add(h["gpu"])
                 try:
-                    info = dict(s=round(warm_device(h["gpu"], spec, set_stream=True), 3), spec=spec is not None, **WARM_INFO)
+                    s = round(warm_device(h["gpu"], spec, set_stream=True), 3)
+                    info = dict(s=s, spec=spec is not None, **WARM_INFO)
                     kv.set(f"standby/warm/{name}/gpu{h['gpu']}", json.dumps(info))
                     print(f"standby {name}: warm-up on GPU {h['gpu']}: {json.dumps(info)}", file=sys.stderr,
                           flush=True)

@@ -240,7 +240,9 @@ def test_standby_full_width_warm_up_from_the_published_spec(cuda):
     before = torch.cuda.memory_allocated(cuda)
     assert _warm_llama(cuda, spec)
     assert warm_device(cuda.index or 0, spec) > 0
-    assert torch.cuda.memory_allocated(cuda) - before < 64 << 20
+    # the model's memory is freed; the GEMM libraries' workspaces (rocBLAS / hipBLASLt under
+    # TunableOp, ~200 MB) stay allocated, as in every process that ran a GEMM
+    assert torch.cuda.memory_allocated(cuda) - before < 256 << 20
 
 
 def test_warm_spec_round_trip_and_sizing():
