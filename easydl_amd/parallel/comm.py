@@ -459,10 +459,12 @@ class Communicator:
         if not ops:
             return
         if self.data_kind == "rccl" and hasattr(self.data, "_start_coalescing"):
-            self.data._start_coalescing(self.device)
+            # ProcessGroupNCCL's coalescing window (torch 2.10: no arguments): every send and
+            # receive below becomes one grouped RCCL launch, so no pairing order can deadlock
+            self.data._start_coalescing()
             for kind, t, peer, tag in ops:
                 (self.data.send if kind == "send" else self.data.recv)([t], peer, tag)
-            self._wait(self.data._end_coalescing(self.device))
+            self._wait(self.data._end_coalescing())
             return
         # gloo: every transfer in flight at once; (peer, tag) pairs match sends to receives
         works = [(self.data.send if kind == "send" else self.data.recv)([t], peer, tag) for kind, t, peer, tag in ops]

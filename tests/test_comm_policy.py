@@ -288,3 +288,43 @@ def test_policy_cache_needs_agreement():
     out = _spawn(2, fn)
     # both ranks read the same key after the barrier: agreed
     assert all(v is not None for v in out.values())
+
+
+def test_rccl_p2p_batch_uses_the_coalescing_window_of_this_torch():
+    """The multi-source state transfer on RCCL groups its sends and receives in
+    ProcessGroupNCCL's coalescing window.  Pin the arity of that (private) API on the
+    installed torch -- no argument, unlike older releases -- and drive _p2p_batch through
+    a stand-in with exactly that interface (RCCL itself needs a rank per GPU)."""
+    assert dist.ProcessGroupNCCL._start_coalescing.__doc__.startswith(
+        "_start_coalescing(self: torch._C._distributed_c10d.Backend) -> None")
+    assert dist.ProcessGroupNCCL._end_coalescing.__doc__.startswith(
+        "_end_coalescing(self: torch._C._distributed_c10d.Backend) -> c10d::Work")
+    calls = []
+
+    class Work:
+        def wait(self, *a):
+            return True
+
+        def is_completed(self):
+            return True
+
+    class FakeNCCL:
+        def _start_coalescing(self):
+            calls.append("start")
+
+        def _end_coalescing(self):
+            calls.append("end")
+            return Work()
+
+        def send(self, tensors, dst, tag):
+            calls.append(("send", dst, tag))
+
+        def recv(self, tensors, src, tag):
+            calls.append(("recv", src, tag))
+
+    c = Communicator.__new__(Communicator)
+    c.data_kind, c.data = "rccl", FakeNCCL()
+    c._wait = lambda w, poll=False: w.wait()
+    t = torch.zeros(4)
+    c._p2p_batch([("send", t, 1, 0), ("recv", t, 2, 0)])
+    assert calls == ["start", ("send", 1, 0), ("recv", 2, 0), "end"]
