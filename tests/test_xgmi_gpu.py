@@ -172,3 +172,18 @@ def test_auto_plane_probe_register_ddp_step_real_engine(cuda, tmp_path, world, m
         assert p2["cached"] and p2["measured_epoch"] == 1 and not r["pending2"], p2
         assert r["backend2"] == "gloo+xgmi" and r["warmup2_s"] < r["warmup_s"], r
     assert len({json.dumps(r["probe"]["policy"], sort_keys=True) for r in rs}) == 1   # agreed
+
+
+@pytest.mark.gpu
+def test_rccl_data_plane_world1_collectives_and_coalesced_p2p(cuda):
+    """Communicator's RCCL path on hardware: every collective it wraps, and the coalesced
+    send/receive batch of the multi-source state transfer (one rank; RCCL refuses two
+    ranks on one GPU).  In a child process with its own time limit."""
+    here = os.path.dirname(os.path.abspath(__file__))
+    p = subprocess.run([sys.executable, os.path.join(here, "helpers", "rccl_world1_proc.py")],
+                       capture_output=True, text=True, timeout=180)
+    assert p.returncode == 0, p.stderr[-3000:]
+    res = json.loads(p.stdout.strip().splitlines()[-1])
+    assert res.pop("data_kind") == "rccl", res
+    res.pop("backend")
+    assert all(res.values()), res
