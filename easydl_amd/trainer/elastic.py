@@ -895,7 +895,7 @@ class ElasticTrainer:
             pass
         else:
             old.shutdown()
-        _retire(old)
+        _retire(old, self.events)
         del old
         if self.rdzv is not None and self.rdzv.kv.exists(f"rdzv/leave/{self.ctx.node_id}"):
             raise SystemExit(0)
@@ -928,7 +928,7 @@ class _null:
         return False
 
 
-def _retire(comm) -> None:
+def _retire(comm, events=None) -> None:
     """Shorten the teardown of an aborted epoch's gloo groups.  A ProcessGroupGloo whose
     collective was abandoned on a dead peer blocks in its destructor until that collective
     times out; two survivors dropping their old groups at once can each wait for the other's
@@ -943,11 +943,14 @@ def _retire(comm) -> None:
         # off the recovery path once its stream has drained (the abort word ends every spin).
         comm.xgmi = None
 
-        def _release(eng=x):
+        def _release(eng=x, epoch=getattr(comm, "epoch", None)):
+            t0 = time.perf_counter()
             try:
                 eng.close_after_abort()
             except Exception as e:  # noqa: BLE001
                 log.warning("releasing an aborted xGMI engine failed: %s", e)
+            if events is not None:
+                events.emit("xgmi_released", epoch=epoch, s=round(time.perf_counter() - t0, 3))
         threading.Thread(target=_release, name="edl-xgmi-release", daemon=True).start()
     import datetime
     for pg in (getattr(comm, "data", None), getattr(comm, "ctrl", None)):
