@@ -169,6 +169,14 @@ class ElasticOperator:
         if max(self.cfg.standby, getattr(self.job, "standby", 0)) > 0:
             # workers export their state buffers, a standby adopts a dead one's (utils/vram.py)
             env.setdefault("EDL_VRAM_HANDOFF", "1")
+        if len(set(self.cfg.gpus)) < len(self.cfg.gpus):
+            # several ranks share a GPU: every process's streams beyond this many share hardware
+            # queues.  With HIP's default (4 per process) the ranks, standbys and replacements
+            # oversubscribe the queues the scheduler maps at once; it then time-slices whole
+            # processes, and the engine's cross-process barriers stall across slices: world-3
+            # steps of 33-460 ms median after a kill + rejoin, 5.8 ms with 2 queues
+            # (profiles/r04_shared_gpu_rejoin_slowdown.md)
+            env["GPU_MAX_HW_QUEUES"] = os.environ.get("EDL_SHARED_GPU_HW_QUEUES", "2")
         for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_USE_AGENT_STORE"):
             env.pop(k, None)
         return env
