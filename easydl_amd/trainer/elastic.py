@@ -353,6 +353,7 @@ class ElasticTrainer:
 
         def build():
             try:
+                _join_releases()
                 # a job's first epoch may measure the all-reduce policy; every later epoch
                 # (shrink, rejoin, scale-up) is on the recovery critical path: cached policy or
                 # RCCL until the deferred probe after its first committed step
@@ -928,6 +929,24 @@ class _null:
         return False
 
 
+_RELEASES: list[threading.Thread] = []   # aborted engines being released (_retire)
+
+
+def _join_releases(timeout_s: float = 10.0) -> None:
+    """Wait for the aborted engines' releases before a new engine allocates and exports its
+    workspace: a workspace exported (hipIpcGetMemHandle) while the old one is being freed on
+    another thread failed with hipErrorInvalidValue in a 4-rank kill drill (batch 30).  The
+    release is quick -- the abort word ends every spin -- (2-40 ms measured)."""
+    t_end = time.monotonic() + timeout_s
+    while _RELEASES:
+        th = _RELEASES[0]
+        th.join(max(0.0, t_end - time.monotonic()))
+        if th.is_alive():
+            log.warning("an aborted xGMI engine is still being released; building the next one anyway")
+            return
+        _RELEASES.pop(0)
+
+
 def _retire(comm, events=None) -> None:
     """Shorten the teardown of an aborted epoch's gloo groups.  A ProcessGroupGloo whose
     collective was abandoned on a dead peer blocks in its destructor until that collective
@@ -951,7 +970,9 @@ def _retire(comm, events=None) -> None:
                 log.warning("releasing an aborted xGMI engine failed: %s", e)
             if events is not None:
                 events.emit("xgmi_released", epoch=epoch, s=round(time.perf_counter() - t0, 3))
-        threading.Thread(target=_release, name="edl-xgmi-release", daemon=True).start()
+        th = threading.Thread(target=_release, name="edl-xgmi-release", daemon=True)
+        _RELEASES.append(th)
+        th.start()
     import datetime
     for pg in (getattr(comm, "data", None), getattr(comm, "ctrl", None)):
         if isinstance(pg, dist.ProcessGroupGloo):
