@@ -506,7 +506,9 @@ class CheckpointManager:
         if not self.sharded and comm.rank != 0:
             return None
         mode = self._decide_mode(trainer, comm, key, *sizes)
-        if mode != "off" and state and state[0][1].is_cuda:
+        if mode != "off" and state and state[0][1].is_cuda and self._ticket is None:
+            # (with a snapshot still in flight, changing segments would first wait for its copy
+            # -- 0.4 s of a 4-rank shrink's recovery in batch 30; the next snapshot does it)
             self._layout_segment(world, shard, tag, state if mode == "full" else lean_state, headroom)
         return mode
 
