@@ -81,7 +81,8 @@ def main():
     if args.scale_up:
         from easydl_amd.trainer import scale_bench
         start, end = args.scale_up.split(":")
-        return scale_bench.main(["--start", start, "--end", end, "--steps", str(args.warmup + args.steps)])
+        return scale_bench.main(["--start", start, "--end", end, "--steps", str(args.warmup + args.steps)]
+                                + (["--share-gpu"] if args.share_gpu else []))
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
