@@ -23,6 +23,7 @@ incarnation's pid, so exit events keep flowing through the supervisor).
 """
 from __future__ import annotations
 
+import gc
 import importlib
 import json
 import os
@@ -96,6 +97,7 @@ def _warm_llama(dev, spec: dict) -> bool:
     model(ids, ids).backward()
     torch.cuda.synchronize(dev)
     del model, flat, ids
+    gc.collect()    # the flat buffers' gradient hooks form reference cycles with the parameters
     return True
 
 
@@ -144,6 +146,7 @@ def warm_device(gpu: int, spec: dict | None = None, set_stream: bool = False) ->
         opt.step()
         torch.cuda.synchronize(dev)
         del model, flat, opt, loss, ids
+        gc.collect()    # (see _warm_llama): otherwise the state stays allocated until a GC cycle
         torch.cuda.empty_cache()
     return time.perf_counter() - t0
 
