@@ -16,14 +16,26 @@ init, synthetic tokens).  W untimed warmup steps, then exactly K steps
 bracketed by barrier + synchronize; the elapsed time is the MAX over ranks;
 rank 0 prints one JSON line.
 
-``--fault-inject`` (not part of the default run) measures time-to-recover with
-the local operator: see ``easydl_amd/trainer/fault_bench.py``.
+Time-to-recover, the other half of the headline metric (BASELINE.json), is
+measured in the same run at N=1: this process then stays GPU-free and runs two
+fresh children one after the other -- the throughput measurement above
+(``--child``), then the no-survivor fault drill at the SAME configuration
+(full Llama-3-8B, seq 8192, 2 x 4 micro-batches, in-memory snapshots every 2
+steps, one hot standby; the only worker is SIGKILLed 40 % into a step once the
+standby is warm).  The drill's TTR, phases, steps lost and time to regain the
+pre-fault step go into ``time_to_recover_s`` / ``ttr`` of the one JSON line; a
+failed drill leaves ``time_to_recover_s: null`` with an ``error`` and never
+fails the throughput line.  ``--ttr off`` skips the drill.  Under torchrun
+(N>1) the ranks belong to the launcher, which tears the job down when one of
+them dies, so TTR comes from the local-operator drill (``--fault-inject``).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import signal
+import subprocess
 import sys
 import time
 
@@ -70,11 +82,105 @@ def parse():
     ap.add_argument("--sp", action="store_true", help="Megatron sequence parallelism inside the TP group")
     ap.add_argument("--tp", type=int, default=1,
                     help="tensor-parallel degree inside each DP replica (BASELINE config 5: --model llama3-70b --tp 8)")
+    ap.add_argument("--fault-mode", default="midstep", choices=["midstep", "in_update", "step_start"],
+                    help="--fault-inject: where the kill lands (trainer/fault_bench.py)")
+    ap.add_argument("--ttr", default="auto", choices=["auto", "off"],
+                    help="N=1 on a GPU host: also run the time-to-recover drill at this config (auto)")
+    ap.add_argument("--ttr-timeout", type=float, default=float(os.environ.get("EDL_TTR_TIMEOUT", 330)),
+                    help="seconds the time-to-recover drill may take before it is abandoned")
+    ap.add_argument("--child", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
+
+
+def _json_line(text: str) -> dict | None:
+    for ln in reversed((text or "").splitlines()):
+        ln = ln.strip()
+        if ln.startswith("{"):
+            try:
+                return json.loads(ln)
+            except ValueError:
+                continue
+    return None
+
+
+def _run_child(argv: list[str], timeout_s: float, env: dict | None = None) -> tuple[int | None, str]:
+    """Run ``argv`` in its own process group (stderr passes through); on timeout the whole
+    group (operator, workers, standbys of a drill) is killed.  Returns (rc or None, stdout)."""
+    p = subprocess.Popen(argv, stdout=subprocess.PIPE, text=True, env=env, start_new_session=True)
+    try:
+        out, _ = p.communicate(timeout=timeout_s)
+        return p.returncode, out
+    except subprocess.TimeoutExpired:
+        try:
+            os.killpg(p.pid, signal.SIGKILL)
+        except OSError:
+            pass
+        out, _ = p.communicate()
+        return None, out
+
+
+def _gpu_host() -> bool:
+    """GPUs on this host, found without initialising HIP in this process (KFD sysfs)."""
+    try:
+        from easydl_amd.brain.collectors import kfd_gpus
+        return bool(kfd_gpus())
+    except Exception:  # noqa: BLE001
+        return False
+
+
+def parent(args) -> int:
+    """N=1 headline: throughput child, then the time-to-recover drill child, one JSON line."""
+    me = os.path.abspath(__file__)
+    rc, out = _run_child([sys.executable, me, *sys.argv[1:], "--child"], timeout_s=3600)
+    res = _json_line(out)
+    if rc != 0 or res is None:
+        sys.stdout.write(out)
+        print(f"[bench] throughput child failed (rc={rc})", file=sys.stderr)
+        return rc if rc else 1
+    ttr = {"mode": "midstep", "hot_standby": 1, "ckpt_interval": 2}
+    t0 = time.perf_counter()
+    try:
+        from easydl_amd.ckpt.manager import unlink_job_segments
+        unlink_job_segments("bench")
+        env = dict(os.environ, EDL_FAULT_STEP_MS=str(res["ms_per_step"]))
+        drill = [sys.executable, me, "--fault-inject", "--gpus", "1", "--model", args.model, "--seq", str(args.seq),
+                 "--mbs", str(args.mbs), "--accum", str(args.accum), "--ckpt-interval", "2", "--standby", "1",
+                 "--fault-mode", "midstep", "--fault-step", "4", "--steps", "0", "--warmup", "0"]
+        if args.layers:
+            drill += ["--layers", str(args.layers)]
+        drc, dout = _run_child(drill, timeout_s=args.ttr_timeout, env=env)
+        d = _json_line(dout)
+        ttr["drill_wall_s"] = round(time.perf_counter() - t0, 1)
+        if d is None or d.get("value") is None:
+            ttr["error"] = ("drill timed out" if drc is None else f"drill rc={drc}") + \
+                ("" if d is None else f", no recovery in the timeline: {json.dumps(d.get('breakdown'))[:300]}")
+        else:
+            res["time_to_recover_s"] = d["value"]
+            b = d.get("breakdown") or {}
+            ttr.update({
+                "time_to_regain_s": d.get("time_to_regain_s"), "steps_lost": d.get("steps_lost"),
+                "restored_from": d.get("restored_from"), "fault_step": (d.get("fault") or {}).get("step"),
+                "fault_spec": (d.get("fault") or {}).get("spec"),
+                "replacement_from_standby": d.get("replacement_from_standby"),
+                "step_s_before_fault": d.get("step_s_before_fault"),
+                "phases": {k: b.get(k) for k in ("detect_s", "replacement_spawn_s", "replacement_joined_s",
+                                                 "comm_ready_s", "state_synced_s", "first_step_s")},
+                "config": d.get("config"), "model": d.get("model"), "operator_rc": d.get("operator_rc")})
+    except Exception as e:  # noqa: BLE001 - the drill never fails the throughput line
+        ttr["error"] = f"{type(e).__name__}: {e}"[:300]
+    res["ttr"] = ttr
+    print(json.dumps(res), flush=True)
+    if args.out:
+        with open(args.out, "w") as f:
+            f.write(json.dumps(res) + "\n")
+    return 0
 
 
 def main():
     args = parse()
+    if (not args.child and not args.fault_inject and not args.scale_up and not args.share_gpu and args.ttr == "auto"
+            and os.environ.get("WORLD_SIZE", "1") == "1" and args.tp == 1 and _gpu_host()):
+        return parent(args)
     if args.fault_inject:
         from easydl_amd.trainer import fault_bench
         return fault_bench.main(args)
@@ -201,6 +307,7 @@ def main():
         "loss": round(float(tr.last_loss), 4) if tr.last_loss is not None else None,
         "peak_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 2**30, 1) if use_cuda else 0.0,
         "setup_and_warmup_s": round(marks["t0"] - t_start, 2),
+        # N=1 on a GPU host: filled in by the parent from the drill; otherwise see --fault-inject
         "time_to_recover_s": None,
         "ckpt": None if ckpt is None else {
             "interval": args.ckpt_interval, "snapshots": ckpt.stats["snapshots"],
@@ -221,4 +328,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

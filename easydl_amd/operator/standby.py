@@ -199,9 +199,13 @@ def main() -> int:
     info = prewarm()
     info.update(pid=os.getpid(), ts=time.time())
     kv.set(f"standby/ready/{name}", json.dumps(info))
+    from easydl_amd.utils import vram
+    if not info.get("gpus"):
+        kv.set("standby/warm_gpu/cpu", json.dumps({"standby": name}))   # nothing to warm on a CPU host
+    elif not vram.enabled():
+        kv.set("standby/warm_gpu/any", json.dumps({"standby": name}))   # no hand-over: nothing per GPU
     key = f"standby/assign/{name}"
     premap = os.environ.get("EDL_STANDBY_PREMAP", "0") == "1"
-    from easydl_amd.utils import vram
     handoff = vram.enabled() and info.get("gpus", 0) > 0
     held: dict[str, dict] = {}     # worker slot -> imported state buffers (utils/vram.py)
     warmed: set[int] = set()       # GPUs this standby has run its warm-up step on
@@ -217,7 +221,11 @@ def main() -> int:
             _import_vram(kv, held)
             next_vram = time.monotonic() + 1.0
             for slot, h in sorted(held.items()):
-                if not warm_on or not h or not h.get("tensors") or h["gpu"] in warmed:
+                if not h or not h.get("tensors") or h["gpu"] in warmed:
+                    continue
+                if not warm_on:
+                    warmed.add(h["gpu"])
+                    kv.set(f"standby/warm_gpu/{h['gpu']}", json.dumps({"standby": name, "warmup": "off"}))
                     continue
                 published, spec = vram.read_warm(kv, slot)
                 if not published:
@@ -227,10 +235,12 @@ def main() -> int:
                     s = round(warm_device(h["gpu"], spec, set_stream=True), 3)
                     info = dict(s=s, spec=spec is not None, **WARM_INFO)
                     kv.set(f"standby/warm/{name}/gpu{h['gpu']}", json.dumps(info))
+                    kv.set(f"standby/warm_gpu/{h['gpu']}", json.dumps(dict(info, standby=name)))
                     print(f"standby {name}: warm-up on GPU {h['gpu']}: {json.dumps(info)}", file=sys.stderr,
                           flush=True)
                 except Exception as e:  # noqa: BLE001 - an optimisation only
                     print(f"standby: warm-up on GPU {h['gpu']} failed: {e}", file=sys.stderr)
+                    kv.set(f"standby/warm_gpu/{h['gpu']}", json.dumps({"standby": name, "error": str(e)[:200]}))
         if premap and time.monotonic() > next_scan:
             from easydl_amd.ckpt.manager import premap_job_segments
             mapped = premap_job_segments(job)

@@ -75,6 +75,18 @@ class FlatAdamW:
         return self.schedule(self.step_count + 1) if self.schedule else self.lr
 
     @torch.no_grad()
+    def reset_state(self) -> None:
+        """Fresh-start optimizer state for the current weights: master = weights, zero moments
+        (after :meth:`FlatParams.reinit_adopted`)."""
+        for g, st in zip(self.flat.groups, self.state):
+            if st["master"].data_ptr() != g.data.data_ptr():
+                st["master"].copy_(g.data)
+            st["m"].zero_()
+            st["v"].zero_()
+        self.step_count = 0
+        self.moment_origin = 0
+
+    @torch.no_grad()
     def step(self, pre_scale: float = 1.0) -> torch.Tensor:
         """Apply one update; ``pre_scale`` multiplies the (summed) gradients, e.g. 1/world."""
         grads = [g.grad for g in self.flat.groups]
@@ -128,6 +140,16 @@ class FlatSGD:
                 "master": g.data.float() if has16 else g.data,
                 "mom": _zeros(f"opt/{g.name}/mom", g) if momentum else None,
             })
+
+    @torch.no_grad()
+    def reset_state(self) -> None:
+        """See :meth:`FlatAdamW.reset_state`."""
+        for g, st in zip(self.flat.groups, self.state):
+            if st["master"].data_ptr() != g.data.data_ptr():
+                st["master"].copy_(g.data)
+            if st["mom"] is not None:
+                st["mom"].zero_()
+        self.step_count = 0
 
     @torch.no_grad()
     def step(self, pre_scale: float = 1.0):

@@ -198,7 +198,11 @@ class Communicator:
         that would otherwise sit between a fault and the first recovered step)."""
         cached = self._cached_policy()
         if cached is not None:
-            self._adopt_probe(dict(cached, cached=True, epoch=self.epoch, measured_epoch=cached.get("epoch")))
+            # an earlier epoch's timings, but THIS epoch's mappings: they must sum exactly first
+            exact = self._exact_gate()
+            self._adopt_probe(dict(cached, cached=True, epoch=self.epoch, measured_epoch=cached.get("epoch"),
+                                   exact_everywhere=bool(cached.get("exact_everywhere")) and exact,
+                                   gate_exact=exact))
             return
         if self.probe_mode == "defer":
             self.probe_pending = True     # RCCL only until run_deferred_probe() / adopt_policy()
@@ -226,9 +230,42 @@ class Communicator:
         if self.xgmi is None or self.xgmi_mode != "auto" or not self.probe_pending:
             return self.apply_allreduce_policy(pol)
         self.probe_pending = False
-        self._adopt_probe({"epoch": self.epoch, "world": self.world_size, "exact_everywhere": True, "policy": pol,
-                           "source": "brain"})
+        exact = self._exact_gate()
+        self._adopt_probe({"epoch": self.epoch, "world": self.world_size, "exact_everywhere": exact, "policy": pol,
+                           "source": "brain", "gate_exact": exact})
         return self.xgmi is not None
+
+    GATE_ELEMS = 1 << 17      # 256 KB of bf16: both engine forms that run on the workspace
+
+    def _exact_gate(self) -> bool:
+        """Correctness gate for a policy adopted without a probe (cached, or the Brain's):
+        one integer-valued all-reduce through the data plane and through the engine's
+        two-shot and one-shot forms on this epoch's freshly mapped workspaces, compared
+        exactly on every rank and agreed (MAX of failures) over the control plane.  The
+        timing sweep is what a cached policy skips; this check is not."""
+        g = torch.Generator(device="cpu").manual_seed(11 + self.rank)
+        src = torch.randint(-4, 5, (self.GATE_ELEMS,), generator=g, dtype=torch.int8).to(self.device, torch.bfloat16)
+        bad = 0.0
+        keep_timeout, self.xgmi.timeout_s = self.xgmi.timeout_s, 5.0
+        try:
+            ref = src.clone()
+            self.data.allreduce([ref]).wait()
+            for algo in ("twoshot", "oneshot"):
+                t = src.clone()
+                self.xgmi.all_reduce(t, algo)
+                self._sync_stream()
+                if not torch.equal(ref, t) or self.xgmi.status() != 0:
+                    bad = 1.0
+        except Exception as e:  # noqa: BLE001
+            log.warning("xGMI exactness gate failed: %s", e)
+            bad = 1.0
+        finally:
+            self.xgmi.timeout_s = keep_timeout
+        bad = float(self.ctrl_all_reduce([bad], dist.ReduceOp.MAX)[0])
+        if bad:
+            log.warning("epoch %d: the xGMI engine did not sum exactly; all-reduce stays on %s", self.epoch,
+                        self.data_kind)
+        return not bad
 
     def _adopt_probe(self, probe: dict) -> None:
         pol = probe.get("policy") or {}

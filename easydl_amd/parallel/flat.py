@@ -121,6 +121,9 @@ class FlatParams:
             key = ("no_decay" if no_decay(n, p) else "decay", p.dtype)
             buckets.setdefault(key, []).append((n, p))
         self.groups: list[FlatGroup] = []
+        # init values of parameters whose storage was adopted from a dead worker (utils/vram.py):
+        # kept until the trainer knows where this process's state comes from (reinit_adopted)
+        self._init_copies: list[tuple[torch.Tensor, torch.Tensor]] = []
         chunks = []
         for (cls, dt), plist in sorted(buckets.items(), key=lambda kv: (kv[0][0], str(kv[0][1]))):
             base = cls if dt == self.dtype else f"{cls}_{str(dt).split('.')[-1]}"
@@ -143,6 +146,8 @@ class FlatParams:
                 if not adopted:
                     with torch.no_grad():
                         view.copy_(p.data)
+                else:
+                    self._init_copies.append((view, p.data))
                 p.data = view
                 if gdt != dt and hasattr(p, "grad_dtype"):
                     # fp32 gradient buffers under bf16 parameters (grad_dtype=fp32): torch >= 2.10
@@ -229,6 +234,22 @@ class FlatParams:
                     s.param.grad.zero_()
                     s.param._edl_fresh = False
 
+    # -- adopted storage ------------------------------------------------------
+    def reinit_adopted(self) -> int:
+        """Adopted weights that nothing will overwrite (no HBM resume, no snapshot, no state
+        transfer): back to this process's own seeded init values, as a fresh start would have
+        them.  Returns the number of parameters re-initialised."""
+        with torch.no_grad():
+            for view, init in self._init_copies:
+                view.copy_(init)
+        n = len(self._init_copies)
+        self._init_copies = []
+        return n
+
+    def drop_init_copies(self) -> None:
+        """The state is settled (resumed, restored or transferred): free the init values."""
+        self._init_copies = []
+
     # -- views ---------------------------------------------------------------
     def params(self):
         for g in self.groups:
@@ -271,13 +292,35 @@ class FlatBuffers:
                 seen.add(id(b))
                 by_dtype.setdefault(b.dtype, []).append((mod, name, b))
         self.tensors: dict[str, torch.Tensor] = {}
+        self._init_copies: list[tuple[torch.Tensor, torch.Tensor]] = []
         for dt, items in by_dtype.items():
-            flat = torch.empty(sum(b.numel() for _, _, b in items), dtype=dt, device=items[0][2].device)
+            key = str(dt).replace("torch.", "")
+            n = sum(b.numel() for _, _, b in items)
+            dev = items[0][2].device
+            # a dead worker's running statistics (utils/vram.py), kept for an HBM resume
+            flat = vram.take(f"bufs/{key}", n, dt, dev, keep=True)
+            adopted = flat is not None
+            flat = torch.empty(n, dtype=dt, device=dev) if flat is None else flat
             off = 0
             with torch.no_grad():
                 for mod, name, b in items:
                     view = flat[off:off + b.numel()].view(b.shape)
-                    view.copy_(b)
+                    if adopted:
+                        self._init_copies.append((view, b))
+                    else:
+                        view.copy_(b)
                     mod._buffers[name] = view
                     off += b.numel()
-            self.tensors[str(dt).replace("torch.", "")] = flat
+            self.tensors[key] = flat
+
+    def reinit_adopted(self) -> int:
+        """See :meth:`FlatParams.reinit_adopted`."""
+        with torch.no_grad():
+            for view, init in self._init_copies:
+                view.copy_(init)
+        n = len(self._init_copies)
+        self._init_copies = []
+        return n
+
+    def drop_init_copies(self) -> None:
+        self._init_copies = []

@@ -294,6 +294,12 @@ class ParameterServer:
                         if wid not in self._push_flag:
                             self._push_flag[wid] = torch.zeros(4, dtype=torch.int32, device=st.device)
                             self._push_status[wid] = torch.zeros(4, dtype=torch.int32, device=st.device)
+                        else:
+                            # a (re)connecting client -- the same worker after a reconnect, or its
+                            # replacement -- counts its push sequence from 0 again: restart the flag
+                            # in stream order, or every wait for a small seq would pass at once
+                            self._push_flag[wid].zero_()
+                            self.stats["flag_resets"] = self.stats.get("flag_resets", 0) + 1
                         desc["flag"] = export_tensor(self._push_flag[wid])
                         cap = int(hdr.get("sparse_cap", 0))
                         if self.tables and cap > 0:

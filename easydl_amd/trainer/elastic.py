@@ -137,6 +137,13 @@ class ElasticTrainer:
         self.metrics = MetricsReporter(
             path=os.path.join(self.ctx.run_dir, f"metrics-{self.ctx.role}{self.ctx.index}.jsonl"))
         self.plan_version = 0
+        self._stop_requested = False
+
+    def request_stop(self) -> None:
+        """End ``fit`` after the current step (from ``on_step``).  Every rank must ask at the
+        same committed step, e.g. from a step-based condition, like any other collective
+        decision."""
+        self._stop_requested = True
 
     # ------------------------------------------------------------------ setup
     def _build_model(self, tp_rank: int) -> None:
@@ -168,10 +175,16 @@ class ElasticTrainer:
             self.opt.norm_weights = w
             self.opt.norm_reduce = lambda t: self.comm.tp.all_reduce(t)
         self.ddp = ElasticDDP(self.flat, None, bucket_mb=a["bucket_mb"])
+        from easydl_amd.utils import vram
+        dropped = vram.release_unused()   # adopted buffers nothing here took: back to the driver
         if self.device.type == "cuda":
             torch.cuda.synchronize(self.device)
         if getattr(self, "events", None) is not None:
-            self.events.emit("model_built", model_s=round(t1 - t0, 4), flat_opt_s=round(time.perf_counter() - t1, 4))
+            self.events.emit("model_built", model_s=round(t1 - t0, 4), flat_opt_s=round(time.perf_counter() - t1, 4),
+                             adopted=len(vram.TAKEN), adopted_unused=len(dropped))
+            if dropped:
+                log.warning("vram: %d adopted buffers matched nothing and were released: %s", len(dropped),
+                            dropped[:8])
 
     def _connect(self):
         if self.ctx.standalone:
@@ -395,16 +408,17 @@ class ElasticTrainer:
         """Make every rank hold the newest committed state."""
         c = self.comm
         if c.world_size == 1:
-            if self.needs_state and self.checkpoint is not None:
+            if self.needs_state:
                 self._maybe_restore()
             self.needs_state = False
+            self._state_settled()
             return
         have = -1 if self.needs_state else self.step
         max_step = int(c.ctrl_all_reduce([have], dist.ReduceOp.MAX)[0])
         holder = max_step >= 0 and not self.needs_state and self.step == max_step
         if max_step < 0:
             # nobody holds trained state: fresh start (or checkpoint restore on rank 0)
-            if c.rank == 0 and self.checkpoint is not None:
+            if c.rank == 0:
                 self._maybe_restore()
             holders = [0]
         else:
@@ -430,6 +444,7 @@ class ElasticTrainer:
             self.events.emit("state_broadcast", src=src_rank, sources=len(holders), bytes=nbytes,
                              s=round(time.time() - t0, 4))
         self.needs_state = False
+        self._state_settled()
 
     def _fence_snapshot_before_overwrite(self, c, src: int, holder: bool) -> None:
         """A state transfer rewrites this rank's buffers unless it is the source, or a
@@ -492,9 +507,12 @@ class ElasticTrainer:
                 self.events.emit("restored", step=self.step, source=src, tp_rank=t)
             elif max_step >= 0:
                 raise RuntimeError(f"TP shard {t} lost at step {max_step} and no in-memory snapshot covers it")
-            # else: fresh start; replicas of a shard are identical by seeding (no broadcast)
+            else:
+                # fresh start; replicas of a shard are identical by seeding (no broadcast)
+                self._reinit_adopted()
         self.held_tp = t
         self.needs_state = False
+        self._state_settled()
 
     def _open_marks(self) -> None:
         """Step-mark page of this worker slot (utils/stepmarks.py), with VRAM hand-over on.
@@ -531,13 +549,7 @@ class ElasticTrainer:
         from easydl_amd.utils import vram
         if not (vram.enabled() and self.device.type == "cuda" and getattr(self, "kv", None) is not None):
             return
-        ts = {}
-        for g in self.flat.groups:
-            ts[f"flat/{g.name}/data"], ts[f"flat/{g.name}/grad"] = g.data, g.grad
-        for g, st in zip(self.flat.groups, getattr(self.opt, "state", [])):
-            for k, t in st.items():
-                if isinstance(t, torch.Tensor) and t is not g.data:
-                    ts[f"opt/{g.name}/{k}"] = t
+        ts = self.vram_state_tensors()
         try:
             n = vram.publish(self.kv, f"{self.ctx.role}{self.ctx.index}", self.ctx.node_id, ts)
         except Exception as e:  # noqa: BLE001 - hand-over is an optimisation; training goes on
@@ -545,6 +557,20 @@ class ElasticTrainer:
             return
         self.events.emit("vram_published", tensors=n, of=len(ts),
                          adopted=dict(vram.STATS, adopted_gb=round(vram.STATS["adopted_bytes"] / 2**30, 1)))
+
+    def vram_state_tensors(self) -> dict[str, torch.Tensor]:
+        """The persistent buffers a hot standby adopts (utils/vram.py names): flat weights and
+        gradients, optimizer state, module buffers (BatchNorm running statistics)."""
+        ts = {}
+        for g in self.flat.groups:
+            ts[f"flat/{g.name}/data"], ts[f"flat/{g.name}/grad"] = g.data, g.grad
+        for g, st in zip(self.flat.groups, getattr(self.opt, "state", [])):
+            for k, t in st.items():
+                if isinstance(t, torch.Tensor) and t is not g.data:
+                    ts[f"opt/{g.name}/{k}"] = t
+        for k, t in getattr(self.bufs, "tensors", {}).items():
+            ts[f"bufs/{k}"] = t
+        return ts
 
     def _publish_warm_spec(self, data) -> None:
         """Tell the parked standby on this GPU what to warm up with (operator/standby.py
@@ -583,26 +609,58 @@ class ElasticTrainer:
         if writer != pid or begin != done:
             self.events.emit("hbm_resume_refused", begin=begin, done=done, writer=writer, adopted_from=pid)
             return None
+        # every tensor of the training state must be the dead worker's: one that was not
+        # exported, not mapped or not taken (size / dtype / layout changed) holds init values
+        from easydl_amd.ckpt.manager import CheckpointManager
+        need = CheckpointManager.state_of(self) + [(f"model.{g.name}", g.data) for g in self.flat.groups]
+        miss = vram.missing(need)
+        if miss:
+            self.events.emit("hbm_resume_refused", reason="incomplete", missing=miss[:8], n_missing=len(miss),
+                             of=len(need), begin=begin, done=done)
+            return None
         return done
 
-    def _maybe_restore(self):
-        if self.checkpoint is None:
-            return
+    def _maybe_restore(self) -> bool:
+        """State of a process that holds none: the dead worker's HBM (HBM resume), else the
+        newest snapshot.  With neither, buffers adopted from a dead worker are reset to this
+        process's seeded init (a fresh start).  True if trained state was recovered."""
         t0 = time.perf_counter()
-        k = self._hbm_resume_step()
-        if k is not None:
-            from easydl_amd.utils import vram
-            pid = vram.ADOPTED_FROM.get("pid")
-            verify = None if vram.reaped(pid) else {"pid": pid, "marks": (k, k), "job": self.ctx.job,
-                                                    "slot": f"{self.ctx.role}{self.ctx.index}"}
-            src = self.checkpoint.resume_from_hbm(self, k, verify)
-            self.events.emit("restored", step=self.step, source=src, s=round(time.perf_counter() - t0, 3))
+        if self.checkpoint is not None:
+            k = self._hbm_resume_step()
+            if k is not None:
+                from easydl_amd.utils import vram
+                pid = vram.ADOPTED_FROM.get("pid")
+                verify = None if vram.reaped(pid) else {"pid": pid, "marks": (k, k), "job": self.ctx.job,
+                                                        "slot": f"{self.ctx.role}{self.ctx.index}"}
+                src = self.checkpoint.resume_from_hbm(self, k, verify)
+                self.events.emit("restored", step=self.step, source=src, s=round(time.perf_counter() - t0, 3))
+                return True
+            st = self.checkpoint.restore_latest(self)
+            if st is not None:
+                from easydl_amd.ckpt import manager as _ckm
+                self.events.emit("restored", step=self.step, source=st, s=round(time.perf_counter() - t0, 3),
+                                 h2d=dict(_ckm.LAST_RESTORE_STATS))
+                return True
+        self._reinit_adopted()
+        return False
+
+    def _reinit_adopted(self) -> None:
+        """Nothing overwrites this process's state: buffers it built on a dead worker's HBM
+        (kept for an HBM resume that did not happen) go back to the seeded init."""
+        from easydl_amd.utils import vram
+        if not vram.adopted_any() or self.flat is None:
             return
-        st = self.checkpoint.restore_latest(self)
-        if st is not None:
-            from easydl_amd.ckpt import manager as _ckm
-            self.events.emit("restored", step=self.step, source=st, s=round(time.perf_counter() - t0, 3),
-                             h2d=dict(_ckm.LAST_RESTORE_STATS))
+        n = self.flat.reinit_adopted() + (self.bufs.reinit_adopted() if self.bufs is not None else 0)
+        self.opt.reset_state()
+        if self.device.type == "cuda":
+            torch.cuda.current_stream(self.device).synchronize()
+        self.events.emit("adopted_reinit", tensors=n)
+
+    def _state_settled(self) -> None:
+        if self.flat is not None:
+            self.flat.drop_init_copies()
+        if self.bufs is not None:
+            self.bufs.drop_init_copies()
 
     # ------------------------------------------------------------------ steps
     def _micro_batches(self, data, plan: ElasticBatchPlan):
@@ -741,7 +799,7 @@ class ElasticTrainer:
                 import cProfile         # diagnostics: host profile of this process's first step
                 prof = cProfile.Profile()
                 prof.enable()
-            while self.step < num_steps:
+            while self.step < num_steps and not self._stop_requested:
                 if prof is not None and self.history:
                     prof.disable()
                     self._dump_profile(prof)
@@ -783,6 +841,7 @@ class ElasticTrainer:
                                           if self.device.type == "cuda" else None)
                     with trace.range("optimizer"):
                         self.opt.step(pre_scale=1.0)
+                    self.fault.maybe_inject("in_update", self.step, trainer=self)
                     self._sync_buffers()
                     if self._marks is not None:
                         self._marks.done(self.step + 1, torch.cuda.current_stream(self.device)
@@ -819,7 +878,7 @@ class ElasticTrainer:
                 if self.rdzv is not None and self.rdzv.plan_version != self.plan_version:
                     self._apply_runtime_plan(self.rdzv.plan_version)
                 need_new = (not ok) or self.comm.aborted or (self.rdzv is not None and latest > self.comm.epoch)
-                if need_new and self.step < num_steps:
+                if need_new and self.step < num_steps and not self._stop_requested:
                     try:
                         self._reconfigure()
                     except JobFinished:

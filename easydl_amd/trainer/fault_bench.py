@@ -17,7 +17,21 @@ processes when no GPU is visible):
 
 TTR = wall time from the ``fault_injected`` event to the first committed step
 after it; the breakdown (detect / abort / new epoch / comm ready / state sync
-/ first step) comes from the merged event timeline.  Prints one JSON line.
+/ first step) comes from the merged event timeline.  ``time_to_regain_s`` is
+the time until the job holds its pre-fault committed step count again.  Prints
+one JSON line.
+
+Where the kill lands (``--fault-mode``, utils/fault.py):
+
+* ``midstep`` (default): 40 % into a step (``after_ms``), once the hot standby
+  has warmed up -- a failure at an arbitrary moment, with that step's GPU work
+  in flight;
+* ``in_update``: inside an optimizer update (after its ``begin`` step mark), so
+  the dead worker's HBM is torn and the state comes back from /dev/shm;
+* ``step_start``: at the host's start of step ``--fault-step`` (round-1..4 form).
+
+After the fault every process trains ``EDL_BENCH_AFTER`` (default 3) more steps
+past the fault step and the job ends.
 """
 from __future__ import annotations
 
@@ -54,11 +68,25 @@ def main(args) -> int:
     unlink_job_segments(job_name)
     steps = args.warmup + args.steps
     fault_step = getattr(args, "fault_step", None) or max(2, args.warmup + 1)
+    mode = getattr(args, "fault_mode", None) or "step_start"
+    standby = getattr(args, "standby", 0)
+    spec = f"kill@step={fault_step},index={n - 1}"
+    if mode == "midstep":
+        # 40 % into the step at its steady length (EDL_FAULT_STEP_MS: the caller's measured
+        # step time; else a guess from the model), so the step's GPU work is in flight
+        spec += f",after_ms={int(float(os.environ.get('EDL_FAULT_STEP_MS', 1000)) * 0.4)}"
+    elif mode == "in_update":
+        spec += ",point=in_update"
+    if standby and mode != "step_start":
+        spec += ",wait=standby"   # a real failure finds the spare parked and warmed up
     env = {
         "EDL_BENCH_MODEL": args.model, "EDL_BENCH_SEQ": str(args.seq), "EDL_BENCH_MBS": str(args.mbs),
-        "EDL_BENCH_ACCUM": str(args.accum), "EDL_BENCH_STEPS": str(steps),
+        "EDL_BENCH_ACCUM": str(args.accum),
+        # step_start keeps the fixed step count; the other modes end a few steps after the fault
+        "EDL_BENCH_STEPS": str(steps if mode == "step_start" else fault_step + 60),
+        "EDL_BENCH_AFTER": os.environ.get("EDL_BENCH_AFTER", "3" if mode != "step_start" else "0"),
         "EDL_BENCH_CKPT": str(getattr(args, "ckpt_interval", 0) or 2),
-        "EDL_FAULT": f"kill@step={fault_step},index={n - 1}",
+        "EDL_FAULT": spec,
         "EDL_PLANNED_WORKERS": str(n),
     }
     if args.layers:
@@ -81,15 +109,25 @@ def main(args) -> int:
     ttr = ttr_breakdown(ev)
     worlds = [e.get("world") for e in ev if e["kind"] == "step_done"]
     restored = [e for e in ev if e["kind"] == "restored"]
+    fault = next((e for e in ev if e["kind"] == "fault_injected"), None)
+    done_ts = [e["ts"] for e in ev if e["kind"] == "step_done" and (fault is None or e["ts"] < fault["ts"])]
+    gaps = sorted(b - a for a, b in zip(done_ts, done_ts[1:]))[-8:]   # the last steps before the fault
     out = {
         "metric": "time-to-recover after SIGKILL of one worker (Llama elastic DDP, local operator)",
         "value": None if not ttr else ttr["ttr_s"], "unit": "s", "higher_is_better": False,
         "n_gpus": (1 if share else n) if gpus else 0,
         "model": (args.model if not args.layers else f"{args.model}-L{args.layers}") if gpus else "llama-tiny (CPU)",
-        "breakdown": ttr, "operator_rc": rc, "hot_standby": getattr(args, "standby", 0),
+        "config": {"seq_len": args.seq if gpus else 64, "micro_batch": args.mbs, "grad_accum": args.accum,
+                   "ckpt_interval": int(env["EDL_BENCH_CKPT"])},
+        "fault": {"mode": mode, "spec": spec, "step": fault.get("step") if fault else None},
+        "breakdown": ttr, "operator_rc": rc, "hot_standby": standby,
+        "time_to_regain_s": ttr.get("time_to_regain_s") if ttr else None,
+        "steps_lost": ttr.get("steps_lost") if ttr else None,
+        "step_s_before_fault": round(gaps[len(gaps) // 2], 4) if gaps else None,
         "shared_gpu": share, "comm": env.get("EDL_COMM", "pg"), "workers": n,
         "replacement_from_standby": any(e["kind"] == "spawn" and e.get("standby") for e in ev),
         "restored_from": restored[0].get("source") if restored else None,
+        "hbm_resume_refused": any(e["kind"] == "hbm_resume_refused" for e in ev),
         "worlds_seen": sorted({w for w in worlds if w}), "run_dir": run_dir,
     }
     print(json.dumps(out), flush=True)
@@ -121,7 +159,17 @@ def worker() -> None:
                         global_batch=None, micro_batch=mbs, checkpoint=ckpt)
     # global batch: the planned world x mbs x accum, fixed across resizes (accumulation absorbs it)
     tr.global_batch = mbs * accum * max(1, int(e.get("EDL_PLANNED_WORKERS", 1)))
-    tr.fit(lambda m, b: m(*b), SyntheticTokens(cfg.vocab_size, seq), num_steps=int(e.get("EDL_BENCH_STEPS", 10)))
+    after = int(e.get("EDL_BENCH_AFTER", 0))
+
+    def on_step(t, _loss):
+        # every rank reads the same store key at the same committed step: they stop together
+        if after > 0 and getattr(t, "kv", None) is not None:
+            fired = t.kv.get_str("fault/fired_step")
+            if fired is not None and t.step >= int(fired) + after:
+                t.request_stop()
+
+    tr.fit(lambda m, b: m(*b), SyntheticTokens(cfg.vocab_size, seq), num_steps=int(e.get("EDL_BENCH_STEPS", 10)),
+           on_step=on_step)
     tr.close()
     ckpt.close()
 

@@ -101,4 +101,12 @@ def ttr_breakdown(events: list[dict]) -> dict | None:
     out["deferred_probe_s"] = rel(deferred)
     out["policy_cached"] = any(e["kind"] == "allreduce_probe" and e.get("cached") for e in in_window)
     out["ttr_s"] = out["first_step_s"]
+    # time to regain: the job holds the pre-fault committed step count again (an HBM resume
+    # or a survivor's state: at state sync; a snapshot restore: once the lost steps are redone)
+    regain = next((e for e in after if in_new(e) and (
+        (e["kind"] == "state_synced" and int(e.get("step", -1)) >= last_before)
+        or (e["kind"] == "step_done" and int(e.get("step", 0)) >= last_before))), None)
+    out["time_to_regain_s"] = rel(regain)
+    out["steps_before_fault"] = last_before
+    out["fault_point"] = fault.get("point")
     return out

@@ -6,16 +6,24 @@
     nan@step=2                   poison the gradients after backward (non-finite skip path)
     delay@step=2,ms=500          sleep before the step (straggler)
     raise@step=6                 raise RuntimeError inside the step
+    kill@step=4,after_ms=1500    SIGKILL 1.5 s after step 4 starts (mid-step on the GPU)
+    kill@step=4,wait=standby     first step >= 4 once the hot standby on this GPU has
+                                 warmed up (``standby/warm_gpu/<gpu>``), at most 30 steps late
+    kill@step=6,point=in_update  SIGKILL inside the optimizer update of step 6: after its
+                                 ``begin`` step mark reached the GPU, before ``done``
 
 Several specs may be joined with ``;``.  ``point`` is ``step_start`` unless the
-spec says ``point=after_backward`` (``nan`` defaults to after_backward).
-Every fired fault emits a ``fault_injected`` event (wall-clock t0 of TTR).
+spec says ``point=after_backward`` / ``point=in_update`` (``nan`` defaults to
+after_backward).  Every fired fault emits a ``fault_injected`` event (wall-clock
+t0 of TTR): for a delayed fault (``after_ms``) the event is written right before
+the signal, so TTR starts at the kill itself.
 """
 from __future__ import annotations
 
 import os
 import signal
 import sys
+import threading
 import time
 
 
@@ -28,6 +36,9 @@ class FaultSpec:
         self.ms = float(args.get("ms", 0))
         self.point = args.get("point", "after_backward" if kind == "nan" else "step_start")
         self.generation = int(args.get("gen", 0))   # only this incarnation fires (replacements do not)
+        self.after_ms = float(args.get("after_ms", 0))
+        self.wait = args.get("wait")               # "standby": hold off until the spare is warm
+        self.max_late = int(args.get("max_late", 30))
         self.fired = False
 
     @classmethod
@@ -59,7 +70,9 @@ class FaultInjector:
 
     def maybe_inject(self, point: str, step: int, trainer=None) -> None:
         for s in self.specs:
-            if s.fired or s.point != point or s.step != step:
+            if s.fired or s.point != point:
+                continue
+            if s.step != step and not (s.wait and s.step <= step):
                 continue
             if s.index is not None and s.index != self.index:
                 continue
@@ -67,10 +80,54 @@ class FaultInjector:
                 continue
             if s.generation != self.generation:
                 continue
+            if s.wait and step < s.step + s.max_late and not self._condition(s, trainer):
+                continue
             s.fired = True
-            if self.events is not None:
-                self.events.emit("fault_injected", fault=s.kind, step=step, index=self.index)
+            if s.after_ms > 0:
+                # the step runs on; the signal lands mid-step (GPU work of this step in flight)
+                threading.Thread(target=self._delayed, args=(s, step, trainer), name="edl-fault",
+                                 daemon=True).start()
+                continue
+            if point == "in_update" and trainer is not None and getattr(trainer, "device", None) is not None \
+                    and trainer.device.type == "cuda":
+                # the update's ``begin`` mark is written in stream order: make sure it landed, so
+                # the kill is inside the update as far as the step marks can tell
+                import torch
+                torch.cuda.current_stream(trainer.device).synchronize()
+            self._emit(s, step, trainer)
             self._fire(s, trainer)
+
+    def _emit(self, s: FaultSpec, step: int, trainer=None) -> None:
+        if self.events is not None:
+            self.events.emit("fault_injected", fault=s.kind, step=step, index=self.index, point=s.point,
+                             after_ms=s.after_ms or None)
+        kv = getattr(trainer, "kv", None)
+        if kv is not None:
+            try:   # drills stop a fixed number of steps after the fault (trainer/fault_bench.py)
+                kv.set("fault/fired_step", str(step))
+            except Exception:  # noqa: BLE001
+                pass
+
+    def _delayed(self, s: FaultSpec, step: int, trainer) -> None:
+        time.sleep(s.after_ms / 1000.0)
+        self._emit(s, step, trainer)
+        self._fire(s, trainer)
+
+    @staticmethod
+    def _condition(s: FaultSpec, trainer) -> bool:
+        """``wait=standby``: the hot standby that would replace this process is ready
+        (GPU jobs: it has run its warm-up on this process's GPU)."""
+        if s.wait != "standby":
+            return True
+        kv = getattr(trainer, "kv", None)
+        if kv is None:
+            return True
+        dev = getattr(trainer, "device", None)
+        where = str(dev.index if dev is not None and dev.type == "cuda" else "cpu")
+        try:
+            return kv.exists(f"standby/warm_gpu/{where}") or kv.exists("standby/warm_gpu/any")
+        except Exception:  # noqa: BLE001 - store unreachable: do not hold the fault back forever
+            return True
 
     def _fire(self, s: FaultSpec, trainer):
         if s.kind == "kill":

@@ -37,6 +37,7 @@ IPC_MAX_BYTES = 2040 << 20       # largest allocation hipIpcOpenMemHandle maps h
 GROUP_MAX_MB = 960               # flat-group cap (bf16) under hand-over: fp32 state < 2 GiB
 
 _ADOPTED: dict[str, torch.Tensor] = {}
+TAKEN: dict[str, int] = {}       # name -> data_ptr of every adopted tensor a buffer was built on
 STATS = {"exported": 0, "adopted": 0, "adopted_bytes": 0}
 
 
@@ -153,6 +154,7 @@ def adopt(tensors: dict[str, torch.Tensor], pid=None) -> None:
     """Takeover: these imported tensors back the next FlatParams / optimizer built here."""
     _ADOPTED.clear()
     _ADOPTED.update(tensors)
+    TAKEN.clear()
     ADOPTED_FROM.clear()
     if pid is not None:
         ADOPTED_FROM["pid"] = int(pid)
@@ -175,9 +177,25 @@ def take(name: str, numel: int, dtype: torch.dtype, device, keep: bool = False) 
         t.zero_()
     STATS["adopted"] += 1
     STATS["adopted_bytes"] += t.numel() * t.element_size()
+    TAKEN[name] = t.data_ptr()
     return t
 
 
-def release_unused() -> None:
-    """Drop adopted tensors nothing took (their memory goes back to the driver)."""
+def adopted_any() -> bool:
+    """True if some buffer of this process was built on a dead worker's HBM."""
+    return bool(TAKEN)
+
+
+def missing(tensors) -> list[str]:
+    """Names of ``(name, tensor)`` pairs whose storage is NOT an adopted buffer."""
+    ptrs = set(TAKEN.values())
+    return [n for n, t in tensors if t.data_ptr() not in ptrs]
+
+
+def release_unused() -> list[str]:
+    """Drop adopted tensors nothing took (their memory goes back to the driver); returns their
+    names (a name or size mismatch, e.g. another gradient dtype, or an optimizer without
+    that state)."""
+    names = sorted(_ADOPTED)
     _ADOPTED.clear()
+    return names

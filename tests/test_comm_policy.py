@@ -53,7 +53,7 @@ class FakeEngine:
     def __init__(self, comm, delay, broken=False):
         self.c, self.delay, self.broken = comm, delay, broken
         self.timeout_s = 60.0
-        self.registered, self.closed, self.calls = [], False, 0
+        self.registered, self.closed, self.calls, self.gate_calls = [], False, 0, 0
 
     def register(self, t):
         self.registered.append(t)
@@ -69,6 +69,12 @@ class FakeEngine:
         return True
 
     def all_reduce(self, t, algo=None):
+        if t.numel() == Communicator.GATE_ELEMS:   # exactness gate of an adopted policy: a real sum
+            self.gate_calls += 1
+            self.c.data.allreduce([t]).wait()
+            if self.broken:
+                t.add_(1)
+            return t
         if not self.calls:   # the exactness check: a real sum (then only the timing matters)
             self.c.data.allreduce([t]).wait()
             if self.broken:
@@ -234,13 +240,34 @@ def test_policy_cache_skips_the_probe_on_reformation():
         eng2 = FakeEngine(c, lambda nb: 1.0)        # would flip the decision if it were timed
         c.xgmi, c.xgmi_mode, c.probe_mode, c.epoch = eng2, "auto", "defer", 2
         c._select_policy()
-        return first, dict(c.xgmi_probe), eng2.calls, c.xgmi_mode, c.probe_pending
+        return first, dict(c.xgmi_probe), eng2.calls, eng2.gate_calls, c.xgmi_mode, c.probe_pending
 
-    for first, second, calls, mode, pending in _spawn(2, fn).values():
+    for first, second, calls, gates, mode, pending in _spawn(2, fn).values():
         assert first["selected"] == "xgmi" and not first.get("cached")
         assert second["cached"] and second["measured_epoch"] == 1 and second["epoch"] == 2
-        assert calls == 0 and mode == "xgmi" and not pending
+        # no timing, but this epoch's engine passed the exactness gate (two-shot + one-shot)
+        assert calls == 0 and gates == 2 and second["gate_exact"] is True
+        assert mode == "xgmi" and not pending
         assert second["policy"] == first["policy"]
+
+
+def test_cached_policy_is_refused_when_the_new_engine_is_not_exact():
+    """A re-formed epoch whose engine mis-sums (e.g. a broken peer mapping) must not route
+    gradients to it on the strength of an earlier epoch's cached verdict."""
+    def fn(c, st):
+        eng = FakeEngine(c, lambda nb: 0.0 if nb > (3 << 20) else 0.05)
+        c.xgmi, c.xgmi_mode = eng, "auto"
+        c.PROBE_KB = (2048, 4096, 8192)
+        c._select_policy()
+        c.barrier()
+        eng2 = FakeEngine(c, lambda nb: 0.0, broken=c.rank == 1)   # only rank 1's sums are off
+        c.xgmi, c.xgmi_mode, c.probe_mode, c.epoch = eng2, "auto", "defer", 2
+        c._select_policy()
+        return dict(c.xgmi_probe), c.xgmi_mode, eng2.closed
+
+    for probe, mode, closed in _spawn(2, fn).values():
+        assert probe["cached"] and probe["gate_exact"] is False
+        assert probe["selected"] == "rccl" and mode is None and closed
 
 
 def test_deferred_probe_runs_after_the_first_commit_only():

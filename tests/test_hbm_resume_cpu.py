@@ -1,0 +1,174 @@
+"""HBM resume / adopted-buffer semantics on the CPU tier (both findings).
+
+A hot standby builds its flat buffers on the dead worker's memory (utils/vram.py ``take``
+with ``keep=True``).  Two guarantees:
+
+* the HBM resume is allowed only when EVERY state tensor -- weights, fp32 master, AdamW
+  moments and the module buffers (BatchNorm running statistics) -- was adopted; otherwise the
+  process restores a snapshot instead;
+* when nothing overwrites the adopted buffers (no HBM resume, no snapshot, no state
+  transfer), they are reset to this process's seeded init: the state equals a fresh start.
+
+The buffers here are CPU tensors standing in for IPC-mapped HBM; the step-mark read is
+patched to report a worker that died between two updates."""
+import subprocess
+
+import torch
+
+from easydl_amd.ckpt.manager import CheckpointManager, unlink_job_segments
+from easydl_amd.trainer.context import TrainerContext
+from easydl_amd.trainer.elastic import ElasticTrainer
+from easydl_amd.utils import stepmarks, vram
+
+
+class _BNNet(torch.nn.Module):
+    def __init__(self, device=None):
+        super().__init__()
+        self.conv = torch.nn.Conv2d(3, 8, 3, padding=1, device=device)
+        self.bn = torch.nn.BatchNorm2d(8, device=device)
+        self.fc = torch.nn.Linear(8, 5, device=device)
+
+    def forward(self, x, y):
+        h = torch.relu(self.bn(self.conv(x))).mean((2, 3))
+        return torch.nn.functional.cross_entropy(self.fc(h), y)
+
+
+class _Images:
+    def __len__(self):
+        return 4096
+
+    def batch(self, idx, device="cpu"):
+        idx = list(idx)
+        g = torch.Generator().manual_seed(int(idx[0]))
+        return torch.randn(len(idx), 3, 6, 6, generator=g) * 3 + 1, torch.tensor([i % 5 for i in idx])
+
+
+JOB = "hbmres"
+
+
+def _mk(tmp_path, seed, ckpt=None, sub="a"):
+    ctx = TrainerContext(job=JOB, run_dir=str(tmp_path / sub))
+    return ElasticTrainer(lambda d: _BNNet(d), global_batch=8, micro_batch=4, lr=1e-2, device="cpu", ctx=ctx,
+                          checkpoint=ckpt, seed=seed)
+
+
+def _state(t):
+    out = {f"data.{g.name}": g.data.clone() for g in t.flat.groups}
+    out.update({k: v.clone() for k, v in t.opt.state_tensors().items()})
+    out.update({f"buf.{k}": v.clone() for k, v in t.bufs.tensors.items()})
+    return out
+
+
+def _dead_pid() -> int:
+    p = subprocess.Popen(["true"])
+    p.wait()
+    return p.pid
+
+
+def _died_worker(tmp_path, steps=3):
+    """A worker trained ``steps`` steps; its buffers copied (the 'dead worker's HBM')."""
+    a = _mk(tmp_path, 1, sub="dead")
+    a.fit(lambda m, b: m(*b), _Images(), num_steps=steps)
+    return a, {k: t.clone() for k, t in a.vram_state_tensors().items()}
+
+
+def _marks(monkeypatch, k, pid):
+    monkeypatch.setattr(stepmarks, "read_slot", lambda job, slot: (k, k, pid))
+
+
+def test_hbm_resume_adopts_every_state_tensor_including_batchnorm_buffers(tmp_path, monkeypatch):
+    unlink_job_segments(JOB)
+    dead, exported = _died_worker(tmp_path)
+    assert {"bufs/float32", "bufs/int64"} <= set(exported)     # running stats + num_batches_tracked
+    pid = _dead_pid()
+    _marks(monkeypatch, 3, pid)
+    vram.adopt(exported, pid=pid)
+    ck = CheckpointManager(JOB, interval=100)
+    try:
+        b = _mk(tmp_path, 5, ck, sub="b")
+        b.fit(lambda m, x: m(*x), _Images(), num_steps=3)   # resumes at 3: no step left to run
+        ev = [r for r in b.events.records if r["kind"] in ("restored", "hbm_resume_refused", "adopted_reinit")]
+        assert [r["kind"] for r in ev] == ["restored"] and ev[0]["source"] == "hbm:step3", ev
+        assert b.step == 3
+        got, want = _state(b), _state(dead)
+        assert set(got) == set(want)
+        for k in want:
+            assert torch.equal(got[k], want[k]), k
+        assert int(b.model.bn.num_batches_tracked) == int(dead.model.bn.num_batches_tracked) == 6
+    finally:
+        ck.close()
+        unlink_job_segments(JOB)
+        vram.adopt({})
+
+
+def test_hbm_resume_refused_when_a_state_tensor_was_not_adopted(tmp_path, monkeypatch):
+    """The running statistics were not exported: no HBM resume (it would pair the dead
+    worker's weights with init statistics); no snapshot either, so a fresh seeded start."""
+    unlink_job_segments(JOB)
+    _, exported = _died_worker(tmp_path)
+    del exported["bufs/float32"]
+    pid = _dead_pid()
+    _marks(monkeypatch, 3, pid)
+    vram.adopt(exported, pid=pid)
+    ck = CheckpointManager(JOB, interval=100)
+    try:
+        b = _mk(tmp_path, 5, ck, sub="b")
+        b.fit(lambda m, x: m(*x), _Images(), num_steps=0)
+        kinds = [r for r in b.events.records if r["kind"] in ("restored", "hbm_resume_refused", "adopted_reinit")]
+        assert kinds[0]["kind"] == "hbm_resume_refused" and kinds[0]["reason"] == "incomplete"
+        assert kinds[0]["missing"] == ["model.buffers.float32"]
+        assert kinds[-1]["kind"] == "adopted_reinit" and b.step == 0
+        vram.adopt({})
+        fresh = _mk(tmp_path, 5, sub="c")
+        got, want = _state(b), _state(fresh)
+        for k in want:
+            assert torch.equal(got[k], want[k]), k
+        assert b.opt.step_count == 0 and b.opt.moment_origin == 0
+    finally:
+        ck.close()
+        unlink_job_segments(JOB)
+        vram.adopt({})
+
+
+def test_adopted_buffers_without_resume_or_snapshot_equal_a_fresh_start(tmp_path, monkeypatch):
+    """Marks refused (the worker died inside an update) and no checkpoint manager at all: the
+    torn weights and non-zero moments must not survive into training."""
+    _, exported = _died_worker(tmp_path)
+    pid = _dead_pid()
+    monkeypatch.setattr(stepmarks, "read_slot", lambda job, slot: (4, 3, pid))   # begin != done
+    vram.adopt(exported, pid=pid)
+    try:
+        b = _mk(tmp_path, 5, None, sub="b")
+        assert vram.adopted_any()
+        b.fit(lambda m, x: m(*x), _Images(), num_steps=0)
+        vram.adopt({})
+        fresh = _mk(tmp_path, 5, sub="c")
+        got, want = _state(b), _state(fresh)
+        for k in want:
+            assert torch.equal(got[k], want[k]), k
+        # and training from there matches the fresh process step for step
+        b.fit(lambda m, x: m(*x), _Images(), num_steps=2)
+        fresh.fit(lambda m, x: m(*x), _Images(), num_steps=2)
+        got, want = _state(b), _state(fresh)
+        for k in want:
+            assert torch.equal(got[k], want[k]), k
+    finally:
+        vram.adopt({})
+
+
+def test_unused_adopted_buffers_are_released(tmp_path):
+    """Adopted tensors that no buffer asks for (here: the momentum buffer of an SGD worker,
+    adopted by an AdamW process) are dropped right after the model is built, not kept mapped
+    for the life of the process; a size / dtype mismatch is dropped at the ``take``."""
+    _, exported = _died_worker(tmp_path)
+    g = next(k for k in exported if k.endswith("/grad"))
+    exported[g] = exported[g].double()
+    exported["opt/decay/mom"] = torch.zeros(4)
+    vram.adopt(exported, pid=_dead_pid())
+    try:
+        b = _mk(tmp_path, 5, None, sub="b")
+        built = next(r for r in b.events.records if r["kind"] == "model_built")
+        assert built["adopted_unused"] == 1
+        assert not vram._ADOPTED
+    finally:
+        vram.adopt({})
