@@ -1014,5 +1014,5 @@ def unlink_job_segments(job: str) -> int:
 
 
 def _comm_error(e: Exception) -> bool:
-    s = str(e).lower()
-    return any(k in s for k in ("nccl", "rccl", "gloo", "connection", "socket", "peer", "aborted", "timed out"))
+    from easydl_amd.parallel.errors import is_comm_error
+    return is_comm_error(e)

@@ -43,6 +43,10 @@ class XgmiError(RuntimeError):
     pass
 
 
+class XgmiAborted(XgmiError):
+    """The engine was aborted (abort word set: a peer of this epoch is gone)."""
+
+
 class _Work:
     def __init__(self, event: torch.cuda.Event, keep):
         self._event, self._keep = event, keep
@@ -305,7 +309,7 @@ class XgmiComm:
 
     def _all_reduce(self, t: torch.Tensor, algo: str | None = None, max_blocks: int | None = None) -> torch.Tensor:
         if self._aborted:
-            raise XgmiError("aborted")
+            raise XgmiAborted("aborted")
         if not self.supports(t):
             raise XgmiError("xGMI all-reduce takes contiguous fp32 / bf16 tensors of 16-byte multiples")
         max_blocks = max_blocks or self.blocks
@@ -356,7 +360,7 @@ class XgmiComm:
 
     def _check(self, *ts):
         if self._aborted:
-            raise XgmiError("aborted")
+            raise XgmiAborted("aborted")
         for t in ts:
             if not self.supports(t):
                 raise XgmiError("xGMI collectives take contiguous fp32 / bf16 tensors of 16-byte multiples")

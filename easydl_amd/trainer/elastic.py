@@ -138,6 +138,9 @@ class ElasticTrainer:
             path=os.path.join(self.ctx.run_dir, f"metrics-{self.ctx.role}{self.ctx.index}.jsonl"))
         self.plan_version = 0
         self._stop_requested = False
+        self._master_lost: str | None = None    # set by the watchdog (see _start_watchdog)
+        self._mb_split = 1           # >1: micro-batches split while a takeover waits for HBM (_memory_plan)
+        self._act_need = 0
 
     def request_stop(self) -> None:
         """End ``fit`` after the current step (from ``on_step``).  Every rank must ask at the
@@ -239,17 +242,42 @@ class ElasticTrainer:
         self.events.emit("prejoin_warmup", s=round(time.perf_counter() - t0, 4))
 
     def _start_watchdog(self):
+        """Abort the epoch's communicators as soon as the master flags the epoch broken.  A
+        store that stays unreachable for ``EDL_MASTER_TIMEOUT_S`` (default 60 s) means the job
+        master is gone: the epoch is aborted too (no collective waits forever) and the step
+        loop raises :class:`MasterUnreachable` instead of re-forming (there is nobody to
+        re-form with); the operator then replaces the whole job's processes."""
+        limit = float(os.environ.get("EDL_MASTER_TIMEOUT_S", 60))
+
         def loop():
+            first_fail = None
             while not self._stop.wait(0.01):
                 c = self.comm
-                if c is None or c.aborted or self.rdzv is None:
+                if c is None or self.rdzv is None:
+                    continue
+                if c.aborted and first_fail is None:
                     continue
                 try:
                     if self.rdzv.aborted(c.epoch):
                         self.events.emit("abort_seen", epoch=c.epoch)
                         c.abort()
-                except Exception:
-                    pass
+                    if first_fail is not None:
+                        self.events.emit("store_reachable", after_s=round(time.monotonic() - first_fail, 3))
+                    first_fail = None
+                except Exception as e:  # noqa: BLE001 - classified below, never swallowed for good
+                    now = time.monotonic()
+                    if first_fail is None:
+                        first_fail = now
+                        self.events.emit("store_unreachable", error=f"{type(e).__name__}: {e}"[:200])
+                    elif now - first_fail > limit and self._master_lost is None:
+                        self._master_lost = f"{type(e).__name__}: {e}"[:300]
+                        self.events.emit("master_lost", after_s=round(now - first_fail, 3), error=self._master_lost)
+                        log.error("job master store unreachable for %.0f s: %s", now - first_fail, e)
+                        try:
+                            c.abort()
+                        except Exception:  # noqa: BLE001
+                            pass
+                        return
 
         self._watchdog = threading.Thread(target=loop, name="edl-watchdog", daemon=True)
         self._watchdog.start()
@@ -313,7 +341,13 @@ class ElasticTrainer:
             # them to the xGMI engine)
             self.ddp.set_comm(self.dp_comm)
             xg = getattr(self.dp_comm, "xgmi", None)
-            self.events.emit("state_synced", epoch=self.comm.epoch, step=self.step,
+            mem = {}
+            if self.device.type == "cuda":
+                free, total = torch.cuda.mem_get_info(self.device)
+                mem = {"gpu_free_gb": round(free / 2**30, 1), "reserved_gb":
+                       round(torch.cuda.memory_reserved(self.device) / 2**30, 1)}
+            self._memory_plan()
+            self.events.emit("state_synced", epoch=self.comm.epoch, step=self.step, **mem,
                              grad_buffers_mapped=len(getattr(xg, "_registered", ())) if xg is not None else 0,
                              probe_pending=[g for g, c in self._comm_groups() if getattr(c, "probe_pending", False)])
             return
@@ -593,6 +627,55 @@ class ElasticTrainer:
             cfg["n_layers"] = 1
             spec = {"model": "llama", "cfg": cfg, "batch": [self.micro_batch, int(seq)]}
         vram.publish_warm(self.kv, f"{self.ctx.role}{self.ctx.index}", spec)
+        # HBM a step needs beyond the persistent state (activations, workspaces): a replacement
+        # that adopts the state checks it against what the GPU has free (_memory_plan)
+        persistent = sum(t.untyped_storage().nbytes() for t in self.vram_state_tensors().values())
+        act = max(0, torch.cuda.max_memory_reserved(self.device) - persistent)
+        vram.publish_act(self.kv, f"{self.ctx.role}{self.ctx.index}", act, self.micro_batch)
+
+    def _hbm_avail(self) -> int:
+        free, _ = torch.cuda.mem_get_info(self.device)
+        return free + torch.cuda.memory_reserved(self.device) - torch.cuda.memory_allocated(self.device)
+
+    def _memory_plan(self) -> None:
+        """A replacement that adopted a dead worker's HBM starts while the driver is still
+        reclaiming the rest of that worker's memory (its activations: ~82 GB for Llama-3-8B at
+        2 x 8k tokens per micro-batch).  A first step that needs more than the GPU has free
+        blocks inside hipMalloc until the reclaim is done -- 6 s of an 8 s time-to-recover
+        (profiles/r05_ttr_headline.md).  Instead, while memory is short, each micro-batch is
+        split into smaller ones: the same samples, the same loss weights, the same gradient sum
+        (only the order of the bf16 additions differs), at roughly half the activation memory.
+        Checked again before every step; full micro-batches return once the memory is back."""
+        from easydl_amd.utils import vram
+        self._mb_split = 1
+        if (self.device.type != "cuda" or self.tp > 1 or not vram.adopted_any() or self.micro_batch <= 1
+                or getattr(self, "kv", None) is None or os.environ.get("EDL_RECOVERY_SPLIT", "1") == "0"):
+            return
+        need, mbs = vram.read_act(self.kv, f"{self.ctx.role}{self.ctx.index}")
+        if not need or mbs != self.micro_batch:
+            return
+        self._act_need = need
+        avail = self._hbm_avail()
+        if avail >= need * 1.05:
+            return
+        k = next((d for d in range(2, mbs + 1) if mbs % d == 0 and need / d * 1.15 <= avail), mbs)
+        self._mb_split = k
+        self.events.emit("memory_limited_steps", split=k, need_gb=round(need / 2**30, 1),
+                         avail_gb=round(avail / 2**30, 1))
+
+    def _split_micro_batches(self, mbs: list) -> list:
+        if self._mb_split > 1 and self._hbm_avail() >= self._act_need * 1.05:
+            self.events.emit("memory_restored", step=self.step, avail_gb=round(self._hbm_avail() / 2**30, 1))
+            self._mb_split = 1
+        k = self._mb_split
+        if k <= 1:
+            return mbs
+        out = []
+        for idx in mbs:
+            idx = list(idx)
+            n = -(-len(idx) // k)
+            out += [idx[i:i + n] for i in range(0, len(idx), n)]
+        return out
 
     def _hbm_resume_step(self) -> int | None:
         """Step K if this process adopted a dead worker's HBM (utils/vram.py) whose step marks
@@ -720,6 +803,8 @@ class ElasticTrainer:
 
     def _run_step(self, loss_fn, data, plan):
         mbs = self._micro_batches(data, plan)
+        if self._mb_split > 1:
+            mbs = self._split_micro_batches(mbs)
         self._seed_step()
         self.flat.zero_grad()
         total = 0.0
@@ -822,6 +907,8 @@ class ElasticTrainer:
                         ok = False
                     else:
                         raise
+                if self._master_lost is not None:
+                    raise MasterUnreachable(f"job master unreachable: {self._master_lost}")
                 if self.rdzv is not None:
                     apply, latest = self.rdzv.commit(self.comm.epoch, self.step, self.comm.world_size, ok,
                                                      gc=self.comm.rank == 0)
@@ -980,6 +1067,10 @@ class ElasticTrainer:
             self.comm.shutdown()
 
 
+class MasterUnreachable(RuntimeError):
+    """The job master's store stopped answering (see ElasticTrainer._start_watchdog)."""
+
+
 class _null:
     def __enter__(self):
         return self
@@ -1042,5 +1133,5 @@ def _retire(comm, events=None) -> None:
 
 
 def _is_comm_error(e: Exception) -> bool:
-    s = str(e).lower()
-    return any(k in s for k in ("nccl", "rccl", "gloo", "connection", "socket", "peer", "aborted", "timed out"))
+    from easydl_amd.parallel.errors import is_comm_error
+    return is_comm_error(e)

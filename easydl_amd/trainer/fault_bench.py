@@ -83,7 +83,8 @@ def main(args) -> int:
         "EDL_BENCH_MODEL": args.model, "EDL_BENCH_SEQ": str(args.seq), "EDL_BENCH_MBS": str(args.mbs),
         "EDL_BENCH_ACCUM": str(args.accum),
         # step_start keeps the fixed step count; the other modes end a few steps after the fault
-        "EDL_BENCH_STEPS": str(steps if mode == "step_start" else fault_step + 60),
+        "EDL_BENCH_STEPS": str(steps if mode == "step_start" else
+                               fault_step + int(os.environ.get("EDL_BENCH_CAP", 60))),
         "EDL_BENCH_AFTER": os.environ.get("EDL_BENCH_AFTER", "3" if mode != "step_start" else "0"),
         "EDL_BENCH_CKPT": str(getattr(args, "ckpt_interval", 0) or 2),
         "EDL_FAULT": spec,
@@ -100,8 +101,11 @@ def main(args) -> int:
         env["EDL_COMM"] = args.comm
     job = ElasticJob(name=job_name, command="python -m easydl_amd.trainer.fault_bench --worker",
                      env=env, min_workers=1, max_workers=n)
+    for k in ("EDL_BENCH_UNTIL_REGROWN",):
+        if k in os.environ:
+            env[k] = os.environ[k]
     jr = JobResource(f"{job_name}-resource", job_name,
-                     {"worker": RoleResource(n, Resource(gpu=1 if gpus else 0, cpu=4))})
+                     {"worker": RoleResource(n, Resource(gpu=1 if gpus else 0, cpu=4 if gpus else 1))})
     cfg = OperatorConfig(gpus=gpus[:n], cpus=[], leave_grace_s=120.0, standby=getattr(args, "standby", 0))
     op = ElasticOperator(job, run_dir, cfg=cfg, job_resource=jr)
     rc = op.run(timeout_s=1000)
@@ -128,6 +132,8 @@ def main(args) -> int:
         "replacement_from_standby": any(e["kind"] == "spawn" and e.get("standby") for e in ev),
         "restored_from": restored[0].get("source") if restored else None,
         "hbm_resume_refused": any(e["kind"] == "hbm_resume_refused" for e in ev),
+        "final_states": [{k: e.get(k) for k in ("proc", "step", "world", "rank", "crc")}
+                         for e in ev if e["kind"] == "final_state"],
         "worlds_seen": sorted({w for w in worlds if w}), "run_dir": run_dir,
     }
     print(json.dumps(out), flush=True)
@@ -161,15 +167,30 @@ def worker() -> None:
     tr.global_batch = mbs * accum * max(1, int(e.get("EDL_PLANNED_WORKERS", 1)))
     after = int(e.get("EDL_BENCH_AFTER", 0))
 
+    planned = max(1, int(e.get("EDL_PLANNED_WORKERS", 1)))
+    regrow = e.get("EDL_BENCH_UNTIL_REGROWN", "0") == "1"
+
     def on_step(t, _loss):
         # every rank reads the same store key at the same committed step: they stop together
+        # (with EDL_BENCH_UNTIL_REGROWN=1 only once the replacement has rejoined: world size is
+        # the same on every rank of an epoch)
         if after > 0 and getattr(t, "kv", None) is not None:
             fired = t.kv.get_str("fault/fired_step")
-            if fired is not None and t.step >= int(fired) + after:
+            if fired is not None and t.step >= int(fired) + after and (
+                    not regrow or t.comm.world_size >= planned):
                 t.request_stop()
 
     tr.fit(lambda m, b: m(*b), SyntheticTokens(cfg.vocab_size, seq), num_steps=int(e.get("EDL_BENCH_STEPS", 10)),
            on_step=on_step)
+    # final state digest per rank: a drill checks every rank ended with the same parameters
+    import zlib
+    if tr.device.type == "cuda":
+        from easydl_amd.ckpt.manager import checksum_tensor
+        digest = [int(checksum_tensor(g.data).item()) for g in tr.flat.groups]
+    else:
+        digest = [zlib.crc32(g.data.detach().float().numpy().tobytes()) for g in tr.flat.groups]
+    tr.events.emit("final_state", step=tr.step, world=tr.comm.world_size if tr.comm is not None else None,
+                   rank=tr.comm.rank if tr.comm is not None else None, crc=digest)
     tr.close()
     ckpt.close()
 

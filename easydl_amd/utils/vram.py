@@ -88,6 +88,19 @@ def read_warm(kv, slot: str) -> tuple[bool, dict | None]:
     return True, json.loads(raw).get("spec")
 
 
+def publish_act(kv, slot: str, act_bytes: int, micro_batch: int) -> None:
+    """HBM one training step of ``slot`` needs beyond its persistent state."""
+    kv.set(f"vram/act/{slot}", json.dumps({"act_bytes": int(act_bytes), "micro_batch": int(micro_batch)}))
+
+
+def read_act(kv, slot: str) -> tuple[int, int]:
+    raw = kv.get_str(f"vram/act/{slot}")
+    if raw is None:
+        return 0, 0
+    d = json.loads(raw)
+    return int(d.get("act_bytes", 0)), int(d.get("micro_batch", 0))
+
+
 def slots(kv) -> list[str]:
     return sorted({s for s in (kv.get_str("vram/slots") or "").split(",") if s})
 

@@ -172,3 +172,49 @@ def test_unused_adopted_buffers_are_released(tmp_path):
         assert not vram._ADOPTED
     finally:
         vram.adopt({})
+
+
+def test_memory_limited_recovery_splits_micro_batches_with_the_same_update(tmp_path):
+    """A replacement short of HBM (the dead worker's activations not reclaimed yet) runs each
+    micro-batch as smaller ones: same samples, same weights -> the same update (up to the
+    order of the additions), then goes back to full micro-batches once memory is back."""
+    from easydl_amd.trainer.data import SyntheticTokens
+
+    class _Tok(torch.nn.Module):
+        def __init__(self, device=None):
+            super().__init__()
+            self.emb = torch.nn.Embedding(64, 32, device=device)
+            self.fc = torch.nn.Linear(32, 64, device=device)
+
+        def forward(self, ids, labels):
+            return torch.nn.functional.cross_entropy(self.fc(torch.tanh(self.emb(ids))).flatten(0, 1),
+                                                     labels.flatten())
+
+    data = SyntheticTokens(64, 16, num_samples=512)
+
+    def mk(sub):
+        ctx = TrainerContext(job="split", run_dir=str(tmp_path / sub))
+        return ElasticTrainer(lambda d: _Tok(d), global_batch=8, micro_batch=4, lr=1e-2, device="cpu", ctx=ctx,
+                              seed=3)
+
+    ref = mk("ref").fit(lambda m, b: m(*b), data, num_steps=2)
+    sp = mk("split")
+    avail = {"v": 0}
+    sp._hbm_avail = lambda: avail["v"]
+    sp._act_need = 1000
+    sp._mb_split = 2
+    sp._memory_plan = lambda: None      # (on a GPU takeover: free HBM < the published need)
+    seen = []
+    orig = sp._split_micro_batches
+
+    def spy(mbs):
+        out = orig(mbs)
+        seen.append([len(x) for x in out])
+        avail["v"] = 10_000          # the driver has reclaimed the memory after the first step
+        return out
+    sp._split_micro_batches = spy
+    sp.fit(lambda m, b: m(*b), data, num_steps=2)
+    assert seen[0] == [2, 2, 2, 2] and seen[1] == [4, 4], seen
+    assert [r["kind"] for r in sp.events.records if r["kind"] == "memory_restored"] == ["memory_restored"]
+    for a, b in zip(ref.flat.groups, sp.flat.groups):
+        assert torch.allclose(a.data, b.data, atol=1e-6, rtol=1e-5)
