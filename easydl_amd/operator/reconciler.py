@@ -116,6 +116,8 @@ class ElasticOperator:
         self.failed = False
         self._free_gpus = list(self.cfg.gpus)
         self.standbys: dict[str, Proc] = {}      # name -> parked spare
+        self._ready_seen: set[str] = set()
+        self._roster = None
         self._standby_seq = 0
         self._last_takeover = 0.0
 
@@ -287,6 +289,31 @@ class ElasticOperator:
             self.standbys[name] = Proc(name, "standby", self._standby_seq - 1, pid, None, Resource(), time.time())
             self.events.emit("standby_spawn", name=name, pid=pid)
 
+    def _publish_roster(self) -> None:
+        """``standby/roster``: the parked standbys that are ready to take over.  Workers wait for
+        their warm-up before the first step, and the fault drills for it before the kill
+        (utils/vram.py standby_warm_on); a standby that took over leaves the roster at once."""
+        if self.kv is None:
+            return
+        ready = []
+        for sname in sorted(self.standbys):
+            if sname in self._ready_seen:
+                ready.append(sname)
+                continue
+            try:
+                if self.kv.get(f"standby/ready/{sname}"):
+                    self._ready_seen.add(sname)
+                    ready.append(sname)
+            except Exception:  # noqa: BLE001 - store unreachable: keep the last roster
+                return
+        roster = ",".join(ready)
+        if roster != self._roster:
+            try:
+                self.kv.set("standby/roster", roster)
+                self._roster = roster
+            except Exception:  # noqa: BLE001
+                pass
+
     def _standby_ready(self) -> bool:
         if self.kv is None:
             return False
@@ -318,6 +345,7 @@ class ElasticOperator:
                 except OSError:
                     pass
             del self.standbys[sname]
+            self._publish_roster()
             self._last_takeover = time.time()
             p = Proc(name, role, index, sp.pid, gpu, res, time.time(), generation=generation)
             p.cpus = cpus
@@ -406,6 +434,7 @@ class ElasticOperator:
         sb = next((q for q in self.standbys.values() if q.pid == ex.pid), None)
         if sb is not None:
             del self.standbys[sb.name]
+            self._publish_roster()
             self.events.emit("standby_exit", name=sb.name, code=ex.exit_code, signal=ex.signal)
             return
         p = next((q for q in list(self.procs.values()) + self.history if q.pid == ex.pid), None)
@@ -545,6 +574,7 @@ class ElasticOperator:
         self._poll_jobresource()
         self.reconcile()
         self._maintain_standbys()
+        self._publish_roster()
         self._enforce_grace()
         if self.job_complete() and not self.done:
             self.done = True

@@ -201,9 +201,9 @@ def main() -> int:
     kv.set(f"standby/ready/{name}", json.dumps(info))
     from easydl_amd.utils import vram
     if not info.get("gpus"):
-        kv.set("standby/warm_gpu/cpu", json.dumps({"standby": name}))   # nothing to warm on a CPU host
+        kv.set(f"standby/warm/{name}/cpu", json.dumps({}))   # nothing to warm on a CPU host
     elif not vram.enabled():
-        kv.set("standby/warm_gpu/any", json.dumps({"standby": name}))   # no hand-over: nothing per GPU
+        kv.set(f"standby/warm/{name}/any", json.dumps({}))   # no hand-over: nothing per GPU
     key = f"standby/assign/{name}"
     premap = os.environ.get("EDL_STANDBY_PREMAP", "0") == "1"
     handoff = vram.enabled() and info.get("gpus", 0) > 0
@@ -219,13 +219,13 @@ def main() -> int:
             return 0
         if handoff and time.monotonic() > next_vram:
             _import_vram(kv, held)
-            next_vram = time.monotonic() + 1.0
+            next_vram = time.monotonic() + 0.25   # a worker waits for this warm-up before its first step
             for slot, h in sorted(held.items()):
                 if not h or not h.get("tensors") or h["gpu"] in warmed:
                     continue
                 if not warm_on:
                     warmed.add(h["gpu"])
-                    kv.set(f"standby/warm_gpu/{h['gpu']}", json.dumps({"standby": name, "warmup": "off"}))
+                    kv.set(f"standby/warm/{name}/gpu{h['gpu']}", json.dumps({"warmup": "off"}))
                     continue
                 published, spec = vram.read_warm(kv, slot)
                 if not published:
@@ -235,12 +235,11 @@ def main() -> int:
                     s = round(warm_device(h["gpu"], spec, set_stream=True), 3)
                     info = dict(s=s, spec=spec is not None, **WARM_INFO)
                     kv.set(f"standby/warm/{name}/gpu{h['gpu']}", json.dumps(info))
-                    kv.set(f"standby/warm_gpu/{h['gpu']}", json.dumps(dict(info, standby=name)))
                     print(f"standby {name}: warm-up on GPU {h['gpu']}: {json.dumps(info)}", file=sys.stderr,
                           flush=True)
                 except Exception as e:  # noqa: BLE001 - an optimisation only
                     print(f"standby: warm-up on GPU {h['gpu']} failed: {e}", file=sys.stderr)
-                    kv.set(f"standby/warm_gpu/{h['gpu']}", json.dumps({"standby": name, "error": str(e)[:200]}))
+                    kv.set(f"standby/warm/{name}/gpu{h['gpu']}", json.dumps({"error": str(e)[:200]}))
         if premap and time.monotonic() > next_scan:
             from easydl_amd.ckpt.manager import premap_job_segments
             mapped = premap_job_segments(job)

@@ -221,7 +221,11 @@ def cross_entropy(logits, labels, ignore_index: int = -100):
 # Llama-3-8B) and 2 B/param of HBM.  EDL_WT_CACHE=0 disables it.
 _WT_GEN = [0]
 _WT_ON = os.environ.get("EDL_WT_CACHE", "1") != "0"
-_WT_BUDGET: list = [None]   # bytes the transposed copies may still take (set at first use)
+# [bytes the transposed copies may still take, weight generation it was measured in]: measured
+# from free HBM at first use and again (once per generation) when a copy does not fit -- copies of
+# dead weights give their memory back, and a hot standby that measured it beside a live worker
+# (utils/vram.py) sees more once it has taken over
+_WT_BUDGET: list = [None, -1]
 # Batched refresh: at the first use of a new generation every stale cached copy on that device is
 # re-transposed in ONE launch (edl_transpose_bf16_multi) instead of one small launch per weight at
 # its first use (a BERT-large weight is 64-256 tiles: 9.4 us per 1024 x 1024 transpose alone).
@@ -273,16 +277,18 @@ def _wt_of(w: torch.Tensor):
         return None
     wt = getattr(w, "_edl_wt", None)
     if wt is None:
-        if getattr(w, "_edl_wt_skip", False):
+        gen = _WT_GEN[0]
+        if getattr(w, "_edl_wt_skip", None) == gen:
             return None
         # HBM budget: the copies never take the last EDL_WT_RESERVE_GB (default 48) of free memory
         # (activations of the first step still have to fit); weights beyond it keep the NN dgrad
-        if _WT_BUDGET[0] is None:
+        need = w.numel() * w.element_size()
+        if _WT_BUDGET[0] is None or (need > _WT_BUDGET[0] and _WT_BUDGET[1] != gen):
             free, _ = torch.cuda.mem_get_info(w.device)
             _WT_BUDGET[0] = free - float(os.environ.get("EDL_WT_RESERVE_GB", 48)) * 2**30
-        need = w.numel() * w.element_size()
+            _WT_BUDGET[1] = gen
         if need > _WT_BUDGET[0]:
-            w._edl_wt_skip = True
+            w._edl_wt_skip = gen      # retried in a later generation, against a fresh measurement
             return None
         _WT_BUDGET[0] -= need
         wt = torch.empty(w.shape[1], w.shape[0], dtype=w.dtype, device=w.device)

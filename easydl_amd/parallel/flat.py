@@ -27,6 +27,7 @@ parameter starts on a 64-element boundary (128 B for bf16) so every view is
 from __future__ import annotations
 
 import os
+import weakref
 from dataclasses import dataclass, field
 
 import torch
@@ -81,6 +82,24 @@ def _split_by_bytes(plist, elem_bytes: int, max_bytes: int) -> list[list]:
     if cur:
         parts.append(cur)
     return parts
+
+
+def _pre_accumulate_hook(ref, key):
+    def hook(g):
+        me = ref()
+        if g is not None and me is not None:   # None: a fused op delivered this gradient itself
+            me.saw_autograd = True
+            me._autograd_slots.add(key)
+        return None
+    return hook
+
+
+def _post_accumulate_hook(ref):
+    def hook(p):
+        me = ref()
+        if me is not None:
+            me._post_accumulate(p)
+    return hook
 
 
 class FlatParams:
@@ -168,23 +187,19 @@ class FlatParams:
         # fused op that delivers its gradient directly returns None, and the post-accumulate
         # hook still fires for it; only the tensor hook sees whether a gradient really
         # reached AccumulateGrad, so that is what marks a slot for zeroing.
+        # The hooks reach this object through a weak reference: a tensor hook lives in the
+        # parameter's C++ autograd metadata, which Python's cycle collector cannot traverse, so
+        # parameter -> hook -> FlatParams -> parameter was a cycle that was never collected (a
+        # standby's warm-up model and its flat buffers stayed allocated: ~7 B/param per warm-up,
+        # scripts/warm_leak_probe3.py).
+        me = weakref.ref(self)
         for g in self.groups:
             for s in g.slots:
-                s.param.register_hook(self._pre_accumulate(s.param))
-                s.param.register_post_accumulate_grad_hook(self._post_accumulate)
+                s.param.register_hook(_pre_accumulate_hook(me, id(s.param)))
+                s.param.register_post_accumulate_grad_hook(_post_accumulate_hook(me))
         self._ready_cb = None
 
     # -- gradient protocol -------------------------------------------------
-    def _pre_accumulate(self, p):
-        key = id(p)
-
-        def hook(g):
-            if g is not None:   # None: a fused op delivered this gradient itself
-                self.saw_autograd = True
-                self._autograd_slots.add(key)
-            return None
-        return hook
-
     def _post_accumulate(self, p):
         p._edl_fresh = False
         if self._ready_cb is not None:

@@ -115,6 +115,7 @@ class ElasticTrainer:
         self.micro_batch = micro_batch
         self.step = 0                # committed optimizer steps
         self._warm_published = False
+        self._act_published = False
         self.needs_state = True     # fresh process: must receive state unless everyone is fresh
         self.comm = None
         self.assignment = None
@@ -610,8 +611,11 @@ class ElasticTrainer:
         """Tell the parked standby on this GPU what to warm up with (operator/standby.py
         warm_device): one layer of this model's width at this job's micro-batch shape, so the
         GEMM solutions, kernels and library handles of the replacement's first step are loaded
-        before it is needed.  Published after this worker's first step, once its allocator holds
-        its peak, so the standby's warm-up never competes with it for memory."""
+        before it is needed.  Published before this worker's first step, and the worker waits
+        for that warm-up (bounded, ``EDL_WARM_WAIT_S``, default 60 s): a warm-up never runs
+        beside a training step of this GPU, and it has the memory the step's activations will
+        take later (a standby that warms up after a takeover, with training running, is the
+        one exception: ``standby_warm_wait`` events show the rest)."""
         from easydl_amd.utils import vram
         if (self._warm_published or not vram.enabled() or self.device.type != "cuda"
                 or getattr(self, "kv", None) is None):
@@ -627,8 +631,24 @@ class ElasticTrainer:
             cfg["n_layers"] = 1
             spec = {"model": "llama", "cfg": cfg, "batch": [self.micro_batch, int(seq)]}
         vram.publish_warm(self.kv, f"{self.ctx.role}{self.ctx.index}", spec)
-        # HBM a step needs beyond the persistent state (activations, workspaces): a replacement
-        # that adopts the state checks it against what the GPU has free (_memory_plan)
+        t0 = time.perf_counter()
+        limit = float(os.environ.get("EDL_WARM_WAIT_S", 60))
+        state = vram.standby_warm_on(self.kv, self.device.index)
+        while state is False and time.perf_counter() - t0 < limit:
+            time.sleep(0.05)
+            state = vram.standby_warm_on(self.kv, self.device.index)
+        if state is not None:
+            self.events.emit("standby_warm_wait", s=round(time.perf_counter() - t0, 3), warm=bool(state))
+
+    def _publish_act(self) -> None:
+        """HBM a step needs beyond the persistent state (activations, workspaces), after the
+        first step: a replacement that adopts the state checks it against what the GPU has free
+        (_memory_plan)."""
+        from easydl_amd.utils import vram
+        if (self._act_published or not vram.enabled() or self.device.type != "cuda"
+                or getattr(self, "kv", None) is None):
+            return
+        self._act_published = True
         persistent = sum(t.untyped_storage().nbytes() for t in self.vram_state_tensors().values())
         act = max(0, torch.cuda.max_memory_reserved(self.device) - persistent)
         vram.publish_act(self.kv, f"{self.ctx.role}{self.ctx.index}", act, self.micro_batch)
@@ -879,6 +899,7 @@ class ElasticTrainer:
                 return self
             self._publish_vram()
             self._open_marks()
+            self._publish_warm_spec(data)
             prof = None
             if os.environ.get("EDL_PROFILE_FIRST_STEP", "0") == "1":
                 import cProfile         # diagnostics: host profile of this process's first step
@@ -955,7 +976,7 @@ class ElasticTrainer:
                     if self.checkpoint is not None:
                         self.checkpoint.on_step(self)
                     self._run_deferred_probes()
-                    self._publish_warm_spec(data)
+                    self._publish_act()
                     if on_step is not None:
                         on_step(self, loss)
                     if self.log_every and self.step % self.log_every == 0 and self.comm.rank == 0:

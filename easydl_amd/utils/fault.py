@@ -8,7 +8,7 @@
     raise@step=6                 raise RuntimeError inside the step
     kill@step=4,after_ms=1500    SIGKILL 1.5 s after step 4 starts (mid-step on the GPU)
     kill@step=4,wait=standby     first step >= 4 once the hot standby on this GPU has
-                                 warmed up (``standby/warm_gpu/<gpu>``), at most 30 steps late
+                                 warmed up (utils/vram.py standby_warm_on), at most 30 steps late
     kill@step=6,point=in_update  SIGKILL inside the optimizer update of step 6: after its
                                  ``begin`` step mark reached the GPU, before ``done``
 
@@ -122,10 +122,10 @@ class FaultInjector:
         kv = getattr(trainer, "kv", None)
         if kv is None:
             return True
+        from easydl_amd.utils.vram import standby_warm_on
         dev = getattr(trainer, "device", None)
-        where = str(dev.index if dev is not None and dev.type == "cuda" else "cpu")
         try:
-            return kv.exists(f"standby/warm_gpu/{where}") or kv.exists("standby/warm_gpu/any")
+            return bool(standby_warm_on(kv, dev.index if dev is not None and dev.type == "cuda" else "cpu"))
         except Exception:  # noqa: BLE001 - store unreachable: do not hold the fault back forever
             return True
 

@@ -88,6 +88,16 @@ def read_warm(kv, slot: str) -> tuple[bool, dict | None]:
     return True, json.loads(raw).get("spec")
 
 
+def standby_warm_on(kv, gpu) -> bool | None:
+    """None: no standby is parked (``standby/roster``, kept by the operator); True: one of the
+    parked standbys has run its warm-up on ``gpu`` (an int, "cpu" or None); False: not yet."""
+    names = [n for n in (kv.get_str("standby/roster") or "").split(",") if n]
+    if not names:
+        return None
+    where = ["any"] + ([f"gpu{gpu}"] if isinstance(gpu, int) else ["cpu"])
+    return any(kv.exists(f"standby/warm/{n}/{w}") for n in names for w in where)
+
+
 def publish_act(kv, slot: str, act_bytes: int, micro_batch: int) -> None:
     """HBM one training step of ``slot`` needs beyond its persistent state."""
     kv.set(f"vram/act/{slot}", json.dumps({"act_bytes": int(act_bytes), "micro_batch": int(micro_batch)}))
