@@ -36,6 +36,7 @@ Periodic plan (from per-rank step metrics)
 from __future__ import annotations
 
 import math
+import os
 import statistics
 from dataclasses import dataclass
 
@@ -80,6 +81,9 @@ class BrainConfig:
     snapshot_host_fraction: float = 0.8   # host DRAM the in-memory snapshot slots may take
     comm_margin: float = 0.03       # the engine must beat RCCL by this share to take a size
     comm_history: int = 8           # probe tables kept per world size
+    # a host-CPU parameter server busier than this share of its window gets twice the cores
+    ps_busy_high: float = float(os.environ.get("EDL_BRAIN_PS_BUSY_HIGH", 0.75))
+    ps_cpu_max: int = int(os.environ.get("EDL_BRAIN_PS_CPU_MAX", 16))
 
 
 def grad_bucket_mb(params: float, world: int, grad_bytes: int = 2) -> float:
@@ -281,14 +285,24 @@ class Planner:
         # per-rank CU plan from rocprofv3 kernel profiles (metrics[n]["rocprof"], see
         # collectors.rocprof_kernel_profile): a rank whose GPU time is mostly bandwidth-bound
         # work (a PS applying AdamW, an evaluator) keeps its speed on a slice of the CUs
+        # (metrics[n]["gpu_mix"]: the same split measured live by the running rank, utils/kmix.py;
+        # a rank is re-planned only when the plan differs from the CUs it runs on now)
         for n, m in metrics.items():
-            prof = m.get("rocprof")
-            if not prof:
-                continue
-            cu = self.cu_for_profile(prof)
-            if cu is not None and plan.per_rank.get(n, {}).get("cu") != cu:
-                plan.per_rank.setdefault(n, {})["cu"] = cu
-                changed.append(f"{n}: {cu} CUs ({100 * prof['memory_frac']:.0f}% of kernel time bandwidth-bound)")
+            prof = m.get("rocprof") or m.get("gpu_mix")
+            if prof and m.get("device", "cuda") == "cuda" or m.get("rocprof"):
+                cu = self.cu_for_profile(prof)
+                if cu is not None and cu != m.get("cu"):
+                    plan.per_rank.setdefault(n, {})["cu"] = cu
+                    src = "rocprofv3" if m.get("rocprof") else "live"
+                    changed.append(f"{n}: {cu} CUs ({100 * prof['memory_frac']:.0f}% of GPU time bandwidth-bound, "
+                                   f"{src})")
+            # a parameter server on host CPUs that is busy most of the time: more cores
+            if m.get("role") == "ps" and m.get("device") == "cpu" and m.get("busy_frac", 0) > self.cfg.ps_busy_high:
+                cpu = int(m.get("cpu") or 1)
+                want = min(self.cfg.ps_cpu_max, 2 * cpu)
+                if want > cpu:
+                    plan.per_rank.setdefault(n, {})["cpu"] = want
+                    changed.append(f"{n}: {want} CPUs (busy {100 * m['busy_frac']:.0f}% on {cpu})")
         # grow into free GPUs
         wr = plan.roles.get("worker")
         if wr is not None and feat.mode != "ps":

@@ -1001,7 +1001,7 @@ def _load_shard(read, table, state, dev, expect: int, what: str, seg=None, slot=
 
 def unlink_job_segments(job: str) -> int:
     n = 0
-    pat = re.compile(rf"^edl-{re.escape(job)}((-t\d+of\d+)?-w\d+-s\d+|-marks-[a-z]+\d+)$")
+    pat = re.compile(rf"^edl-{re.escape(job)}((-t\d+of\d+)?-w\d+-s\d+|-marks-[a-z]+\d+|-ps\d+)$")
     for path in glob.glob(f"/dev/shm/edl-{job}-*"):
         if not pat.match(os.path.basename(path)):
             continue

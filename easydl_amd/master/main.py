@@ -136,7 +136,7 @@ def main(argv=None):
     ap.add_argument("--run-dir", default=os.environ.get("EDL_RUN_DIR"))
     ap.add_argument("--job-spec", default=None, help="ElasticJob JSON/YAML: enables the Brain plan loop")
     ap.add_argument("--brain-url", default=os.environ.get("EDL_BRAIN_URL"))
-    ap.add_argument("--plan-period", type=float, default=30.0)
+    ap.add_argument("--plan-period", type=float, default=float(os.environ.get("EDL_PLAN_PERIOD_S", 30.0)))
     ap.add_argument("--job-resource", default=None, help="user JobResource JSON/YAML (Brain not consulted)")
     ap.add_argument("--metrics-port", type=int, default=-1, help="Prometheus endpoint port (0 = any, -1 = off)")
     a = ap.parse_args(argv)

@@ -40,6 +40,9 @@ class PlanLoop:
         self._last = 0.0
         self.started = False
         self._features = None
+        # resource_updation issued per process name -> (node id it was issued for, time): not
+        # issued again until a new incarnation of that name reports its metrics
+        self._updating: dict[str, tuple[str, float]] = {}
 
     def features(self) -> dict:
         """Extracted job features (meta-device model analysis) + the user's hints."""
@@ -109,8 +112,13 @@ class PlanLoop:
         if self.period_s <= 0 or now - self._last < self.period_s:
             return
         self._last = now
-        members = master.rdzv.members()
-        metrics = {n: m for n in members if (m := master.kv.get(f"metrics/{n}"))}
+        # rendezvous members (workers) and the roles that registered their own metrics
+        # (parameter servers, evaluators: utils/metrics.py publish_role_metrics); a role's record
+        # older than a few periods belongs to a process that is gone
+        extra = [n for n in (master.kv.get_str("metrics/extra_nodes") or "").split(",") if n]
+        members = list(dict.fromkeys(master.rdzv.members() + extra))
+        fresh = time.time() - max(60.0, 3 * self.period_s)
+        metrics = {n: m for n in members if (m := master.kv.get(f"metrics/{n}")) and m.get("ts", 0) >= fresh}
         if not metrics:
             return
         # rocprofv3 kernel profiles the roles left under <run_dir>/rocprof/<process>/ (Brain CU signal)
@@ -128,11 +136,26 @@ class PlanLoop:
         jr = newp.to_job_resource(self.job.name)
         for node, d in newp.per_rank.items():
             name = node.split(":")[0]
+            now = metrics.get(node) or {}
+            pend = self._updating.get(name)
+            if pend is not None and (pend[0] == node or time.time() - pend[1] < 5.0) \
+                    and time.time() - pend[1] < 120.0:
+                continue     # its replacement has not reported yet
             if d.get("evict"):
                 jr.resource_updation.append(ResourceUpdation(name=name, resource=Resource()))
-            elif d.get("cu") and d.get("cu") != (self.plan.per_rank.get(node) or {}).get("cu"):
-                # CU plan from the rank's kernel mix: re-create it with a CU-masked stream
-                jr.resource_updation.append(ResourceUpdation(name=name, resource=Resource(cu=int(d["cu"]))))
+                continue
+            res = Resource()
+            if d.get("cu") and int(d["cu"]) != now.get("cu"):
+                # CU plan from the rank's kernel mix (live, utils/kmix.py, or a rocprofv3 profile):
+                # re-create it with CU-masked streams
+                res.cu = int(d["cu"])
+            if d.get("cpu") and int(d["cpu"]) != now.get("cpu"):
+                res.cpu = float(d["cpu"])     # a CPU-bound parameter server gets more cores
+            if res.cu or res.cpu:
+                jr.resource_updation.append(ResourceUpdation(name=name, resource=res))
+        for u in jr.resource_updation:
+            node = next((n for n in newp.per_rank if n.split(":")[0] == u.name), u.name)
+            self._updating[u.name] = (node, time.time())
         for d in newp.per_rank.values():
             d.pop("evict", None)
         self.plan = newp

@@ -124,6 +124,13 @@ class ElasticOperator:
     # ------------------------------------------------------------- master
     def start(self) -> None:
         """Create ONLY the trainer (job master) process first (reference :47,105-106)."""
+        if os.environ.get("EDL_KEEP_SEGMENTS", "0") != "1":
+            # the operator owns the job's /dev/shm segments (snapshots, PS shards, step marks):
+            # a new job of the same name must not restore a previous run's state
+            from easydl_amd.ckpt.manager import unlink_job_segments
+            n = unlink_job_segments(self.job.name)
+            if n:
+                self.events.emit("stale_segments_removed", n=n)
         with open(os.path.join(self.run_dir, "job.json"), "w") as f:
             json.dump(self.job.to_dict(), f)
         argv = self.master_argv or [self.cfg.python, "-m", "easydl_amd.master.main", "--job", self.job.name,
@@ -446,6 +453,8 @@ class ElasticOperator:
             return
         p.exit_code = ex.exit_code if not ex.signal else -ex.signal
         self.events.emit("exit", name=p.name, pid=p.pid, code=ex.exit_code, signal=ex.signal, role=p.role)
+        if self.kv is not None:
+            self.kv.delete(f"metrics/{p.node_id}")   # the plan loop must not re-plan a process that is gone
         if p.role == "trainer":
             p.state = "exited"
             if not self.done:

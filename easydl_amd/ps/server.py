@@ -136,6 +136,12 @@ class ParameterServer:
         self.host, self.port = self._srv.getsockname()
         self._stop = threading.Event()
         self._threads = []
+        # graceful hand-over (retire): no new requests, in-flight ones finish, final snapshot
+        self._retiring = threading.Event()
+        self._conns: set = set()
+        self._busy = 0
+        from easydl_amd.utils.kmix import KernelMixMeter
+        self.kmix = KernelMixMeter(self.state.device)   # live kernel mix for the Brain (utils/kmix.py)
 
     # -- optimizer -------------------------------------------------------------
     def _fence_snapshot(self) -> None:
@@ -206,7 +212,7 @@ class ParameterServer:
 
     def _push(self, worker: str, grads: dict[str, torch.Tensor], inbox: torch.Tensor | None = None,
               slot: int = 0, sparse_inbox: bool = False) -> int:
-        with self.lock:
+        with self.lock, self.kmix.phase("memory"):   # accumulate + AdamW/Adagrad: HBM-bound
             st = self.state
             # sparse-table rows are updated below, before _apply: they are part of the
             # snapshot too, so the fence must come first
@@ -241,7 +247,9 @@ class ParameterServer:
             self.round_pushers.add(worker)
             target = self.version + 1
             while self.version < target:
-                if len(self.round_pushers) >= max(1, self.expected_workers()):
+                if len(self.round_pushers) >= max(1, self.expected_workers()) or (
+                        self._retiring.is_set() and self.round_pushers):
+                    # (retiring: the other workers' pushes go to the successor; close this round)
                     n = len(self.round_pushers)
                     self.round_pushers = set()
                     self._apply(1.0 / n)
@@ -252,134 +260,182 @@ class ParameterServer:
 
     # -- serving ---------------------------------------------------------------
     def _serve(self, conn: socket.socket):
+        with self.lock:
+            self._conns.add(conn)
         try:
-            while not self._stop.is_set():
+            while not self._stop.is_set() and not self._retiring.is_set():
                 try:
                     hdr, tensors = recv_msg(conn)
                 except (ConnectionError, OSError):
                     return
-                op = hdr.get("op")
-                if op == "pull":
-                    minv = int(hdr.get("min_version", 0))
+                with self.lock:
+                    if self._retiring.is_set():
+                        return     # never started: the client re-sends it to the successor
+                    self._busy += 1
+                try:
+                    self._handle(conn, hdr, tensors)
+                finally:
                     with self.lock:
-                        t_end = time.monotonic() + float(hdr.get("timeout", 60))
-                        while self.version < minv and time.monotonic() < t_end:
-                            self.lock.wait(timeout=0.05)
-                        self.stats["pulls"] += 1
-                        out = {n: t.clone() for n, t in self.state.tensors(names=hdr.get("names")).items()}
-                        ver = self.version
-                    send_msg(conn, {"ok": True, "version": ver}, out)
-                elif op == "pull_rows":
-                    t = self.tables[hdr["table"]]
-                    ids = tensors["ids"].to(t.w.device)
-                    dt = torch.bfloat16 if hdr.get("bf16") else torch.float32
-                    with self.lock:
-                        rows = sparse.embed_gather(t.w, ids, out_dtype=dt)
-                        ver = self.version
-                    self.stats["pulls"] += 1
-                    send_msg(conn, {"ok": True, "version": ver}, {"rows": rows})
-                elif op == "ipc_open":
-                    from easydl_amd.ps.ipc import export_tensor
-                    st = self.state
-                    if not st.w.is_cuda:
-                        send_msg(conn, {"ok": False, "error": "PS shard is not on a GPU"})
-                        continue
-                    with self.lock:
-                        wid = hdr.get("worker", "?")
-                        if wid not in self.inboxes:
-                            self.inboxes[wid] = [torch.zeros_like(st.w), torch.zeros_like(st.w)]
-                            self._inbox_ev[wid] = [None, None]
-                        desc = {"w": export_tensor(st.w), "inbox": [export_tensor(x) for x in self.inboxes[wid]],
-                                "layout": {n: [st.offsets[n], list(st.shapes[n])] for n in st.names}}
-                        if wid not in self._push_flag:
-                            self._push_flag[wid] = torch.zeros(4, dtype=torch.int32, device=st.device)
-                            self._push_status[wid] = torch.zeros(4, dtype=torch.int32, device=st.device)
-                        else:
-                            # a (re)connecting client -- the same worker after a reconnect, or its
-                            # replacement -- counts its push sequence from 0 again: restart the flag
-                            # in stream order, or every wait for a small seq would pass at once
-                            self._push_flag[wid].zero_()
-                            self.stats["flag_resets"] = self.stats.get("flag_resets", 0) + 1
-                        desc["flag"] = export_tensor(self._push_flag[wid])
-                        cap = int(hdr.get("sparse_cap", 0))
-                        if self.tables and cap > 0:
-                            if wid not in self.sp_inboxes or any(
-                                    b[0][0].numel() != cap for b in self.sp_inboxes[wid].values()):
-                                dev = st.device
-                                self.sp_inboxes[wid] = {
-                                    n: [(torch.zeros(cap, dtype=torch.int64, device=dev),
-                                         torch.zeros(cap, t.dim, dtype=torch.float32, device=dev),
-                                         torch.zeros(4, dtype=torch.int32, device=dev)) for _ in range(2)]
-                                    for n, t in self.tables.items()}
-                            desc["tables"] = {n: {"w": export_tensor(t.w), "rows": t.rows}
-                                              for n, t in self.tables.items()}
-                            desc["sparse_inbox"] = {n: [[export_tensor(x) for x in b] for b in bufs]
-                                                    for n, bufs in self.sp_inboxes[wid].items()}
-                            desc["sparse_cap"] = cap
-                    send_msg(conn, {"ok": True, "ipc": desc, "version": self.version})
-                elif op == "pull_ipc":
-                    minv = int(hdr.get("min_version", 0))
-                    with self.lock:
-                        t_end = time.monotonic() + float(hdr.get("timeout", 60))
-                        while self.version < minv and time.monotonic() < t_end:
-                            self.lock.wait(timeout=0.05)
-                        self.stats["pulls"] += 1
-                        ver, ev = self.version, self._apply_ev
-                    if ev is not None:
-                        ev.synchronize()   # the worker reads the shard next: that version must be written
-                    send_msg(conn, {"ok": True, "version": ver})
-                elif op == "push_ipc":
-                    wid, slot = hdr["worker"], int(hdr.get("slot", 0))
-                    if hdr.get("seq") is not None:   # the worker's inbox writes before our reads
-                        dev = self.state.device
-                        sparse.ps_wait(self._push_flag[wid], int(hdr["seq"]), self.push_wait_s,
-                                       self._push_status[wid], torch.cuda.current_stream(dev))
-                    ver = self._push(wid, tensors, inbox=self.inboxes[wid][slot], slot=slot,
-                                     sparse_inbox=bool(hdr.get("sparse_ipc")))
-                    with self.lock:
-                        other = self._inbox_ev[wid][1 - slot]   # read by the previous push's update
-                        mine = self._apply_ev if hdr.get("pull") else None
-                    # outside the lock: other workers' pushes keep flowing meanwhile
-                    if other is not None:
-                        other.synchronize()
-                    if mine is not None:
-                        mine.synchronize()   # push + pull in one message: the update is written
-                    if hdr.get("seq") is not None and (other is not None or mine is not None):
-                        # a bounded wait that gave up (a worker killed mid-push): counted
-                        stw = self._push_status[wid]
-                        if int(stw[0]):
-                            self.stats["push_wait_timeouts"] = self.stats.get("push_wait_timeouts", 0) + 1
-                            log.warning("PS %d: push of %s applied after its ordering wait gave up", self.index,
-                                        wid)
-                            stw.zero_()
-                    send_msg(conn, {"ok": True, "version": ver})
-                elif op == "push":
-                    ver = self._push(hdr.get("worker", "?"), tensors)
-                    send_msg(conn, {"ok": True, "version": ver})
-                elif op == "state":
-                    with self.lock:
-                        out = {f"b{i}": b.clone() for i, b in enumerate(self.state_buffers())}
-                        meta = {"version": self.version, "step": self.step,
-                                "table_steps": [t.step for t in self.tables.values()]}
-                    send_msg(conn, {"ok": True, **meta}, out)
-                elif op == "load":
-                    with self.lock:
-                        self._fence_snapshot()
-                        self.load([tensors[f"b{i}"] for i in range(len(tensors))], hdr["version"], hdr["step"],
-                                  hdr.get("table_steps"))
-                    send_msg(conn, {"ok": True})
-                elif op == "stats":
-                    s = dict(self.stats)
-                    s["workers"] = sorted(s["workers"])
-                    send_msg(conn, {"ok": True, "version": self.version, "stats": s, "index": self.index})
-                elif op == "shutdown":
-                    send_msg(conn, {"ok": True})
-                    self._stop.set()
-                    return
-                else:
-                    send_msg(conn, {"ok": False, "error": f"unknown op {op}"})
+                        self._busy -= 1
+                        self.lock.notify_all()
         finally:
+            with self.lock:
+                self._conns.discard(conn)
             conn.close()
+
+    def _handle(self, conn: socket.socket, hdr: dict, tensors) -> None:
+        op = hdr.get("op")
+        if op == "pull":
+            minv = int(hdr.get("min_version", 0))
+            with self.lock:
+                t_end = time.monotonic() + float(hdr.get("timeout", 60))
+                while self.version < minv and time.monotonic() < t_end:
+                    self.lock.wait(timeout=0.05)
+                self.stats["pulls"] += 1
+                out = {n: t.clone() for n, t in self.state.tensors(names=hdr.get("names")).items()}
+                ver = self.version
+            send_msg(conn, {"ok": True, "version": ver}, out)
+        elif op == "pull_rows":
+            t = self.tables[hdr["table"]]
+            ids = tensors["ids"].to(t.w.device)
+            dt = torch.bfloat16 if hdr.get("bf16") else torch.float32
+            with self.lock:
+                rows = sparse.embed_gather(t.w, ids, out_dtype=dt)
+                ver = self.version
+            self.stats["pulls"] += 1
+            send_msg(conn, {"ok": True, "version": ver}, {"rows": rows})
+        elif op == "ipc_open":
+            from easydl_amd.ps.ipc import export_tensor
+            st = self.state
+            if not st.w.is_cuda:
+                send_msg(conn, {"ok": False, "error": "PS shard is not on a GPU"})
+                return
+            with self.lock:
+                wid = hdr.get("worker", "?")
+                if wid not in self.inboxes:
+                    self.inboxes[wid] = [torch.zeros_like(st.w), torch.zeros_like(st.w)]
+                    self._inbox_ev[wid] = [None, None]
+                desc = {"w": export_tensor(st.w), "inbox": [export_tensor(x) for x in self.inboxes[wid]],
+                        "layout": {n: [st.offsets[n], list(st.shapes[n])] for n in st.names}}
+                if wid not in self._push_flag:
+                    self._push_flag[wid] = torch.zeros(4, dtype=torch.int32, device=st.device)
+                    self._push_status[wid] = torch.zeros(4, dtype=torch.int32, device=st.device)
+                else:
+                    # a (re)connecting client -- the same worker after a reconnect, or its
+                    # replacement -- counts its push sequence from 0 again: restart the flag
+                    # in stream order, or every wait for a small seq would pass at once
+                    self._push_flag[wid].zero_()
+                    self.stats["flag_resets"] = self.stats.get("flag_resets", 0) + 1
+                desc["flag"] = export_tensor(self._push_flag[wid])
+                cap = int(hdr.get("sparse_cap", 0))
+                if self.tables and cap > 0:
+                    if wid not in self.sp_inboxes or any(
+                            b[0][0].numel() != cap for b in self.sp_inboxes[wid].values()):
+                        dev = st.device
+                        self.sp_inboxes[wid] = {
+                            n: [(torch.zeros(cap, dtype=torch.int64, device=dev),
+                                 torch.zeros(cap, t.dim, dtype=torch.float32, device=dev),
+                                 torch.zeros(4, dtype=torch.int32, device=dev)) for _ in range(2)]
+                            for n, t in self.tables.items()}
+                    desc["tables"] = {n: {"w": export_tensor(t.w), "rows": t.rows}
+                                      for n, t in self.tables.items()}
+                    desc["sparse_inbox"] = {n: [[export_tensor(x) for x in b] for b in bufs]
+                                            for n, bufs in self.sp_inboxes[wid].items()}
+                    desc["sparse_cap"] = cap
+            send_msg(conn, {"ok": True, "ipc": desc, "version": self.version})
+        elif op == "pull_ipc":
+            minv = int(hdr.get("min_version", 0))
+            with self.lock:
+                t_end = time.monotonic() + float(hdr.get("timeout", 60))
+                while self.version < minv and time.monotonic() < t_end:
+                    self.lock.wait(timeout=0.05)
+                self.stats["pulls"] += 1
+                ver, ev = self.version, self._apply_ev
+            if ev is not None:
+                ev.synchronize()   # the worker reads the shard next: that version must be written
+            send_msg(conn, {"ok": True, "version": ver})
+        elif op == "push_ipc":
+            wid, slot = hdr["worker"], int(hdr.get("slot", 0))
+            if hdr.get("seq") is not None:   # the worker's inbox writes before our reads
+                dev = self.state.device
+                sparse.ps_wait(self._push_flag[wid], int(hdr["seq"]), self.push_wait_s,
+                               self._push_status[wid], torch.cuda.current_stream(dev))
+            ver = self._push(wid, tensors, inbox=self.inboxes[wid][slot], slot=slot,
+                             sparse_inbox=bool(hdr.get("sparse_ipc")))
+            with self.lock:
+                other = self._inbox_ev[wid][1 - slot]   # read by the previous push's update
+                mine = self._apply_ev if hdr.get("pull") else None
+            # outside the lock: other workers' pushes keep flowing meanwhile
+            if other is not None:
+                other.synchronize()
+            if mine is not None:
+                mine.synchronize()   # push + pull in one message: the update is written
+            if hdr.get("seq") is not None and (other is not None or mine is not None):
+                # a bounded wait that gave up (a worker killed mid-push): counted
+                stw = self._push_status[wid]
+                if int(stw[0]):
+                    self.stats["push_wait_timeouts"] = self.stats.get("push_wait_timeouts", 0) + 1
+                    log.warning("PS %d: push of %s applied after its ordering wait gave up", self.index,
+                                wid)
+                    stw.zero_()
+            send_msg(conn, {"ok": True, "version": ver})
+        elif op == "push":
+            ver = self._push(hdr.get("worker", "?"), tensors)
+            send_msg(conn, {"ok": True, "version": ver})
+        elif op == "state":
+            with self.lock:
+                out = {f"b{i}": b.clone() for i, b in enumerate(self.state_buffers())}
+                meta = {"version": self.version, "step": self.step,
+                        "table_steps": [t.step for t in self.tables.values()]}
+            send_msg(conn, {"ok": True, **meta}, out)
+        elif op == "load":
+            with self.lock:
+                self._fence_snapshot()
+                self.load([tensors[f"b{i}"] for i in range(len(tensors))], hdr["version"], hdr["step"],
+                          hdr.get("table_steps"))
+            send_msg(conn, {"ok": True})
+        elif op == "stats":
+            s = dict(self.stats)
+            s["workers"] = sorted(s["workers"])
+            send_msg(conn, {"ok": True, "version": self.version, "stats": s, "index": self.index})
+        elif op == "shutdown":
+            send_msg(conn, {"ok": True})
+            self._stop.set()
+            return
+        else:
+            send_msg(conn, {"ok": False, "error": f"unknown op {op}"})
+
+    def retire(self, timeout_s: float = 60.0) -> int:
+        """Graceful hand-over to a successor (vertical resize by replacement, reference
+        docs/design/elastic-training-operator.md:99-101): stop accepting connections, cut the
+        idle ones (a request already read runs to its reply; one not yet read fails on the
+        client, which re-sends it to the successor -- so every acknowledged update is in the
+        final snapshot, and none is applied twice), then snapshot the final version and wait
+        for the snapshot to be committed.  Returns that version."""
+        self._retiring.set()
+        try:
+            self._srv.close()
+        except OSError:
+            pass
+        with self.lock:
+            for c in list(self._conns):
+                try:
+                    c.shutdown(socket.SHUT_RD)
+                except OSError:
+                    pass
+            self.lock.notify_all()
+            t_end = time.monotonic() + timeout_s
+            while self._busy and time.monotonic() < t_end:
+                self.lock.wait(timeout=0.05)
+            if self.snapshot is not None:
+                self._fence_snapshot()
+                self.snapshot(self)
+                wait = getattr(self.snapshot, "wait", None)
+                if wait is not None:
+                    wait()
+            ver = self.version
+        self._stop.set()
+        return ver
 
     def state_buffers(self) -> list[torch.Tensor]:
         """Every fp32 state buffer in a fixed order: dense w, m, v, then per table w, m, v."""
@@ -495,6 +551,12 @@ class PSSnapshotter:
         if t < 0:
             raise RuntimeError(f"PS snapshot enqueue failed: hipError {-t}")
         self.ticket, self._keep = t, csum
+
+    def wait(self) -> None:
+        """Block until the in-flight snapshot (GPU engine) is committed."""
+        if self.ticket is not None and self.engine is not None:
+            from easydl_amd import _native
+            _native.runtime()("edl_ckpt_wait", self.engine, self.ticket, 600000)
 
     def fence(self, device) -> None:
         """The next update of the shard waits (on the GPU) for the in-flight copy."""

@@ -46,6 +46,7 @@ def run_ps(model_fn, num_ps: int, ctx: TrainerContext | None = None, *, optimize
     ctx = ctx or TrainerContext.from_env()
     kv = _kv(ctx)
     events = EventLog(os.path.join(ctx.run_dir, f"events-ps{ctx.index}.jsonl"), proc=f"ps{ctx.index}")
+    gen = int(os.environ.get("EDL_GENERATION", 0))
     torch.manual_seed(seed)
     model = model_fn(device)
     snap = PSSnapshotter(ctx.job, ctx.index)
@@ -54,17 +55,67 @@ def run_ps(model_fn, num_ps: int, ctx: TrainerContext | None = None, *, optimize
                          snapshot_every=snapshot_every, tables=table_shard_spec(model, num_ps, ctx.index),
                          sparse_optimizer=sparse_optimizer, sparse_lr=sparse_lr, seed=seed)
     del model  # the PS keeps only its shard
+    handoff = _await_predecessor(kv, ctx.index, gen, events)
     if snap.restore(ps):
-        events.emit("ps_restored", version=ps.version)
+        events.emit("ps_restored", version=ps.version, handoff=handoff)
     ps.start()
-    kv.set(f"ps/addr/{ctx.index}", json.dumps({"host": ps.host, "port": ps.port, "pid": os.getpid(),
-                                                "gen": int(os.environ.get("EDL_GENERATION", 0))}))
-    events.emit("ps_started", port=ps.port, params=ps.state.numel)
+    kv.set(f"ps/addr/{ctx.index}", json.dumps({"host": ps.host, "port": ps.port, "pid": os.getpid(), "gen": gen}))
+    events.emit("ps_started", port=ps.port, params=ps.state.numel, gen=gen)
+    from easydl_amd.utils.metrics import cu_count, publish_role_metrics
+    t_start, next_pub = time.time(), 0.0
     try:
         while not kv.exists("job/done") and not ps._stop.is_set():
+            if kv.exists(f"rdzv/leave/{ctx.node_id}"):
+                # replaced (resource_updation) or scaled down: hand the shard over, then exit 0
+                t0 = time.perf_counter()
+                ver = ps.retire()
+                kv.delete(f"metrics/{ctx.node_id}")
+                kv.set(f"ps/handoff/{ctx.index}", json.dumps({"gen": gen, "version": ver, "pid": os.getpid()}))
+                events.emit("ps_retired", version=ver, s=round(time.perf_counter() - t0, 3), gen=gen)
+                return
+            if time.time() >= next_pub:
+                # live metrics for the Brain: this rank is no rendezvous member, so it registers itself
+                mix = ps.kmix.snapshot()
+                up = max(1e-3, min(time.time() - t_start, ps.kmix.window_s))
+                publish_role_metrics(kv, ctx.node_id, {
+                    "role": "ps", "step": ps.version, "ts": time.time(), "gpu_mix": mix,
+                    "busy_frac": round(mix["gpu_s"] / up, 4) if mix else 0.0, "device": ps.state.device.type,
+                    "cu": cu_count(ctx.cu_mask), "cpu": int(os.environ.get("OMP_NUM_THREADS", 0) or 0)})
+                next_pub = time.time() + float(os.environ.get("EDL_PS_METRICS_S", 2.0))
             time.sleep(0.2)
     finally:
         ps.stop()
+
+
+def _await_predecessor(kv, index: int, gen: int, events, timeout_s: float = 120.0) -> dict | None:
+    """A PS replacing a LIVE predecessor (vertical resize) restores only once that one has
+    retired and committed its final snapshot (``ps/handoff/<index>``); a dead predecessor's
+    newest snapshot is all there is (the crash path)."""
+    prev = kv.get(f"ps/addr/{index}")
+    if not prev or int(prev.get("gen", -1)) >= gen or not _alive(prev.get("pid")):
+        return None
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < timeout_s:
+        h = kv.get(f"ps/handoff/{index}")
+        if h and int(h.get("gen", -1)) == int(prev.get("gen", -1)):
+            events.emit("ps_handoff_received", version=h.get("version"), wait_s=round(time.perf_counter() - t0, 3))
+            return h
+        if not _alive(prev.get("pid")):
+            break
+        time.sleep(0.05)
+    events.emit("ps_handoff_missing", predecessor=prev.get("pid"), wait_s=round(time.perf_counter() - t0, 3))
+    return None
+
+
+def _alive(pid) -> bool:
+    try:
+        os.kill(int(pid), 0)
+    except (ProcessLookupError, TypeError, ValueError):
+        return False
+    except PermissionError:
+        return True
+    from easydl_amd.utils.procfs import mm_released
+    return not mm_released(int(pid))
 
 
 def _transport(device) -> str:
@@ -132,6 +183,10 @@ class PSWorker:
                         on_step(self, loss)
                 disp.complete(shard)
                 self.events.emit("shard_done", shard=shard, steps=self.steps)
+                if self.kv.exists(f"rdzv/leave/{self.ctx.node_id}"):
+                    # replaced or scaled down: leave between shards (none half-done, none repeated)
+                    self.events.emit("worker_left", steps=self.steps)
+                    break
         finally:
             self.rdzv.leave()
             self.rdzv.stop_heartbeat()

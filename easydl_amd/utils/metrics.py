@@ -22,7 +22,9 @@ class MetricsReporter:
             os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
 
     def record(self, step: int, dt: float, samples: int = 0, tokens: int = 0, world: int = 1, loss=None,
-               mem_gb: float | None = None) -> dict | None:
+               mem_gb: float | None = None, extra=None) -> dict | None:
+        """``extra``: a dict, or a callable returning one, merged into the published record
+        (evaluated only when a record is published, every ``every`` steps)."""
         self.times.append(dt)
         self.n += 1
         if self.n % self.every:
@@ -34,6 +36,8 @@ class MetricsReporter:
             m["loss"] = float(loss)
         if mem_gb is not None:
             m["mem_gb"] = mem_gb
+        if extra is not None:
+            m.update({k: v for k, v in (extra() if callable(extra) else extra).items() if v is not None})
         self.last = m
         if self.kv is not None:
             try:
@@ -54,3 +58,22 @@ def render_prometheus(metrics: dict[str, dict], job: str) -> str:
             if key in m:
                 lines.append(f'edl_{key}{{job="{job}",node="{node}"}} {m[key]}')
     return "\n".join(lines) + "\n"
+
+
+def cu_count(mask_hex: str | None) -> int | None:
+    """CUs enabled by an ``EDL_CU_MASK`` hex string (None: no mask, every CU)."""
+    if not mask_hex:
+        return None
+    try:
+        return bin(int(str(mask_hex), 16)).count("1")
+    except ValueError:
+        return None
+
+
+def publish_role_metrics(kv, node: str, m: dict) -> None:
+    """Metrics of a role that is not a rendezvous member (a parameter server, an evaluator):
+    ``metrics/<node>`` plus a registry the master's plan loop reads besides the members."""
+    kv.set(f"metrics/{node}", json.dumps(m))
+    reg = set((kv.get_str("metrics/extra_nodes") or "").split(","))
+    if node not in reg:
+        kv.append("metrics/extra_nodes", node + ",")

@@ -1,0 +1,110 @@
+"""Live kernel-mix signal (utils/kmix.py) and what the Brain does with it."""
+import time
+
+import pytest
+
+import torch
+
+from easydl_amd.api.spec import Resource, ResourcePlan, RoleResource
+from easydl_amd.brain.collectors import GpuInfo, NodeInventory
+from easydl_amd.brain.planner import JobFeatures, Planner
+from easydl_amd.utils.kmix import KernelMixMeter
+from easydl_amd.utils.metrics import cu_count
+
+
+def _inv():
+    return NodeInventory(gpus=[GpuInfo(i, "gfx950", 256, 288.0, busy_pct=90) for i in range(8)], cpus=128,
+                         host_mem_gb=2048)
+
+
+def _plan():
+    return ResourcePlan(roles={"worker": RoleResource(4, Resource(gpu=1))}, bucket_mb=128.0)
+
+
+def test_meter_splits_phase_time_by_class_on_the_host():
+    m = KernelMixMeter("cpu", window_s=30)
+    assert m.snapshot() is None
+    with m.phase("compute"):
+        time.sleep(0.03)
+    with m.phase("memory"):
+        time.sleep(0.01)
+    s = m.snapshot()
+    assert s["source"] == "host-timer" and s["phases"] == 2
+    assert 0.6 < s["compute_frac"] < 0.9 and abs(s["compute_frac"] + s["memory_frac"] - 1) < 1e-3
+
+
+def test_meter_forgets_phases_older_than_its_window():
+    m = KernelMixMeter("cpu", window_s=0.05)
+    with m.phase("memory"):
+        pass
+    time.sleep(0.1)
+    assert m.snapshot() is None
+
+
+def test_live_mix_gives_a_running_bandwidth_bound_rank_a_cu_plan_once():
+    """A PS whose live GPU time is all HBM-bound updates gets a CU slice; once it runs on that
+    slice (its metrics report the CUs) the Brain does not plan it again; a compute-bound
+    trainer keeps the whole GPU; CPU-hosted roles get no CU plan at all."""
+    ps_mix = {"compute_frac": 0.02, "memory_frac": 0.98, "gpu_s": 3.0, "source": "hip-events"}
+    tr_mix = {"compute_frac": 0.93, "memory_frac": 0.07, "gpu_s": 30.0, "source": "hip-events"}
+    metrics = {"job-ps-0:11": {"role": "ps", "device": "cuda", "gpu_mix": ps_mix, "cu": None},
+               "job-worker-0:12": {"role": "worker", "device": "cuda", "gpu_mix": tr_mix, "step_time": 1.0},
+               "job-ps-1:13": {"role": "ps", "device": "cpu", "gpu_mix": ps_mix, "busy_frac": 0.1, "cpu": 4}}
+    nxt = Planner().next_plan(JobFeatures(mode="ps", params=3.3e8), _inv(), _plan(), metrics)
+    cu = nxt.per_rank["job-ps-0:11"]["cu"]
+    assert 0 < cu < 256 and cu % 8 == 0 and "live" in nxt.reason
+    assert "cu" not in nxt.per_rank.get("job-worker-0:12", {}) and "job-ps-1:13" not in nxt.per_rank
+    metrics["job-ps-0:21"] = dict(metrics.pop("job-ps-0:11"), cu=cu)      # the replacement, on its slice
+    again = Planner().next_plan(JobFeatures(mode="ps", params=3.3e8), _inv(), _plan(), metrics)
+    assert again is None or "job-ps-0:21" not in again.per_rank
+
+
+def test_busy_cpu_parameter_server_gets_more_cores_up_to_the_cap():
+    from easydl_amd.brain.planner import BrainConfig
+    metrics = {"job-ps-0:5": {"role": "ps", "device": "cpu", "busy_frac": 0.9, "cpu": 4}}
+    p = Planner(BrainConfig(ps_busy_high=0.75, ps_cpu_max=6))
+    nxt = p.next_plan(JobFeatures(mode="ps", params=1e5), _inv(), _plan(), metrics)
+    assert nxt.per_rank["job-ps-0:5"]["cpu"] == 6
+    metrics["job-ps-0:5"]["cpu"] = 6
+    assert Planner(BrainConfig(ps_busy_high=0.75, ps_cpu_max=6)).next_plan(
+        JobFeatures(mode="ps", params=1e5), _inv(), _plan(), metrics) is None
+    metrics["job-ps-0:5"].update(cpu=2, busy_frac=0.3)
+    assert p.next_plan(JobFeatures(mode="ps", params=1e5), _inv(), _plan(), metrics) is None
+
+
+def test_cu_count_of_operator_masks():
+    from easydl_amd.operator.reconciler import cu_mask_hex
+    assert cu_count(None) is None and cu_count(cu_mask_hex(64)) == 64 and cu_count(cu_mask_hex(256)) == 256
+
+
+def test_trainer_publishes_its_live_mix_with_its_metrics(tmp_path):
+    from easydl_amd.trainer.context import TrainerContext
+    from easydl_amd.trainer.data import SyntheticTokens
+    from easydl_amd.trainer.elastic import ElasticTrainer
+    from easydl_amd.models.llama import Llama, get_config
+    cfg = get_config("llama-tiny")
+    tr = ElasticTrainer(lambda d: Llama(cfg, device=d, dtype=torch.float32), global_batch=2, micro_batch=1,
+                        device="cpu", ctx=TrainerContext(job="km", run_dir=str(tmp_path)))
+    tr.metrics.every = 5
+    tr.fit(lambda m, b: m(*b), SyntheticTokens(cfg.vocab_size, 32, num_samples=64), num_steps=5)
+    mix = tr.metrics.last["gpu_mix"]
+    assert mix["phases"] == 10 and mix["compute_frac"] > 0.5 and tr.metrics.last["role"] == "worker"
+
+
+@pytest.mark.gpu
+def test_meter_reads_hip_event_times_without_synchronising(cuda):
+    m = KernelMixMeter(cuda, window_s=60)
+    a = torch.randn(8192, 8192, device=cuda, dtype=torch.bfloat16)
+    x = torch.randn(64 << 20, device=cuda)
+    for _ in range(3):
+        with m.phase("compute"):
+            for _ in range(4):
+                a @ a
+        with m.phase("memory"):
+            for _ in range(4):
+                x.mul_(1.0001)
+    torch.cuda.synchronize(cuda)
+    s = m.snapshot()
+    assert s["source"] == "hip-events" and s["phases"] == 6 and s["gpu_s"] > 0
+    # 4 x 1.1 TFLOP of MFMA work vs 4 x 512 MB of streaming: mostly compute
+    assert 0.5 < s["compute_frac"] < 1.0
