@@ -88,6 +88,9 @@ def parse():
                     help="N=1 on a GPU host: also run the time-to-recover drill at this config (auto)")
     ap.add_argument("--ttr-timeout", type=float, default=float(os.environ.get("EDL_TTR_TIMEOUT", 330)),
                     help="seconds the time-to-recover drill may take before it is abandoned")
+    ap.add_argument("--moments", default="auto", choices=["auto", "fp32", "bf16"],
+                    help="AdamW moment dtype; auto = bf16 only when fp32 moments would not fit two full in-memory "
+                         "snapshot slots in this rank's host DRAM (config 5), else fp32")
     ap.add_argument("--child", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
 
@@ -233,7 +236,7 @@ def main():
         model_fn = lambda d: Llama(cfg, device=d, dtype=dtype)  # noqa: E731
     tr = ElasticTrainer(model_fn, lr=3e-4, betas=(0.9, 0.95), weight_decay=0.1,
                         max_grad_norm=1.0, global_batch=gb, micro_batch=B, device=dev, bucket_mb=args.bucket_mb,
-                        checkpoint=ckpt, tp=tp,
+                        checkpoint=ckpt, tp=tp, moment_dtype=args.moments,
                         grad_dtype=torch.float32 if (args.grad_dtype == "fp32" or not use_cuda) else torch.bfloat16)
     marks = {}
 
@@ -293,7 +296,8 @@ def main():
             "parallelism": f"dp{comm.world_size // tp}" + (f"tp{tp}" if tp > 1 else "") + ("sp" if args.sp else ""),
             "micro_batch": B,
             "grad_accum": args.accum,
-            "optimizer": "AdamW fp32 master/moments, clip 1.0",
+            "optimizer": f"AdamW fp32 master, {str(getattr(tr.opt, 'moment_dtype', 'fp32')).replace('torch.', '')}"
+                         " moments, clip 1.0",
             "grad_dtype": str(tr.flat.grad_dtype).replace("torch.", "") if tr.flat is not None else args.grad_dtype,
             "bucket_mb": tr.ddp.bucket_mb,
             "comm": getattr(getattr(comm, "dp", comm), "backend", "local"),
@@ -312,7 +316,8 @@ def main():
         "ckpt": None if ckpt is None else {
             "interval": args.ckpt_interval, "snapshots": ckpt.stats["snapshots"],
             "bytes_per_snapshot": ckpt.stats["d2h_bytes"] // max(1, ckpt.stats["snapshots"]),
-            "pinned": ckpt.pin, "staged_last": ckpt.stats.get("staged_last")},
+            "pinned": ckpt.pin, "staged_last": ckpt.stats.get("staged_last"),
+            "mode": ckpt.mode, "host_budget_gb": ckpt.stats.get("host_budget_gb")},
     }
     if comm.rank == 0:
         line = json.dumps(res)

@@ -33,6 +33,8 @@ c_fp = ctypes.POINTER(ctypes.c_float)
 _KERNEL_SIGS = {
     "edl_adamw_flat": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_i64, c_float, c_float, c_float,
                        c_float, c_float, c_i64, c_float, c_void_p, c_void_p],
+    "edl_adamw_flat_m16": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_i64, c_float, c_float,
+                           c_float, c_float, c_float, c_i64, c_float, c_void_p, c_void_p],
     "edl_sgd_flat": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_i64, c_float, c_float, c_float, c_float,
                      c_void_p, c_void_p],
     "edl_sumsq_nparts": [c_i64],

@@ -73,17 +73,21 @@ def adamw_flat_(param16, master, m, v, grad, *, lr, beta1, beta2, eps, weight_de
     """In-place AdamW over flat buffers.
 
     ``param16``: bf16 model weights (or None when ``master`` is the parameter),
-    ``master``/``m``/``v``: fp32, ``grad``: bf16 or fp32, all the same numel.
+    ``master``: fp32, ``m``/``v``: fp32, or bf16 (stochastically rounded, deterministic in
+    (element, step): see ``edl_adamw_flat_m16``), ``grad``: bf16 or fp32, all the same numel.
     """
     n = master.numel()
+    m16 = m.dtype == torch.bfloat16
+    if m16 != (v.dtype == torch.bfloat16):
+        raise TypeError("m and v must have the same dtype")
     if _native.use_hip(master):
         k = _native.kernels()
         for t in (param16, master, m, v, grad):
             if t is not None and (t.data_ptr() % 16 or not t.is_contiguous()):
                 raise ValueError("flat optimizer buffers must be contiguous and 16-byte aligned")
-        k.check("edl_adamw_flat", _native.ptr(param16), master.data_ptr(), m.data_ptr(), v.data_ptr(),
-                grad.data_ptr(), _gdtype(grad), n, lr, beta1, beta2, eps, weight_decay, int(step), float(scale),
-                _native.ptr(dscale), _native.stream_of(master))
+        k.check("edl_adamw_flat_m16" if m16 else "edl_adamw_flat", _native.ptr(param16), master.data_ptr(),
+                m.data_ptr(), v.data_ptr(), grad.data_ptr(), _gdtype(grad), n, lr, beta1, beta2, eps, weight_decay,
+                int(step), float(scale), _native.ptr(dscale), _native.stream_of(master))
         return
     # reference (same operation order as the kernel / torch.optim.AdamW)
     g = grad.float() * scale
@@ -93,12 +97,47 @@ def adamw_flat_(param16, master, m, v, grad, *, lr, beta1, beta2, eps, weight_de
         g = g * dscale[0]
     bc1 = 1.0 - beta1 ** step
     bc2 = 1.0 - beta2 ** step
-    m.mul_(beta1).add_(g, alpha=1 - beta1)
-    v.mul_(beta2).addcmul_(g, g, value=1 - beta2)
-    denom = v.sqrt() / math.sqrt(bc2) + eps
-    master.mul_(1 - lr * weight_decay).addcdiv_(m, denom, value=-lr / bc1)
+    if m16:
+        mf = m.float().mul_(beta1).add_(g, alpha=1 - beta1)
+        vf = v.float().mul_(beta2).addcmul_(g, g, value=1 - beta2)
+        denom = vf.sqrt() / math.sqrt(bc2) + eps
+        master.mul_(1 - lr * weight_decay).addcdiv_(mf, denom, value=-lr / bc1)
+        base = (int(step) * 0x85EBCA77) & _M32
+        m.copy_(bf16_stochastic(mf, (base + 0x27D4EB2F) & _M32))
+        v.copy_(bf16_stochastic(vf, (base + 0x165667B1) & _M32))
+    else:
+        m.mul_(beta1).add_(g, alpha=1 - beta1)
+        v.mul_(beta2).addcmul_(g, g, value=1 - beta2)
+        denom = v.sqrt() / math.sqrt(bc2) + eps
+        master.mul_(1 - lr * weight_decay).addcdiv_(m, denom, value=-lr / bc1)
     if param16 is not None:
         param16.copy_(master)
+
+
+_M32 = 0xFFFFFFFF
+
+
+def _mix32(x: torch.Tensor) -> torch.Tensor:
+    """lowbias32 on uint32 values held in int64 (products wrap mod 2^64; the low 32 bits are exact)."""
+    x = x ^ (x >> 16)
+    x = (x * 0x7FEB352D) & _M32
+    x = x ^ (x >> 15)
+    x = (x * 0x846CA68B) & _M32
+    return x ^ (x >> 16)
+
+
+def bf16_stochastic(x: torch.Tensor, seed: int) -> torch.Tensor:
+    """fp32 -> bf16 rounded stochastically with the random bits of element e = mix32(e * golden + seed),
+    bit-identical to ``f2bf_sr_bits`` in csrc/kernels/optim.hip (inf / NaN: round to nearest)."""
+    flat = x.detach().reshape(-1).float().contiguous()
+    e = torch.arange(flat.numel(), dtype=torch.int64, device=flat.device)
+    r = _mix32(((e * 0x9E3779B1) & _M32) + seed & _M32) & 0xFFFF
+    u = flat.view(torch.int32).to(torch.int64) & _M32
+    sr = ((u + r) >> 16) & 0xFFFF
+    special = (u & 0x7F800000) == 0x7F800000
+    rne = flat.to(torch.bfloat16).view(torch.int16).to(torch.int64) & 0xFFFF
+    bits = torch.where(special, rne, sr)
+    return bits.to(torch.int32).to(torch.int16).view(torch.bfloat16).reshape(x.shape)
 
 
 def sgd_flat_(param16, master, mom, grad, *, lr, momentum=0.0, weight_decay=0.0, scale=1.0, dscale=None):

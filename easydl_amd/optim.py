@@ -35,16 +35,25 @@ class LRSchedule:
         return dict(lr=self.lr, warmup=self.warmup, total=self.total, min_ratio=self.min_ratio)
 
 
-def _zeros(name: str, g) -> torch.Tensor:
-    """fp32 optimizer state of flat group ``g``: a buffer handed over by the previous worker on
+def _zeros(name: str, g, dtype=torch.float32) -> torch.Tensor:
+    """Optimizer state of flat group ``g``: a buffer handed over by the previous worker on
     this GPU (utils/vram.py, its values kept for an HBM resume), or a new zeroed one."""
-    t = vram.take(name, g.numel, torch.float32, g.data.device, keep=True)
-    return torch.zeros(g.numel, dtype=torch.float32, device=g.data.device) if t is None else t
+    t = vram.take(name, g.numel, dtype, g.data.device, keep=True)
+    return torch.zeros(g.numel, dtype=dtype, device=g.data.device) if t is None else t
 
 
 class FlatAdamW:
+    """``moment_dtype``: fp32 (default) or bf16 moments -- 8 instead of 12 B/param of state,
+    stochastically rounded with deterministic random bits (ops/optim.py bf16_stochastic), so
+    snapshot + resume stays bit-exact; chosen when fp32 moments would not fit two full
+    in-memory snapshot slots in the rank's host DRAM (ElasticTrainer, ``moment_dtype="auto"``)."""
+
     def __init__(self, flat: FlatParams, lr: float = 3e-4, betas=(0.9, 0.95), eps: float = 1e-8,
-                 weight_decay: float | None = None, max_grad_norm: float = 1.0, schedule: LRSchedule | None = None):
+                 weight_decay: float | None = None, max_grad_norm: float = 1.0, schedule: LRSchedule | None = None,
+                 moment_dtype: torch.dtype = torch.float32):
+        if moment_dtype not in (torch.float32, torch.bfloat16):
+            raise ValueError(f"moment_dtype must be float32 or bfloat16, got {moment_dtype}")
+        self.moment_dtype = moment_dtype
         self.flat = flat
         self.lr = lr
         self.beta1, self.beta2 = betas
@@ -69,7 +78,8 @@ class FlatAdamW:
                 master = g.data.float() if master is None else master
             else:
                 master = g.data
-            self.state.append({"master": master, "m": _zeros(f"opt/{g.name}/m", g), "v": _zeros(f"opt/{g.name}/v", g)})
+            self.state.append({"master": master, "m": _zeros(f"opt/{g.name}/m", g, moment_dtype),
+                               "v": _zeros(f"opt/{g.name}/v", g, moment_dtype)})
 
     def current_lr(self) -> float:
         return self.schedule(self.step_count + 1) if self.schedule else self.lr

@@ -59,7 +59,7 @@ class ElasticTrainer:
                  grad_dtype=None, ctx: TrainerContext | None = None, seed: int = 1234,
                  schedule: LRSchedule | None = None,
                  rdzv_config: RendezvousConfig | None = None, checkpoint=None, log_every: int = 0,
-                 store=None, tp: int | None = None):
+                 store=None, tp: int | None = None, moment_dtype: str = "fp32"):
         self.ctx = ctx or TrainerContext.from_env()
         hang = float(os.environ.get("EDL_HANG_DUMP_S", 0) or 0)
         if hang > 0:   # diagnostics: every thread's Python stack to stderr every `hang` seconds
@@ -97,9 +97,12 @@ class ElasticTrainer:
         if optimizer not in ("adamw", "sgd"):
             raise ValueError(f"unknown optimizer {optimizer}")
         self._model_fn, self._seed = model_fn, seed
+        if moment_dtype not in ("fp32", "bf16", "auto"):
+            raise ValueError(f"moment_dtype must be fp32, bf16 or auto, got {moment_dtype}")
         self._opt_args = dict(optimizer=optimizer, lr=lr, weight_decay=weight_decay, betas=betas, momentum=momentum,
                               max_grad_norm=max_grad_norm, schedule=schedule, grad_dtype=grad_dtype,
-                              bucket_mb=bucket_mb)
+                              bucket_mb=bucket_mb, moment_dtype=moment_dtype)
+        self.checkpoint = checkpoint
         # tensor parallelism (Megatron layout inside each DP replica): model_fn(device, tp_group);
         # the model is built at the first epoch, once this process's TP rank is known
         self.tp = int(tp if tp is not None else os.environ.get("EDL_TP", 1))
@@ -107,6 +110,7 @@ class ElasticTrainer:
         self.held_tp = None          # TP rank whose parameter shard this process holds
         self.ckpt_tag = ""
         self.dp_comm = None
+        self.comm = None
         self.model = self.flat = self.bufs = self.opt = self.ddp = None
         if self.tp == 1:
             self._build_model(0)
@@ -166,7 +170,8 @@ class ElasticTrainer:
         self.bufs = FlatBuffers(self.model)
         if a["optimizer"] == "adamw":
             self.opt = FlatAdamW(self.flat, lr=a["lr"], betas=a["betas"], weight_decay=a["weight_decay"],
-                                 max_grad_norm=a["max_grad_norm"], schedule=a["schedule"])
+                                 max_grad_norm=a["max_grad_norm"], schedule=a["schedule"],
+                                 moment_dtype=self._choose_moment_dtype(a["moment_dtype"]))
         else:
             self.opt = FlatSGD(self.flat, lr=a["lr"], momentum=a["momentum"], weight_decay=a["weight_decay"],
                                max_grad_norm=a["max_grad_norm"], schedule=a["schedule"])
@@ -191,6 +196,33 @@ class ElasticTrainer:
             if dropped:
                 log.warning("vram: %d adopted buffers matched nothing and were released: %s", len(dropped),
                             dropped[:8])
+
+    def _choose_moment_dtype(self, want: str) -> torch.dtype:
+        """``auto``: bf16 moments exactly when the host DRAM budget of this rank (ckpt/manager.py
+        host_budget_bytes) holds two FULL snapshot slots with bf16 moments but not with fp32 ones
+        -- e.g. a Llama-3-70B TP=8 shard on an 8-GPU node: 2 x 106 GB > 151 GB >= 2 x 71 GB --
+        so the in-memory snapshots keep the Adam moments instead of going lean (a lean restore
+        restarts them).  The state of a DP replica is sharded over the DP group."""
+        if want != "auto":
+            return torch.bfloat16 if want == "bf16" else torch.float32
+        ck = self.checkpoint
+        if ck is None or not hasattr(ck, "host_budget_bytes"):
+            return torch.float32
+        dp = 1
+        if self.comm is not None:
+            dp = getattr(getattr(self.comm, "dp", None), "world_size", None) or (self.comm.world_size // self.tp)
+        elif self.ctx.static_world:
+            dp = max(1, self.ctx.static_world // self.tp)
+        n = sum(g.numel for g in self.flat.groups)
+        bufs = sum(t.numel() * t.element_size() for t in self.bufs.tensors.values())
+        full32, full16 = (n * 12 + bufs) / dp, (n * 8 + bufs) / dp
+        budget = ck.host_budget_bytes(self)
+        pick = torch.bfloat16 if 2 * full32 > budget >= 2 * full16 else torch.float32
+        if getattr(self, "events", None) is not None:
+            self.events.emit("moment_dtype", dtype=str(pick).replace("torch.", ""), budget_bytes=int(budget),
+                             full_fp32_bytes=int(full32), full_bf16_bytes=int(full16),
+                             budget_gb=round(budget / 2**30, 2), full_fp32_gb=round(full32 / 2**30, 3))
+        return pick
 
     def _connect(self):
         if self.ctx.standalone:

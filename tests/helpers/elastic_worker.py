@@ -30,13 +30,19 @@ ckpt = None
 if os.environ.get("TEST_CKPT"):
     from easydl_amd.ckpt.manager import CheckpointManager  # noqa: E402
     ckpt = CheckpointManager(os.environ["TEST_CKPT_JOB"], interval=int(os.environ["TEST_CKPT"]), pin=False)
-tr = ElasticTrainer(model_fn, global_batch=gb, micro_batch=2, lr=1e-3, device="cpu", checkpoint=ckpt)
+tr = ElasticTrainer(model_fn, global_batch=gb, micro_batch=2, lr=1e-3, device="cpu", checkpoint=ckpt,
+                    moment_dtype=os.environ.get("TEST_MOMENTS", "fp32"))
 tr.fit(lambda m, b: m(*b), SyntheticTokens(cfg.vocab_size, 16, num_samples=4096), num_steps=steps,
        on_step=lambda t, l: time.sleep(float(os.environ.get("TEST_STEP_SLEEP", 0))))
 h = hashlib.sha256()
 for g in (tr.flat.groups if tr.flat is not None else []):
     h.update(g.data.numpy().tobytes())
+hs = hashlib.sha256(h.digest())
+for t in (tr.opt.state_tensors().values() if tr.opt is not None else []):
+    hs.update(t.contiguous().view(torch.uint8).numpy().tobytes())     # master AND moments
 res = {"index": tr.ctx.index, "step": tr.step, "hash": h.hexdigest(), "tp_rank": tr.held_tp,
+       "state_hash": hs.hexdigest(), "snapshot_mode": getattr(ckpt, "mode", None),
+       "moment_dtype": str(getattr(tr.opt, "moment_dtype", "")).replace("torch.", ""),
        "dp_rank": tr.dp_comm.rank if tr.dp_comm is not None else None,
        "worlds": [r["world"] for r in tr.history], "epochs": [r["epoch"] for r in tr.history],
        "loss": float(tr.last_loss) if tr.last_loss is not None else None,

@@ -422,3 +422,61 @@ def test_retire_releases_an_aborted_engine_off_thread():
     _retire(dead)
     assert e_dead.closed.wait(5) and dead.xgmi is None
     assert live.xgmi is e_live and not e_live.closed.is_set()
+
+
+@pytest.mark.slow
+def test_tp_shard_restore_keeps_moments_when_fp32_slots_do_not_fit(tmp_path):
+    """Config 5's host-DRAM squeeze on the CPU tier: the per-rank budget (EDL_CKPT_HOST_GB) holds
+    two full snapshot slots only with bf16 moments (two fp32-moment slots would force LEAN, i.e.
+    a restore that restarts Adam).  moment_dtype=auto picks bf16 moments; the TP shard that loses
+    its only holder restores weights AND moments, and the run ends bit-identical -- every weight,
+    master and moment byte -- to an uninterrupted run of the same configuration."""
+    from easydl_amd.ckpt.manager import unlink_job_segments
+    from easydl_amd.models.llama import get_config
+    cfg = get_config("llama-tiny", n_layers=1, dim=64, n_heads=4, n_kv_heads=2, ffn_dim=128, vocab_size=128)
+    # one TP rank's shard of that model (~half the parameters): 12 B/param fp32-moment slots vs 8 B/param
+    n = sum(p.numel() for p in __import__("easydl_amd.models.llama", fromlist=["Llama"]).Llama(cfg).parameters())
+    budget_gb = 2 * (n / 2 * 10) / 2**30              # between 2 x 8 B and 2 x 12 B per shard parameter
+
+    def run(sub, fault):
+        job = f"tpm{sub}{os.getpid()}"
+        unlink_job_segments(job)
+        out = tmp_path / sub
+        out.mkdir()
+        port = free_port()
+        m = _start_master(out, port, 2, 2, initial=2, granule=2)
+        try:
+            base = {"EDL_MASTER_ADDR": "127.0.0.1", "EDL_MASTER_PORT": str(port), "TEST_STEPS": "8", "TEST_GB": "4",
+                    "EDL_TP": "2", "TEST_CKPT": "2", "TEST_CKPT_JOB": job, "TEST_MOMENTS": "auto",
+                    "EDL_CKPT_HOST_GB": repr(budget_gb)}
+            procs = {i: subprocess.Popen([sys.executable, WORKER], cwd=ROOT, env=_env(
+                out, i, dict(base, EDL_FAULT="kill@step=5,index=1" if (fault and i == 1) else ""))) for i in range(2)}
+            if fault:
+                t_end = time.time() + 240
+                while time.time() < t_end:
+                    rc = procs[1].poll()
+                    if rc is not None:
+                        _report_exit(port, 1, rc)
+                        break
+                    time.sleep(0.05)
+                env = _env(out, 1, dict(base, EDL_GENERATION="1", TEST_OUT=str(out / "res1.json")))
+                procs[1] = subprocess.Popen([sys.executable, WORKER], env=env, cwd=ROOT)
+            codes = _wait(procs)
+            assert codes == {0: 0, 1: 0}, codes
+            res = _results(out, [0, 1])
+            from easydl_amd.utils.events import read_events
+            return res, read_events(str(out))
+        finally:
+            m.terminate()
+            unlink_job_segments(job)
+
+    ref, _ = run("ref", False)
+    got, ev = run("kill", True)
+    for r in list(ref.values()) + list(got.values()):
+        assert r["step"] == 8 and r["moment_dtype"] == "bfloat16" and r["snapshot_mode"] == "full", r
+    md = [e for e in ev if e["kind"] == "moment_dtype"]
+    assert md and all(2 * e["full_fp32_bytes"] > e["budget_bytes"] >= 2 * e["full_bf16_bytes"] for e in md), md
+    rs = [e for e in ev if e["kind"] == "restored"]
+    assert len(rs) == 2 and {e["step"] for e in rs} == {4}, rs
+    by_tp = lambda res: {r["tp_rank"]: r["state_hash"] for r in res.values()}  # noqa: E731
+    assert by_tp(got) == by_tp(ref)          # weights, fp32 master and bf16 moments: bit for bit

@@ -145,6 +145,44 @@ def test_adamw_flat_matches_torch(cuda, gdt):
     _close(p16, ref.detach(), 1e-2)
 
 
+@pytest.mark.gpu
+def test_adamw_bf16_moments_match_the_fp32_reference_and_round_like_the_cpu(cuda):
+    """bf16 moments: the weights follow an fp32-moment AdamW closely (the update uses the
+    unrounded moments), and the stochastically rounded m / v bits equal the CPU reference
+    (ops/optim.py bf16_stochastic): the random bits are a function of (element, step)."""
+    torch.manual_seed(7)
+    n = 4096 * 33
+    w0 = torch.randn(n, device=cuda)
+    master, m, v = w0.clone(), torch.zeros(n, device=cuda, dtype=torch.bfloat16), \
+        torch.zeros(n, device=cuda, dtype=torch.bfloat16)
+    p16 = w0.to(torch.bfloat16)
+    cm, cmm, cvv = w0.cpu().clone(), m.cpu().clone(), v.cpu().clone()
+    ref = torch.nn.Parameter(w0.clone())
+    opt = torch.optim.AdamW([ref], lr=1e-2, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1)
+    for step in range(1, 6):
+        g = torch.randn(n, device=cuda).to(torch.bfloat16)
+        kw = dict(lr=1e-2, beta1=0.9, beta2=0.95, eps=1e-8, weight_decay=0.1, step=step, scale=0.5)
+        adamw_flat_(p16, master, m, v, g, **kw)
+        adamw_flat_(None, cm, cmm, cvv, g.cpu(), **kw)          # CPU reference of the same rounding
+        ref.grad = g.float() * 0.5
+        opt.step()
+    _close(master, ref.detach(), 2e-3)
+    # same random bits as the CPU path: equal wherever the fp32 moment agrees (the GPU contracts
+    # into FMAs, so a few differ in the last fp32 bit and may round the other way: 1 bf16 ulp)
+    for a, b in ((m.cpu(), cmm), (v.cpu(), cvv)):
+        ai, bi = a.view(torch.int16).to(torch.int32), b.view(torch.int16).to(torch.int32)
+        assert (ai == bi).float().mean() > 0.995 and int((ai - bi).abs().max()) <= 1
+    assert torch.allclose(master.cpu(), cm, rtol=1e-5, atol=1e-6)
+    # deterministic: the same update from the same state gives the same bits (resume exactness)
+    st = [t.clone() for t in (p16, master, m, v)]
+    g = torch.randn(n, device=cuda).to(torch.bfloat16)
+    kw = dict(lr=1e-2, beta1=0.9, beta2=0.95, eps=1e-8, weight_decay=0.1, step=6, scale=0.5)
+    adamw_flat_(p16, master, m, v, g, **kw)
+    again = [t.clone() for t in st]
+    adamw_flat_(*again, g, **kw)
+    assert all(torch.equal(x.view(torch.uint8), y.view(torch.uint8)) for x, y in zip((p16, master, m, v), again))
+
+
 def test_grad_clip(cuda):
     torch.manual_seed(6)
     gs = [torch.randn(4096 * 7, device=cuda).to(torch.bfloat16), torch.randn(1024, device=cuda)]
