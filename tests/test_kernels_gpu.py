@@ -170,8 +170,10 @@ def test_adamw_bf16_moments_match_the_fp32_reference_and_round_like_the_cpu(cuda
     # same random bits as the CPU path: equal wherever the fp32 moment agrees (the GPU contracts
     # into FMAs, so a few differ in the last fp32 bit and may round the other way: 1 bf16 ulp)
     for a, b in ((m.cpu(), cmm), (v.cpu(), cvv)):
-        ai, bi = a.view(torch.int16).to(torch.int32), b.view(torch.int16).to(torch.int32)
-        assert (ai == bi).float().mean() > 0.995 and int((ai - bi).abs().max()) <= 1
+        ai, bi = a.view(torch.int16), b.view(torch.int16)
+        assert (ai == bi).float().mean() > 0.995
+        # where they differ: one bf16 ulp apart, or both next to zero (opposite signs)
+        assert torch.allclose(a.float(), b.float(), rtol=2 ** -7, atol=1e-3 * float(b.float().abs().max()))
     assert torch.allclose(master.cpu(), cm, rtol=1e-5, atol=1e-6)
     # deterministic: the same update from the same state gives the same bits (resume exactness)
     st = [t.clone() for t in (p16, master, m, v)]
