@@ -35,6 +35,9 @@ _KERNEL_SIGS = {
                        c_float, c_float, c_i64, c_float, c_void_p, c_void_p],
     "edl_adamw_flat_m16": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_i64, c_float, c_float,
                            c_float, c_float, c_float, c_i64, c_float, c_void_p, c_void_p],
+    "edl_gemm_nt": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
+    "edl_gemm_nt_diag": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                         c_void_p],
     "edl_sgd_flat": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_i64, c_float, c_float, c_float, c_float,
                      c_void_p, c_void_p],
     "edl_sumsq_nparts": [c_i64],

@@ -49,7 +49,12 @@ def main():
     ap.add_argument("--out", default="")
     ap.add_argument("--layouts", action="store_true", help="also time the W^T [in,out] storage variants")
     ap.add_argument("--blas", default="", help="hipblaslt | rocblas (torch.backends.cuda.preferred_blas_library)")
+    ap.add_argument("--select", action="store_true", help="the trainer's GEMM configuration (shipped TunableOp "
+                                                               "selections, easydl_amd/ops/gemm_tuning.py)")
     a = ap.parse_args()
+    if a.select:
+        from easydl_amd.ops import gemm_tuning
+        print(json.dumps({"gemm_tuning": gemm_tuning.apply("select")}), flush=True)
     if a.blas:
         torch.backends.cuda.preferred_blas_library(a.blas)
     if a.tune:
