@@ -90,6 +90,22 @@ def cu_mask_hex(n_cu: int, total: int = 256, start: int = 0) -> str:
     return hex(bits)
 
 
+def hw_queues_capped(gpus: list, standbys: int, per_gpu_queues: int = 8) -> bool:
+    """Whether the job's processes must run with fewer hardware queues each.
+
+    Every process holds HIP's default of 4 hardware queues on each GPU it touches.  A standby
+    touches EVERY GPU of the node (it imports each worker's exported HBM and warms up on each),
+    and a rank's GPU may be shared by several ranks; the contexts on the busiest GPU are
+    therefore ``max ranks per GPU + standbys``.  Past ``per_gpu_queues`` (8: a worker and one
+    standby at 4 each, the N=8 layout) the cap applies to all of them -- standbys included,
+    since they run the replacement in-process."""
+    counts: dict = {}
+    for g in gpus:
+        counts[g] = counts.get(g, 0) + 1
+    busiest = max(counts.values(), default=1)
+    return busiest > 1 or (busiest + max(0, int(standbys))) * 4 > per_gpu_queues
+
+
 class ElasticOperator:
     def __init__(self, job: ElasticJob, run_dir: str, launcher=None, cfg: OperatorConfig | None = None,
                  job_resource: JobResource | None = None, master_argv: list[str] | None = None, kv=None):
@@ -178,13 +194,13 @@ class ElasticOperator:
         if max(self.cfg.standby, getattr(self.job, "standby", 0)) > 0:
             # workers export their state buffers, a standby adopts a dead one's (utils/vram.py)
             env.setdefault("EDL_VRAM_HANDOFF", "1")
-        if len(set(self.cfg.gpus)) < len(self.cfg.gpus):
-            # several ranks share a GPU: every process's streams beyond this many share hardware
-            # queues.  With HIP's default (4 per process) the ranks, standbys and replacements
-            # oversubscribe the queues the scheduler maps at once; it then time-slices whole
-            # processes, and the engine's cross-process barriers stall across slices: world-3
-            # steps of 33-460 ms median after a kill + rejoin, 5.8 ms with 2 queues
-            # (profiles/r04_shared_gpu_rejoin_slowdown.md)
+        if hw_queues_capped(self.cfg.gpus, max(self.cfg.standby, getattr(self.job, "standby", 0))):
+            # too many processes hold a context on one GPU: every process's streams beyond this
+            # many share hardware queues.  With HIP's default (4 per process) the ranks, standbys
+            # and replacements oversubscribe the queues the scheduler maps at once; it then
+            # time-slices whole processes, and the engine's cross-process barriers stall across
+            # slices: world-3 steps of 33-460 ms median after a kill + rejoin, 5.8 ms with 2
+            # queues (profiles/r04_shared_gpu_rejoin_slowdown.md)
             env["GPU_MAX_HW_QUEUES"] = os.environ.get("EDL_SHARED_GPU_HW_QUEUES", "2")
         for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_USE_AGENT_STORE"):
             env.pop(k, None)

@@ -1010,7 +1010,14 @@ class ElasticTrainer:
                                         loss=None, extra=self._metrics_extra)
                     if self.checkpoint is not None:
                         self.checkpoint.on_step(self)
-                    self._run_deferred_probes()
+                    if latest > self.comm.epoch:
+                        # the agreed decision already names a newer epoch (a rejoin, a scale-up):
+                        # a probe of THIS world would be thrown away, and would hold the rejoin
+                        # back by its length (8 s with 7 ranks time-slicing one GPU,
+                        # profiles/r05_world8_shared_gpu.md).  Every rank read the same decision.
+                        self._skip_deferred_probes(latest)
+                    else:
+                        self._run_deferred_probes()
                     self._publish_act()
                     if on_step is not None:
                         on_step(self, loss)
@@ -1047,6 +1054,12 @@ class ElasticTrainer:
         st.sort_stats("tottime").print_stats(25)
         log.warning("first-step host profile (step %d):\n%s", self.step, out.getvalue())
         print(out.getvalue(), file=__import__("sys").stderr, flush=True)
+
+    def _skip_deferred_probes(self, latest: int) -> None:
+        for group, c in self._comm_groups():
+            if getattr(c, "probe_pending", False):
+                self.events.emit("allreduce_probe_skipped", epoch=self.comm.epoch, group=group, step=self.step,
+                                 next_epoch=latest)
 
     def _run_deferred_probes(self) -> None:
         """A re-formed epoch's all-reduce probe, deferred off the recovery path: run after

@@ -370,18 +370,23 @@ def test_early_hand_over_only_when_a_standby_is_ready():
 def test_shared_gpu_layout_limits_hardware_queues(monkeypatch):
     """Ranks sharing a GPU get 2 hardware queues per process (the box's default is 4); a
     one-rank-per-GPU layout keeps the default, so its snapshot and engine streams keep their
-    own queues."""
+    own queues -- unless the standbys (each holds a context on every GPU) push the busiest
+    GPU past 8 queues."""
     from types import SimpleNamespace
 
     from easydl_amd.operator.reconciler import ElasticOperator
     monkeypatch.setenv("GPU_MAX_HW_QUEUES", "4")
 
-    def env_for(gpus):
+    def env_for(gpus, standby=1):
         op = SimpleNamespace(job=SimpleNamespace(env={}, name="j", standby=0), master_port=1, run_dir="/tmp",
-                             cfg=SimpleNamespace(standby=1, gpus=gpus))
+                             cfg=SimpleNamespace(standby=standby, gpus=gpus))
         return ElasticOperator._base_env(op)
 
     assert env_for([0, 0, 0])["GPU_MAX_HW_QUEUES"] == "2"
     assert env_for([0, 1, 2])["GPU_MAX_HW_QUEUES"] == "4"
+    # N=8, one standby holding a context on every GPU: worker + standby = 8 queues per GPU
+    assert env_for(list(range(8)))["GPU_MAX_HW_QUEUES"] == "4"
+    # a second standby would put 12 per GPU: everyone, standbys included, drops to 2
+    assert env_for(list(range(8)), standby=2)["GPU_MAX_HW_QUEUES"] == "2"
     monkeypatch.setenv("EDL_SHARED_GPU_HW_QUEUES", "3")
     assert env_for([0, 0])["GPU_MAX_HW_QUEUES"] == "3"
