@@ -116,6 +116,7 @@ def main(args) -> int:
     fault = next((e for e in ev if e["kind"] == "fault_injected"), None)
     done_ts = [e["ts"] for e in ev if e["kind"] == "step_done" and (fault is None or e["ts"] < fault["ts"])]
     gaps = sorted(b - a for a, b in zip(done_ts, done_ts[1:]))[-8:]   # the last steps before the fault
+    steady = sorted(b - a for a, b in zip(done_ts[2:], done_ts[3:]))     # every step before it, first 3 out
     out = {
         "metric": "time-to-recover after SIGKILL of one worker (Llama elastic DDP, local operator)",
         "value": None if not ttr else ttr["ttr_s"], "unit": "s", "higher_is_better": False,
@@ -128,6 +129,7 @@ def main(args) -> int:
         "time_to_regain_s": ttr.get("time_to_regain_s") if ttr else None,
         "steps_lost": ttr.get("steps_lost") if ttr else None,
         "step_s_before_fault": round(gaps[len(gaps) // 2], 4) if gaps else None,
+        "step_s_median": round(steady[len(steady) // 2], 5) if steady else None,
         "shared_gpu": share, "comm": env.get("EDL_COMM", "pg"), "workers": n,
         "replacement_from_standby": any(e["kind"] == "spawn" and e.get("standby") for e in ev),
         "restored_from": restored[0].get("source") if restored else None,

@@ -1,0 +1,53 @@
+"""The hot standby's warm-up never overlaps a training step of its GPU (VERDICT r4 Next #3).
+
+Two runs of the same one-GPU job (``bench.py --fault-inject`` with no fault reached; Llama-3-8B
+width, 2 layers, seq 8192, 2 micro-batches per step, synced steps): without
+a standby, and with one that imports the worker's exported HBM and runs its full-width warm-up
+on that GPU.  The worker waits for the standby's warm-up before its first step
+(``standby_warm_wait``, ElasticTrainer._publish_warm_spec), so its steady step time is the
+same with and without the standby."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from easydl_amd.utils.events import read_events
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(tmp_path, standby: int):
+    env = dict(os.environ, EDL_TTR_DIR=str(tmp_path), EDL_TTR_KEEP="1", EDL_STEP_SYNC="1")
+    cmd = [sys.executable, "bench.py", "--fault-inject", "--gpus", "1", "--standby", str(standby),
+           "--model", "llama3-8b", "--layers", "2", "--seq", "8192", "--mbs", "1", "--accum", "2", "--steps", "30",
+           "--warmup", "0", "--fault-step", "100000", "--fault-mode", "step_start"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=400)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    d = json.loads(lines[-1]) if lines else {}
+    if d.get("operator_rc") != 0 or not d.get("final_states"):    # (rc 1 = no TTR: no fault was reached)
+        logs = ""
+        for root, _, files in os.walk(d.get("run_dir") or str(tmp_path)):
+            for f in sorted(files):
+                if f.endswith(".log"):
+                    with open(os.path.join(root, f), errors="replace") as fh:
+                        logs += f"--- {f}\n" + "".join(ln for ln in fh.readlines() if "socket.cpp" not in ln)[-2500:]
+        err = "".join(ln + "\n" for ln in r.stderr.splitlines() if "socket.cpp" not in ln)
+        raise AssertionError(f"rc={r.returncode}\n{r.stdout[-1500:]}\n{err[-4000:]}\n{logs[-6000:]}")
+    return d, read_events(d["run_dir"])
+
+
+@pytest.mark.gpu
+def test_standby_warm_up_never_overlaps_a_training_step(tmp_path):
+    d0, ev0 = _run(tmp_path, 0)
+    d1, ev1 = _run(tmp_path, 1)
+    assert not any(e["kind"] == "standby_warm_wait" for e in ev0)
+    wait = [e for e in ev1 if e["kind"] == "standby_warm_wait"]
+    assert wait and wait[0]["warm"], wait            # the standby reported its warm-up done ...
+    first_step = min(e["ts"] for e in ev1 if e["kind"] == "step_done")
+    assert wait[0]["ts"] < first_step                 # ... before the worker's first step
+    ratio = d1["step_s_median"] / d0["step_s_median"]
+    print(json.dumps({"step_s_no_standby": d0["step_s_median"], "step_s_with_standby": d1["step_s_median"],
+                      "ratio": round(ratio, 4), "warm_wait_s": wait[0]["s"]}))
+    assert ratio < 1.03, (d0["step_s_median"], d1["step_s_median"])
