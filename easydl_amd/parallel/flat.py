@@ -191,7 +191,7 @@ class FlatParams:
         # parameter's C++ autograd metadata, which Python's cycle collector cannot traverse, so
         # parameter -> hook -> FlatParams -> parameter was a cycle that was never collected (a
         # standby's warm-up model and its flat buffers stayed allocated: ~7 B/param per warm-up,
-        # scripts/warm_leak_probe3.py).
+        # profiles/r05_ttr_headline.md, "What changed" item 3).
         me = weakref.ref(self)
         for g in self.groups:
             for s in g.slots:
