@@ -49,14 +49,25 @@ def main():
         run_evaluator(lambda d: BertMLM(cfg, device=d, dtype=wdtype), num_ps, score, ctx, interval_s=2.0,
                       device=dev)
     else:
-        w = PSWorker(lambda d: BertMLM(cfg, device=d, dtype=wdtype), num_ps, ctx, device=dev)
+        # async PS: pushes pipelined under the next step (bounded staleness, PSWorker)
+        w = PSWorker(lambda d: BertMLM(cfg, device=d, dtype=wdtype), num_ps, ctx, device=dev,
+                     pipeline=os.environ.get("EDL_PS_PIPELINE", "1") == "1")
         bs = int(os.environ.get("EDL_BATCH", 8))
+        losses = {}
+
+        def on_step(wk, loss):   # first loss now (one sync), the last one kept as a tensor
+            if "first" not in losses:
+                losses["first"] = float(loss.detach())
+            losses["last"] = loss.detach()
+
         t0 = time.perf_counter()
         w.fit(lambda m, b: m(*b), data, batch_size=bs, shard_size=int(os.environ.get("EDL_SHARD", 64)),
-              epochs=1)
+              epochs=1, on_step=on_step)
         dt = time.perf_counter() - t0
         res = {"worker": ctx.index, "steps": w.steps, "samples_per_s": round(w.steps * bs / dt, 2),
-               "transport": w.client.transport}
+               "transport": w.client.transport, "pipeline": w.pipeline, "versions": list(w.client.versions),
+               "first_loss": losses.get("first"),
+               "last_loss": float(losses["last"]) if "last" in losses else None}
         w.events.emit("worker_done", **res)
         print(json.dumps(res), flush=True)
 

@@ -69,6 +69,7 @@ class PSClient:
         self.sparse_cap = int(os.environ.get("EDL_PS_SPARSE_CAP", 65536))
         self._sp_plan: dict = {}
         self.sparse_path = {"ipc_pulls": 0, "ipc_pushes": 0, "tcp_pulls": 0, "tcp_pushes": 0}
+        self._inflight = None    # futures of the pipelined push in flight (push_async)
 
     def bind(self, model: torch.nn.Module) -> None:
         from easydl_amd.ps.embedding import tables_of
@@ -379,10 +380,71 @@ class PSClient:
             self.pull(model)
         return self.versions
 
+    # -- pipelined async pushes (bounded staleness) -------------------------------------
+    # An async PS answers push k as soon as the update that read inbox (k - 1) % 2 has
+    # finished and update k is launched.  So the worker need not wait for the answer before
+    # its next step: it copies whatever the shard holds now (pull_local: at least the version
+    # of push k - 2, usually k - 1) and sends push k + 1 once the answer to push k is in --
+    # which is also what frees the inbox push k + 1 overwrites.  The PS's update of step k
+    # then runs under the worker's step k + 1 instead of between the two.
+    def pipelined(self) -> bool:
+        return self.transport == "ipc" and not self.tables
+
+    def push_async(self, model: torch.nn.Module, step: int = 0) -> None:
+        """Enqueue this step's push (inbox copies and flag stores on the current stream) and
+        send its control messages from the pool; returns at once.  Waits first for the
+        previous push's answers (their inbox slot is the one this push writes)."""
+        if not self.pipelined():
+            raise RuntimeError("push_async needs the GPU transport and a dense model")
+        self.drain()
+        params = dict(model.named_parameters())
+        slots = [self._push_launch(i, params) for i in range(self.num_ps)]
+        dev = next(iter(params.values())).device
+        stream = torch.cuda.current_stream(dev)
+        seqs = [None] * self.num_ps
+        if all(self._ipc[i].get("flag") is not None for i in range(self.num_ps)):
+            from easydl_amd.ops.sparse import ps_signal
+            for i in range(self.num_ps):
+                m = self._ipc[i]
+                m["seq"] += 1
+                seqs[i] = m["seq"]
+                ps_signal(m["flag"], m["seq"], stream)
+        ready = torch.cuda.Event()
+        ready.record(stream)
+
+        def one(i):
+            ready.synchronize()     # the message leaves once the stream passed the flag stores
+            hdr = {"op": "push_ipc", "worker": self.worker_id, "step": step, "slot": slots[i], "pull": False,
+                   "sparse_ipc": False, "seq": seqs[i]}
+            h, _ = self._call(i, hdr, {})
+            return h["version"]
+
+        self._inflight = [self._pool.submit(one, i) for i in range(self.num_ps)]
+
+    def drain(self) -> list[int]:
+        """Wait for the answers to the push in flight (if any); returns the shard versions."""
+        fl, self._inflight = getattr(self, "_inflight", None), None
+        if fl:
+            self.versions = [f.result() for f in fl]
+        return self.versions
+
+    def pull_local(self, model: torch.nn.Module) -> None:
+        """Copy every shard's current parameters into ``model`` (one kernel per shard on the
+        current stream, no control message).  Async semantics: an update of the shard may be
+        running meanwhile, so the copy holds each parameter word of version >= the last
+        answered push - 1."""
+        params = dict(model.named_parameters())
+        for i in range(self.num_ps):
+            self._pull_launch(i, params)
+
     def stats(self) -> list[dict]:
         return [self._call(i, {"op": "stats"})[0] for i in range(self.num_ps)]
 
     def close(self):
+        try:
+            self.drain()
+        except Exception:  # noqa: BLE001 - closing: the PS may be gone
+            pass
         for s in self._socks.values():
             try:
                 s.close()

@@ -95,7 +95,8 @@ class ParameterServer:
                  betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0, momentum: float = 0.9,
                  mode: str = "async", expected_workers=None, host: str = "127.0.0.1", port: int = 0,
                  device="cpu", snapshot=None, snapshot_every: int = 50, tables: dict[str, dict] | None = None,
-                 sparse_optimizer: str | None = None, sparse_lr: float | None = None, seed: int = 1234):
+                 sparse_optimizer: str | None = None, sparse_lr: float | None = None, seed: int = 1234,
+                 snapshot_min_s: float = 0.0):
         self.index = index
         self.state = ShardState(tensors, device)
         # row-sparse embedding stripes (easydl_amd/ps/embedding.py), lazily updated
@@ -128,6 +129,11 @@ class ParameterServer:
         self.stats = {"pushes": 0, "pulls": 0, "applied": 0, "workers": set()}
         self.snapshot = snapshot
         self.snapshot_every = snapshot_every
+        # ... and at least this many seconds apart: a snapshot copies the whole shard state (4 GB
+        # for BERT-large) to host DRAM, which on a GPU shared with workers costs copy kernels
+        # beside their steps (profiles/r05_ps_per_gpu.md)
+        self.snapshot_min_s = snapshot_min_s
+        self._last_snap_t = 0.0
         self.push_wait_s = 30.0
         self._srv = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
         self._srv.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
@@ -177,7 +183,9 @@ class ParameterServer:
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream(st.device))
             self._apply_ev = ev
-        if self.snapshot is not None and self.version % self.snapshot_every == 0:
+        if self.snapshot is not None and self.snapshot_every > 0 and self.version % self.snapshot_every == 0 \
+                and time.monotonic() - self._last_snap_t >= self.snapshot_min_s:
+            self._last_snap_t = time.monotonic()
             self.snapshot(self)
         self.lock.notify_all()
 
@@ -494,9 +502,38 @@ class PSSnapshotter:
         self.engine = None
         self.ticket = None
         self._keep = None
+        self._prep = None
+
+    def prepare(self, ps: ParameterServer) -> None:
+        """Create, pin and pre-fault the snapshot segment (and the copy engine) of an HBM shard
+        on a background thread, so that the first snapshot does not stall the updates: mapping
+        and pinning 2 x 4 GB (BERT-large) took seconds inside the first snapshot, while every
+        worker's push waited (profiles/r05_ps_per_gpu.md)."""
+        bufs = ps.state_buffers()
+        if not bufs or not bufs[0].is_cuda or self.seg is not None:
+            return
+        nbytes = sum(b.numel() * 4 for b in bufs) + 8
+        dev = bufs[0].device
+
+        def run():
+            from easydl_amd.ckpt.manager import CheckpointManager, ShmSegment
+            try:
+                torch.cuda.set_device(dev)
+                seg = ShmSegment(self.name, nbytes, create=True, pin=True)
+                seg.populate_async(8)
+                self.engine = self.engine or CheckpointManager._make_engine(dev.index or 0)
+                self.seg = seg
+            except Exception as e:  # noqa: BLE001 - the first snapshot creates it then
+                log.warning("PS snapshot segment preparation failed: %s", e)
+
+        self._prep = threading.Thread(target=run, name="ps-snap-prep", daemon=True)
+        self._prep.start()
 
     def __call__(self, ps: ParameterServer) -> None:
         from easydl_amd.ckpt.manager import ShmSegment, checksum_np
+        if self._prep is not None:
+            self._prep.join()
+            self._prep = None
         bufs = ps.state_buffers()
         sizes = [b.numel() * 4 for b in bufs]
         total_bytes = sum(sizes)

@@ -41,8 +41,17 @@ def _world(kv) -> int:
 
 
 def run_ps(model_fn, num_ps: int, ctx: TrainerContext | None = None, *, optimizer="adam", lr=1e-3, mode="async",
-           snapshot_every: int = 20, device="cpu", seed: int = 1234, sparse_optimizer: str | None = None,
+           snapshot_every: int | None = None, device="cpu", seed: int = 1234, sparse_optimizer: str | None = None,
            sparse_lr: float | None = None) -> None:
+    """``snapshot_every``: updates between in-memory snapshots of the shard (EDL_PS_SNAPSHOT_EVERY,
+    default 20; 0 = none), and for a GPU shard at least EDL_PS_SNAPSHOT_S seconds apart (default
+    5).  Each snapshot copies the whole shard state to host DRAM, which a PS sharing its GPU pays
+    in copy kernels beside the workers: every 20 updates cost BERT-large 28 % of a per-GPU
+    layout's throughput (profiles/r05_ps_per_gpu.md).  Async SGD loses at most those seconds of
+    updates on a PS failure."""
+    if snapshot_every is None:
+        snapshot_every = int(os.environ.get("EDL_PS_SNAPSHOT_EVERY", 20))
+    snapshot_min_s = float(os.environ.get("EDL_PS_SNAPSHOT_S", 5.0 if torch.device(device).type == "cuda" else 0))
     ctx = ctx or TrainerContext.from_env()
     kv = _kv(ctx)
     events = EventLog(os.path.join(ctx.run_dir, f"events-ps{ctx.index}.jsonl"), proc=f"ps{ctx.index}")
@@ -52,12 +61,15 @@ def run_ps(model_fn, num_ps: int, ctx: TrainerContext | None = None, *, optimize
     snap = PSSnapshotter(ctx.job, ctx.index)
     ps = ParameterServer(ctx.index, shard_of(model, num_ps, ctx.index), optimizer=optimizer, lr=lr, mode=mode,
                          expected_workers=lambda: _world(kv), device=device, snapshot=snap,
-                         snapshot_every=snapshot_every, tables=table_shard_spec(model, num_ps, ctx.index),
+                         snapshot_every=snapshot_every, snapshot_min_s=snapshot_min_s,
+                         tables=table_shard_spec(model, num_ps, ctx.index),
                          sparse_optimizer=sparse_optimizer, sparse_lr=sparse_lr, seed=seed)
     del model  # the PS keeps only its shard
     handoff = _await_predecessor(kv, ctx.index, gen, events)
     if snap.restore(ps):
         events.emit("ps_restored", version=ps.version, handoff=handoff)
+    if snapshot_every > 0:
+        snap.prepare(ps)
     ps.start()
     kv.set(f"ps/addr/{ctx.index}", json.dumps({"host": ps.host, "port": ps.port, "pid": os.getpid(), "gen": gen}))
     events.emit("ps_started", port=ps.port, params=ps.state.numel, gen=gen)
@@ -125,7 +137,13 @@ def _transport(device) -> str:
 
 
 class PSWorker:
-    def __init__(self, model_fn, num_ps: int, ctx: TrainerContext | None = None, device="cpu", seed: int = 1234):
+    def __init__(self, model_fn, num_ps: int, ctx: TrainerContext | None = None, device="cpu", seed: int = 1234,
+                 pipeline: bool | None = None):
+        """``pipeline`` (async PS only; EDL_PS_PIPELINE): with the GPU transport and a dense
+        model, each step's push is sent without waiting for its answer and the next step
+        starts from the shard's current parameters (bounded staleness: at most 2 updates
+        behind, usually 1), so the PS update runs under the worker's next step
+        (PSClient.push_async)."""
         self.ctx = ctx or TrainerContext.from_env()
         self.device = torch.device(device)
         torch.manual_seed(seed)
@@ -140,6 +158,9 @@ class PSWorker:
         self.fault = fault.FaultInjector.from_env(self.ctx, self.events)
         self.steps = 0
         self._phase = [0.0, 0.0, 0.0]
+        if pipeline is None:
+            pipeline = os.environ.get("EDL_PS_PIPELINE", "0") == "1"
+        self.pipeline = bool(pipeline) and self.client.pipelined()
 
     def fit(self, loss_fn, data, batch_size: int, shard_size: int, epochs: int = 1, on_step=None):
         self.rdzv.join()
@@ -160,6 +181,9 @@ class PSWorker:
                     t0 = time.perf_counter()
                     if need_pull:
                         self.client.pull(self.model)
+                        need_pull = False
+                    elif self.pipeline:
+                        self.client.pull_local(self.model)
                     t1 = time.perf_counter()
                     self.model.zero_grad(set_to_none=False)
                     loss = loss_fn(self.model, data.batch(range(b0, min(hi, b0 + batch_size)), self.device))
@@ -169,8 +193,11 @@ class PSWorker:
                         # transport otherwise never synchronises the stream on the main thread
                         torch.cuda.current_stream(self.device).synchronize()
                     t2 = time.perf_counter()
-                    self.client.push(self.model, self.steps, then_pull=fused)
-                    need_pull = not fused
+                    if self.pipeline:
+                        self.client.push_async(self.model, self.steps)
+                    else:
+                        self.client.push(self.model, self.steps, then_pull=fused)
+                        need_pull = not fused
                     t3 = time.perf_counter()
                     self.steps += 1
                     self._phase = [a + b for a, b in zip(self._phase, (t1 - t0, t2 - t1, t3 - t2))]
@@ -181,6 +208,8 @@ class PSWorker:
                         self._phase = [0.0, 0.0, 0.0]
                     if on_step is not None:
                         on_step(self, loss)
+                if self.pipeline:
+                    self.client.drain()   # a shard is done once its last push is answered
                 disp.complete(shard)
                 self.events.emit("shard_done", shard=shard, steps=self.steps)
                 if self.kv.exists(f"rdzv/leave/{self.ctx.node_id}"):
@@ -188,6 +217,11 @@ class PSWorker:
                     self.events.emit("worker_left", steps=self.steps)
                     break
         finally:
+            if self.pipeline:
+                try:
+                    self.client.drain()
+                except Exception as e:  # noqa: BLE001 - leaving anyway; the PS side logs it
+                    log.warning("last pipelined push not answered: %s", e)
             self.rdzv.leave()
             self.rdzv.stop_heartbeat()
         if disp.done() >= disp.total:

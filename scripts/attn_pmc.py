@@ -9,7 +9,7 @@ os.environ["EDL_ATTN"] = "hip"
 from easydl_amd.ops.attention import flash_attention  # noqa: E402
 
 dev = torch.device("cuda", 0)
-B, S, H, KV = 1, int(os.environ.get("S", 8192)), 32, 8
+B, S, H, KV = int(os.environ.get("B", 2)), int(os.environ.get("S", 8192)), 32, 8
 q = torch.randn(B, S, H, 128, device=dev, dtype=torch.bfloat16).transpose(1, 2).requires_grad_()
 k = torch.randn(B, S, KV, 128, device=dev, dtype=torch.bfloat16).transpose(1, 2).requires_grad_()
 v = torch.randn(B, S, KV, 128, device=dev, dtype=torch.bfloat16).transpose(1, 2).requires_grad_()
