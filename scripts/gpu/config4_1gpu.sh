@@ -4,7 +4,7 @@
 # every role sharing GPU 0 (--gpus 0,...,0), PS traffic over the IPC transport.
 set -u
 mkdir -p gpurun_out
-OUT=gpurun_out/bert_ps_1gpu
+OUT=gpurun_out/${TAG:-config4_1gpu}
 rm -rf $OUT
 python - <<'PY' > /tmp/bert_ps_1gpu.yaml
 import yaml
@@ -30,4 +30,17 @@ p = rocprof_rank_profiles('$OUT')
 print(json.dumps({k: dict(v, planned_cu=Planner.cu_for_profile(v)) for k, v in p.items()}))
 " > $OUT/rocprof_profiles.json
 cat $OUT/rocprof_profiles.json
+# steady aggregate: per worker, batch / (pull + compute + push) over its ps_step_phases windows
+# after the first one, summed over the workers (profiles/r04_bert_ps_flag_wait.md "Method")
+python - $OUT <<'PY'
+import glob, json, sys
+tot, per = 0.0, {}
+for f in sorted(glob.glob(f"{sys.argv[1]}/events-worker*.jsonl")):
+    ph = [json.loads(l) for l in open(f) if '"ps_step_phases"' in l][1:]
+    if ph:
+        step = sum(p["pull_s"] + p["compute_s"] + p["push_s"] for p in ph) / len(ph)
+        per[f.rsplit("events-", 1)[1][:-6]] = round(8 / step, 1)
+        tot += 8 / step
+print(json.dumps({"steady_aggregate_samples_per_s": round(tot, 1), "per_worker": per}))
+PY
 exit $rc

@@ -168,12 +168,17 @@ def test_adamw_bf16_moments_match_the_fp32_reference_and_round_like_the_cpu(cuda
         opt.step()
     _close(master, ref.detach(), 2e-3)
     # same random bits as the CPU path: equal wherever the fp32 moment agrees (the GPU contracts
-    # into FMAs, so a few differ in the last fp32 bit and may round the other way: 1 bf16 ulp)
+    # into FMAs, so a few differ in the last fp32 bit and may round the other way)
     for a, b in ((m.cpu(), cmm), (v.cpu(), cvv)):
         ai, bi = a.view(torch.int16), b.view(torch.int16)
         assert (ai == bi).float().mean() > 0.995
-        # where they differ: one bf16 ulp apart, or both next to zero (opposite signs)
-        assert torch.allclose(a.float(), b.float(), rtol=2 ** -7, atol=1e-3 * float(b.float().abs().max()))
+        # where they differ: a few bf16 ulps apart (a 1-ulp split at one step is carried and may
+        # round apart again at the next), or both next to zero with opposite signs
+        tiny = 1e-3 * float(b.float().abs().max())
+        near_zero = (a.float().abs() <= tiny) & (b.float().abs() <= tiny)
+        ulps = (ai.int() - bi.int()).abs()
+        far = (ulps > 4) & ((ai < 0) == (bi < 0)) | ((ai < 0) != (bi < 0))
+        assert int((far & ~near_zero).sum()) == 0, (int((far & ~near_zero).sum()), int(ulps[~near_zero].max()))
     assert torch.allclose(master.cpu(), cm, rtol=1e-5, atol=1e-6)
     # deterministic: the same update from the same state gives the same bits (resume exactness)
     st = [t.clone() for t in (p16, master, m, v)]
