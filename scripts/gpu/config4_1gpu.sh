@@ -15,7 +15,7 @@ from easydl_amd.master.features import extract
 job, _ = load_specs("examples/bert_ps.yaml")
 inv = NodeInventory(gpus=[GpuInfo(i, "gfx950", 256, 288.0) for i in range(8)], cpus=128, host_mem_gb=2048)
 plan = Planner().startup_plan(JobFeatures.from_dict(extract(job)), inv)
-job.env.update({"EDL_SAMPLES": "3072", "EDL_SHARD": "64", "EDL_ROCPROF_ROLES": "parameter_server"})
+job.env.update({"EDL_SAMPLES": "12288", "EDL_SHARD": "64", "EDL_ROCPROF_ROLES": "parameter_server"})
 jr = JobResource(f"{job.name}-resource", job.name, plan.roles)
 print(yaml.safe_dump_all([job.to_dict(), jr.to_dict()]))
 PY
@@ -30,17 +30,19 @@ p = rocprof_rank_profiles('$OUT')
 print(json.dumps({k: dict(v, planned_cu=Planner.cu_for_profile(v)) for k, v in p.items()}))
 " > $OUT/rocprof_profiles.json
 cat $OUT/rocprof_profiles.json
-# steady aggregate: per worker, batch / (pull + compute + push) over its ps_step_phases windows
-# after the first one, summed over the workers (profiles/r04_bert_ps_flag_wait.md "Method")
+# steady aggregate: samples of the 16-step ps_step_phases windows that end while EVERY worker is
+# still running (from the latest first-window end to the earliest last-window end), divided by that
+# span.  Workers claim shards dynamically, so their step counts differ and a sum of per-worker
+# rates would count the tail, when fewer workers share the GPU, as if it were concurrent.
 python - $OUT <<'PY'
 import glob, json, sys
-tot, per = 0.0, {}
+ends = {}
 for f in sorted(glob.glob(f"{sys.argv[1]}/events-worker*.jsonl")):
-    ph = [json.loads(l) for l in open(f) if '"ps_step_phases"' in l][1:]
-    if ph:
-        step = sum(p["pull_s"] + p["compute_s"] + p["push_s"] for p in ph) / len(ph)
-        per[f.rsplit("events-", 1)[1][:-6]] = round(8 / step, 1)
-        tot += 8 / step
-print(json.dumps({"steady_aggregate_samples_per_s": round(tot, 1), "per_worker": per}))
+    ends[f] = [json.loads(l)["ts"] for l in open(f) if '"ps_step_phases"' in l]
+ends = {f: v for f, v in ends.items() if v}
+t0, t1 = max(min(v) for v in ends.values()), min(max(v) for v in ends.values())
+n = sum(16 * 8 for v in ends.values() for t in v if t0 < t <= t1)
+print(json.dumps({"steady_aggregate_samples_per_s": round(n / (t1 - t0), 1) if t1 > t0 else None,
+                  "window_s": round(t1 - t0, 2), "workers": len(ends)}))
 PY
 exit $rc
