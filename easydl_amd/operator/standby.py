@@ -29,6 +29,7 @@ import json
 import os
 import runpy
 import sys
+import threading
 import time
 
 
@@ -70,9 +71,10 @@ def _llama_warm_bytes(cfg, tokens: int) -> int:
 
 
 WARM_INFO: dict = {}     # what the last warm_device did (logged by the standby)
+WARM_STREAMS: dict = {}  # GPU -> the stream its warm-up ran on (the replacement's trainer keeps it)
 
 
-def _warm_llama(dev, spec: dict) -> bool:
+def _warm_llama(dev, spec: dict, info: dict | None = None) -> bool:
     """Forward + backward of one layer of the worker's model at its micro-batch shape, with its
     parameters in flat buffers as the trainer has them (parallel/flat.py: weight gradients are
     GEMMs accumulating into the flat gradient buffer, a different hipBLASLt solution than a
@@ -87,7 +89,7 @@ def _warm_llama(dev, spec: dict) -> bool:
     b, s = (int(x) for x in spec["batch"])
     free, _ = torch.cuda.mem_get_info(dev)
     need = _llama_warm_bytes(cfg, b * s)
-    WARM_INFO.update(free_gb=round(free / 2**30, 1), need_gb=round(need / 2**30, 1))
+    (WARM_INFO if info is None else info).update(free_gb=round(free / 2**30, 1), need_gb=round(need / 2**30, 1))
     if free < 2 * need + (4 << 30):
         return False
     from easydl_amd.parallel.flat import FlatParams
@@ -101,7 +103,7 @@ def _warm_llama(dev, spec: dict) -> bool:
     return True
 
 
-def warm_device(gpu: int, spec: dict | None = None, set_stream: bool = False) -> float:
+def warm_device(gpu: int, spec: dict | None = None, set_stream: bool = False, info: dict | None = None) -> float:
     """One forward + backward + optimizer step of a small Llama of head dim 128 on ``gpu``,
     preceded, when the worker published its shape (``spec``, ElasticTrainer._publish_warm_spec),
     by a forward + backward of one layer of its model at full width.
@@ -129,14 +131,17 @@ def warm_device(gpu: int, spec: dict | None = None, set_stream: bool = False) ->
     # workspace; the process's current stream stays set)
     gemm_tuning.apply()
     if set_stream and torch.cuda.current_stream(dev).cuda_stream == 0:
-        torch.cuda.set_stream(torch.cuda.Stream(dev))
+        # (the current stream is per thread: a warm-up thread records it for the takeover)
+        WARM_STREAMS[gpu] = torch.cuda.Stream(dev)
+        torch.cuda.set_stream(WARM_STREAMS[gpu])
     cfg = LlamaConfig(vocab_size=1024, dim=512, n_layers=1, n_heads=4, n_kv_heads=2, ffn_dim=1024, max_seq_len=256)
+    wi = WARM_INFO if info is None else info
     with torch.cuda.device(dev):
-        WARM_INFO.clear()
+        wi.clear()
         if spec and spec.get("model") == "llama":
             t1 = time.perf_counter()
-            WARM_INFO["full_width"] = _warm_llama(dev, spec)
-            WARM_INFO["full_width_s"] = round(time.perf_counter() - t1, 3)
+            wi["full_width"] = _warm_llama(dev, spec, wi)
+            wi["full_width_s"] = round(time.perf_counter() - t1, 3)
         model = Llama(cfg, device=dev)
         flat = FlatParams(model)
         opt = FlatAdamW(flat)
@@ -149,6 +154,19 @@ def warm_device(gpu: int, spec: dict | None = None, set_stream: bool = False) ->
         gc.collect()    # (see _warm_llama): otherwise the state stays allocated until a GC cycle
         torch.cuda.empty_cache()
     return time.perf_counter() - t0
+
+
+def _warm_one(kv, name: str, gpu: int, spec) -> None:
+    """Warm-up of one GPU (a thread of the parked standby); its key tells the worker it is done."""
+    info: dict = {}
+    try:
+        s = round(warm_device(gpu, spec, set_stream=True, info=info), 3)
+        info = dict(s=s, spec=spec is not None, **info)
+        kv.set(f"standby/warm/{name}/gpu{gpu}", json.dumps(info))
+        print(f"standby {name}: warm-up on GPU {gpu}: {json.dumps(info)}", file=sys.stderr, flush=True)
+    except Exception as e:  # noqa: BLE001 - an optimisation only
+        print(f"standby: warm-up on GPU {gpu} failed: {e}", file=sys.stderr)
+        kv.set(f"standby/warm/{name}/gpu{gpu}", json.dumps({"error": str(e)[:200]}))
 
 
 def _import_vram(kv, held: dict) -> None:
@@ -208,7 +226,8 @@ def main() -> int:
     premap = os.environ.get("EDL_STANDBY_PREMAP", "0") == "1"
     handoff = vram.enabled() and info.get("gpus", 0) > 0
     held: dict[str, dict] = {}     # worker slot -> imported state buffers (utils/vram.py)
-    warmed: set[int] = set()       # GPUs this standby has run its warm-up step on
+    warmed: set[int] = set()       # GPUs this standby has run (or is running) its warm-up step on
+    warming: list = []             # their warm-up threads
     warm_on = os.environ.get("EDL_STANDBY_WARMUP", "1") != "0"
     next_scan = next_vram = 0.0
     while True:
@@ -229,17 +248,14 @@ def main() -> int:
                     continue
                 published, spec = vram.read_warm(kv, slot)
                 if not published:
-                    continue            # the worker has not finished its first step yet
+                    continue            # the worker has not published its shape yet
                 warmed.add(h["gpu"])
-                try:
-                    s = round(warm_device(h["gpu"], spec, set_stream=True), 3)
-                    info = dict(s=s, spec=spec is not None, **WARM_INFO)
-                    kv.set(f"standby/warm/{name}/gpu{h['gpu']}", json.dumps(info))
-                    print(f"standby {name}: warm-up on GPU {h['gpu']}: {json.dumps(info)}", file=sys.stderr,
-                          flush=True)
-                except Exception as e:  # noqa: BLE001 - an optimisation only
-                    print(f"standby: warm-up on GPU {h['gpu']} failed: {e}", file=sys.stderr)
-                    kv.set(f"standby/warm/{name}/gpu{h['gpu']}", json.dumps({"error": str(e)[:200]}))
+                # one thread per GPU: at N=8 every worker waits for its own GPU's warm-up before its
+                # first step, and eight warm-ups in a row would hold the last one back ~8 x 1.3 s
+                t = threading.Thread(target=_warm_one, args=(kv, name, h["gpu"], spec), daemon=True,
+                                     name=f"warm-gpu{h['gpu']}")
+                t.start()
+                warming.append(t)
         if premap and time.monotonic() > next_scan:
             from easydl_amd.ckpt.manager import premap_job_segments
             mapped = premap_job_segments(job)
@@ -247,8 +263,14 @@ def main() -> int:
                 kv.set(f"standby/premapped/{name}", json.dumps(mapped))
             next_scan = time.monotonic() + 2.0
         time.sleep(0.005)
+    for t in warming:   # a takeover right after start-up: let the warm-ups finish first
+        t.join()
     a = a if isinstance(a, dict) else json.loads(a)
     os.environ.update({k: str(v) for k, v in a["env"].items()})
+    gpu = a["env"].get("EDL_GPU")
+    if gpu is not None and int(gpu) in WARM_STREAMS:
+        import torch
+        torch.cuda.set_stream(WARM_STREAMS[int(gpu)])   # the stream the warm-up ran on (its hipBLASLt workspace)
     if handoff:
         _adopt_vram(held, f"worker{a['env'].get('EDL_INDEX', '')}", kv, name)
     argv = a["argv"]
