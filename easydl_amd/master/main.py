@@ -61,11 +61,35 @@ class JobMaster:
                 info = self.kv.get(f"ev/exit/{n}")
                 self.rdzv.mark_dead(n, f"process exit {info}")
 
+    def _grant_warm_windows(self) -> None:
+        """A parked standby's request for a warm-up window (utils/vram.py) becomes a runtime plan
+        with a ``warm_window``: every rank applies it at one committed step, the ranks on its
+        GPUs pause for the warm-up, and no warm-up GEMM runs beside a training step."""
+        now = time.monotonic()
+        if now < getattr(self, "_next_warm_scan", 0.0):
+            return
+        self._next_warm_scan = now + 0.5
+        from easydl_amd.utils import vram
+        done = self.__dict__.setdefault("_warm_granted", set())
+        for name in vram.roster(self.kv):
+            req = vram.read_warm_request(self.kv, name)
+            if not req or (name, req["id"]) in done:
+                continue
+            done.add((name, req["id"]))
+            cur = self.kv.counter("plan/version")
+            doc = self.kv.get(f"plan/runtime/{cur}") if cur else None
+            doc = dict(doc) if isinstance(doc, dict) else {}
+            doc["warm_window"] = {"standby": name, "id": req["id"], "gpus": req["gpus"]}
+            self.kv.set(f"plan/runtime/{cur + 1}", json.dumps(doc))
+            self.kv.add("plan/version", 1)
+            self.events.emit("warm_window_planned", standby=name, id=req["id"], gpus=req["gpus"], version=cur + 1)
+
     def _loop(self, period):
         while not self._stop.is_set():
             try:
                 self._scan_exit_events()
                 self.rdzv.tick()
+                self._grant_warm_windows()
                 if self.planner is not None:
                     self.planner.maybe_replan(self)
             except Exception as e:

@@ -228,6 +228,9 @@ def main() -> int:
     held: dict[str, dict] = {}     # worker slot -> imported state buffers (utils/vram.py)
     warmed: set[int] = set()       # GPUs this standby has run (or is running) its warm-up step on
     warming: list = []             # their warm-up threads
+    late: dict = {}                # GPU -> warm spec, waiting for a window (its worker already trains)
+    requested: set = set()         # GPUs of the window request filed
+    req_id = 0
     warm_on = os.environ.get("EDL_STANDBY_WARMUP", "1") != "0"
     next_scan = next_vram = 0.0
     while True:
@@ -240,7 +243,9 @@ def main() -> int:
             _import_vram(kv, held)
             next_vram = time.monotonic() + 0.25   # a worker waits for this warm-up before its first step
             for slot, h in sorted(held.items()):
-                if not h or not h.get("tensors") or h["gpu"] in warmed:
+                # (a worker's export may hold no tensors -- a replacement that itself adopted HBM
+                # re-publishes only what it can: the warm-up of its GPU still applies)
+                if not h or h["gpu"] in warmed:
                     continue
                 if not warm_on:
                     warmed.add(h["gpu"])
@@ -249,6 +254,12 @@ def main() -> int:
                 published, spec = vram.read_warm(kv, slot)
                 if not published:
                     continue            # the worker has not published its shape yet
+                if vram.trained(kv, slot):
+                    # that worker trains already (this standby is a refill after a takeover):
+                    # warm up only in a window between two of its steps (utils/vram.py)
+                    late[h["gpu"]] = spec
+                    warmed.add(h["gpu"])
+                    continue
                 warmed.add(h["gpu"])
                 # one thread per GPU: at N=8 every worker waits for its own GPU's warm-up before its
                 # first step, and eight warm-ups in a row would hold the last one back ~8 x 1.3 s
@@ -256,6 +267,16 @@ def main() -> int:
                                      name=f"warm-gpu{h['gpu']}")
                 t.start()
                 warming.append(t)
+            if late and set(late) != requested:
+                requested = set(late)
+                req_id += 1
+                vram.request_warm_window(kv, name, req_id, requested)
+            for g in sorted(late):
+                if kv.exists(f"standby/warm_grant/{name}/gpu{g}"):
+                    t = threading.Thread(target=_warm_one, args=(kv, name, g, late.pop(g)), daemon=True,
+                                         name=f"warm-gpu{g}")
+                    t.start()
+                    warming.append(t)
         if premap and time.monotonic() > next_scan:
             from easydl_amd.ckpt.manager import premap_job_segments
             mapped = premap_job_segments(job)
@@ -265,6 +286,7 @@ def main() -> int:
         time.sleep(0.005)
     for t in warming:   # a takeover right after start-up: let the warm-ups finish first
         t.join()
+    kv.delete(f"standby/warm_req/{name}")
     a = a if isinstance(a, dict) else json.loads(a)
     os.environ.update({k: str(v) for k, v in a["env"].items()})
     gpu = a["env"].get("EDL_GPU")

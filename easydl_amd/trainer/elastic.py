@@ -120,6 +120,7 @@ class ElasticTrainer:
         self.global_batch = global_batch
         self.micro_batch = micro_batch
         self.step = 0                # committed optimizer steps
+        self._warm_windows: set = set()   # (standby, request id) warm-up windows granted
         self._warm_published = False
         self._act_published = False
         self.needs_state = True     # fresh process: must receive state unless everyone is fresh
@@ -648,8 +649,8 @@ class ElasticTrainer:
         before it is needed.  Published before this worker's first step, and the worker waits
         for that warm-up (bounded, ``EDL_WARM_WAIT_S``, default 60 s): a warm-up never runs
         beside a training step of this GPU, and it has the memory the step's activations will
-        take later (a standby that warms up after a takeover, with training running, is the
-        one exception: ``standby_warm_wait`` events show the rest)."""
+        take later.  A standby that arrives later, with training running, warms up in a window
+        the job master plans and every rank applies at one step (_warm_window)."""
         from easydl_amd.utils import vram
         if (self._warm_published or not vram.enabled() or self.device.type != "cuda"
                 or getattr(self, "kv", None) is None):
@@ -674,6 +675,29 @@ class ElasticTrainer:
         if state is not None:
             self.events.emit("standby_warm_wait", s=round(time.perf_counter() - t0, 3), warm=bool(state))
 
+    def _warm_window(self, ww: dict) -> None:
+        """Runtime plan ``warm_window`` (master/main.py _grant_warm_windows): a standby that
+        arrived while this job trains warms up on this rank's GPU now, between two steps --
+        grant it and wait (bounded, EDL_WARM_WINDOW_S) for its warm key.  Every rank applies the
+        plan at the same committed step; ranks on other GPUs go on and meet this one at the next
+        collective.  A request that is gone (handled, or its standby took over) is skipped."""
+        from easydl_amd.utils import vram
+        name, gpu = ww.get("standby"), self.device.index
+        if (self.device.type != "cuda" or gpu not in (ww.get("gpus") or []) or not name
+                or (name, ww.get("id")) in self._warm_windows):
+            return
+        self._warm_windows.add((name, ww.get("id")))
+        req = vram.read_warm_request(self.kv, name)
+        if not req or req.get("id") != ww.get("id") or name not in vram.roster(self.kv):
+            return
+        t0 = time.perf_counter()
+        self.kv.set(f"standby/warm_grant/{name}/gpu{gpu}", str(ww.get("id")))
+        limit = float(os.environ.get("EDL_WARM_WINDOW_S", 60))
+        while not self.kv.exists(f"standby/warm/{name}/gpu{gpu}") and time.perf_counter() - t0 < limit:
+            time.sleep(0.02)
+        self.events.emit("standby_warm_window", standby=name, step=self.step, s=round(time.perf_counter() - t0, 3),
+                         warm=self.kv.exists(f"standby/warm/{name}/gpu{gpu}"))
+
     def _publish_act(self) -> None:
         """HBM a step needs beyond the persistent state (activations, workspaces), after the
         first step: a replacement that adopts the state checks it against what the GPU has free
@@ -683,7 +707,12 @@ class ElasticTrainer:
                 or getattr(self, "kv", None) is None):
             return
         self._act_published = True
-        persistent = sum(t.untyped_storage().nbytes() for t in self.vram_state_tensors().values())
+        # only this process's own allocations count against its allocator's peak: state adopted
+        # from a dead worker is imported memory the caching allocator never reserved (counting it
+        # published 0 for a replacement, and the next replacement would not have split its step)
+        adopted = set(vram.TAKEN.values())
+        persistent = sum(t.untyped_storage().nbytes() for t in self.vram_state_tensors().values()
+                         if t.data_ptr() not in adopted)
         act = max(0, torch.cuda.max_memory_reserved(self.device) - persistent)
         vram.publish_act(self.kv, f"{self.ctx.role}{self.ctx.index}", act, self.micro_batch)
 
@@ -1100,6 +1129,8 @@ class ElasticTrainer:
         ci = doc.get("ckpt_interval")
         if ci and self.checkpoint is not None:
             self.checkpoint.interval = max(1, int(ci))
+        if doc.get("warm_window"):
+            self._warm_window(doc["warm_window"])
         for group, c in self._comm_groups():
             ar = (doc.get("allreduce") or {}).get(group)
             apply = getattr(c, "adopt_policy", None) or getattr(c, "apply_allreduce_policy", None)

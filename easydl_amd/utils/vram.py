@@ -91,11 +91,29 @@ def read_warm(kv, slot: str) -> tuple[bool, dict | None]:
 def standby_warm_on(kv, gpu) -> bool | None:
     """None: no standby is parked (``standby/roster``, kept by the operator); True: one of the
     parked standbys has run its warm-up on ``gpu`` (an int, "cpu" or None); False: not yet."""
-    names = [n for n in (kv.get_str("standby/roster") or "").split(",") if n]
+    names = roster(kv)
     if not names:
         return None
     where = ["any"] + ([f"gpu{gpu}"] if isinstance(gpu, int) else ["cpu"])
     return any(kv.exists(f"standby/warm/{n}/{w}") for n in names for w in where)
+
+
+# Warm-up windows for a standby that arrives while the workers train (a refill after a takeover):
+# its warm-up of a GPU must not run beside that GPU's training steps.  The standby files a request
+# (``standby/warm_req/<name>`` = {"id", "gpus"}); the job master turns it into a runtime plan
+# (``warm_window``), which every rank applies at the same committed step; the ranks on those GPUs
+# grant it (``standby/warm_grant/<name>/gpu<g>``) and pause until the standby's warm key appears.
+def request_warm_window(kv, name: str, req_id: int, gpus) -> None:
+    kv.set(f"standby/warm_req/{name}", json.dumps({"id": int(req_id), "gpus": sorted(int(g) for g in gpus)}))
+
+
+def read_warm_request(kv, name: str) -> dict | None:
+    raw = kv.get_str(f"standby/warm_req/{name}")
+    return json.loads(raw) if raw else None
+
+
+def roster(kv) -> list[str]:
+    return [n for n in (kv.get_str("standby/roster") or "").split(",") if n]
 
 
 def publish_act(kv, slot: str, act_bytes: int, micro_batch: int) -> None:
@@ -109,6 +127,11 @@ def read_act(kv, slot: str) -> tuple[int, int]:
         return 0, 0
     d = json.loads(raw)
     return int(d.get("act_bytes", 0)), int(d.get("micro_batch", 0))
+
+
+def trained(kv, slot: str) -> bool:
+    """``slot``'s worker has committed its first step (it published its step's HBM need)."""
+    return kv.exists(f"vram/act/{slot}")
 
 
 def slots(kv) -> list[str]:
