@@ -117,8 +117,10 @@ class PlanLoop:
         # older than a few periods belongs to a process that is gone
         extra = [n for n in (master.kv.get_str("metrics/extra_nodes") or "").split(",") if n]
         members = list(dict.fromkeys(master.rdzv.members() + extra))
-        fresh = time.time() - max(60.0, 3 * self.period_s)
-        metrics = {n: m for n in members if (m := master.kv.get(f"metrics/{n}")) and m.get("ts", 0) >= fresh}
+        wall = time.time()
+        fresh = wall - max(60.0, 3 * self.period_s)
+        # (a record without a timestamp cannot be judged stale: kept)
+        metrics = {n: m for n in members if (m := master.kv.get(f"metrics/{n}")) and m.get("ts", wall) >= fresh}
         if not metrics:
             return
         # rocprofv3 kernel profiles the roles left under <run_dir>/rocprof/<process>/ (Brain CU signal)
