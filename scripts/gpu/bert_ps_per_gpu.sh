@@ -5,7 +5,7 @@
 # per-GPU batch.  BATCHES (default "8 32": config 4's worker batch and the DDP headline batch);
 # SNAP = PS updates between in-memory snapshots (20; 0 = none), PIPE = pipelined pushes (1),
 # STEPS = worker steps per run (96).
-set -o pipefail
+set -uo pipefail
 out=gpurun_out/${TAG:-bert_ps_per_gpu}
 mkdir -p $out
 for B in ${BATCHES:-8 32}; do

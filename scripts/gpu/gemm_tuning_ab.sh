@@ -1,7 +1,7 @@
 #!/bin/bash
 # Same-box A/B of the shipped TunableOp selection (EDL_GEMM_TUNING=select) against a full tuning file
 # (FILE, default the round-5 full tuning of the training step), two alternating rounds of bench.py --child.
-set -o pipefail
+set -uo pipefail
 out=gpurun_out/r05_tune_ab; mkdir -p $out
 for i in 1 2; do
   for v in select r05; do

@@ -1,6 +1,6 @@
 #!/bin/bash
 # The N=1 time-to-recover drill alone, at the headline config (args override), run dir kept.
-set -o pipefail
+set -uo pipefail
 out=gpurun_out/r05_${TAG:-drill}
 mkdir -p $out/ttr
 export EDL_TTR_DIR=$out/ttr EDL_TTR_KEEP=1 EDL_FAULT_STEP_MS=${STEP_MS:-2850}

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-end validation on one MI355X, as the driver runs it: the GPU test tier, smoke(), the
 # headline bench (throughput child + time-to-recover drill child).  Stops at the first failure.
-set -o pipefail
+set -uo pipefail
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 out=gpurun_out/${TAG:-validate}
 mkdir -p $out

@@ -2,7 +2,7 @@
 # World-8 kill -> shrink -> rejoin on ONE GPU (VERDICT r4 Next #2c): 8 workers + 1 hot standby
 # share the card over the default auto plane with gloo fallback (--comm auto-gloo), tiny model.
 # The 8-GPU node form is the driver's; this rehearses its membership paths on real HIP contexts.
-set -o pipefail
+set -uo pipefail
 out=gpurun_out/r05_${TAG:-world8}
 mkdir -p $out/ttr
 export EDL_TTR_DIR=$out/ttr EDL_TTR_KEEP=1 EDL_BENCH_UNTIL_REGROWN=1 EDL_BENCH_CAP=${CAP:-400} \

@@ -77,7 +77,8 @@ def main():
                     round(tot(1, key, "SQ_INSTS_VALU") / waves, 1), round(lds / waves, 1),
                     round(bc / lds, 3) if lds else "", round(tot(1, key, "SQ_WAIT_ANY") / wc, 3),
                     round(tot(0, key, "SQ_WAIT_INST_LDS") / wc, 3) if tot(1, key, "SQ_WAVE_CYCLES") else "",
-                    round(tot(1, key, "SQ_ACTIVE_INST_VALU") / wc, 3), round(tot(1, key, "SQ_ACTIVE_INST_MFMA") / wc, 3)])
+                    round(tot(1, key, "SQ_ACTIVE_INST_VALU") / wc, 3),
+                    round(tot(1, key, "SQ_ACTIVE_INST_MFMA") / wc, 3)])
 
 
 if __name__ == "__main__":

@@ -58,6 +58,9 @@ class FakeKV:
     def exists(self, k):
         return k in self.d
 
+    def delete(self, k):
+        self.d.pop(k, None)
+
 
 JOB = ElasticJob.from_dict({"apiVersion": "elastic.easydl.org/v1alpha1", "kind": "ElasticJob",
                             "metadata": {"name": "j"}, "spec": {"command": "python -m x",

@@ -21,7 +21,6 @@ import textwrap
 import threading
 from http.server import BaseHTTPRequestHandler, HTTPServer
 
-import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
