@@ -47,6 +47,18 @@ def _td(s: float) -> datetime.timedelta:
     return datetime.timedelta(seconds=s)
 
 
+def _rccl_nonblocking(opts) -> bool:
+    """Non-blocking RCCL communicator init (EDL_RCCL_NONBLOCKING, default on) where this torch
+    exposes the config field."""
+    if os.environ.get("EDL_RCCL_NONBLOCKING", "1") != "1":
+        return False
+    cfg = getattr(opts, "config", None)
+    if cfg is None or not hasattr(cfg, "blocking"):
+        return False
+    cfg.blocking = 0
+    return True
+
+
 class Communicator:
     def __init__(self, store: dist.Store, rank: int, world_size: int, epoch: int, *, device: torch.device,
                  job: str = "job", timeout_s: float = 120.0, control_timeout_s: float = 30.0,
@@ -86,6 +98,7 @@ class Communicator:
         # "auto-gloo" (tests): the auto engine/probe path with gloo on GPU tensors standing in
         # for RCCL, so several ranks can share one GPU (RCCL refuses duplicate devices)
         self.data_kind = "rccl"
+        self.nonblocking = False
         if data_backend == "auto-gloo":
             data_backend, self.data_kind = "auto", "gloo"
         if not data:
@@ -126,7 +139,18 @@ class Communicator:
                 opts = dist.ProcessGroupNCCL.Options()
                 opts.is_high_priority_stream = high_priority
                 opts._timeout = _td(timeout_s)
+                self.nonblocking = _rccl_nonblocking(opts)
                 self.data = dist.ProcessGroupNCCL(dist.PrefixStore("data", base), rank, world_size, opts)
+                if self.nonblocking:
+                    # ncclCommInitRankConfig with blocking = 0, started now: the bootstrap runs while
+                    # the epoch entry goes on (state sync over the control plane, the engine's
+                    # mappings), the first collective waits for it, and abort() -- the watchdog's,
+                    # when a peer dies during the bootstrap -- can end an init still in progress
+                    # (non-blocking init + async error + abort)
+                    try:
+                        self.data.eager_connect_single_device(self.device)
+                    except Exception as e:  # noqa: BLE001 - lazy init at the first collective instead
+                        log.debug("eager RCCL connect failed: %s", e)
             self.backend = self.data_kind + ("+xgmi" if self.xgmi_mode == "xgmi" else "")
         else:
             self.data = dist.ProcessGroupGloo(dist.PrefixStore("data", base), rank, world_size, _td(timeout_s))

@@ -1,7 +1,8 @@
 """The RCCL data plane of ``Communicator`` on real hardware at world 1 (RCCL refuses two
-ranks on one GPU): every collective the trainer calls, plus the coalesced point-to-point
-batch of the multi-source state transfer (a send to and a receive from this rank in one
-grouped launch).  Prints one JSON line."""
+ranks on one GPU): non-blocking communicator init (an epoch aborted while its init may still be
+in progress, then a fresh one), every collective the trainer calls, plus the coalesced
+point-to-point batch of the multi-source state transfer (a send to and a receive from this rank
+in one grouped launch).  Prints one JSON line."""
 import datetime
 import json
 import os
@@ -16,8 +17,13 @@ from easydl_amd.parallel.comm import Communicator  # noqa: E402
 dev = torch.device("cuda", 0)
 torch.cuda.set_device(dev)
 store = dist.TCPStore("127.0.0.1", 0, 1, True, timeout=datetime.timedelta(seconds=60))
+# an epoch aborted while its non-blocking RCCL init may still be in progress: abort returns
+c0 = Communicator(store, 0, 1, 0, device=dev, job="rccl1", timeout_s=60.0, data_backend="auto")
+res0 = {"nonblocking": c0.nonblocking}
+c0.abort()
 c = Communicator(store, 0, 1, 1, device=dev, job="rccl1", timeout_s=60.0, data_backend="auto")
-res = {"data_kind": c.data_kind, "backend": c.backend}
+res = {"data_kind": c.data_kind, "backend": c.backend, "nonblocking": c.nonblocking and res0["nonblocking"],
+       "aborted_during_init": c0.aborted}
 c.warmup()
 x = torch.arange(1 << 20, device=dev, dtype=torch.float32)
 res["all_reduce"] = bool(torch.equal(c.all_reduce(x.clone()), x))
