@@ -244,6 +244,8 @@ class CheckpointManager:
         self.populate_threads = int(os.environ.get("EDL_SHM_POPULATE_THREADS", 4))
         self._skip_populating = False
         self._verify = None         # pending post-teardown check of an early hand-over (fence)
+        self._deferred: list = []   # moment copies of the last restore still running (complete_restore)
+        self._deferred_segs: list = []
         self._marks_check = None    # background post-reap check of an HBM resume
         self._seg: ShmSegment | None = None
         self._seg_key = None
@@ -518,6 +520,8 @@ class CheckpointManager:
         return self._segment(world, shard, cs_off + 8, pin=state[0][1].is_cuda, tag=tag, alloc_bytes=alloc)
 
     def snapshot(self, trainer) -> None:
+        if self._deferred:
+            self.complete_restore()   # the moments of the last restore are read below
         comm, tag, world, shard, state, layout, cs_off, lean_state, headroom, key, sizes = self._plan(trainer)
         if not self.sharded and comm.rank != 0:
             return
@@ -657,8 +661,35 @@ class CheckpointManager:
         c = self._marks_check
         return c is not None and c["result"] is None
 
+    def complete_restore(self, check: bool = True) -> None:
+        """Join the deferred moment copies of the last restore (restore_latest ``defer_moments``):
+        the current stream waits for them and the snapshot's checksum is verified as a whole.
+        A mismatch raises before any update reads the moments."""
+        pending, self._deferred = self._deferred, []
+        segs, self._deferred_segs = self._deferred_segs, []
+        try:
+            for h in pending:
+                t0 = time.perf_counter()
+                h["thread"].join()
+                if h["error"] is not None:
+                    if check:
+                        raise RuntimeError(f"deferred restore of {h['what']} failed: {h['error']}")
+                    continue
+                torch.cuda.current_stream(h["acc"].device).wait_event(h["event"])
+                if check:
+                    got = (int(h["acc"].item()) + int(h["acc2"].item())) & ((1 << 64) - 1)
+                    if got != h["expect"]:
+                        raise RuntimeError(f"checksum mismatch in {h['what']} (deferred moments): "
+                                           f"{got:#x} != {h['expect']:#x}")
+                self.stats["deferred_restore_wait_s"] = round(time.perf_counter() - t0, 3)
+        finally:
+            for seg in segs:
+                threading.Thread(target=seg.close, name="edl-shm-unmap", daemon=True).start()
+
     def fence(self) -> None:
         """Make the current stream wait for the in-flight snapshot (call before the optimizer)."""
+        if self._deferred:
+            self.complete_restore()
         c = self._marks_check
         if c is not None and c["result"] is not None:
             self._marks_check = None
@@ -742,12 +773,18 @@ class CheckpointManager:
         found = self.find_latest(self._tag(trainer))
         return -1 if found is None else found[1]
 
-    def restore_latest(self, trainer, max_step: int | None = None) -> str | None:
+    def restore_latest(self, trainer, max_step: int | None = None, defer_moments: bool = False) -> str | None:
+        """Restore the newest snapshot.  ``defer_moments`` (a rank that will not send its state
+        to others before its first update, e.g. world 1): the Adam moments -- 2/3 of a full
+        fp32 snapshot -- are copied under the first training step instead of before it
+        (EDL_RESTORE_DEFER=0 turns that off); ``complete_restore`` (called by fence) joins them
+        and verifies the whole checksum before the update reads them."""
         # Drain this rank's in-flight snapshot first: its D2H reads the very buffers the
         # restore is about to overwrite, and its commit must not publish a slot that
         # mixes pre- and post-rollback bytes under a pre-restore checksum.
         t_start = time.perf_counter()
         LAST_RESTORE_STATS.clear()
+        self.complete_restore(check=False)
         self.wait()
         tag = self._tag(trainer)
         found = self.find_latest(tag, max_step)
@@ -762,6 +799,10 @@ class CheckpointManager:
         phases = {"find_s": round(t0 - t_start, 3)}
         own = self._own_key(trainer)
         verify = []
+        later = frozenset()
+        if (defer_moments and dev.type == "cuda" and not infos[0]["meta"].get("lean")
+                and os.environ.get("EDL_RESTORE_DEFER", "1") == "1"):
+            later = frozenset(self._moment_names(trainer))
         for s, info in enumerate(infos):
             t1 = time.perf_counter()
             seg = _open_segment(self.seg_name(world, s, tag))
@@ -769,7 +810,8 @@ class CheckpointManager:
             keep = False
             try:
                 loaded = _load_shard(lambda off, nb: seg.view(info["slot"], off, nb), info["meta"]["t"], state, dev,
-                                     info["checksum"], f"shm shard {s} of step {step}", seg=seg, slot=info["slot"])
+                                     info["checksum"], f"shm shard {s} of step {step}", seg=seg, slot=info["slot"],
+                                     later=later, deferred=self._deferred)
                 if loaded is not None:
                     verify.append(loaded)
                 # The segment this rank will write next (same layout, e.g. the only worker restarted):
@@ -787,6 +829,8 @@ class CheckpointManager:
                         # allocated off the recovery path; snapshots wait for that by skipping
                         seg.populate_async(self.populate_threads)
                         self._skip_populating = True
+                elif later:
+                    self._deferred_segs.append(seg)   # closed once the deferred copy is done
                 else:
                     threading.Thread(target=seg.close, name="edl-shm-unmap", daemon=True).start()
         t2 = time.perf_counter()
@@ -884,6 +928,7 @@ class CheckpointManager:
         return None
 
     def close(self, unlink: bool = False) -> None:
+        self.complete_restore(check=False)
         self.wait()
         self._join_persist(60)
         if unlink:
@@ -939,48 +984,81 @@ def _load_host_state(trainer, h) -> None:
 LAST_RESTORE_STATS: dict = {}   # where the newest shm -> HBM restore spent its time (copy vs DMA wait)
 
 
-def _load_shard(read, table, state, dev, expect: int, what: str, seg=None, slot=None) -> None:
+def _restore_items(seg, slot, items, dev, stream, stats: dict) -> None:
+    """Native pipelined shm -> HBM copy of ``items`` ((dst view, segment offset), ...) on ``stream``."""
+    n = len(items)
+    if n == 0:
+        return
+    arr = lambda v: (ctypes.c_uint64 * n)(*v)  # noqa: E731
+    ptrs = [d.data_ptr() for d, _ in items]
+    sizes = [d.numel() * d.element_size() for d, _ in items]
+    offs = [o for _, o in items]
+    cs = ctypes.c_void_p(stream.cuda_stream)
+    if os.environ.get("EDL_RESTORE_V1") == "1":   # A/B: per-chunk threads, 2 stages of 256 MiB
+        rc = _native.runtime()("edl_ckpt_restore_pipelined", seg.h, slot, n, arr(ptrs), arr(sizes), arr(offs),
+                               cs, 256 << 20, 16)
+    else:
+        st = (ctypes.c_double * 4)()
+        rc = _native.runtime()("edl_ckpt_restore_pipelined2", seg.h, slot, n, arr(ptrs), arr(sizes), arr(offs),
+                               cs, int(os.environ.get("EDL_RESTORE_CHUNK_MB", 128)) << 20,
+                               int(os.environ.get("EDL_RESTORE_THREADS", 16)),
+                               int(os.environ.get("EDL_RESTORE_STAGES", 4)), st)
+        stats.update(copy_s=round(st[0], 3), dma_wait_s=round(st[1], 3), total_s=round(st[2], 3),
+                     gb=round(st[3] / 2**30, 2), gbps=round(st[3] / 2**30 / max(st[2], 1e-9), 1))
+    if rc != 0:
+        raise RuntimeError(f"pipelined restore failed: hipError {rc}")
+
+
+def _load_shard(read, table, state, dev, expect: int, what: str, seg=None, slot=None, later=frozenset(),
+                deferred: list | None = None) -> None:
     """Copy one shard's tensor slices to their device buffers and verify the checksum
     (on the GPU for device tensors: no host pass over tens of GB).  From a shm
     segment to a GPU the copy runs through the native pipelined restore
-    (multi-threaded memcpy into pinned staging buffers overlapped with DMA)."""
+    (multi-threaded memcpy into pinned staging buffers overlapped with DMA).
+
+    ``later`` (names; shm -> GPU only): those tensors -- the Adam moments, which nothing reads
+    before the first optimizer update -- are copied by a background thread on a side stream
+    while training resumes; their checksum half is folded in at ``deferred`` completion
+    (CheckpointManager.complete_restore, before that update)."""
     acc = torch.zeros(1, dtype=torch.int64, device=dev) if dev.type == "cuda" else None
     if acc is not None and seg is not None:
-        ptrs, sizes, offs, items = [], [], [], []
+        now, items_later = [], []
         for name, dt, numel, lo, hi, off in table:
             t = state[name]
-            nbytes = (hi - lo) * t.element_size()
-            if nbytes:
-                dst = t.view(-1)[lo:hi]
-                ptrs.append(dst.data_ptr())
-                sizes.append(nbytes)
-                offs.append(off)
-                items.append((dst, off))
-        n = len(ptrs)
-        arr = lambda v: (ctypes.c_uint64 * n)(*v)  # noqa: E731
-        stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
-        if os.environ.get("EDL_RESTORE_V1") == "1":   # A/B: per-chunk threads, 2 stages of 256 MiB
-            rc = _native.runtime()("edl_ckpt_restore_pipelined", seg.h, slot, n, arr(ptrs), arr(sizes), arr(offs),
-                                   stream, 256 << 20, 16)
-        else:
-            st = (ctypes.c_double * 4)()
-            rc = _native.runtime()("edl_ckpt_restore_pipelined2", seg.h, slot, n, arr(ptrs), arr(sizes), arr(offs),
-                                   stream, int(os.environ.get("EDL_RESTORE_CHUNK_MB", 128)) << 20,
-                                   int(os.environ.get("EDL_RESTORE_THREADS", 16)),
-                                   int(os.environ.get("EDL_RESTORE_STAGES", 4)), st)
-            LAST_RESTORE_STATS.update(copy_s=round(st[0], 3), dma_wait_s=round(st[1], 3), total_s=round(st[2], 3),
-                                      gb=round(st[3] / 2**30, 2),
-                                      gbps=round(st[3] / 2**30 / max(st[2], 1e-9), 1))
-        if rc != 0:
-            raise RuntimeError(f"pipelined restore failed: hipError {rc}")
+            if (hi - lo) * t.element_size():
+                (items_later if name in later and deferred is not None else now).append((t.view(-1)[lo:hi], off))
+        _restore_items(seg, slot, now, dev, torch.cuda.current_stream(dev), LAST_RESTORE_STATS)
         t_cs = time.perf_counter()
-        for dst, off in items:
+        for dst, off in now:
             checksum_tensor(dst, acc, base_index=off // 4)
+        if items_later:
+            side = torch.cuda.Stream(dev)
+            acc2 = torch.zeros(1, dtype=torch.int64, device=dev)
+            ev = torch.cuda.Event()
+            nb = sum(d.numel() * d.element_size() for d, _ in items_later)
+            h = {"acc": acc, "acc2": acc2, "event": ev, "expect": expect, "what": what, "error": None,
+                 "bytes": nb, "stats": {}}
+
+            def run():
+                try:
+                    with torch.cuda.device(dev), torch.cuda.stream(side):
+                        _restore_items(seg, slot, items_later, dev, side, h["stats"])
+                        for dst, off in items_later:
+                            checksum_tensor(dst, acc2, base_index=off // 4)
+                        ev.record(side)
+                except Exception as e:  # noqa: BLE001 - reported at completion, before the update
+                    h["error"] = e
+
+            h["thread"] = threading.Thread(target=run, name="edl-restore-deferred", daemon=True)
+            h["thread"].start()
+            deferred.append(h)
+            LAST_RESTORE_STATS["deferred_bytes"] = LAST_RESTORE_STATS.get("deferred_bytes", 0) + nb
+            return now + items_later, expect
         got = int(acc.item()) & ((1 << 64) - 1)
         LAST_RESTORE_STATS["checksum_s"] = round(time.perf_counter() - t_cs, 3)
         if got != expect:
             raise RuntimeError(f"checksum mismatch in {what}: {got:#x} != {expect:#x}")
-        return items, expect
+        return now, expect
     total = 0
     for name, dt, numel, lo, hi, off in table:
         t = state[name]

@@ -479,7 +479,8 @@ class ElasticTrainer:
         c = self.comm
         if c.world_size == 1:
             if self.needs_state:
-                self._maybe_restore()
+                # nobody to send the state to: the moments may arrive under the first step
+                self._maybe_restore(defer_moments=True)
             self.needs_state = False
             self._state_settled()
             return
@@ -786,7 +787,7 @@ class ElasticTrainer:
             return None
         return done
 
-    def _maybe_restore(self) -> bool:
+    def _maybe_restore(self, defer_moments: bool = False) -> bool:
         """State of a process that holds none: the dead worker's HBM (HBM resume), else the
         newest snapshot.  With neither, buffers adopted from a dead worker are reset to this
         process's seeded init (a fresh start).  True if trained state was recovered."""
@@ -801,7 +802,7 @@ class ElasticTrainer:
                 src = self.checkpoint.resume_from_hbm(self, k, verify)
                 self.events.emit("restored", step=self.step, source=src, s=round(time.perf_counter() - t0, 3))
                 return True
-            st = self.checkpoint.restore_latest(self)
+            st = self.checkpoint.restore_latest(self, defer_moments=defer_moments)
             if st is not None:
                 from easydl_amd.ckpt import manager as _ckm
                 self.events.emit("restored", step=self.step, source=st, s=round(time.perf_counter() - t0, 3),

@@ -132,3 +132,45 @@ def test_staged_snapshots_into_an_adopted_segment_resume_bit_exactly(cuda, tmp_p
         ck_a.close()
         ck_b.close()
         unlink_job_segments("ckg")
+
+
+def test_restore_with_deferred_moments_is_bit_exact_and_verified(cuda, tmp_path):
+    """World-1 restore (ElasticTrainer._sync_state): the master weights come back before the
+    first step, the Adam moments on a side stream under it (CheckpointManager.restore_latest
+    ``defer_moments``); the update waits for them and the whole checksum.  Training then matches
+    an uninterrupted run bit for bit; a corrupted moment byte is caught before the update."""
+    from easydl_amd.ckpt import manager as ckm
+    unlink_job_segments("ckg")
+    data = SyntheticTokens(CFG.vocab_size, 64, num_samples=4096)
+    ckpt = CheckpointManager("ckg", interval=2)
+    try:
+        a = _trainer(tmp_path, ckpt, 1, cuda)
+        a.fit(lambda m, b: m(*b), data, num_steps=5)
+        ckpt.wait()
+        assert ckpt.last_snapshot_step == 4
+        ck_b = CheckpointManager("ckg", interval=1000)
+        b = _trainer(tmp_path, ck_b, 2, cuda)
+        b.fit(lambda m, b_: m(*b_), data, num_steps=7)       # restores step 4, moments deferred
+        assert ckm.LAST_RESTORE_STATS.get("deferred_bytes", 0) > 0, ckm.LAST_RESTORE_STATS
+        assert "deferred_restore_wait_s" in ck_b.stats and not ck_b._deferred
+        ref = _trainer(tmp_path, None, 1, cuda)
+        ref.fit(lambda m, b_: m(*b_), data, num_steps=7)
+        assert torch.equal(_flat(b), _flat(ref))
+
+        # a flipped byte inside a moment tensor of the newest slot: the deferred half fails the check
+        from easydl_amd.ckpt.manager import ShmSegment
+        tag = ck_b._tag(b)
+        world, step, infos = ck_b.find_latest(tag)
+        seg = ShmSegment(ck_b.seg_name(world, 0, tag), create=False)
+        try:
+            ent = next(e for e in infos[0]["meta"]["t"] if e[0].endswith(".m") and e[4] > e[3])
+            v = seg.view(infos[0]["slot"], ent[5], 4)
+            v[1] ^= 0x40
+        finally:
+            seg.close()
+        c = _trainer(tmp_path, CheckpointManager("ckg", interval=1000), 3, cuda)
+        with pytest.raises(RuntimeError, match="deferred moments"):
+            c.fit(lambda m, b_: m(*b_), data, num_steps=9)   # raised at the first update's fence
+    finally:
+        ckpt.close()
+        unlink_job_segments("ckg")
