@@ -484,6 +484,10 @@ class ElasticTrainer:
             self.needs_state = False
             self._state_settled()
             return
+        if self.checkpoint is not None:
+            # a world-1 restore may still be copying its moments (deferred under the first step);
+            # this rank may now send its state to others: it must hold all of it
+            self.checkpoint.complete_restore()
         have = -1 if self.needs_state else self.step
         max_step = int(c.ctrl_all_reduce([have], dist.ReduceOp.MAX)[0])
         holder = max_step >= 0 and not self.needs_state and self.step == max_step
