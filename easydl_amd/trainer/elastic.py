@@ -698,8 +698,13 @@ class ElasticTrainer:
         t0 = time.perf_counter()
         self.kv.set(f"standby/warm_grant/{name}/gpu{gpu}", str(ww.get("id")))
         limit = float(os.environ.get("EDL_WARM_WINDOW_S", 60))
+        next_roster = t0 + 0.5
         while not self.kv.exists(f"standby/warm/{name}/gpu{gpu}") and time.perf_counter() - t0 < limit:
             time.sleep(0.02)
+            if time.perf_counter() > next_roster:     # a standby that took over or died ends the window
+                next_roster = time.perf_counter() + 0.5
+                if name not in vram.roster(self.kv):
+                    break
         self.events.emit("standby_warm_window", standby=name, step=self.step, s=round(time.perf_counter() - t0, 3),
                          warm=self.kv.exists(f"standby/warm/{name}/gpu{gpu}"))
 

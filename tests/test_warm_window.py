@@ -94,3 +94,24 @@ def test_stale_window_is_skipped(tmp_path):
     kv.set("standby/roster", "")
     ElasticTrainer._warm_window(tr, {"standby": "sb0", "id": 5, "gpus": [0]})   # standby gone
     assert not tr.events.got and not kv.exists("standby/warm_grant/sb0/gpu0")
+
+
+def test_window_ends_when_the_standby_leaves(tmp_path):
+    m = JobMaster("ww4", 0, run_dir=str(tmp_path))
+    kv = m.kv
+    kv.set("standby/roster", "sb0")
+    vram.request_warm_window(kv, "sb0", 1, [0])
+
+    def leave():     # the standby took over a dead worker instead of warming up
+        time.sleep(0.3)
+        kv.set("standby/roster", "")
+
+    th = threading.Thread(target=leave)
+    th.start()
+    tr = _fake_trainer(kv, 0)
+    t0 = time.perf_counter()
+    ElasticTrainer._warm_window(tr, {"standby": "sb0", "id": 1, "gpus": [0]})
+    th.join()
+    assert time.perf_counter() - t0 < 5
+    ev = [e for e in tr.events.got if e["kind"] == "standby_warm_window"]
+    assert len(ev) == 1 and not ev[0]["warm"]
