@@ -35,6 +35,18 @@ class LRSchedule:
         return dict(lr=self.lr, warmup=self.warmup, total=self.total, min_ratio=self.min_ratio)
 
 
+def rehome_state(state: list, adopted_ptrs: set) -> int:
+    """Optimizer-state tensors on adopted memory -> own copies (see FlatParams.rehome)."""
+    n = 0
+    with torch.no_grad():
+        for st in state:
+            for k, t in list(st.items()):
+                if isinstance(t, torch.Tensor) and t.data_ptr() in adopted_ptrs:
+                    st[k] = t.clone()
+                    n += 1
+    return n
+
+
 def _zeros(name: str, g, dtype=torch.float32) -> torch.Tensor:
     """Optimizer state of flat group ``g``: a buffer handed over by the previous worker on
     this GPU (utils/vram.py, its values kept for an HBM resume), or a new zeroed one."""

@@ -265,6 +265,31 @@ class FlatParams:
         """The state is settled (resumed, restored or transferred): free the init values."""
         self._init_copies = []
 
+    def rehome(self, adopted_ptrs: set) -> int:
+        """Move every buffer built on adopted memory (a dead worker's HBM, mapped over IPC) into
+        this process's own allocation -- same values, parameters and gradients re-pointed --
+        one group at a time, so the extra memory is one group.  A process cannot export memory
+        it imported, so only re-homed state can be handed to the next standby.  Returns the
+        number of buffers moved."""
+        n = 0
+        with torch.no_grad():
+            for g in self.groups:
+                if g.data.data_ptr() in adopted_ptrs:
+                    new = torch.empty_like(g.data)
+                    new.copy_(g.data)
+                    for s in g.slots:
+                        s.param.data = new[s.offset:s.offset + s.numel].view(s.shape)
+                    g.data = new
+                    n += 1
+                if g.grad.data_ptr() in adopted_ptrs:
+                    new = torch.empty_like(g.grad)
+                    new.copy_(g.grad)
+                    for s in g.slots:
+                        s.param.grad = new[s.offset:s.offset + s.numel].view(s.shape)
+                    g.grad = new
+                    n += 1
+        return n
+
     # -- views ---------------------------------------------------------------
     def params(self):
         for g in self.groups:
@@ -308,6 +333,7 @@ class FlatBuffers:
                 by_dtype.setdefault(b.dtype, []).append((mod, name, b))
         self.tensors: dict[str, torch.Tensor] = {}
         self._init_copies: list[tuple[torch.Tensor, torch.Tensor]] = []
+        self._where: dict[str, list] = {}   # dtype key -> (module, buffer name, offset, shape)
         for dt, items in by_dtype.items():
             key = str(dt).replace("torch.", "")
             n = sum(b.numel() for _, _, b in items)
@@ -325,6 +351,7 @@ class FlatBuffers:
                     else:
                         view.copy_(b)
                     mod._buffers[name] = view
+                    self._where.setdefault(key, []).append((mod, name, off, tuple(b.shape)))
                     off += b.numel()
             self.tensors[key] = flat
 
@@ -339,3 +366,20 @@ class FlatBuffers:
 
     def drop_init_copies(self) -> None:
         self._init_copies = []
+
+    def rehome(self, adopted_ptrs: set) -> int:
+        """See :meth:`FlatParams.rehome`."""
+        n = 0
+        with torch.no_grad():
+            for key, flat in list(self.tensors.items()):
+                if flat.data_ptr() not in adopted_ptrs:
+                    continue
+                new = flat.clone()
+                for mod, name, off, shape in self._where.get(key, []):
+                    numel = 1
+                    for d in shape:
+                        numel *= d
+                    mod._buffers[name] = new[off:off + numel].view(shape)
+                self.tensors[key] = new
+                n += 1
+        return n

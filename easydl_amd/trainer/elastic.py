@@ -123,6 +123,7 @@ class ElasticTrainer:
         self._warm_windows: set = set()   # (standby, request id) warm-up windows granted
         self._warm_published = False
         self._act_published = False
+        self._rehomed = False        # state adopted from a dead worker moved into own memory (_maybe_rehome)
         self.needs_state = True     # fresh process: must receive state unless everyone is fresh
         self.comm = None
         self.assignment = None
@@ -726,6 +727,57 @@ class ElasticTrainer:
         act = max(0, torch.cuda.max_memory_reserved(self.device) - persistent)
         vram.publish_act(self.kv, f"{self.ctx.role}{self.ctx.index}", act, self.micro_batch)
 
+    def _maybe_rehome(self) -> None:
+        """Once a takeover's state is settled, move everything built on the dead worker's HBM into
+        this process's own allocations, between two steps (FlatParams.rehome: one group at a
+        time).  Imported memory cannot be exported again, so until then this process has
+        nothing to hand to the next standby: a second failure of this rank would restore from
+        /dev/shm instead of resuming from HBM.  Waits until the adopted state is verified (the
+        post-reap step-mark check, an early hand-over's check, a deferred restore), full
+        micro-batches are back and one group's copy fits in free HBM."""
+        from easydl_amd.optim import rehome_state
+        from easydl_amd.utils import vram
+        if self._rehomed or not vram.adopted_any() or self.flat is None or self.opt is None:
+            return
+        ck = self.checkpoint
+        if ck is not None and (getattr(ck, "_marks_check", None) is not None or getattr(ck, "_verify", None) is not None
+                               or getattr(ck, "_deferred", None)):
+            return
+        if self._mb_split > 1:
+            return
+        adopted = set(vram.TAKEN.values())
+        sizes = [t.untyped_storage().nbytes() for t in self.vram_state_tensors().values() if t.data_ptr() in adopted]
+        if self.device.type == "cuda" and sizes and self._hbm_avail() < 2 * max(sizes):
+            return
+        t0 = time.perf_counter()
+        if ck is not None:
+            ck.wait()           # no snapshot copy may read a buffer while it moves
+        if self.device.type == "cuda":
+            # the new buffers get segments of their own (fresh allocations, not blocks split out
+            # of a cached activation segment): an IPC export maps a buffer's whole segment
+            torch.cuda.empty_cache()
+        alias = [st.get("master") is not None and st["master"].data_ptr() == g.data.data_ptr()
+                 for g, st in zip(self.flat.groups, self.opt.state)]
+        n = self.flat.rehome(adopted)
+        for g, st, a in zip(self.flat.groups, self.opt.state, alias):
+            if a:
+                st["master"] = g.data   # an fp32 model's master IS its weight buffer
+        n += rehome_state(self.opt.state, adopted)
+        if self.bufs is not None:
+            n += self.bufs.rehome(adopted)
+        if self.ddp is not None:
+            self.ddp.set_bucket_mb(self.ddp.bucket_mb)      # bucket views of the new gradient buffers
+            if self.dp_comm is not None and self.dp_comm.world_size > 1:
+                self.ddp.set_comm(self.dp_comm)             # the engine maps the new buffers
+        if self.device.type == "cuda":
+            torch.cuda.current_stream(self.device).synchronize()
+        vram.TAKEN.clear()
+        vram.ADOPTED_FROM.clear()
+        self._rehomed = True
+        self.events.emit("rehomed", buffers=n, gb=round(sum(sizes) / 2**30, 2), step=self.step,
+                         s=round(time.perf_counter() - t0, 3))
+        self._publish_vram()    # the next standby can adopt this state again
+
     def _hbm_avail(self) -> int:
         free, _ = torch.cuda.mem_get_info(self.device)
         return free + torch.cuda.memory_reserved(self.device) - torch.cuda.memory_allocated(self.device)
@@ -1058,6 +1110,7 @@ class ElasticTrainer:
                     else:
                         self._run_deferred_probes()
                     self._publish_act()
+                    self._maybe_rehome()
                     if on_step is not None:
                         on_step(self, loss)
                     if self.log_every and self.step % self.log_every == 0 and self.comm.rank == 0:

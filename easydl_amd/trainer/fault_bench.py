@@ -79,6 +79,7 @@ def main(args) -> int:
         spec += ",point=in_update"
     if standby and mode != "step_start":
         spec += ",wait=standby"   # a real failure finds the spare parked and warmed up
+    spec = os.environ.get("EDL_BENCH_FAULT_SPEC") or spec   # e.g. a second kill of the replacement (gen=1)
     env = {
         "EDL_BENCH_MODEL": args.model, "EDL_BENCH_SEQ": str(args.seq), "EDL_BENCH_MBS": str(args.mbs),
         "EDL_BENCH_ACCUM": str(args.accum),

@@ -58,6 +58,8 @@ def publish(kv, slot: str, owner: str, tensors: dict[str, torch.Tensor]) -> int:
     """Export ``tensors`` (name -> CUDA tensor owning its whole allocation) for the standby."""
     from easydl_amd.ps.ipc import export_tensor
     descs = {}
+    STATS["export_failed"] = 0
+    STATS.pop("export_error", None)
     for name, t in tensors.items():
         if t is None or not t.is_cuda or _block_bytes(t) > IPC_MAX_BYTES:
             continue
@@ -65,6 +67,8 @@ def publish(kv, slot: str, owner: str, tensors: dict[str, torch.Tensor]) -> int:
             descs[name] = export_tensor(t)
         except RuntimeError as e:   # e.g. a tensor this process itself imported (an adopted buffer)
             log.debug("vram: %s not exportable: %s", name, e)
+            STATS["export_failed"] += 1
+            STATS["export_error"] = f"{name}: {e}"[:200]
     gpu = next((t.device.index for t in tensors.values() if t is not None and t.is_cuda), 0)
     kv.set(key(slot), json.dumps({"owner": owner, "pid": os.getpid(), "gpu": gpu, "gen": time.time_ns(),
                                   "tensors": descs}))

@@ -218,3 +218,39 @@ def test_memory_limited_recovery_splits_micro_batches_with_the_same_update(tmp_p
     assert [r["kind"] for r in sp.events.records if r["kind"] == "memory_restored"] == ["memory_restored"]
     for a, b in zip(ref.flat.groups, sp.flat.groups):
         assert torch.allclose(a.data, b.data, atol=1e-6, rtol=1e-5)
+
+
+def test_resumed_state_is_rehomed_and_training_continues_bit_exactly(tmp_path, monkeypatch):
+    """After an HBM resume the replacement moves the adopted buffers into its own memory at the
+    first step boundary (ElasticTrainer._maybe_rehome: imported memory cannot be exported to the
+    next standby) and trains on exactly as an uninterrupted run."""
+    unlink_job_segments(JOB)
+    monkeypatch.setenv("EDL_VRAM_HANDOFF", "1")
+    _, exported = _died_worker(tmp_path)
+    pid = _dead_pid()
+    _marks(monkeypatch, 3, pid)
+    vram.adopt(exported, pid=pid)
+    ck = CheckpointManager(JOB, interval=100)
+    try:
+        b = _mk(tmp_path, 5, ck, sub="b")
+        b.fit(lambda m, x: m(*x), _Images(), num_steps=6)
+        kinds = [r["kind"] for r in b.events.records]
+        assert "rehomed" in kinds and kinds.count("rehomed") == 1, kinds
+        ev = next(r for r in b.events.records if r["kind"] == "rehomed")
+        assert ev["step"] == 4 and ev["buffers"] == len(exported), ev
+        adopted_ptrs = {t.data_ptr() for t in exported.values()}
+        mine = b.vram_state_tensors()
+        assert not ({t.data_ptr() for t in mine.values()} & adopted_ptrs)   # nothing left on adopted memory
+        for g in b.flat.groups:                                             # params view the new buffers
+            for s in g.slots:
+                assert s.param.data_ptr() == g.data[s.offset:].data_ptr()
+        assert not vram.adopted_any()      # (on a GPU it is re-published for the next standby here)
+        ref = _mk(tmp_path, 1, sub="ref")
+        ref.fit(lambda m, x: m(*x), _Images(), num_steps=6)
+        got, want = _state(b), _state(ref)
+        for k in want:
+            assert torch.equal(got[k], want[k]), k
+    finally:
+        ck.close()
+        unlink_job_segments(JOB)
+        vram.adopt({})
