@@ -293,8 +293,17 @@ def main() -> int:
     if gpu is not None and int(gpu) in WARM_STREAMS:
         import torch
         torch.cuda.set_stream(WARM_STREAMS[int(gpu)])   # the stream the warm-up ran on (its hipBLASLt workspace)
+    # the parked loop's variables still name the imported state ("h" is the last slot's record,
+    # "t" a warm-up thread): this frame lives as long as the role it runs, so without this the
+    # dead worker's HBM would stay mapped after the trainer re-homed its state into its own
+    # memory -- 120 GB at Llama-3-8B, and the next step ran out of memory
+    h = t = None  # noqa: F841
     if handoff:
         _adopt_vram(held, f"worker{a['env'].get('EDL_INDEX', '')}", kv, name)
+    held.clear()
+    warming.clear()
+    late.clear()
+    gc.collect()
     argv = a["argv"]
     mod = module_of(argv)
     if mod is None:

@@ -35,13 +35,13 @@ class LRSchedule:
         return dict(lr=self.lr, warmup=self.warmup, total=self.total, min_ratio=self.min_ratio)
 
 
-def rehome_state(state: list, adopted_ptrs: set) -> int:
+def rehome_state(state: list, adopted, can_continue=lambda: True) -> int:
     """Optimizer-state tensors on adopted memory -> own copies (see FlatParams.rehome)."""
     n = 0
     with torch.no_grad():
         for st in state:
             for k, t in list(st.items()):
-                if isinstance(t, torch.Tensor) and t.data_ptr() in adopted_ptrs:
+                if isinstance(t, torch.Tensor) and adopted(t) and can_continue():
                     st[k] = t.clone()
                     n += 1
     return n

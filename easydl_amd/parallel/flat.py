@@ -265,23 +265,25 @@ class FlatParams:
         """The state is settled (resumed, restored or transferred): free the init values."""
         self._init_copies = []
 
-    def rehome(self, adopted_ptrs: set) -> int:
-        """Move every buffer built on adopted memory (a dead worker's HBM, mapped over IPC) into
+    def rehome(self, adopted, can_continue=lambda: True) -> int:
+        """Move every buffer ``adopted(tensor)`` says is built on adopted memory (a dead worker's HBM, mapped over IPC) into
         this process's own allocation -- same values, parameters and gradients re-pointed --
         one group at a time, so the extra memory is one group.  A process cannot export memory
-        it imported, so only re-homed state can be handed to the next standby.  Returns the
-        number of buffers moved."""
+        it imported, so only re-homed state can be handed to the next standby.  Stops before a
+        group when ``can_continue()`` is False.  Returns the number of buffers moved."""
         n = 0
         with torch.no_grad():
             for g in self.groups:
-                if g.data.data_ptr() in adopted_ptrs:
+                if not can_continue():
+                    break
+                if adopted(g.data):
                     new = torch.empty_like(g.data)
                     new.copy_(g.data)
                     for s in g.slots:
                         s.param.data = new[s.offset:s.offset + s.numel].view(s.shape)
                     g.data = new
                     n += 1
-                if g.grad.data_ptr() in adopted_ptrs:
+                if adopted(g.grad):
                     new = torch.empty_like(g.grad)
                     new.copy_(g.grad)
                     for s in g.slots:
@@ -367,12 +369,12 @@ class FlatBuffers:
     def drop_init_copies(self) -> None:
         self._init_copies = []
 
-    def rehome(self, adopted_ptrs: set) -> int:
+    def rehome(self, adopted, can_continue=lambda: True) -> int:
         """See :meth:`FlatParams.rehome`."""
         n = 0
         with torch.no_grad():
             for key, flat in list(self.tensors.items()):
-                if flat.data_ptr() not in adopted_ptrs:
+                if not adopted(flat) or not can_continue():
                     continue
                 new = flat.clone()
                 for mod, name, off, shape in self._where.get(key, []):

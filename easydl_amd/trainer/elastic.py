@@ -29,6 +29,7 @@ import logging
 import os
 import threading
 import time
+import weakref
 
 import torch
 import torch.distributed as dist
@@ -746,7 +747,15 @@ class ElasticTrainer:
         if self._mb_split > 1:
             return
         adopted = set(vram.TAKEN.values())
-        sizes = [t.untyped_storage().nbytes() for t in self.vram_state_tensors().values() if t.data_ptr() in adopted]
+        before = {k: t for k, t in self.vram_state_tensors().items() if t.data_ptr() in adopted}
+        sizes = [t.untyped_storage().nbytes() for t in before.values()]
+        # weak references: which buffer still is the adopted one afterwards (a freed adopted
+        # range's address can come back for a new allocation, so pointers cannot tell)
+        before = {k: weakref.ref(t) for k, t in before.items()}
+        refs = list(before.values())
+
+        def is_adopted(t):
+            return any(r() is t for r in refs)
         if self.device.type == "cuda" and sizes and self._hbm_avail() < 2 * max(sizes):
             return
         t0 = time.perf_counter()
@@ -756,24 +765,36 @@ class ElasticTrainer:
             # the new buffers get segments of their own (fresh allocations, not blocks split out
             # of a cached activation segment): an IPC export maps a buffer's whole segment
             torch.cuda.empty_cache()
+        # each moved buffer frees its adopted original as the last reference goes; should one stay
+        # referenced, HBM would shrink by a buffer per move: stop while the next step's
+        # activations and two buffers still fit (the rest stays on adopted memory, still correct)
+        reserve = getattr(self, "_act_need", 0) + 2 * max(sizes, default=0)
+        can_continue = (lambda: self._hbm_avail() >= reserve) if self.device.type == "cuda" else (lambda: True)
         alias = [st.get("master") is not None and st["master"].data_ptr() == g.data.data_ptr()
                  for g, st in zip(self.flat.groups, self.opt.state)]
-        n = self.flat.rehome(adopted)
+        n = self.flat.rehome(is_adopted, can_continue)
         for g, st, a in zip(self.flat.groups, self.opt.state, alias):
             if a:
                 st["master"] = g.data   # an fp32 model's master IS its weight buffer
-        n += rehome_state(self.opt.state, adopted)
+        n += rehome_state(self.opt.state, is_adopted, can_continue)
         if self.bufs is not None:
-            n += self.bufs.rehome(adopted)
+            n += self.bufs.rehome(is_adopted, can_continue)
+        left = [k for k, t in self.vram_state_tensors().items() if k in before and before[k]() is t]
         if self.ddp is not None:
             self.ddp.set_bucket_mb(self.ddp.bucket_mb)      # bucket views of the new gradient buffers
             if self.dp_comm is not None and self.dp_comm.world_size > 1:
                 self.ddp.set_comm(self.dp_comm)             # the engine maps the new buffers
         if self.device.type == "cuda":
             torch.cuda.current_stream(self.device).synchronize()
+        self._rehomed = True    # (once: a partial move is not retried)
+        if left:
+            for k in [k for k in vram.TAKEN if k not in left]:
+                vram.TAKEN.pop(k)
+            self.events.emit("rehome_partial", buffers=n, left=left[:8], n_left=len(left), step=self.step,
+                             avail_gb=round(self._hbm_avail() / 2**30, 1), s=round(time.perf_counter() - t0, 3))
+            return
         vram.TAKEN.clear()
         vram.ADOPTED_FROM.clear()
-        self._rehomed = True
         self.events.emit("rehomed", buffers=n, gb=round(sum(sizes) / 2**30, 2), step=self.step,
                          s=round(time.perf_counter() - t0, 3))
         self._publish_vram()    # the next standby can adopt this state again
