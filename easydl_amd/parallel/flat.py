@@ -266,8 +266,8 @@ class FlatParams:
         self._init_copies = []
 
     def rehome(self, adopted, can_continue=lambda: True) -> int:
-        """Move every buffer ``adopted(tensor)`` says is built on adopted memory (a dead worker's HBM, mapped over IPC) into
-        this process's own allocation -- same values, parameters and gradients re-pointed --
+        """Move every buffer ``adopted(tensor)`` says is built on adopted memory (a dead worker's
+        HBM, mapped over IPC) into this process's own allocation -- same values, parameters and gradients re-pointed --
         one group at a time, so the extra memory is one group.  A process cannot export memory
         it imported, so only re-homed state can be handed to the next standby.  Stops before a
         group when ``can_continue()`` is False.  Returns the number of buffers moved."""
