@@ -162,7 +162,8 @@ def parent(args) -> int:
             b = d.get("breakdown") or {}
             ttr.update({
                 "time_to_regain_s": d.get("time_to_regain_s"), "steps_lost": d.get("steps_lost"),
-                "restored_from": d.get("restored_from"), "fault_step": (d.get("fault") or {}).get("step"),
+                "restored_from": d.get("restored_from"), "resumed_mid_step": d.get("resumed_mid_step"),
+                "fault_step": (d.get("fault") or {}).get("step"),
                 "fault_spec": (d.get("fault") or {}).get("spec"),
                 "replacement_from_standby": d.get("replacement_from_standby"),
                 "step_s_before_fault": d.get("step_s_before_fault"),

@@ -653,9 +653,10 @@ class CheckpointManager:
         t0 = time.perf_counter()
         while not vram.reaped(v["pid"]) and time.perf_counter() - t0 < 120:
             time.sleep(0.01)
-        now = read_slot(v["job"], v["slot"])
+        now = read_slot(v["job"], v["slot"], shadow=True)
         out["s"] = round(time.perf_counter() - t0, 3)
-        out["result"] = "ok" if now is not None and now[:2] == v["marks"] else f"marks moved: {v['marks']} -> {now}"
+        ok = now is not None and now[:2] == v["marks"] and (v.get("shadow") is None or now[3:5] == v["shadow"])
+        out["result"] = "ok" if ok else f"marks moved: {v['marks']} {v.get('shadow')} -> {now}"
 
     def hbm_unverified(self) -> bool:
         c = self._marks_check

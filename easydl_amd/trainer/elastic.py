@@ -150,6 +150,9 @@ class ElasticTrainer:
         self._stop_requested = False
         self._master_lost: str | None = None    # set by the watchdog (see _start_watchdog)
         self._mb_split = 1           # >1: micro-batches split while a takeover waits for HBM (_memory_plan)
+        self._shadow_stream = None   # gradient shadow copies (_shadow_grads)
+        self._shadow_pending = False
+        self._shadow_resume = None   # {"step", "mb"}: resume that step at that micro-batch
         self._act_need = 0
 
     def request_stop(self) -> None:
@@ -626,6 +629,8 @@ class ElasticTrainer:
         from easydl_amd.utils import vram
         if not (vram.enabled() and self.device.type == "cuda" and getattr(self, "kv", None) is not None):
             return
+        if self._shadow_wanted():
+            self.flat.ensure_shadow()
         ts = self.vram_state_tensors()
         try:
             n = vram.publish(self.kv, f"{self.ctx.role}{self.ctx.index}", self.ctx.node_id, ts)
@@ -647,6 +652,7 @@ class ElasticTrainer:
                     ts[f"opt/{g.name}/{k}"] = t
         for k, t in getattr(self.bufs, "tensors", {}).items():
             ts[f"bufs/{k}"] = t
+        ts.update(self.flat.shadow_tensors())
         return ts
 
     def _publish_warm_spec(self, data) -> None:
@@ -837,10 +843,10 @@ class ElasticTrainer:
         if k <= 1:
             return mbs
         out = []
-        for idx in mbs:
+        for mb, idx in mbs:     # (micro-batch index, sample indices): the pieces keep the index
             idx = list(idx)
             n = -(-len(idx) // k)
-            out += [idx[i:i + n] for i in range(0, len(idx), n)]
+            out += [(mb, idx[i:i + n]) for i in range(0, len(idx), n)]
         return out
 
     def _hbm_resume_step(self) -> int | None:
@@ -851,10 +857,11 @@ class ElasticTrainer:
         if (pid is None or self.tp > 1 or self.comm is None or self.comm.world_size != 1
                 or os.environ.get("EDL_HBM_RESUME", "1") == "0"):
             return None
-        marks = stepmarks.read_slot(self.ctx.job, f"{self.ctx.role}{self.ctx.index}")
+        marks = stepmarks.read_slot(self.ctx.job, f"{self.ctx.role}{self.ctx.index}", shadow=True)
         if marks is None:
             return None
-        begin, done, writer = marks
+        begin, done, writer, gstep, gmb = marks
+        self._shadow_cand = (gstep, gmb)
         if writer != pid or begin != done:
             self.events.emit("hbm_resume_refused", begin=begin, done=done, writer=writer, adopted_from=pid)
             return None
@@ -881,6 +888,14 @@ class ElasticTrainer:
                 pid = vram.ADOPTED_FROM.get("pid")
                 verify = None if vram.reaped(pid) else {"pid": pid, "marks": (k, k), "job": self.ctx.job,
                                                         "slot": f"{self.ctx.role}{self.ctx.index}"}
+                gstep, gmb = getattr(self, "_shadow_cand", (0, 0))
+                sh = self.flat.shadow_tensors()
+                if gmb and gstep == k + 1 and sh and not vram.missing(list(sh.items())):
+                    # the dead worker had finished gmb micro-batches of step k + 1 (their gradients
+                    # are in its shadow): that step resumes at micro-batch gmb (_run_step)
+                    self._shadow_resume = {"step": gstep, "mb": gmb}
+                    if verify is not None:
+                        verify["shadow"] = (gstep, gmb)
                 src = self.checkpoint.resume_from_hbm(self, k, verify)
                 self.events.emit("restored", step=self.step, source=src, s=round(time.perf_counter() - t0, 3))
                 return True
@@ -930,7 +945,7 @@ class ElasticTrainer:
         except CommAborted:
             pass   # the epoch broke after the commit: the next epoch's state sync covers it
 
-    def _seed_step(self) -> None:
+    def _seed_step(self, mb: int = 0) -> None:
         """Random streams keyed by (seed, committed step, data-parallel rank): dropout
         masks of step k do not depend on how the job got to step k (restarts, world
         changes), so a resume from a snapshot of step k replays step k+1 bit-exactly
@@ -938,7 +953,7 @@ class ElasticTrainer:
         of one replica share the stream (replicated activations need equal masks)."""
         c = self.dp_comm or self.comm
         r = c.rank if c is not None else 0
-        torch.manual_seed((self._seed * 1_000_003 + self.step * 7_919 + r * 104_729) % (1 << 62))
+        torch.manual_seed((self._seed * 1_000_003 + self.step * 7_919 + r * 104_729 + mb * 15_485_863) % (1 << 62))
 
     def host_state(self) -> dict:
         """Host-side training state a resume needs besides the tensors (recorded in every
@@ -968,28 +983,47 @@ class ElasticTrainer:
                                                                     lr["min_ratio"])
 
     def _run_step(self, loss_fn, data, plan):
-        mbs = self._micro_batches(data, plan)
-        if self._mb_split > 1:
-            mbs = self._split_micro_batches(mbs)
-        self._seed_step()
+        mbs = list(enumerate(self._micro_batches(data, plan)))   # (micro-batch index, sample indices)
         self.flat.zero_grad()
         total = 0.0
         loss_acc = None
+        res, self._shadow_resume = self._shadow_resume, None
+        if res is not None and res["step"] == self.step + 1 and 0 < res["mb"] < len(mbs):
+            # mid-step resume: the dead worker's gradients of micro-batches [0, mb) from its shadow
+            self.flat.load_shadow()
+            loss_acc = self.flat.gshadow_loss[0].clone()
+            total = sum(len(idx) for _, idx in mbs[:res["mb"]]) / plan.global_batch
+            self.events.emit("resumed_mid_step", step=self.step + 1, micro_batches_done=res["mb"], of=len(mbs))
+            mbs = mbs[res["mb"]:]
+        if self._mb_split > 1:
+            mbs = self._split_micro_batches(mbs)
+        shadow = self._shadow_active()
+        seeded = None
         with self.kmix.phase("compute"):
-            for i, idx in enumerate(mbs):
+            for j, (i, idx) in enumerate(mbs):
                 if self.comm is not None and self.comm.aborted:  # epoch broke: do not start more work
                     raise CommAborted(f"epoch {self.comm.epoch} aborted before micro-batch {i}")
+                if i != seeded:
+                    self._seed_step(i)      # random streams keyed by micro-batch: a mid-step resume replays them
+                    seeded = i
                 batch = data.batch(idx, self.device)
                 w = len(idx) / plan.global_batch
-                ctxm = self.ddp.no_sync() if i < len(mbs) - 1 else _null()
+                last = j == len(mbs) - 1
+                ctxm = self.ddp.no_sync() if not last else _null()
                 with ctxm, trace.range(f"microbatch{i}"):
                     with trace.range("fwd"):
                         loss = loss_fn(self.model, batch)
+                    if self._shadow_pending:
+                        # the shadow copy of the previous micro-batch's gradients must finish first
+                        torch.cuda.current_stream(self.device).wait_stream(self._shadow_stream)
+                        self._shadow_pending = False
                     with trace.range("bwd"):
                         (loss * w).backward() if w != 1.0 else loss.backward()
                 ld = loss.detach() * w
                 loss_acc = ld if loss_acc is None else loss_acc + ld
                 total += w
+                if shadow and not last:
+                    self._shadow_grads(i + 1, loss_acc)
         t_mb = time.perf_counter()
         if self._phases and self.device.type == "cuda":
             # diagnostic mode: drain the compute stream so 'finish' is the gradient all-reduce alone
@@ -1005,6 +1039,45 @@ class ElasticTrainer:
         self.fault.maybe_inject("after_backward", self.step, trainer=self)
         self._t_mb = t_mb
         return None if loss_acc is None else loss_acc / total
+
+    def _shadow_wanted(self) -> bool:
+        """Gradient shadows pay off where a replacement resumes from this process's HBM: one rank
+        (HBM resume needs world 1), VRAM hand-over on, several micro-batches per step."""
+        from easydl_amd.utils import vram
+        return (vram.enabled() and self.device.type == "cuda" and self.tp == 1 and self.flat is not None
+                and self.comm is not None and self.comm.world_size == 1 and self.global_batch is not None
+                and self.global_batch > self.micro_batch and os.environ.get("EDL_GRAD_SHADOW", "1") != "0")
+
+    def _shadow_active(self) -> bool:
+        return (self._marks is not None and self.flat.gshadow is not None and self._mb_split == 1
+                and self.comm.world_size == 1)
+
+    def _shadow_grads(self, mbs_done: int, loss_acc) -> None:
+        """After a micro-batch's backward: copy the accumulated gradients (and the partial loss)
+        into the shadow on a side stream, under the next micro-batch's forward, between an
+        invalidating and a validating step mark (utils/stepmarks.py).  The next backward waits
+        for the copy.  Gradients no micro-batch has written yet are zeroed first (as the end of
+        the step would), so the shadow is exact."""
+        self.flat.finalize_untouched()
+
+        def copy(st):
+            self._marks.shadow(self.step + 1, 0, st)
+            with torch.no_grad():
+                for g, t in zip(self.flat.groups, self.flat.gshadow):
+                    t.copy_(g.grad)
+                self.flat.gshadow_loss.copy_(loss_acc.reshape(1))
+            self._marks.shadow(self.step + 1, mbs_done, st)
+        if self.device.type != "cuda":
+            copy(None)
+            return
+        if self._shadow_stream is None:
+            self._shadow_stream = torch.cuda.Stream(device=self.device)
+        st = self._shadow_stream
+        st.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(st):
+            copy(st)
+        loss_acc.record_stream(st)
+        self._shadow_pending = True
 
     def _sync_point(self) -> bool:
         """Host-side completion of every gradient all-reduce; False if the epoch broke.

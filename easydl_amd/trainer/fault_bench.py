@@ -135,6 +135,8 @@ def main(args) -> int:
         "replacement_from_standby": any(e["kind"] == "spawn" and e.get("standby") for e in ev),
         "restored_from": restored[0].get("source") if restored else None,
         "hbm_resume_refused": any(e["kind"] == "hbm_resume_refused" for e in ev),
+        "resumed_mid_step": next(({k: e.get(k) for k in ("step", "micro_batches_done", "of")}
+                                  for e in ev if e["kind"] == "resumed_mid_step"), None),
         "final_states": [{k: e.get(k) for k in ("proc", "step", "world", "rank", "crc")}
                          for e in ev if e["kind"] == "final_state"],
         "worlds_seen": sorted({w for w in worlds if w}), "run_dir": run_dir,

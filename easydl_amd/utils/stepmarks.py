@@ -6,13 +6,19 @@ page-locked and device-mapped), read by the process that replaces it:
 
 * ``begin`` = the step whose update is about to start (written before the optimizer kernels),
 * ``done``  = the step whose update has finished (written after them),
-* ``pid``   = the writer.
+* ``pid``   = the writer,
+* ``gstep``, ``gmb`` = the gradient shadow (``FlatParams.ensure_shadow``) holds the summed
+  gradients of micro-batches ``[0, gmb)`` of step ``gstep``; ``gmb = 0``: no valid shadow.  The
+  shadow is copied on a side stream after a micro-batch's backward, between an invalidating
+  write (``gmb = 0``) and this mark, so a kill in the middle of the copy leaves ``gmb = 0``.
 
 When a worker is SIGKILLed, its GPU queues stop (utils/procfs.py).  If ``begin == done == K``
 no update was in flight, so the weights, fp32 master and moments in its HBM are exactly the
 state after step K.  A replacement that adopted that HBM (utils/vram.py) then resumes from
 step K without restoring a snapshot: no host -> HBM copy, no lost steps, and the same
-per-step seeds as an uninterrupted run.  With ``begin != done`` it restores from /dev/shm.
+per-step seeds as an uninterrupted run.  With ``begin != done`` it restores from /dev/shm.  When the
+shadow also names step K + 1, the replacement copies it into its gradient buffers and runs
+only the micro-batches of step K + 1 the dead worker had not finished (a mid-step resume).
 
 Reference: the reference's recovery contract ("resume the training" after a failure,
 /root/reference/README.md:25-29); the mechanism is ours.
@@ -26,7 +32,7 @@ import torch
 
 from easydl_amd import _native
 
-BEGIN, DONE, PID = 0, 4, 8     # byte offsets in the page
+BEGIN, DONE, PID, GSTEP, GMB = 0, 4, 8, 16, 20     # byte offsets in the page
 
 
 def page_name(job: str, slot: str) -> str:
@@ -54,6 +60,7 @@ class StepMarks:
         """Host write of begin = done = ``step`` (no update in flight; the stream is idle)."""
         self._u32(BEGIN).value = step & 0xFFFFFFFF
         self._u32(DONE).value = step & 0xFFFFFFFF
+        self._u32(GMB).value = 0
         ctypes.c_int64.from_address(self.host + PID).value = os.getpid()
 
     def _mark(self, off: int, step: int, stream) -> None:
@@ -69,9 +76,19 @@ class StepMarks:
     def done(self, step: int, stream=None) -> None:
         self._mark(DONE, step, stream)
 
+    def shadow(self, step: int, mb: int, stream=None) -> None:
+        """Gradient shadow: ``mb`` = 0 before a copy starts, then (``step``, ``mb``) after it."""
+        if mb:
+            self._mark(GSTEP, step, stream)
+        self._mark(GMB, mb, stream)
+
     def read(self) -> tuple[int, int, int]:
         return (self._u32(BEGIN).value, self._u32(DONE).value,
                 ctypes.c_int64.from_address(self.host + PID).value)
+
+    def read_shadow(self) -> tuple[int, int]:
+        """(gstep, gmb) of the gradient shadow."""
+        return self._u32(GSTEP).value, self._u32(GMB).value
 
     def close(self, unlink: bool = False) -> None:
         if self.h:
@@ -79,13 +96,14 @@ class StepMarks:
             self.h = None
 
 
-def read_slot(job: str, slot: str) -> tuple[int, int, int] | None:
-    """(begin, done, pid) of a slot's page, or None if there is none."""
+def read_slot(job: str, slot: str, shadow: bool = False) -> tuple | None:
+    """(begin, done, pid) of a slot's page -- plus (gstep, gmb) with ``shadow`` -- or None if
+    there is none."""
     try:
         m = StepMarks(job, slot, create=False)
     except OSError:
         return None
     try:
-        return m.read()
+        return m.read() + (m.read_shadow() if shadow else ())
     finally:
         m.close()

@@ -231,6 +231,11 @@ def take(name: str, numel: int, dtype: torch.dtype, device, keep: bool = False) 
     return t
 
 
+def pending(name: str) -> bool:
+    """An adopted tensor of this name is waiting to be taken."""
+    return name in _ADOPTED
+
+
 def adopted_any() -> bool:
     """True if some buffer of this process was built on a dead worker's HBM."""
     return bool(TAKEN)

@@ -73,7 +73,8 @@ def _died_worker(tmp_path, steps=3):
 
 
 def _marks(monkeypatch, k, pid):
-    monkeypatch.setattr(stepmarks, "read_slot", lambda job, slot: (k, k, pid))
+    monkeypatch.setattr(stepmarks, "read_slot",
+                        lambda job, slot, shadow=False: (k, k, pid) + ((0, 0) if shadow else ()))
 
 
 def test_hbm_resume_adopts_every_state_tensor_including_batchnorm_buffers(tmp_path, monkeypatch):
@@ -135,7 +136,8 @@ def test_adopted_buffers_without_resume_or_snapshot_equal_a_fresh_start(tmp_path
     torn weights and non-zero moments must not survive into training."""
     _, exported = _died_worker(tmp_path)
     pid = _dead_pid()
-    monkeypatch.setattr(stepmarks, "read_slot", lambda job, slot: (4, 3, pid))   # begin != done
+    monkeypatch.setattr(stepmarks, "read_slot",
+                        lambda job, slot, shadow=False: (4, 3, pid) + ((0, 0) if shadow else ()))   # begin != done
     vram.adopt(exported, pid=pid)
     try:
         b = _mk(tmp_path, 5, None, sub="b")
@@ -209,7 +211,7 @@ def test_memory_limited_recovery_splits_micro_batches_with_the_same_update(tmp_p
 
     def spy(mbs):
         out = orig(mbs)
-        seen.append([len(x) for x in out])
+        seen.append([len(x) for _, x in out])
         avail["v"] = 10_000          # the driver has reclaimed the memory after the first step
         return out
     sp._split_micro_batches = spy
@@ -250,6 +252,63 @@ def test_resumed_state_is_rehomed_and_training_continues_bit_exactly(tmp_path, m
         got, want = _state(b), _state(ref)
         for k in want:
             assert torch.equal(got[k], want[k]), k
+    finally:
+        ck.close()
+        unlink_job_segments(JOB)
+        vram.adopt({})
+
+
+def test_mid_step_resume_from_the_gradient_shadow_is_bit_exact(tmp_path, monkeypatch):
+    """The worker dies in step 4 after 2 of its 4 micro-batches (the gradient buffer itself is
+    torn: a backward was in flight).  Its shadow holds the gradients of micro-batches 0-1 and
+    the partial loss, its step marks say (gstep, gmb) = (4, 2): the replacement resumes step 4
+    at micro-batch 2 and ends bit-identical to an uninterrupted run -- BatchNorm running
+    statistics included, which a whole-step replay would have updated twice."""
+    unlink_job_segments(JOB)
+    pid = _dead_pid()
+
+    def mk(sub, seed, ckpt=None):
+        ctx = TrainerContext(job=JOB, run_dir=str(tmp_path / sub))
+        return ElasticTrainer(lambda d: _BNNet(d), global_batch=16, micro_batch=4, lr=1e-2, device="cpu",
+                              ctx=ctx, checkpoint=ckpt, seed=seed)
+
+    a = mk("dead", 1)
+    a.fit(lambda m, b: m(*b), _Images(), num_steps=3)
+    a._marks = stepmarks.StepMarks(JOB, "shadowtest")      # host-written page (CPU)
+    a.flat.ensure_shadow()
+    calls = {"n": 0}
+
+    def dies(m, b):
+        calls["n"] += 1
+        if calls["n"] == 3:
+            raise KeyboardInterrupt("killed before micro-batch 2 of step 4")
+        return m(*b)
+    try:
+        a.fit(dies, _Images(), num_steps=4)
+    except KeyboardInterrupt:
+        pass
+    assert a.step == 3 and a._marks.read_shadow() == (4, 2)
+    for g in a.flat.groups:
+        g.grad.add_(1.0)            # the in-flight backward's partial adds: the shadow must be used
+    exported = {k: t.clone() for k, t in a.vram_state_tensors().items()}
+    a._marks.close(unlink=True)
+    assert "flat/gshadow_loss" in exported
+    monkeypatch.setattr(stepmarks, "read_slot",
+                        lambda job, slot, shadow=False: (3, 3, pid) + ((4, 2) if shadow else ()))
+    vram.adopt(exported, pid=pid)
+    ck = CheckpointManager(JOB, interval=100)
+    try:
+        b = mk("b", 5, ck)
+        b.fit(lambda m, x: m(*x), _Images(), num_steps=6)
+        ev = [r for r in b.events.records if r["kind"] in ("restored", "resumed_mid_step")]
+        assert [r["kind"] for r in ev] == ["restored", "resumed_mid_step"], ev
+        assert ev[1]["step"] == 4 and ev[1]["micro_batches_done"] == 2 and ev[1]["of"] == 4
+        vram.adopt({})
+        ref = mk("ref", 1).fit(lambda m, x: m(*x), _Images(), num_steps=6)
+        got, want = _state(b), _state(ref)
+        for k in want:
+            assert torch.equal(got[k], want[k]), k
+        assert int(b.model.bn.num_batches_tracked) == int(ref.model.bn.num_batches_tracked) == 24
     finally:
         ck.close()
         unlink_job_segments(JOB)
