@@ -150,6 +150,7 @@ class ElasticTrainer:
         self._stop_requested = False
         self._master_lost: str | None = None    # set by the watchdog (see _start_watchdog)
         self._mb_split = 1           # >1: micro-batches split while a takeover waits for HBM (_memory_plan)
+        self._mb_recompute = None    # not None: the model's recompute flag to restore (_memory_plan)
         self._shadow_stream = None   # gradient shadow copies (_shadow_grads)
         self._shadow_pending = False
         self._shadow_resume = None   # {"step", "mb"}: resume that step at that micro-batch
@@ -629,8 +630,6 @@ class ElasticTrainer:
         from easydl_amd.utils import vram
         if not (vram.enabled() and self.device.type == "cuda" and getattr(self, "kv", None) is not None):
             return
-        if self._shadow_wanted():
-            self.flat.ensure_shadow()
         ts = self.vram_state_tensors()
         try:
             n = vram.publish(self.kv, f"{self.ctx.role}{self.ctx.index}", self.ctx.node_id, ts)
@@ -724,6 +723,8 @@ class ElasticTrainer:
         if (self._act_published or not vram.enabled() or self.device.type != "cuda"
                 or getattr(self, "kv", None) is None):
             return
+        if self._mb_split > 1 or self._mb_recompute is not None:
+            return      # a memory-limited step's peak is not a full step's (_memory_plan)
         self._act_published = True
         # only this process's own allocations count against its allocator's peak: state adopted
         # from a dead worker is imported memory the caching allocator never reserved (counting it
@@ -733,6 +734,31 @@ class ElasticTrainer:
                          if t.data_ptr() not in adopted)
         act = max(0, torch.cuda.max_memory_reserved(self.device) - persistent)
         vram.publish_act(self.kv, f"{self.ctx.role}{self.ctx.index}", act, self.micro_batch)
+        self._maybe_shadow(act)
+
+    def _maybe_shadow(self, act: int) -> None:
+        """Turn the gradient shadow on after the first step if the GPU can afford it: a
+        replacement starts with only the HBM this worker leaves free (the rest of its memory
+        is reclaimed seconds after it dies), and its first step must still fit one sample per
+        micro-batch there (_memory_plan).  At Llama-3-8B (2 x 8k tokens per micro-batch) the
+        16 GB shadow does not fit that budget: the first step then blocked in hipMalloc and
+        the time-to-recover doubled (profiles/r05_ttr_headline.md), so it stays off there."""
+        if self.flat.gshadow is not None or not self._shadow_wanted():
+            return
+        from easydl_amd.utils import vram
+        free = torch.cuda.mem_get_info(self.device)[0]
+        if not vram.standby_warm_on(self.kv, self.device.index):
+            # no warm standby on this GPU yet (a replacement before its refill arrives): keep the
+            # room one will take (a context, the GEMM libraries' workspaces, its warm-up's cache)
+            free -= int(float(os.environ.get("EDL_STANDBY_RESERVE_GB", "16")) * 2**30)
+        shadow = sum(g.grad.untyped_storage().nbytes() for g in self.flat.groups)
+        need = act / max(1, self.micro_batch) * 1.15
+        on = free - shadow >= need or os.environ.get("EDL_GRAD_SHADOW") == "force"
+        self.events.emit("grad_shadow", on=on, gb=round(shadow / 2**30, 1), free_gb=round(free / 2**30, 1),
+                         replacement_need_gb=round(need / 2**30, 1))
+        if on:
+            self.flat.ensure_shadow()
+            self._publish_vram()
 
     def _maybe_rehome(self) -> None:
         """Once a takeover's state is settled, move everything built on the dead worker's HBM into
@@ -742,7 +768,6 @@ class ElasticTrainer:
         /dev/shm instead of resuming from HBM.  Waits until the adopted state is verified (the
         post-reap step-mark check, an early hand-over's check, a deferred restore), full
         micro-batches are back and one group's copy fits in free HBM."""
-        from easydl_amd.optim import rehome_state
         from easydl_amd.utils import vram
         if self._rehomed or not vram.adopted_any() or self.flat is None or self.opt is None:
             return
@@ -750,7 +775,7 @@ class ElasticTrainer:
         if ck is not None and (getattr(ck, "_marks_check", None) is not None or getattr(ck, "_verify", None) is not None
                                or getattr(ck, "_deferred", None)):
             return
-        if self._mb_split > 1:
+        if self._mb_split > 1 or self._mb_recompute is not None:
             return
         adopted = set(vram.TAKEN.values())
         before = {k: t for k, t in self.vram_state_tensors().items() if t.data_ptr() in adopted}
@@ -776,20 +801,8 @@ class ElasticTrainer:
         # activations and two buffers still fit (the rest stays on adopted memory, still correct)
         reserve = getattr(self, "_act_need", 0) + 2 * max(sizes, default=0)
         can_continue = (lambda: self._hbm_avail() >= reserve) if self.device.type == "cuda" else (lambda: True)
-        alias = [st.get("master") is not None and st["master"].data_ptr() == g.data.data_ptr()
-                 for g, st in zip(self.flat.groups, self.opt.state)]
-        n = self.flat.rehome(is_adopted, can_continue)
-        for g, st, a in zip(self.flat.groups, self.opt.state, alias):
-            if a:
-                st["master"] = g.data   # an fp32 model's master IS its weight buffer
-        n += rehome_state(self.opt.state, is_adopted, can_continue)
-        if self.bufs is not None:
-            n += self.bufs.rehome(is_adopted, can_continue)
+        n = self._move_state(is_adopted, can_continue)
         left = [k for k, t in self.vram_state_tensors().items() if k in before and before[k]() is t]
-        if self.ddp is not None:
-            self.ddp.set_bucket_mb(self.ddp.bucket_mb)      # bucket views of the new gradient buffers
-            if self.dp_comm is not None and self.dp_comm.world_size > 1:
-                self.ddp.set_comm(self.dp_comm)             # the engine maps the new buffers
         if self.device.type == "cuda":
             torch.cuda.current_stream(self.device).synchronize()
         self._rehomed = True    # (once: a partial move is not retried)
@@ -804,6 +817,48 @@ class ElasticTrainer:
         self.events.emit("rehomed", buffers=n, gb=round(sum(sizes) / 2**30, 2), step=self.step,
                          s=round(time.perf_counter() - t0, 3))
         self._publish_vram()    # the next standby can adopt this state again
+        for attempt in range(3):
+            # a buffer whose export failed (seen: 1 of 115 at Llama-3-8B, "invalid argument") moves
+            # once more, to another fresh allocation, and the state is published again
+            if not vram.FAILED or self.device.type != "cuda":
+                break
+            names = list(vram.FAILED)
+            ts = self.vram_state_tensors()
+            targets = [ts[k] for k in names if k in ts]
+            del ts
+            self._move_state(lambda t: any(t is x for x in targets))
+            del targets
+            torch.cuda.current_stream(self.device).synchronize()
+            self.events.emit("rehome_export_retry", names=names[:8], attempt=attempt + 1)
+            self._publish_vram()
+
+    def _move_state(self, pick, can_continue=lambda: True) -> int:
+        """Move the state buffers ``pick(tensor)`` selects to fresh allocations of this process
+        (FlatParams.rehome, optim.rehome_state, FlatBuffers.rehome).  Allocated from a private
+        pool: every buffer gets a segment of its own, never a block of a cached (possibly
+        > 2 GiB) segment, which fails to export."""
+        from easydl_amd.optim import rehome_state
+        alias = [st.get("master") is not None and st["master"].data_ptr() == g.data.data_ptr()
+                 for g, st in zip(self.flat.groups, self.opt.state)]
+        pool = torch.cuda.use_mem_pool(self._state_pool()) if self.device.type == "cuda" else _null()
+        with pool:
+            n = self.flat.rehome(pick, can_continue)
+            for g, st, a in zip(self.flat.groups, self.opt.state, alias):
+                if a:
+                    st["master"] = g.data   # an fp32 model's master IS its weight buffer
+            n += rehome_state(self.opt.state, pick, can_continue)
+            if self.bufs is not None:
+                n += self.bufs.rehome(pick, can_continue)
+        if self.ddp is not None:
+            self.ddp.set_bucket_mb(self.ddp.bucket_mb)      # bucket views of the new gradient buffers
+            if self.dp_comm is not None and self.dp_comm.world_size > 1:
+                self.ddp.set_comm(self.dp_comm)             # the engine maps the new buffers
+        return n
+
+    def _state_pool(self):
+        if getattr(self, "_pool", None) is None:
+            self._pool = torch.cuda.MemPool()
+        return self._pool
 
     def _hbm_avail(self) -> int:
         free, _ = torch.cuda.mem_get_info(self.device)
@@ -817,10 +872,14 @@ class ElasticTrainer:
         (profiles/r05_ttr_headline.md).  Instead, while memory is short, each micro-batch is
         split into smaller ones: the same samples, the same loss weights, the same gradient sum
         (only the order of the bf16 additions differs), at roughly half the activation memory.
+        When not even one sample per micro-batch fits, a model with a ``cfg.recompute`` switch
+        (Llama) recomputes its layers' activations in the backward instead.
         Checked again before every step; full micro-batches return once the memory is back."""
         from easydl_amd.utils import vram
         self._mb_split = 1
-        if (self.device.type != "cuda" or self.tp > 1 or not vram.adopted_any() or self.micro_batch <= 1
+        if self._mb_recompute is not None:
+            self.model.cfg.recompute, self._mb_recompute = self._mb_recompute, None
+        if (self.device.type != "cuda" or self.tp > 1 or not vram.adopted_any()
                 or getattr(self, "kv", None) is None or os.environ.get("EDL_RECOVERY_SPLIT", "1") == "0"):
             return
         need, mbs = vram.read_act(self.kv, f"{self.ctx.role}{self.ctx.index}")
@@ -830,15 +889,25 @@ class ElasticTrainer:
         avail = self._hbm_avail()
         if avail >= need * 1.05:
             return
-        k = next((d for d in range(2, mbs + 1) if mbs % d == 0 and need / d * 1.15 <= avail), mbs)
-        self._mb_split = k
-        self.events.emit("memory_limited_steps", split=k, need_gb=round(need / 2**30, 1),
-                         avail_gb=round(avail / 2**30, 1))
+        k = next((d for d in range(2, mbs + 1) if mbs % d == 0 and need / d * 1.15 <= avail), None)
+        cfg = getattr(self.model, "cfg", None)
+        if k is None and cfg is not None and isinstance(getattr(cfg, "recompute", None), bool):
+            # even one sample per micro-batch would not fit: recompute each layer's activations in
+            # the backward instead (same values, ~1/3 more compute) until the memory is back --
+            # a step that blocks in hipMalloc behind the driver's reclaim costs seconds
+            self._mb_recompute = cfg.recompute
+            cfg.recompute = True
+            k = 1
+        self._mb_split = mbs if k is None else k
+        self.events.emit("memory_limited_steps", split=self._mb_split, recompute=self._mb_recompute is not None,
+                         need_gb=round(need / 2**30, 1), avail_gb=round(avail / 2**30, 1))
 
     def _split_micro_batches(self, mbs: list) -> list:
-        if self._mb_split > 1 and self._hbm_avail() >= self._act_need * 1.05:
+        if (self._mb_split > 1 or self._mb_recompute is not None) and self._hbm_avail() >= self._act_need * 1.05:
             self.events.emit("memory_restored", step=self.step, avail_gb=round(self._hbm_avail() / 2**30, 1))
             self._mb_split = 1
+            if self._mb_recompute is not None:
+                self.model.cfg.recompute, self._mb_recompute = self._mb_recompute, None
         k = self._mb_split
         if k <= 1:
             return mbs
@@ -995,7 +1064,7 @@ class ElasticTrainer:
             total = sum(len(idx) for _, idx in mbs[:res["mb"]]) / plan.global_batch
             self.events.emit("resumed_mid_step", step=self.step + 1, micro_batches_done=res["mb"], of=len(mbs))
             mbs = mbs[res["mb"]:]
-        if self._mb_split > 1:
+        if self._mb_split > 1 or self._mb_recompute is not None:
             mbs = self._split_micro_batches(mbs)
         shadow = self._shadow_active()
         seeded = None

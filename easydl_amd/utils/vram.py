@@ -39,6 +39,7 @@ GROUP_MAX_MB = 960               # flat-group cap (bf16) under hand-over: fp32 s
 _ADOPTED: dict[str, torch.Tensor] = {}
 TAKEN: dict[str, int] = {}       # name -> data_ptr of every adopted tensor a buffer was built on
 STATS = {"exported": 0, "adopted": 0, "adopted_bytes": 0}
+FAILED: list[str] = []           # names the last publish could not export
 
 
 def enabled() -> bool:
@@ -60,6 +61,7 @@ def publish(kv, slot: str, owner: str, tensors: dict[str, torch.Tensor]) -> int:
     descs = {}
     STATS["export_failed"] = 0
     STATS.pop("export_error", None)
+    FAILED.clear()
     for name, t in tensors.items():
         if t is None or not t.is_cuda or _block_bytes(t) > IPC_MAX_BYTES:
             continue
@@ -69,6 +71,7 @@ def publish(kv, slot: str, owner: str, tensors: dict[str, torch.Tensor]) -> int:
             log.debug("vram: %s not exportable: %s", name, e)
             STATS["export_failed"] += 1
             STATS["export_error"] = f"{name}: {e}"[:200]
+            FAILED.append(name)
     gpu = next((t.device.index for t in tensors.values() if t is not None and t.is_cuda), 0)
     kv.set(key(slot), json.dumps({"owner": owner, "pid": os.getpid(), "gpu": gpu, "gen": time.time_ns(),
                                   "tensors": descs}))
