@@ -959,6 +959,8 @@ class ElasticTrainer:
                                                         "slot": f"{self.ctx.role}{self.ctx.index}"}
                 gstep, gmb = getattr(self, "_shadow_cand", (0, 0))
                 sh = self.flat.shadow_tensors()
+                if sh and (gstep, gmb) != (0, 0) and not (gmb and gstep == k + 1):
+                    self.events.emit("grad_shadow_unused", gstep=gstep, gmb=gmb, resume_step=k)
                 if gmb and gstep == k + 1 and sh and not vram.missing(list(sh.items())):
                     # the dead worker had finished gmb micro-batches of step k + 1 (their gradients
                     # are in its shadow): that step resumes at micro-batch gmb (_run_step)
@@ -1093,6 +1095,8 @@ class ElasticTrainer:
                 total += w
                 if shadow and not last:
                     self._shadow_grads(i + 1, loss_acc)
+                if not last:
+                    self.fault.maybe_inject("microbatch", self.step, trainer=self, mb=i)
         t_mb = time.perf_counter()
         if self._phases and self.device.type == "cuda":
             # diagnostic mode: drain the compute stream so 'finish' is the gradient all-reduce alone

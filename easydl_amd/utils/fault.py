@@ -11,6 +11,9 @@
                                  warmed up (utils/vram.py standby_warm_on), at most 30 steps late
     kill@step=6,point=in_update  SIGKILL inside the optimizer update of step 6: after its
                                  ``begin`` step mark reached the GPU, before ``done``
+    kill@step=4,point=microbatch,mb=3
+                                 SIGKILL once the GPU has finished micro-batch 3 of step 4
+                                 (its backward and the gradient shadow's copy), before the next
 
 Several specs may be joined with ``;``.  ``point`` is ``step_start`` unless the
 spec says ``point=after_backward`` / ``point=in_update`` (``nan`` defaults to
@@ -39,6 +42,7 @@ class FaultSpec:
         self.after_ms = float(args.get("after_ms", 0))
         self.wait = args.get("wait")               # "standby": hold off until the spare is warm
         self.max_late = int(args.get("max_late", 30))
+        self.mb = int(args.get("mb", -1))          # point=microbatch: after this micro-batch
         self.fired = False
 
     @classmethod
@@ -68,9 +72,9 @@ class FaultInjector:
         return cls(FaultSpec.parse(os.environ.get("EDL_FAULT", "")), ctx.index, ctx.role, events,
                    int(os.environ.get("EDL_GENERATION", 0)))
 
-    def maybe_inject(self, point: str, step: int, trainer=None) -> None:
+    def maybe_inject(self, point: str, step: int, trainer=None, mb: int | None = None) -> None:
         for s in self.specs:
-            if s.fired or s.point != point:
+            if s.fired or s.point != point or (point == "microbatch" and s.mb != mb):
                 continue
             if s.step != step and not (s.wait and s.step <= step):
                 continue
@@ -88,12 +92,12 @@ class FaultInjector:
                 threading.Thread(target=self._delayed, args=(s, step, trainer), name="edl-fault",
                                  daemon=True).start()
                 continue
-            if point == "in_update" and trainer is not None and getattr(trainer, "device", None) is not None \
-                    and trainer.device.type == "cuda":
-                # the update's ``begin`` mark is written in stream order: make sure it landed, so
-                # the kill is inside the update as far as the step marks can tell
+            if point in ("in_update", "microbatch") and trainer is not None \
+                    and getattr(trainer, "device", None) is not None and trainer.device.type == "cuda":
+                # the update's ``begin`` mark (the micro-batch's shadow copy) is written in stream
+                # order: make sure it landed, so the kill is where the step marks say it is
                 import torch
-                torch.cuda.current_stream(trainer.device).synchronize()
+                torch.cuda.synchronize(trainer.device)
             self._emit(s, step, trainer)
             self._fire(s, trainer)
 
