@@ -13,7 +13,8 @@
                                  ``begin`` step mark reached the GPU, before ``done``
     kill@step=4,point=microbatch,mb=3
                                  SIGKILL once the GPU has finished micro-batch 3 of step 4
-                                 (its backward and the gradient shadow's copy), before the next
+                                 (its backward and the gradient shadow's copy), before the next;
+                                 with ``after_ms``: that long after (inside micro-batch 4)
 
 Several specs may be joined with ``;``.  ``point`` is ``step_start`` unless the
 spec says ``point=after_backward`` / ``point=in_update`` (``nan`` defaults to
@@ -87,17 +88,17 @@ class FaultInjector:
             if s.wait and step < s.step + s.max_late and not self._condition(s, trainer):
                 continue
             s.fired = True
-            if s.after_ms > 0:
-                # the step runs on; the signal lands mid-step (GPU work of this step in flight)
-                threading.Thread(target=self._delayed, args=(s, step, trainer), name="edl-fault",
-                                 daemon=True).start()
-                continue
             if point in ("in_update", "microbatch") and trainer is not None \
                     and getattr(trainer, "device", None) is not None and trainer.device.type == "cuda":
                 # the update's ``begin`` mark (the micro-batch's shadow copy) is written in stream
                 # order: make sure it landed, so the kill is where the step marks say it is
                 import torch
                 torch.cuda.synchronize(trainer.device)
+            if s.after_ms > 0:
+                # the step runs on; the signal lands mid-step (GPU work of this step in flight)
+                threading.Thread(target=self._delayed, args=(s, step, trainer), name="edl-fault",
+                                 daemon=True).start()
+                continue
             self._emit(s, step, trainer)
             self._fire(s, trainer)
 
