@@ -47,10 +47,14 @@ def _td(s: float) -> datetime.timedelta:
     return datetime.timedelta(seconds=s)
 
 
-def _rccl_nonblocking(opts) -> bool:
-    """Non-blocking RCCL communicator init (EDL_RCCL_NONBLOCKING, default on) where this torch
-    exposes the config field."""
-    if os.environ.get("EDL_RCCL_NONBLOCKING", "1") != "1":
+def _rccl_nonblocking(opts, reformed: bool) -> bool:
+    """Non-blocking RCCL communicator init where this torch exposes the config field.
+    ``EDL_RCCL_NONBLOCKING``: "auto" (default) for epochs re-formed after a failure or a
+    membership change only -- the recovery path, where an abort must be able to end an init in
+    progress -- while a job's first epoch keeps RCCL's default blocking init; "1" always; "0"
+    never."""
+    mode = os.environ.get("EDL_RCCL_NONBLOCKING", "auto")
+    if mode == "0" or (mode != "1" and not reformed):
         return False
     cfg = getattr(opts, "config", None)
     if cfg is None or not hasattr(cfg, "blocking"):
@@ -139,7 +143,7 @@ class Communicator:
                 opts = dist.ProcessGroupNCCL.Options()
                 opts.is_high_priority_stream = high_priority
                 opts._timeout = _td(timeout_s)
-                self.nonblocking = _rccl_nonblocking(opts)
+                self.nonblocking = _rccl_nonblocking(opts, reformed=probe != "now")
                 self.data = dist.ProcessGroupNCCL(dist.PrefixStore("data", base), rank, world_size, opts)
                 if self.nonblocking:
                     # ncclCommInitRankConfig with blocking = 0, started now: the bootstrap runs while

@@ -14,6 +14,7 @@ import torch.distributed as dist
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from easydl_amd.parallel.comm import Communicator  # noqa: E402
 
+os.environ.setdefault("EDL_RCCL_NONBLOCKING", "1")     # (default "auto": re-formed epochs only)
 dev = torch.device("cuda", 0)
 torch.cuda.set_device(dev)
 store = dist.TCPStore("127.0.0.1", 0, 1, True, timeout=datetime.timedelta(seconds=60))
