@@ -26,6 +26,8 @@ parameter starts on a 64-element boundary (128 B for bf16) so every view is
 """
 from __future__ import annotations
 
+import contextlib
+
 import os
 import weakref
 from dataclasses import dataclass, field
@@ -204,7 +206,7 @@ class FlatParams:
             self.ensure_shadow()    # a dead worker's shadow: taken now, before unused adoptions are dropped
 
     # -- gradient shadow ------------------------------------------------------
-    def ensure_shadow(self) -> None:
+    def ensure_shadow(self, pool=None) -> None:
         """A second copy of every gradient buffer, plus the partial loss: the trainer copies the
         accumulated gradients into it after each micro-batch but the last (ElasticTrainer
         _shadow_grads, step marks ``gstep`` / ``gmb``).  A replacement that adopts the dead
@@ -214,12 +216,16 @@ class FlatParams:
         if self.gshadow is not None:
             return
         sh = []
-        for g in self.groups:
-            t = vram.take(f"flat/{g.name}/gshadow", g.grad.numel(), g.grad.dtype, self.device, keep=True)
-            sh.append(torch.empty_like(g.grad) if t is None else t)
-        loss = vram.take("flat/gshadow_loss", 1, torch.float32, self.device, keep=True)
+        # ``pool`` (a torch.cuda.MemPool): allocated after training started, a buffer must not be
+        # carved out of a cached activation segment -- its IPC export would map that whole segment
+        ctx = torch.cuda.use_mem_pool(pool) if pool is not None else contextlib.nullcontext()
+        with ctx:
+            for g in self.groups:
+                t = vram.take(f"flat/{g.name}/gshadow", g.grad.numel(), g.grad.dtype, self.device, keep=True)
+                sh.append(torch.empty_like(g.grad) if t is None else t)
+            loss = vram.take("flat/gshadow_loss", 1, torch.float32, self.device, keep=True)
+            self.gshadow_loss = torch.zeros(1, dtype=torch.float32, device=self.device) if loss is None else loss
         self.gshadow = sh
-        self.gshadow_loss = torch.zeros(1, dtype=torch.float32, device=self.device) if loss is None else loss
 
     def shadow_tensors(self) -> dict[str, torch.Tensor]:
         if self.gshadow is None:

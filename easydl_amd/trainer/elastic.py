@@ -757,7 +757,7 @@ class ElasticTrainer:
         self.events.emit("grad_shadow", on=on, gb=round(shadow / 2**30, 1), free_gb=round(free / 2**30, 1),
                          replacement_need_gb=round(need / 2**30, 1))
         if on:
-            self.flat.ensure_shadow()
+            self.flat.ensure_shadow(self._state_pool())
             self._publish_vram()
 
     def _maybe_rehome(self) -> None:
@@ -889,6 +889,10 @@ class ElasticTrainer:
         avail = self._hbm_avail()
         if avail >= need * 1.05:
             return
+        # this process's cached blocks (the standby's warm-up, the model build) go back to the
+        # driver: the short step's allocations then come from one free pool instead of blocks of
+        # other shapes plus new hipMallocs that wait for the driver's reclaim
+        torch.cuda.empty_cache()
         k = next((d for d in range(2, mbs + 1) if mbs % d == 0 and need / d * 1.15 <= avail), None)
         cfg = getattr(self.model, "cfg", None)
         if k is None and cfg is not None and isinstance(getattr(cfg, "recompute", None), bool):

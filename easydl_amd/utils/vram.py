@@ -55,15 +55,41 @@ def _block_bytes(t: torch.Tensor) -> int:
     return t.untyped_storage().nbytes()
 
 
+def _segments(device) -> list[tuple[int, int]]:
+    """(base address, bytes) of every caching-allocator segment on ``device``, sorted."""
+    idx = torch.device(device).index
+    return sorted((int(sg["address"]), int(sg["total_size"])) for sg in torch.cuda.memory_snapshot()
+                  if sg.get("device") == idx)
+
+
+def _segment_bytes(segs: list[tuple[int, int]], ptr: int) -> int:
+    """Size of the segment holding ``ptr`` (0: not a caching-allocator allocation, e.g. imported)."""
+    import bisect
+    i = bisect.bisect_right(segs, (ptr, float("inf"))) - 1
+    if i >= 0 and segs[i][0] <= ptr < segs[i][0] + segs[i][1]:
+        return segs[i][1]
+    return 0
+
+
 def publish(kv, slot: str, owner: str, tensors: dict[str, torch.Tensor]) -> int:
-    """Export ``tensors`` (name -> CUDA tensor owning its whole allocation) for the standby."""
+    """Export ``tensors`` (name -> CUDA tensor owning its whole allocation) for the standby.
+    An IPC handle maps the tensor's whole caching-allocator segment: a tensor that sits in a
+    segment of IPC_MAX_BYTES or more (e.g. a buffer allocated after a step, carved out of a
+    cached activation segment) is not exported -- the standby's open would hang."""
     from easydl_amd.ps.ipc import export_tensor
     descs = {}
     STATS["export_failed"] = 0
     STATS.pop("export_error", None)
     FAILED.clear()
+    devs = {t.device for t in tensors.values() if t is not None and t.is_cuda}
+    segs = {d: _segments(d) for d in devs}
     for name, t in tensors.items():
         if t is None or not t.is_cuda or _block_bytes(t) > IPC_MAX_BYTES:
+            continue
+        if _segment_bytes(segs[t.device], t.data_ptr()) > IPC_MAX_BYTES:
+            STATS["export_failed"] += 1
+            STATS["export_error"] = f"{name}: in a segment of 2 GiB or more"
+            FAILED.append(name)
             continue
         try:
             descs[name] = export_tensor(t)
