@@ -893,7 +893,8 @@ class ElasticTrainer:
         # driver: the short step's allocations then come from one free pool instead of blocks of
         # other shapes plus new hipMallocs that wait for the driver's reclaim
         torch.cuda.empty_cache()
-        k = next((d for d in range(2, mbs + 1) if mbs % d == 0 and need / d * 1.15 <= avail), None)
+        margin = float(os.environ.get("EDL_RECOVERY_MARGIN", "1.15"))
+        k = next((d for d in range(2, mbs + 1) if mbs % d == 0 and need / d * margin <= avail), None)
         cfg = getattr(self.model, "cfg", None)
         if k is None and cfg is not None and isinstance(getattr(cfg, "recompute", None), bool):
             # even one sample per micro-batch would not fit: recompute each layer's activations in

@@ -5,8 +5,10 @@
 set -uo pipefail
 out=gpurun_out/r05_${TAG:-shadow_headline}
 mkdir -p $out
+specs=("" "kill@step=4,index=0,point=microbatch,mb=1,after_ms=350,wait=standby")
+[ -n "${ONLY:-}" ] && specs=("${specs[$ONLY]}")
 i=0
-for spec in "" "kill@step=4,index=0,point=microbatch,mb=1,after_ms=350,wait=standby"; do
+for spec in "${specs[@]}"; do
   i=$((i+1)); mkdir -p $out/k$i
   EDL_BENCH_FAULT_SPEC="$spec" EDL_GRAD_SHADOW=${SHADOW:-force} EDL_TTR_DIR=$out/k$i EDL_TTR_KEEP=1 \
   EDL_FAULT_STEP_MS=2850 timeout -k 10 600 python -u bench.py --fault-inject --gpus 1 --fault-mode midstep \
