@@ -97,10 +97,10 @@ def shard_layout(tensors: list[tuple[str, torch.Tensor]], rank: int, world: int)
 class ShmSegment:
     """Python handle of one /dev/shm A/B segment (csrc/runtime/shm_store.cpp)."""
 
-    def __init__(self, name: str, slot_bytes: int = 0, create: bool = True, pin: bool = False):
+    def __init__(self, name: str, slot_bytes: int = 0, create: bool = True, pin: bool = False, nslots: int = 2):
         self.rt = _native.runtime()
         self.name = name
-        self.h = self.rt("edl_shm_open", name.encode(), slot_bytes, 2, 1 if create else 0)
+        self.h = self.rt("edl_shm_open", name.encode(), slot_bytes, nslots, 1 if create else 0)
         if not self.h:
             raise OSError(f"cannot open shm segment {name}")
         self.slot_bytes = self.rt("edl_shm_slot_bytes", self.h)
@@ -1080,7 +1080,7 @@ def _load_shard(read, table, state, dev, expect: int, what: str, seg=None, slot=
 
 def unlink_job_segments(job: str) -> int:
     n = 0
-    pat = re.compile(rf"^edl-{re.escape(job)}((-t\d+of\d+)?-w\d+-s\d+|-marks-[a-z]+\d+|-ps\d+)$")
+    pat = re.compile(rf"^edl-{re.escape(job)}((-t\d+of\d+)?-w\d+-s\d+|-(marks|gshadow)-[a-z]+\d+|-ps\d+)$")
     for path in glob.glob(f"/dev/shm/edl-{job}-*"):
         if not pat.match(os.path.basename(path)):
             continue

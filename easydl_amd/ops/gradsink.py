@@ -23,7 +23,21 @@ def is_flat(p: torch.Tensor) -> bool:
     return getattr(p, "_edl_flat", False) and p.grad is not None
 
 
+def await_shadow(p: torch.Tensor) -> None:
+    """The caller's stream is about to write ``p``'s gradient: order it after the pending
+    device -> host copy of p's gradient group into the host gradient shadow, if any
+    (utils/gshadow.py; the copy overlaps the next micro-batch until its first write there)."""
+    ev = getattr(p, "_edl_wait", None)
+    if ev is not None:
+        p._edl_wait = None
+        torch.cuda.current_stream(p.device).wait_event(ev)
+
+
 def is_fresh(p: torch.Tensor) -> bool:
+    """True: the next write overwrites ``p``'s gradient (first of the accumulation window).
+    Every direct writer asks this right before it writes, so this is also where the write waits
+    for a pending gradient-shadow copy of it (await_shadow)."""
+    await_shadow(p)
     return getattr(p, "_edl_fresh", True)
 
 

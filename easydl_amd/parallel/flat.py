@@ -34,6 +34,7 @@ from dataclasses import dataclass, field
 
 import torch
 
+from easydl_amd.ops import gradsink
 from easydl_amd.utils import vram
 
 ALIGN = 64
@@ -92,6 +93,7 @@ def _pre_accumulate_hook(ref, key):
         if g is not None and me is not None:   # None: a fused op delivered this gradient itself
             me.saw_autograd = True
             me._autograd_slots.add(key)
+            gradsink.await_shadow(me._slot_of[key][1].param)   # AccumulateGrad writes it next
         return None
     return hook
 
@@ -239,6 +241,10 @@ class FlatParams:
         with torch.no_grad():
             for g, t in zip(self.groups, self.gshadow):
                 g.grad.copy_(t)
+        self.mark_accumulating()
+
+    def mark_accumulating(self) -> None:
+        """The gradient buffers hold a partial sum: every later write accumulates onto it."""
         for g in self.groups:
             for s in g.slots:
                 s.param._edl_fresh = False
@@ -289,7 +295,7 @@ class FlatParams:
         """Zero gradients of parameters that received none this window (unused params)."""
         for g in self.groups:
             for s in g.slots:
-                if s.param._edl_fresh:
+                if gradsink.is_fresh(s.param):
                     s.param.grad.zero_()
                     s.param._edl_fresh = False
 

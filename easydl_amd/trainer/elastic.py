@@ -153,7 +153,8 @@ class ElasticTrainer:
         self._mb_recompute = None    # not None: the model's recompute flag to restore (_memory_plan)
         self._shadow_stream = None   # gradient shadow copies (_shadow_grads)
         self._shadow_pending = False
-        self._shadow_resume = None   # {"step", "mb"}: resume that step at that micro-batch
+        self._shadow_resume = None   # {"step", "mb", "host"}: resume that step at that micro-batch
+        self._hshadow = None         # host gradient shadow (utils/gshadow.py), when HBM has no room
         self._act_need = 0
 
     def request_stop(self) -> None:
@@ -753,12 +754,31 @@ class ElasticTrainer:
             free -= int(float(os.environ.get("EDL_STANDBY_RESERVE_GB", "16")) * 2**30)
         shadow = sum(g.grad.untyped_storage().nbytes() for g in self.flat.groups)
         need = act / max(1, self.micro_batch) * 1.15
-        on = free - shadow >= need or os.environ.get("EDL_GRAD_SHADOW") == "force"
-        self.events.emit("grad_shadow", on=on, gb=round(shadow / 2**30, 1), free_gb=round(free / 2**30, 1),
-                         replacement_need_gb=round(need / 2**30, 1))
-        if on:
+        mode = os.environ.get("EDL_GRAD_SHADOW", "1")
+        where = ("hbm" if mode == "force" or (mode != "host" and free - shadow >= need) else "host")
+        self.events.emit("grad_shadow", on=True, where=where, gb=round(shadow / 2**30, 1),
+                         free_gb=round(free / 2**30, 1), replacement_need_gb=round(need / 2**30, 1))
+        if where == "hbm":
             self.flat.ensure_shadow(self._state_pool())
             self._publish_vram()
+            return
+        # host memory: the page-locked segment is created and registered off the step path; the
+        # shadow copies start once it is ready
+        from easydl_amd.utils.gshadow import HostShadow
+        slot = f"{self.ctx.role}{self.ctx.index}"
+
+        def make():
+            t0 = time.perf_counter()
+            try:
+                hs = HostShadow(self.ctx.job, slot, self.flat.groups)
+            except Exception as e:  # noqa: BLE001 - an optimisation: without it a step is recomputed
+                self.events.emit("grad_shadow_failed", where="host", error=str(e)[:200])
+                return
+            self._hshadow_views = (hs.group_views(), hs.loss_view())
+            self._hshadow = hs
+            self.events.emit("grad_shadow_ready", where="host", pinned=hs.pinned, gb=round(hs.total / 2**30, 1),
+                             s=round(time.perf_counter() - t0, 3))
+        threading.Thread(target=make, name="edl-gshadow", daemon=True).start()
 
     def _maybe_rehome(self) -> None:
         """Once a takeover's state is settled, move everything built on the dead worker's HBM into
@@ -964,12 +984,13 @@ class ElasticTrainer:
                                                         "slot": f"{self.ctx.role}{self.ctx.index}"}
                 gstep, gmb = getattr(self, "_shadow_cand", (0, 0))
                 sh = self.flat.shadow_tensors()
-                if sh and (gstep, gmb) != (0, 0) and not (gmb and gstep == k + 1):
+                host = not sh and self._host_shadow_exists()
+                if (sh or host) and (gstep, gmb) != (0, 0) and not (gmb and gstep == k + 1):
                     self.events.emit("grad_shadow_unused", gstep=gstep, gmb=gmb, resume_step=k)
-                if gmb and gstep == k + 1 and sh and not vram.missing(list(sh.items())):
+                if gmb and gstep == k + 1 and (host or (sh and not vram.missing(list(sh.items())))):
                     # the dead worker had finished gmb micro-batches of step k + 1 (their gradients
                     # are in its shadow): that step resumes at micro-batch gmb (_run_step)
-                    self._shadow_resume = {"step": gstep, "mb": gmb}
+                    self._shadow_resume = {"step": gstep, "mb": gmb, "host": host}
                     if verify is not None:
                         verify["shadow"] = (gstep, gmb)
                 src = self.checkpoint.resume_from_hbm(self, k, verify)
@@ -1063,14 +1084,21 @@ class ElasticTrainer:
         self.flat.zero_grad()
         total = 0.0
         loss_acc = None
+        if self._hshadow is not None and self._shadow_stream is not None:
+            torch.cuda.current_stream(self.device).wait_stream(self._shadow_stream)
         res, self._shadow_resume = self._shadow_resume, None
         if res is not None and res["step"] == self.step + 1 and 0 < res["mb"] < len(mbs):
             # mid-step resume: the dead worker's gradients of micro-batches [0, mb) from its shadow
-            self.flat.load_shadow()
-            loss_acc = self.flat.gshadow_loss[0].clone()
-            total = sum(len(idx) for _, idx in mbs[:res["mb"]]) / plan.global_batch
-            self.events.emit("resumed_mid_step", step=self.step + 1, micro_batches_done=res["mb"], of=len(mbs))
-            mbs = mbs[res["mb"]:]
+            if res.get("host"):
+                loss_acc = self._load_host_shadow()
+            else:
+                self.flat.load_shadow()
+                loss_acc = self.flat.gshadow_loss[0].clone()
+            if loss_acc is not None:
+                total = sum(len(idx) for _, idx in mbs[:res["mb"]]) / plan.global_batch
+                self.events.emit("resumed_mid_step", step=self.step + 1, micro_batches_done=res["mb"],
+                                 of=len(mbs), host=bool(res.get("host")))
+                mbs = mbs[res["mb"]:]
         if self._mb_split > 1 or self._mb_recompute is not None:
             mbs = self._split_micro_batches(mbs)
         shadow = self._shadow_active()
@@ -1118,6 +1146,11 @@ class ElasticTrainer:
         self._t_mb = t_mb
         return None if loss_acc is None else loss_acc / total
 
+    def _host_shadow_exists(self) -> bool:
+        from easydl_amd.utils.gshadow import seg_name
+        return self.device.type == "cuda" and os.path.exists(
+            "/dev/shm" + seg_name(self.ctx.job, f"{self.ctx.role}{self.ctx.index}"))
+
     def _shadow_wanted(self) -> bool:
         """Gradient shadows pay off where a replacement resumes from this process's HBM: one rank
         (HBM resume needs world 1), VRAM hand-over on, several micro-batches per step."""
@@ -1127,8 +1160,8 @@ class ElasticTrainer:
                 and self.global_batch > self.micro_batch and os.environ.get("EDL_GRAD_SHADOW", "1") != "0")
 
     def _shadow_active(self) -> bool:
-        return (self._marks is not None and self.flat.gshadow is not None and self._mb_split == 1
-                and self.comm.world_size == 1)
+        return (self._marks is not None and (self.flat.gshadow is not None or self._hshadow is not None)
+                and self._mb_split == 1 and self.comm.world_size == 1)
 
     def _shadow_grads(self, mbs_done: int, loss_acc) -> None:
         """After a micro-batch's backward: copy the accumulated gradients (and the partial loss)
@@ -1137,6 +1170,9 @@ class ElasticTrainer:
         for the copy.  Gradients no micro-batch has written yet are zeroed first (as the end of
         the step would), so the shadow is exact."""
         self.flat.finalize_untouched()
+        if self.flat.gshadow is None:
+            self._shadow_to_host(mbs_done, loss_acc)
+            return
 
         def copy(st):
             self._marks.shadow(self.step + 1, 0, st)
@@ -1156,6 +1192,56 @@ class ElasticTrainer:
             copy(st)
         loss_acc.record_stream(st)
         self._shadow_pending = True
+
+    def _load_host_shadow(self):
+        """The dead worker's host shadow -> this process's gradient buffers (pipelined shm -> HBM
+        copy); returns the partial loss (a 0-d CUDA tensor)."""
+        from easydl_amd.utils.gshadow import HostShadow
+        t0 = time.perf_counter()
+        loss = torch.zeros(1, dtype=torch.float32, device=self.device)
+        stats: dict = {}
+        try:
+            hs = HostShadow(self.ctx.job, f"{self.ctx.role}{self.ctx.index}", self.flat.groups, create=False,
+                            pin=False)
+            try:
+                hs.load_into(self.flat.groups, loss, stats)
+            finally:
+                hs.close()
+        except (OSError, RuntimeError) as e:
+            # the whole step is recomputed instead, from zeroed gradients (a failed copy may have
+            # written part of them)
+            with torch.no_grad():
+                for g in self.flat.groups:
+                    g.grad.zero_()
+            self.events.emit("grad_shadow_load_failed", where="host", error=str(e)[:200])
+            return None
+        self.flat.mark_accumulating()
+        self.events.emit("grad_shadow_loaded", where="host", s=round(time.perf_counter() - t0, 3),
+                         gbps=stats.get("gbps"))
+        return loss[0]
+
+    def _shadow_to_host(self, mbs_done: int, loss_acc) -> None:
+        """Host gradient shadow (utils/gshadow.py): device -> host copies group by group on a side
+        stream, in the order the next backward writes the groups; each parameter's next write
+        waits for its group's copy only (gradsink.await_shadow), not the next micro-batch for all
+        of them."""
+        views, loss_view = self._hshadow_views
+        main = torch.cuda.current_stream(self.device)
+        if self._shadow_stream is None:
+            self._shadow_stream = torch.cuda.Stream(device=self.device)
+        st = self._shadow_stream
+        st.wait_stream(main)
+        with torch.cuda.stream(st):
+            self._marks.shadow(self.step + 1, 0, st)
+            for g, hv in zip(self.flat.groups, views):
+                hv.copy_(g.grad.view(-1), non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(st)
+                for sl in g.slots:
+                    sl.param._edl_wait = ev
+            loss_view.copy_(loss_acc.reshape(1).float(), non_blocking=True)
+            self._marks.shadow(self.step + 1, mbs_done, st)
+        loss_acc.record_stream(st)
 
     def _sync_point(self) -> bool:
         """Host-side completion of every gradient all-reduce; False if the epoch broke.
