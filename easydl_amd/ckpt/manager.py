@@ -655,7 +655,7 @@ class CheckpointManager:
             time.sleep(0.01)
         now = read_slot(v["job"], v["slot"], shadow=True)
         out["s"] = round(time.perf_counter() - t0, 3)
-        ok = now is not None and now[:2] == v["marks"] and (v.get("shadow") is None or now[3:5] == v["shadow"])
+        ok = now is not None and now[:2] == v["marks"] and (v.get("shadow") is None or now[3:7] == v["shadow"])
         out["result"] = "ok" if ok else f"marks moved: {v['marks']} {v.get('shadow')} -> {now}"
 
     def hbm_unverified(self) -> bool:

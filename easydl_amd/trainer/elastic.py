@@ -774,7 +774,7 @@ class ElasticTrainer:
             except Exception as e:  # noqa: BLE001 - an optimisation: without it a step is recomputed
                 self.events.emit("grad_shadow_failed", where="host", error=str(e)[:200])
                 return
-            self._hshadow_views = (hs.group_views(), hs.loss_view())
+            self._hshadow_views = [(hs.group_views(i), hs.loss_view(i)) for i in (0, 1)]
             self._hshadow = hs
             self.events.emit("grad_shadow_ready", where="host", pinned=hs.pinned, gb=round(hs.total / 2**30, 1),
                              s=round(time.perf_counter() - t0, 3))
@@ -954,8 +954,8 @@ class ElasticTrainer:
         marks = stepmarks.read_slot(self.ctx.job, f"{self.ctx.role}{self.ctx.index}", shadow=True)
         if marks is None:
             return None
-        begin, done, writer, gstep, gmb = marks
-        self._shadow_cand = (gstep, gmb)
+        begin, done, writer, *shadow = marks
+        self._shadow_cand = tuple(shadow)
         if writer != pid or begin != done:
             self.events.emit("hbm_resume_refused", begin=begin, done=done, writer=writer, adopted_from=pid)
             return None
@@ -982,17 +982,19 @@ class ElasticTrainer:
                 pid = vram.ADOPTED_FROM.get("pid")
                 verify = None if vram.reaped(pid) else {"pid": pid, "marks": (k, k), "job": self.ctx.job,
                                                         "slot": f"{self.ctx.role}{self.ctx.index}"}
-                gstep, gmb = getattr(self, "_shadow_cand", (0, 0))
+                from easydl_amd.utils.stepmarks import best_shadow
+                cand = getattr(self, "_shadow_cand", (0, 0, 0, 0))
                 sh = self.flat.shadow_tensors()
                 host = not sh and self._host_shadow_exists()
-                if (sh or host) and (gstep, gmb) != (0, 0) and not (gmb and gstep == k + 1):
-                    self.events.emit("grad_shadow_unused", gstep=gstep, gmb=gmb, resume_step=k)
-                if gmb and gstep == k + 1 and (host or (sh and not vram.missing(list(sh.items())))):
-                    # the dead worker had finished gmb micro-batches of step k + 1 (their gradients
-                    # are in its shadow): that step resumes at micro-batch gmb (_run_step)
-                    self._shadow_resume = {"step": gstep, "mb": gmb, "host": host}
+                best = best_shadow(cand if host else cand[:2], k + 1)   # (the HBM shadow: slot 0 only)
+                if (sh or host) and best is None and any(cand[1::2]):
+                    self.events.emit("grad_shadow_unused", marks=list(cand), resume_step=k)
+                if best is not None and (host or not vram.missing(list(sh.items()))):
+                    # the dead worker had finished best[1] micro-batches of step k + 1 (their
+                    # gradients are in its shadow): that step resumes there (_run_step)
+                    self._shadow_resume = {"step": k + 1, "mb": best[1], "host": host, "slot": best[0]}
                     if verify is not None:
-                        verify["shadow"] = (gstep, gmb)
+                        verify["shadow"] = tuple(cand)
                 src = self.checkpoint.resume_from_hbm(self, k, verify)
                 self.events.emit("restored", step=self.step, source=src, s=round(time.perf_counter() - t0, 3))
                 return True
@@ -1090,7 +1092,7 @@ class ElasticTrainer:
         if res is not None and res["step"] == self.step + 1 and 0 < res["mb"] < len(mbs):
             # mid-step resume: the dead worker's gradients of micro-batches [0, mb) from its shadow
             if res.get("host"):
-                loss_acc = self._load_host_shadow()
+                loss_acc = self._load_host_shadow(res["slot"])
             else:
                 self.flat.load_shadow()
                 loss_acc = self.flat.gshadow_loss[0].clone()
@@ -1193,9 +1195,9 @@ class ElasticTrainer:
         loss_acc.record_stream(st)
         self._shadow_pending = True
 
-    def _load_host_shadow(self):
-        """The dead worker's host shadow -> this process's gradient buffers (pipelined shm -> HBM
-        copy); returns the partial loss (a 0-d CUDA tensor)."""
+    def _load_host_shadow(self, slot: int):
+        """The dead worker's host shadow ``slot`` -> this process's gradient buffers (pipelined
+        shm -> HBM copy); returns the partial loss (a 0-d CUDA tensor), None if it failed."""
         from easydl_amd.utils.gshadow import HostShadow
         t0 = time.perf_counter()
         loss = torch.zeros(1, dtype=torch.float32, device=self.device)
@@ -1204,7 +1206,7 @@ class ElasticTrainer:
             hs = HostShadow(self.ctx.job, f"{self.ctx.role}{self.ctx.index}", self.flat.groups, create=False,
                             pin=False)
             try:
-                hs.load_into(self.flat.groups, loss, stats)
+                hs.load_into(self.flat.groups, loss, slot, stats)
             finally:
                 hs.close()
         except (OSError, RuntimeError) as e:
@@ -1216,7 +1218,7 @@ class ElasticTrainer:
             self.events.emit("grad_shadow_load_failed", where="host", error=str(e)[:200])
             return None
         self.flat.mark_accumulating()
-        self.events.emit("grad_shadow_loaded", where="host", s=round(time.perf_counter() - t0, 3),
+        self.events.emit("grad_shadow_loaded", where="host", slot=slot, s=round(time.perf_counter() - t0, 3),
                          gbps=stats.get("gbps"))
         return loss[0]
 
@@ -1225,14 +1227,15 @@ class ElasticTrainer:
         stream, in the order the next backward writes the groups; each parameter's next write
         waits for its group's copy only (gradsink.await_shadow), not the next micro-batch for all
         of them."""
-        views, loss_view = self._hshadow_views
+        slot = self._hshadow_next = 1 - getattr(self, "_hshadow_next", 1)   # alternate: 0, 1, 0, ...
+        views, loss_view = self._hshadow_views[slot]
         main = torch.cuda.current_stream(self.device)
         if self._shadow_stream is None:
             self._shadow_stream = torch.cuda.Stream(device=self.device)
         st = self._shadow_stream
         st.wait_stream(main)
         with torch.cuda.stream(st):
-            self._marks.shadow(self.step + 1, 0, st)
+            self._marks.shadow(self.step + 1, 0, st, slot)
             for g, hv in zip(self.flat.groups, views):
                 hv.copy_(g.grad.view(-1), non_blocking=True)
                 ev = torch.cuda.Event()
@@ -1240,7 +1243,7 @@ class ElasticTrainer:
                 for sl in g.slots:
                     sl.param._edl_wait = ev
             loss_view.copy_(loss_acc.reshape(1).float(), non_blocking=True)
-            self._marks.shadow(self.step + 1, mbs_done, st)
+            self._marks.shadow(self.step + 1, mbs_done, st, slot)
         loss_acc.record_stream(st)
 
     def _sync_point(self) -> bool:

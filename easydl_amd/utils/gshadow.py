@@ -17,9 +17,11 @@ instead (``/edl-<job>-gshadow-<slot>``, csrc/runtime/shm_store.cpp, one slot):
   shm -> HBM restore (ckpt/manager.py ``_restore_items``) and runs only the remaining
   micro-batches.
 
-Layout: the groups' gradient bytes at 4 KiB-aligned offsets in group order, then the partial loss
-(fp32).  A reader derives the same offsets from its own (identical) flat groups and checks the
-segment size.
+Two slots, written alternately: while one is being copied into (its step mark invalidated) the
+other still holds the previous micro-batch's sum, so a kill during a copy loses one micro-batch,
+not the step.  Layout of a slot: the groups' gradient bytes at 4 KiB-aligned offsets in group
+order, then the partial loss (fp32).  A reader derives the same offsets from its own (identical)
+flat groups and checks the segment size.
 """
 from __future__ import annotations
 
@@ -48,30 +50,30 @@ class HostShadow:
         from easydl_amd.ckpt.manager import ShmSegment
         self.sizes = [g.grad.numel() * g.grad.element_size() for g in groups]
         self.offsets, self.loss_off, self.total = layout(self.sizes)
-        self.seg = ShmSegment(seg_name(job, slot), self.total, create=create, pin=pin, nslots=1)
+        self.seg = ShmSegment(seg_name(job, slot), self.total, create=create, pin=pin, nslots=2)
         if self.seg.slot_bytes < self.total:
             self.seg.close()
             raise OSError(f"gradient shadow segment {seg_name(job, slot)}: {self.seg.slot_bytes} < {self.total} bytes")
-        self.base = self.seg.data(0)
+        self.bases = [self.seg.data(0), self.seg.data(1)]
         self.pinned = self.seg.pinned
         self.dtypes = [g.grad.dtype for g in groups]
 
-    def _host(self, off: int, nbytes: int, dtype: torch.dtype) -> torch.Tensor:
-        buf = (ctypes.c_uint8 * nbytes).from_address(self.base + off)
+    def _host(self, slot: int, off: int, nbytes: int, dtype: torch.dtype) -> torch.Tensor:
+        buf = (ctypes.c_uint8 * nbytes).from_address(self.bases[slot] + off)
         return torch.frombuffer(buf, dtype=torch.uint8).view(dtype)
 
-    def group_views(self) -> list[torch.Tensor]:
-        return [self._host(o, n, dt) for o, n, dt in zip(self.offsets, self.sizes, self.dtypes)]
+    def group_views(self, slot: int) -> list[torch.Tensor]:
+        return [self._host(slot, o, n, dt) for o, n, dt in zip(self.offsets, self.sizes, self.dtypes)]
 
-    def loss_view(self) -> torch.Tensor:
-        return self._host(self.loss_off, 4, torch.float32)
+    def loss_view(self, slot: int) -> torch.Tensor:
+        return self._host(slot, self.loss_off, 4, torch.float32)
 
-    def load_into(self, groups, loss_out: torch.Tensor, stats: dict | None = None) -> None:
-        """Shadow -> the gradient buffers and ``loss_out`` (a CUDA fp32 [1]), pipelined."""
+    def load_into(self, groups, loss_out: torch.Tensor, slot: int, stats: dict | None = None) -> None:
+        """Shadow ``slot`` -> the gradient buffers and ``loss_out`` (a CUDA fp32 [1]), pipelined."""
         from easydl_amd.ckpt.manager import _restore_items
         items = [(g.grad.view(-1), o) for g, o in zip(groups, self.offsets)] + [(loss_out, self.loss_off)]
         dev = loss_out.device
-        _restore_items(self.seg, 0, items, dev, torch.cuda.current_stream(dev), {} if stats is None else stats)
+        _restore_items(self.seg, slot, items, dev, torch.cuda.current_stream(dev), {} if stats is None else stats)
 
     def close(self, unlink: bool = False) -> None:
         self.seg.close(unlink)

@@ -7,10 +7,12 @@ page-locked and device-mapped), read by the process that replaces it:
 * ``begin`` = the step whose update is about to start (written before the optimizer kernels),
 * ``done``  = the step whose update has finished (written after them),
 * ``pid``   = the writer,
-* ``gstep``, ``gmb`` = the gradient shadow (``FlatParams.ensure_shadow``) holds the summed
-  gradients of micro-batches ``[0, gmb)`` of step ``gstep``; ``gmb = 0``: no valid shadow.  The
-  shadow is copied on a side stream after a micro-batch's backward, between an invalidating
-  write (``gmb = 0``) and this mark, so a kill in the middle of the copy leaves ``gmb = 0``.
+* ``gstep``, ``gmb`` (one pair per shadow slot, 2 slots) = that slot of the gradient shadow
+  (``FlatParams.ensure_shadow`` in HBM: slot 0 only; utils/gshadow.py in host memory: the two
+  slots alternate) holds the summed gradients of micro-batches ``[0, gmb)`` of step ``gstep``;
+  ``gmb = 0``: not valid.  A slot is copied on a side stream after a micro-batch's backward,
+  between an invalidating write (``gmb = 0``) and its mark, so a kill in the middle of the copy
+  leaves ``gmb = 0`` there -- and the other host slot still holds the previous micro-batch.
 
 When a worker is SIGKILLed, its GPU queues stop (utils/procfs.py).  If ``begin == done == K``
 no update was in flight, so the weights, fp32 master and moments in its HBM are exactly the
@@ -32,7 +34,17 @@ import torch
 
 from easydl_amd import _native
 
-BEGIN, DONE, PID, GSTEP, GMB = 0, 4, 8, 16, 20     # byte offsets in the page
+BEGIN, DONE, PID, GSTEP, GMB = 0, 4, 8, 16, 20     # byte offsets in the page (GSTEP/GMB: + 8 per slot)
+
+
+def best_shadow(marks: tuple, step: int) -> tuple[int, int] | None:
+    """(shadow slot, micro-batches) of the fullest valid shadow of ``step`` among the
+    (gstep, gmb) pairs ``marks`` = (gstep0, gmb0, gstep1, gmb1); None if none is."""
+    ok = [(marks[2 * s + 1], s) for s in range(len(marks) // 2) if marks[2 * s + 1] and marks[2 * s] == step]
+    if not ok:
+        return None
+    mb, s = max(ok)
+    return s, mb
 
 
 def page_name(job: str, slot: str) -> str:
@@ -61,6 +73,7 @@ class StepMarks:
         self._u32(BEGIN).value = step & 0xFFFFFFFF
         self._u32(DONE).value = step & 0xFFFFFFFF
         self._u32(GMB).value = 0
+        self._u32(GMB + 8).value = 0
         ctypes.c_int64.from_address(self.host + PID).value = os.getpid()
 
     def _mark(self, off: int, step: int, stream) -> None:
@@ -76,19 +89,19 @@ class StepMarks:
     def done(self, step: int, stream=None) -> None:
         self._mark(DONE, step, stream)
 
-    def shadow(self, step: int, mb: int, stream=None) -> None:
-        """Gradient shadow: ``mb`` = 0 before a copy starts, then (``step``, ``mb``) after it."""
+    def shadow(self, step: int, mb: int, stream=None, slot: int = 0) -> None:
+        """Gradient shadow ``slot``: ``mb`` = 0 before a copy starts, then (``step``, ``mb``) after it."""
         if mb:
-            self._mark(GSTEP, step, stream)
-        self._mark(GMB, mb, stream)
+            self._mark(GSTEP + 8 * slot, step, stream)
+        self._mark(GMB + 8 * slot, mb, stream)
 
     def read(self) -> tuple[int, int, int]:
         return (self._u32(BEGIN).value, self._u32(DONE).value,
                 ctypes.c_int64.from_address(self.host + PID).value)
 
-    def read_shadow(self) -> tuple[int, int]:
-        """(gstep, gmb) of the gradient shadow."""
-        return self._u32(GSTEP).value, self._u32(GMB).value
+    def read_shadow(self, slot: int = 0) -> tuple[int, int]:
+        """(gstep, gmb) of gradient-shadow ``slot``."""
+        return self._u32(GSTEP + 8 * slot).value, self._u32(GMB + 8 * slot).value
 
     def close(self, unlink: bool = False) -> None:
         if self.h:
@@ -97,13 +110,13 @@ class StepMarks:
 
 
 def read_slot(job: str, slot: str, shadow: bool = False) -> tuple | None:
-    """(begin, done, pid) of a slot's page -- plus (gstep, gmb) with ``shadow`` -- or None if
-    there is none."""
+    """(begin, done, pid) of a slot's page -- plus (gstep0, gmb0, gstep1, gmb1) with ``shadow``
+    -- or None if there is none."""
     try:
         m = StepMarks(job, slot, create=False)
     except OSError:
         return None
     try:
-        return m.read() + (m.read_shadow() if shadow else ())
+        return m.read() + ((m.read_shadow(0) + m.read_shadow(1)) if shadow else ())
     finally:
         m.close()

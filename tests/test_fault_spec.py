@@ -42,3 +42,13 @@ def test_index_role_and_generation_filters():
     inj3 = _Recorder(FaultSpec.parse("kill@step=1;raise@step=1,gen=1"), generation=1)
     inj3.maybe_inject("step_start", 1)
     assert [k for k, _, _ in inj3.fired] == ["raise"]
+
+
+def test_best_shadow_picks_the_fullest_valid_slot_of_the_step():
+    from easydl_amd.utils.stepmarks import best_shadow
+    assert best_shadow((5, 1, 5, 2), 5) == (1, 2)
+    assert best_shadow((5, 3, 5, 0), 5) == (0, 3)        # slot 1 invalidated mid-copy
+    assert best_shadow((5, 1, 4, 3), 5) == (0, 1)        # slot 1 is the previous step's
+    assert best_shadow((4, 3, 4, 2), 5) is None
+    assert best_shadow((5, 0, 5, 0), 5) is None
+    assert best_shadow((5, 2), 5) == (0, 2)              # the HBM shadow: one slot

@@ -74,7 +74,7 @@ def _died_worker(tmp_path, steps=3):
 
 def _marks(monkeypatch, k, pid):
     monkeypatch.setattr(stepmarks, "read_slot",
-                        lambda job, slot, shadow=False: (k, k, pid) + ((0, 0) if shadow else ()))
+                        lambda job, slot, shadow=False: (k, k, pid) + ((0, 0, 0, 0) if shadow else ()))
 
 
 def test_hbm_resume_adopts_every_state_tensor_including_batchnorm_buffers(tmp_path, monkeypatch):
@@ -137,7 +137,7 @@ def test_adopted_buffers_without_resume_or_snapshot_equal_a_fresh_start(tmp_path
     _, exported = _died_worker(tmp_path)
     pid = _dead_pid()
     monkeypatch.setattr(stepmarks, "read_slot",
-                        lambda job, slot, shadow=False: (4, 3, pid) + ((0, 0) if shadow else ()))   # begin != done
+                        lambda job, slot, shadow=False: (4, 3, pid) + ((0,) * 4 if shadow else ()))   # begin != done
     vram.adopt(exported, pid=pid)
     try:
         b = _mk(tmp_path, 5, None, sub="b")
@@ -294,7 +294,7 @@ def test_mid_step_resume_from_the_gradient_shadow_is_bit_exact(tmp_path, monkeyp
     a._marks.close(unlink=True)
     assert "flat/gshadow_loss" in exported
     monkeypatch.setattr(stepmarks, "read_slot",
-                        lambda job, slot, shadow=False: (3, 3, pid) + ((4, 2) if shadow else ()))
+                        lambda job, slot, shadow=False: (3, 3, pid) + ((4, 2, 0, 0) if shadow else ()))
     vram.adopt(exported, pid=pid)
     ck = CheckpointManager(JOB, interval=100)
     try:

@@ -48,7 +48,7 @@ def test_mid_step_resume_from_the_host_shadow_is_bit_exact(cuda, tmp_path, monke
     slot = f"{a.ctx.role}{a.ctx.index}"
     a._marks = stepmarks.StepMarks(JOB, slot, device=cuda)          # GPU-written marks
     hs = HostShadow(JOB, slot, a.flat.groups)
-    a._hshadow, a._hshadow_views = hs, (hs.group_views(), hs.loss_view())
+    a._hshadow, a._hshadow_views = hs, [(hs.group_views(i), hs.loss_view(i)) for i in (0, 1)]
     calls = {"n": 0}
 
     def dies(m, b):
@@ -61,7 +61,8 @@ def test_mid_step_resume_from_the_host_shadow_is_bit_exact(cuda, tmp_path, monke
     except KeyboardInterrupt:
         pass
     torch.cuda.synchronize()
-    assert a.step == 3 and a._marks.read_shadow() == (4, 2), a._marks.read_shadow()
+    # two slots, alternating: micro-batch 0's sum in slot 0, micro-batches 0-1 in slot 1
+    assert a.step == 3 and (a._marks.read_shadow(0), a._marks.read_shadow(1)) == ((4, 1), (4, 2))
     for g in a.flat.groups:
         g.grad.add_(1.0)            # the in-flight backward's partial adds: the shadow must be used
     exported = {k: t.clone() for k, t in a.vram_state_tensors().items()}
@@ -69,7 +70,7 @@ def test_mid_step_resume_from_the_host_shadow_is_bit_exact(cuda, tmp_path, monke
     hs.close()
     a._marks.close()
     monkeypatch.setattr(stepmarks, "read_slot",
-                        lambda job, s, shadow=False: (3, 3, dead) + ((4, 2) if shadow else ()))
+                        lambda job, s, shadow=False: (3, 3, dead) + ((4, 1, 4, 2) if shadow else ()))
     vram.adopt(exported, pid=dead)
     ck = CheckpointManager(JOB, interval=100)
     try:
@@ -78,7 +79,7 @@ def test_mid_step_resume_from_the_host_shadow_is_bit_exact(cuda, tmp_path, monke
         ev = [r for r in b.events.records if r["kind"] in ("restored", "resumed_mid_step", "grad_shadow_loaded")]
         kinds = [r["kind"] for r in ev]
         assert kinds == ["restored", "grad_shadow_loaded", "resumed_mid_step"], ev
-        assert ev[2]["micro_batches_done"] == 2 and ev[2]["host"] is True
+        assert ev[2]["micro_batches_done"] == 2 and ev[2]["host"] is True and ev[1]["slot"] == 1
         vram.adopt({})
         ref = _mk(tmp_path, "ref", 1, cuda).fit(lambda m, x: m(*x), data, num_steps=6)
         got, want = _state(b), _state(ref)
