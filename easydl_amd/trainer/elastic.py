@@ -755,9 +755,17 @@ class ElasticTrainer:
         shadow = sum(g.grad.untyped_storage().nbytes() for g in self.flat.groups)
         need = act / max(1, self.micro_batch) * 1.15
         mode = os.environ.get("EDL_GRAD_SHADOW", "1")
-        where = ("hbm" if mode == "force" or (mode != "host" and free - shadow >= need) else "host")
-        self.events.emit("grad_shadow", on=True, where=where, gb=round(shadow / 2**30, 1),
+        # default: HBM where it fits, else none.  The host shadow is opt-in ("host"): at the 8B
+        # headline its device -> host copies share the host link with the snapshots' (every 2
+        # steps), so a kill right after a snapshot step found no finished copy, and the dead
+        # worker's 30 GB of page-locked memory delayed its teardown and the replacement's first
+        # step by ~0.3 s (profiles/r05_grad_shadow_ab.md)
+        where = ("hbm" if mode == "force" or (mode != "host" and free - shadow >= need)
+                 else "host" if mode == "host" else None)
+        self.events.emit("grad_shadow", on=where is not None, where=where, gb=round(shadow / 2**30, 1),
                          free_gb=round(free / 2**30, 1), replacement_need_gb=round(need / 2**30, 1))
+        if where is None:
+            return
         if where == "hbm":
             self.flat.ensure_shadow(self._state_pool())
             self._publish_vram()
