@@ -917,10 +917,6 @@ class ElasticTrainer:
         avail = self._hbm_avail()
         if avail >= need * 1.05:
             return
-        # this process's cached blocks (the standby's warm-up, the model build) go back to the
-        # driver: the short step's allocations then come from one free pool instead of blocks of
-        # other shapes plus new hipMallocs that wait for the driver's reclaim
-        torch.cuda.empty_cache()
         margin = float(os.environ.get("EDL_RECOVERY_MARGIN", "1.15"))
         k = next((d for d in range(2, mbs + 1) if mbs % d == 0 and need / d * margin <= avail), None)
         cfg = getattr(self.model, "cfg", None)
