@@ -845,8 +845,9 @@ class ElasticTrainer:
         self.events.emit("rehomed", buffers=n, gb=round(sum(sizes) / 2**30, 2), step=self.step,
                          s=round(time.perf_counter() - t0, 3))
         self._publish_vram()    # the next standby can adopt this state again
-        for attempt in range(3):
-            # a buffer whose export failed (seen: 1 of 115 at Llama-3-8B, "invalid argument") moves
+        for attempt in range(5):
+            # a buffer whose export failed ("invalid argument": 1-8 of 95 at Llama-3-8B, where a new
+            # allocation reuses an address range an imported buffer had; profiles/r05_three_failures_8b.md) moves
             # once more, to another fresh allocation, and the state is published again
             if not vram.FAILED or self.device.type != "cuda":
                 break
