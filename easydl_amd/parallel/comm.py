@@ -127,8 +127,12 @@ class Communicator:
                 if xgmi_factory is None:
                     from easydl_amd.parallel.xgmi import XgmiComm as xgmi_factory
                 try:
+                    # the engine's bounded waits: a peer that never arrives (or a mapping that does not
+                    # work between two GPUs) ends a collective after this long, not after the data
+                    # plane's full timeout -- the probe then keeps RCCL
+                    eng_timeout = min(timeout_s, float(os.environ.get("EDL_XGMI_TIMEOUT_S", 30)))
                     self.xgmi = xgmi_factory(dist.PrefixStore("xgmi", base), "ws", rank, world_size, self.device,
-                                             timeout_s=timeout_s)
+                                             timeout_s=eng_timeout)
                     self.xgmi_mode = data_backend
                 except Exception as e:  # noqa: BLE001
                     if data_backend == "xgmi":
