@@ -1086,14 +1086,26 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv64_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
     const bf16_t* __restrict__ dout, const float* __restrict__ lse, const float* __restrict__ delta,
     bf16_t* __restrict__ dk, bf16_t* __restrict__ dv, float* __restrict__ ws, int S, int H, int KV, int gsplit,
-    float scale_log2, float scale, int64_t dkvs, int64_t kvs) {
+    float scale_log2, float scale, int64_t dkvs, int64_t kvs, int xcd) {
   constexpr int QT = 64;   // queries per staged tile
   constexpr int KW = 64;   // keys per wave
   constexpr int KB = 4 * KW;
   constexpr int TILE = 64 * 2 * D, STAGE = 2 * TILE;   // one 64-row Q (or dO, or V) tile; Q + dO
   // [Q|dO] x 2 stages (64 KiB at D 128), softmax row terms (1 KiB), this block's V rows per wave (4 tiles)
   __shared__ __attribute__((aligned(16))) char smem[2 * STAGE + 2 * 512 + 4 * TILE];
-  const int hk = blockIdx.y / gsplit, gs = blockIdx.y % gsplit, b = blockIdx.z;
+  int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+  if (xcd) {
+    // linear block L is dispatched to XCD L % 8: renumber so that each XCD runs whole (kv head,
+    // batch) groups -- the workgroups that re-read one group's Q and dO then share an L2
+    const int nx = gridDim.x, ny = gridDim.y;
+    const int n = nx * ny * gridDim.z;
+    const int L = bx + nx * (by + ny * bz);
+    const int M = (L % 8) * (n / 8) + L / 8;
+    bx = M % nx;
+    by = (M / nx) % ny;
+    bz = M / (nx * ny);
+  }
+  const int hk = by / gsplit, gs = by % gsplit, b = bz;
   const int lane = threadIdx.x & 63, h = lane >> 5, l31 = lane & 31;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // provably wave-uniform
   const int heads = (H / KV) / gsplit, hq0 = hk * (H / KV) + gs * heads;
@@ -1101,7 +1113,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv64_kernel(
   const int nkb = (S + KB - 1) / KB, nqt = (S + QT - 1) / QT;
   const int64_t nBHS = (int64_t)gridDim.z * H * S;  // delta = [delta | -lse*log2e]
   const DmaPlan<QT, 4, D> plan(qs, w, lane);
-  const int blocks[2] = {(int)blockIdx.x, nkb - 1 - (int)blockIdx.x};
+  const int blocks[2] = {bx, nkb - 1 - bx};
   const int nblocks = CAUSAL && blocks[1] != blocks[0] ? 2 : 1;
 #pragma unroll 1
   for (int bi = 0; bi < nblocks; ++bi) {
@@ -1413,14 +1425,19 @@ static int attn_bwd_impl(const void* q, const void* k, const void* v, const void
   const int keys_per_wave = D == 128 ? dkdv_keys_per_wave() : (force64 ? 64 : 32);
   dim3 gkv64;
   const int gsplit = dkdv64_plan(B, S, H, KV, causal, &gkv64);
+  static const int dkdv_xcd = [] {
+    const char* e = getenv("EDL_ATTN_DKDV_XCD");
+    return e ? atoi(e) : 0;
+  }();
+  const int xcd64 = dkdv_xcd && (gkv64.x * gkv64.y * gkv64.z) % 8 == 0 ? 1 : 0;
   const bf16_t *bq = (const bf16_t*)q, *bk = (const bf16_t*)k, *bv = (const bf16_t*)v, *bdo = (const bf16_t*)dout;
   if (keys_per_wave == 64) {
     if (causal)
       attn_bwd_dkdv64_kernel<true, D><<<gkv64, 256, 0, s>>>(bq, bk, bv, bdo, lse, delta, (bf16_t*)dk, (bf16_t*)dv,
-                                                            ws, S, H, KV, gsplit, sl2, scale, dkvs, kvs);
+                                                            ws, S, H, KV, gsplit, sl2, scale, dkvs, kvs, xcd64);
     else
       attn_bwd_dkdv64_kernel<false, D><<<gkv64, 256, 0, s>>>(bq, bk, bv, bdo, lse, delta, (bf16_t*)dk, (bf16_t*)dv,
-                                                             ws, S, H, KV, gsplit, sl2, scale, dkvs, kvs);
+                                                             ws, S, H, KV, gsplit, sl2, scale, dkvs, kvs, xcd64);
     if (gsplit > 1) {
       EDL_LAUNCH_CHECK();
       const int64_t rows = (int64_t)B * S * KV;
