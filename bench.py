@@ -163,6 +163,7 @@ def parent(args) -> int:
             ttr.update({
                 "time_to_regain_s": d.get("time_to_regain_s"), "steps_lost": d.get("steps_lost"),
                 "restored_from": d.get("restored_from"), "resumed_mid_step": d.get("resumed_mid_step"),
+                "grad_shadow": d.get("grad_shadow"),
                 "fault_step": (d.get("fault") or {}).get("step"),
                 "fault_spec": (d.get("fault") or {}).get("spec"),
                 "replacement_from_standby": d.get("replacement_from_standby"),

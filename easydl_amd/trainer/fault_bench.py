@@ -137,6 +137,8 @@ def main(args) -> int:
         "hbm_resume_refused": any(e["kind"] == "hbm_resume_refused" for e in ev),
         "resumed_mid_step": next(({k: e.get(k) for k in ("step", "micro_batches_done", "of")}
                                   for e in ev if e["kind"] == "resumed_mid_step"), None),
+        "grad_shadow": next(({k: e.get(k) for k in ("on", "where", "gb", "free_gb", "replacement_need_gb")}
+                             for e in ev if e["kind"] == "grad_shadow"), None),
         "final_states": [{k: e.get(k) for k in ("proc", "step", "world", "rank", "crc")}
                          for e in ev if e["kind"] == "final_state"],
         "worlds_seen": sorted({w for w in worlds if w}), "run_dir": run_dir,
