@@ -799,6 +799,11 @@ class ElasticTrainer:
         from easydl_amd.utils import vram
         if self._rehomed or not vram.adopted_any() or self.flat is None or self.opt is None:
             return
+        if self.comm is None or self.comm.world_size > 1:
+            # only one rank moves its buffers, and re-registering the moved gradients with the xGMI
+            # engine is collective (a world-8 drill hung there); an HBM resume -- what the re-published
+            # state is for -- happens at world 1 only, so the move waits for a world of one
+            return
         ck = self.checkpoint
         if ck is not None and (getattr(ck, "_marks_check", None) is not None or getattr(ck, "_verify", None) is not None
                                or getattr(ck, "_deferred", None)):
@@ -862,7 +867,7 @@ class ElasticTrainer:
             self._publish_vram()
 
     def _move_state(self, pick, can_continue=lambda: True) -> int:
-        """Move the state buffers ``pick(tensor)`` selects to fresh allocations of this process
+        """(World 1.) Move the state buffers ``pick(tensor)`` selects to fresh allocations of this process
         (FlatParams.rehome, optim.rehome_state, FlatBuffers.rehome).  Allocated from a private
         pool: every buffer gets a segment of its own, never a block of a cached (possibly
         > 2 GiB) segment, which fails to export."""
@@ -880,8 +885,6 @@ class ElasticTrainer:
                 n += self.bufs.rehome(pick, can_continue)
         if self.ddp is not None:
             self.ddp.set_bucket_mb(self.ddp.bucket_mb)      # bucket views of the new gradient buffers
-            if self.dp_comm is not None and self.dp_comm.world_size > 1:
-                self.ddp.set_comm(self.dp_comm)             # the engine maps the new buffers
         return n
 
     def _state_pool(self):

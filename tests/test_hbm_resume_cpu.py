@@ -313,3 +313,24 @@ def test_mid_step_resume_from_the_gradient_shadow_is_bit_exact(tmp_path, monkeyp
         ck.close()
         unlink_job_segments(JOB)
         vram.adopt({})
+
+
+def test_no_rehome_while_other_ranks_train(tmp_path):
+    """Re-homing is one rank's move, and re-registering its gradient buffers with the xGMI engine
+    would be collective: a replacement in a world of several ranks keeps the adopted buffers (a
+    world-8 drill hung there).  The move happens once the world is one rank."""
+    from types import SimpleNamespace
+    _, exported = _died_worker(tmp_path)
+    vram.adopt(exported, pid=_dead_pid())
+    try:
+        b = _mk(tmp_path, 5, None, sub="b")
+        assert vram.adopted_any()
+        b.comm = SimpleNamespace(world_size=8)
+        b._maybe_rehome()
+        assert vram.adopted_any() and not b._rehomed
+        assert "rehomed" not in [r["kind"] for r in b.events.records]
+        b.comm = SimpleNamespace(world_size=1)
+        b._maybe_rehome()
+        assert b._rehomed and not vram.adopted_any()
+    finally:
+        vram.adopt({})
