@@ -26,6 +26,7 @@ import torch.nn.functional as F
 import torch.utils.checkpoint as ckpt
 
 from easydl_amd.ops import fused, norms
+from easydl_amd.parallel.flat import await_update
 
 
 @dataclass
@@ -185,6 +186,7 @@ class Llama(nn.Module):
     def __init__(self, cfg: LlamaConfig, device=None, dtype=torch.bfloat16):
         super().__init__()
         self.cfg = cfg
+        self._edl_awaits_own = True   # hidden()/forward() await their direct parameters' updates
         d = cfg.dim
         self.embed = _param((cfg.vocab_size, d), cfg.init_std, device, dtype)
         self.layers = nn.ModuleList([LlamaBlock(cfg, device, dtype) for _ in range(cfg.n_layers)])
@@ -202,6 +204,7 @@ class Llama(nn.Module):
     def hidden(self, ids):
         B, S = ids.shape
         cos, sin = self.rope(S, ids.device)
+        await_update(self.embed)      # (its own parameters: see install_update_waits)
         x = fused.embedding(ids.reshape(-1), self.embed)
         resid, delta = x, None
         for layer in self.layers:
@@ -209,12 +212,14 @@ class Llama(nn.Module):
                 resid, delta = ckpt.checkpoint(layer, resid, delta, B, S, cos, sin, use_reentrant=False)
             else:
                 resid, delta = layer(resid, delta, B, S, cos, sin)
+        await_update(self.norm)
         n, _ = norms.add_rmsnorm(delta, resid, self.norm, self.cfg.norm_eps)
         return n
 
     def forward(self, ids, labels=None):
         n = self.hidden(ids)
         w = self.embed if self.lm_head is None else self.lm_head
+        await_update(w)
         logits = fused.linear(n, w)
         if labels is None:
             return logits.view(*ids.shape, -1)

@@ -24,9 +24,10 @@ def is_flat(p: torch.Tensor) -> bool:
 
 
 def await_shadow(p: torch.Tensor) -> None:
-    """The caller's stream is about to write ``p``'s gradient: order it after the pending
-    device -> host copy of p's gradient group into the host gradient shadow, if any
-    (utils/gshadow.py; the copy overlaps the next micro-batch until its first write there)."""
+    """The caller's stream is about to write ``p``'s gradient: order it after whatever still
+    reads p's gradient group on another stream -- the device -> host copy into the host gradient
+    shadow (utils/gshadow.py), or the optimizer update overlapping the next step's forward
+    (ElasticTrainer._opt_overlap)."""
     ev = getattr(p, "_edl_wait", None)
     if ev is not None:
         p._edl_wait = None

@@ -108,18 +108,28 @@ class FlatAdamW:
         self.step_count = 0
         self.moment_origin = 0
 
+    supports_group_done = True
+
     @torch.no_grad()
-    def step(self, pre_scale: float = 1.0) -> torch.Tensor:
-        """Apply one update; ``pre_scale`` multiplies the (summed) gradients, e.g. 1/world."""
+    def step(self, pre_scale: float = 1.0, group_done=None) -> torch.Tensor:
+        """Apply one update; ``pre_scale`` multiplies the (summed) gradients, e.g. 1/world.
+        ``group_done(i)``: called after group i's update is enqueued; the groups then go last
+        to first -- the order the next forward reads them (FlatParams lays parameters out in
+        reverse registration order), so it can start on the first groups while the rest update
+        (ElasticTrainer._opt_overlap)."""
         grads = [g.grad for g in self.flat.groups]
         stats = grad_clip_scale(grads, self.max_grad_norm, pre_scale, self.norm_weights, self.norm_reduce)
         self.step_count += 1
         lr = self.schedule(self.step_count) if self.schedule else self.lr
-        for g, st in zip(self.flat.groups, self.state):
+        order = range(len(self.state) - 1, -1, -1) if group_done is not None else range(len(self.state))
+        for i in order:
+            g, st = self.flat.groups[i], self.state[i]
             p16 = g.data if g.data.dtype != torch.float32 else None
             adamw_flat_(p16, st["master"], st["m"], st["v"], g.grad, lr=lr, beta1=self.beta1, beta2=self.beta2,
                         eps=self.eps, weight_decay=g.weight_decay, step=self.step_count - self.moment_origin,
                         dscale=stats)
+            if group_done is not None:
+                group_done(i)
         self.last_stats = stats
         return stats
 

@@ -87,6 +87,38 @@ def _split_by_bytes(plist, elem_bytes: int, max_bytes: int) -> list[list]:
     return parts
 
 
+def await_update(p: torch.Tensor) -> None:
+    """The caller's stream is about to read parameter ``p``: order it after the pending update of
+    p's group on the optimizer stream, if any (ElasticTrainer._opt_overlap)."""
+    ev = getattr(p, "_edl_fwd_wait", None)
+    if ev is not None:
+        p._edl_fwd_wait = None
+        torch.cuda.current_stream(p.device).wait_event(ev)
+
+
+def install_update_waits(model: torch.nn.Module) -> int:
+    """Forward pre-hooks that make each module wait for the updates of the parameters it reads
+    (await_update): every submodule waits for its whole subtree's parameters -- the first hook to
+    run consumes the waits -- and the root for its own direct parameters, unless the model
+    awaits those itself where it reads them (``model._edl_awaits_own = True``; Llama's embedding
+    at the start and its head at the end).  Returns the number of hooks."""
+    n = 0
+    for name, mod in model.named_modules():
+        root = name == ""
+        if root and getattr(model, "_edl_awaits_own", False):
+            continue
+        params = list(mod.parameters(recurse=not root))
+        if not params:
+            continue
+
+        def hook(_m, _inp, params=params):
+            for p in params:
+                await_update(p)
+        mod.register_forward_pre_hook(hook)
+        n += 1
+    return n
+
+
 def _pre_accumulate_hook(ref, key):
     def hook(g):
         me = ref()
@@ -277,10 +309,13 @@ class FlatParams:
             # ResNet-50 / Llama no longer memset their whole gradient buffer every step
             if len(self._autograd_slots) * 4 > sum(len(g.slots) for g in self.groups):
                 for g in self.groups:
+                    for s in g.slots:
+                        gradsink.await_shadow(s.param)   # (an optimizer still reading them)
                     g.grad.zero_()
             else:
                 for key in self._autograd_slots:
                     g, s = self._slot_of[key]
+                    gradsink.await_shadow(s.param)
                     g.grad[s.offset:s.offset + s.numel].zero_()
             self.saw_autograd = False
             self._autograd_slots = set()

@@ -155,6 +155,8 @@ class ElasticTrainer:
         self._shadow_pending = False
         self._shadow_resume = None   # {"step", "mb", "host"}: resume that step at that micro-batch
         self._hshadow = None         # host gradient shadow (utils/gshadow.py), when HBM has no room
+        self._opt_stream = None      # optimizer update overlapping the next forward (_opt_overlap)
+        self._opt_overlap_off = False
         self._act_need = 0
 
     def request_stop(self) -> None:
@@ -327,6 +329,7 @@ class ElasticTrainer:
 
     def _enter_epoch(self):
         """Join the next live epoch; retries when the epoch breaks while it is being built."""
+        self.wait_update()      # the state may be sent to a joiner, snapshotted or restored next
         self._sync_next = True
         while True:
             t0 = time.time()
@@ -823,6 +826,7 @@ class ElasticTrainer:
         if self.device.type == "cuda" and sizes and self._hbm_avail() < 2 * max(sizes):
             return
         t0 = time.perf_counter()
+        self.wait_update()
         if ck is not None:
             ck.wait()           # no snapshot copy may read a buffer while it moves
         if self.device.type == "cuda":
@@ -1161,6 +1165,48 @@ class ElasticTrainer:
         return self.device.type == "cuda" and os.path.exists(
             "/dev/shm" + seg_name(self.ctx.job, f"{self.ctx.role}{self.ctx.index}"))
 
+    def _opt_overlap(self):
+        """The optimizer stream when the update may overlap the next step's forward, else None.
+
+        The update of 8B parameters is ~42 ms a step of memory-bound kernels (AdamW reads and
+        writes 30 B per parameter) that the compute-bound forward GEMMs leave bandwidth for.  So
+        the update runs on a side stream, group by group in the order the next forward reads the
+        groups.  Every module waits only for its own parameters' group before its forward
+        (FlatParams install_update_waits; Llama awaits its embedding and head itself), and every
+        gradient write waits for the update that still reads that gradient (gradsink
+        await_shadow).  Off for models with module buffers (BatchNorm statistics are broadcast
+        after the update), tensor parallelism, optimizers without per-group callbacks, and with
+        ``EDL_OPT_OVERLAP=0``.  An ``on_step`` callback runs while the update may still be in
+        flight: one that reads parameters directly calls ``wait_update()`` first."""
+        if self._opt_stream is not None:
+            return self._opt_stream
+        if self._opt_overlap_off:
+            return None
+        if (self.device.type != "cuda" or self.tp > 1 or os.environ.get("EDL_OPT_OVERLAP", "0") == "0"
+                or not getattr(self.opt, "supports_group_done", False)
+                or (self.bufs is not None and self.bufs.tensors)):
+            self._opt_overlap_off = True
+            return None
+        from easydl_amd.ops import fused
+        from easydl_amd.parallel.flat import install_update_waits
+        install_update_waits(self.model)
+        fused._WT_BATCH = False     # the batched W^T refresh would read every weight at the first use
+        self._opt_stream = torch.cuda.Stream(device=self.device)
+        self._opt_stream.wait_stream(torch.cuda.current_stream(self.device))
+        return self._opt_stream
+
+    def _opt_group_done(self, i: int) -> None:
+        ev = torch.cuda.Event()
+        ev.record(self._opt_stream)
+        for sl in self.flat.groups[i].slots:
+            sl.param._edl_fwd_wait = ev      # its next reader waits for this group's update
+            sl.param._edl_wait = ev          # its next gradient write waits for the update's read
+
+    def wait_update(self) -> None:
+        """Order the current stream after the last optimizer update (see _opt_overlap)."""
+        if self._opt_stream is not None:
+            torch.cuda.current_stream(self.device).wait_stream(self._opt_stream)
+
     def _shadow_wanted(self) -> bool:
         """Gradient shadows pay off where a replacement resumes from this process's HBM: one rank
         (HBM resume needs world 1), VRAM hand-over on, several micro-batches per step."""
@@ -1332,23 +1378,29 @@ class ElasticTrainer:
                     apply, latest = ok, 0
                 t_commit = time.perf_counter()
                 if apply:
-                    if self.checkpoint is not None:
-                        self.checkpoint.fence()  # never update params under an in-flight snapshot
-                        hv = self.checkpoint.stats.pop("handover_verified_s", None)
-                        if hv is not None:
-                            self.events.emit("handover_verified", step=self.step, s=hv)
-                            self._open_marks()
-                    t_fence = time.perf_counter()
-                    if self._marks is not None:
-                        self._marks.begin(self.step + 1, torch.cuda.current_stream(self.device)
-                                          if self.device.type == "cuda" else None)
-                    with trace.range("optimizer"), self.kmix.phase("memory"):
-                        self.opt.step(pre_scale=1.0)
-                    self.fault.maybe_inject("in_update", self.step, trainer=self)
-                    self._sync_buffers()
-                    if self._marks is not None:
-                        self._marks.done(self.step + 1, torch.cuda.current_stream(self.device)
-                                         if self.device.type == "cuda" else None)
+                    ovl = self._opt_overlap()
+                    upd = _null() if ovl is None else torch.cuda.stream(ovl)
+                    with upd:   # (overlap: the update runs on its own stream under the next forward)
+                        if self.checkpoint is not None:
+                            self.checkpoint.fence()  # never update params under an in-flight snapshot
+                            hv = self.checkpoint.stats.pop("handover_verified_s", None)
+                            if hv is not None:
+                                self.events.emit("handover_verified", step=self.step, s=hv)
+                                self._open_marks()
+                        t_fence = time.perf_counter()
+                        if self._marks is not None:
+                            self._marks.begin(self.step + 1, torch.cuda.current_stream(self.device)
+                                              if self.device.type == "cuda" else None)
+                        with trace.range("optimizer"), self.kmix.phase("memory"):
+                            if ovl is None:
+                                self.opt.step(pre_scale=1.0)
+                            else:
+                                self.opt.step(pre_scale=1.0, group_done=self._opt_group_done)
+                        self.fault.maybe_inject("in_update", self.step, trainer=self)
+                        self._sync_buffers()
+                        if self._marks is not None:
+                            self._marks.done(self.step + 1, torch.cuda.current_stream(self.device)
+                                             if self.device.type == "cuda" else None)
                     if self._phases and ok:
                         # host-side split of one step (EDL_STEP_PHASES=1): enqueue of the micro-batches,
                         # wait for the GPU (compute + all-reduce), commit round, snapshot fence, optimizer
@@ -1369,7 +1421,8 @@ class ElasticTrainer:
                                         tokens=self.global_batch * self.tokens_per_sample, world=self.comm.world_size,
                                         loss=None, extra=self._metrics_extra)
                     if self.checkpoint is not None:
-                        self.checkpoint.on_step(self)
+                        with upd:       # a snapshot copies the state after the update
+                            self.checkpoint.on_step(self)
                     if latest > self.comm.epoch:
                         # the agreed decision already names a newer epoch (a rejoin, a scale-up):
                         # a probe of THIS world would be thrown away, and would hold the rejoin
@@ -1399,6 +1452,8 @@ class ElasticTrainer:
                 self.rdzv.kv.set("train/done", str(self.step))  # releases spare waiting workers
         finally:
             self._stop.set()
+            if self.device.type == "cuda":
+                self.wait_update()      # the caller reads the trained state next
         return self
 
     def _metrics_extra(self) -> dict:
