@@ -1182,7 +1182,7 @@ class ElasticTrainer:
             return self._opt_stream
         if self._opt_overlap_off:
             return None
-        if (self.device.type != "cuda" or self.tp > 1 or os.environ.get("EDL_OPT_OVERLAP", "0") == "0"
+        if (self.device.type != "cuda" or self.tp > 1 or os.environ.get("EDL_OPT_OVERLAP", "1") == "0"
                 or not getattr(self.opt, "supports_group_done", False)
                 or (self.bufs is not None and self.bufs.tensors)):
             self._opt_overlap_off = True
