@@ -263,6 +263,13 @@ __global__ __launch_bounds__(256) void clip_finalize_kernel(const float* __restr
 }
 
 inline int grid_for(int64_t n4, int cap = 2048) {
+  // EDL_ADAMW_GRID: fewer workgroups for the grid-stride update kernels, e.g. while they overlap
+  // the next forward on another stream (read once per process)
+  static const int env_cap = [] {
+    const char* e = getenv("EDL_ADAMW_GRID");
+    return e && atoi(e) > 0 ? atoi(e) : 0;
+  }();
+  if (env_cap > 0 && env_cap < cap) cap = env_cap;
   int64_t b = (n4 + 255) / 256;
   if (b < 1) b = 1;
   return (int)(b < cap ? b : cap);
