@@ -1021,6 +1021,15 @@ def _load_shard(read, table, state, dev, expect: int, what: str, seg=None, slot=
     before the first optimizer update -- are copied by a background thread on a side stream
     while training resumes; their checksum half is folded in at ``deferred`` completion
     (CheckpointManager.complete_restore, before that update)."""
+    for name, dt, numel, lo, hi, off in table:
+        t = state.get(name)
+        if t is None:
+            raise RuntimeError(f"{what}: snapshot holds {name}, which this process's state does not have")
+        if _DT[t.dtype] != dt or t.numel() != numel:
+            # the bytes are copied raw: another dtype (e.g. bf16 vs fp32 Adam moments) or size
+            # would load garbage under a matching checksum
+            raise RuntimeError(f"{what}: {name} is {dt}[{numel}] in the snapshot but {_DT[t.dtype]}[{t.numel()}] "
+                               "here (moment dtype / model mismatch); refusing to restore")
     acc = torch.zeros(1, dtype=torch.int64, device=dev) if dev.type == "cuda" else None
     if acc is not None and seg is not None:
         now, items_later = [], []

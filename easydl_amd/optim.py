@@ -97,6 +97,20 @@ class FlatAdamW:
         return self.schedule(self.step_count + 1) if self.schedule else self.lr
 
     @torch.no_grad()
+    def set_moment_dtype(self, dtype: torch.dtype) -> bool:
+        """Switch the moment buffers to ``dtype`` (the job's agreed choice, ElasticTrainer
+        _agree_moment_dtype); values are converted.  Returns True if anything changed."""
+        if dtype not in (torch.float32, torch.bfloat16):
+            raise ValueError(f"moment_dtype must be float32 or bfloat16, got {dtype}")
+        if dtype == self.moment_dtype:
+            return False
+        for st in self.state:
+            st["m"] = st["m"].to(dtype)
+            st["v"] = st["v"].to(dtype)
+        self.moment_dtype = dtype
+        return True
+
+    @torch.no_grad()
     def reset_state(self) -> None:
         """Fresh-start optimizer state for the current weights: master = weights, zero moments
         (after :meth:`FlatParams.reinit_adopted`)."""

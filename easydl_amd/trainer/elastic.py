@@ -185,6 +185,7 @@ class ElasticTrainer:
         else:
             self.opt = FlatSGD(self.flat, lr=a["lr"], momentum=a["momentum"], weight_decay=a["weight_decay"],
                                max_grad_norm=a["max_grad_norm"], schedule=a["schedule"])
+        self._agree_moment_dtype()    # store known (TP: built at the first epoch): publish / adopt now
         if self.tp > 1:
             # grad norm over the whole model: replicated groups (norms) count once
             w = []
@@ -215,6 +216,14 @@ class ElasticTrainer:
         restarts them).  The state of a DP replica is sharded over the DP group."""
         if want != "auto":
             return torch.bfloat16 if want == "bf16" else torch.float32
+        from easydl_amd.utils import vram
+        inherited = vram.adopted_dtype("opt/", "/m")
+        if inherited is not None:
+            # a takeover keeps the dead worker's (job-agreed) choice: its moments are adopted as they are
+            return inherited
+        agreed = self._job_moment_dtype()
+        if agreed is not None:
+            return agreed
         ck = self.checkpoint
         if ck is None or not hasattr(ck, "host_budget_bytes"):
             return torch.float32
@@ -234,6 +243,31 @@ class ElasticTrainer:
                              budget_gb=round(budget / 2**30, 2), full_fp32_gb=round(full32 / 2**30, 3))
         return pick
 
+    _MOMENT_KEY = "job/moment_dtype"
+
+    def _job_moment_dtype(self) -> torch.dtype | None:
+        """The moment dtype this job already decided (job store), None before the first decision."""
+        kv = getattr(self, "kv", None)
+        if kv is None:
+            return None
+        v = kv.get_str(self._MOMENT_KEY)
+        return None if v is None else (torch.bfloat16 if v == "bf16" else torch.float32)
+
+    def _agree_moment_dtype(self) -> None:
+        """``moment_dtype="auto"`` is decided once per JOB, not per process: the first process to
+        reach the store publishes its pick (compare-and-set) and every later one -- a replacement
+        started while the dead worker's segments still fill /dev/shm, a rank on a busier node --
+        adopts it.  Otherwise a state transfer or snapshot restore would copy raw moment bytes
+        into buffers of another dtype (ckpt/manager.py _load_shard now refuses that loudly)."""
+        if (self._opt_args["moment_dtype"] != "auto" or getattr(self, "kv", None) is None
+                or not hasattr(self.opt, "set_moment_dtype")):
+            return
+        mine = "bf16" if self.opt.moment_dtype == torch.bfloat16 else "fp32"
+        got = self.kv.compare_set(self._MOMENT_KEY, "", mine) or mine
+        if got != mine:
+            self.opt.set_moment_dtype(torch.bfloat16 if got == "bf16" else torch.float32)
+            self.events.emit("moment_dtype", dtype=got, adopted_from_job=True, local_pick=mine)
+
     def _connect(self):
         if self.ctx.standalone:
             self.kv = None
@@ -244,6 +278,8 @@ class ElasticTrainer:
             is_server = self.ctx.embedded_master and self.ctx.index == 0 and not agent
             self._store = make_tcp_store(self.ctx.master_addr, self.ctx.master_port, is_server)
         self.kv = KV(self._store, f"edl/{self.ctx.job}")
+        if self.opt is not None:
+            self._agree_moment_dtype()     # (TP models are built later, with the store already known)
         if self.ctx.embedded_master and self.ctx.index == 0:
             cfg = self.rdzv_config or RendezvousConfig(min_nodes=self.ctx.static_world,
                                                        max_nodes=self.ctx.static_world, granule=self.tp)
@@ -908,6 +944,9 @@ class ElasticTrainer:
         (profiles/r05_ttr_headline.md).  Instead, while memory is short, each micro-batch is
         split into smaller ones: the same samples, the same loss weights, the same gradient sum
         (only the order of the bf16 additions differs), at roughly half the activation memory.
+        Models with dropout are the exception: the pieces of micro-batch i are seeded once and draw
+        their masks one after another, so a split step is NOT bit-exact with the unsplit one there
+        (Llama, the only model this path serves, has no dropout).
         When not even one sample per micro-batch fits, a model with a ``cfg.recompute`` switch
         (Llama) recomputes its layers' activations in the backward instead.
         Checked again before every step; full micro-batches return once the memory is back."""
@@ -1195,6 +1234,15 @@ class ElasticTrainer:
         self._opt_stream.wait_stream(torch.cuda.current_stream(self.device))
         return self._opt_stream
 
+    def _order_update_after_step(self, ovl) -> None:
+        """The update of step k reads step k's gradients and rewrites the weights its backward
+        read for dgrad: it starts after everything the compute stream holds at the commit (every
+        micro-batch's backward, the fused ops' side-stream weight gradients, which ddp.finish
+        joined into it, and finalize_untouched).  Every step, not once at stream creation: at
+        world 1 the host does not drain the step (_sync_point), so without this edge the update
+        could run while the backward still writes the gradients it reads."""
+        ovl.wait_stream(torch.cuda.current_stream(self.device))
+
     def _opt_group_done(self, i: int) -> None:
         ev = torch.cuda.Event()
         ev.record(self._opt_stream)
@@ -1379,6 +1427,8 @@ class ElasticTrainer:
                 t_commit = time.perf_counter()
                 if apply:
                     ovl = self._opt_overlap()
+                    if ovl is not None:
+                        self._order_update_after_step(ovl)
                     upd = _null() if ovl is None else torch.cuda.stream(ovl)
                     with upd:   # (overlap: the update runs on its own stream under the next forward)
                         if self.checkpoint is not None:

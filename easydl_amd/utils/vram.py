@@ -260,6 +260,15 @@ def take(name: str, numel: int, dtype: torch.dtype, device, keep: bool = False) 
     return t
 
 
+def adopted_dtype(prefix: str, suffix: str) -> torch.dtype | None:
+    """dtype of an adopted tensor named ``prefix...suffix`` (``opt/``, ``/m``: the dead worker's
+    Adam moment dtype, which its replacement must keep), None if there is none."""
+    for name, t in _ADOPTED.items():
+        if name.startswith(prefix) and name.endswith(suffix):
+            return t.dtype
+    return None
+
+
 def pending(name: str) -> bool:
     """An adopted tensor of this name is waiting to be taken."""
     return name in _ADOPTED

@@ -3,9 +3,16 @@ the same training as the serialized update, bit for bit.
 
 The update runs on its own stream, group by group in the order the next forward reads them;
 each module waits for its own parameters' update, each gradient write for the update that still
-reads that gradient, and the transposed-weight cache refreshes each weight at its own first use.
-A missing wait would let the forward read half-updated weights (or a backward overwrite gradients
-the update has not read yet) and the two runs would drift apart."""
+reads that gradient, the transposed-weight cache refreshes each weight at its own first use, and
+the update itself waits for the step's backward (ElasticTrainer._order_update_after_step).
+A missing wait would let the forward read half-updated weights (or the update read gradients
+the backward has not written yet) and the two runs would drift apart.
+
+llama-tiny is host-bound: left alone, each backward finishes on the GPU before the host queues
+the update, and no missing edge could show.  So every micro-batch starts with a GPU spin
+(``torch.cuda._sleep``) that keeps the compute stream well behind the host, and the losses stay
+on the GPU until the run ends (no per-step ``float(loss)`` sync).  The negative control removes
+the per-step update->backward edge and must see the runs differ: the test has teeth."""
 import pytest
 import torch
 
@@ -16,6 +23,7 @@ from easydl_amd.trainer.elastic import ElasticTrainer
 
 pytestmark = pytest.mark.gpu
 CFG = get_config("llama-tiny")
+LAG_CYCLES = 20_000_000      # ~10 ms of spinning per micro-batch: the GPU lags the host by steps
 
 
 def _run(tmp, sub, cuda, overlap: bool, monkeypatch):
@@ -26,12 +34,16 @@ def _run(tmp, sub, cuda, overlap: bool, monkeypatch):
     tr = ElasticTrainer(lambda d: Llama(CFG, device=d), global_batch=8, micro_batch=2, lr=1e-3, device=cuda,
                         ctx=ctx, seed=3)
     losses = []
-    tr.fit(lambda m, b: m(*b), SyntheticTokens(CFG.vocab_size, 256, num_samples=4096), num_steps=8,
-           on_step=lambda t, loss: losses.append(float(loss)))
+
+    def loss_fn(m, b):
+        torch.cuda._sleep(LAG_CYCLES)     # the compute stream falls behind the host here
+        return m(*b)
+    tr.fit(loss_fn, SyntheticTokens(CFG.vocab_size, 256, num_samples=4096), num_steps=8,
+           on_step=lambda t, loss: losses.append(loss.detach().clone()))
     torch.cuda.synchronize()
     state = {f"data.{g.name}": g.data.clone() for g in tr.flat.groups}
     state.update({k: v.clone() for k, v in tr.opt.state_tensors().items()})
-    return tr, losses, state
+    return tr, [float(x) for x in losses], state
 
 
 def test_overlapped_update_matches_the_serialized_one(cuda, tmp_path, monkeypatch):
@@ -42,3 +54,12 @@ def test_overlapped_update_matches_the_serialized_one(cuda, tmp_path, monkeypatc
     assert la == lb
     for k in sa:
         assert torch.equal(sa[k], sb[k]), k
+
+
+def test_update_without_the_backward_edge_diverges(cuda, tmp_path, monkeypatch):
+    """Negative control: the lagging GPU really exposes a missing update->backward edge."""
+    _, la, sa = _run(tmp_path, "serial", cuda, False, monkeypatch)
+    monkeypatch.setattr(ElasticTrainer, "_order_update_after_step", lambda self, ovl: None)
+    _, lb, sb = _run(tmp_path, "racy", cuda, True, monkeypatch)
+    same = la == lb and all(torch.equal(sa[k], sb[k]) for k in sa)
+    assert not same, "a racy update matched the serialized one: the lag no longer exposes the race"
