@@ -43,7 +43,9 @@ class LlamaConfig:
     rope_scaling: dict | None = None
     tie_embeddings: bool = False
     init_std: float = 0.02
-    recompute: bool = False
+    # True: every layer's activations are recomputed in the backward; an int r: the first r layers
+    # only (a takeover short of HBM recomputes just enough of them, trainer/recovery.py)
+    recompute: bool | int = False
 
     @property
     def head_dim(self) -> int:
@@ -207,8 +209,10 @@ class Llama(nn.Module):
         await_update(self.embed)      # (its own parameters: see install_update_waits)
         x = fused.embedding(ids.reshape(-1), self.embed)
         resid, delta = x, None
-        for layer in self.layers:
-            if self.cfg.recompute and self.training:
+        rc = self.cfg.recompute
+        n_rc = len(self.layers) if rc is True else int(rc or 0)
+        for i, layer in enumerate(self.layers):
+            if i < n_rc and self.training:
                 resid, delta = ckpt.checkpoint(layer, resid, delta, B, S, cos, sin, use_reentrant=False)
             else:
                 resid, delta = layer(resid, delta, B, S, cos, sin)

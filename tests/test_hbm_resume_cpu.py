@@ -179,7 +179,9 @@ def test_unused_adopted_buffers_are_released(tmp_path):
 def test_memory_limited_recovery_splits_micro_batches_with_the_same_update(tmp_path):
     """A replacement short of HBM (the dead worker's activations not reclaimed yet) runs each
     micro-batch as smaller ones: same samples, same weights -> the same update (up to the
-    order of the additions), then goes back to full micro-batches once memory is back."""
+    order of the additions).  The plan is re-made before every micro-batch: the moment the driver
+    has reclaimed the memory -- here between the first and second micro-batch of the first step --
+    the rest of the step runs full micro-batches again."""
     from easydl_amd.trainer.data import SyntheticTokens
 
     class _Tok(torch.nn.Module):
@@ -201,23 +203,26 @@ def test_memory_limited_recovery_splits_micro_batches_with_the_same_update(tmp_p
 
     ref = mk("ref").fit(lambda m, b: m(*b), data, num_steps=2)
     sp = mk("split")
-    avail = {"v": 0}
+    avail = {"v": 600}                  # 1000 B needed per micro-batch of 4: two pieces of 2 fit
     sp._hbm_avail = lambda: avail["v"]
     sp._act_need = 1000
-    sp._mb_split = 2
+    sp._mb_limited = True
     sp._memory_plan = lambda: None      # (on a GPU takeover: free HBM < the published need)
-    seen = []
-    orig = sp._split_micro_batches
+    orig = sp._replan_memory
+    sizes = []
 
-    def spy(mbs):
-        out = orig(mbs)
-        seen.append([len(x) for _, x in out])
-        avail["v"] = 10_000          # the driver has reclaimed the memory after the first step
-        return out
-    sp._split_micro_batches = spy
-    sp.fit(lambda m, b: m(*b), data, num_steps=2)
-    assert seen[0] == [2, 2, 2, 2] and seen[1] == [4, 4], seen
-    assert [r["kind"] for r in sp.events.records if r["kind"] == "memory_restored"] == ["memory_restored"]
+    def replan(mb):
+        orig(mb)
+        avail["v"] = 10_000             # the driver reclaims the memory during micro-batch 0
+    sp._replan_memory = replan
+
+    def loss_fn(m, b):
+        sizes.append(int(b[0].shape[0]))
+        return m(*b)
+    sp.fit(loss_fn, data, num_steps=2)
+    assert sizes == [2, 2, 4, 4, 4], sizes
+    kinds = [(r["kind"], r.get("mb")) for r in sp.events.records if r["kind"].startswith("memory_")]
+    assert kinds == [("memory_replanned", 0), ("memory_restored", 1)], kinds
     for a, b in zip(ref.flat.groups, sp.flat.groups):
         assert torch.allclose(a.data, b.data, atol=1e-6, rtol=1e-5)
 
