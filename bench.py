@@ -4,7 +4,8 @@
 Metric/config come from BASELINE.json (``tokens/sec ... Llama-3-8B elastic
 DDP 1->8 GPUs``).  One process per GPU; for N>1 the driver launches this file
 with ``torch.distributed.run`` and every rank reads RANK / LOCAL_RANK /
-WORLD_SIZE / MASTER_ADDR / MASTER_PORT from the environment.
+WORLD_SIZE / MASTER_ADDR / MASTER_PORT from the environment; the plain form
+``python bench.py --gpus N`` launches the N ranks itself (see below).
 
 The timed loop IS the framework's elastic training loop
 (:class:`easydl_amd.trainer.elastic.ElasticTrainer`): rank 0 embeds the
@@ -17,17 +18,23 @@ bracketed by barrier + synchronize; the elapsed time is the MAX over ranks;
 rank 0 prints one JSON line.
 
 Time-to-recover, the other half of the headline metric (BASELINE.json), is
-measured in the same run at N=1: this process then stays GPU-free and runs two
-fresh children one after the other -- the throughput measurement above
-(``--child``), then the no-survivor fault drill at the SAME configuration
-(full Llama-3-8B, seq 8192, 2 x 4 micro-batches, in-memory snapshots every 2
-steps, one hot standby; the only worker is SIGKILLed 40 % into a step once the
-standby is warm).  The drill's TTR, phases, steps lost and time to regain the
-pre-fault step go into ``time_to_recover_s`` / ``ttr`` of the one JSON line; a
-failed drill leaves ``time_to_recover_s: null`` with an ``error`` and never
-fails the throughput line.  ``--ttr off`` skips the drill.  Under torchrun
-(N>1) the ranks belong to the launcher, which tears the job down when one of
-them dies, so TTR comes from the local-operator drill (``--fault-inject``).
+measured by the plain command at any N (``python bench.py --gpus N``): this
+process stays GPU-free and starts the throughput run -- one ``--child`` at
+N = 1, N rank children at N > 1 (it sets RANK / LOCAL_RANK / WORLD_SIZE /
+MASTER_* itself, exactly as torchrun would; never an exec of itself) -- and
+then the fault drill at the SAME configuration (full Llama-3-8B, seq 8192,
+2 x 4 micro-batches, in-memory snapshots every 2 steps, one hot standby):
+worker N-1 is SIGKILLed 40 % into a step (counted from the GPU's start of the
+step) once the standby is warm.  N = 1: the standby resumes from the dead
+worker's HBM.  N > 1: the survivors shrink to N-1 and go on, the standby
+rejoins, world N again, every rank ends with identical parameters.  TTR,
+phases, the first recovered step's memory plan and duration, steps lost, time
+to regain the pre-fault step and (N > 1) to regrow to N ranks go into
+``time_to_recover_s`` / ``ttr`` of the one JSON line; a failed drill leaves
+``time_to_recover_s: null`` with an ``error`` and never fails the throughput
+line.  ``--ttr off`` skips the drill.  Under torchrun the launcher owns the
+ranks (it tears the job down when one dies): the throughput line is the same
+and ``ttr.error`` says TTR needs the plain form.
 """
 from __future__ import annotations
 
@@ -131,49 +138,146 @@ def _gpu_host() -> bool:
         return False
 
 
-def parent(args) -> int:
-    """N=1 headline: throughput child, then the time-to-recover drill child, one JSON line."""
+def _free_port() -> int:
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def _launch_ranks(args, n: int, timeout_s: float) -> tuple[int | None, str]:
+    """N > 1 from the plain command: this GPU-free process starts N rank processes of this file
+    itself, with the environment torchrun would give them (RANK / LOCAL_RANK / WORLD_SIZE /
+    LOCAL_WORLD_SIZE / MASTER_ADDR / MASTER_PORT; rank 0 hosts the job store).  Each is a child
+    process in its own session -- never an exec of this one.  A rank that fails ends the others.
+    Returns (rc or None on timeout, rank 0's stdout)."""
     me = os.path.abspath(__file__)
-    rc, out = _run_child([sys.executable, me, *sys.argv[1:], "--child"], timeout_s=3600)
-    res = _json_line(out)
-    if rc != 0 or res is None:
-        sys.stdout.write(out)
-        print(f"[bench] throughput child failed (rc={rc})", file=sys.stderr)
-        return rc if rc else 1
-    ttr = {"mode": "midstep", "hot_standby": 1, "ckpt_interval": 2}
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", ROLE_RANK=str(r), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        env.pop("TORCHELASTIC_USE_AGENT_STORE", None)
+        procs.append(subprocess.Popen([sys.executable, me, *sys.argv[1:], "--child"], env=env, text=True,
+                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL,
+                                      start_new_session=True))
+    out = []
+    reader = __import__("threading").Thread(target=lambda: out.append(procs[0].stdout.read()), daemon=True)
+    reader.start()
+    t_end = time.monotonic() + timeout_s
+    rc = 0
+    live = set(range(n))
+    while live and time.monotonic() < t_end:
+        for r in sorted(live):
+            c = procs[r].poll()
+            if c is None:
+                continue
+            live.discard(r)
+            if c != 0:
+                rc = c
+                print(f"[bench] rank {r} exited with {c}: stopping the other ranks", file=sys.stderr)
+                live.clear()
+                break
+        time.sleep(0.05)
+    if live or rc:
+        rc = None if live else rc
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    os.killpg(p.pid, signal.SIGKILL)
+                except OSError:
+                    pass
+    for p in procs:
+        p.wait()
+    reader.join(10)
+    return rc, "".join(out)
+
+
+def _drill(args, res: dict, n: int) -> dict:
+    """The time-to-recover drill at the headline configuration, after the throughput run.
+    N = 1: the only worker is SIGKILLed 40 % into a step once the hot standby is warm; the
+    standby resumes from the dead worker's HBM.  N > 1: worker N-1 is SIGKILLed the same way;
+    the N-1 survivors abort, shrink and go on; the hot standby takes the dead worker's place and
+    rejoins (world N again); every final rank must hold the same parameters."""
+    me = os.path.abspath(__file__)
+    ttr = {"mode": "midstep", "hot_standby": 1, "ckpt_interval": 2, "workers": n}
     t0 = time.perf_counter()
     try:
         from easydl_amd.ckpt.manager import unlink_job_segments
         unlink_job_segments("bench")
         env = dict(os.environ, EDL_FAULT_STEP_MS=str(res["ms_per_step"]))
-        drill = [sys.executable, me, "--fault-inject", "--gpus", "1", "--model", args.model, "--seq", str(args.seq),
-                 "--mbs", str(args.mbs), "--accum", str(args.accum), "--ckpt-interval", "2", "--standby", "1",
-                 "--fault-mode", "midstep", "--fault-step", "4", "--steps", "0", "--warmup", "0"]
+        if n > 1:
+            env.setdefault("EDL_BENCH_UNTIL_REGROWN", "1")    # end once the replacement is back in
+        for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+            env.pop(k, None)
+        drill = [sys.executable, me, "--fault-inject", "--gpus", str(n), "--model", args.model, "--seq",
+                 str(args.seq), "--mbs", str(args.mbs), "--accum", str(args.accum), "--ckpt-interval", "2",
+                 "--standby", "1", "--fault-mode", "midstep", "--fault-step", "4", "--steps", "0", "--warmup", "0"]
         if args.layers:
             drill += ["--layers", str(args.layers)]
-        drc, dout = _run_child(drill, timeout_s=args.ttr_timeout, env=env)
+        timeout = args.ttr_timeout if n == 1 else max(args.ttr_timeout, 480.0)
+        drc, dout = _run_child(drill, timeout_s=timeout, env=env)
         d = _json_line(dout)
         ttr["drill_wall_s"] = round(time.perf_counter() - t0, 1)
         if d is None or d.get("value") is None:
             ttr["error"] = ("drill timed out" if drc is None else f"drill rc={drc}") + \
                 ("" if d is None else f", no recovery in the timeline: {json.dumps(d.get('breakdown'))[:300]}")
-        else:
-            res["time_to_recover_s"] = d["value"]
-            b = d.get("breakdown") or {}
-            ttr.update({
-                "time_to_regain_s": d.get("time_to_regain_s"), "steps_lost": d.get("steps_lost"),
-                "restored_from": d.get("restored_from"), "resumed_mid_step": d.get("resumed_mid_step"),
-                "grad_shadow": d.get("grad_shadow"),
-                "fault_step": (d.get("fault") or {}).get("step"),
-                "fault_spec": (d.get("fault") or {}).get("spec"),
-                "replacement_from_standby": d.get("replacement_from_standby"),
-                "step_s_before_fault": d.get("step_s_before_fault"),
-                "phases": {k: b.get(k) for k in ("detect_s", "replacement_spawn_s", "replacement_joined_s",
-                                                 "comm_ready_s", "state_synced_s", "first_step_s")},
-                "config": d.get("config"), "model": d.get("model"), "operator_rc": d.get("operator_rc")})
+            return ttr
+        res["time_to_recover_s"] = d["value"]
+        b = d.get("breakdown") or {}
+        finals = d.get("final_states") or []
+        ttr.update({
+            "time_to_regain_s": d.get("time_to_regain_s"), "steps_lost": d.get("steps_lost"),
+            "time_to_regrow_s": d.get("time_to_regrow_s"), "worlds_seen": d.get("worlds_seen"),
+            "restored_from": d.get("restored_from"), "resumed_mid_step": d.get("resumed_mid_step"),
+            "grad_shadow": d.get("grad_shadow"),
+            "fault_step": (d.get("fault") or {}).get("step"),
+            "fault_spec": (d.get("fault") or {}).get("spec"),
+            "replacement_from_standby": d.get("replacement_from_standby"),
+            "step_s_before_fault": d.get("step_s_before_fault"),
+            "step_s_before_fault_clock": d.get("step_s_before_fault_clock"),
+            "first_step": d.get("first_step"),
+            "phases": {k: b.get(k) for k in ("detect_s", "abort_s", "epoch_formed_s", "replacement_spawn_s",
+                                             "replacement_joined_s", "comm_ready_s", "state_synced_s",
+                                             "first_step_s")},
+            "final_ranks": len(finals),
+            "final_states_equal": len({json.dumps(f.get("crc")) for f in finals}) == 1 if finals else None,
+            "final_worlds": sorted({f.get("world") for f in finals if f.get("world")}),
+            "timeline": d.get("timeline"),
+            "config": d.get("config"), "model": d.get("model"), "operator_rc": d.get("operator_rc")})
     except Exception as e:  # noqa: BLE001 - the drill never fails the throughput line
         ttr["error"] = f"{type(e).__name__}: {e}"[:300]
-    res["ttr"] = ttr
+    return ttr
+
+
+def parent(args) -> int:
+    """The plain command at any N: the throughput run (one child at N = 1, N rank children at
+    N > 1), then the time-to-recover drill child at the same configuration; one JSON line."""
+    n = max(1, args.gpus)
+    if n > 1 and _gpu_host():
+        from easydl_amd.brain.collectors import kfd_gpus
+        have = len(kfd_gpus())
+        if have < n:
+            print(f"[bench] --gpus {n} but this host has {have} GPU(s)", file=sys.stderr)
+            return 2
+    me = os.path.abspath(__file__)
+    if n == 1:
+        rc, out = _run_child([sys.executable, me, *sys.argv[1:], "--child"], timeout_s=3600)
+    else:
+        rc, out = _launch_ranks(args, n, timeout_s=3600)
+    res = _json_line(out)
+    if rc != 0 or res is None:
+        sys.stdout.write(out)
+        print(f"[bench] throughput run failed (rc={rc})", file=sys.stderr)
+        return rc if rc else 1
+    if n > 1:
+        res["launch"] = f"bench.py parent: {n} rank processes (RANK/LOCAL_RANK/WORLD_SIZE set by it)"
+    if args.ttr == "off":
+        res["ttr"] = {"skipped": "--ttr off"}
+    elif args.tp > 1:
+        res["ttr"] = {"error": "the time-to-recover drill runs the data-parallel headline only (--tp 1)"}
+    else:
+        res["ttr"] = _drill(args, res, n)
     print(json.dumps(res), flush=True)
     if args.out:
         with open(args.out, "w") as f:
@@ -183,8 +287,11 @@ def parent(args) -> int:
 
 def main():
     args = parse()
-    if (not args.child and not args.fault_inject and not args.scale_up and not args.share_gpu and args.ttr == "auto"
-            and os.environ.get("WORLD_SIZE", "1") == "1" and args.tp == 1 and _gpu_host()):
+    plain = not (args.child or args.fault_inject or args.scale_up or args.share_gpu)
+    if plain and "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return parent(args)          # N ranks launched from here, then the N-rank drill
+    if (plain and args.ttr == "auto" and os.environ.get("WORLD_SIZE", "1") == "1" and args.tp == 1
+            and _gpu_host()):
         return parent(args)
     if args.fault_inject:
         from easydl_amd.trainer import fault_bench
@@ -321,6 +428,11 @@ def main():
             "pinned": ckpt.pin, "staged_last": ckpt.stats.get("staged_last"),
             "mode": ckpt.mode, "host_budget_gb": ckpt.stats.get("host_budget_gb")},
     }
+    if not args.child and comm.world_size > 1:
+        # launched by torchrun: the launcher owns the ranks and tears the job down when one dies
+        res["ttr"] = {"error": "time-to-recover needs the plain form `python bench.py --gpus N` (its parent "
+                               "launches the N ranks, then the N-rank kill -> shrink -> rejoin drill); under "
+                               "torchrun a killed rank ends the whole launch"}
     if comm.rank == 0:
         line = json.dumps(res)
         print(line, flush=True)

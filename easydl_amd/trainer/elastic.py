@@ -160,6 +160,9 @@ class ElasticTrainer(RecoveryMixin):
         self._opt_stream = None      # optimizer update overlapping the next forward (_opt_overlap)
         self._opt_overlap_off = False
         self._act_need = 0
+        self._step_ev = None         # GPU event at the current step's start (fault after_ms counts from it)
+        self._gpu_step_evs = []      # (step, start event) not yet paired: GPU step durations
+        self._gpu_last = None        # (step, seconds) newest GPU-timed step
 
     def request_stop(self) -> None:
         """End ``fit`` after the current step (from ``on_step``).  Every rank must ask at the
@@ -866,6 +869,7 @@ class ElasticTrainer(RecoveryMixin):
                     self._dump_profile(prof)
                     prof = None
                 t0 = self._t_step = time.perf_counter()
+                self._mark_gpu_step_start()
                 ok = True
                 loss = None
                 try:
@@ -932,7 +936,7 @@ class ElasticTrainer(RecoveryMixin):
                            "dt": time.perf_counter() - t0}
                     self.history.append(rec)
                     self.events.emit("step_done", step=self.step, epoch=self.comm.epoch,
-                                     world=self.comm.world_size)
+                                     world=self.comm.world_size, dt=round(rec["dt"], 4), **self._gpu_step_time())
                     self.metrics.record(self.step, rec["dt"], samples=self.global_batch,
                                         tokens=self.global_batch * self.tokens_per_sample, world=self.comm.world_size,
                                         loss=None, extra=self._metrics_extra)
@@ -971,6 +975,30 @@ class ElasticTrainer(RecoveryMixin):
             if self.device.type == "cuda":
                 self.wait_update()      # the caller reads the trained state next
         return self
+
+    def _mark_gpu_step_start(self) -> None:
+        """Record a GPU event where this step starts on the compute stream.  At world 1 the host
+        runs ahead of the GPU (no per-step drain, _sync_point), so host timestamps are enqueue
+        times; GPU step durations (start of step k to start of step k+1, read without blocking)
+        and the fault injector's ``after_ms`` (utils/fault.py) use these events instead."""
+        if self.device.type != "cuda":
+            return
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record(torch.cuda.current_stream(self.device))
+        self._step_ev = ev
+        q = self._gpu_step_evs
+        q.append((self.step, ev))
+        while len(q) >= 2 and q[1][1].query():
+            (s0, e0), (_, e1) = q[0], q[1]
+            self._gpu_last = (s0 + 1, e0.elapsed_time(e1) / 1000.0)
+            q.pop(0)
+        del q[:-64]
+
+    def _gpu_step_time(self) -> dict:
+        """Newest completed GPU step duration for the step_done event (empty on the CPU)."""
+        if self._gpu_last is None:
+            return {}
+        return {"gpu_step": self._gpu_last[0], "gpu_s": round(self._gpu_last[1], 5)}
 
     def _metrics_extra(self) -> dict:
         from easydl_amd.utils.metrics import cu_count

@@ -118,6 +118,10 @@ def main(args) -> int:
     done_ts = [e["ts"] for e in ev if e["kind"] == "step_done" and (fault is None or e["ts"] < fault["ts"])]
     gaps = sorted(b - a for a, b in zip(done_ts, done_ts[1:]))[-8:]   # the last steps before the fault
     steady = sorted(b - a for a, b in zip(done_ts[2:], done_ts[3:]))     # every step before it, first 3 out
+    # GPU step durations (start of step k -> start of step k+1 on the compute stream, ElasticTrainer
+    # _mark_gpu_step_start): at world 1 the host enqueues ahead of the GPU, so host gaps are not steps
+    gpu = sorted(e["gpu_s"] for e in ev if e["kind"] == "step_done" and e.get("gpu_s") is not None
+                 and (fault is None or e["ts"] < fault["ts"]) and int(e.get("gpu_step", 0)) > 2)
     out = {
         "metric": "time-to-recover after SIGKILL of one worker (Llama elastic DDP, local operator)",
         "value": None if not ttr else ttr["ttr_s"], "unit": "s", "higher_is_better": False,
@@ -129,7 +133,11 @@ def main(args) -> int:
         "breakdown": ttr, "operator_rc": rc, "hot_standby": standby,
         "time_to_regain_s": ttr.get("time_to_regain_s") if ttr else None,
         "steps_lost": ttr.get("steps_lost") if ttr else None,
-        "step_s_before_fault": round(gaps[len(gaps) // 2], 4) if gaps else None,
+        "step_s_before_fault": (round(gpu[len(gpu) // 2], 4) if gpu else
+                                round(gaps[len(gaps) // 2], 4) if gaps else None),
+        "step_s_before_fault_clock": "gpu" if gpu else "host",
+        "first_step": _first_step(ev, fault, ttr),
+        "time_to_regrow_s": _regrow(ev, fault, n),
         "step_s_median": round(steady[len(steady) // 2], 5) if steady else None,
         "shared_gpu": share, "comm": env.get("EDL_COMM", "pg"), "workers": n,
         "replacement_from_standby": any(e["kind"] == "spawn" and e.get("standby") for e in ev),
@@ -142,12 +150,80 @@ def main(args) -> int:
         "final_states": [{k: e.get(k) for k in ("proc", "step", "world", "rank", "crc")}
                          for e in ev if e["kind"] == "final_state"],
         "worlds_seen": sorted({w for w in worlds if w}), "run_dir": run_dir,
+        "timeline": _timeline(ev, fault, ttr),
     }
     print(json.dumps(out), flush=True)
     unlink_job_segments(job_name)
     if os.environ.get("EDL_TTR_KEEP") != "1":
         shutil.rmtree(run_dir, ignore_errors=True)
     return 0 if rc == 0 and ttr else 1
+
+
+def _rel(e, fault):
+    return None if e is None or fault is None else round(e["ts"] - fault["ts"], 4)
+
+
+def _first_step(ev: list[dict], fault, ttr) -> dict | None:
+    """The first committed step after the fault: its own duration, and the memory plan it ran
+    under (a takeover short of HBM: split / recomputed layers, ElasticTrainer _memory_plan) with
+    when the memory came back -- the evidence of where a time-to-recover went."""
+    if fault is None or not ttr or ttr.get("first_step_s") is None:
+        return None
+    t_done = fault["ts"] + ttr["first_step_s"]
+    after = [e for e in ev if e["ts"] >= fault["ts"]]
+    done = next((e for e in after if e["kind"] == "step_done" and abs(e["ts"] - t_done) < 1e-3), None)
+    plan = next((e for e in after if e["kind"] == "memory_limited_steps"), None)
+    restored = next((e for e in after if e["kind"] == "memory_restored"), None)
+    return {
+        "s": done.get("dt") if done else None, "proc": done.get("proc") if done else None,
+        "world": done.get("world") if done else None,
+        "memory_plan": None if plan is None else {k: plan.get(k) for k in (
+            "split", "recompute_layers", "layers", "need_gb", "avail_gb", "margin")},
+        "memory_replans": sum(1 for e in after if e["kind"] == "memory_replanned" and e["ts"] <= t_done),
+        "memory_restored_s": _rel(restored, fault),
+        "memory_restored_at": None if restored is None else {"step": restored.get("step"), "mb": restored.get("mb"),
+                                                             "avail_gb": restored.get("avail_gb")},
+    }
+
+
+def _regrow(ev: list[dict], fault, n: int) -> float | None:
+    """N > 1: fault -> the first committed step at the full world size again (the replacement rejoined)."""
+    if fault is None or n <= 1:
+        return None
+    formed = next((x for x in ev if x["kind"] == "epoch_formed" and x["ts"] > fault["ts"] and x.get("world") == n),
+                  None)
+    if formed is None:
+        return None
+    done = next((d for d in ev if d["kind"] == "step_done" and d["ts"] > formed["ts"] and d.get("world") == n), None)
+    return _rel(done, fault)
+
+
+_TIMELINE_KINDS = ("fault_injected", "node_dead", "epoch_abort", "epoch_formed", "spawn", "exit_early", "joined",
+                   "restored", "comm_ready", "state_synced", "state_broadcast", "memory_limited_steps",
+                   "memory_replanned", "memory_restored", "step_done", "hbm_resume_refused", "rehomed")
+
+
+def _timeline(ev: list[dict], fault, ttr, limit: int = 48) -> list[dict]:
+    """Compact event timeline from the fault to one second past the first recovered step (the
+    drill's run directory is temporary: this is what stays in the JSON)."""
+    if fault is None:
+        return []
+    end = fault["ts"] + ((ttr or {}).get("first_step_s") or 30.0) + 1.0
+    out, seen = [], {}
+    for e in ev:
+        if e["ts"] < fault["ts"] or e["ts"] > end or e["kind"] not in _TIMELINE_KINDS:
+            continue
+        key = (e["kind"], e.get("epoch"), e.get("world"), e.get("step"))
+        if key in seen:     # N ranks doing the same thing: the first one, with a count
+            seen[key]["ranks"] = seen[key].get("ranks", 1) + 1
+            continue
+        rec = seen[key] = {"t": _rel(e, fault), "proc": e.get("proc"), "kind": e["kind"]}
+        for k in ("step", "epoch", "world", "dt", "split", "recompute_layers", "need_gb", "avail_gb", "source",
+                  "mb", "gpu_free_gb"):
+            if e.get(k) is not None:
+                rec[k] = e[k]
+        out.append(rec)
+    return out[:limit]
 
 
 def worker() -> None:

@@ -6,7 +6,8 @@
     nan@step=2                   poison the gradients after backward (non-finite skip path)
     delay@step=2,ms=500          sleep before the step (straggler)
     raise@step=6                 raise RuntimeError inside the step
-    kill@step=4,after_ms=1500    SIGKILL 1.5 s after step 4 starts (mid-step on the GPU)
+    kill@step=4,after_ms=1500    SIGKILL 1.5 s after step 4 starts on the GPU (mid-step; the
+                                 trainer's step-start GPU event, not the host's enqueue time)
     kill@step=4,wait=standby     first step >= 4 once the hot standby on this GPU has
                                  warmed up (utils/vram.py standby_warm_on), at most 30 steps late
     kill@step=6,point=in_update  SIGKILL inside the optimizer update of step 6: after its
@@ -95,8 +96,10 @@ class FaultInjector:
                 import torch
                 torch.cuda.synchronize(trainer.device)
             if s.after_ms > 0:
-                # the step runs on; the signal lands mid-step (GPU work of this step in flight)
-                threading.Thread(target=self._delayed, args=(s, step, trainer), name="edl-fault",
+                # the step runs on; the signal lands mid-step (GPU work of this step in flight),
+                # ``after_ms`` after the GPU reached the step's start (the trainer's step event)
+                ev = getattr(trainer, "_step_ev", None) if point == "step_start" else None
+                threading.Thread(target=self._delayed, args=(s, step, trainer, ev), name="edl-fault",
                                  daemon=True).start()
                 continue
             self._emit(s, step, trainer)
@@ -113,7 +116,12 @@ class FaultInjector:
             except Exception:  # noqa: BLE001
                 pass
 
-    def _delayed(self, s: FaultSpec, step: int, trainer) -> None:
+    def _delayed(self, s: FaultSpec, step: int, trainer, gpu_start=None) -> None:
+        if gpu_start is not None:
+            try:
+                gpu_start.synchronize()     # the GPU starts the step now (the host enqueued it earlier)
+            except Exception:  # noqa: BLE001 - fall back to the host clock
+                pass
         time.sleep(s.after_ms / 1000.0)
         self._emit(s, step, trainer)
         self._fire(s, trainer)
