@@ -49,6 +49,12 @@ void* edl_stream_create_cumask(int device, const uint32_t* mask, int nwords, int
 
 int edl_stream_destroy(void* s) { return (int)hipStreamDestroy((hipStream_t)s); }
 
+// The CU mask a stream's kernels are restricted to (32-bit words over the CUs);
+// returns a hipError_t.  Lets tests check every stream of a CU-planned rank.
+int edl_stream_get_cumask(void* s, uint32_t* out, int nwords) {
+  return (int)hipExtStreamGetCUMask((hipStream_t)s, (uint32_t)nwords, out);
+}
+
 int edl_roctx_available() {
   load_roctx();
   return g_push != nullptr;

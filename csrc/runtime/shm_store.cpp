@@ -27,6 +27,7 @@
 #include <time.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <atomic>
 #include <condition_variable>
 #include <deque>
@@ -657,14 +658,33 @@ void* edl_ckpt_engine_create(int device, uint64_t chunk_bytes, int copy_cus) {
     int ncu = 0;
     hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device);
     if (ncu >= 8 && copy_cus < ncu) {
+      // a rank under a Brain CU plan (EDL_CU_MASK, hex over the CUs) copies on CUs of its
+      // own share only: the engine's CUs are picked from the plan's set
+      std::vector<uint32_t> allowed((ncu + 31) / 32, 0xFFFFFFFFu);
+      if (const char* plan = getenv("EDL_CU_MASK")) {
+        std::fill(allowed.begin(), allowed.end(), 0u);
+        const char* p = plan;
+        if (p[0] == '0' && (p[1] == 'x' || p[1] == 'X')) p += 2;
+        const int len = (int)strlen(p);
+        for (int i = 0; i < len; ++i) {  // hex digit i from the right holds CUs 4i .. 4i+3
+          const char ch = p[len - 1 - i];
+          const int v = (ch >= '0' && ch <= '9') ? ch - '0' : (ch >= 'a' && ch <= 'f') ? ch - 'a' + 10
+                        : (ch >= 'A' && ch <= 'F') ? ch - 'A' + 10 : 0;
+          for (int b = 0; b < 4; ++b)
+            if ((v >> b) & 1 && 4 * i + b < ncu) allowed[(4 * i + b) / 32] |= 1u << ((4 * i + b) % 32);
+        }
+      }
       std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
       const int per_xcd = ncu / 8;
-      for (int i = 0; i < copy_cus; ++i) {
+      int picked = 0;
+      for (int i = 0; i < ncu && picked < copy_cus; ++i) {
         const int xcd = i % 8, c = (i / 8) % per_xcd;
         const int cu = c * 8 + xcd;  // hardware CU ids interleave the XCDs
+        if (!((allowed[cu / 32] >> (cu % 32)) & 1u)) continue;
         mask[cu / 32] |= 1u << (cu % 32);
+        ++picked;
       }
-      err = hipExtStreamCreateWithCUMask(&e->side, (uint32_t)mask.size(), mask.data());
+      if (picked > 0) err = hipExtStreamCreateWithCUMask(&e->side, (uint32_t)mask.size(), mask.data());
     }
   }
   if (err != hipSuccess) {

@@ -60,6 +60,7 @@ SIGS = {
                                           ctypes.POINTER(ctypes.c_double)]),
     "edl_stream_create_cumask": (vp, [i32, ctypes.POINTER(ctypes.c_uint32), i32, i32]),
     "edl_stream_destroy": (i32, [vp]),
+    "edl_stream_get_cumask": (i32, [vp, ctypes.POINTER(ctypes.c_uint32), i32]),
     "edl_roctx_available": (i32, []),
     "edl_roctx_push": (i32, [cp]),
     "edl_roctx_pop": (i32, []),

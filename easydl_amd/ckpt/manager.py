@@ -1042,7 +1042,8 @@ def _load_shard(read, table, state, dev, expect: int, what: str, seg=None, slot=
         for dst, off in now:
             checksum_tensor(dst, acc, base_index=off // 4)
         if items_later:
-            side = torch.cuda.Stream(dev)
+            from easydl_amd.utils.resources import new_stream
+            side = new_stream(dev)
             acc2 = torch.zeros(1, dtype=torch.int64, device=dev)
             ev = torch.cuda.Event()
             nb = sum(d.numel() * d.element_size() for d, _ in items_later)

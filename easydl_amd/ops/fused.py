@@ -574,7 +574,8 @@ def _deliver_wgrad(w, a, b_, side: bool = False, tn: bool = False):
             main = torch.cuda.current_stream(a.device)
             side = _SIDE.get(i)
             if side is None:
-                side = _SIDE[i] = torch.cuda.Stream(device=a.device)
+                from easydl_amd.utils.resources import new_stream
+                side = _SIDE[i] = new_stream(a.device)   # CU-masked under a Brain CU plan
             _MAIN[i] = main
             side.wait_stream(main)
             with torch.cuda.stream(side):

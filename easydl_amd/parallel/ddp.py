@@ -141,7 +141,8 @@ class ElasticDDP:
             # weight gradients may still be queued on the fused ops' side stream: launch the
             # collectives from a stream that waits for the caller's stream and for those
             if self._launch_stream is None:
-                self._launch_stream = torch.cuda.Stream(device=self.device)
+                from easydl_amd.utils.resources import new_stream
+                self._launch_stream = new_stream(self.device)
             ls = self._launch_stream
             ls.wait_stream(torch.cuda.current_stream(self.device))
             for st in others:

@@ -725,9 +725,12 @@ class ElasticTrainer(RecoveryMixin):
         shadow = self._shadow_active()
         seeded = None
         with self.kmix.phase("compute"):
+            ptrace = self._piece_trace_begin()
             for i, idx, last in self._pieces(mbs):   # (a memory-limited step: pieces, recompute)
                 if self.comm is not None and self.comm.aborted:  # epoch broke: do not start more work
                     raise CommAborted(f"epoch {self.comm.epoch} aborted before micro-batch {i}")
+                if ptrace is not None:
+                    self._piece_trace_mark(ptrace, i, len(idx))
                 if i != seeded:
                     self._seed_step(i)      # random streams keyed by micro-batch: a mid-step resume replays them
                     seeded = i
@@ -750,6 +753,8 @@ class ElasticTrainer(RecoveryMixin):
                     self._shadow_grads(i + 1, loss_acc)
                 if not last:
                     self.fault.maybe_inject("microbatch", self.step, trainer=self, mb=i)
+            if ptrace is not None:
+                self._piece_trace_mark(ptrace, None, 0)
         t_mb = time.perf_counter()
         if self._phases and self.device.type == "cuda":
             # diagnostic mode: drain the compute stream so 'finish' is the gradient all-reduce alone
@@ -792,7 +797,8 @@ class ElasticTrainer(RecoveryMixin):
         from easydl_amd.parallel.flat import install_update_waits
         install_update_waits(self.model)
         fused._WT_BATCH = False     # the batched W^T refresh would read every weight at the first use
-        self._opt_stream = torch.cuda.Stream(device=self.device)
+        from easydl_amd.utils.resources import new_stream
+        self._opt_stream = new_stream(self.device)     # CU-masked under a Brain CU plan
         self._opt_stream.wait_stream(torch.cuda.current_stream(self.device))
         return self._opt_stream
 
@@ -951,6 +957,7 @@ class ElasticTrainer(RecoveryMixin):
                         self._skip_deferred_probes(latest)
                     else:
                         self._run_deferred_probes()
+                    self._piece_trace_emit()
                     self._publish_act()
                     self._maybe_rehome()
                     if on_step is not None:

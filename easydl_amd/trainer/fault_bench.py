@@ -121,7 +121,7 @@ def main(args) -> int:
     # GPU step durations (start of step k -> start of step k+1 on the compute stream, ElasticTrainer
     # _mark_gpu_step_start): at world 1 the host enqueues ahead of the GPU, so host gaps are not steps
     gpu = sorted(e["gpu_s"] for e in ev if e["kind"] == "step_done" and e.get("gpu_s") is not None
-                 and (fault is None or e["ts"] < fault["ts"]) and int(e.get("gpu_step", 0)) > 2)
+                 and (fault is None or e["ts"] < fault["ts"]) and int(e.get("gpu_step", 0)) >= 2)
     out = {
         "metric": "time-to-recover after SIGKILL of one worker (Llama elastic DDP, local operator)",
         "value": None if not ttr else ttr["ttr_s"], "unit": "s", "higher_is_better": False,
@@ -174,8 +174,11 @@ def _first_step(ev: list[dict], fault, ttr) -> dict | None:
     done = next((e for e in after if e["kind"] == "step_done" and abs(e["ts"] - t_done) < 1e-3), None)
     plan = next((e for e in after if e["kind"] == "memory_limited_steps"), None)
     restored = next((e for e in after if e["kind"] == "memory_restored"), None)
+    pieces = next((e for e in after if e["kind"] == "limited_step_pieces"), None)
     return {
         "s": done.get("dt") if done else None, "proc": done.get("proc") if done else None,
+        "pieces": None if pieces is None else {"gpu_s": pieces.get("gpu_s"), "host_s": pieces.get("host_s"),
+                                               "each": pieces.get("pieces")},
         "world": done.get("world") if done else None,
         "memory_plan": None if plan is None else {k: plan.get(k) for k in (
             "split", "recompute_layers", "layers", "need_gb", "avail_gb", "margin")},

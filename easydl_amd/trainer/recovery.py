@@ -436,6 +436,33 @@ class RecoveryMixin:
             self.events.emit("memory_replanned", step=self.step, mb=mb, split=split, recompute_layers=rc,
                              avail_gb=round(avail / 2**30, 1))
 
+    def _piece_trace_begin(self):
+        """Per-piece timing of a memory-limited step (the evidence of where a takeover's first
+        step goes: host time per piece is enqueue + allocator stalls, GPU time is the kernels)."""
+        if not self._mb_limited or self.device.type != "cuda":
+            return None
+        return []
+
+    def _piece_trace_mark(self, tr: list, mb, n: int) -> None:
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record(torch.cuda.current_stream(self.device))
+        tr.append((mb, n, time.perf_counter(), ev, self._mb_plan, self._hbm_avail()))
+        if mb is None:
+            self._piece_trace = tr
+
+    def _piece_trace_emit(self) -> None:
+        """After the (drained) step: one event with every piece's host and GPU time."""
+        tr, self._piece_trace = getattr(self, "_piece_trace", None), None
+        if not tr or len(tr) < 2:
+            return
+        tr[-1][3].synchronize()
+        pieces = [{"mb": a[0], "n": a[1], "host_s": round(b[2] - a[2], 4),
+                   "gpu_s": round(a[3].elapsed_time(b[3]) / 1e3, 4), "split": a[4][0], "recompute": a[4][1],
+                   "avail_gb": round(a[5] / 2**30, 1)} for a, b in zip(tr, tr[1:])]
+        self.events.emit("limited_step_pieces", step=self.step, pieces=pieces,
+                         gpu_s=round(sum(p["gpu_s"] for p in pieces), 4),
+                         host_s=round(sum(p["host_s"] for p in pieces), 4))
+
     def _pieces(self, mbs: list):
         """(micro-batch index, sample indices, last) of a step's forward/backward passes: the
         micro-batches themselves, or -- in a memory-limited step -- their pieces, re-planned
@@ -565,7 +592,8 @@ class RecoveryMixin:
             copy(None)
             return
         if self._shadow_stream is None:
-            self._shadow_stream = torch.cuda.Stream(device=self.device)
+            from easydl_amd.utils.resources import new_stream
+            self._shadow_stream = new_stream(self.device)
         st = self._shadow_stream
         st.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(st):
@@ -609,7 +637,8 @@ class RecoveryMixin:
         views, loss_view = self._hshadow_views[slot]
         main = torch.cuda.current_stream(self.device)
         if self._shadow_stream is None:
-            self._shadow_stream = torch.cuda.Stream(device=self.device)
+            from easydl_amd.utils.resources import new_stream
+            self._shadow_stream = new_stream(self.device)
         st = self._shadow_stream
         st.wait_stream(main)
         with torch.cuda.stream(st):
