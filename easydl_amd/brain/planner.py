@@ -176,15 +176,65 @@ class Planner:
         return plan
 
     @staticmethod
-    def cu_for_profile(prof: dict, total_cus: int = 256) -> int | None:
-        """CUs for a rank from its kernel mix: matrix-core heavy ranks keep every CU;
-        bandwidth-bound ranks need only enough CUs to saturate HBM (~1/4 of the chip
-        drives 6 TB/s with 16-byte accesses), scaled by their compute share."""
+    def cu_for_sensitivity(s: float | None, total_cus: int = 256, tol: float = 0.05,
+                           floor: float = 0.25) -> int | None:
+        """Fewest CUs that keep a rank within ``tol`` of its full-chip speed, from its MEASURED
+        CU sensitivity ``s`` (utils/kmix.py: the share of its GPU time that scales with CUs).
+        With ``t(c) = t_C * (1 + s * (C / c - 1))`` the slowdown stays <= tol for
+        ``c >= C * s / (s + tol)``; never below ``floor`` of the chip (~1/4 of the CUs saturate
+        HBM with 16-byte accesses).  None (keep every CU) when that is >= 90 % of the chip."""
+        if s is None:
+            return None
+        frac = max(floor, s / (s + tol)) if s > 0 else floor
+        if frac >= 0.9:
+            return None
+        return int(math.ceil(total_cus * frac / 8)) * 8   # whole CUs per XCD
+
+    @classmethod
+    def cu_for_profile(cls, prof: dict, total_cus: int = 256) -> int | None:
+        """CUs for a rank from a measured profile: its probed CU sensitivity (``cu_sensitivity``,
+        live) when present; else a rocprofv3 kernel profile's MFMA share (kernel names:
+        matrix-core heavy ranks keep every CU, bandwidth-bound ranks need only enough CUs to
+        saturate HBM, scaled by their compute share).  A phase split alone (which block
+        launched the kernels, utils/kmix.py) is a label, not a measurement: no CU plan."""
+        if prof.get("cu_sensitivity") is not None:
+            return cls.cu_for_sensitivity(float(prof["cu_sensitivity"]), total_cus)
+        if "top" not in prof and prof.get("source") != "rocprofv3":
+            return None
         comp = prof.get("compute_frac", 1.0)
         if comp >= 0.5:
             return None
         frac = max(0.25, min(1.0, 0.25 + comp))
         return int(round(total_cus * frac / 8)) * 8   # whole CUs per XCD
+
+    @staticmethod
+    def sensitivity_from_telemetry(g) -> float | None:
+        """A GPU that runs ONE rank and has no probe yet: amd-smi's memory-controller activity
+        over its graphics activity (``average_umc_activity`` / ``average_gfx_activity``) --
+        bandwidth-bound kernels keep the memory controllers busy for most of the GPU's busy
+        time, matrix-core kernels for a fraction of it.  Coarse: used only at the extremes."""
+        busy, umc = getattr(g, "busy_pct", None), getattr(g, "umc_pct", None)
+        if busy is None or umc is None or busy < 30:
+            return None
+        share = umc / busy
+        if share >= 0.7:
+            return 0.05          # bandwidth-bound
+        if share <= 0.35:
+            return 1.0           # matrix-core bound
+        return None
+
+    @staticmethod
+    def hbm_for_rank(m: dict, margin: float = 1.15, slack_gb: float = 2.0) -> float | None:
+        """Per-rank HBM cap from what the rank's allocator really held at its peak
+        (``hbm_peak_gb``, trainer metrics): peak x margin + slack, when that is clearly below
+        the cap it runs under now (its current plan, else the whole GPU) -- the headroom goes
+        back to the GPU's other tenants (a PS, an evaluator, a hot standby)."""
+        peak = m.get("hbm_peak_gb")
+        if not peak:
+            return None
+        want = float(math.ceil(peak * margin + slack_gb))
+        cap = m.get("hbm_cap_gb") or m.get("hbm_total_gb") or HBM_GB
+        return want if want < 0.85 * cap else None
 
     # ------------------------------------------------------------------ communication
     GROUPS = ("dp", "tp")
@@ -282,20 +332,40 @@ class Planner:
                 elif best != cur:
                     plan.bucket_mb = best
                     changed.append(f"bucket autotune: best {best} MB")
-        # per-rank CU plan from rocprofv3 kernel profiles (metrics[n]["rocprof"], see
-        # collectors.rocprof_kernel_profile): a rank whose GPU time is mostly bandwidth-bound
-        # work (a PS applying AdamW, an evaluator) keeps its speed on a slice of the CUs
-        # (metrics[n]["gpu_mix"]: the same split measured live by the running rank, utils/kmix.py;
-        # a rank is re-planned only when the plan differs from the CUs it runs on now)
+        # per-rank CU and HBM plans from measurements (no role or phase labels): the rank's probed
+        # CU sensitivity (metrics[n]["gpu_mix"]["cu_sensitivity"], utils/kmix.py), a rocprofv3
+        # kernel profile (metrics[n]["rocprof"]), or -- a GPU with one rank and no probe -- its
+        # amd-smi memory-controller vs graphics activity; the HBM cap from the rank's allocator
+        # peak.  A rank is re-planned only when the plan differs from what it runs under now.
+        per_gpu: dict = {}
+        for n, m in metrics.items():
+            if m.get("gpu") is not None and m.get("device", "cuda") == "cuda":
+                per_gpu.setdefault(int(m["gpu"]), []).append(n)
         for n, m in metrics.items():
             prof = m.get("rocprof") or m.get("gpu_mix")
-            if prof and m.get("device", "cuda") == "cuda" or m.get("rocprof"):
+            cu, src = None, None
+            if prof and (m.get("device", "cuda") == "cuda" or m.get("rocprof")):
                 cu = self.cu_for_profile(prof)
-                if cu is not None and cu != m.get("cu"):
-                    plan.per_rank.setdefault(n, {})["cu"] = cu
-                    src = "rocprofv3" if m.get("rocprof") else "live"
-                    changed.append(f"{n}: {cu} CUs ({100 * prof['memory_frac']:.0f}% of GPU time bandwidth-bound, "
-                                   f"{src})")
+                if prof.get("cu_sensitivity") is not None:
+                    src = f"CU sensitivity {prof['cu_sensitivity']:.2f} measured on half the CUs"
+                elif m.get("rocprof"):
+                    src = f"rocprofv3: {100 * prof.get('memory_frac', 0):.0f}% of GPU time bandwidth-bound"
+            has_probe = bool(prof and prof.get("cu_sensitivity") is not None)
+            g = m.get("gpu")
+            if (cu is None and not has_probe and not m.get("rocprof") and g is not None
+                    and len(per_gpu.get(int(g), [])) == 1 and int(g) < len(inv.gpus)):
+                s_tel = self.sensitivity_from_telemetry(inv.gpus[int(g)])
+                cu = self.cu_for_sensitivity(s_tel)
+                if cu is not None:
+                    gi = inv.gpus[int(g)]
+                    src = f"amd-smi: umc {gi.umc_pct:.0f}% of gfx {gi.busy_pct:.0f}%"
+            if cu is not None and cu != m.get("cu"):
+                plan.per_rank.setdefault(n, {})["cu"] = cu
+                changed.append(f"{n}: {cu} CUs ({src})")
+            hbm = self.hbm_for_rank(m) if m.get("device", "cuda") == "cuda" else None
+            if hbm is not None and hbm != m.get("hbm_cap_gb"):
+                plan.per_rank.setdefault(n, {})["hbm_gb"] = hbm
+                changed.append(f"{n}: HBM cap {hbm:.0f} GB (peak {m['hbm_peak_gb']:.1f} GB)")
             # a parameter server on host CPUs that is busy most of the time: more cores
             if m.get("role") == "ps" and m.get("device") == "cpu" and m.get("busy_frac", 0) > self.cfg.ps_busy_high:
                 cpu = int(m.get("cpu") or 1)

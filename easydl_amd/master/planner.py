@@ -153,7 +153,9 @@ class PlanLoop:
                 res.cu = int(d["cu"])
             if d.get("cpu") and int(d["cpu"]) != now.get("cpu"):
                 res.cpu = float(d["cpu"])     # a CPU-bound parameter server gets more cores
-            if res.cu or res.cpu:
+            if d.get("hbm_gb") and float(d["hbm_gb"]) != now.get("hbm_cap_gb"):
+                res.hbm_gb = float(d["hbm_gb"])   # HBM cap from the rank's measured allocator peak
+            if res.cu or res.cpu or res.hbm_gb:
                 jr.resource_updation.append(ResourceUpdation(name=name, resource=res))
         for u in jr.resource_updation:
             node = next((n for n in newp.per_rank if n.split(":")[0] == u.name), u.name)

@@ -44,6 +44,12 @@ def shard_of(model: torch.nn.Module, num_ps: int, index: int) -> dict[str, torch
     return {n: p.detach() for n, p in params.items() if assign[n] == index}
 
 
+class PSReconnected(ConnectionError):
+    """An IPC-bound request (``push_ipc``: its gradients sit in the OLD PS's mapped inbox) could
+    not be delivered: the PS died and a replacement took its place.  Not re-sent -- the push is
+    lost (async PS: counted in ``lost_pushes``); the client maps the replacement's buffers."""
+
+
 class PSClient:
     def __init__(self, num_ps: int, resolve, worker_id: str, retry_s: float = 120.0, transport: str = "tcp"):
         """``resolve(i) -> (host, port)`` returns the current address of PS i.
@@ -70,6 +76,11 @@ class PSClient:
         self._sp_plan: dict = {}
         self.sparse_path = {"ipc_pulls": 0, "ipc_pushes": 0, "tcp_pulls": 0, "tcp_pushes": 0}
         self._inflight = None    # futures of the pipelined push in flight (push_async)
+        # maps of a PS that died: kept until the device has drained every kernel that may still
+        # read or write them (closing an IPC mapping under an in-flight kernel would fault)
+        self._retired: list[dict] = []
+        self.lost_pushes = [0] * num_ps
+        self.reconnects: list[dict] = []  # {"ps", "lost", "version_before", "version_after", "s"}
 
     def bind(self, model: torch.nn.Module) -> None:
         from easydl_amd.ps.embedding import tables_of
@@ -145,26 +156,66 @@ class PSClient:
                 out[f"sparse/{n}/grad"] = g[pos]
         return out
 
-    def _call(self, i: int, header: dict, tensors=None):
+    def _call(self, i: int, header: dict, tensors=None, ipc_bound: bool = False):
+        """One request to PS i; a broken connection is re-resolved and the request re-sent to
+        the replacement PS -- unless it is ``ipc_bound`` (it refers to the dead PS's mapped
+        buffers), which raises :class:`PSReconnected` instead."""
         t_end = time.monotonic() + self.retry_s
         while True:
             with self._locks[i]:
                 try:
                     if i not in self._socks:
+                        if ipc_bound and i not in self._ipc:
+                            raise PSReconnected(f"PS {i}: mapping gone before {header.get('op')}")
                         self._socks[i] = connect(*self.resolve(i))
                     send_msg(self._socks[i], header, tensors)
-                    return recv_msg(self._socks[i])
+                    h = recv_msg(self._socks[i])
+                    if ipc_bound and isinstance(h[0], dict) and h[0].get("error") == "remap":
+                        raise PSReconnected(f"PS {i} does not know this worker's mapping")
+                    return h
+                except PSReconnected:
+                    self._retire_map(i)
+                    raise
                 except (ConnectionError, OSError, TimeoutError):
-                    self._ipc.pop(i, None)  # a replacement PS exports new handles
+                    self._retire_map(i)     # a replacement PS exports new handles
                     s = self._socks.pop(i, None)
                     if s is not None:
                         try:
                             s.close()
                         except OSError:
                             pass
+                    if ipc_bound:
+                        raise PSReconnected(f"PS {i} connection lost during {header.get('op')}")
                     if time.monotonic() > t_end:
                         raise
             time.sleep(0.2)  # PS being replaced: re-resolve and retry
+
+    def _retire_map(self, i: int) -> None:
+        m = self._ipc.pop(i, None)
+        if m is not None:
+            self._retired.append(m)
+
+    def _release_retired(self, device) -> None:
+        """Drop dead PSs' mappings once no kernel of this process can still touch them.  Called
+        only at the entry of pull / push (the thread that launches the copy kernels): the pool
+        threads that notice a dead PS only move its map here, so a kernel the launching thread
+        enqueued from that map keeps it referenced until this device-wide drain."""
+        if self._retired and device is not None and torch.device(device).type == "cuda":
+            torch.cuda.synchronize(device)
+            self._retired.clear()
+
+    def _remap_after_loss(self, i: int, device, t0: float) -> int:
+        """The push to PS i was lost with its PS: map the replacement (which restored its newest
+        snapshot and continues the version count from the highest version any worker saw) and
+        go on from its current version."""
+        before = self.versions[i]
+        self.lost_pushes[i] += 1
+        m = self._ipc_map(i, device)
+        after = int(m.get("version", before))
+        self.versions[i] = max(before, after)
+        self.reconnects.append({"ps": i, "lost": 1, "version_before": before, "version_after": after,
+                                "s": round(time.monotonic() - t0, 3)})
+        return self.versions[i]
 
     # -- GPU transport ---------------------------------------------------------------
     # Bulk bytes never cross TCP: per PS, ONE kernel launch moves every parameter
@@ -177,14 +228,20 @@ class PSClient:
         m = self._ipc.get(i)
         if m is None or m["sock"] is not self._socks.get(i):
             from easydl_amd.ps.ipc import import_tensor
-            hdr = {"op": "ipc_open", "worker": self.worker_id, "sparse_cap": self.sparse_cap if self.tables else 0}
+            if m is not None:
+                self._retire_map(i)
+            # seen_version: a replacement PS continues the version count from the highest one
+            # its workers saw, so no worker ever observes a version going back
+            hdr = {"op": "ipc_open", "worker": self.worker_id, "sparse_cap": self.sparse_cap if self.tables else 0,
+                   "seen_version": int(self.versions[i])}
             h, _ = self._call(i, hdr)
             if not h.get("ok"):
                 raise RuntimeError(f"PS {i}: {h.get('error')}")
             d = h["ipc"]
             m = {"w": import_tensor(d["w"]), "inbox": [import_tensor(x) for x in d["inbox"]], "layout": d["layout"],
                  "sock": self._socks.get(i), "slot": 0, "pull_plan": None, "push_plan": None,
-                 "flag": import_tensor(d["flag"]) if "flag" in d else None, "seq": 0}
+                 "flag": import_tensor(d["flag"]) if "flag" in d else None, "seq": 0,
+                 "version": int(h.get("version", 0))}
             if "tables" in d:
                 m["tables"] = {n: (import_tensor(x["w"]), int(x["rows"])) for n, x in d["tables"].items()}
                 m["sp_inbox"] = {n: [[import_tensor(x) for x in b] for b in bufs]
@@ -260,6 +317,7 @@ class PSClient:
 
     def pull(self, model: torch.nn.Module, min_versions=None) -> list[int]:
         params = dict(model.named_parameters())
+        self._release_retired(next(iter(params.values())).device)
         if self.transport == "ipc":
             # control round trips in parallel (version / bounded-staleness wait; the PS
             # answers once the update of that version has finished writing), then one
@@ -299,6 +357,7 @@ class PSClient:
         same round trip returns once the shard has applied them, and the fresh
         parameters are copied right away — push + pull in ONE control message per PS."""
         params = dict(model.named_parameters())
+        self._release_retired(next(iter(params.values())).device)
         sparse_dev = {}
         if self.transport == "ipc" and self.tables:
             dev = next(iter(params.values())).device
@@ -357,7 +416,11 @@ class PSClient:
                 ready.synchronize()
                 hdr = {"op": "push_ipc", "worker": self.worker_id, "step": step, "slot": slots[i],
                        "pull": bool(then_pull), "sparse_ipc": sp_ipc, "seq": seqs[i]}
-                h, _ = self._call(i, hdr, self._sparse_grads(i, sparse_grads))
+                t0 = time.monotonic()
+                try:
+                    h, _ = self._call(i, hdr, self._sparse_grads(i, sparse_grads), ipc_bound=True)
+                except PSReconnected:
+                    return self._remap_after_loss(i, dev, t0)
                 return h["version"]
 
             self.versions = list(self._pool.map(one, range(self.num_ps)))
@@ -398,6 +461,7 @@ class PSClient:
             raise RuntimeError("push_async needs the GPU transport and a dense model")
         self.drain()
         params = dict(model.named_parameters())
+        self._release_retired(next(iter(params.values())).device)
         slots = [self._push_launch(i, params) for i in range(self.num_ps)]
         dev = next(iter(params.values())).device
         stream = torch.cuda.current_stream(dev)
@@ -416,7 +480,11 @@ class PSClient:
             ready.synchronize()     # the message leaves once the stream passed the flag stores
             hdr = {"op": "push_ipc", "worker": self.worker_id, "step": step, "slot": slots[i], "pull": False,
                    "sparse_ipc": False, "seq": seqs[i]}
-            h, _ = self._call(i, hdr, {})
+            t0 = time.monotonic()
+            try:
+                h, _ = self._call(i, hdr, {}, ipc_bound=True)
+            except PSReconnected:
+                return self._remap_after_loss(i, dev, t0)
             return h["version"]
 
         self._inflight = [self._pool.submit(one, i) for i in range(self.num_ps)]
@@ -434,6 +502,7 @@ class PSClient:
         running meanwhile, so the copy holds each parameter word of version >= the last
         answered push - 1."""
         params = dict(model.named_parameters())
+        self._release_retired(next(iter(params.values())).device)
         for i in range(self.num_ps):
             self._pull_launch(i, params)
 

@@ -148,6 +148,8 @@ class ParameterServer:
         self._busy = 0
         from easydl_amd.utils.kmix import KernelMixMeter
         self.kmix = KernelMixMeter(self.state.device)   # live kernel mix for the Brain (utils/kmix.py)
+        self.events = None           # EventLog of the PS process (run_ps)
+        self.on_apply = None         # callback after every update (run_ps: fault injection, first-apply event)
 
     # -- optimizer -------------------------------------------------------------
     def _fence_snapshot(self) -> None:
@@ -179,6 +181,8 @@ class ParameterServer:
                 self._apply_table(t, ids, grads, scale)
         self.version += 1
         self.stats["applied"] += 1
+        if self.on_apply is not None:
+            self.on_apply(self)
         if st.w.is_cuda:
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream(st.device))
@@ -320,6 +324,7 @@ class ParameterServer:
                 return
             with self.lock:
                 wid = hdr.get("worker", "?")
+                self._adopt_seen_version(int(hdr.get("seen_version", 0)), wid)
                 if wid not in self.inboxes:
                     self.inboxes[wid] = [torch.zeros_like(st.w), torch.zeros_like(st.w)]
                     self._inbox_ev[wid] = [None, None]
@@ -364,6 +369,11 @@ class ParameterServer:
             send_msg(conn, {"ok": True, "version": ver})
         elif op == "push_ipc":
             wid, slot = hdr["worker"], int(hdr.get("slot", 0))
+            if wid not in self.inboxes or wid not in self._push_flag:
+                # a worker that mapped a PREVIOUS incarnation of this shard (it died): its
+                # gradients are in that PS's inbox, not ours -- it must map this one first
+                send_msg(conn, {"ok": False, "error": "remap", "version": self.version})
+                return
             if hdr.get("seq") is not None:   # the worker's inbox writes before our reads
                 dev = self.state.device
                 sparse.ps_wait(self._push_flag[wid], int(hdr["seq"]), self.push_wait_s,
@@ -412,6 +422,25 @@ class ParameterServer:
             return
         else:
             send_msg(conn, {"ok": False, "error": f"unknown op {op}"})
+
+    def _adopt_seen_version(self, seen: int, worker: str) -> None:
+        """(Lock held.)  A replacement PS restored its newest snapshot (version V_snap), but its
+        workers may have seen versions up to V_hwm from the dead PS: the count continues from
+        the highest version any worker reports, so versions never go back (sync-mode waits for
+        ``min_version`` and bounded staleness rely on that).  ``lost_updates`` = the updates the
+        dead PS applied after its last snapshot, as far as the workers saw them."""
+        if seen <= self.version:
+            return
+        base = self.stats.get("restored_version")
+        if base is not None:
+            self.stats["lost_updates"] = max(self.stats.get("lost_updates", 0), seen - int(base))
+        self.stats["version_adopted_from"] = worker
+        self.version = seen
+        self.lock.notify_all()
+        ev = getattr(self, "events", None)
+        if ev is not None:
+            ev.emit("ps_version_adopted", version=seen, worker=worker, restored_version=base,
+                    lost_updates=self.stats.get("lost_updates"))
 
     def retire(self, timeout_s: float = 60.0) -> int:
         """Graceful hand-over to a successor (vertical resize by replacement, reference
@@ -628,6 +657,7 @@ class PSSnapshotter:
                 log.error("PS snapshot checksum mismatch: ignoring")
                 return False
             ps.load(bufs, info["step"], info["meta"]["step"], info["meta"].get("table_steps"))
+            ps.stats["restored_version"] = ps.version
             return True
         finally:
             seg.close()

@@ -724,7 +724,8 @@ class ElasticTrainer(RecoveryMixin):
                 mbs = mbs[res["mb"]:]
         shadow = self._shadow_active()
         seeded = None
-        with self.kmix.phase("compute"):
+        probe = self.kmix.probe_due(self.step) and not self._mb_limited and self.tp == 1
+        with self.kmix.phase("compute", probe=probe):   # (probe: on half the CUs, utils/kmix.py)
             ptrace = self._piece_trace_begin()
             for i, idx, last in self._pieces(mbs):   # (a memory-limited step: pieces, recompute)
                 if self.comm is not None and self.comm.aborted:  # epoch broke: do not start more work
@@ -1009,8 +1010,14 @@ class ElasticTrainer(RecoveryMixin):
 
     def _metrics_extra(self) -> dict:
         from easydl_amd.utils.metrics import cu_count
-        return {"role": self.ctx.role, "gpu_mix": self.kmix.snapshot(), "cu": cu_count(self.ctx.cu_mask),
-                "device": self.device.type}
+        out = {"role": self.ctx.role, "gpu_mix": self.kmix.snapshot(), "cu": cu_count(self.ctx.cu_mask),
+               "device": self.device.type}
+        if self.device.type == "cuda":
+            # the Brain's per-rank HBM plan: what this rank's allocator actually holds at its peak
+            out.update(gpu=self.device.index, hbm_peak_gb=round(torch.cuda.max_memory_reserved(self.device) / 2**30, 2),
+                       hbm_total_gb=round(torch.cuda.get_device_properties(self.device).total_memory / 2**30, 1),
+                       hbm_cap_gb=self.ctx.hbm_gb)
+        return out
 
     def _dump_profile(self, prof) -> None:
         import io
@@ -1064,6 +1071,8 @@ class ElasticTrainer(RecoveryMixin):
         if mb and float(mb) != self.ddp.bucket_mb:
             self.ddp.set_bucket_mb(float(mb))
             self.events.emit("plan_bucket_mb", mb=float(mb), step=self.step)
+        if doc.get("cu_probe"):
+            self.kmix.request_probe()     # the Brain wants a fresh CU-sensitivity measurement
         ci = doc.get("ckpt_interval")
         if ci and self.checkpoint is not None:
             self.checkpoint.interval = max(1, int(ci))

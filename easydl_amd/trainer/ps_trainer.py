@@ -65,9 +65,23 @@ def run_ps(model_fn, num_ps: int, ctx: TrainerContext | None = None, *, optimize
                          tables=table_shard_spec(model, num_ps, ctx.index),
                          sparse_optimizer=sparse_optimizer, sparse_lr=sparse_lr, seed=seed)
     del model  # the PS keeps only its shard
+    ps.events = events
     handoff = _await_predecessor(kv, ctx.index, gen, events)
+    t_restore = time.perf_counter()
     if snap.restore(ps):
-        events.emit("ps_restored", version=ps.version, handoff=handoff)
+        events.emit("ps_restored", version=ps.version, handoff=handoff, gen=gen,
+                    s=round(time.perf_counter() - t_restore, 3))
+    inj = fault.FaultInjector.from_env(ctx, events)
+    first = {"done": gen == 0}
+
+    def on_apply(p):
+        # a PS fault fires at an update count (``kill@step=<version>,role=ps``): mid-traffic,
+        # with workers' pushes in flight; a replacement marks its first applied update (PS TTR)
+        if not first["done"]:
+            first["done"] = True
+            events.emit("ps_first_update", version=p.version, gen=gen)
+        inj.maybe_inject("step_start", p.version)
+    ps.on_apply = on_apply
     if snapshot_every > 0:
         snap.prepare(ps)
     ps.start()
@@ -161,6 +175,21 @@ class PSWorker:
         if pipeline is None:
             pipeline = os.environ.get("EDL_PS_PIPELINE", "0") == "1"
         self.pipeline = bool(pipeline) and self.client.pipelined()
+        self._reconnects_seen = 0
+        self._max_versions = [0] * num_ps
+
+    def _watch_versions(self) -> None:
+        """PS failures seen by this worker: each reconnect to a replacement PS (with the push it
+        lost) becomes an event, and a shard version lower than one already seen is flagged --
+        a replacement continues the count from the highest version its workers report."""
+        rc = self.client.reconnects
+        while self._reconnects_seen < len(rc):
+            self.events.emit("ps_reconnected", step=self.steps, **rc[self._reconnects_seen])
+            self._reconnects_seen += 1
+        for i, v in enumerate(self.client.versions):
+            if v < self._max_versions[i]:
+                self.events.emit("ps_version_went_back", ps=i, version=v, seen=self._max_versions[i])
+            self._max_versions[i] = max(self._max_versions[i], v)
 
     def fit(self, loss_fn, data, batch_size: int, shard_size: int, epochs: int = 1, on_step=None):
         self.rdzv.join()
@@ -199,6 +228,7 @@ class PSWorker:
                         self.client.push(self.model, self.steps, then_pull=fused)
                         need_pull = not fused
                     t3 = time.perf_counter()
+                    self._watch_versions()
                     self.steps += 1
                     self._phase = [a + b for a, b in zip(self._phase, (t1 - t0, t2 - t1, t3 - t2))]
                     if self.steps % 16 == 0:  # where a PS step's time goes (pull / compute / push)

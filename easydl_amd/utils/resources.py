@@ -43,7 +43,7 @@ def mask_words(hex_mask: str, ncu: int = 256) -> list[int]:
     return [(v >> (32 * i)) & 0xFFFFFFFF for i in range((ncu + 31) // 32)]
 
 
-def _masked_stream(device: torch.device, words: list[int]):
+def masked_stream(device: torch.device, words: list[int]):
     rt = _native.runtime()
     arr = (ctypes.c_uint32 * len(words))(*words)
     h = rt("edl_stream_create_cumask", device.index or 0, arr, len(words), 0)
@@ -58,7 +58,7 @@ def apply_cu_mask(device: torch.device, hex_mask: str):
     """Create a CU-masked stream and make it current; returns the ExternalStream.  Later
     streams of this rank (:func:`new_stream`) get the same mask."""
     words = mask_words(hex_mask)
-    s = _masked_stream(device, words)
+    s = masked_stream(device, words)
     if s is None:
         log.warning("CU mask %s could not be applied", hex_mask)
         return None
@@ -86,11 +86,33 @@ def new_stream(device, priority: int = 0):
     device = torch.device(device)
     words = _PLAN.get(device.index or 0)
     if words is not None:
-        s = _masked_stream(device, words)
+        s = masked_stream(device, words)
         if s is not None:
             return s
         log.warning("CU-masked side stream could not be created; using an unmasked one")
     return torch.cuda.Stream(device=device, priority=priority)
+
+
+def half_cu_mask(device) -> tuple[list[int] | None, int]:
+    """(mask words over half of this rank's CUs, spread evenly over the 8 XCDs; the rank's CU
+    count): the CU-sensitivity probe's stream (utils/kmix.py).  Hardware CU ids interleave the
+    XCDs (id = c * 8 + xcd), so the half keeps the first half of each XCD's CUs."""
+    device = torch.device(device)
+    ncu = torch.cuda.get_device_properties(device).multi_processor_count
+    words = _PLAN.get(device.index or 0) or [0xFFFFFFFF] * ((ncu + 31) // 32)
+    cus = [i for i in range(ncu) if (words[i // 32] >> (i % 32)) & 1]
+    if len(cus) < 2:
+        return None, len(cus)
+    keep = []
+    for x in range(8):
+        mine = [c for c in cus if c % 8 == x]
+        keep += mine[:max(1, len(mine) // 2)] if mine else []
+    if len(keep) >= len(cus):
+        return None, len(cus)
+    out = [0] * len(words)
+    for c in keep:
+        out[c // 32] |= 1 << (c % 32)
+    return out, len(cus)
 
 
 def stream_cu_mask(stream) -> list[int] | None:

@@ -41,22 +41,65 @@ def test_meter_forgets_phases_older_than_its_window():
     assert m.snapshot() is None
 
 
-def test_live_mix_gives_a_running_bandwidth_bound_rank_a_cu_plan_once():
-    """A PS whose live GPU time is all HBM-bound updates gets a CU slice; once it runs on that
-    slice (its metrics report the CUs) the Brain does not plan it again; a compute-bound
-    trainer keeps the whole GPU; CPU-hosted roles get no CU plan at all."""
-    ps_mix = {"compute_frac": 0.02, "memory_frac": 0.98, "gpu_s": 3.0, "source": "hip-events"}
-    tr_mix = {"compute_frac": 0.93, "memory_frac": 0.07, "gpu_s": 30.0, "source": "hip-events"}
-    metrics = {"job-ps-0:11": {"role": "ps", "device": "cuda", "gpu_mix": ps_mix, "cu": None},
+def test_measured_cu_sensitivity_gives_a_bandwidth_bound_rank_a_cu_plan_once():
+    """A rank whose probe measured almost no slowdown on half the CUs (HBM-bound: a PS applying
+    AdamW) gets a CU slice; once it runs on that slice (its metrics report the CUs) the Brain
+    does not plan it again; a rank that slows down ~2x on half the CUs keeps the whole GPU;
+    CPU-hosted roles get no CU plan at all.  No role or phase label enters the decision."""
+    ps_mix = {"compute_frac": 0.93, "memory_frac": 0.07, "gpu_s": 3.0, "source": "hip-events",
+              "cu_sensitivity": 0.03}
+    tr_mix = {"compute_frac": 0.93, "memory_frac": 0.07, "gpu_s": 30.0, "source": "hip-events",
+              "cu_sensitivity": 0.92}
+    metrics = {"job-ps-0:11": {"role": "worker", "device": "cuda", "gpu_mix": ps_mix, "cu": None},
                "job-worker-0:12": {"role": "worker", "device": "cuda", "gpu_mix": tr_mix, "step_time": 1.0},
                "job-ps-1:13": {"role": "ps", "device": "cpu", "gpu_mix": ps_mix, "busy_frac": 0.1, "cpu": 4}}
     nxt = Planner().next_plan(JobFeatures(mode="ps", params=3.3e8), _inv(), _plan(), metrics)
     cu = nxt.per_rank["job-ps-0:11"]["cu"]
-    assert 0 < cu < 256 and cu % 8 == 0 and "live" in nxt.reason
+    assert 0 < cu < 256 and cu % 8 == 0 and "measured on half the CUs" in nxt.reason
     assert "cu" not in nxt.per_rank.get("job-worker-0:12", {}) and "job-ps-1:13" not in nxt.per_rank
     metrics["job-ps-0:21"] = dict(metrics.pop("job-ps-0:11"), cu=cu)      # the replacement, on its slice
     again = Planner().next_plan(JobFeatures(mode="ps", params=3.3e8), _inv(), _plan(), metrics)
     assert again is None or "job-ps-0:21" not in again.per_rank
+
+
+def test_a_phase_label_alone_never_plans_cus():
+    """the phase split says where kernels were launched from, not what they do."""
+    mix = {"compute_frac": 0.02, "memory_frac": 0.98, "gpu_s": 3.0, "source": "hip-events"}
+    metrics = {"job-ps-0:11": {"role": "ps", "device": "cuda", "gpu_mix": mix}}
+    nxt = Planner().next_plan(JobFeatures(mode="ps", params=3.3e8), _inv(), _plan(), metrics)
+    assert nxt is None or "job-ps-0:11" not in nxt.per_rank
+
+
+def test_cu_for_sensitivity_keeps_the_slowdown_small():
+    p = Planner
+    assert p.cu_for_sensitivity(None) is None and p.cu_for_sensitivity(0.9) is None
+    assert p.cu_for_sensitivity(0.0) == 64                      # HBM saturates at ~1/4 of the chip
+    for s in (0.01, 0.03, 0.1, 0.3):
+        c = p.cu_for_sensitivity(s)
+        assert c % 8 == 0 and s * (256 / c - 1) <= 0.05 + 1e-9, (s, c)
+    assert p.cu_for_sensitivity(0.03) < p.cu_for_sensitivity(0.1) < p.cu_for_sensitivity(0.3)
+
+
+def test_hbm_plan_from_the_allocator_peak():
+    m = {"device": "cuda", "gpu": 0, "hbm_peak_gb": 20.0, "hbm_total_gb": 288.0, "hbm_cap_gb": None}
+    nxt = Planner().next_plan(JobFeatures(mode="ps", params=3.3e8), _inv(), _plan(), {"w:1": m})
+    assert nxt.per_rank["w:1"]["hbm_gb"] == 25.0 and "HBM cap 25 GB" in nxt.reason
+    full = dict(m, hbm_peak_gb=250.0)                           # no headroom: no cap
+    again = Planner().next_plan(JobFeatures(mode="ps", params=3.3e8), _inv(), _plan(), {"w:1": full})
+    assert again is None or "hbm_gb" not in again.per_rank.get("w:1", {})
+    capped = dict(m, hbm_cap_gb=25.0)                           # already running under it
+    assert Planner.hbm_for_rank(capped) is None
+
+
+def test_single_rank_gpu_without_a_probe_uses_amdsmi_activity():
+    inv = _inv()
+    inv.gpus[3].busy_pct, inv.gpus[3].umc_pct = 95.0, 85.0      # memory controllers busy all along
+    inv.gpus[4].busy_pct, inv.gpus[4].umc_pct = 98.0, 20.0      # matrix cores busy, HBM idle-ish
+    metrics = {"a:1": {"device": "cuda", "gpu": 3, "gpu_mix": {"compute_frac": 0.9, "source": "hip-events"}},
+               "b:2": {"device": "cuda", "gpu": 4, "gpu_mix": {"compute_frac": 0.1, "source": "hip-events"}}}
+    nxt = Planner().next_plan(JobFeatures(mode="ps", params=3.3e8), inv, _plan(), metrics)
+    assert 0 < nxt.per_rank["a:1"]["cu"] < 256 and "amd-smi" in nxt.reason
+    assert "cu" not in nxt.per_rank.get("b:2", {})
 
 
 def test_busy_cpu_parameter_server_gets_more_cores_up_to_the_cap():
@@ -108,3 +151,28 @@ def test_meter_reads_hip_event_times_without_synchronising(cuda):
     assert s["source"] == "hip-events" and s["phases"] == 6 and s["gpu_s"] > 0
     # 4 x 1.1 TFLOP of MFMA work vs 4 x 512 MB of streaming: mostly compute
     assert 0.5 < s["compute_frac"] < 1.0
+
+
+@pytest.mark.gpu
+def test_cu_probe_separates_matrix_core_work_from_streaming(cuda):
+    """The CU-sensitivity probe on real kernels: GEMMs on half the CUs take ~2x longer (s near
+    1), a streaming update barely changes (s near 0) -- measured, not labelled."""
+    out = {}
+    a = torch.randn(8192, 8192, device=cuda, dtype=torch.bfloat16)
+    x = torch.randn(256 << 20, device=cuda)
+    work = {"gemm": lambda: [a @ a for _ in range(4)], "stream": lambda: [x.mul_(1.0001) for _ in range(4)]}
+    for name, fn in work.items():
+        m = KernelMixMeter(cuda, window_s=60, probe_every=0)
+        for i in range(8):
+            with m.phase("compute", probe=m.probe_due(i) if i in (4, 6) else False):
+                fn()
+            if i == 3:
+                m.request_probe()
+            if i == 5:
+                m.request_probe()
+        torch.cuda.synchronize(cuda)
+        out[name] = m.cu_sensitivity()
+    print(f"\n[cu-probe] {out}")
+    assert out["gemm"]["probes"] == 2 and out["stream"]["probes"] == 2
+    assert out["gemm"]["s"] > 0.6, out
+    assert out["stream"]["s"] < 0.25, out
