@@ -236,6 +236,9 @@ def _drill(args, res: dict, n: int) -> dict:
             "replacement_from_standby": d.get("replacement_from_standby"),
             "step_s_before_fault": d.get("step_s_before_fault"),
             "step_s_before_fault_clock": d.get("step_s_before_fault_clock"),
+            "gpu_steps_before_fault": d.get("gpu_steps_before_fault"),
+            "step_s_steady": round(res["ms_per_step"] / 1e3, 4),    # the throughput run's step
+            "standby_slab_gb": d.get("standby_slab_gb"),
             "first_step": d.get("first_step"),
             "phases": {k: b.get(k) for k in ("detect_s", "abort_s", "epoch_formed_s", "replacement_spawn_s",
                                              "replacement_joined_s", "comm_ready_s", "state_synced_s",

@@ -169,6 +169,69 @@ def _warm_one(kv, name: str, gpu: int, spec) -> None:
         kv.set(f"standby/warm/{name}/gpu{gpu}", json.dumps({"error": str(e)[:200]}))
 
 
+SLABS: dict = {}   # GPU -> bytes of HBM this parked standby holds reserved in its caching allocator
+
+
+def _reserve_slab(kv, name: str, gpu: int, slot: str) -> None:
+    """Once ``slot``'s worker has run its first step (it published its step's HBM need): reserve
+    what the GPU still has free, less a margin the worker keeps for itself, in THIS process's
+    caching allocator on the stream the replacement will compute on (WARM_STREAMS) -- allocated
+    and freed, so it stays cached.
+
+    Why: a replacement's first step allocates its activations right after the dead worker died,
+    and fresh HBM is slow to hand out then (the r06 drill: 0.8-2.7 s per micro-batch that needed
+    new segments vs 0.35-0.7 s steady; profiles/r06_ttr_first_step.md).  Blocks carved from a
+    slab reserved while everything was calm cost nothing.  The slab is at most the worker's
+    published need, and ``EDL_STANDBY_SLAB_MARGIN_GB`` (default 12) stays free for the worker.
+    ``EDL_STANDBY_SLAB=0`` turns it off."""
+    import torch
+    if os.environ.get("EDL_STANDBY_SLAB", "1") == "0" or gpu in SLABS:
+        return
+    from easydl_amd.utils import vram
+    act, _, _ = vram.read_act(kv, slot)
+    if not act:
+        return
+    dev = torch.device("cuda", gpu)
+    margin = int(float(os.environ.get("EDL_STANDBY_SLAB_MARGIN_GB", 12)) * 2**30)
+    free, _ = torch.cuda.mem_get_info(dev)
+    want = min(act, free - margin) // (2 << 20) * (2 << 20)
+    SLABS[gpu] = 0
+    if want < (2 << 30):
+        kv.set(f"standby/slab/{name}/gpu{gpu}", json.dumps({"gb": 0, "free_gb": round(free / 2**30, 1)}))
+        return
+    st = WARM_STREAMS.get(gpu)
+    t0 = time.perf_counter()
+    try:
+        with torch.cuda.device(dev), torch.cuda.stream(st) if st is not None else _Null():
+            buf = torch.empty(want, dtype=torch.uint8, device=dev)
+            del buf
+        SLABS[gpu] = want
+    except RuntimeError as e:     # (out of memory: the worker grew meanwhile) -- an optimisation only
+        print(f"standby {name}: slab of {want / 2**30:.1f} GB on GPU {gpu} failed: {e}", file=sys.stderr)
+    kv.set(f"standby/slab/{name}/gpu{gpu}", json.dumps({"gb": round(SLABS[gpu] / 2**30, 1),
+                                                        "free_gb": round(free / 2**30, 1),
+                                                        "s": round(time.perf_counter() - t0, 3)}))
+    print(f"standby {name}: GPU {gpu}: slab {SLABS[gpu] / 2**30:.1f} GB reserved ({free / 2**30:.1f} GB were "
+          f"free) in {time.perf_counter() - t0:.3f} s", file=sys.stderr, flush=True)
+
+
+def _release_slabs(keep: int | None) -> None:
+    """Takeover of ``keep``'s GPU: the slabs on every other GPU go back to the driver."""
+    import torch
+    for g in [g for g in SLABS if g != keep]:
+        if SLABS.pop(g):
+            with torch.cuda.device(g):
+                torch.cuda.empty_cache()
+
+
+class _Null:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
 def _import_vram(kv, held: dict) -> None:
     """Map (IPC) the state buffers every worker published; keep them referenced while parked."""
     from easydl_amd.utils import vram
@@ -229,6 +292,7 @@ def main() -> int:
     warmed: set[int] = set()       # GPUs this standby has run (or is running) its warm-up step on
     warming: list = []             # their warm-up threads
     late: dict = {}                # GPU -> warm spec, waiting for a window (its worker already trains)
+    warm_thread: dict = {}         # GPU -> its warm-up thread (a slab is reserved once it is done)
     requested: set = set()         # GPUs of the window request filed
     req_id = 0
     warm_on = os.environ.get("EDL_STANDBY_WARMUP", "1") != "0"
@@ -267,6 +331,13 @@ def main() -> int:
                                      name=f"warm-gpu{h['gpu']}")
                 t.start()
                 warming.append(t)
+                warm_thread[h["gpu"]] = t
+            for slot, h in sorted(held.items()):
+                # the worker has trained a step and this GPU's warm-up is over: reserve the slab
+                g = h["gpu"] if h else None
+                if (g is not None and g in warmed and g not in SLABS and g not in late
+                        and not (warm_thread.get(g) is not None and warm_thread[g].is_alive())):
+                    _reserve_slab(kv, name, g, slot)
             if late and set(late) != requested:
                 requested = set(late)
                 req_id += 1
@@ -277,6 +348,8 @@ def main() -> int:
                                          name=f"warm-gpu{g}")
                     t.start()
                     warming.append(t)
+                    warm_thread[g] = t
+                    SLABS.pop(g, None)     # (its warm-up empties the cache: reserve again after it)
         if premap and time.monotonic() > next_scan:
             from easydl_amd.ckpt.manager import premap_job_segments
             mapped = premap_job_segments(job)
@@ -293,6 +366,8 @@ def main() -> int:
     if gpu is not None and int(gpu) in WARM_STREAMS:
         import torch
         torch.cuda.set_stream(WARM_STREAMS[int(gpu)])   # the stream the warm-up ran on (its hipBLASLt workspace)
+    if SLABS:
+        _release_slabs(int(gpu) if gpu is not None else None)   # this GPU's slab feeds the first step
     # the parked loop's variables still name the imported state ("h" is the last slot's record,
     # "t" a warm-up thread): this frame lives as long as the role it runs, so without this the
     # dead worker's HBM would stay mapped after the trainer re-homed its state into its own

@@ -136,6 +136,8 @@ def main(args) -> int:
         "step_s_before_fault": (round(gpu[len(gpu) // 2], 4) if gpu else
                                 round(gaps[len(gaps) // 2], 4) if gaps else None),
         "step_s_before_fault_clock": "gpu" if gpu else "host",
+        # every GPU-timed step before the fault (they include the first snapshots' set-up)
+        "gpu_steps_before_fault": [round(x, 4) for x in gpu],
         "first_step": _first_step(ev, fault, ttr),
         "time_to_regrow_s": _regrow(ev, fault, n),
         "step_s_median": round(steady[len(steady) // 2], 5) if steady else None,
@@ -151,12 +153,25 @@ def main(args) -> int:
                          for e in ev if e["kind"] == "final_state"],
         "worlds_seen": sorted({w for w in worlds if w}), "run_dir": run_dir,
         "timeline": _timeline(ev, fault, ttr),
+        "standby_slab_gb": _slab_gb(run_dir),
     }
     print(json.dumps(out), flush=True)
     unlink_job_segments(job_name)
     if os.environ.get("EDL_TTR_KEEP") != "1":
         shutil.rmtree(run_dir, ignore_errors=True)
     return 0 if rc == 0 and ttr else 1
+
+
+def _slab_gb(run_dir: str) -> float | None:
+    """HBM the parked standby had reserved for the replacement's first step (its log line)."""
+    import glob
+    import re
+    for f in glob.glob(os.path.join(run_dir, "logs", "*standby*.log")):
+        with open(f, errors="replace") as fh:
+            m = re.findall(r"slab ([0-9.]+) GB", fh.read())
+        if m:
+            return float(m[-1])
+    return None
 
 
 def _rel(e, fault):

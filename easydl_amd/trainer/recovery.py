@@ -190,7 +190,10 @@ class RecoveryMixin:
         persistent = sum(t.untyped_storage().nbytes() for t in self.vram_state_tensors().values()
                          if t.data_ptr() not in adopted)
         act = max(0, torch.cuda.max_memory_reserved(self.device) - persistent)
-        vram.publish_act(self.kv, f"{self.ctx.role}{self.ctx.index}", act, self.micro_batch)
+        # what stays allocated between steps beyond the state (transposed-weight caches, workspaces):
+        # a split micro-batch does not shrink it
+        fixed = min(act, max(0, torch.cuda.memory_allocated(self.device) - persistent))
+        vram.publish_act(self.kv, f"{self.ctx.role}{self.ctx.index}", act, self.micro_batch, fixed)
         self._maybe_shadow(act)
 
     def _maybe_shadow(self, act: int) -> None:
@@ -378,10 +381,10 @@ class RecoveryMixin:
         if (self.device.type != "cuda" or self.tp > 1 or not vram.adopted_any()
                 or getattr(self, "kv", None) is None or os.environ.get("EDL_RECOVERY_SPLIT", "1") == "0"):
             return
-        need, mbs = vram.read_act(self.kv, f"{self.ctx.role}{self.ctx.index}")
+        need, mbs, fixed = vram.read_act(self.kv, f"{self.ctx.role}{self.ctx.index}")
         if not need or mbs != self.micro_batch:
             return
-        self._act_need = need
+        self._act_need, self._act_fixed = need, fixed
         avail = self._hbm_avail()
         if avail >= need * 1.05:
             return
@@ -405,7 +408,7 @@ class RecoveryMixin:
     def _apply_memory_plan(self, avail: int) -> tuple[int, int]:
         """Set the split and the recomputed layer count for ``avail`` bytes of free HBM."""
         split, rc = plan_memory(self._act_need, avail, self.micro_batch, self._recompute_layers_total(),
-                                self._memory_margin())
+                                self._memory_margin(), fixed=getattr(self, "_act_fixed", 0))
         self._mb_split, self._mb_plan = split, (split, rc)
         cfg = getattr(self.model, "cfg", None)
         if rc > 0:
@@ -422,15 +425,24 @@ class RecoveryMixin:
         if self._mb_recompute is not None:
             self.model.cfg.recompute, self._mb_recompute = self._mb_recompute, None
 
-    def _replan_memory(self, mb: int) -> None:
+    def _replan_memory(self, mb: int, grow: bool = True) -> None:
         """Before micro-batch ``mb`` of a memory-limited step: full micro-batches if the memory
-        is back, else the plan for what is free now."""
+        is back, else the plan for what is free now.  ``grow=False`` (inside a step): the plan
+        may only shrink -- pieces that grow need new, larger allocator segments, and fresh HBM
+        right after the driver's reclaim costs seconds to hand out (r06 drill: a mid-step return
+        to full micro-batches took 2.7 s instead of 0.7 s, profiles/r06_ttr_first_step.md)."""
         avail = self._hbm_avail()
+        before = self._mb_plan
         if avail >= self._act_need * 1.05:
+            if not grow:
+                return
             self.events.emit("memory_restored", step=self.step, mb=mb, avail_gb=round(avail / 2**30, 1))
             self._restore_full_batches()
             return
-        before = self._mb_plan
+        split, rc = plan_memory(self._act_need, avail, self.micro_batch, self._recompute_layers_total(),
+                                self._memory_margin(), fixed=getattr(self, "_act_fixed", 0))
+        if not grow and (split < before[0] or rc < before[1]):
+            return
         split, rc = self._apply_memory_plan(avail)
         if (split, rc) != before:
             self.events.emit("memory_replanned", step=self.step, mb=mb, split=split, recompute_layers=rc,
@@ -469,7 +481,7 @@ class RecoveryMixin:
         before every micro-batch (the pieces keep their micro-batch's index)."""
         for n, (mb, idx) in enumerate(mbs):
             if self._mb_limited:
-                self._replan_memory(mb)
+                self._replan_memory(mb, grow=n == 0)
             k = self._mb_split
             idx = list(idx)
             step = -(-len(idx) // k) if k > 1 else max(1, len(idx))
@@ -655,23 +667,29 @@ class RecoveryMixin:
 
 
 def plan_memory(need: int, avail: int, mbs: int, layers: int = 0, margin: float = 1.15,
-                layer_frac: float = 0.9) -> tuple[int, int]:
+                layer_frac: float = 0.9, fixed: int = 0) -> tuple[int, int]:
     """(split, recompute_layers) for a step whose full micro-batch of ``mbs`` samples needs
-    ``need`` bytes of activations when ``avail`` bytes are free.
+    ``need`` bytes beyond the state -- ``fixed`` of them whatever the micro-batch (transposed-
+    weight caches, workspaces), the rest activations that scale with it -- when ``avail`` bytes
+    are free.
 
     * enough memory: (1, 0);
-    * else the smallest split ``d`` (a divisor of ``mbs``) with ``need / d * margin <= avail``;
+    * else the smallest split ``d`` (a divisor of ``mbs``) whose piece fits:
+      ``(fixed + (need - fixed) / d) * margin <= avail``;
     * else one sample per piece, with the fewest recomputed layers that fit: recomputing ``r`` of
       ``layers`` layers frees about ``r / layers`` of the ``layer_frac`` share of a sample's
       activations that the layers hold (the rest: embedding, logits, loss).  ``layers == 0``
       (no recompute knob): (mbs, 0) and the allocator waits for the memory."""
     if avail >= need * 1.05:
         return 1, 0
+    fixed = max(0, min(fixed, need))
+    scaling = need - fixed
     for d in range(2, mbs + 1):
-        if mbs % d == 0 and need / d * margin <= avail:
+        if mbs % d == 0 and (fixed + scaling / d) * margin <= avail:
             return d, 0
     if layers <= 0:
         return mbs, 0
-    piece = need / max(1, mbs) * margin
-    r = math.ceil(layers * (1.0 - avail / piece) / layer_frac) if piece > 0 else 0
+    sample = scaling / max(1, mbs)
+    room = avail / margin - fixed          # what one sample's activations may take
+    r = math.ceil(layers * (1.0 - room / sample) / layer_frac) if sample > 0 else 0
     return mbs, max(1, min(layers, r))

@@ -46,6 +46,7 @@ class KernelMixMeter:
         self._probe_stream = None
         self._probe_cus = (0, 0)             # (CUs of the probe stream, CUs of the rank)
         self._probe_next = False             # one probe requested (runtime plan)
+        self._n_compute = 0                  # compute phases timed on the rank's own stream
 
     def request_probe(self) -> None:
         """Probe at the next compute phase (the Brain's ``cu_probe`` runtime knob)."""
@@ -54,7 +55,7 @@ class KernelMixMeter:
     def probe_due(self, step: int) -> bool:
         """Run this step's compute phase on half the CUs?  Never the first two steps (kernel
         loads, allocator growth), and only once normal phases exist to compare against."""
-        if not self.cuda or step < 2 or not any(c == "compute" for _, c, _ in self._done):
+        if not self.cuda or step < 2 or self._n_compute < 2:
             return False
         if self._probe_next:
             return True
@@ -101,6 +102,8 @@ class KernelMixMeter:
                 if torch.cuda.memory_reserved(self.device) > 0.4 * total:
                     torch.cuda.empty_cache()
             return
+        if cls == "compute":
+            self._n_compute += 1
         if not self.cuda:
             t0 = time.perf_counter()
             try:

@@ -149,17 +149,20 @@ def roster(kv) -> list[str]:
     return [n for n in (kv.get_str("standby/roster") or "").split(",") if n]
 
 
-def publish_act(kv, slot: str, act_bytes: int, micro_batch: int) -> None:
-    """HBM one training step of ``slot`` needs beyond its persistent state."""
-    kv.set(f"vram/act/{slot}", json.dumps({"act_bytes": int(act_bytes), "micro_batch": int(micro_batch)}))
+def publish_act(kv, slot: str, act_bytes: int, micro_batch: int, fixed_bytes: int = 0) -> None:
+    """HBM one training step of ``slot`` needs beyond its persistent state; ``fixed_bytes`` of it
+    do not shrink with a smaller micro-batch (transposed-weight caches, library workspaces)."""
+    kv.set(f"vram/act/{slot}", json.dumps({"act_bytes": int(act_bytes), "micro_batch": int(micro_batch),
+                                           "fixed_bytes": int(fixed_bytes)}))
 
 
-def read_act(kv, slot: str) -> tuple[int, int]:
+def read_act(kv, slot: str) -> tuple[int, int, int]:
+    """(act bytes, micro-batch, fixed bytes) ``slot``'s worker published; zeros if none."""
     raw = kv.get_str(f"vram/act/{slot}")
     if raw is None:
-        return 0, 0
+        return 0, 0, 0
     d = json.loads(raw)
-    return int(d.get("act_bytes", 0)), int(d.get("micro_batch", 0))
+    return int(d.get("act_bytes", 0)), int(d.get("micro_batch", 0)), int(d.get("fixed_bytes", 0))
 
 
 def trained(kv, slot: str) -> bool:

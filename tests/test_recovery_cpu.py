@@ -33,6 +33,17 @@ def test_plan_memory_recomputes_only_as_many_layers_as_needed():
     assert plan_memory(need, 40 * GB, 2, 0) == (2, 0)                # no recompute knob
 
 
+def test_plan_memory_counts_the_part_a_split_does_not_shrink():
+    # 97.8 GB of which 14 GB stay whatever the micro-batch (transposed-weight caches): a half
+    # needs 14 + 41.9 GB, not 48.9 GB -- with 60 GB free that still fits, with 55 GB it does not
+    need, fixed = int(97.8 * GB), 14 * GB
+    assert plan_memory(need, 68 * GB, 2, 32, fixed=fixed) == (2, 0)
+    split, r = plan_memory(need, 55 * GB, 2, 32, fixed=fixed)
+    assert split == 2 and r >= 1
+    split0, r0 = plan_memory(need, 55 * GB, 2, 32)
+    assert r > r0 or r0 == 0                                         # the fixed part costs layers
+
+
 class _Host(RecoveryMixin):
     """The mixin's piece generator on its own (no trainer)."""
 
