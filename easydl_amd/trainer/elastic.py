@@ -928,6 +928,7 @@ class ElasticTrainer(RecoveryMixin):
                         if self._marks is not None:
                             self._marks.done(self.step + 1, torch.cuda.current_stream(self.device)
                                              if self.device.type == "cuda" else None)
+                        self._mark_gpu_step_end()   # (on the update's stream)
                     if self._phases and ok:
                         # host-side split of one step (EDL_STEP_PHASES=1): enqueue of the micro-batches,
                         # wait for the GPU (compute + all-reduce), commit round, snapshot fence, optimizer
@@ -987,20 +988,31 @@ class ElasticTrainer(RecoveryMixin):
     def _mark_gpu_step_start(self) -> None:
         """Record a GPU event where this step starts on the compute stream.  At world 1 the host
         runs ahead of the GPU (no per-step drain, _sync_point), so host timestamps are enqueue
-        times; GPU step durations (start of step k to start of step k+1, read without blocking)
-        and the fault injector's ``after_ms`` (utils/fault.py) use these events instead."""
+        times; GPU step durations and the fault injector's ``after_ms`` (utils/fault.py) use
+        these events instead."""
         if self.device.type != "cuda":
             return
         ev = torch.cuda.Event(enable_timing=True)
         ev.record(torch.cuda.current_stream(self.device))
         self._step_ev = ev
+        self._gpu_step_evs.append([self.step, ev, None])
+        del self._gpu_step_evs[:-64]
+
+    def _mark_gpu_step_end(self) -> None:
+        """The step's update is enqueued (current stream: the update's): its end event.  A GPU
+        step = start of its forward -> end of its update, read without blocking once both have
+        completed -- idle gaps BETWEEN steps (a host busy pinning snapshot memory) do not count."""
+        if self.device.type != "cuda" or not self._gpu_step_evs or self._gpu_step_evs[-1][2] is not None:
+            return
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record(torch.cuda.current_stream(self.device))
+        self._gpu_step_evs[-1][2] = ev
         q = self._gpu_step_evs
-        q.append((self.step, ev))
-        while len(q) >= 2 and q[1][1].query():
-            (s0, e0), (_, e1) = q[0], q[1]
+        while q and q[0][2] is not None and q[0][2].query():
+            s0, e0, e1 = q.pop(0)
             self._gpu_last = (s0 + 1, e0.elapsed_time(e1) / 1000.0)
+        while q and q[0][2] is None and len(q) > 1:    # a dropped step: no end event
             q.pop(0)
-        del q[:-64]
 
     def _gpu_step_time(self) -> dict:
         """Newest completed GPU step duration for the step_done event (empty on the CPU)."""

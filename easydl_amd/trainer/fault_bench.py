@@ -118,8 +118,8 @@ def main(args) -> int:
     done_ts = [e["ts"] for e in ev if e["kind"] == "step_done" and (fault is None or e["ts"] < fault["ts"])]
     gaps = sorted(b - a for a, b in zip(done_ts, done_ts[1:]))[-8:]   # the last steps before the fault
     steady = sorted(b - a for a, b in zip(done_ts[2:], done_ts[3:]))     # every step before it, first 3 out
-    # GPU step durations (start of step k -> start of step k+1 on the compute stream, ElasticTrainer
-    # _mark_gpu_step_start): at world 1 the host enqueues ahead of the GPU, so host gaps are not steps
+    # GPU step durations (start of step k's forward -> end of its update, HIP events, ElasticTrainer
+    # _mark_gpu_step_start/_end): at world 1 the host enqueues ahead of the GPU, so host gaps are not steps
     gpu = sorted(e["gpu_s"] for e in ev if e["kind"] == "step_done" and e.get("gpu_s") is not None
                  and (fault is None or e["ts"] < fault["ts"]) and int(e.get("gpu_step", 0)) >= 2)
     out = {
@@ -136,7 +136,7 @@ def main(args) -> int:
         "step_s_before_fault": (round(gpu[len(gpu) // 2], 4) if gpu else
                                 round(gaps[len(gaps) // 2], 4) if gaps else None),
         "step_s_before_fault_clock": "gpu" if gpu else "host",
-        # every GPU-timed step before the fault (they include the first snapshots' set-up)
+        # every GPU-timed step before the fault
         "gpu_steps_before_fault": [round(x, 4) for x in gpu],
         "first_step": _first_step(ev, fault, ttr),
         "time_to_regrow_s": _regrow(ev, fault, n),

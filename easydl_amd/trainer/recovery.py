@@ -488,6 +488,9 @@ class RecoveryMixin:
             parts = [idx[i:i + step] for i in range(0, len(idx), step)] or [idx]
             for j, part in enumerate(parts):
                 yield mb, part, n == len(mbs) - 1 and j == len(parts) - 1
+                # the step-invariant part (transposed-weight caches, workspaces) is resident after
+                # the first piece: later plans count only what scales with the piece
+                self._act_fixed = 0
 
     def _hbm_resume_step(self) -> int | None:
         """Step K if this process adopted a dead worker's HBM (utils/vram.py) whose step marks

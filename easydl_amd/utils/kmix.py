@@ -138,6 +138,7 @@ class KernelMixMeter:
     def cu_sensitivity(self) -> dict | None:
         """``{"s", "t_half_ms", "t_full_ms", "probes", "cus"}`` from the newest probes against
         the median compute phase of the window; None before a probe completed."""
+        self.collect()
         full = [sec for _, c, sec in self._done if c == "compute"]
         if not self._probes or not full:
             return None
