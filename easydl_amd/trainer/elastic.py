@@ -163,6 +163,7 @@ class ElasticTrainer(RecoveryMixin):
         self._step_ev = None         # GPU event at the current step's start (fault after_ms counts from it)
         self._gpu_step_evs = []      # (step, start event) not yet paired: GPU step durations
         self._gpu_last = None        # (step, seconds) newest GPU-timed step
+        self._snap_steps: set = set()   # steps whose update waited for a snapshot copy (GPU step clock)
 
     def request_stop(self) -> None:
         """End ``fit`` after the current step (from ``on_step``).  Every rank must ask at the
@@ -945,6 +946,9 @@ class ElasticTrainer(RecoveryMixin):
                     self.history.append(rec)
                     self.events.emit("step_done", step=self.step, epoch=self.comm.epoch,
                                      world=self.comm.world_size, dt=round(rec["dt"], 4), **self._gpu_step_time())
+                    if self.checkpoint is not None and self.step % max(1, int(getattr(self.checkpoint, "interval", 0)
+                                                                            or 1)) == 0:
+                        self._snap_steps.add(self.step + 1)   # its update waits for this snapshot's copy
                     self.metrics.record(self.step, rec["dt"], samples=self.global_batch,
                                         tokens=self.global_batch * self.tokens_per_sample, world=self.comm.world_size,
                                         loss=None, extra=self._metrics_extra)
@@ -1015,10 +1019,15 @@ class ElasticTrainer(RecoveryMixin):
             q.pop(0)
 
     def _gpu_step_time(self) -> dict:
-        """Newest completed GPU step duration for the step_done event (empty on the CPU)."""
+        """Newest completed GPU step duration for the step_done event (empty on the CPU); a step
+        whose update waited for an in-memory snapshot's copy is flagged."""
         if self._gpu_last is None:
             return {}
-        return {"gpu_step": self._gpu_last[0], "gpu_s": round(self._gpu_last[1], 5)}
+        k = self._gpu_last[0]
+        out = {"gpu_step": k, "gpu_s": round(self._gpu_last[1], 5)}
+        if k in self._snap_steps:
+            out["gpu_after_snapshot"] = True
+        return out
 
     def _metrics_extra(self) -> dict:
         from easydl_amd.utils.metrics import cu_count

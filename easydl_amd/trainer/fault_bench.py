@@ -120,8 +120,12 @@ def main(args) -> int:
     steady = sorted(b - a for a, b in zip(done_ts[2:], done_ts[3:]))     # every step before it, first 3 out
     # GPU step durations (start of step k's forward -> end of its update, HIP events, ElasticTrainer
     # _mark_gpu_step_start/_end): at world 1 the host enqueues ahead of the GPU, so host gaps are not steps
-    gpu = sorted(e["gpu_s"] for e in ev if e["kind"] == "step_done" and e.get("gpu_s") is not None
-                 and (fault is None or e["ts"] < fault["ts"]) and int(e.get("gpu_step", 0)) >= 2)
+    timed = {int(e["gpu_step"]): (e["gpu_s"], bool(e.get("gpu_after_snapshot"))) for e in ev
+             if e["kind"] == "step_done" and e.get("gpu_s") is not None and (fault is None or e["ts"] < fault["ts"])
+             and int(e.get("gpu_step", 0)) >= 2}
+    # the median excludes steps whose update waited for a snapshot's device-to-host copy (the first
+    # snapshots also create and pin their segments: seconds)
+    gpu = sorted(v for v, snap in timed.values() if not snap) or sorted(v for v, _ in timed.values())
     out = {
         "metric": "time-to-recover after SIGKILL of one worker (Llama elastic DDP, local operator)",
         "value": None if not ttr else ttr["ttr_s"], "unit": "s", "higher_is_better": False,
@@ -137,7 +141,8 @@ def main(args) -> int:
                                 round(gaps[len(gaps) // 2], 4) if gaps else None),
         "step_s_before_fault_clock": "gpu" if gpu else "host",
         # every GPU-timed step before the fault
-        "gpu_steps_before_fault": [round(x, 4) for x in gpu],
+        "gpu_steps_before_fault": {str(k): {"s": round(v, 4), "after_snapshot": snap}
+                                   for k, (v, snap) in sorted(timed.items())},
         "first_step": _first_step(ev, fault, ttr),
         "time_to_regrow_s": _regrow(ev, fault, n),
         "step_s_median": round(steady[len(steady) // 2], 5) if steady else None,

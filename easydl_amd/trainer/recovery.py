@@ -490,7 +490,9 @@ class RecoveryMixin:
                 yield mb, part, n == len(mbs) - 1 and j == len(parts) - 1
                 # the step-invariant part (transposed-weight caches, workspaces) is resident after
                 # the first piece: later plans count only what scales with the piece
-                self._act_fixed = 0
+                if getattr(self, "_act_fixed", 0):
+                    self._act_need = max(0, self._act_need - self._act_fixed)
+                    self._act_fixed = 0
 
     def _hbm_resume_step(self) -> int | None:
         """Step K if this process adopted a dead worker's HBM (utils/vram.py) whose step marks
