@@ -968,6 +968,109 @@ __device__ __forceinline__ void mfma_d_fence(f32x16 (&x)[2], f32x16 (&y)[2]) {
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 4" : "+v"(x[0]), "+v"(x[1]), "+v"(y[0]), "+v"(y[1]));
 }
 
+// Software-pipelined form of the slice below (EDL_ATTN_DKDV=64p).  The plain form reads each
+// fragment right before its MFMAs, and the compiler puts an lgkmcnt(0) in front of every MFMA
+// pair: the LDS latency is exposed 40+ times per slice (the ISA of the unmasked loop: 45
+// s_waitcnt for 64 MFMAs; the kernel ran at 36 % of the MFMA peak, 0.9 PF/s).  Here
+//  * S = Q K^T and dP = dO V^T run in ONE k-loop: 4 fragment reads + 4 MFMAs per k-step, the
+//    next k-step's 4 reads issued before this step's MFMAs (128 MFMA cycles cover them);
+//  * dV += dO^T P and dK += Q^T dS read their transposed fragments one MFMA pair ahead;
+// each step is a sched_barrier region, so the reads stay ahead of the MFMAs they feed.
+template <bool MASK, bool CAUSAL, int D>
+__device__ __forceinline__ void dkdv64p_slice(const char* Qs, const char* Ds, const float* NL,
+                                              const float* DL, int rb, const bf16x8 (&kf)[2][D / 16],
+                                              const char* Vw, f32x16 (&dka)[2][D / 32], f32x16 (&dva)[2][D / 32],
+                                              int qs0, int key0, int S,
+                                              float sl2, int lane) {
+  const int h = lane >> 5, l31 = lane & 31;
+  f32x16 sa[2], dp[2];
+  uint32_t vo = (uint32_t)(uintptr_t)(lds_char*)Vw;
+  asm volatile("" : "+v"(vo));
+  const lds_char* Vl = (const lds_char*)(uintptr_t)vo;
+  constexpr int NS = D / 16;
+  bf16x8 fq[2], fd[2], fv0[2], fv1[2];
+  auto rd = [&](int s, int b) {
+    fq[b] = row_read<D>(Qs, rb + l31, s, h);
+    fd[b] = row_read<D>(Ds, rb + l31, s, h);
+    fv0[b] = *(lds_bf16x8*)(Vl + swzd<D>(l31, 2 * s + h));
+    fv1[b] = *(lds_bf16x8*)(Vl + swzd<D>(32 + l31, 2 * s + h));
+  };
+  rd(0, 0);
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const int b = s & 1;
+    if (s + 1 < NS) rd(s + 1, b ^ 1);
+    __builtin_amdgcn_sched_barrier(0);
+    if (s == 0) {
+      mfma_v_first(sa[0], fq[b], kf[0][s]);
+      mfma_v_first(sa[1], fq[b], kf[1][s]);
+      mfma_v_first(dp[0], fd[b], fv0[b]);
+      mfma_v_first(dp[1], fd[b], fv1[b]);
+    } else {
+      mfma_v(sa[0], fq[b], kf[0][s]);
+      mfma_v(sa[1], fq[b], kf[1][s]);
+      mfma_v(dp[0], fd[b], fv0[b]);
+      mfma_v(dp[1], fd[b], fv1[b]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  mfma_d_fence(sa, dp);
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const f32x4 nl = *reinterpret_cast<const f32x4*>(NL + rb + 8 * g + 4 * h);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) sa[t][4 * g + e] = fast_exp2(__builtin_fmaf(sa[t][4 * g + e], sl2, nl[e]));
+    }
+  }
+  if (MASK) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int mykey = key0 + 32 * t + l31;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int qi = qs0 + acc_row(i, h);
+        if (qi >= S || mykey >= S || (CAUSAL && mykey > qi)) sa[t][i] = 0.f;
+      }
+    }
+  }
+  const bf16x8 p[2][2] = {{acc_to_b(sa[0], 0), acc_to_b(sa[0], 1)}, {acc_to_b(sa[1], 0), acc_to_b(sa[1], 1)}};
+  // dS = P (dP - delta), computed before the dV MFMAs so the dK loop below reads only LDS
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const f32x4 dl = *reinterpret_cast<const f32x4*>(DL + rb + 8 * g + 4 * h);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) dp[t][4 * g + e] = sa[t][4 * g + e] * (dp[t][4 * g + e] - dl[e]);
+    }
+  }
+  const bf16x8 ds[2][2] = {{acc_to_b(dp[0], 0), acc_to_b(dp[0], 1)}, {acc_to_b(dp[1], 0), acc_to_b(dp[1], 1)}};
+  constexpr int NT = 2 * (D / 32);     // (s2, dt) pairs
+  bf16x8 ta[2];
+  ta[0] = tr_read<D>(Ds, rb + 4 * h, 0, lane);
+#pragma unroll
+  for (int i = 0; i < NT; ++i) {
+    const int s2 = i / (D / 32), dt = i % (D / 32);
+    if (i + 1 < NT) ta[(i + 1) & 1] = tr_read<D>(Ds, rb + 16 * ((i + 1) / (D / 32)) + 4 * h, (i + 1) % (D / 32), lane);
+    __builtin_amdgcn_sched_barrier(0);
+    dva[0][dt] = mfma(ta[i & 1], p[0][s2], dva[0][dt]);
+    dva[1][dt] = mfma(ta[i & 1], p[1][s2], dva[1][dt]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  ta[0] = tr_read<D>(Qs, rb + 4 * h, 0, lane);
+#pragma unroll
+  for (int i = 0; i < NT; ++i) {
+    const int s2 = i / (D / 32), dt = i % (D / 32);
+    if (i + 1 < NT) ta[(i + 1) & 1] = tr_read<D>(Qs, rb + 16 * ((i + 1) / (D / 32)) + 4 * h, (i + 1) % (D / 32), lane);
+    __builtin_amdgcn_sched_barrier(0);
+    dka[0][dt] = mfma(ta[i & 1], ds[0][s2], dka[0][dt]);
+    dka[1][dt] = mfma(ta[i & 1], ds[1][s2], dka[1][dt]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
 template <bool MASK, bool CAUSAL, int D>
 __device__ __forceinline__ void dkdv64_slice(const char* Qs, const char* Ds, const float* NL,
                                              const float* DL, int rb, const bf16x8 (&kf)[2][D / 16],
@@ -1081,7 +1184,7 @@ __device__ __forceinline__ void store_accT_f32(float* rowp, const f32x16 (&acc)[
 // fewer than ~2 workgroups per CU the GQA group's query heads are split over
 // `gsplit` workgroups that write fp32 partials to `ws`, summed by
 // attn_dkdv_reduce_kernel.
-template <bool CAUSAL, int D>
+template <bool CAUSAL, int D, bool PF = false>
 __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv64_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
     const bf16_t* __restrict__ dout, const float* __restrict__ lse, const float* __restrict__ delta,
@@ -1175,8 +1278,12 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv64_kernel(
         for (int sub = 0; sub < QT / 32; ++sub) {
           const int qs0 = q0 + 32 * sub;
           if (CAUSAL && qs0 + 31 < key0) continue;  // wave-uniform: every key of the wave is after every query
-          dkdv64_slice<MASK, CAUSAL, D>(Qs, Ds, NL, NL + QT, 32 * sub, kf, Vw, dka, dva, qs0, key0, S, scale_log2,
-                                        lane);
+          if constexpr (PF)
+            dkdv64p_slice<MASK, CAUSAL, D>(Qs, Ds, NL, NL + QT, 32 * sub, kf, Vw, dka, dva, qs0, key0, S,
+                                           scale_log2, lane);
+          else
+            dkdv64_slice<MASK, CAUSAL, D>(Qs, Ds, NL, NL + QT, 32 * sub, kf, Vw, dka, dva, qs0, key0, S, scale_log2,
+                                          lane);
         }
         wait_vm();
         __syncthreads();   // also fences the LDS buffers before the next block's first fetch
@@ -1431,13 +1538,20 @@ static int attn_bwd_impl(const void* q, const void* k, const void* v, const void
   }();
   const int xcd64 = dkdv_xcd && (gkv64.x * gkv64.y * gkv64.z) % 8 == 0 ? 1 : 0;
   const bf16_t *bq = (const bf16_t*)q, *bk = (const bf16_t*)k, *bv = (const bf16_t*)v, *bdo = (const bf16_t*)dout;
+  static const bool dkdv_pf = [] {   // software-pipelined slices (dkdv64p_slice)
+    const char* e = getenv("EDL_ATTN_DKDV_PF");
+    return e && atoi(e) == 1;
+  }();
   if (keys_per_wave == 64) {
-    if (causal)
-      attn_bwd_dkdv64_kernel<true, D><<<gkv64, 256, 0, s>>>(bq, bk, bv, bdo, lse, delta, (bf16_t*)dk, (bf16_t*)dv,
-                                                            ws, S, H, KV, gsplit, sl2, scale, dkvs, kvs, xcd64);
-    else
-      attn_bwd_dkdv64_kernel<false, D><<<gkv64, 256, 0, s>>>(bq, bk, bv, bdo, lse, delta, (bf16_t*)dk, (bf16_t*)dv,
-                                                             ws, S, H, KV, gsplit, sl2, scale, dkvs, kvs, xcd64);
+#define EDL_DKDV64(C, P)                                                                                    \
+  attn_bwd_dkdv64_kernel<C, D, P><<<gkv64, 256, 0, s>>>(bq, bk, bv, bdo, lse, delta, (bf16_t*)dk, (bf16_t*)dv, \
+                                                        ws, S, H, KV, gsplit, sl2, scale, dkvs, kvs, xcd64)
+    if (causal) {
+      if (dkdv_pf) EDL_DKDV64(true, true); else EDL_DKDV64(true, false);
+    } else {
+      if (dkdv_pf) EDL_DKDV64(false, true); else EDL_DKDV64(false, false);
+    }
+#undef EDL_DKDV64
     if (gsplit > 1) {
       EDL_LAUNCH_CHECK();
       const int64_t rows = (int64_t)B * S * KV;
