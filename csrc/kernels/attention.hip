@@ -1015,59 +1015,91 @@ __device__ __forceinline__ void dkdv64p_slice(const char* Qs, const char* Ds, co
     __builtin_amdgcn_sched_barrier(0);
   }
   mfma_d_fence(sa, dp);
+  // Softmax terms and dS in four row groups g (accumulator registers 4g .. 4g+3; groups 0-1 feed
+  // the bf16 operands of k-half s2 = 0, groups 2-3 those of s2 = 1).  The dV / dK MFMAs of one
+  // k-half run while the VALU finishes the next: only groups 0-1's exp is exposed.  The order is
+  // spelled out in sched_barrier chunks (MFMA, a quarter group of VALU, MFMA, ...): left to itself
+  // the scheduler put all of a group's VALU after its k-half's MFMAs.
+  auto expq = [&](int g, int t, const f32x4& nl) {   // one quarter: 4 scores of one key tile
 #pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    const f32x4 nl = *reinterpret_cast<const f32x4*>(NL + rb + 8 * g + 4 * h);
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) sa[t][4 * g + e] = fast_exp2(__builtin_fmaf(sa[t][4 * g + e], sl2, nl[e]));
-    }
-  }
-  if (MASK) {
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      const int mykey = key0 + 32 * t + l31;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int qi = qs0 + acc_row(i, h);
-        if (qi >= S || mykey >= S || (CAUSAL && mykey > qi)) sa[t][i] = 0.f;
+    for (int e = 0; e < 4; ++e) {
+      float x = fast_exp2(__builtin_fmaf(sa[t][4 * g + e], sl2, nl[e]));
+      if (MASK) {
+        const int mykey = key0 + 32 * t + l31, qi = qs0 + acc_row(4 * g + e, h);
+        if (qi >= S || mykey >= S || (CAUSAL && mykey > qi)) x = 0.f;
       }
+      sa[t][4 * g + e] = x;
     }
+  };
+  auto dsq = [&](int g, int t, const f32x4& dl) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) dp[t][4 * g + e] = sa[t][4 * g + e] * (dp[t][4 * g + e] - dl[e]);
+  };
+  auto ld4 = [&](const float* base, int g) { return *reinterpret_cast<const f32x4*>(base + rb + 8 * g + 4 * h); };
+  constexpr int NDT = D / 32;
+  auto trq = [&](const char* T, int i) { return tr_read<D>(T, rb + 16 * (i / NDT) + 4 * h, i % NDT, lane); };
+  {
+    const f32x4 n0 = ld4(NL, 0), n1 = ld4(NL, 1);
+    expq(0, 0, n0); expq(0, 1, n0); expq(1, 0, n1); expq(1, 1, n1);
   }
-  const bf16x8 p[2][2] = {{acc_to_b(sa[0], 0), acc_to_b(sa[0], 1)}, {acc_to_b(sa[1], 0), acc_to_b(sa[1], 1)}};
-  // dS = P (dP - delta), computed before the dV MFMAs so the dK loop below reads only LDS
-#pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    const f32x4 dl = *reinterpret_cast<const f32x4*>(DL + rb + 8 * g + 4 * h);
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) dp[t][4 * g + e] = sa[t][4 * g + e] * (dp[t][4 * g + e] - dl[e]);
-    }
-  }
-  const bf16x8 ds[2][2] = {{acc_to_b(dp[0], 0), acc_to_b(dp[0], 1)}, {acc_to_b(dp[1], 0), acc_to_b(dp[1], 1)}};
-  constexpr int NT = 2 * (D / 32);     // (s2, dt) pairs
+  const bf16x8 p0[2] = {acc_to_b(sa[0], 0), acc_to_b(sa[1], 0)};
   bf16x8 ta[2];
-  ta[0] = tr_read<D>(Ds, rb + 4 * h, 0, lane);
+  ta[0] = trq(Ds, 0);
+  f32x4 nq[2] = {ld4(NL, 2), ld4(NL, 3)};
+  EDL_SB();
+  // dV, k-half 0  ||  exp of groups 2-3 (one quarter per MFMA)
 #pragma unroll
-  for (int i = 0; i < NT; ++i) {
-    const int s2 = i / (D / 32), dt = i % (D / 32);
-    if (i + 1 < NT) ta[(i + 1) & 1] = tr_read<D>(Ds, rb + 16 * ((i + 1) / (D / 32)) + 4 * h, (i + 1) % (D / 32), lane);
-    __builtin_amdgcn_sched_barrier(0);
-    dva[0][dt] = mfma(ta[i & 1], p[0][s2], dva[0][dt]);
-    dva[1][dt] = mfma(ta[i & 1], p[1][s2], dva[1][dt]);
-    __builtin_amdgcn_sched_barrier(0);
+  for (int i = 0; i < NDT; ++i) {
+    ta[(i + 1) & 1] = trq(Ds, i + 1);
+    EDL_SB();
+    dva[0][i] = mfma(ta[i & 1], p0[0], dva[0][i]);
+    EDL_SB();
+    expq(2 + (i >> 1), i & 1, nq[i >> 1]);
+    EDL_SB();
+    dva[1][i] = mfma(ta[i & 1], p0[1], dva[1][i]);
+    EDL_SB();
   }
-  ta[0] = tr_read<D>(Qs, rb + 4 * h, 0, lane);
+  const bf16x8 p1[2] = {acc_to_b(sa[0], 1), acc_to_b(sa[1], 1)};
+  f32x4 dq[2] = {ld4(DL, 0), ld4(DL, 1)};
+  EDL_SB();
+  // dV, k-half 1  ||  dS of groups 0-1
 #pragma unroll
-  for (int i = 0; i < NT; ++i) {
-    const int s2 = i / (D / 32), dt = i % (D / 32);
-    if (i + 1 < NT) ta[(i + 1) & 1] = tr_read<D>(Qs, rb + 16 * ((i + 1) / (D / 32)) + 4 * h, (i + 1) % (D / 32), lane);
-    __builtin_amdgcn_sched_barrier(0);
-    dka[0][dt] = mfma(ta[i & 1], ds[0][s2], dka[0][dt]);
-    dka[1][dt] = mfma(ta[i & 1], ds[1][s2], dka[1][dt]);
-    __builtin_amdgcn_sched_barrier(0);
+  for (int i = NDT; i < 2 * NDT; ++i) {
+    ta[(i + 1) & 1] = i + 1 < 2 * NDT ? trq(Ds, i + 1) : trq(Qs, 0);
+    EDL_SB();
+    dva[0][i - NDT] = mfma(ta[i & 1], p1[0], dva[0][i - NDT]);
+    EDL_SB();
+    dsq((i - NDT) >> 1, i & 1, dq[(i - NDT) >> 1]);
+    EDL_SB();
+    dva[1][i - NDT] = mfma(ta[i & 1], p1[1], dva[1][i - NDT]);
+    EDL_SB();
+  }
+  const bf16x8 d0[2] = {acc_to_b(dp[0], 0), acc_to_b(dp[1], 0)};
+  dq[0] = ld4(DL, 2);
+  dq[1] = ld4(DL, 3);
+  EDL_SB();
+  // dK, k-half 0  ||  dS of groups 2-3
+#pragma unroll
+  for (int i = 0; i < NDT; ++i) {
+    ta[(i + 1) & 1] = trq(Qs, i + 1);
+    EDL_SB();
+    dka[0][i] = mfma(ta[i & 1], d0[0], dka[0][i]);
+    EDL_SB();
+    dsq(2 + (i >> 1), i & 1, dq[i >> 1]);
+    EDL_SB();
+    dka[1][i] = mfma(ta[i & 1], d0[1], dka[1][i]);
+    EDL_SB();
+  }
+  const bf16x8 d1[2] = {acc_to_b(dp[0], 1), acc_to_b(dp[1], 1)};
+  EDL_SB();
+  // dK, k-half 1
+#pragma unroll
+  for (int i = NDT; i < 2 * NDT; ++i) {
+    if (i + 1 < 2 * NDT) ta[(i + 1) & 1] = trq(Qs, i + 1);
+    EDL_SB();
+    dka[0][i - NDT] = mfma(ta[i & 1], d1[0], dka[0][i - NDT]);
+    dka[1][i - NDT] = mfma(ta[i & 1], d1[1], dka[1][i - NDT]);
+    EDL_SB();
   }
 }
 
