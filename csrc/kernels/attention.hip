@@ -976,6 +976,10 @@ __device__ __forceinline__ void mfma_d_fence(f32x16 (&x)[2], f32x16 (&y)[2]) {
 //    next k-step's 4 reads issued before this step's MFMAs (128 MFMA cycles cover them);
 //  * dV += dO^T P and dK += Q^T dS read their transposed fragments one MFMA pair ahead;
 // each step is a sched_barrier region, so the reads stay ahead of the MFMAs they feed.
+__device__ __forceinline__ void mfma_d_fence2(f32x16 (&x)[2]) {
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 4" : "+v"(x[0]), "+v"(x[1]));
+}
+
 template <bool MASK, bool CAUSAL, int D>
 __device__ __forceinline__ void dkdv64p_slice(const char* Qs, const char* Ds, const float* NL,
                                               const float* DL, int rb, const bf16x8 (&kf)[2][D / 16],
@@ -987,40 +991,11 @@ __device__ __forceinline__ void dkdv64p_slice(const char* Qs, const char* Ds, co
   uint32_t vo = (uint32_t)(uintptr_t)(lds_char*)Vw;
   asm volatile("" : "+v"(vo));
   const lds_char* Vl = (const lds_char*)(uintptr_t)vo;
-  constexpr int NS = D / 16;
-  bf16x8 fq[2], fd[2], fv0[2], fv1[2];
-  auto rd = [&](int s, int b) {
-    fq[b] = row_read<D>(Qs, rb + l31, s, h);
-    fd[b] = row_read<D>(Ds, rb + l31, s, h);
-    fv0[b] = *(lds_bf16x8*)(Vl + swzd<D>(l31, 2 * s + h));
-    fv1[b] = *(lds_bf16x8*)(Vl + swzd<D>(32 + l31, 2 * s + h));
-  };
-  rd(0, 0);
-#pragma unroll
-  for (int s = 0; s < NS; ++s) {
-    const int b = s & 1;
-    if (s + 1 < NS) rd(s + 1, b ^ 1);
-    __builtin_amdgcn_sched_barrier(0);
-    if (s == 0) {
-      mfma_v_first(sa[0], fq[b], kf[0][s]);
-      mfma_v_first(sa[1], fq[b], kf[1][s]);
-      mfma_v_first(dp[0], fd[b], fv0[b]);
-      mfma_v_first(dp[1], fd[b], fv1[b]);
-    } else {
-      mfma_v(sa[0], fq[b], kf[0][s]);
-      mfma_v(sa[1], fq[b], kf[1][s]);
-      mfma_v(dp[0], fd[b], fv0[b]);
-      mfma_v(dp[1], fd[b], fv1[b]);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  mfma_d_fence(sa, dp);
-  // Softmax terms and dS in four row groups g (accumulator registers 4g .. 4g+3; groups 0-1 feed
-  // the bf16 operands of k-half s2 = 0, groups 2-3 those of s2 = 1).  The dV / dK MFMAs of one
-  // k-half run while the VALU finishes the next: only groups 0-1's exp is exposed.  The order is
-  // spelled out in sched_barrier chunks (MFMA, a quarter group of VALU, MFMA, ...): left to itself
-  // the scheduler put all of a group's VALU after its k-half's MFMAs.
-  auto expq = [&](int g, int t, const f32x4& nl) {   // one quarter: 4 scores of one key tile
+  constexpr int NS = D / 16, NDT = D / 32;
+#define EDL_SB() __builtin_amdgcn_sched_barrier(0)
+  // Softmax terms and dS per quarter (one key tile t, one row group g = accumulator registers
+  // 4g .. 4g+3; groups 0-1 feed the bf16 operands of k-half s2 = 0, groups 2-3 those of s2 = 1)
+  auto expq = [&](int g, int t, const f32x4& nl) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       float x = fast_exp2(__builtin_fmaf(sa[t][4 * g + e], sl2, nl[e]));
@@ -1036,71 +1011,97 @@ __device__ __forceinline__ void dkdv64p_slice(const char* Qs, const char* Ds, co
     for (int e = 0; e < 4; ++e) dp[t][4 * g + e] = sa[t][4 * g + e] * (dp[t][4 * g + e] - dl[e]);
   };
   auto ld4 = [&](const float* base, int g) { return *reinterpret_cast<const f32x4*>(base + rb + 8 * g + 4 * h); };
-  constexpr int NDT = D / 32;
   auto trq = [&](const char* T, int i) { return tr_read<D>(T, rb + 16 * (i / NDT) + 4 * h, i % NDT, lane); };
-  {
-    const f32x4 n0 = ld4(NL, 0), n1 = ld4(NL, 1);
-    expq(0, 0, n0); expq(0, 1, n0); expq(1, 0, n1); expq(1, 1, n1);
+
+  // phase 1a: S = Q K^T, the next k-step's Q fragment read ahead of this step's MFMAs
+  bf16x8 fq[2];
+  fq[0] = row_read<D>(Qs, rb + l31, 0, h);
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    if (s + 1 < NS) fq[(s + 1) & 1] = row_read<D>(Qs, rb + l31, s + 1, h);
+    EDL_SB();
+    if (s == 0) {
+      mfma_v_first(sa[0], fq[0], kf[0][0]);
+      mfma_v_first(sa[1], fq[0], kf[1][0]);
+    } else {
+      mfma_v(sa[0], fq[s & 1], kf[0][s]);
+      mfma_v(sa[1], fq[s & 1], kf[1][s]);
+    }
+    EDL_SB();
+  }
+  // phase 1b: dP = dO V^T (reads one k-step ahead)  ||  P = exp2(S sl2 - lse log2e), a quarter
+  // per MFMA: S is final here, so the softmax runs under the dP MFMAs instead of after them
+  bf16x8 fd[2], fv0[2], fv1[2];
+  auto rdp = [&](int s, int b) {
+    fd[b] = row_read<D>(Ds, rb + l31, s, h);
+    fv0[b] = *(lds_bf16x8*)(Vl + swzd<D>(l31, 2 * s + h));
+    fv1[b] = *(lds_bf16x8*)(Vl + swzd<D>(32 + l31, 2 * s + h));
+  };
+  rdp(0, 0);
+  f32x4 nl[4] = {ld4(NL, 0), ld4(NL, 1), ld4(NL, 2), ld4(NL, 3)};
+  mfma_d_fence2(sa);
+  EDL_SB();
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const int b = s & 1;
+    if (s + 1 < NS) rdp(s + 1, b ^ 1);
+    EDL_SB();
+    if (s == 0) mfma_v_first(dp[0], fd[0], fv0[0]); else mfma_v(dp[0], fd[b], fv0[b]);
+    EDL_SB();
+    expq(s >> 1, s & 1, nl[s >> 1]);
+    EDL_SB();
+    if (s == 0) mfma_v_first(dp[1], fd[0], fv1[0]); else mfma_v(dp[1], fd[b], fv1[b]);
+    EDL_SB();
   }
   const bf16x8 p0[2] = {acc_to_b(sa[0], 0), acc_to_b(sa[1], 0)};
+  const bf16x8 p1[2] = {acc_to_b(sa[0], 1), acc_to_b(sa[1], 1)};
   bf16x8 ta[2];
   ta[0] = trq(Ds, 0);
-  f32x4 nq[2] = {ld4(NL, 2), ld4(NL, 3)};
+  f32x4 dq[2] = {ld4(DL, 0), ld4(DL, 1)};
+  mfma_d_fence2(dp);
   EDL_SB();
-  // dV, k-half 0  ||  exp of groups 2-3 (one quarter per MFMA)
+  // phase 2: dV += dO^T P (k-half 0)  ||  dS = P (dP - delta), groups 0-1
 #pragma unroll
   for (int i = 0; i < NDT; ++i) {
     ta[(i + 1) & 1] = trq(Ds, i + 1);
     EDL_SB();
     dva[0][i] = mfma(ta[i & 1], p0[0], dva[0][i]);
     EDL_SB();
-    expq(2 + (i >> 1), i & 1, nq[i >> 1]);
+    dsq(i >> 1, i & 1, dq[i >> 1]);
     EDL_SB();
     dva[1][i] = mfma(ta[i & 1], p0[1], dva[1][i]);
-    EDL_SB();
-  }
-  const bf16x8 p1[2] = {acc_to_b(sa[0], 1), acc_to_b(sa[1], 1)};
-  f32x4 dq[2] = {ld4(DL, 0), ld4(DL, 1)};
-  EDL_SB();
-  // dV, k-half 1  ||  dS of groups 0-1
-#pragma unroll
-  for (int i = NDT; i < 2 * NDT; ++i) {
-    ta[(i + 1) & 1] = i + 1 < 2 * NDT ? trq(Ds, i + 1) : trq(Qs, 0);
-    EDL_SB();
-    dva[0][i - NDT] = mfma(ta[i & 1], p1[0], dva[0][i - NDT]);
-    EDL_SB();
-    dsq((i - NDT) >> 1, i & 1, dq[(i - NDT) >> 1]);
-    EDL_SB();
-    dva[1][i - NDT] = mfma(ta[i & 1], p1[1], dva[1][i - NDT]);
     EDL_SB();
   }
   const bf16x8 d0[2] = {acc_to_b(dp[0], 0), acc_to_b(dp[1], 0)};
   dq[0] = ld4(DL, 2);
   dq[1] = ld4(DL, 3);
   EDL_SB();
-  // dK, k-half 0  ||  dS of groups 2-3
+  // dV k-half 1  ||  dS groups 2-3
 #pragma unroll
-  for (int i = 0; i < NDT; ++i) {
-    ta[(i + 1) & 1] = trq(Qs, i + 1);
+  for (int i = NDT; i < 2 * NDT; ++i) {
+    ta[(i + 1) & 1] = i + 1 < 2 * NDT ? trq(Ds, i + 1) : trq(Qs, 0);
     EDL_SB();
-    dka[0][i] = mfma(ta[i & 1], d0[0], dka[0][i]);
+    dva[0][i - NDT] = mfma(ta[i & 1], p1[0], dva[0][i - NDT]);
     EDL_SB();
-    dsq(2 + (i >> 1), i & 1, dq[i >> 1]);
+    dsq(2 + ((i - NDT) >> 1), i & 1, dq[(i - NDT) >> 1]);
     EDL_SB();
-    dka[1][i] = mfma(ta[i & 1], d0[1], dka[1][i]);
+    dva[1][i - NDT] = mfma(ta[i & 1], p1[1], dva[1][i - NDT]);
     EDL_SB();
   }
   const bf16x8 d1[2] = {acc_to_b(dp[0], 1), acc_to_b(dp[1], 1)};
   EDL_SB();
-  // dK, k-half 1
+  // phase 3: dK += Q^T dS
 #pragma unroll
-  for (int i = NDT; i < 2 * NDT; ++i) {
+  for (int i = 0; i < 2 * NDT; ++i) {
     if (i + 1 < 2 * NDT) ta[(i + 1) & 1] = trq(Qs, i + 1);
     EDL_SB();
-    dka[0][i - NDT] = mfma(ta[i & 1], d1[0], dka[0][i - NDT]);
-    dka[1][i - NDT] = mfma(ta[i & 1], d1[1], dka[1][i - NDT]);
+    const bf16x8* dsv = i < NDT ? d0 : d1;
+    dka[0][i % NDT] = mfma(ta[i & 1], dsv[0], dka[0][i % NDT]);
+    dka[1][i % NDT] = mfma(ta[i & 1], dsv[1], dka[1][i % NDT]);
     EDL_SB();
   }
+#undef EDL_SB
+#define EDL_SB() __builtin_amdgcn_sched_barrier(0)
 }
 
 template <bool MASK, bool CAUSAL, int D>
