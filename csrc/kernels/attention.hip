@@ -1571,9 +1571,9 @@ static int attn_bwd_impl(const void* q, const void* k, const void* v, const void
   }();
   const int xcd64 = dkdv_xcd && (gkv64.x * gkv64.y * gkv64.z) % 8 == 0 ? 1 : 0;
   const bf16_t *bq = (const bf16_t*)q, *bk = (const bf16_t*)k, *bv = (const bf16_t*)v, *bdo = (const bf16_t*)dout;
-  static const bool dkdv_pf = [] {   // software-pipelined slices (dkdv64p_slice)
+  static const bool dkdv_pf = [] {   // software-pipelined slices (dkdv64p_slice); EDL_ATTN_DKDV_PF=0: round 5's
     const char* e = getenv("EDL_ATTN_DKDV_PF");
-    return e && atoi(e) == 1;
+    return !(e && atoi(e) == 0);
   }();
   if (keys_per_wave == 64) {
 #define EDL_DKDV64(C, P)                                                                                    \
