@@ -8,9 +8,9 @@ out=gpurun_out/r06_tree_ab.jsonl
 for i in 1 2 3; do
   (cd abtmp/r02 && timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > ../../gpurun_out/ab_r02_$i.json 2> ../../gpurun_out/ab_r02_$i.err)
   rc=$?; [ $rc -ne 0 ] && { echo "r02 run $i rc=$rc"; exit $rc; }
-  python -c "import json; d=json.loads(open('gpurun_out/ab_r02_$i.json').read().strip().splitlines()[-1]); print(json.dumps({'tree':'r02-8f7fe00','run':$i,'value':d['value'],'ms_per_step':d['ms_per_step']}))" >> $out
+  python scripts/ab_line.py gpurun_out/ab_r02_$i.json r02-8f7fe00 $i >> $out
   timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 --ttr off > gpurun_out/ab_head_$i.json 2> gpurun_out/ab_head_$i.err
   rc=$?; [ $rc -ne 0 ] && { echo "head run $i rc=$rc"; exit $rc; }
-  python -c "import json; d=json.loads(open('gpurun_out/ab_head_$i.json').read().strip().splitlines()[-1]); print(json.dumps({'tree':'head','run':$i,'value':d['value'],'ms_per_step':d['ms_per_step']}))" >> $out
+  python scripts/ab_line.py gpurun_out/ab_head_$i.json head $i >> $out
   tail -2 $out
 done
