@@ -341,9 +341,19 @@ class Planner:
         for n, m in metrics.items():
             if m.get("gpu") is not None and m.get("device", "cuda") == "cuda":
                 per_gpu.setdefault(int(m["gpu"]), []).append(n)
+        # ranks sharing a GPU: the most CU-sensitive one keeps every CU (a slice is only worth
+        # giving to the co-tenants that lose least from it)
+        keep_all = set()
+        for g, names in per_gpu.items():
+            probed = [(float((metrics[n].get("gpu_mix") or {}).get("cu_sensitivity")), n) for n in names
+                      if (metrics[n].get("gpu_mix") or {}).get("cu_sensitivity") is not None]
+            if len(probed) >= 2:
+                keep_all.add(max(probed)[1])
         for n, m in metrics.items():
             prof = m.get("rocprof") or m.get("gpu_mix")
             cu, src = None, None
+            if n in keep_all:
+                prof = None         # keeps every CU; its HBM cap is still planned below
             if prof and (m.get("device", "cuda") == "cuda" or m.get("rocprof")):
                 cu = self.cu_for_profile(prof)
                 if prof.get("cu_sensitivity") is not None:

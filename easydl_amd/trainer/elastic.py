@@ -1012,7 +1012,9 @@ class ElasticTrainer(RecoveryMixin):
         ev.record(torch.cuda.current_stream(self.device))
         self._gpu_step_evs[-1][2] = ev
         q = self._gpu_step_evs
-        while q and q[0][2] is not None and q[0][2].query():
+        # both events: start and end sit on different streams (compute / update), so an end
+        # can complete first when the update is not ordered after the step
+        while q and q[0][2] is not None and q[0][2].query() and q[0][1].query():
             s0, e0, e1 = q.pop(0)
             self._gpu_last = (s0 + 1, e0.elapsed_time(e1) / 1000.0)
         while q and q[0][2] is None and len(q) > 1:    # a dropped step: no end event

@@ -1,7 +1,9 @@
 """VERDICT r5 Next #7: the Brain decides per-rank CU and HBM plans from measured signals.
 
-Two ranks share ONE GPU and train at the same time: a matrix-core-bound Llama block stack and an
-HBM-bound batch-1 GEMV stack (tests/helpers/cu_probe_rank.py).  Both run the same trainer code,
+Two ranks of one job on ONE GPU: a matrix-core-bound Llama block stack and an HBM-bound batch-1
+GEMV stack (tests/helpers/cu_probe_rank.py).  They measure one after the other, as they would on
+their own GPUs: a half-CU probe taken while another process saturates the card measures that
+process, not the rank (the full GPU tier saw the two signals swap when they ran together).  Both run the same trainer code,
 so no role and no phase label tells them apart.  Each measures its CU sensitivity on half its
 CUs (utils/kmix.py) and its allocator peak; the Planner must give the HBM-bound rank a CU slice,
 keep every CU for the matrix-core-bound one, and tighten both HBM caps to their measured
@@ -25,11 +27,11 @@ HELPER = os.path.join(ROOT, "tests", "helpers", "cu_probe_rank.py")
 def test_measured_signals_give_different_cu_plans_on_one_gpu(tmp_path):
     env = dict(os.environ, PYTHONPATH=ROOT)
     env.pop("EDL_CU_MASK", None)
-    procs = {k: subprocess.Popen([sys.executable, HELPER, k, str(tmp_path / f"{k}.json")], env=env, cwd=ROOT)
-             for k in ("compute", "bandwidth")}
-    for k, p in procs.items():
-        assert p.wait(timeout=240) == 0, k
-    rec = {k: json.load(open(tmp_path / f"{k}.json")) for k in procs}
+    kinds = ("compute", "bandwidth")
+    for k in kinds:
+        p = subprocess.run([sys.executable, HELPER, k, str(tmp_path / f"{k}.json")], env=env, cwd=ROOT, timeout=240)
+        assert p.returncode == 0, k
+    rec = {k: json.load(open(tmp_path / f"{k}.json")) for k in kinds}
     print("\n[brain-measured]", json.dumps({k: {"gpu_mix": v["gpu_mix"], "hbm_peak_gb": v["hbm_peak_gb"]}
                                             for k, v in rec.items()}))
     for k, v in rec.items():
