@@ -223,9 +223,272 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_kernel(const bf16_t* __restric
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// v2: the same 256 x 256 x 64 tile, 8 waves of 128 x 64, now an 8-phase ping-pong pipeline
+// (cdna_hip_programming.md §5 "The 256^2 8-phase template", T3-T5):
+//  * a K-tile lives in LDS as four 16-KiB half-tiles: h0 = the A rows of every wave's m-half 0,
+//    h1 = the B rows of n-half 0, h2 = B n-half 1, h3 = A m-half 1 (128 rows x 128 B each);
+//  * a wave computes its 128 x 64 in four quadrant phases per K-tile, 16 MFMAs each:
+//    s0 (m0, n0) reads h0 + h1, s1 (m0, n1) reads h2, s2 (m1, n1) reads h3, s3 (m1, n0)
+//    reads nothing (A m-half 1 and B n-half 0 still in registers);
+//  * every phase issues one half-tile of LDS-DMA, two K-tiles ahead at most:
+//    s0 -> h2 of tile u+1, s1 -> h3 of u+1, s2 -> h0 of u+2, s3 -> h1 of u+2: each half-tile
+//    is refilled >= 2 phases after its last ds_read (WAR) and waited for with a COUNTED
+//    vmcnt(6) -- three half-tiles (48 KiB per CU) stay in flight across every barrier --
+//    one phase before it is read (RAW: wait, barrier, read);
+//  * waves of m-row 1 run one barrier behind m-row 0 (an extra s_barrier before the loop):
+//    on every SIMD one wave's MFMAs overlap the other wave's ds_reads and DMA issue;
+//    s_setprio(1) around each MFMA cluster keeps the compiler from moving MFMAs across the
+//    raw barriers (T5).
+// LDS swizzle: chunk c of half-tile row r sits at c ^ f(r), f(r) = ((r >> 1) & 7) ^ (((r >> 4) & 1) << 1),
+// found by exhaustive search (43,008 linear candidates) conflict-free for both read patterns.
+constexpr int HT = 128 * ROWB;             // one half-tile: 16 KiB
+__device__ __forceinline__ int swz8(int r) { return ((r >> 1) & 7) ^ (((r >> 4) & 1) << 1); }
+__device__ __forceinline__ void bar() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("" ::: "memory");
+}
+template <int N>
+__device__ __forceinline__ void vmwait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int ACC, bool PRE>
+__global__ __launch_bounds__(512, 1) void gemm_nt8_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
+                                                          bf16_t* __restrict__ C, int M, int N, int K, int lda,
+                                                          int ldb, int ldc, int group_m) {
+  __shared__ __attribute__((aligned(16))) char smem[8 * HT];   // [buffer 0..1][half 0..3]
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = w >> 2, wn = w & 3;
+  const int tm_n = M / BM, tn_n = N / BN;
+  const int nwg = tm_n * tn_n;
+  int wg = blockIdx.x;
+  {
+    const int q = nwg >> 3, r = nwg & 7, x = wg & 7;
+    wg = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (wg >> 3);
+  }
+  const int width = group_m * tn_n;
+  const int g = wg / width, first_m = g * group_m;
+  const int gsize = min(tm_n - first_m, group_m);
+  const int tm = first_m + (wg % width) % gsize, tn = (wg % width) / gsize;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  // ---- DMA plan: half-tile row hr = 64 p + 8 w + (lane >> 3) (p = the half-tile's two
+  // wave-instructions), physical chunk lane & 7 <- logical chunk (lane & 7) ^ swz8(hr).
+  // A half qm: global row 128 (hr >> 6) + 64 qm + (hr & 63); B half qn: global row
+  // 64 (hr >> 5) + 16 ((hr >> 3) & 3) + 8 qn + (hr & 7).
+  uint32_t va[2][2], vb[2][2];
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const int hr = 64 * p + 8 * w + (lane >> 3);
+    const int c = (lane & 7) ^ swz8(hr);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int ra_ = 128 * (hr >> 6) + 64 * h + (hr & 63);
+      const int rb_ = 64 * (hr >> 5) + 16 * ((hr >> 3) & 3) + 8 * h + (hr & 7);
+      va[h][p] = (uint32_t)(((int64_t)ra_ * lda + 8 * c) * 2);
+      vb[h][p] = (uint32_t)(((int64_t)rb_ * ldb + 8 * c) * 2);
+    }
+  }
+  const rsrc_t ra = make_rsrc(A + (int64_t)m0 * lda, (uint32_t)(BM * (int64_t)lda * 2));
+  const rsrc_t rb = make_rsrc(B + (int64_t)n0 * ldb, (uint32_t)(BN * (int64_t)ldb * 2));
+  // half-tile H of K-tile kt into buffer kt & 1 (H: 0 = A m0, 1 = B n0, 2 = B n1, 3 = A m1)
+  auto dma = [&](int kt, auto hc) {
+    constexpr int H = decltype(hc)::value;
+    const uint32_t soff = (uint32_t)(kt * BK * 2);
+    char* dst = smem + ((kt & 1) * 4 + H) * HT + w * 1024;
+    if constexpr (H == 0 || H == 3) {
+      buffer_load_lds16(ra, dst, va[H == 3][0], soff);
+      buffer_load_lds16(ra, dst + 8192, va[H == 3][1], soff);
+    } else {
+      buffer_load_lds16(rb, dst, vb[H == 2][0], soff);
+      buffer_load_lds16(rb, dst + 8192, vb[H == 2][1], soff);
+    }
+  };
+  using H0 = std::integral_constant<int, 0>;
+  using H1 = std::integral_constant<int, 1>;
+  using H2 = std::integral_constant<int, 2>;
+  using H3 = std::integral_constant<int, 3>;
+
+  // ---- fragment read offsets within a half-tile.  A (MFMA B input): hr = 64 wm + 16 mb + i,
+  // swz8 = ((i >> 1) & 7) ^ ((mb & 1) << 1).  B (MFMA A input): hr = 32 wn + 8 (i >> 2) + 4 nl + (i & 3).
+  uint32_t oa[2][2], ob[2][2];
+  {
+    const int i = lane & 15, q = lane >> 4;
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int hra = 64 * wm + 16 * x + i;
+        const int hrb = 32 * wn + 8 * (i >> 2) + 4 * x + (i & 3);
+        oa[x][kk] = (uint32_t)(hra * ROWB + (((4 * kk + q) ^ swz8(hra)) << 4));
+        ob[x][kk] = (uint32_t)(hrb * ROWB + (((4 * kk + q) ^ swz8(hrb)) << 4));
+      }
+  }
+  const lds_c* L = (const lds_c*)smem;
+  f32x4v acc[8][4];
+#pragma unroll
+  for (int mb = 0; mb < 8; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb) acc[mb][nb] = f32x4v{0.f, 0.f, 0.f, 0.f};
+  bf16x8 fa[4][2], fb0[2][2], fbx[2][2], fb1[2][2];   // [block][kk]
+
+  auto read_a = [&](int base) {
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) fa[mb][kk] = lds_frag(L + base + 32 * (mb >> 1) * ROWB, oa[mb & 1][kk]);
+  };
+  auto read_b = [&](int base, bf16x8 (&fb)[2][2]) {
+#pragma unroll
+    for (int nl = 0; nl < 2; ++nl)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) fb[nl][kk] = lds_frag(L + base, ob[nl][kk]);
+  };
+  auto mma = [&](int qm, int qn, bf16x8 (&fb)[2][2]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+        for (int nl = 0; nl < 2; ++nl)
+          acc[4 * qm + mb][2 * qn + nl] = mfma16(fb[nl][kk], fa[mb][kk], acc[4 * qm + mb][2 * qn + nl]);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  // one K-tile: 4 phases.  Wv = the vmcnt before phase v's DMA issue (-1: no wait); IS bit v:
+  // phase v issues its half-tile.  PRE: B n-half 0 of the NEXT tile is read in s3 (into fbn;
+  // its wait moves to s2, vmcnt(4)), so s0 reads only A m-half 0: 8 / 4 / 8 / 4 reads per
+  // phase instead of 12 / 4 / 8 / 0.
+  auto tile = [&](int u, auto w0, auto w1, auto w2, auto w3, auto iss, bf16x8 (&fbc)[2][2],
+                  bf16x8 (&fbn)[2][2]) {
+    constexpr int W0 = decltype(w0)::value, W1 = decltype(w1)::value, W2 = decltype(w2)::value,
+                  W3 = decltype(w3)::value;
+    constexpr int IS = decltype(iss)::value;   // bit 4: pre-read the next tile's B n-half 0
+    const int buf = (u & 1) * 4 * HT;
+    // s0: quadrant (m0, n0)
+    read_a(buf + 0 * HT);
+    if constexpr (!PRE) read_b(buf + 1 * HT, fbc);
+    if constexpr (W0 >= 0) vmwait<W0>();
+    if constexpr (IS & 1) dma(u + 1, H2{});
+    bar();
+    mma(0, 0, fbc);
+    bar();
+    // s1: (m0, n1)
+    read_b(buf + 2 * HT, fb1);
+    if constexpr (W1 >= 0) vmwait<W1>();
+    if constexpr (IS & 2) dma(u + 1, H3{});
+    bar();
+    mma(0, 1, fb1);
+    bar();
+    // s2: (m1, n1)
+    read_a(buf + 3 * HT);
+    if constexpr (W2 >= 0) vmwait<W2>();
+    if constexpr (IS & 4) dma(u + 2, H0{});
+    bar();
+    mma(1, 1, fb1);
+    bar();
+    // s3: (m1, n0)
+    if constexpr (PRE && (IS & 16)) read_b(((u + 1) & 1) * 4 * HT + 1 * HT, fbn);
+    if constexpr (W3 >= 0) vmwait<W3>();
+    if constexpr (IS & 8) dma(u + 2, H1{});
+    bar();
+    mma(1, 0, fbc);
+    bar();
+  };
+  using I = std::integral_constant<int, 0>;
+  using N1 = std::integral_constant<int, -1>;
+  const int nk = K / BK;   // >= 2 (host check)
+  // prologue: tile 0 whole, h0/h1 of tile 1; wait for h0/h1 of tile 0
+  dma(0, H0{}); dma(0, H1{}); dma(0, H2{}); dma(0, H3{});
+  dma(1, H0{}); dma(1, H1{});
+  vmwait<8>();
+  bar();
+  if constexpr (PRE) read_b(1 * HT, fb0);
+  if (wm == 1) bar();   // m-row 1 runs one barrier behind
+  using C6 = std::integral_constant<int, 6>;
+  using C4 = std::integral_constant<int, 4>;
+  using C2 = std::integral_constant<int, 2>;
+  if constexpr (PRE) {
+    // steady: W2 = 4 (h0 / h1 of u + 1 before the s3 pre-read), no s3 wait; nk even (host
+    // check), so the tiles pair up and the last two always start from fb0
+#pragma unroll 1
+    for (int u = 0; u + 2 < nk; u += 2) {
+      tile(u, C6{}, C6{}, C4{}, N1{}, std::integral_constant<int, 31>{}, fb0, fbx);
+      tile(u + 1, C6{}, C6{}, C4{}, N1{}, std::integral_constant<int, 31>{}, fbx, fb0);
+    }
+    tile(nk - 2, C6{}, C6{}, C4{}, N1{}, std::integral_constant<int, 19>{}, fb0, fbx);
+    tile(nk - 1, C2{}, I{}, N1{}, N1{}, I{}, fbx, fb0);
+  } else {
+#pragma unroll 1
+    for (int u = 0; u + 2 < nk; ++u) tile(u, C6{}, C6{}, N1{}, C6{}, std::integral_constant<int, 15>{}, fb0, fbx);
+    tile(nk - 2, C6{}, C6{}, N1{}, C4{}, std::integral_constant<int, 3>{}, fb0, fbx);
+    tile(nk - 1, C2{}, I{}, N1{}, I{}, I{}, fb0, fbx);
+  }
+  if (wm == 0) bar();
+
+  const int q = lane >> 4;
+#pragma unroll
+  for (int mb = 0; mb < 8; ++mb) {
+    const int m = m0 + 128 * wm + 16 * mb + (lane & 15);
+    bf16_t* p = C + (int64_t)m * ldc + n0 + 64 * wn + 16 * q;
+    float v[16];
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[4 * nb + r] = acc[mb][nb][r];
+    if (ACC) {
+      const u32x4 o0 = reinterpret_cast<const u32x4*>(p)[0], o1 = reinterpret_cast<const u32x4*>(p)[1];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[2 * e] += bflo(o0[e]);
+        v[2 * e + 1] += bfhi(o0[e]);
+        v[8 + 2 * e] += bflo(o1[e]);
+        v[8 + 2 * e + 1] += bfhi(o1[e]);
+      }
+    }
+    u32x4 s0, s1;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      s0[e] = pack2(v[2 * e], v[2 * e + 1]);
+      s1[e] = pack2(v[8 + 2 * e], v[8 + 2 * e + 1]);
+    }
+    reinterpret_cast<u32x4*>(p)[0] = s0;
+    reinterpret_cast<u32x4*>(p)[1] = s1;
+  }
+}
+
 }  // namespace
 
 extern "C" {
+
+// v2 (8-phase); same contract as edl_gemm_nt, K >= 128
+int edl_gemm_nt8(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
+                 int accumulate, int group_m, hipStream_t stream) {
+  const bool pre = (accumulate & 2) && K % (2 * BK) == 0;
+  accumulate &= 1;
+  if (M % BM || N % BN || K % BK || K < 2 * BK || lda % 8 || ldb % 8 || ldc % 8 || M <= 0 || N <= 0)
+    return (int)hipErrorInvalidValue;
+  if ((int64_t)BM * lda * 2 >= (1ll << 32) || (int64_t)BN * ldb * 2 >= (1ll << 32))
+    return (int)hipErrorInvalidValue;
+  if (group_m <= 0) group_m = 8;
+  const int nwg = (M / BM) * (N / BN);
+#define EDL_NT8(ACC_, PRE_)                                                                                 \
+  gemm_nt8_kernel<ACC_, PRE_><<<nwg, 512, 0, stream>>>((const bf16_t*)A, (const bf16_t*)B, (bf16_t*)C, M, N, K, lda, \
+                                                       ldb, ldc, group_m)
+  if (accumulate) {
+    if (pre) EDL_NT8(1, true); else EDL_NT8(1, false);
+  } else {
+    if (pre) EDL_NT8(0, true); else EDL_NT8(0, false);
+  }
+#undef EDL_NT8
+  EDL_LAUNCH_CHECK();
+  return 0;
+}
 
 // C (+)= A B^T; returns hipErrorInvalidValue for shapes the kernel does not take.
 int edl_gemm_nt(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,

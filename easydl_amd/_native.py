@@ -36,6 +36,7 @@ _KERNEL_SIGS = {
     "edl_adamw_flat_m16": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_i64, c_float, c_float,
                            c_float, c_float, c_float, c_i64, c_float, c_void_p, c_void_p],
     "edl_gemm_nt": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
+    "edl_gemm_nt8": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
     "edl_gemm_nt_diag": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                          c_void_p],
     "edl_sgd_flat": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_i64, c_float, c_float, c_float, c_float,

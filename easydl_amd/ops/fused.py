@@ -313,6 +313,20 @@ _NT_WGRAD = os.environ.get("EDL_NT_WGRAD", "1") != "0"
 _NT_WGRAD_MAX_K = 8192
 # fused MLP (SwiGLU kernels emit the transposed wgrad operands); EDL_MLP_FUSED=0 -> generic path
 _MLP_FUSED = os.environ.get("EDL_MLP_FUSED", "1") != "0"
+# the gate/up input gradient dX = dGU W_gu (K = 2 x ffn) on the hand-written 8-phase NT GEMM
+# (csrc/kernels/gemm_nt.hip, group 4): 1,569-1,585 vs hipBLASLt's 1,517-1,527 TF/s at Llama-3-8B
+# (profiles/r06_gemm_nt8.md); every other shape stays with hipBLASLt.  EDL_GEMM_NT8_DGRAD=0 disables.
+_NT8_DGRAD = os.environ.get("EDL_GEMM_NT8_DGRAD", "1") != "0"
+
+
+def _dgrad_gu(dgu: torch.Tensor, wt_gu, w_gu) -> torch.Tensor:
+    if wt_gu is None:
+        return torch.mm(dgu, w_gu)
+    if _NT8_DGRAD and dgu.shape[1] % 128 == 0:
+        from easydl_amd.ops import gemm
+        if gemm.supported(dgu, wt_gu):
+            return gemm.gemm_nt(dgu, wt_gu, group_m=4, kernel="nt8")
+    return torch.mm(dgu, wt_gu.t())
 
 
 def _transposed(t: torch.Tensor) -> torch.Tensor:
@@ -665,8 +679,7 @@ class _SwiGLUMLPFn(torch.autograd.Function):
         del dh
         dx = fin = None
         if ctx.needs_input_grad[0]:
-            dx = torch.mm(dgu, wt_gu.t()) if wt_gu is not None else torch.mm(dgu, w_gu)
-            dx = dx.view(*dy.shape[:-1], w_gu.shape[1])
+            dx = _dgrad_gu(dgu, wt_gu, w_gu).view(*dy.shape[:-1], w_gu.shape[1])
         if not tn:
             del dgu
         if overlap:

@@ -21,10 +21,12 @@ def main():
     ap.add_argument("--group", type=int, default=8)
     ap.add_argument("--tokens", type=int, default=16384)
     ap.add_argument("--only", default="")
+    ap.add_argument("--arms", default="", help="8-phase kernel arms name:flags:group_m,... (flags bit 1: B pre-read)")
     ap.add_argument("--diag", action="store_true", help="also time the kernel without DMA, the DMA alone, and F.linear")
     a = ap.parse_args()
     from easydl_amd.ops import gemm_tuning
     from easydl_amd.ops.gemm import gemm_nt
+    from easydl_amd import _native
     gemm_tuning.apply("select")
     dev = torch.device("cuda", 0)
     T = a.tokens
@@ -45,6 +47,19 @@ def main():
         rel = ((C.float() - ref.float()).norm() / ref.float().norm()).item()
         flops = 2.0 * M * N * K
         res = {"edl": [], "hipblaslt": []}
+        C8 = torch.empty_like(C)
+        arms = {}
+        for spec in (a.arms.split(",") if a.arms else []):
+            nm, flag, grp = spec.split(":")
+            arms[nm] = (lambda flag=int(flag), grp=int(grp): _native.kernels().check(
+                "edl_gemm_nt8", A.data_ptr(), B.data_ptr(), C8.data_ptr(), M, N, K, K, K, N, flag, grp,
+                _native.stream_of(A)))
+        rels = {}
+        for nm, fn in arms.items():
+            C8.zero_()
+            fn()
+            rels[nm] = round(((C8.float() - ref.float()).norm() / ref.float().norm()).item(), 5)
+            res[nm] = []
 
         def timed(fn):
             fn()
@@ -55,7 +70,6 @@ def main():
             torch.cuda.synchronize()
             return (time.perf_counter() - t0) / a.iters
 
-        from easydl_amd import _native
         k = _native.kernels()
 
         def diag(mode):
@@ -66,6 +80,8 @@ def main():
         for _ in range(a.rounds):
             res["edl"].append(timed(lambda: gemm_nt(A, B, out=C, group_m=a.group)))
             res["hipblaslt"].append(timed(lambda: torch.mm(A, B.t(), out=C)))
+            for nm, fn in arms.items():
+                res[nm].append(timed(fn))
             if a.diag:
                 res["diag_no_dma"].append(timed(lambda: diag(1)))
                 res["diag_dma_only"].append(timed(lambda: diag(2)))
@@ -77,6 +93,9 @@ def main():
             out[k] = {"ms": round(best * 1e3, 4), "tflops": round(flops / best / 1e12, 1),
                       "median_ms": round(sorted(v)[len(v) // 2] * 1e3, 4)}
         out["speedup"] = round(out["hipblaslt"]["ms"] / out["edl"]["ms"], 3)
+        for nm in arms:
+            out[nm]["rel_err"] = rels[nm]
+            out[nm]["vs_hipblaslt"] = round(out["hipblaslt"]["ms"] / out[nm]["ms"], 3)
         print(json.dumps(out), flush=True)
         del A, B, C, ref
         torch.cuda.empty_cache()
