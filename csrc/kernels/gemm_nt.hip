@@ -256,7 +256,9 @@ __device__ __forceinline__ void vmwait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int ACC, bool PRE>
+// DEPTH (probe only): 0 = the counted waits derived above; 1 / 2 = stricter steady waits
+// (fewer half-tiles in flight) to measure how much the prefetch depth is worth
+template <int ACC, bool PRE, int DEPTH = 0>
 __global__ __launch_bounds__(512, 1) void gemm_nt8_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
                                                           bf16_t* __restrict__ C, int M, int N, int K, int lda,
                                                           int ldb, int ldc, int group_m) {
@@ -370,6 +372,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt8_kernel(const bf16_t* __restri
                   W3 = decltype(w3)::value;
     constexpr int IS = decltype(iss)::value;   // bit 4: pre-read the next tile's B n-half 0
     const int buf = (u & 1) * 4 * HT;
+    if constexpr (DEPTH == 3) { bar(); bar(); }
     // s0: quadrant (m0, n0)
     read_a(buf + 0 * HT);
     if constexpr (!PRE) read_b(buf + 1 * HT, fbc);
@@ -378,6 +381,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt8_kernel(const bf16_t* __restri
     bar();
     mma(0, 0, fbc);
     bar();
+    if constexpr (DEPTH == 3) { bar(); bar(); }
     // s1: (m0, n1)
     read_b(buf + 2 * HT, fb1);
     if constexpr (W1 >= 0) vmwait<W1>();
@@ -385,6 +389,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt8_kernel(const bf16_t* __restri
     bar();
     mma(0, 1, fb1);
     bar();
+    if constexpr (DEPTH == 3) { bar(); bar(); }
     // s2: (m1, n1)
     read_a(buf + 3 * HT);
     if constexpr (W2 >= 0) vmwait<W2>();
@@ -392,6 +397,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt8_kernel(const bf16_t* __restri
     bar();
     mma(1, 1, fb1);
     bar();
+    if constexpr (DEPTH == 3) { bar(); bar(); }
     // s3: (m1, n0)
     if constexpr (PRE && (IS & 16)) read_b(((u + 1) & 1) * 4 * HT + 1 * HT, fbn);
     if constexpr (W3 >= 0) vmwait<W3>();
@@ -418,8 +424,10 @@ __global__ __launch_bounds__(512, 1) void gemm_nt8_kernel(const bf16_t* __restri
     // check), so the tiles pair up and the last two always start from fb0
 #pragma unroll 1
     for (int u = 0; u + 2 < nk; u += 2) {
-      tile(u, C6{}, C6{}, C4{}, N1{}, std::integral_constant<int, 31>{}, fb0, fbx);
-      tile(u + 1, C6{}, C6{}, C4{}, N1{}, std::integral_constant<int, 31>{}, fbx, fb0);
+      using SW = std::integral_constant<int, DEPTH == 0 || DEPTH == 3 ? 6 : DEPTH == 1 ? 4 : 2>;
+      using SW2 = std::integral_constant<int, DEPTH == 2 ? 2 : 4>;
+      tile(u, SW{}, SW{}, SW2{}, N1{}, std::integral_constant<int, 31>{}, fb0, fbx);
+      tile(u + 1, SW{}, SW{}, SW2{}, N1{}, std::integral_constant<int, 31>{}, fbx, fb0);
     }
     tile(nk - 2, C6{}, C6{}, C4{}, N1{}, std::integral_constant<int, 19>{}, fb0, fbx);
     tile(nk - 1, C2{}, I{}, N1{}, N1{}, I{}, fbx, fb0);
@@ -470,6 +478,7 @@ extern "C" {
 int edl_gemm_nt8(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
                  int accumulate, int group_m, hipStream_t stream) {
   const bool pre = (accumulate & 2) && K % (2 * BK) == 0;
+  const int depth = (accumulate >> 2) & 3;
   accumulate &= 1;
   if (M % BM || N % BN || K % BK || K < 2 * BK || lda % 8 || ldb % 8 || ldc % 8 || M <= 0 || N <= 0)
     return (int)hipErrorInvalidValue;
@@ -482,6 +491,15 @@ int edl_gemm_nt8(const void* A, const void* B, void* C, int M, int N, int K, int
                                                        ldb, ldc, group_m)
   if (accumulate) {
     if (pre) EDL_NT8(1, true); else EDL_NT8(1, false);
+  } else if (pre && depth == 1) {
+    gemm_nt8_kernel<0, true, 1><<<nwg, 512, 0, stream>>>((const bf16_t*)A, (const bf16_t*)B, (bf16_t*)C, M, N, K, lda,
+                                                         ldb, ldc, group_m);
+  } else if (pre && depth == 3) {
+    gemm_nt8_kernel<0, true, 3><<<nwg, 512, 0, stream>>>((const bf16_t*)A, (const bf16_t*)B, (bf16_t*)C, M, N, K, lda,
+                                                         ldb, ldc, group_m);
+  } else if (pre && depth == 2) {
+    gemm_nt8_kernel<0, true, 2><<<nwg, 512, 0, stream>>>((const bf16_t*)A, (const bf16_t*)B, (bf16_t*)C, M, N, K, lda,
+                                                         ldb, ldc, group_m);
   } else {
     if (pre) EDL_NT8(0, true); else EDL_NT8(0, false);
   }
