@@ -43,6 +43,17 @@ def _signature(kind: str, t: torch.Tensor, extra: int = 0) -> int:
     return zlib.crc32(f"{kind}:{t.numel()}:{t.dtype}:{extra}".encode()) & 0x7FFFFFFF
 
 
+def _ranks_per_device(store, rank: int, world: int, device) -> int:
+    """The most ranks any one GPU carries in this group (device UUIDs through the store)."""
+    uuid = str(torch.cuda.get_device_properties(device).uuid)
+    store.set(str(rank), uuid)
+    seen: dict[str, int] = {}
+    for p in range(world):
+        u = uuid if p == rank else store.get(str(p)).decode()
+        seen[u] = seen.get(u, 0) + 1
+    return max(seen.values())
+
+
 def _td(s: float) -> datetime.timedelta:
     return datetime.timedelta(seconds=s)
 
@@ -120,6 +131,13 @@ class Communicator:
             self.xgmi_mode = "xgmi"
             self.backend = self.data_kind = "xgmi"
         elif self.device.type == "cuda":
+            if (data_backend == "auto" and world_size > 1 and os.environ.get("EDL_XGMI_CROSS_GPU", "0") != "1"
+                    and _ranks_per_device(dist.PrefixStore("devs", base), rank, world_size, self.device) == 1):
+                # every rank on its own GPU: the engine's peer reads over xGMI between GPUs have
+                # not run on hardware yet (only ranks sharing one GPU have), so "auto" keeps RCCL
+                # there; EDL_XGMI_CROSS_GPU=1 (or EDL_COMM=xgmi) lets the probe decide
+                self.xgmi_probe = {"selected": "rccl", "reason": "one rank per GPU; EDL_XGMI_CROSS_GPU=1 probes"}
+                data_backend = "rccl"
             if data_backend in ("xgmi", "auto") and world_size > 1:
                 # csrc/kernels/xgmi.hip: abortable direct all-reduce over IPC-mapped peer
                 # memory; RCCL keeps the other collectives (and all-reduce in "auto" until
