@@ -192,4 +192,4 @@ def test_cu_probe_separates_matrix_core_work_from_streaming(cuda):
     assert out["gemm"]["probes"] == 4 and out["stream"]["probes"] == 4
     assert out["gemm"]["s"] > 0.45, out
     assert out["stream"]["s"] < 0.4, out
-    assert out["gemm"]["s"] > out["stream"]["s"] + 0.2, out
+    assert out["gemm"]["s"] > out["stream"]["s"] + 0.15, out
