@@ -2,7 +2,8 @@
 """Headline benchmark: Llama-3-8B elastic-DDP training throughput (tokens/s).
 
 Metric/config come from BASELINE.json (``tokens/sec ... Llama-3-8B elastic
-DDP 1->8 GPUs``).  One process per GPU; for N>1 the driver launches this file
+DDP 1->8 GPUs``); the recovery and elasticity it drills are the reference's fault-tolerance
+and elasticity claims (/root/reference/README.md:25-35).  One process per GPU; for N>1 the driver launches this file
 with ``torch.distributed.run`` and every rank reads RANK / LOCAL_RANK /
 WORLD_SIZE / MASTER_ADDR / MASTER_PORT from the environment; the plain form
 ``python bench.py --gpus N`` launches the N ranks itself (see below).

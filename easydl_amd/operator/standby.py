@@ -1,5 +1,8 @@
 """Hot-standby role processes (SURVEY.md §5.3 "hot-standby processes ... remove
-the multi-second Python/torch import from TTR", §7.3 hard part 3).
+the multi-second Python/torch import from TTR", §7.3 hard part 3; the capability is the
+reference's "recover failed parameter servers and workers and resume the training",
+/root/reference/README.md:25-29, and the operator's replace-a-Pod flow,
+/root/reference/docs/design/elastic-training-operator.md:97-101).
 
 A standby is started by the local ElasticOperator ahead of any failure as
 ``python -m easydl_amd.operator.standby``.  It pays every start-up cost that

@@ -1,4 +1,5 @@
-"""Hand-written bf16 NT GEMM for gfx950 (csrc/kernels/gemm_nt.hip):
+"""Hand-written bf16 NT GEMM for gfx950 (csrc/kernels/gemm_nt.hip; the reference publishes no
+kernels -- its training performance claim is /root/reference/README.md:19-23):
 ``C (+)= A @ B^T`` with A [M, K] and B [N, K] both K-contiguous -- the form every large GEMM
 of the Llama step takes in this framework's layouts (forward X W^T, input gradient from the
 cached W^T, weight gradient from the transposed activations).

@@ -5,7 +5,9 @@ first onto the least-loaded shard); it is a pure function of the model's
 parameter names and sizes, so every role computes the same assignment without
 coordination.  PS addresses are discovered through the job master's store
 (``ps/addr/<i>``), and a client transparently reconnects when a PS is replaced
-(new incarnation, new port).
+(new incarnation, new port).  A replaced GPU PS (reference "recover failed parameter
+servers", /root/reference/README.md:27; replace-by-name, docs/design/elastic-training-operator.md:97-101)
+is re-mapped over IPC: pushes in flight to the dead one are counted lost, never resent.
 """
 from __future__ import annotations
 
