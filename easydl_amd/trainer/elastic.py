@@ -773,6 +773,8 @@ class ElasticTrainer(RecoveryMixin):
         self._t_mb = t_mb
         return None if loss_acc is None else loss_acc / total
 
+    _OVERLAP_MIN_GROUPS = 4
+
     def _opt_overlap(self):
         """The optimizer stream when the update may overlap the next step's forward, else None.
 
@@ -785,12 +787,21 @@ class ElasticTrainer(RecoveryMixin):
         await_shadow).  Off for models with module buffers (BatchNorm statistics are broadcast
         after the update), tensor parallelism, optimizers without per-group callbacks, and with
         ``EDL_OPT_OVERLAP=0``.  An ``on_step`` callback runs while the update may still be in
-        flight: one that reads parameters directly calls ``wait_update()`` first."""
+        flight: one that reads parameters directly calls ``wait_update()`` first.
+
+        Default ("auto"): only for models of at least ``_OVERLAP_MIN_GROUPS`` flat groups (each
+        <= 1.9 GB of gradients): with one or two groups the next forward waits for the whole
+        update anyway, and the per-module wait hooks cost host time a short step cannot hide --
+        BERT-large (1 group, 46 ms steps) ran 662 vs 700 samples/s with it on; Llama-3-8B
+        (9 groups) 23,677 vs 23,649 tok/s (profiles/r06_opt_overlap_ab.jsonl,
+        r06_bert_groups.jsonl).  ``EDL_OPT_OVERLAP=1`` forces it on."""
         if self._opt_stream is not None:
             return self._opt_stream
         if self._opt_overlap_off:
             return None
-        if (self.device.type != "cuda" or self.tp > 1 or os.environ.get("EDL_OPT_OVERLAP", "1") == "0"
+        mode = os.environ.get("EDL_OPT_OVERLAP", "auto")
+        if (self.device.type != "cuda" or self.tp > 1 or mode == "0"
+                or (mode != "1" and (self.flat is None or len(self.flat.groups) < self._OVERLAP_MIN_GROUPS))
                 or not getattr(self.opt, "supports_group_done", False)
                 or (self.bufs is not None and self.bufs.tensors)):
             self._opt_overlap_off = True
