@@ -21,7 +21,7 @@ import re
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SKIP_DIRS = {".git", "gpurun_out", "__pycache__", "lib", "profiles", ".pytest_cache"}
+SKIP_DIRS = {".git", "gpurun_out", "__pycache__", "lib", "profiles", ".pytest_cache", "abtmp"}  # abtmp: A/B worktrees
 MAXLEN = 120
 CXX_BANNED = [
     (re.compile(r"#\s*include\s*[<\"]cuda"), "CUDA header in a gfx950-only source"),

@@ -4,10 +4,10 @@ Two ranks of one job on ONE GPU: a matrix-core-bound Llama block stack and an HB
 GEMV stack (tests/helpers/cu_probe_rank.py).  They measure one after the other, as they would on
 their own GPUs: a half-CU probe taken while another process saturates the card measures that
 process, not the rank (the full GPU tier saw the two signals swap when they ran together).
-Both run the same trainer code, so no role and no phase label tells them apart.  Each measures its CU sensitivity on half its
-CUs (utils/kmix.py) and its allocator peak; the Planner must give the HBM-bound rank a CU slice,
-keep every CU for the more sensitive one (ranks sharing a GPU), and tighten both HBM caps to
-their measured peaks."""
+Both run the same trainer code, so no role and no phase label tells them apart.  Each measures
+its CU sensitivity on half its CUs (utils/kmix.py) and its allocator peak; the Planner must give
+the HBM-bound rank a CU slice, keep every CU for the more sensitive one (ranks sharing a GPU),
+and tighten both HBM caps to their measured peaks."""
 import json
 import os
 import subprocess
