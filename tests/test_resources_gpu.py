@@ -88,6 +88,7 @@ def test_cu_plan_holds_for_every_stream_of_a_rank(cuda, tmp_path, monkeypatch):
     from easydl_amd.trainer.elastic import ElasticTrainer
     cfg = get_config("llama-tiny")
     monkeypatch.setattr(fused, "_WGRAD_STREAM", True)      # weight gradients on the side stream
+    monkeypatch.setenv("EDL_OPT_OVERLAP", "1")             # the update's stream (auto: >= 4 groups only)
     monkeypatch.setattr(fused, "_SIDE", {})
     monkeypatch.setattr(fused, "_WT_BATCH", fused._WT_BATCH)
     prev = torch.cuda.current_stream()
