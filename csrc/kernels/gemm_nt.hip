@@ -470,6 +470,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt8_kernel(const bf16_t* __restri
   }
 }
 
+
 }  // namespace
 
 extern "C" {

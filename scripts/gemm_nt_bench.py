@@ -21,7 +21,7 @@ def main():
     ap.add_argument("--group", type=int, default=8)
     ap.add_argument("--tokens", type=int, default=16384)
     ap.add_argument("--only", default="")
-    ap.add_argument("--arms", default="", help="8-phase kernel arms name:flags:group_m,... (flags bit 1: B pre-read)")
+    ap.add_argument("--arms", default="", help="kernel arms name:flags:group_m,... (the 8-phase kernel)")
     ap.add_argument("--diag", action="store_true", help="also time the kernel without DMA, the DMA alone, and F.linear")
     a = ap.parse_args()
     from easydl_amd.ops import gemm_tuning
@@ -50,9 +50,10 @@ def main():
         C8 = torch.empty_like(C)
         arms = {}
         for spec in (a.arms.split(",") if a.arms else []):
-            nm, flag, grp = spec.split(":")
-            arms[nm] = (lambda flag=int(flag), grp=int(grp): _native.kernels().check(
-                "edl_gemm_nt8", A.data_ptr(), B.data_ptr(), C8.data_ptr(), M, N, K, K, K, N, flag, grp,
+            nm, flag, grp = spec.split(":")[:3]
+            fn_name = "edl_gemm_nt8"
+            arms[nm] = (lambda flag=int(flag), grp=int(grp), fn_name=fn_name: _native.kernels().check(
+                fn_name, A.data_ptr(), B.data_ptr(), C8.data_ptr(), M, N, K, K, K, N, flag, grp,
                 _native.stream_of(A)))
         rels = {}
         for nm, fn in arms.items():
