@@ -218,13 +218,26 @@ def _reserve_slab(kv, name: str, gpu: int, slot: str) -> None:
           f"free) in {time.perf_counter() - t0:.3f} s", file=sys.stderr, flush=True)
 
 
-def _release_slabs(keep: int | None) -> None:
-    """Takeover of ``keep``'s GPU: the slabs on every other GPU go back to the driver."""
+def _release_device_cache(g: int) -> None:
+    """Return ONE GPU's cached blocks to the driver.  ``torch.cuda.empty_cache()`` empties the
+    caching allocator of every device -- at a takeover that would also drop the slab on the GPU
+    the replacement is about to compute on, the very memory its first step needs.  An allocation
+    larger than the device makes that device's allocator (and only it) free its cached blocks
+    and retry before it gives up, which is the per-device release we want."""
     import torch
+    try:
+        torch.empty(2 * torch.cuda.get_device_properties(g).total_memory, dtype=torch.uint8,
+                    device=torch.device("cuda", g))
+    except torch.cuda.OutOfMemoryError:
+        pass
+
+
+def _release_slabs(keep: int | None) -> None:
+    """Takeover of ``keep``'s GPU: the slabs on every other GPU go back to the driver; ``keep``'s
+    stays cached for the replacement's first step."""
     for g in [g for g in SLABS if g != keep]:
         if SLABS.pop(g):
-            with torch.cuda.device(g):
-                torch.cuda.empty_cache()
+            _release_device_cache(g)
 
 
 class _Null:
