@@ -330,10 +330,14 @@ class ElasticOperator:
             except Exception:  # noqa: BLE001 - store unreachable: keep the last roster
                 return
         roster = ",".join(ready)
-        if roster != self._roster:
+        # spawned but not ready yet (still importing): a worker about to take its first step waits
+        # for their warm-up too (standby_warm_on), instead of racing a standby that is coming
+        pending = ",".join(n for n in sorted(self.standbys) if n not in ready)
+        if (roster, pending) != (self._roster, getattr(self, "_pending", None)):
             try:
+                self.kv.set("standby/pending", pending)
                 self.kv.set("standby/roster", roster)
-                self._roster = roster
+                self._roster, self._pending = roster, pending
             except Exception:  # noqa: BLE001
                 pass
 

@@ -155,7 +155,9 @@ def warm_device(gpu: int, spec: dict | None = None, set_stream: bool = False, in
         torch.cuda.synchronize(dev)
         del model, flat, opt, loss, ids
         gc.collect()    # (see _warm_llama): otherwise the state stays allocated until a GC cycle
-        torch.cuda.empty_cache()
+        # this GPU's cache only: a global empty_cache from a late warm-up thread would drop the
+        # slab already reserved on another GPU (_reserve_slab)
+        _release_device_cache(dev.index if dev.index is not None else torch.cuda.current_device())
     return time.perf_counter() - t0
 
 

@@ -137,10 +137,13 @@ class RecoveryMixin:
         vram.publish_warm(self.kv, f"{self.ctx.role}{self.ctx.index}", spec)
         t0 = time.perf_counter()
         limit = float(os.environ.get("EDL_WARM_WAIT_S", 60))
-        state = vram.standby_warm_on(self.kv, self.device.index)
+        # a first-generation worker also waits for a standby that is still starting (it would
+        # otherwise race its warm-up); a replacement never waits for the refill behind it
+        first = os.environ.get("EDL_GENERATION", "0") == "0" and not vram.ADOPTED_FROM
+        state = vram.standby_warm_on(self.kv, self.device.index, pending=first)
         while state is False and time.perf_counter() - t0 < limit:
             time.sleep(0.05)
-            state = vram.standby_warm_on(self.kv, self.device.index)
+            state = vram.standby_warm_on(self.kv, self.device.index, pending=first)
         if state is not None:
             self.events.emit("standby_warm_wait", s=round(time.perf_counter() - t0, 3), warm=bool(state))
 

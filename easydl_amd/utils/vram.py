@@ -121,12 +121,15 @@ def read_warm(kv, slot: str) -> tuple[bool, dict | None]:
     return True, json.loads(raw).get("spec")
 
 
-def standby_warm_on(kv, gpu) -> bool | None:
+def standby_warm_on(kv, gpu, pending: bool = False) -> bool | None:
     """None: no standby is parked (``standby/roster``, kept by the operator); True: one of the
-    parked standbys has run its warm-up on ``gpu`` (an int, "cpu" or None); False: not yet."""
+    parked standbys has run its warm-up on ``gpu`` (an int, "cpu" or None); False: not yet.
+    ``pending``: a standby the operator spawned that is still starting (``standby/pending``)
+    counts as "not yet" -- for a job's first workers, which would otherwise race it; never for
+    a replacement, whose first step must not wait for the refill standby spawned behind it."""
     names = roster(kv)
     if not names:
-        return None
+        return False if (pending and (kv.get_str("standby/pending") or "")) else None
     where = ["any"] + ([f"gpu{gpu}"] if isinstance(gpu, int) else ["cpu"])
     return any(kv.exists(f"standby/warm/{n}/{w}") for n in names for w in where)
 

@@ -41,13 +41,23 @@ def _run(tmp_path, standby: int):
     return d, read_events(d["run_dir"])
 
 
+def _logs(d) -> str:
+    out = ""
+    for root, _, files in os.walk(d.get("run_dir") or ""):
+        for f in sorted(files):
+            if f.endswith(".log") or f.startswith("events"):
+                with open(os.path.join(root, f), errors="replace") as fh:
+                    out += f"--- {f}\n" + "".join(ln for ln in fh.readlines() if "socket.cpp" not in ln)[-3000:]
+    return out[-12000:]
+
+
 @pytest.mark.gpu
 def test_standby_warm_up_never_overlaps_a_training_step(tmp_path):
     d0, ev0 = _run(tmp_path, 0)
     d1, ev1 = _run(tmp_path, 1)
     assert not any(e["kind"] == "standby_warm_wait" for e in ev0)
     wait = [e for e in ev1 if e["kind"] == "standby_warm_wait"]
-    assert wait and wait[0]["warm"], wait            # the standby reported its warm-up done ...
+    assert wait and wait[0]["warm"], (wait, _logs(d1))   # the standby reported its warm-up done ...
     first_step = min(e["ts"] for e in ev1 if e["kind"] == "step_done")
     assert wait[0]["ts"] < first_step                 # ... before the worker's first step
     ratio = d1["step_s_median"] / d0["step_s_median"]

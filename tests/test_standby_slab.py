@@ -27,3 +27,24 @@ def test_per_device_release_returns_cached_blocks(cuda):
     assert after <= before - (4 << 30), (before, after)
     y = torch.ones(1 << 20, device=cuda)          # the allocator still works afterwards
     assert float(y.sum()) == float(1 << 20)
+
+
+class _KV:
+    def __init__(self, d):
+        self.d = d
+
+    def get_str(self, k):
+        return self.d.get(k)
+
+    def exists(self, k):
+        return k in self.d
+
+
+def test_first_workers_wait_for_a_starting_standby_replacements_do_not():
+    from easydl_amd.utils import vram
+    starting = _KV({"standby/roster": "", "standby/pending": "sb-0"})
+    assert vram.standby_warm_on(starting, 0) is None                   # a replacement: no wait
+    assert vram.standby_warm_on(starting, 0, pending=True) is False    # a first worker: wait
+    assert vram.standby_warm_on(_KV({}), 0, pending=True) is None      # no standby at all
+    parked = _KV({"standby/roster": "sb-0", "standby/warm/sb-0/gpu0": "{}"})
+    assert vram.standby_warm_on(parked, 0) is True and vram.standby_warm_on(parked, 1, pending=True) is False
