@@ -6,4 +6,4 @@ timeout -k 10 600 python -u -m pytest -v --timeout 400 --timeout-method thread -
   tests/test_second_failure_gpu.py > gpurun_out/r06_g29.log 2>&1
 rc=$?; grep -E "passed|failed" gpurun_out/r06_g29.log | tail -3; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 900 python -u bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/r06_bench_v4.json 2> gpurun_out/r06_bench_v4.err || exit 1
-python -c "import json;d=json.loads(open('gpurun_out/r06_bench_v4.json').read().strip().splitlines()[-1]);t=d['ttr'];print(d['value'],d['time_to_recover_s'],t['step_s_steady'],t.get('standby_slab_gb'),t['first_step']['s'])"
+python scripts/ab_line.py gpurun_out/r06_bench_v4.json head-final 1
