@@ -159,6 +159,16 @@ class Communicator:
                     log.warning("xGMI engine unavailable (%s); RCCL only", e)
                     self.xgmi_probe = {"selected": "rccl", "error": str(e)[:200]}
                     self.xgmi = None
+                if data_backend == "auto":
+                    # the engine is used by every rank or by none: a rank whose mapping failed
+                    # (hipIpcOpenMemHandle, after every handle was published) falls back alone
+                    # otherwise, and its peers would wait in engine collectives it never joins
+                    failed = float(self.ctrl_all_reduce([0.0 if self.xgmi is not None else 1.0],
+                                                        dist.ReduceOp.MAX)[0])
+                    if failed and self.xgmi is not None:
+                        self.xgmi.close()
+                        self.xgmi = None
+                        self.xgmi_probe = {"selected": "rccl", "error": "a peer's xGMI engine failed"}
             if self.data_kind == "gloo":
                 self.data = dist.ProcessGroupGloo(dist.PrefixStore("data", base), rank, world_size, _td(timeout_s))
             else:

@@ -84,6 +84,17 @@ class XgmiComm:
     # take the staged path, its state transfer the staged pull)
     REGISTER_MAX = int(os.environ.get("EDL_XGMI_REGISTER_MAX_MB", 2040)) << 20
 
+    _FAIL = b"FAIL:"
+
+    def _fail(self, store, prefix: str, rank: int, msg: str) -> None:
+        """This rank cannot take part: publish a failure marker in place of its handles (so every
+        peer gives up the engine at once, ``__init__``), then raise."""
+        try:
+            store.set(f"{prefix}/ipc/{rank}", self._FAIL + msg.encode()[:200])
+        except Exception:  # noqa: BLE001 - the raise below still ends this rank's attempt
+            pass
+        raise XgmiError(msg)
+
     def __init__(self, store, prefix: str, rank: int, world: int, device, ws_bytes: int | None = None,
                  timeout_s: float = 60.0):
         self.rank, self.world_size = rank, world
@@ -97,17 +108,32 @@ class XgmiComm:
         h = ctypes.c_void_p()
         rc = self._rt("edl_xgmi_ws_create", self.device.index or 0, ws_bytes, ctypes.byref(h))
         if rc != 0:
-            raise XgmiError(f"workspace allocation failed: hipError {rc}")
+            self._fail(store, prefix, rank, f"workspace allocation failed: hipError {rc}")
         self._ws = h
         self.ws_bytes = self._rt("edl_xgmi_ws_bytes", h)
         mine = ctypes.create_string_buffer(128)
         rc = self._rt("edl_xgmi_ws_handles", h, mine)
+        # fault injection (tests): these ranks fail their export as hipIpcGetMemHandle once did on a
+        # world-8 drill's re-formed epoch (profiles/r06_world8_engine_fail.md)
+        if str(rank) in os.environ.get("EDL_XGMI_FAIL_EXPORT", "").split(","):
+            rc = 1
         if rc != 0:
-            raise XgmiError(f"hipIpcGetMemHandle failed: hipError {rc}")
+            self._rt("edl_xgmi_ws_destroy", h)
+            self._ws = None
+            self._fail(store, prefix, rank, f"hipIpcGetMemHandle failed: hipError {rc}")
         # device identity travels with the handles: ranks on the SAME GPU are counted
         uuid = str(torch.cuda.get_device_properties(self.device).uuid).encode()[:64].ljust(64, b" ")
         store.set(f"{prefix}/ipc/{rank}", mine.raw + uuid)
         entries = [mine.raw + uuid if p == rank else store.get(f"{prefix}/ipc/{p}") for p in range(world)]
+        failed = [p for p, e in enumerate(entries) if e.startswith(self._FAIL)]
+        if failed:
+            # a peer could not export its workspace: nobody builds the engine this epoch (the peers
+            # learn it at once from its marker instead of waiting out the store timeout for a key
+            # that never comes, which left them 300 s behind the rank that had fallen back)
+            self._rt("edl_xgmi_ws_destroy", h)
+            self._ws = None
+            raise XgmiError(f"peer rank(s) {failed} could not export their workspace: "
+                            f"{entries[failed[0]][len(self._FAIL):].decode(errors='replace')[:120]}")
         allh = b"".join(e[:128] for e in entries)
         # the most ranks any one GPU carries (every rank sees the same records): the grid cap
         # below must be identical on every rank, since workgroup b meets workgroup b of each peer

@@ -187,3 +187,19 @@ def test_rccl_data_plane_world1_collectives_and_coalesced_p2p(cuda):
     assert res.pop("data_kind") == "rccl", res
     res.pop("backend")
     assert all(res.values()), res
+
+
+@pytest.mark.gpu
+def test_one_rank_failing_its_engine_export_sends_every_rank_to_the_fallback(cuda, tmp_path, monkeypatch):
+    """A rank whose workspace export fails (hipIpcGetMemHandle) publishes a failure marker: its
+    peers give the engine up at once instead of waiting out the store timeout for its handles,
+    and every rank trains on the fallback plane, correctly (round-6 world-8 drill regression)."""
+    import time as _t
+    monkeypatch.setenv("EDL_XGMI_FAIL_EXPORT", "1")
+    t0 = _t.perf_counter()
+    rs = _run(2, tmp_path, worker=os.path.join(ROOT, "tests", "helpers", "auto_comm_worker.py"), timeout=120)
+    assert _t.perf_counter() - t0 < 90
+    for r in rs:
+        assert r["ok"], r["errors"]
+        assert r["backend"] == "gloo" and r["registered"] == 0, r
+        assert "error" in (r["probe"] or {}), r["probe"]
