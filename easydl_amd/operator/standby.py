@@ -92,9 +92,20 @@ def _warm_llama(dev, spec: dict, info: dict | None = None) -> bool:
     b, s = (int(x) for x in spec["batch"])
     free, _ = torch.cuda.mem_get_info(dev)
     need = _llama_warm_bytes(cfg, b * s)
-    (WARM_INFO if info is None else info).update(free_gb=round(free / 2**30, 1), need_gb=round(need / 2**30, 1))
+    wi = WARM_INFO if info is None else info
+    wi.update(free_gb=round(free / 2**30, 1), need_gb=round(need / 2**30, 1))
     if free < 2 * need + (4 << 30):
-        return False
+        # Not room for the micro-batch shape: still run the layer at the worker's widths on a
+        # short sequence.  The GEMM solutions for the real M differ, but hipBLASLt's library,
+        # the attention / norm / loss kernels at these widths and their code objects are then
+        # loaded HERE, while HBM is calm -- not in the replacement's first step, when the dead
+        # worker's memory is still being reclaimed and a failed code-object load is fatal (the
+        # r06 three-failure soak: "Could not initialize Tensile host", then SIGSEGV).
+        b, s = 1, min(s, 512)
+        need = _llama_warm_bytes(cfg, b * s)
+        if free < 2 * need + (4 << 30):
+            return False
+        wi["reduced_tokens"] = b * s
     from easydl_amd.parallel.flat import FlatParams
     model = Llama(cfg, device=dev)
     flat = FlatParams(model)

@@ -262,6 +262,23 @@ def test_standby_full_width_warm_up_from_the_published_spec(cuda):
     assert after - before < 32 << 20, (after - before) >> 20
 
 
+@pytest.mark.gpu
+def test_standby_warm_up_without_room_for_the_micro_batch_runs_the_widths_on_a_short_sequence(cuda):
+    """A micro-batch whose one-layer pass needs more than half of the GPU: the warm-up still runs
+    the layer at the worker's widths, on 512 tokens (libraries and code objects loaded while HBM
+    is calm)."""
+    from easydl_amd.operator.standby import _warm_llama
+    spec = {"model": "llama", "batch": [256, 8192],
+            "cfg": {"vocab_size": 4096, "dim": 1024, "n_layers": 4, "n_heads": 8, "n_kv_heads": 2, "ffn_dim": 2048,
+                    "max_seq_len": 8192}}
+    info: dict = {}
+    try:
+        assert _warm_llama(cuda, spec, info)
+    finally:
+        torch.cuda.tunable.enable(False)
+    assert info["reduced_tokens"] == 512 and 2 * info["need_gb"] > info["free_gb"], info
+
+
 def test_flat_params_are_collected_with_their_model():
     """No reference cycle through the parameters' C++ hook tables keeps a dropped model's
     flat buffers alive (the standby warm-up leak of round 4)."""
