@@ -369,7 +369,9 @@ def test_tp2_dp3_replacement_receives_shard_from_every_holder(tmp_path):
     port = free_port()
     m = _start_master(tmp_path, port, 2, 6, initial=6, granule=2, window=0.3)
     try:
-        common = {"EDL_MASTER_ADDR": "127.0.0.1", "EDL_MASTER_PORT": str(port), "TEST_STEPS": "24",
+        # 60 steps of >= 0.2 s: the world-4 epoch must still be training when the replacement (a fresh
+        # interpreter, slow to import under a loaded CPU tier) joins, or the job ends at world 4
+        common = {"EDL_MASTER_ADDR": "127.0.0.1", "EDL_MASTER_PORT": str(port), "TEST_STEPS": "60",
                   "TEST_GB": "6", "EDL_TP": "2", "TEST_STEP_SLEEP": "0.2"}
         procs = {}
         for i in range(6):
@@ -379,19 +381,23 @@ def test_tp2_dp3_replacement_receives_shard_from_every_holder(tmp_path):
         while time.time() < t_end and procs[5].poll() is None:
             time.sleep(0.05)
         _report_exit(port, 5, procs[5].poll())
-        time.sleep(2.0)     # the world-4 epoch trains a few steps
+        from easydl_amd.utils.events import read_events
+        t_end = time.time() + 60        # the world-4 epoch forms and trains a few steps
+        while time.time() < t_end and not any(e["kind"] == "epoch_formed" and e.get("world") == 4
+                                              for e in read_events(str(tmp_path))):
+            time.sleep(0.1)
+        time.sleep(1.0)
         env = _env(tmp_path, 6, dict(common, TEST_OUT=str(tmp_path / "res6.json")))
         procs[6] = subprocess.Popen([sys.executable, WORKER], env=env, cwd=ROOT)
         codes = _wait({i: p for i, p in procs.items() if i != 5})
         assert all(v == 0 for v in codes.values()), codes
         r = _results(tmp_path, [0, 1, 2, 3, 4, 6])
-        assert all(x["step"] == 24 for x in r.values()), {i: x["step"] for i, x in r.items()}
+        assert all(x["step"] == 60 for x in r.values()), {i: (x["step"], x["worlds"]) for i, x in r.items()}
         assert 6 in r[6]["worlds"] and any(4 in x["worlds"] for x in r.values()), {i: x["worlds"] for i, x in r.items()}
         by_tp = {}
         for x in r.values():
             by_tp.setdefault(x["tp_rank"], set()).add(x["hash"])
         assert sorted(by_tp) == [0, 1] and all(len(v) == 1 for v in by_tp.values()), by_tp
-        from easydl_amd.utils.events import read_events
         sends = [e for e in read_events(str(tmp_path)) if e["kind"] == "state_broadcast" and e.get("group") == "dp"]
         assert sends and max(e.get("sources", 1) for e in sends) == 2, sends
     finally:
