@@ -95,24 +95,15 @@ def _warm_llama(dev, spec: dict, info: dict | None = None) -> bool:
     wi = WARM_INFO if info is None else info
     wi.update(free_gb=round(free / 2**30, 1), need_gb=round(need / 2**30, 1))
     if free < 2 * need + (4 << 30):
-        # Not room for the micro-batch shape: still run the layer at the worker's widths, on the
-        # largest shape that fits -- first ONE sequence of the micro-batch (the piece a memory-
-        # limited first step runs, recovery.py plan_memory: its GEMM solutions exactly), then
-        # shorter sequences down to 512 tokens.  hipBLASLt's library, the attention / norm / loss
-        # kernels at these widths and their code objects are then loaded HERE, while HBM is calm
-        # -- not in the replacement's first step, when the dead worker's memory is still being
-        # reclaimed and a failed code-object load is fatal (the r06 three-failure soak: "Could not
-        # initialize Tensile host", then SIGSEGV; profiles/r06_three_failures_8b.md).
-        shapes = [(1, s)] if b > 1 else []
-        t = s // 2
-        while t >= 512:
-            shapes.append((1, t))
-            t //= 2
-        for b, s in shapes:
-            need = _llama_warm_bytes(cfg, b * s)
-            if free >= 2 * need + (4 << 30):
-                break
-        else:
+        # Not room for the micro-batch shape: still run the layer at the worker's widths on a
+        # short sequence.  The GEMM solutions for the real M differ, but hipBLASLt's library,
+        # the attention / norm / loss kernels at these widths and their code objects are then
+        # loaded HERE, while HBM is calm, not in the replacement's first step.  (It does not
+        # prevent the third-takeover crash of profiles/r06_three_failures_8b.md; a one-sequence
+        # warm-up at 8k tokens did not either.)
+        b, s = 1, min(s, 512)
+        need = _llama_warm_bytes(cfg, b * s)
+        if free < 2 * need + (4 << 30):
             return False
         wi["reduced_tokens"] = b * s
     from easydl_amd.parallel.flat import FlatParams

@@ -50,15 +50,14 @@ def test_first_workers_wait_for_a_starting_standby_replacements_do_not():
     assert vram.standby_warm_on(parked, 0) is True and vram.standby_warm_on(parked, 1, pending=True) is False
 
 
-def test_warm_up_without_room_for_the_micro_batch_runs_one_sequence_of_it(monkeypatch):
-    """(CPU) the shape ladder of ``_warm_llama``: the micro-batch when it fits twice over, else
-    ONE of its sequences (the split piece a memory-limited first step runs), else shorter ones,
-    else nothing."""
+def test_warm_up_without_room_for_the_micro_batch_runs_a_short_sequence(monkeypatch):
+    """(CPU) the shapes of ``_warm_llama``: the micro-batch when it fits twice over, else one
+    512-token sequence at the worker's widths, else nothing."""
     spec = {"model": "llama", "batch": [4, 2048],
             "cfg": {"vocab_size": 1024, "dim": 256, "n_layers": 2, "n_heads": 4, "n_kv_heads": 2, "ffn_dim": 512,
                     "max_seq_len": 2048}}
     monkeypatch.setattr(torch.cuda, "synchronize", lambda dev=None: None)
-    for free_gib, want in ((8.0, None), (4.3, 2048), (4.1, 1024), (4.05, 512), (3.9, False)):
+    for free_gib, want in ((8.0, None), (4.3, 512), (4.05, 512), (3.9, False)):
         monkeypatch.setattr(torch.cuda, "mem_get_info", lambda dev=None, f=free_gib: (int(f * 2**30), 8 << 30))
         info: dict = {}
         ok = standby._warm_llama(torch.device("cpu"), spec, info)

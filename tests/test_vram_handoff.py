@@ -263,10 +263,10 @@ def test_standby_full_width_warm_up_from_the_published_spec(cuda):
 
 
 @pytest.mark.gpu
-def test_standby_warm_up_without_room_for_the_micro_batch_runs_one_sequence_of_it(cuda):
+def test_standby_warm_up_without_room_for_the_micro_batch_runs_the_widths_on_a_short_sequence(cuda):
     """A micro-batch whose one-layer pass needs more than half of the GPU: the warm-up still runs
-    the layer at the worker's widths, on one of its sequences (the piece a memory-limited first
-    step runs; libraries and code objects loaded while HBM is calm)."""
+    the layer at the worker's widths, on 512 tokens (libraries and code objects loaded while HBM
+    is calm)."""
     from easydl_amd.operator.standby import _warm_llama
     spec = {"model": "llama", "batch": [256, 8192],
             "cfg": {"vocab_size": 4096, "dim": 1024, "n_layers": 4, "n_heads": 8, "n_kv_heads": 2, "ffn_dim": 2048,
@@ -276,7 +276,7 @@ def test_standby_warm_up_without_room_for_the_micro_batch_runs_one_sequence_of_i
         assert _warm_llama(cuda, spec, info)
     finally:
         torch.cuda.tunable.enable(False)
-    assert info["reduced_tokens"] == 8192 and 2 * info["need_gb"] > info["free_gb"], info
+    assert info["reduced_tokens"] == 512 and 2 * info["need_gb"] > info["free_gb"], info
 
 
 def test_flat_params_are_collected_with_their_model():
