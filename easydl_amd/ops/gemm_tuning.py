@@ -55,10 +55,13 @@ def apply(mode: str | None = None, path: str | None = None) -> str:
         return "off"
     tun.enable(True)
     tun.tuning_enable(False)
-    # TunableOp writes its results at exit even with tuning off: point that at ONE scratch
-    # file per user (never the shipped file or the working directory's default; a
-    # per-process name would pile up).  Ranks may overwrite it concurrently: nothing reads it.
-    tun.set_filename(os.path.join(tempfile.gettempdir(), f"edl_tunableop_scratch_{os.getuid()}.csv"))
+    # TunableOp READS the file named here when it starts (before read_file below) and writes it
+    # at exit when it holds results that were not loaded: never the shipped file or the working
+    # directory's default, and never a name another process writes -- an entry left there by
+    # any earlier run would be taken as a selection (scripts/tunableop_scratch_probe.py: a
+    # stale entry naming a solution this library lacks fails that GEMM).  With tuning off
+    # nothing is written, so a per-process name does not pile up.
+    tun.set_filename(os.path.join(tempfile.gettempdir(), f"edl_tunableop_scratch_{os.getuid()}_{os.getpid()}.csv"))
     ok = tun.read_file(path)
     if not ok:
         log.warning("TunableOp results %s not loaded (validator mismatch?): library heuristics", path)

@@ -1,6 +1,8 @@
 """Job feature extraction (meta-device model analysis) feeding the Brain; shipped tuning files."""
 import os
 
+import pytest
+
 from easydl_amd.api.spec import ElasticJob
 from easydl_amd.brain.collectors import GpuInfo, NodeInventory
 from easydl_amd.brain.planner import JobFeatures, Planner
@@ -67,6 +69,19 @@ def test_gemm_tuning_select_file_is_curated(monkeypatch):
     assert entries and all(e[0].startswith("GemmTunableOp_BFloat16") and e[2].startswith("Gemm_Hipblaslt")
                            for e in entries)
     assert any(e[1] == "tn_14336_4096_16384_ld_16384_16384_14336" for e in entries)   # down-proj wgrad
+
+
+@pytest.mark.gpu
+def test_a_stale_shared_tunableop_file_is_not_read():
+    """TunableOp reads its output file when it starts.  A file left under the old shared per-user
+    name, holding a solution index this hipBLASLt lacks, must not reach a new process's GEMMs
+    (scripts/tunableop_scratch_probe.py; before the fix the GEMM failed)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "scripts", "tunableop_scratch_probe.py"), "bogus"],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "gemm ok True" in r.stdout, (r.stdout[-2000:], r.stderr[-2000:])
 
 
 def test_shipped_miopen_find_db_installs_into_a_scratch_copy(monkeypatch, tmp_path):
