@@ -392,7 +392,6 @@ class RecoveryMixin:
         if avail >= need * 1.05:
             return
         self._mb_limited = True
-        self._pregrow = None
         split, rc = self._apply_memory_plan(avail)
         self.events.emit("memory_limited_steps", step=self.step, split=split, recompute=rc > 0, recompute_layers=rc,
                          layers=self._recompute_layers_total(), need_gb=round(need / 2**30, 1),
@@ -440,14 +439,6 @@ class RecoveryMixin:
         if avail >= self._act_need * 1.05:
             if not grow:
                 return
-            if self._pregrow_pending():
-                # the cache is growing on a side thread: plan from the blocks already cached
-                cached = torch.cuda.memory_reserved(self.device) - torch.cuda.memory_allocated(self.device)
-                split, rc = self._apply_memory_plan(cached)
-                if (split, rc) != before:
-                    self.events.emit("memory_replanned", step=self.step, mb=mb, split=split, recompute_layers=rc,
-                                     avail_gb=round(cached / 2**30, 1), cached_only=True)
-                return
             self.events.emit("memory_restored", step=self.step, mb=mb, avail_gb=round(avail / 2**30, 1))
             self._restore_full_batches()
             return
@@ -459,50 +450,6 @@ class RecoveryMixin:
         if (split, rc) != before:
             self.events.emit("memory_replanned", step=self.step, mb=mb, split=split, recompute_layers=rc,
                              avail_gb=round(avail / 2**30, 1))
-
-    def _pregrow_pending(self) -> bool:
-        """The memory is back: before the step returns to full micro-batches, a side thread grows
-        the caching allocator (on the compute stream's pool) by what a full micro-batch needs beyond
-        the blocks already cached, while the main thread keeps running the split pieces from those
-        blocks.  HBM the driver is still tearing down after the dead worker was reaped is slow to
-        hand out (2.5-3.5 s for the first full micro-batch after a recovery, profiles/
-        r06_ttr_first_step.md); the side thread pays that instead of the step, and a thread
-        growing the allocator does not hold up the main thread's cached allocations
-        (scripts/bg_grow_probe.py).  True while the growth runs.  ``EDL_RECOVERY_PREGROW=0``: off."""
-        if self.device.type != "cuda" or os.environ.get("EDL_RECOVERY_PREGROW", "1") == "0":
-            return False
-        th = getattr(self, "_pregrow", None)
-        if th is None:
-            cached = torch.cuda.memory_reserved(self.device) - torch.cuda.memory_allocated(self.device)
-            want = int(self._act_need * 1.05) - cached
-            if want < (2 << 30):
-                self._pregrow = False
-                return False
-            want = want // (2 << 20) * (2 << 20)
-            stream, dev = torch.cuda.current_stream(self.device), self.device
-            res: dict = {}
-
-            def grow():
-                t0 = time.perf_counter()
-                try:
-                    with torch.cuda.device(dev), torch.cuda.stream(stream):
-                        buf = torch.empty(want, dtype=torch.uint8, device=dev)
-                        del buf     # stays cached for the compute stream
-                    res["ok"] = True
-                except RuntimeError as e:   # (out of memory: the full micro-batches will wait for it)
-                    res["error"] = str(e)[:200]
-                res["s"] = round(time.perf_counter() - t0, 3)
-            self._pregrow_res, self._pregrow_gb = res, round(want / 2**30, 1)
-            self._pregrow = threading.Thread(target=grow, name="edl-pregrow", daemon=True)
-            self._pregrow.start()
-            return True
-        if th is False:
-            return False
-        if th.is_alive():
-            return True
-        self.events.emit("memory_pregrown", step=self.step, gb=self._pregrow_gb, **self._pregrow_res)
-        self._pregrow = False
-        return False
 
     def _piece_trace_begin(self):
         """Per-piece timing of a memory-limited step (the evidence of where a takeover's first
