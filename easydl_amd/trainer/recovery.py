@@ -29,7 +29,6 @@ Unit tests: ``tests/test_recovery_cpu.py`` (memory-plan policy, micro-batch piec
 """
 from __future__ import annotations
 
-import ctypes
 import logging
 import math
 import os
@@ -48,29 +47,6 @@ class _null:
 
     def __exit__(self, *a):
         return False
-
-
-_HIP = []
-
-
-def _hip_runtime():
-    """The HIP runtime this process already runs on (torch's), by path from /proc/self/maps:
-    dlopen of that path returns the loaded library, never a second runtime.  None if not found."""
-    if not _HIP:
-        lib = None
-        try:
-            with open("/proc/self/maps") as f:
-                for line in f:
-                    if "libamdhip64" in line and line.split()[-1].startswith("/"):
-                        lib = ctypes.CDLL(line.split()[-1])
-                        lib.hipMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t]
-                        lib.hipFree.argtypes = [ctypes.c_void_p]
-                        lib.hipSetDevice.argtypes = [ctypes.c_int]
-                        break
-        except OSError:
-            lib = None
-        _HIP.append(lib)
-    return _HIP[0]
 
 
 class RecoveryMixin:
@@ -416,7 +392,6 @@ class RecoveryMixin:
         if avail >= need * 1.05:
             return
         self._mb_limited = True
-        self._regrow = None
         split, rc = self._apply_memory_plan(avail)
         self.events.emit("memory_limited_steps", step=self.step, split=split, recompute=rc > 0, recompute_layers=rc,
                          layers=self._recompute_layers_total(), need_gb=round(need / 2**30, 1),
@@ -462,7 +437,7 @@ class RecoveryMixin:
         avail = self._hbm_avail()
         before = self._mb_plan
         if avail >= self._act_need * 1.05:
-            if not grow or self._regrow_pending():
+            if not grow:
                 return
             self.events.emit("memory_restored", step=self.step, mb=mb, avail_gb=round(avail / 2**30, 1))
             self._restore_full_batches()
@@ -475,50 +450,6 @@ class RecoveryMixin:
         if (split, rc) != before:
             self.events.emit("memory_replanned", step=self.step, mb=mb, split=split, recompute_layers=rc,
                              avail_gb=round(avail / 2**30, 1))
-
-    def _regrow_pending(self) -> bool:
-        """The memory is back (the driver reports it free): before the step returns to full
-        micro-batches, a side thread asks HIP -- not the caching allocator -- for what a full
-        micro-batch needs beyond the cached blocks, and frees it again.  While the driver is
-        still tearing the dead worker down, that request waits (2.5-3.5 s for the first full
-        micro-batch after a recovery, profiles/r06_ttr_first_step.md); made by the side thread it
-        waits there while the main thread keeps running the split pieces from cached blocks.
-        (Growing through the caching allocator on a side thread holds its lock across the wait
-        and stalled the main thread: tried, reverted.)  True while the request runs.
-        ``EDL_RECOVERY_REGROW=0``: off."""
-        if self.device.type != "cuda" or os.environ.get("EDL_RECOVERY_REGROW", "1") == "0":
-            return False
-        th = getattr(self, "_regrow", None)
-        if th is None:
-            cached = torch.cuda.memory_reserved(self.device) - torch.cuda.memory_allocated(self.device)
-            want = int(self._act_need * 1.05) - cached
-            hip = _hip_runtime()
-            if want < (2 << 30) or hip is None:
-                self._regrow = False
-                return False
-            idx = self.device.index if self.device.index is not None else torch.cuda.current_device()
-            res: dict = {"gb": round(want / 2**30, 1)}
-
-            def absorb():
-                t0 = time.perf_counter()
-                p = ctypes.c_void_p()
-                hip.hipSetDevice(idx)
-                rc = hip.hipMalloc(ctypes.byref(p), ctypes.c_size_t(want))
-                res["malloc_s"] = round(time.perf_counter() - t0, 3)
-                if rc == 0:
-                    hip.hipFree(p)
-                res.update(rc=rc, s=round(time.perf_counter() - t0, 3))
-            self._regrow_res = res
-            self._regrow = threading.Thread(target=absorb, name="edl-regrow", daemon=True)
-            self._regrow.start()
-            return True
-        if th is False:
-            return False
-        if th.is_alive():
-            return True
-        self.events.emit("memory_regrow_wait", step=self.step, **self._regrow_res)
-        self._regrow = False
-        return False
 
     def _piece_trace_begin(self):
         """Per-piece timing of a memory-limited step (the evidence of where a takeover's first
