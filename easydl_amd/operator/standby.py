@@ -103,7 +103,7 @@ def _warm_llama(dev, spec: dict, info: dict | None = None) -> bool:
         # warm-up at 8k tokens did not either.)
         b, s = 1, min(s, 512)
         need = _llama_warm_bytes(cfg, b * s)
-        if free < 2 * need + (4 << 30):
+        if free < 2 * need + (4 << 30) or os.environ.get("EDL_STANDBY_WARM_SHORT", "1") == "0":
             return False
         wi["reduced_tokens"] = b * s
     from easydl_amd.parallel.flat import FlatParams
